@@ -1,0 +1,276 @@
+/*
+ * kbgpu.h — C ABI of the MI355X allocate path (kube-batch v0.4 semantics).
+ *
+ * The boundary sits at the allocate ACTION, not at the per-pair predicate:
+ * the reference exposes `framework.Action{Name, Initialize, Execute(*Session),
+ * UnInitialize}` (pkg/scheduler/framework/interface.go:20-32) and registers
+ * `allocate` by name (pkg/scheduler/framework/plugins.go:53-58,
+ * pkg/scheduler/factory.go:34-46). A per-pair `api.PredicateFn`
+ * (pkg/scheduler/api/types.go:101) offload would pay one cgo call and one
+ * kernel launch per (task,node), so the entry points below replace the whole
+ * of allocateAction.Execute (pkg/scheduler/actions/allocate/allocate.go:41-176)
+ * and report its decisions; the caller replays them through its own
+ * ssn.Allocate / ssn.Pipeline (pkg/scheduler/framework/session.go:205-293) so
+ * event handlers, gang dispatch and cache.Bind stay on the host.
+ *
+ * Conventions: plain C structs and pointers only; the library copies what it
+ * needs during kbg_session_open and keeps no caller pointer after any call
+ * returns (cgo-safe). One session = one thread = one HIP stream. Every
+ * function returns a kbg_status; kbg_last_error() gives the message.
+ * All strings (UIDs, names, label keys/values, operators, effects) travel as
+ * indices into one string table; the empty string must be interned like any
+ * other. String ordering is bytewise, as Go's `<` on strings.
+ */
+#ifndef KBGPU_H_
+#define KBGPU_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KBG_ABI_VERSION 1
+
+typedef enum kbg_status {
+  KBG_OK = 0,
+  KBG_E_INVALID = 1,     /* malformed snapshot / arguments */
+  KBG_E_UNSUPPORTED = 2, /* session uses a predicate the device path does not run
+                            (pending hostPort, pod (anti)affinity): run the
+                            reference path instead. Never a silent fallback. */
+  KBG_E_REF_PANIC = 3,   /* the reference would panic here (Resource.Sub underflow
+                            resource_info.go:100-110, proportion water-fill F9
+                            proportion.go:119-140, nil-Node predicate
+                            predicates.go:122-123). Decisions made before the
+                            panic point are returned. */
+  KBG_E_HIP = 4,         /* HIP runtime error (no device, launch failure, ...) */
+  KBG_E_RCCL = 5,
+  KBG_E_NOMEM = 6,
+  KBG_E_CAPACITY = 7     /* caller's output buffer is too small */
+} kbg_status;
+
+/* api.TaskStatus bit values (pkg/scheduler/api/types.go:23-58) */
+enum {
+  KBG_PENDING = 1 << 0,
+  KBG_ALLOCATED = 1 << 1,
+  KBG_PIPELINED = 1 << 2,
+  KBG_BINDING = 1 << 3,
+  KBG_BOUND = 1 << 4,
+  KBG_RUNNING = 1 << 5,
+  KBG_RELEASING = 1 << 6,
+  KBG_SUCCEEDED = 1 << 7,
+  KBG_FAILED = 1 << 8,
+  KBG_UNKNOWN = 1 << 9
+};
+
+/* conf.PluginOption disable flags (pkg/scheduler/conf/scheduler_conf.go:33-50) */
+enum {
+  KBG_DISABLE_JOB_ORDER = 1 << 0,
+  KBG_DISABLE_JOB_READY = 1 << 1,
+  KBG_DISABLE_TASK_ORDER = 1 << 2,
+  KBG_DISABLE_PREEMPTABLE = 1 << 3,
+  KBG_DISABLE_RECLAIMABLE = 1 << 4,
+  KBG_DISABLE_QUEUE_ORDER = 1 << 5,
+  KBG_DISABLE_PREDICATE = 1 << 6
+};
+
+enum { KBG_KIND_ALLOCATE = 0, KBG_KIND_PIPELINE = 1 };
+
+/* api.Resource without MaxTaskNum (resource_info.go:26-33); fp64 throughout. */
+typedef struct kbg_resource {
+  double milli_cpu;
+  double memory;
+  double milli_gpu;
+} kbg_resource;
+
+/* One session node = api.NodeInfo after cache.Snapshot() (node_info.go:26-42). */
+typedef struct kbg_node {
+  int32_t name;            /* string id of NodeInfo.Name ("" for a nil Node) */
+  int32_t has_node;        /* 0 => NodeInfo.Node == nil (node_info.go:44-56) */
+  kbg_resource allocatable;
+  kbg_resource idle;       /* NodeInfo.Idle */
+  kbg_resource releasing;  /* NodeInfo.Releasing */
+  int32_t max_task_num;    /* Allocatable.MaxTaskNum ("pods" allocatable) */
+  int32_t num_tasks;       /* len(NodeInfo.Tasks) */
+  int32_t unschedulable;   /* Node.Spec.Unschedulable */
+  int32_t label_off, label_len; /* Node.Labels: pairs (key,value) at labels[2*i] */
+  int32_t taint_off, taint_len; /* Node.Spec.Taints: taints[taint_off ..] */
+} kbg_node;
+
+typedef struct kbg_taint {
+  int32_t key, value, effect; /* string ids */
+} kbg_taint;
+
+/* One api.JobInfo in ssn.Jobs order (job_info.go:118-145). */
+typedef struct kbg_job {
+  int32_t uid;           /* string id of JobID */
+  int32_t queue;         /* index into queues (the snapshot keeps only jobs whose queue exists) */
+  int32_t min_available; /* PodGroup.Spec.MinMember / PDB minAvailable */
+  int32_t priority;      /* JobInfo.Priority (never set in v0.4: 0) */
+  int64_t creation_ns;   /* CreationTimestamp, nanoseconds */
+} kbg_job;
+
+/* One api.QueueInfo in ssn.Queues order (queue_info.go:27-45). */
+typedef struct kbg_queue {
+  int32_t uid;    /* string id of QueueID */
+  int32_t weight; /* Queue.Spec.Weight */
+} kbg_queue;
+
+/* One api.TaskInfo of a session job, any status (job_info.go:36-50). */
+typedef struct kbg_task {
+  int32_t uid;       /* string id of TaskID (pod UID) */
+  int32_t job;       /* index into jobs */
+  int32_t status;    /* KBG_PENDING, ... */
+  int32_t priority;  /* TaskInfo.Priority (pod priority, default 1) */
+  kbg_resource resreq;
+  int32_t spec;      /* index into specs (the pod's predicate inputs) */
+  int32_t node_name; /* string id of TaskInfo.NodeName */
+} kbg_task;
+
+/* Predicate-relevant part of a pod spec (predicates.go:121-201). */
+typedef struct kbg_spec {
+  int32_t selector_off, selector_len; /* Spec.NodeSelector pairs at selectors[2*i] */
+  int32_t has_required_affinity;      /* Affinity.NodeAffinity.RequiredDuringScheduling... != nil */
+  int32_t term_off, term_len;         /* its NodeSelectorTerms */
+  int32_t toleration_off, toleration_len;
+  int32_t has_host_ports;             /* some container port has hostPort > 0 */
+  int32_t has_pod_affinity;           /* Affinity.PodAffinity or PodAntiAffinity set */
+} kbg_spec;
+
+typedef struct kbg_term {
+  int32_t expr_off, expr_len;   /* MatchExpressions: reqs[expr_off ..] */
+  int32_t field_off, field_len; /* MatchFields: reqs[field_off ..] */
+} kbg_term;
+
+typedef struct kbg_requirement {
+  int32_t key;                  /* string id */
+  int32_t op;                   /* string id of the operator text ("In", "NotIn", ...) */
+  int32_t value_off, value_len; /* values[value_off ..] string ids */
+} kbg_requirement;
+
+typedef struct kbg_toleration {
+  int32_t key, op, value, effect; /* string ids */
+} kbg_toleration;
+
+typedef struct kbg_plugin_option {
+  int32_t name;   /* string id of the plugin name; unknown names are ignored (framework.go:30-35) */
+  uint32_t flags; /* KBG_DISABLE_* */
+} kbg_plugin_option;
+
+typedef struct kbg_snapshot {
+  const char* const* strings;
+  int32_t n_strings;
+  const kbg_node* nodes;           int32_t n_nodes;
+  const kbg_job* jobs;             int32_t n_jobs;
+  const kbg_queue* queues;         int32_t n_queues;
+  const kbg_task* tasks;           int32_t n_tasks;
+  const kbg_resource* others;      int32_t n_others;   /* Session.Others resreq, in order */
+  const kbg_spec* specs;           int32_t n_specs;
+  const kbg_term* terms;           int32_t n_terms;
+  const kbg_requirement* reqs;     int32_t n_reqs;
+  const int32_t* values;           int32_t n_values;
+  const kbg_toleration* tolerations; int32_t n_tolerations;
+  const int32_t* labels;           int32_t n_labels;    /* 2*n_labels ints */
+  const kbg_taint* taints;         int32_t n_taints;
+  const int32_t* selectors;        int32_t n_selectors; /* 2*n_selectors ints */
+  const kbg_plugin_option* plugins; int32_t n_plugins;
+  const int32_t* tier_sizes;       int32_t n_tiers;     /* plugins grouped by tier, in order */
+} kbg_snapshot;
+
+typedef struct kbg_options {
+  int32_t device;       /* HIP device ordinal; -1 = current */
+  int32_t heap_rule;    /* container/heap down() tie rule: 0 = Go 1.11 (default), 1 = Go >= 1.13 */
+  int32_t batch_tasks;  /* speculative batch size K (0 = default) */
+  int32_t candidates;   /* first-M feasible nodes kept per task (0 = default) */
+  int32_t full_scan;    /* 1 = every task evaluation scans the full node table */
+  int32_t reserved[7];
+} kbg_options;
+
+/* One placement decision, in reference order. */
+typedef struct kbg_decision {
+  int32_t task;          /* index into snapshot tasks */
+  int32_t node;          /* index into snapshot nodes */
+  int32_t kind;          /* KBG_KIND_ALLOCATE / KBG_KIND_PIPELINE */
+  int32_t dispatched_at; /* index of the decision whose ssn.Allocate dispatched
+                            (bound) this task (session.go:283-290), or -1 */
+} kbg_decision;
+
+typedef struct kbg_job_state {
+  int32_t ready_num;     /* gang readyTaskNum (gang.go:44-55) */
+  int32_t ready;         /* ssn.JobReady(job) */
+  double drf_share;      /* drf attr.share (drf.go:152-166); 0 if drf is off */
+  kbg_resource drf_allocated;
+} kbg_job_state;
+
+typedef struct kbg_queue_state {
+  double share;          /* proportion attr.share (proportion.go:225-237) */
+  kbg_resource deserved, allocated, request;
+  int32_t overused;
+  int32_t has_attr;      /* 0 if the queue has no job in the session */
+} kbg_queue_state;
+
+typedef struct kbg_node_state {
+  kbg_resource idle, releasing;
+  int32_t num_tasks;
+} kbg_node_state;
+
+typedef struct kbg_stats {
+  int64_t evaluations;     /* task evaluations scanned on the device */
+  int64_t node_visits;     /* (task,node) pairs evaluated on the device */
+  int64_t batches;
+  int64_t mispredictions;  /* batches cut by an unpredicted failure */
+  int64_t truncations;     /* batches cut by an exhausted candidate list */
+  int64_t scan_launches;
+  double scan_kernel_ms;   /* summed HIP-event time of the scan kernel */
+  double select_kernel_ms; /* summed HIP-event time of the candidate-select kernel */
+  double allocate_ms;      /* wall time of the last kbg_allocate */
+  double open_ms;          /* wall time of kbg_session_open */
+  int32_t n_classes;       /* static predicate classes on the device */
+  int32_t reserved[5];
+} kbg_stats;
+
+typedef struct kbg_session kbg_session;
+
+/* ABI version and the last error message of this thread. */
+int32_t kbg_abi_version(void);
+const char* kbg_last_error(void);
+/* Number of visible HIP devices (0 when none); never fails. */
+int32_t kbg_device_count(void);
+
+/* framework.OpenSession (framework.go:26-46) for the allocate path: copies the
+ * snapshot, runs the plugins' OnSessionOpen (drf.go:55-78, proportion.go:54-144,
+ * gang.go:80-166, priority.go:36-77, predicates.go:112-202) on the host, uploads
+ * the node table to HBM and builds the static predicate masks on the device. */
+kbg_status kbg_session_open(const kbg_snapshot* snap, const kbg_options* opts, kbg_session** out);
+
+/* allocateAction.Execute (allocate.go:41-176). Writes at most `cap` decisions.
+ * Can be called once per opened or reset session. */
+kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out);
+
+/* Restores the state captured at kbg_session_open (device-side copy); used to
+ * re-run a cycle on the same snapshot without re-uploading it. */
+kbg_status kbg_session_reset(kbg_session* s);
+
+/* Low-level node-loop offload (allocate.go:105-171 for ONE job pop): evaluates
+ * tasks[0..n) in order against the current device table with first-fit, stops
+ * after the first success when stop_at_first_success != 0, and commits every
+ * success to the device table (NodeInfo.AddTask, node_info.go:101-129).
+ * out_node[i] = -1 when task i fits nowhere. Returns the number evaluated. */
+kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t stop_at_first_success,
+                      int32_t* out_node, int32_t* out_kind, int32_t* n_evaluated);
+
+/* Applies one placement to the device table as NodeInfo.AddTask does. */
+kbg_status kbg_apply(kbg_session* s, int32_t node, const kbg_resource* req, int32_t kind);
+
+kbg_status kbg_job_state_get(kbg_session* s, int32_t job, kbg_job_state* out);
+kbg_status kbg_queue_state_get(kbg_session* s, int32_t queue, kbg_queue_state* out);
+kbg_status kbg_node_state_get(kbg_session* s, int32_t node, kbg_node_state* out);
+kbg_status kbg_stats_get(kbg_session* s, kbg_stats* out);
+
+void kbg_session_close(kbg_session* s);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KBGPU_H_ */

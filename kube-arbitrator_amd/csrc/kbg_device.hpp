@@ -1,0 +1,116 @@
+// Device-side data layout and kernel launchers of the MI355X allocate path.
+//
+// Node table (HBM, struct-of-arrays, one entry per ssn.Nodes position):
+//   idle_{cpu,mem,gpu}, rel_{cpu,mem,gpu}  f64[N]   NodeInfo.Idle / .Releasing
+//   ntasks, maxtasks                       i32[N]   len(NodeInfo.Tasks), Allocatable.MaxTaskNum
+// 56 B of dynamic state per node; the static part of the predicate
+// (selector/affinity, taints, unschedulable) is resolved once per session into
+// class_mask[class][word] (1 bit per node) by kbg_build_class_mask.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kbg {
+
+// resource_info.go:54-56 LessEqual tolerances
+constexpr double kMinMilliCPU = 10.0;
+constexpr double kMinMemory = 10.0 * 1024.0 * 1024.0;
+constexpr double kMinMilliGPU = 10.0;
+
+// select kernel result encoding
+constexpr uint32_t kCandPipelineBit = 0x80000000u;  // candidate fits Releasing only
+constexpr uint32_t kCountIncompleteBit = 0x40000000u;
+constexpr uint32_t kCountMask = 0x3fffffffu;
+
+struct NodeSoA {
+  double* idle_cpu;
+  double* idle_mem;
+  double* idle_gpu;
+  double* rel_cpu;
+  double* rel_mem;
+  double* rel_gpu;
+  int32_t* ntasks;
+  int32_t* maxtasks;
+};
+
+// One task evaluation request (32 B, SURVEY §8(d) task record).
+struct TaskRec {
+  double req[3];
+  int32_t cls;
+  int32_t pad;
+};
+
+// Node row written back after the host commits placements (AddTask delta).
+struct NodeDelta {
+  int32_t node;
+  int32_t ntasks;
+  double idle[3];
+  double rel[3];
+};
+
+// ---- static predicate programs (built on host, evaluated on device) ----
+enum ReqKind : int32_t {
+  REQ_FALSE = 0,
+  REQ_TRUE = 1,
+  REQ_ALL = 2,      // (label_bits & mask) == mask
+  REQ_ANY = 3,      // (label_bits & mask) != 0
+  REQ_NONE = 4,     // (label_bits & mask) == 0
+  REQ_GT = 5,       // numeric label column > value
+  REQ_LT = 6,       // numeric label column < value
+  REQ_NAME_EQ = 7,  // node name id == value
+  REQ_NAME_NE = 8,  // node name id != value
+};
+
+struct ReqProg {
+  int32_t kind;
+  int32_t mask_off;  // offset (in u64 words) into the mask pool, label_words wide
+  int32_t col;       // numeric column for GT/LT
+  int32_t pad;
+  int64_t value;
+};
+
+struct TermProg {
+  int32_t req_off, req_len;  // AND of reqs; a skipped term is not emitted
+};
+
+struct ClassProg {
+  int32_t sel_req;           // index of the nodeSelector requirement, -1 = none
+  int32_t has_affinity;      // required node affinity present: OR over terms
+  int32_t term_off, term_len;
+  int32_t tol_off;           // offset into the tolerated-mask pool (taint_words wide)
+  int32_t always;            // 1 = predicate always true for this class (predicates inactive)
+};
+
+struct StaticTables {
+  int32_t n_nodes;
+  int32_t label_words;       // u64 words per node label bitset
+  int32_t taint_words;       // u64 words per node taint bitset
+  int32_t n_numcols;
+  const uint64_t* label_bits;    // [label_words][N]  (word-major => coalesced)
+  const uint64_t* taint_bits;    // [taint_words][N]
+  const int64_t* num_vals;       // [n_numcols][N]
+  const uint8_t* num_ok;         // [n_numcols][N]
+  const int32_t* name_id;        // [N]
+  const uint8_t* node_flags;     // [N] bit0 = unschedulable, bit1 = nil Node, bit2 = ghost-failed
+  const uint64_t* mask_pool;
+  const uint64_t* tol_pool;
+  const ReqProg* reqs;
+  const TermProg* terms;
+  const ClassProg* classes;
+};
+
+enum NodeFlag : uint8_t { NF_UNSCHED = 1, NF_NIL = 2, NF_DEAD = 4 };
+
+// ---- launchers (all asynchronous on `stream`) ----
+hipError_t launch_build_class_mask(const StaticTables& t, int32_t n_classes, int32_t W, uint64_t* class_mask,
+                                   hipStream_t stream);
+
+hipError_t launch_scan(const NodeSoA& n, int32_t n_nodes, int32_t W, const uint64_t* class_mask, const TaskRec* tasks,
+                       int32_t n_tasks, int32_t cap_check, uint64_t* out_feas, uint64_t* out_idle, hipStream_t stream);
+
+hipError_t launch_select(const uint64_t* feas, const uint64_t* idlem, int32_t W, int32_t n_tasks, int32_t M,
+                         uint32_t* out_cand, uint32_t* out_count, hipStream_t stream);
+
+hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream);
+
+}  // namespace kbg

@@ -1,0 +1,238 @@
+// HIP kernels of the MI355X allocate path (gfx950, wave64).
+//
+// kbg_scan_kernel   — the hot kernel: for a batch of task evaluations, the
+//                     feasibility of every (task, node) pair exactly as the
+//                     reference's node loop decides it (allocate.go:119-162):
+//                       PredicateFn == nil (predicates.go:121-201, resolved
+//                       statically into class_mask + the dynamic pod-count cap
+//                       predicates.go:125-127)
+//                     && (Resreq.LessEqual(Idle) || Resreq.LessEqual(Releasing))
+//                     (resource_info.go:142-146). One wave = 64 consecutive
+//                     nodes held in registers; tasks are wave-uniform (scalar
+//                     loads); results leave as 64-bit ballots.
+// kbg_select_kernel — per task, the first M feasible node indices in
+//                     ssn.Nodes order (first-fit = min index), with
+//                     the Allocate/Pipeline kind of each.
+// kbg_mask_kernel   — session-open static predicate masks (class x node bits).
+// kbg_apply_kernel  — NodeInfo.AddTask deltas committed by the host.
+//
+// fp64 is compared with the reference's own expression; the file is compiled
+// with -ffp-contract=off so nothing is fused.
+#include "kbg_device.hpp"
+
+namespace kbg {
+
+__device__ __forceinline__ bool le(double r, double a, double mn) {
+  // (r < a || |a - r| < min)  — resource_info.go:142-146, one dimension
+  return r < a || fabs(a - r) < mn;
+}
+
+// ------------------------------------------------------------------ scan
+constexpr int kScanWaves = 4;          // waves per workgroup (256 threads)
+constexpr int kScanTasksPerBlock = 64; // task evaluations per workgroup
+
+__global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, int32_t n_nodes, int32_t W,
+                                                       const uint64_t* __restrict__ class_mask,
+                                                       const TaskRec* __restrict__ tasks, int32_t n_tasks,
+                                                       int32_t cap_check, uint64_t* __restrict__ out_feas,
+                                                       uint64_t* __restrict__ out_idle) {
+  const int lane = threadIdx.x & 63;
+  const int chunk = blockIdx.x * kScanWaves + (threadIdx.x >> 6);
+  if (chunk >= W) return;  // wave-uniform exit
+  const int node = chunk * 64 + lane;
+  const bool valid = node < n_nodes;
+  double ic = 0, im = 0, ig = 0, rc = 0, rm = 0, rg = 0;
+  int32_t nt = 0, mt = 0;
+  if (valid) {
+    ic = nd.idle_cpu[node];
+    im = nd.idle_mem[node];
+    ig = nd.idle_gpu[node];
+    rc = nd.rel_cpu[node];
+    rm = nd.rel_mem[node];
+    rg = nd.rel_gpu[node];
+    nt = nd.ntasks[node];
+    mt = nd.maxtasks[node];
+  }
+  const bool node_ok = valid && (!cap_check || nt < mt);
+  const int t0 = blockIdx.y * kScanTasksPerBlock;
+  const int t1 = min(n_tasks, t0 + kScanTasksPerBlock);
+  for (int t = t0; t < t1; ++t) {
+    const double q0 = tasks[t].req[0];
+    const double q1 = tasks[t].req[1];
+    const double q2 = tasks[t].req[2];
+    const int32_t cls = tasks[t].cls;
+    const uint64_t mw = class_mask[(size_t)cls * W + chunk];
+    const bool sbit = (mw >> lane) & 1ull;
+    const bool ifit = le(q0, ic, kMinMilliCPU) && le(q1, im, kMinMemory) && le(q2, ig, kMinMilliGPU);
+    const bool rfit = le(q0, rc, kMinMilliCPU) && le(q1, rm, kMinMemory) && le(q2, rg, kMinMilliGPU);
+    const bool feas = node_ok && sbit && (ifit || rfit);
+    const uint64_t fm = __ballot(feas);
+    const uint64_t imk = __ballot(feas && ifit);
+    if (lane == 0) {
+      out_feas[(size_t)t * W + chunk] = fm;
+      out_idle[(size_t)t * W + chunk] = imk;
+    }
+  }
+}
+
+hipError_t launch_scan(const NodeSoA& n, int32_t n_nodes, int32_t W, const uint64_t* class_mask, const TaskRec* tasks,
+                       int32_t n_tasks, int32_t cap_check, uint64_t* out_feas, uint64_t* out_idle,
+                       hipStream_t stream) {
+  if (n_tasks <= 0 || W <= 0) return hipSuccess;
+  dim3 grid((W + kScanWaves - 1) / kScanWaves, (n_tasks + kScanTasksPerBlock - 1) / kScanTasksPerBlock);
+  hipLaunchKernelGGL(kbg_scan_kernel, grid, dim3(64 * kScanWaves), 0, stream, n, n_nodes, W, class_mask, tasks,
+                     n_tasks, cap_check, out_feas, out_idle);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- select
+__global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restrict__ feas,
+                                                         const uint64_t* __restrict__ idlem, int32_t W,
+                                                         int32_t n_tasks, int32_t M, uint32_t* __restrict__ out_cand,
+                                                         uint32_t* __restrict__ out_count) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= n_tasks) return;
+  const uint64_t* frow = feas + (size_t)t * W;
+  const uint64_t* irow = idlem + (size_t)t * W;
+  int found = 0;
+  int base = 0;
+  for (; base < W && found < M; base += 64) {
+    const int c = base + lane;
+    uint64_t f = c < W ? frow[c] : 0ull;
+    const uint64_t iw = c < W ? irow[c] : 0ull;
+    const int pc = __popcll(f);
+    int incl = pc;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += v;
+    }
+    const int total = __shfl(incl, 63, 64);
+    int r = found + incl - pc;
+    while (f != 0ull && r < M) {
+      const int b = __ffsll((unsigned long long)f) - 1;
+      f &= f - 1ull;
+      const uint32_t kind = ((iw >> b) & 1ull) ? 0u : kCandPipelineBit;
+      out_cand[(size_t)t * M + r] = (uint32_t)(c * 64 + b) | kind;
+      ++r;
+    }
+    found += total;
+  }
+  if (lane == 0) {
+    const bool complete = base >= W && found <= M;
+    const uint32_t cnt = (uint32_t)(found < M ? found : M);
+    out_count[t] = cnt | (complete ? 0u : kCountIncompleteBit);
+  }
+}
+
+hipError_t launch_select(const uint64_t* feas, const uint64_t* idlem, int32_t W, int32_t n_tasks, int32_t M,
+                         uint32_t* out_cand, uint32_t* out_count, hipStream_t stream) {
+  if (n_tasks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kbg_select_kernel, dim3((n_tasks + 3) / 4), dim3(256), 0, stream, feas, idlem, W, n_tasks, M,
+                     out_cand, out_count);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------- apply
+__global__ __launch_bounds__(256) void kbg_apply_kernel(NodeSoA nd, const NodeDelta* __restrict__ d, int32_t n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int node = d[i].node;
+  nd.idle_cpu[node] = d[i].idle[0];
+  nd.idle_mem[node] = d[i].idle[1];
+  nd.idle_gpu[node] = d[i].idle[2];
+  nd.rel_cpu[node] = d[i].rel[0];
+  nd.rel_mem[node] = d[i].rel[1];
+  nd.rel_gpu[node] = d[i].rel[2];
+  nd.ntasks[node] = d[i].ntasks;
+}
+
+hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream) {
+  if (n_deltas <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kbg_apply_kernel, dim3((n_deltas + 255) / 256), dim3(256), 0, stream, n, deltas, n_deltas);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------- static mask
+// One lane = one (class, node) pair; vendor predicates.go:807-850 (selector +
+// required node affinity), predicates.go:105-110 (unschedulable),
+// predicates.go:1489-1517 (taints), with requirement validity already folded
+// into the program on the host.
+__device__ bool eval_req(const StaticTables& t, const ReqProg& r, int node) {
+  switch (r.kind) {
+    case REQ_FALSE: return false;
+    case REQ_TRUE: return true;
+    case REQ_ALL:
+    case REQ_ANY:
+    case REQ_NONE: {
+      bool any = false, all = true;
+      for (int w = 0; w < t.label_words; ++w) {
+        const uint64_t m = t.mask_pool[r.mask_off + w];
+        const uint64_t b = t.label_bits[(size_t)w * t.n_nodes + node] & m;
+        any |= b != 0ull;
+        all &= b == m;
+      }
+      return r.kind == REQ_ALL ? all : (r.kind == REQ_ANY ? any : !any);
+    }
+    case REQ_GT:
+    case REQ_LT: {
+      const size_t k = (size_t)r.col * t.n_nodes + node;
+      if (!t.num_ok[k]) return false;
+      return r.kind == REQ_GT ? t.num_vals[k] > r.value : t.num_vals[k] < r.value;
+    }
+    case REQ_NAME_EQ: return (int64_t)t.name_id[node] == r.value;
+    case REQ_NAME_NE: return (int64_t)t.name_id[node] != r.value;
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void kbg_mask_kernel(StaticTables t, int32_t W, uint64_t* __restrict__ class_mask) {
+  const int lane = threadIdx.x & 63;
+  const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int cls = blockIdx.y;
+  if (chunk >= W) return;
+  const int node = chunk * 64 + lane;
+  bool ok = false;
+  if (node < t.n_nodes) {
+    const ClassProg c = t.classes[cls];
+    const uint8_t fl = t.node_flags[node];
+    if (c.always) {
+      ok = true;
+    } else if (fl & NF_NIL) {
+      ok = true;  // SetNode(nil) panics before any check: the host reports it when reached
+    } else if (fl & (NF_UNSCHED | NF_DEAD)) {
+      ok = false;
+    } else {
+      ok = true;
+      if (c.sel_req >= 0) ok = eval_req(t, t.reqs[c.sel_req], node);
+      if (ok && c.has_affinity) {
+        bool any_term = false;
+        for (int i = 0; i < c.term_len && !any_term; ++i) {
+          const TermProg tp = t.terms[c.term_off + i];
+          bool all = true;
+          for (int j = 0; j < tp.req_len && all; ++j) all = eval_req(t, t.reqs[tp.req_off + j], node);
+          any_term = all;
+        }
+        ok = any_term;
+      }
+      if (ok) {
+        for (int w = 0; w < t.taint_words; ++w) {
+          const uint64_t nb = t.taint_bits[(size_t)w * t.n_nodes + node];
+          if (nb & ~t.tol_pool[c.tol_off + w]) { ok = false; break; }
+        }
+      }
+    }
+  }
+  const uint64_t m = __ballot(ok);
+  if (lane == 0) class_mask[(size_t)cls * W + chunk] = m;
+}
+
+hipError_t launch_build_class_mask(const StaticTables& t, int32_t n_classes, int32_t W, uint64_t* class_mask,
+                                   hipStream_t stream) {
+  if (n_classes <= 0 || W <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kbg_mask_kernel, dim3((W + 3) / 4, n_classes), dim3(256), 0, stream, t, W, class_mask);
+  return hipGetLastError();
+}
+
+}  // namespace kbg

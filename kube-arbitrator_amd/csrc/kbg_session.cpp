@@ -1,0 +1,1117 @@
+// Session open, ordering engine, speculative batch driver and the C ABI of
+// the MI355X allocate path.
+//
+// Split of work:
+//   host   — the reference's control flow, exactly: util.PriorityQueue over
+//            Go 1.11 container/heap (util/priority_queue.go:25-88) for queues,
+//            per-queue jobs and per-job tasks; the session tier walks
+//            (session_plugins.go:142-295); drf/proportion/gang/priority state
+//            (drf.go, proportion.go, gang.go, priority.go). Cost: O(log J)
+//            integer/fp64 compares per placement.
+//   device — the O(N) part: every (task, node) feasibility test of the node
+//            loop (allocate.go:119-162), as a batched scan kernel over the
+//            HBM-resident node table, and the first-M candidate extraction.
+//
+// Why batching is exact: during allocate a node's Idle,
+// Releasing and pod count only move in the "less feasible" direction, and the
+// static predicate never changes, so a node infeasible for a task at batch
+// start stays infeasible. The task ORDER depends only on whether earlier
+// tasks were placed, never on where. So the host predicts the next K task
+// evaluations (success unless a task of the same shape already failed), the
+// device evaluates all of them against the batch-start table, and the host
+// commits in order: a task takes its first candidate that no earlier commit
+// in the batch touched, re-checking touched candidates against the host
+// mirror. An unpredicted outcome or an exhausted candidate list cuts the
+// batch; the engine is restored from a checkpoint and replayed to the cut.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "kbg_session.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+kbg_status fail(kbg_status code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess) return fail(KBG_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+using kbg::Engine;
+using kbg::Res;
+using kbg::Session;
+
+inline Res to_res(const kbg_resource& r) { return Res{r.milli_cpu, r.memory, r.milli_gpu}; }
+inline kbg_resource to_kres(const Res& r) { return kbg_resource{r.c, r.m, r.g}; }
+
+bool allocated_status(int32_t s) {  // api/helpers.go:63-70
+  return s == KBG_BOUND || s == KBG_BINDING || s == KBG_RUNNING || s == KBG_ALLOCATED;
+}
+bool ready_status(int32_t s) {  // gang.go:44-55
+  return allocated_status(s) || s == KBG_SUCCEEDED || s == KBG_PIPELINED;
+}
+
+// drf.go:156-166 / proportion.go:225-237 with helpers.Share (helpers/helpers.go:35-48)
+double share_of(const Res& a, const Res& tot) {
+  auto sh = [](double l, double r) { return r == 0 ? (l == 0 ? 0.0 : 1.0) : l / r; };
+  double res = 0;
+  double s = sh(a.c, tot.c);
+  if (s > res) res = s;
+  s = sh(a.m, tot.m);
+  if (s > res) res = s;
+  s = sh(a.g, tot.g);
+  if (s > res) res = s;
+  return res;
+}
+
+// Go math.Min
+double go_min(double x, double y) {
+  if (std::isinf(x) && x < 0) return x;
+  if (std::isinf(y) && y < 0) return y;
+  if (std::isnan(x) || std::isnan(y)) return NAN;
+  if (x == 0 && x == y) return std::signbit(x) ? x : y;
+  return x < y ? x : y;
+}
+
+// ---------------------------------------------------------------- heaps
+// Go container/heap: up/down exactly (j-1)/2 truncating, right-child rule
+// selectable (Go <= 1.11 "!Less(j1,j2)", later "Less(j2,j1)").
+template <class L>
+inline void go_up(int32_t* h, int j, L less) {
+  for (;;) {
+    const int i = (j - 1) / 2;
+    if (i == j || !less(h[j], h[i])) break;
+    std::swap(h[i], h[j]);
+    j = i;
+  }
+}
+template <class L>
+inline void go_down(int32_t* h, int i0, int n, L less, bool go111) {
+  int i = i0;
+  for (;;) {
+    const int j1 = 2 * i + 1;
+    if (j1 >= n || j1 < 0) break;
+    int j = j1;
+    const int j2 = j1 + 1;
+    if (j2 < n && (go111 ? !less(h[j1], h[j2]) : less(h[j2], h[j1]))) j = j2;
+    if (!less(h[j], h[i])) break;
+    std::swap(h[i], h[j]);
+    i = j;
+  }
+}
+
+struct Ops {
+  const Session& S;
+  Engine& E;
+
+  bool job_ready(int32_t j) const { return E.jready[j] >= S.jobs_in[j].min_available; }
+
+  // Session.JobOrderFn (session_plugins.go:196-221) over the configured tiers.
+  bool job_less(int32_t a, int32_t b) const {
+    const kbg_job& ja = S.jobs_in[a];
+    const kbg_job& jb = S.jobs_in[b];
+    for (int32_t p : S.job_chain) {
+      if (p == kbg::JO_PRIORITY) {  // priority.go:58-74
+        if (ja.priority > jb.priority) return true;
+        if (ja.priority < jb.priority) return false;
+      } else if (p == kbg::JO_GANG) {  // gang.go:129-163
+        const bool ra = job_ready(a), rb = job_ready(b);
+        if (ra && rb) continue;
+        if (ra) return false;
+        if (rb) return true;
+        if (ja.creation_ns == jb.creation_ns) return S.job_rank[a] < S.job_rank[b];
+        return ja.creation_ns < jb.creation_ns;
+      } else {  // drf.go:109-125
+        const double sa = E.jshare[a], sb = E.jshare[b];
+        if (sa == sb) continue;
+        return sa < sb;
+      }
+    }
+    if (ja.creation_ns == jb.creation_ns) return S.job_rank[a] < S.job_rank[b];
+    return ja.creation_ns < jb.creation_ns;
+  }
+  // Session.QueueOrderFn (session_plugins.go:223-245); proportion.go:146-159
+  bool queue_less(int32_t a, int32_t b) const {
+    if (S.queue_order_prop) {
+      const double sa = E.qshare[a], sb = E.qshare[b];
+      if (sa != sb) return sa < sb;
+    }
+    return S.queue_rank[a] < S.queue_rank[b];
+  }
+  // proportion.go:188-193
+  bool overused(int32_t q) const {
+    if (!S.has_prop || !S.q_has_attr[q]) return false;
+    return kbg::res_le(S.q_deserved[q], E.qalloc[q]);
+  }
+  void qpush(int32_t q) {
+    E.qheap.push_back(q);
+    go_up(E.qheap.data(), (int)E.qheap.size() - 1, [this](int32_t x, int32_t y) { return queue_less(x, y); });
+  }
+  int32_t qpop() {
+    const int n = (int)E.qheap.size() - 1;
+    std::swap(E.qheap[0], E.qheap[n]);
+    go_down(E.qheap.data(), 0, n, [this](int32_t x, int32_t y) { return queue_less(x, y); }, S.heap_go111);
+    const int32_t q = E.qheap.back();
+    E.qheap.pop_back();
+    return q;
+  }
+  void jpush(int32_t q, int32_t j) {
+    int32_t* h = E.jheap.data() + S.joff[q];
+    const int n = E.jlen[q]++;
+    h[n] = j;
+    go_up(h, n, [this](int32_t x, int32_t y) { return job_less(x, y); });
+  }
+  int32_t jpop(int32_t q) {
+    int32_t* h = E.jheap.data() + S.joff[q];
+    const int n = --E.jlen[q];
+    std::swap(h[0], h[n]);
+    go_down(h, 0, n, [this](int32_t x, int32_t y) { return job_less(x, y); }, S.heap_go111);
+    return h[n];
+  }
+
+  // allocate.go:65-112: advance the control flow to the next task whose node
+  // loop has to run; -1 when the queue heap is exhausted.
+  int32_t next_task() {
+    for (;;) {
+      if (E.in_job) {
+        const int32_t j = E.cur_j;
+        if (E.cursor[j] < S.pend_len[j]) return S.pend[S.pend_off[j] + E.cursor[j]++];
+        qpush(E.cur_q);  // no task of the job fitted: allocate.go:173-174
+        E.in_job = false;
+        continue;
+      }
+      if (E.qheap.empty()) return -1;
+      const int32_t q = qpop();
+      if (overused(q)) continue;     // :71-74
+      if (E.jlen[q] == 0) continue;  // :78-81
+      E.cur_j = jpop(q);             // :85
+      E.cur_q = q;
+      E.in_job = true;
+    }
+  }
+  // Outcome of the node loop for the task returned by next_task().
+  // Success = ssn.Allocate / ssn.Pipeline: drf + proportion AllocateFunc
+  // (drf.go:131-139, proportion.go:197-206), then jobs.Push / queues.Push.
+  void apply(int32_t t, bool success) {
+    if (!success) return;
+    const int32_t j = E.cur_j, q = E.cur_q;
+    const Res& r = S.treq[t];
+    if (S.has_drf) {
+      kbg::res_add(E.jalloc[j], r);
+      E.jshare[j] = share_of(E.jalloc[j], S.drf_total);
+    }
+    if (S.has_prop) {
+      const int32_t jq = S.job_queue[j];
+      kbg::res_add(E.qalloc[jq], r);
+      E.qshare[jq] = share_of(E.qalloc[jq], S.q_deserved[jq]);
+    }
+    E.jready[j]++;
+    jpush(q, j);  // :164-168
+    qpush(q);     // :174
+    E.in_job = false;
+  }
+};
+
+struct ShapeKey {
+  int32_t cls;
+  double c, m, g;
+  bool operator==(const ShapeKey& o) const {
+    return cls == o.cls && std::memcmp(&c, &o.c, 8) == 0 && std::memcmp(&m, &o.m, 8) == 0 && std::memcmp(&g, &o.g, 8) == 0;
+  }
+};
+struct ShapeHash {
+  size_t operator()(const ShapeKey& k) const {
+    uint64_t h = (uint64_t)k.cls * 0x9E3779B97F4A7C15ull;
+    uint64_t v;
+    std::memcpy(&v, &k.c, 8);
+    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    std::memcpy(&v, &k.m, 8);
+    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    std::memcpy(&v, &k.g, 8);
+    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    return (size_t)h;
+  }
+};
+
+// ---------------------------------------------------------------- device
+template <class T>
+kbg_status dalloc(Session& S, T** p, size_t count) {
+  void* q = nullptr;
+  if (count == 0) count = 1;
+  HIP_TRY(hipMalloc(&q, count * sizeof(T)));
+  S.d_allocs.push_back(q);
+  *p = (T*)q;
+  return KBG_OK;
+}
+template <class T>
+kbg_status hupload(Session& S, T** p, const std::vector<T>& v) {
+  kbg_status st = dalloc(S, p, v.size());
+  if (st != KBG_OK) return st;
+  if (!v.empty()) HIP_TRY(hipMemcpyAsync(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, S.stream));
+  return KBG_OK;
+}
+
+kbg_status alloc_soa(Session& S, kbg::NodeSoA* soa) {
+  const size_t N = (size_t)S.n_nodes;
+  kbg_status st;
+  if ((st = dalloc(S, &soa->idle_cpu, N)) || (st = dalloc(S, &soa->idle_mem, N)) || (st = dalloc(S, &soa->idle_gpu, N)) ||
+      (st = dalloc(S, &soa->rel_cpu, N)) || (st = dalloc(S, &soa->rel_mem, N)) || (st = dalloc(S, &soa->rel_gpu, N)) ||
+      (st = dalloc(S, &soa->ntasks, N)) || (st = dalloc(S, &soa->maxtasks, N)))
+    return st;
+  return KBG_OK;
+}
+
+kbg_status copy_soa(Session& S, const kbg::NodeSoA& dst, const kbg::NodeSoA& src) {
+  const size_t N = (size_t)S.n_nodes;
+  HIP_TRY(hipMemcpyAsync(dst.idle_cpu, src.idle_cpu, N * 8, hipMemcpyDeviceToDevice, S.stream));
+  HIP_TRY(hipMemcpyAsync(dst.idle_mem, src.idle_mem, N * 8, hipMemcpyDeviceToDevice, S.stream));
+  HIP_TRY(hipMemcpyAsync(dst.idle_gpu, src.idle_gpu, N * 8, hipMemcpyDeviceToDevice, S.stream));
+  HIP_TRY(hipMemcpyAsync(dst.rel_cpu, src.rel_cpu, N * 8, hipMemcpyDeviceToDevice, S.stream));
+  HIP_TRY(hipMemcpyAsync(dst.rel_mem, src.rel_mem, N * 8, hipMemcpyDeviceToDevice, S.stream));
+  HIP_TRY(hipMemcpyAsync(dst.rel_gpu, src.rel_gpu, N * 8, hipMemcpyDeviceToDevice, S.stream));
+  HIP_TRY(hipMemcpyAsync(dst.ntasks, src.ntasks, N * 4, hipMemcpyDeviceToDevice, S.stream));
+  HIP_TRY(hipMemcpyAsync(dst.maxtasks, src.maxtasks, N * 4, hipMemcpyDeviceToDevice, S.stream));
+  return KBG_OK;
+}
+
+void free_device(Session& S) {
+  if (S.h_tasks) (void)hipHostFree(S.h_tasks);
+  if (S.h_cand) (void)hipHostFree(S.h_cand);
+  if (S.h_count) (void)hipHostFree(S.h_count);
+  if (S.h_deltas) (void)hipHostFree(S.h_deltas);
+  S.h_tasks = nullptr;
+  S.h_cand = S.h_count = nullptr;
+  S.h_deltas = nullptr;
+  for (void* p : S.d_allocs) (void)hipFree(p);
+  S.d_allocs.clear();
+  for (auto& e : S.ev)
+    if (e) {
+      (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+  if (S.stream) (void)hipStreamDestroy(S.stream);
+  S.stream = nullptr;
+}
+
+// Node state as the device scans it: a nil Node under an active predicates
+// plugin is "always feasible" so the first scan reaching it reports the
+// reference's panic (predicates.go:122-123 SetNode(nil)).
+void device_row(const Session& S, int32_t n, double* ic, double* im, double* ig, double* rc, double* rm, double* rg,
+                int32_t* nt, int32_t* mt) {
+  if (S.nil_node[n] && S.pred_active) {
+    *ic = *im = *ig = INFINITY;
+    *rc = *rm = *rg = 0;
+    *nt = 0;
+    *mt = INT32_MAX;
+    return;
+  }
+  *ic = S.idle[n].c;
+  *im = S.idle[n].m;
+  *ig = S.idle[n].g;
+  *rc = S.rel[n].c;
+  *rm = S.rel[n].m;
+  *rg = S.rel[n].g;
+  *nt = S.ntasks[n];
+  *mt = S.maxtasks[n];
+}
+
+kbg_status upload_nodes(Session& S) {
+  const int32_t N = S.n_nodes;
+  std::vector<double> ic(N), im(N), ig(N), rc(N), rm(N), rg(N);
+  std::vector<int32_t> nt(N), mt(N);
+  for (int32_t n = 0; n < N; ++n) device_row(S, n, &ic[n], &im[n], &ig[n], &rc[n], &rm[n], &rg[n], &nt[n], &mt[n]);
+  auto up = [&](void* d, const void* h, size_t b) { return hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, S.stream); };
+  HIP_TRY(up(S.d_nodes0.idle_cpu, ic.data(), N * 8));
+  HIP_TRY(up(S.d_nodes0.idle_mem, im.data(), N * 8));
+  HIP_TRY(up(S.d_nodes0.idle_gpu, ig.data(), N * 8));
+  HIP_TRY(up(S.d_nodes0.rel_cpu, rc.data(), N * 8));
+  HIP_TRY(up(S.d_nodes0.rel_mem, rm.data(), N * 8));
+  HIP_TRY(up(S.d_nodes0.rel_gpu, rg.data(), N * 8));
+  HIP_TRY(up(S.d_nodes0.ntasks, nt.data(), N * 4));
+  HIP_TRY(up(S.d_nodes0.maxtasks, mt.data(), N * 4));
+  HIP_TRY(hipStreamSynchronize(S.stream));  // host vectors die here
+  return copy_soa(S, S.d_nodes, S.d_nodes0);
+}
+
+// Evaluates tasks[0..n) (n <= K) on the device against the current table.
+kbg_status device_scan(Session& S, const int32_t* tasks, int32_t n) {
+  for (int32_t i = 0; i < n; ++i) {
+    const int32_t t = tasks[i];
+    kbg::TaskRec& r = S.h_tasks[i];
+    r.req[0] = S.treq[t].c;
+    r.req[1] = S.treq[t].m;
+    r.req[2] = S.treq[t].g;
+    r.cls = S.task_class[t];
+    r.pad = 0;
+  }
+  HIP_TRY(hipMemcpyAsync(S.d_tasks, S.h_tasks, (size_t)n * sizeof(kbg::TaskRec), hipMemcpyHostToDevice, S.stream));
+  HIP_TRY(hipEventRecord(S.ev[0], S.stream));
+  HIP_TRY(kbg::launch_scan(S.d_nodes, S.n_nodes, S.W, S.d_class_mask, S.d_tasks, n, S.pred_active ? 1 : 0, S.d_feas,
+                           S.d_idlem, S.stream));
+  HIP_TRY(hipEventRecord(S.ev[1], S.stream));
+  HIP_TRY(kbg::launch_select(S.d_feas, S.d_idlem, S.W, n, S.M, S.d_cand, S.d_count, S.stream));
+  HIP_TRY(hipEventRecord(S.ev[2], S.stream));
+  HIP_TRY(hipMemcpyAsync(S.h_count, S.d_count, (size_t)n * 4, hipMemcpyDeviceToHost, S.stream));
+  HIP_TRY(hipMemcpyAsync(S.h_cand, S.d_cand, (size_t)n * S.M * 4, hipMemcpyDeviceToHost, S.stream));
+  HIP_TRY(hipStreamSynchronize(S.stream));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, S.ev[0], S.ev[1]));
+  S.stats.scan_kernel_ms += ms;
+  HIP_TRY(hipEventElapsedTime(&ms, S.ev[1], S.ev[2]));
+  S.stats.select_kernel_ms += ms;
+  S.stats.scan_launches++;
+  S.stats.evaluations += n;
+  S.stats.node_visits += (int64_t)n * S.n_nodes;
+  return KBG_OK;
+}
+
+// Writes the rows of the nodes touched by the last commits back to HBM.
+kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
+  size_t done = 0;
+  while (done < touched.size()) {
+    const size_t cnt = std::min<size_t>(touched.size() - done, (size_t)S.K);
+    for (size_t i = 0; i < cnt; ++i) {
+      const int32_t n = touched[done + i];
+      kbg::NodeDelta& d = S.h_deltas[i];
+      int32_t mt;
+      d.node = n;
+      device_row(S, n, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &mt);
+    }
+    HIP_TRY(hipMemcpyAsync(S.d_deltas, S.h_deltas, cnt * sizeof(kbg::NodeDelta), hipMemcpyHostToDevice, S.stream));
+    HIP_TRY(kbg::launch_apply(S.d_nodes, S.d_deltas, (int32_t)cnt, S.stream));
+    HIP_TRY(hipStreamSynchronize(S.stream));  // the pinned staging buffer is reused
+    done += cnt;
+  }
+  return KBG_OK;
+}
+
+// Sequential commit of one task against its batch-start candidate list.
+enum { RES_OK = 0, RES_TRUNC = 1, RES_PANIC = 2 };
+struct Resolver {
+  Session& S;
+  std::vector<int32_t>& mark;
+  int32_t stamp;
+  int resolve(int32_t i, int32_t t, int32_t* node, int32_t* kind) {
+    const uint32_t cnt = S.h_count[i];
+    const int32_t n = (int32_t)(cnt & kbg::kCountMask);
+    const uint32_t* c = S.h_cand + (size_t)i * S.M;
+    const Res& r = S.treq[t];
+    for (int32_t k = 0; k < n; ++k) {
+      const int32_t nd = (int32_t)(c[k] & ~kbg::kCandPipelineBit);
+      if (S.nil_node[nd] && S.pred_active) return RES_PANIC;
+      if (mark[nd] != stamp) {
+        *node = nd;
+        *kind = (c[k] & kbg::kCandPipelineBit) ? KBG_KIND_PIPELINE : KBG_KIND_ALLOCATE;
+        return RES_OK;
+      }
+      // touched by an earlier commit of this batch: re-check on the host mirror
+      if (S.pred_active && S.ntasks[nd] >= S.maxtasks[nd]) continue;
+      if (kbg::res_le(r, S.idle[nd])) {
+        *node = nd;
+        *kind = KBG_KIND_ALLOCATE;
+        return RES_OK;
+      }
+      if (kbg::res_le(r, S.rel[nd])) {
+        *node = nd;
+        *kind = KBG_KIND_PIPELINE;
+        return RES_OK;
+      }
+    }
+    if (cnt & kbg::kCountIncompleteBit) return RES_TRUNC;
+    *node = -1;
+    return RES_OK;
+  }
+};
+
+// NodeInfo.AddTask on the host mirror (node_info.go:101-129): Allocated ->
+// Idle -= req; Pipelined -> Releasing -= req; both add a task.
+void mirror_add(Session& S, int32_t t, int32_t nd, int32_t kind) {
+  if (!S.nil_node[nd]) {
+    if (kind == KBG_KIND_ALLOCATE) kbg::res_sub(S.idle[nd], S.treq[t]);
+    else kbg::res_sub(S.rel[nd], S.treq[t]);
+  }
+  S.ntasks[nd]++;
+}
+
+kbg_status validate(const kbg_snapshot* s) {
+  if (!s) return fail(KBG_E_INVALID, "null snapshot");
+  auto in = [](int32_t v, int32_t n) { return v >= 0 && v < n; };
+  auto range = [](int32_t off, int32_t len, int32_t n) { return off >= 0 && len >= 0 && (int64_t)off + len <= n; };
+  if (s->n_strings < 0 || (s->n_strings > 0 && !s->strings)) return fail(KBG_E_INVALID, "strings");
+  for (int32_t i = 0; i < s->n_strings; ++i)
+    if (!s->strings[i]) return fail(KBG_E_INVALID, "null string " + std::to_string(i));
+  const int32_t NS = s->n_strings;
+  for (int32_t i = 0; i < s->n_nodes; ++i) {
+    const kbg_node& n = s->nodes[i];
+    if (!in(n.name, NS) || !range(n.label_off, n.label_len, s->n_labels) || !range(n.taint_off, n.taint_len, s->n_taints))
+      return fail(KBG_E_INVALID, "node " + std::to_string(i));
+  }
+  for (int32_t i = 0; i < s->n_labels * 2; ++i)
+    if (!in(s->labels[i], NS)) return fail(KBG_E_INVALID, "label string");
+  for (int32_t i = 0; i < s->n_selectors * 2; ++i)
+    if (!in(s->selectors[i], NS)) return fail(KBG_E_INVALID, "selector string");
+  for (int32_t i = 0; i < s->n_taints; ++i) {
+    const kbg_taint& t = s->taints[i];
+    if (!in(t.key, NS) || !in(t.value, NS) || !in(t.effect, NS)) return fail(KBG_E_INVALID, "taint");
+  }
+  for (int32_t i = 0; i < s->n_queues; ++i)
+    if (!in(s->queues[i].uid, NS)) return fail(KBG_E_INVALID, "queue");
+  for (int32_t i = 0; i < s->n_jobs; ++i)
+    if (!in(s->jobs[i].uid, NS) || !in(s->jobs[i].queue, s->n_queues)) return fail(KBG_E_INVALID, "job " + std::to_string(i));
+  for (int32_t i = 0; i < s->n_tasks; ++i) {
+    const kbg_task& t = s->tasks[i];
+    if (!in(t.uid, NS) || !in(t.job, s->n_jobs) || !(t.spec == -1 || in(t.spec, s->n_specs)) || !in(t.node_name, NS))
+      return fail(KBG_E_INVALID, "task " + std::to_string(i));
+    if (t.status <= 0 || t.status > KBG_UNKNOWN || (t.status & (t.status - 1))) return fail(KBG_E_INVALID, "task status");
+  }
+  for (int32_t i = 0; i < s->n_specs; ++i) {
+    const kbg_spec& p = s->specs[i];
+    if (!range(p.selector_off, p.selector_len, s->n_selectors) || !range(p.term_off, p.term_len, s->n_terms) ||
+        !range(p.toleration_off, p.toleration_len, s->n_tolerations))
+      return fail(KBG_E_INVALID, "spec " + std::to_string(i));
+  }
+  for (int32_t i = 0; i < s->n_terms; ++i) {
+    const kbg_term& t = s->terms[i];
+    if (!range(t.expr_off, t.expr_len, s->n_reqs) || !range(t.field_off, t.field_len, s->n_reqs))
+      return fail(KBG_E_INVALID, "term");
+  }
+  for (int32_t i = 0; i < s->n_reqs; ++i) {
+    const kbg_requirement& r = s->reqs[i];
+    if (!in(r.key, NS) || !in(r.op, NS) || !range(r.value_off, r.value_len, s->n_values)) return fail(KBG_E_INVALID, "req");
+  }
+  for (int32_t i = 0; i < s->n_values; ++i)
+    if (!in(s->values[i], NS)) return fail(KBG_E_INVALID, "value");
+  for (int32_t i = 0; i < s->n_tolerations; ++i) {
+    const kbg_toleration& t = s->tolerations[i];
+    if (!in(t.key, NS) || !in(t.op, NS) || !in(t.value, NS) || !in(t.effect, NS)) return fail(KBG_E_INVALID, "toleration");
+  }
+  int32_t np = 0;
+  for (int32_t i = 0; i < s->n_tiers; ++i) {
+    if (s->tier_sizes[i] < 0) return fail(KBG_E_INVALID, "tier size");
+    np += s->tier_sizes[i];
+  }
+  if (np != s->n_plugins) return fail(KBG_E_INVALID, "tier sizes do not sum to n_plugins");
+  for (int32_t i = 0; i < s->n_plugins; ++i)
+    if (!in(s->plugins[i].name, NS)) return fail(KBG_E_INVALID, "plugin name");
+  return KBG_OK;
+}
+
+template <class T>
+std::vector<T> copy_arr(const T* p, int32_t n) {
+  return (p && n > 0) ? std::vector<T>(p, p + n) : std::vector<T>();
+}
+
+std::vector<int32_t> ranks_of(const Session& S, const std::vector<int32_t>& ids) {
+  std::vector<int32_t> idx(ids.size());
+  std::iota(idx.begin(), idx.end(), 0);
+  std::stable_sort(idx.begin(), idx.end(), [&](int32_t a, int32_t b) { return S.strs[ids[a]] < S.strs[ids[b]]; });
+  std::vector<int32_t> rank(ids.size());
+  int32_t r = 0;
+  for (size_t i = 0; i < idx.size(); ++i) {
+    if (i > 0 && S.strs[ids[idx[i]]] != S.strs[ids[idx[i - 1]]]) ++r;
+    rank[idx[i]] = r;
+  }
+  return rank;
+}
+
+kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
+  const auto t_open = std::chrono::steady_clock::now();
+  kbg_status st = validate(snap);
+  if (st != KBG_OK) return st;
+  if (o) S.opts = *o;
+  S.heap_go111 = S.opts.heap_rule == 0;
+  S.K = S.opts.batch_tasks > 0 ? S.opts.batch_tasks : 2048;
+  S.M = S.opts.candidates > 0 ? S.opts.candidates : 32;
+  if (S.M > 4096) return fail(KBG_E_INVALID, "candidates > 4096");
+
+  S.strs.assign(snap->strings, snap->strings + snap->n_strings);
+  {
+    std::unordered_map<std::string, int32_t> first;
+    S.canon.resize(S.strs.size());
+    for (size_t i = 0; i < S.strs.size(); ++i) S.canon[i] = first.emplace(S.strs[i], (int32_t)i).first->second;
+  }
+  S.n_nodes = snap->n_nodes;
+  S.n_jobs = snap->n_jobs;
+  S.n_queues = snap->n_queues;
+  S.n_tasks = snap->n_tasks;
+  S.nodes_in = copy_arr(snap->nodes, snap->n_nodes);
+  S.jobs_in = copy_arr(snap->jobs, snap->n_jobs);
+  S.queues_in = copy_arr(snap->queues, snap->n_queues);
+  S.tasks_in = copy_arr(snap->tasks, snap->n_tasks);
+  S.specs_in = copy_arr(snap->specs, snap->n_specs);
+  S.terms_in = copy_arr(snap->terms, snap->n_terms);
+  S.reqs_in = copy_arr(snap->reqs, snap->n_reqs);
+  S.values_in = copy_arr(snap->values, snap->n_values);
+  S.labels_in = copy_arr(snap->labels, 2 * snap->n_labels);
+  S.selectors_in = copy_arr(snap->selectors, 2 * snap->n_selectors);
+  S.tols_in = copy_arr(snap->tolerations, snap->n_tolerations);
+  S.taints_in = copy_arr(snap->taints, snap->n_taints);
+
+  // ---- plugins (framework.go:26-46; unknown names ignored)
+  {
+    int32_t p = 0;
+    bool seen_prio = false, seen_gang = false, seen_drf = false;
+    for (int32_t ti = 0; ti < snap->n_tiers; ++ti)
+      for (int32_t k = 0; k < snap->tier_sizes[ti]; ++k, ++p) {
+        const kbg_plugin_option& po = snap->plugins[p];
+        const std::string& name = S.strs[po.name];
+        const uint32_t f = po.flags;
+        if (name == "priority") {
+          S.has_prio = true;
+          if (!(f & KBG_DISABLE_TASK_ORDER)) S.task_order_prio = true;
+          if (!(f & KBG_DISABLE_JOB_ORDER) && !seen_prio) { S.job_chain.push_back(kbg::JO_PRIORITY); seen_prio = true; }
+        } else if (name == "gang") {
+          S.has_gang = true;
+          if (!(f & KBG_DISABLE_JOB_READY)) S.ready_gang = true;
+          if (!(f & KBG_DISABLE_JOB_ORDER) && !seen_gang) { S.job_chain.push_back(kbg::JO_GANG); seen_gang = true; }
+        } else if (name == "drf") {
+          S.has_drf = true;
+          if (!(f & KBG_DISABLE_JOB_ORDER) && !seen_drf) { S.job_chain.push_back(kbg::JO_DRF); seen_drf = true; }
+        } else if (name == "proportion") {
+          S.has_prop = true;
+          if (!(f & KBG_DISABLE_QUEUE_ORDER)) S.queue_order_prop = true;
+        } else if (name == "predicates") {
+          if (!(f & KBG_DISABLE_PREDICATE)) S.pred_active = true;
+        }
+      }
+  }
+
+  // ---- ranks, tasks
+  {
+    std::vector<int32_t> ids(S.n_jobs);
+    for (int32_t j = 0; j < S.n_jobs; ++j) ids[j] = S.jobs_in[j].uid;
+    S.job_rank = ranks_of(S, ids);
+    ids.resize(S.n_queues);
+    for (int32_t q = 0; q < S.n_queues; ++q) ids[q] = S.queues_in[q].uid;
+    S.queue_rank = ranks_of(S, ids);
+    ids.resize(S.n_tasks);
+    for (int32_t t = 0; t < S.n_tasks; ++t) ids[t] = S.tasks_in[t].uid;
+    S.task_rank = ranks_of(S, ids);
+  }
+  S.treq.resize(S.n_tasks);
+  S.pending_candidate.assign(S.n_tasks, 0);
+  for (int32_t t = 0; t < S.n_tasks; ++t) {
+    S.treq[t] = to_res(S.tasks_in[t].resreq);
+    // allocate.go:88-96: only Pending, non-BestEffort tasks enter the node loop
+    S.pending_candidate[t] = S.tasks_in[t].status == KBG_PENDING && !kbg::res_empty(S.treq[t]);
+  }
+  S.job_queue.resize(S.n_jobs);
+  for (int32_t j = 0; j < S.n_jobs; ++j) S.job_queue[j] = S.jobs_in[j].queue;
+
+  // ---- nodes
+  const int32_t N = S.n_nodes;
+  S.idle.resize(N);
+  S.rel.resize(N);
+  S.ntasks.resize(N);
+  S.maxtasks.resize(N);
+  S.nil_node.resize(N);
+  for (int32_t n = 0; n < N; ++n) {
+    S.idle[n] = to_res(S.nodes_in[n].idle);
+    S.rel[n] = to_res(S.nodes_in[n].releasing);
+    S.ntasks[n] = S.nodes_in[n].num_tasks;
+    S.maxtasks[n] = S.nodes_in[n].max_task_num;
+    S.nil_node[n] = S.nodes_in[n].has_node ? 0 : 1;
+  }
+  S.idle0 = S.idle;
+  S.rel0 = S.rel;
+  S.ntasks0 = S.ntasks;
+
+  // ---- engine initial state
+  Engine& E = S.init;
+  E.jalloc.assign(S.n_jobs, Res{});
+  E.jshare.assign(S.n_jobs, 0.0);
+  E.jready.assign(S.n_jobs, 0);
+  E.qalloc.assign(S.n_queues, Res{});
+  E.qshare.assign(S.n_queues, 0.0);
+  E.cursor.assign(S.n_jobs, 0);
+  S.q_has_attr.assign(S.n_queues, 0);
+  S.q_deserved.assign(S.n_queues, Res{});
+  S.q_request.assign(S.n_queues, Res{});
+
+  std::vector<std::vector<int32_t>> job_tasks(S.n_jobs);
+  for (int32_t t = 0; t < S.n_tasks; ++t) job_tasks[S.tasks_in[t].job].push_back(t);
+  for (int32_t j = 0; j < S.n_jobs; ++j)
+    for (int32_t t : job_tasks[j])
+      if (ready_status(S.tasks_in[t].status)) E.jready[j]++;
+  S.job_ready0 = E.jready;
+
+  // drf.go:55-78
+  if (S.has_drf) {
+    for (int32_t n = 0; n < N; ++n) kbg::res_add(S.drf_total, to_res(S.nodes_in[n].allocatable));
+    for (int32_t j = 0; j < S.n_jobs; ++j) {
+      for (int32_t t : job_tasks[j])
+        if (allocated_status(S.tasks_in[t].status)) kbg::res_add(E.jalloc[j], S.treq[t]);
+      E.jshare[j] = share_of(E.jalloc[j], S.drf_total);
+    }
+  }
+  // proportion.go:54-144 (queue attrs in order of first job)
+  if (S.has_prop) {
+    for (int32_t n = 0; n < N; ++n) kbg::res_add(S.prop_total, to_res(S.nodes_in[n].allocatable));
+    for (int32_t i = 0; i < snap->n_others; ++i)
+      if (!kbg::res_sub(S.prop_total, to_res(snap->others[i])))
+        return fail(KBG_E_REF_PANIC, "proportion: Others exceed the cluster total (proportion.go:61-63)");
+    std::vector<int32_t> qorder;
+    for (int32_t j = 0; j < S.n_jobs; ++j) {
+      const int32_t q = S.job_queue[j];
+      if (!S.q_has_attr[q]) {
+        S.q_has_attr[q] = 1;
+        qorder.push_back(q);
+      }
+      for (int32_t t : job_tasks[j]) {
+        const int32_t s = S.tasks_in[t].status;
+        if (allocated_status(s)) {
+          kbg::res_add(E.qalloc[q], S.treq[t]);
+          kbg::res_add(S.q_request[q], S.treq[t]);
+        } else if (s == KBG_PENDING) {
+          kbg::res_add(S.q_request[q], S.treq[t]);
+        }
+      }
+    }
+    Res remaining = S.prop_total;
+    std::vector<char> meet(S.n_queues, 0);
+    for (;;) {
+      int32_t total_w = 0;
+      for (int32_t q : qorder)
+        if (!meet[q]) total_w += S.queues_in[q].weight;
+      if (total_w == 0) break;
+      Res deserved;
+      for (int32_t q : qorder) {
+        if (meet[q]) continue;
+        const double ratio = (double)S.queues_in[q].weight / (double)total_w;
+        Res part{remaining.c * ratio, remaining.m * ratio, remaining.g * ratio};
+        kbg::res_add(S.q_deserved[q], part);
+        if (!kbg::res_le(S.q_deserved[q], S.q_request[q])) {
+          const Res d = S.q_deserved[q], r = S.q_request[q];
+          S.q_deserved[q] = Res{go_min(d.c, r.c), go_min(d.m, r.m), go_min(d.g, r.g)};
+          meet[q] = 1;
+        }
+        E.qshare[q] = share_of(E.qalloc[q], S.q_deserved[q]);
+        kbg::res_add(deserved, S.q_deserved[q]);
+      }
+      if (!kbg::res_sub(remaining, deserved))
+        return fail(KBG_E_REF_PANIC, "proportion water-fill: remaining.Sub(deserved) underflow (proportion.go:140, SURVEY F9)");
+      if (kbg::res_empty(remaining)) break;
+    }
+  }
+
+  // ---- predicates preconditions
+  if (S.pred_active) {
+    std::unordered_set<int32_t> names;
+    for (int32_t n = 0; n < N; ++n) names.insert(S.canon[S.nodes_in[n].name]);
+    for (int32_t t = 0; t < S.n_tasks; ++t) {
+      const kbg_task& tk = S.tasks_in[t];
+      const kbg_spec* sp = tk.spec >= 0 ? &S.specs_in[tk.spec] : nullptr;
+      if (sp && sp->has_pod_affinity)
+        return fail(KBG_E_UNSUPPORTED, "inter-pod (anti)affinity present: run the reference predicate path");
+      if (sp && sp->has_host_ports && S.pending_candidate[t])
+        return fail(KBG_E_UNSUPPORTED, "pending task declares hostPort: run the reference predicate path");
+      if (allocated_status(tk.status) && !names.count(S.canon[tk.node_name])) S.ghost = true;
+    }
+  }
+
+  // ---- pending task lists in TaskOrderFn order (session_plugins.go:266-276)
+  S.pend_off.assign(S.n_jobs, 0);
+  S.pend_len.assign(S.n_jobs, 0);
+  S.pend.clear();
+  for (int32_t j = 0; j < S.n_jobs; ++j) {
+    S.pend_off[j] = (int32_t)S.pend.size();
+    for (int32_t t : job_tasks[j])
+      if (S.pending_candidate[t]) S.pend.push_back(t);
+    auto b = S.pend.begin() + S.pend_off[j];
+    std::sort(b, S.pend.end(), [&](int32_t a, int32_t c) {
+      if (S.task_order_prio && S.tasks_in[a].priority != S.tasks_in[c].priority)
+        return S.tasks_in[a].priority > S.tasks_in[c].priority;
+      return S.task_rank[a] < S.task_rank[c];
+    });
+    S.pend_len[j] = (int32_t)S.pend.size() - S.pend_off[j];
+  }
+
+  // ---- per-queue job heaps (allocate.go:45-59)
+  S.joff.assign(S.n_queues, 0);
+  S.jcap.assign(S.n_queues, 0);
+  for (int32_t j = 0; j < S.n_jobs; ++j) S.jcap[S.job_queue[j]]++;
+  for (int32_t q = 1; q < S.n_queues; ++q) S.joff[q] = S.joff[q - 1] + S.jcap[q - 1];
+  E.jheap.assign(S.n_jobs, -1);
+  E.jlen.assign(S.n_queues, 0);
+  E.qheap.clear();
+  E.qheap.reserve(S.n_jobs);
+  {
+    Ops ops{S, E};
+    for (int32_t j = 0; j < S.n_jobs; ++j) {
+      ops.qpush(S.job_queue[j]);
+      ops.jpush(S.job_queue[j], j);
+    }
+  }
+
+  // ---- static predicates
+  kbg::StaticHost sh;
+  compile_static_predicates(S, &sh);
+  S.n_classes = sh.n_classes;
+  S.W = (N + 63) / 64;
+
+  // ---- device
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(KBG_E_HIP, "no HIP device visible");
+  S.device = S.opts.device >= 0 ? S.opts.device : 0;
+  if (S.opts.device < 0) HIP_TRY(hipGetDevice(&S.device));
+  HIP_TRY(hipSetDevice(S.device));
+  HIP_TRY(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
+  for (auto& e : S.ev) HIP_TRY(hipEventCreate(&e));
+  if ((st = alloc_soa(S, &S.d_nodes)) || (st = alloc_soa(S, &S.d_nodes0))) return st;
+  if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) || (st = dalloc(S, &S.d_tasks, S.K)) ||
+      (st = dalloc(S, &S.d_feas, (size_t)S.K * S.W)) || (st = dalloc(S, &S.d_idlem, (size_t)S.K * S.W)) ||
+      (st = dalloc(S, &S.d_cand, (size_t)S.K * S.M)) || (st = dalloc(S, &S.d_count, S.K)) ||
+      (st = dalloc(S, &S.d_deltas, S.K)))
+    return st;
+  HIP_TRY(hipHostMalloc((void**)&S.h_tasks, (size_t)S.K * sizeof(kbg::TaskRec), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&S.h_cand, (size_t)S.K * S.M * 4, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&S.h_count, (size_t)S.K * 4, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&S.h_deltas, (size_t)S.K * sizeof(kbg::NodeDelta), hipHostMallocDefault));
+  if ((st = upload_nodes(S))) return st;
+
+  {
+    kbg::StaticTables t{};
+    uint64_t *lb, *tb, *mp, *tp;
+    int64_t* nv;
+    uint8_t *nok, *nf;
+    int32_t* nid;
+    kbg::ReqProg* rq;
+    kbg::TermProg* tm;
+    kbg::ClassProg* cl;
+    if ((st = hupload(S, &lb, sh.label_bits)) || (st = hupload(S, &tb, sh.taint_bits)) || (st = hupload(S, &mp, sh.mask_pool)) ||
+        (st = hupload(S, &tp, sh.tol_pool)) || (st = hupload(S, &nv, sh.num_vals)) || (st = hupload(S, &nok, sh.num_ok)) ||
+        (st = hupload(S, &nf, sh.node_flags)) || (st = hupload(S, &nid, sh.name_id)) || (st = hupload(S, &rq, sh.reqs)) ||
+        (st = hupload(S, &tm, sh.terms)) || (st = hupload(S, &cl, sh.classes)))
+      return st;
+    t.n_nodes = N;
+    t.label_words = sh.label_words;
+    t.taint_words = sh.taint_words;
+    t.n_numcols = sh.n_numcols;
+    t.label_bits = lb;
+    t.taint_bits = tb;
+    t.num_vals = nv;
+    t.num_ok = nok;
+    t.name_id = nid;
+    t.node_flags = nf;
+    t.mask_pool = mp;
+    t.tol_pool = tp;
+    t.reqs = rq;
+    t.terms = tm;
+    t.classes = cl;
+    HIP_TRY(kbg::launch_build_class_mask(t, S.n_classes, S.W, S.d_class_mask, S.stream));
+    HIP_TRY(hipStreamSynchronize(S.stream));  // sh's host vectors end with this scope
+  }
+  S.stats.n_classes = S.n_classes;
+  S.stats.open_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_open).count();
+  return KBG_OK;
+}
+
+kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
+  if (S.allocated) return fail(KBG_E_INVALID, "kbg_allocate already ran on this session; call kbg_session_reset");
+  const auto t0 = std::chrono::steady_clock::now();
+  S.stats.batches = S.stats.mispredictions = S.stats.truncations = 0;
+  S.stats.evaluations = S.stats.node_visits = S.stats.scan_launches = 0;
+  S.stats.scan_kernel_ms = S.stats.select_kernel_ms = 0;
+
+  Engine E = S.init;
+  Engine ckpt;
+  Ops ops{S, E};
+  std::vector<kbg_decision> dec;
+  dec.reserve(S.pend.size());
+  std::vector<std::vector<int32_t>> undispatched(S.n_jobs);
+  S.committed_ready = S.job_ready0;
+  std::unordered_set<ShapeKey, ShapeHash> failed;
+  std::vector<int32_t> bt, mark(S.n_nodes, -1), touched;
+  std::vector<char> bpred, bactual;
+  bt.reserve(S.K);
+  int32_t stamp = 0;
+  kbg_status result = KBG_OK;
+
+  auto shape = [&](int32_t t) { return ShapeKey{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g}; };
+  auto job_ready_committed = [&](int32_t j) {
+    return !S.ready_gang || S.committed_ready[j] >= S.jobs_in[j].min_available;
+  };
+
+  for (;;) {
+    // 1. predict the next K evaluations
+    ckpt = E;
+    bt.clear();
+    bpred.clear();
+    while ((int32_t)bt.size() < S.K) {
+      const int32_t t = ops.next_task();
+      if (t < 0) break;
+      const bool p = !failed.count(shape(t));
+      bt.push_back(t);
+      bpred.push_back(p);
+      ops.apply(t, p);
+    }
+    if (bt.empty()) break;
+    S.stats.batches++;
+    // 2. device: feasibility scan + first-M candidates against the batch-start table
+    kbg_status st = device_scan(S, bt.data(), (int32_t)bt.size());
+    if (st != KBG_OK) return st;
+    // 3. commit in order
+    ++stamp;
+    touched.clear();
+    bactual.assign(bt.size(), 0);
+    Resolver rs{S, mark, stamp};
+    int32_t cut = -1;
+    bool panic = false;
+    for (int32_t i = 0; i < (int32_t)bt.size(); ++i) {
+      const int32_t t = bt[i];
+      int32_t node = -1, kind = 0;
+      const int r = rs.resolve(i, t, &node, &kind);
+      if (r == RES_TRUNC) {
+        cut = i;
+        S.stats.truncations++;
+        break;
+      }
+      if (r == RES_PANIC) {
+        panic = true;
+        break;
+      }
+      const bool ok = node >= 0;
+      bactual[i] = ok;
+      if (ok) {
+        mirror_add(S, t, node, kind);
+        if (mark[node] != stamp) {
+          mark[node] = stamp;
+          touched.push_back(node);
+        }
+        const int32_t di = (int32_t)dec.size();
+        dec.push_back(kbg_decision{t, node, kind, -1});
+        const int32_t j = S.tasks_in[t].job;
+        S.committed_ready[j]++;
+        if (kind == KBG_KIND_ALLOCATE) {  // session.go:283-290
+          undispatched[j].push_back(di);
+          if (job_ready_committed(j)) {
+            for (int32_t d : undispatched[j]) dec[d].dispatched_at = di;
+            undispatched[j].clear();
+          }
+        }
+      } else {
+        failed.insert(shape(t));
+      }
+      if (ok != (bool)bpred[i]) {
+        cut = i + 1;
+        S.stats.mispredictions++;
+        break;
+      }
+    }
+    if ((st = push_deltas(S, touched)) != KBG_OK) return st;
+    if (panic) {
+      result = fail(KBG_E_REF_PANIC, "allocate reached a node whose NodeInfo.Node is nil with the predicates plugin on "
+                                     "(predicates.go:122-123)");
+      break;
+    }
+    // 4. on a cut, rebuild the engine state at the cut from the checkpoint
+    if (cut >= 0) {
+      E = ckpt;
+      for (int32_t k = 0; k < cut; ++k) {
+        const int32_t t = ops.next_task();
+        if (t != bt[k]) return fail(KBG_E_INVALID, "internal: replay diverged");
+        ops.apply(t, bactual[k]);
+      }
+    }
+  }
+  S.fin = E;
+  S.allocated = true;
+  S.stats.allocate_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (n_out) *n_out = (int32_t)dec.size();
+  if ((int32_t)dec.size() > cap || (!out && !dec.empty())) {
+    if (result == KBG_OK) result = fail(KBG_E_CAPACITY, "decision buffer too small: need " + std::to_string(dec.size()));
+    return result;
+  }
+  if (!dec.empty()) std::memcpy(out, dec.data(), dec.size() * sizeof(kbg_decision));
+  return result;
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" {
+
+int32_t kbg_abi_version(void) { return KBG_ABI_VERSION; }
+
+const char* kbg_last_error(void) { return g_err.c_str(); }
+
+int32_t kbg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+kbg_status kbg_session_open(const kbg_snapshot* snap, const kbg_options* opts, kbg_session** out) {
+  if (!out) return fail(KBG_E_INVALID, "null out");
+  *out = nullptr;
+  kbg_session* s = new (std::nothrow) kbg_session();
+  if (!s) return fail(KBG_E_NOMEM, "session");
+  kbg_status st;
+  try {
+    st = open_session(s->s, snap, opts);
+  } catch (const std::bad_alloc&) {
+    st = fail(KBG_E_NOMEM, "host allocation failed");
+  }
+  if (st != KBG_OK) {
+    free_device(s->s);
+    delete s;
+    return st;
+  }
+  *out = s;
+  return KBG_OK;
+}
+
+kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out) {
+  if (!s) return fail(KBG_E_INVALID, "null session");
+  HIP_TRY(hipSetDevice(s->s.device));
+  try {
+    return allocate_cycle(s->s, out, cap, n_out);
+  } catch (const std::bad_alloc&) {
+    return fail(KBG_E_NOMEM, "host allocation failed");
+  }
+}
+
+kbg_status kbg_session_reset(kbg_session* s) {
+  if (!s) return fail(KBG_E_INVALID, "null session");
+  Session& S = s->s;
+  HIP_TRY(hipSetDevice(S.device));
+  S.idle = S.idle0;
+  S.rel = S.rel0;
+  S.ntasks = S.ntasks0;
+  S.allocated = false;
+  kbg_status st = copy_soa(S, S.d_nodes, S.d_nodes0);
+  if (st != KBG_OK) return st;
+  HIP_TRY(hipStreamSynchronize(S.stream));
+  return KBG_OK;
+}
+
+kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t stop_at_first_success, int32_t* out_node,
+                      int32_t* out_kind, int32_t* n_evaluated) {
+  if (!s || (n > 0 && (!tasks || !out_node))) return fail(KBG_E_INVALID, "null argument");
+  Session& S = s->s;
+  HIP_TRY(hipSetDevice(S.device));
+  for (int32_t i = 0; i < n; ++i)
+    if (tasks[i] < 0 || tasks[i] >= S.n_tasks) return fail(KBG_E_INVALID, "task index");
+  std::vector<int32_t> mark(S.n_nodes, -1), touched;
+  int32_t done = 0;
+  bool stop = false;
+  while (done < n && !stop) {
+    const int32_t cnt = std::min(n - done, S.K);
+    kbg_status st = device_scan(S, tasks + done, cnt);
+    if (st != KBG_OK) return st;
+    touched.clear();
+    Resolver rs{S, mark, 1};
+    int32_t i = 0;
+    for (; i < cnt; ++i) {
+      int32_t node = -1, kind = 0;
+      const int r = rs.resolve(i, tasks[done + i], &node, &kind);
+      if (r == RES_TRUNC) break;  // rescan from this task with the updated table
+      if (r == RES_PANIC) {
+        if ((st = push_deltas(S, touched)) != KBG_OK) return st;
+        if (n_evaluated) *n_evaluated = done + i;
+        return fail(KBG_E_REF_PANIC, "node with nil Node reached (predicates.go:122-123)");
+      }
+      out_node[done + i] = node;
+      if (out_kind) out_kind[done + i] = kind;
+      if (node >= 0) {
+        mirror_add(S, tasks[done + i], node, kind);
+        if (mark[node] != 1) {
+          mark[node] = 1;
+          touched.push_back(node);
+        }
+        if (stop_at_first_success) {
+          ++i;
+          stop = true;
+          break;
+        }
+      }
+    }
+    for (int32_t nd : touched) mark[nd] = -1;
+    if ((st = push_deltas(S, touched)) != KBG_OK) return st;
+    done += i;
+  }
+  if (n_evaluated) *n_evaluated = done;
+  return KBG_OK;
+}
+
+kbg_status kbg_apply(kbg_session* s, int32_t node, const kbg_resource* req, int32_t kind) {
+  if (!s || !req) return fail(KBG_E_INVALID, "null argument");
+  Session& S = s->s;
+  if (node < 0 || node >= S.n_nodes) return fail(KBG_E_INVALID, "node index");
+  HIP_TRY(hipSetDevice(S.device));
+  const Res r = to_res(*req);
+  if (!S.nil_node[node]) {
+    Res& target = kind == KBG_KIND_PIPELINE ? S.rel[node] : S.idle[node];
+    if (!kbg::res_sub(target, r)) return fail(KBG_E_REF_PANIC, "Resource.Sub underflow (resource_info.go:100-110)");
+  }
+  S.ntasks[node]++;
+  return push_deltas(S, std::vector<int32_t>{node});
+}
+
+kbg_status kbg_job_state_get(kbg_session* s, int32_t job, kbg_job_state* out) {
+  if (!s || !out) return fail(KBG_E_INVALID, "null argument");
+  Session& S = s->s;
+  if (job < 0 || job >= S.n_jobs) return fail(KBG_E_INVALID, "job index");
+  const Engine& E = S.allocated ? S.fin : S.init;
+  out->ready_num = S.allocated ? S.committed_ready[job] : S.job_ready0[job];
+  out->ready = (!S.ready_gang || out->ready_num >= S.jobs_in[job].min_available) ? 1 : 0;
+  out->drf_share = S.has_drf ? E.jshare[job] : 0.0;
+  out->drf_allocated = to_kres(E.jalloc[job]);
+  return KBG_OK;
+}
+
+kbg_status kbg_queue_state_get(kbg_session* s, int32_t queue, kbg_queue_state* out) {
+  if (!s || !out) return fail(KBG_E_INVALID, "null argument");
+  Session& S = s->s;
+  if (queue < 0 || queue >= S.n_queues) return fail(KBG_E_INVALID, "queue index");
+  const Engine& E = S.allocated ? S.fin : S.init;
+  out->has_attr = S.has_prop && S.q_has_attr[queue];
+  out->share = E.qshare[queue];
+  out->deserved = to_kres(S.q_deserved[queue]);
+  out->allocated = to_kres(E.qalloc[queue]);
+  out->request = to_kres(S.q_request[queue]);
+  out->overused = out->has_attr && kbg::res_le(S.q_deserved[queue], E.qalloc[queue]);
+  return KBG_OK;
+}
+
+kbg_status kbg_node_state_get(kbg_session* s, int32_t node, kbg_node_state* out) {
+  if (!s || !out) return fail(KBG_E_INVALID, "null argument");
+  Session& S = s->s;
+  if (node < 0 || node >= S.n_nodes) return fail(KBG_E_INVALID, "node index");
+  out->idle = to_kres(S.idle[node]);
+  out->releasing = to_kres(S.rel[node]);
+  out->num_tasks = S.ntasks[node];
+  return KBG_OK;
+}
+
+kbg_status kbg_stats_get(kbg_session* s, kbg_stats* out) {
+  if (!s || !out) return fail(KBG_E_INVALID, "null argument");
+  *out = s->s.stats;
+  return KBG_OK;
+}
+
+void kbg_session_close(kbg_session* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->s.device);
+  free_device(s->s);
+  delete s;
+}
+
+}  // extern "C"

@@ -1,0 +1,152 @@
+// Host-side session state of the MI355X allocate path.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/kbgpu.h"
+#include "kbg_device.hpp"
+
+namespace kbg {
+
+struct Res {
+  double c = 0, m = 0, g = 0;
+};
+
+// resource_info.go:142-146
+inline bool res_le(const Res& r, const Res& a) {
+  return (r.c < a.c || __builtin_fabs(a.c - r.c) < kMinMilliCPU) &&
+         (r.m < a.m || __builtin_fabs(a.m - r.m) < kMinMemory) &&
+         (r.g < a.g || __builtin_fabs(a.g - r.g) < kMinMilliGPU);
+}
+inline void res_add(Res& r, const Res& b) {
+  r.c += b.c;
+  r.m += b.m;
+  r.g += b.g;
+}
+// Resource.Sub: false when the reference would panic (resource_info.go:100-110)
+inline bool res_sub(Res& r, const Res& b) {
+  if (!res_le(b, r)) return false;
+  r.c -= b.c;
+  r.m -= b.m;
+  r.g -= b.g;
+  return true;
+}
+// resource_info.go:75-77
+inline bool res_empty(const Res& r) { return r.c < kMinMilliCPU && r.m < kMinMemory && r.g < kMinMilliGPU; }
+
+struct StaticHost {
+  int32_t n_classes = 0;
+  int32_t label_words = 1, taint_words = 1, n_numcols = 0;
+  std::vector<uint64_t> label_bits, taint_bits, mask_pool, tol_pool;
+  std::vector<int64_t> num_vals;
+  std::vector<uint8_t> num_ok, node_flags;
+  std::vector<int32_t> name_id;
+  std::vector<ReqProg> reqs;
+  std::vector<TermProg> terms;
+  std::vector<ClassProg> classes;
+};
+
+enum JobOrderPlugin : int32_t { JO_PRIORITY = 1, JO_GANG = 2, JO_DRF = 3 };
+
+// Mutable state of the ordering engine (queue/job/task priority queues and
+// the plugin state they read). Flat arrays so a batch checkpoint is a copy.
+struct Engine {
+  std::vector<int32_t> qheap;   // queue heap items (queue index), util.PriorityQueue
+  std::vector<int32_t> jheap;   // per-queue job heaps, flat at joff[q]
+  std::vector<int32_t> jlen;    // live length of each per-queue heap
+  std::vector<int32_t> cursor;  // per job: next position in its sorted pending list
+  int32_t cur_q = -1, cur_j = -1;
+  bool in_job = false;
+  std::vector<Res> jalloc;      // drf attr.allocated
+  std::vector<double> jshare;   // drf attr.share
+  std::vector<int32_t> jready;  // gang readyTaskNum
+  std::vector<Res> qalloc;      // proportion attr.allocated
+  std::vector<double> qshare;   // proportion attr.share
+};
+
+struct Session {
+  // ---- copied snapshot
+  std::vector<std::string> strs;
+  std::vector<int32_t> canon;  // string id -> canonical id of its content
+  int32_t n_nodes = 0, n_jobs = 0, n_queues = 0, n_tasks = 0;
+  std::vector<kbg_node> nodes_in;
+  std::vector<kbg_job> jobs_in;
+  std::vector<kbg_queue> queues_in;
+  std::vector<kbg_task> tasks_in;
+  std::vector<kbg_spec> specs_in;
+  std::vector<kbg_term> terms_in;
+  std::vector<kbg_requirement> reqs_in;
+  std::vector<int32_t> values_in, labels_in, selectors_in;
+  std::vector<kbg_toleration> tols_in;
+  std::vector<kbg_taint> taints_in;
+  kbg_options opts{};
+
+  // ---- plugin configuration (session_plugins.go tier walks, flattened)
+  bool has_drf = false, has_prop = false, has_gang = false, has_prio = false;
+  bool pred_active = false;         // some tier entry "predicates" without disablePredicate
+  std::vector<int32_t> job_chain;   // JobOrderPlugin in tier order (disabled entries removed)
+  bool queue_order_prop = false;
+  bool task_order_prio = false;
+  bool ready_gang = false;
+  bool heap_go111 = true;
+
+  // ---- derived, immutable after open
+  std::vector<int32_t> job_rank, queue_rank, task_rank;  // bytewise UID order
+  std::vector<int32_t> job_queue;                        // job -> queue index
+  std::vector<int32_t> joff, jcap;                       // per-queue job-heap segment
+  std::vector<int32_t> pend, pend_off, pend_len;         // per-job pending tasks in TaskOrderFn order
+  std::vector<char> pending_candidate;                   // task is Pending and not BestEffort
+  std::vector<int32_t> task_class;
+  std::vector<Res> treq;
+  Res drf_total, prop_total;
+  std::vector<char> q_has_attr;
+  std::vector<Res> q_deserved, q_request;
+  std::vector<int32_t> job_ready0;
+  bool ghost = false;
+  Engine init;  // engine state at session open
+
+  // ---- node state (host mirror of the device table)
+  std::vector<Res> idle0, rel0, idle, rel;
+  std::vector<int32_t> ntasks0, ntasks, maxtasks;
+  std::vector<char> nil_node;
+
+  // ---- results of the last allocate
+  Engine fin;
+  bool allocated = false;
+  std::vector<int32_t> committed_ready;
+
+  // ---- device
+  int32_t device = 0;
+  hipStream_t stream = nullptr;
+  int32_t W = 0;            // u64 words per node bitmap row
+  int32_t n_classes = 0;
+  int32_t K = 0, M = 0;     // batch tasks, candidates per task
+  NodeSoA d_nodes{};
+  NodeSoA d_nodes0{};       // pristine copy for kbg_session_reset
+  uint64_t* d_class_mask = nullptr;
+  TaskRec* d_tasks = nullptr;
+  uint64_t* d_feas = nullptr;
+  uint64_t* d_idlem = nullptr;
+  uint32_t* d_cand = nullptr;
+  uint32_t* d_count = nullptr;
+  NodeDelta* d_deltas = nullptr;
+  TaskRec* h_tasks = nullptr;    // pinned
+  uint32_t* h_cand = nullptr;    // pinned
+  uint32_t* h_count = nullptr;   // pinned
+  NodeDelta* h_deltas = nullptr; // pinned
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<void*> d_allocs;
+
+  kbg_stats stats{};
+};
+
+bool parse_go_int64(const std::string& s, int64_t* out);
+void compile_static_predicates(Session& S, StaticHost* out);
+
+}  // namespace kbg
+
+struct kbg_session {
+  kbg::Session s;
+};

@@ -1,0 +1,131 @@
+"""framework: Session, plugin/action registries (pkg/scheduler/framework).
+
+`open_session` / `close_session` mirror framework.OpenSession / CloseSession
+(framework.go:26-54). The plugins named in the tiers (drf, proportion, gang,
+priority, predicates) run their OnSessionOpen inside the device library
+(kbg_session_open), which also uploads the node table to HBM; plugin names the
+library does not know are ignored, exactly like GetPluginBuilder misses
+(framework.go:30-35). `Session.allocate` / `Session.pipeline` /
+`Session.dispatch` replay device decisions into the host objects with the
+reference's bookkeeping (session.go:205-316).
+"""
+import ctypes
+
+from . import _abi
+from .api import ALLOCATED, BINDING, PIPELINED
+from .snapshot import FlatSnapshot
+
+KNOWN_PLUGINS = ("priority", "gang", "drf", "predicates", "proportion")
+
+_plugin_builders = {n: n for n in KNOWN_PLUGINS}
+_actions = {}
+
+
+def register_plugin_builder(name, builder=None):  # plugins.go:28-33
+    _plugin_builders[name] = builder or name
+
+
+def cleanup_plugin_builders():  # plugins.go:35-40
+    _plugin_builders.clear()
+
+
+def get_plugin_builder(name):  # plugins.go:42-49
+    return _plugin_builders.get(name)
+
+
+def register_action(action):  # plugins.go:53-58
+    _actions[action.name()] = action
+
+
+def get_action(name):  # plugins.go:60-66
+    return _actions.get(name)
+
+
+class Session:
+    """framework.Session (session.go:35-61) plus the device handle."""
+
+    def __init__(self, cache, tiers, options=None):
+        snap = cache.snapshot()
+        self.cache = cache
+        self.jobs = snap.jobs  # JobValid is a no-op at openSession time
+        self.job_index = {j.uid: j for j in self.jobs}
+        self.nodes = snap.nodes
+        self.node_index = {n.name: n for n in self.nodes}
+        self.queues = snap.queues
+        self.queue_index = {q.uid: q for q in self.queues}
+        self.others = snap.others
+        self.tiers = tiers
+        self.plugins = [p.name for t in tiers for p in t.plugins if get_plugin_builder(p.name) is not None]
+        self.flat = FlatSnapshot(self.nodes, self.jobs, self.queues, self.others, self._active_tiers())
+        self.handle = ctypes.c_void_p()
+        opts = _abi.kbg_options()
+        opts.device = -1
+        for k, v in (options or {}).items():
+            setattr(opts, k, v)
+        L = _abi.lib()
+        _abi.check(L.kbg_session_open(ctypes.byref(self.flat.snap), ctypes.byref(opts), ctypes.byref(self.handle)))
+        self.decisions = []
+
+    def _active_tiers(self):
+        from .conf import Tier
+        return [Tier([p for p in t.plugins if get_plugin_builder(p.name) is not None]) for t in self.tiers]
+
+    # ---- session.go:205-241
+    def pipeline(self, task, hostname):
+        job = self.job_index.get(task.job)
+        if job is not None:
+            job.update_task_status(task, PIPELINED)
+        task.node_name = hostname
+        node = self.node_index.get(hostname)
+        if node is not None:
+            node.add_task(task)
+
+    # ---- session.go:243-293 (the JobReady/dispatch decision comes from the device log)
+    def allocate(self, task, hostname):
+        job = self.job_index.get(task.job)
+        if job is not None:
+            job.update_task_status(task, ALLOCATED)
+        task.node_name = hostname
+        node = self.node_index.get(hostname)
+        if node is not None:
+            node.add_task(task)
+
+    # ---- session.go:295-316
+    def dispatch(self, task):
+        self.cache.bind(task, task.node_name)
+        job = self.job_index.get(task.job)
+        if job is not None:
+            job.update_task_status(task, BINDING)
+
+    def job_state(self, j):
+        st = _abi.kbg_job_state()
+        _abi.check(_abi.lib().kbg_job_state_get(self.handle, j, ctypes.byref(st)))
+        return st
+
+    def queue_state(self, q):
+        st = _abi.kbg_queue_state()
+        _abi.check(_abi.lib().kbg_queue_state_get(self.handle, q, ctypes.byref(st)))
+        return st
+
+    def node_state(self, n):
+        st = _abi.kbg_node_state()
+        _abi.check(_abi.lib().kbg_node_state_get(self.handle, n, ctypes.byref(st)))
+        return st
+
+    def stats(self):
+        st = _abi.kbg_stats()
+        _abi.check(_abi.lib().kbg_stats_get(self.handle, ctypes.byref(st)))
+        return st
+
+    def close(self):
+        if self.handle:
+            _abi.lib().kbg_session_close(self.handle)
+            self.handle = ctypes.c_void_p()
+
+
+def open_session(cache, tiers, options=None):
+    return Session(cache, tiers, options)
+
+
+def close_session(ssn):
+    ssn.close()

@@ -1,0 +1,175 @@
+"""Marshals an opened session into the flat kbg_snapshot of include/kbgpu.h.
+
+This is the work a Go cgo adapter would do in front of the device path
+(INTEGRATION.md): intern every string, flatten ssn.Nodes / ssn.Jobs /
+ssn.Queues / ssn.Others and each pod's predicate inputs into plain arrays.
+"""
+import ctypes
+import json
+
+import numpy as np
+
+from . import _abi
+from .api import PENDING
+
+
+class Interner:
+    def __init__(self):
+        self.ids = {}
+        self.strings = []
+
+    def __call__(self, s):
+        s = "" if s is None else str(s)
+        i = self.ids.get(s)
+        if i is None:
+            i = len(self.strings)
+            self.ids[s] = i
+            self.strings.append(s)
+        return i
+
+
+def _spec_key(pod):
+    aff = pod.get("affinity") or None
+    has_ports = any((pt.get("hostPort") or 0) > 0 for c in pod.get("containers", []) for pt in (c.get("ports") or []))
+    return json.dumps([pod.get("nodeSelector") or {}, aff, pod.get("tolerations") or [], has_ports], sort_keys=True)
+
+
+class FlatSnapshot:
+    """Owns the arrays behind one kbg_snapshot (keeps them alive for the call)."""
+
+    def __init__(self, nodes, jobs, queues, others, tiers):
+        S = Interner()
+        self.interner = S
+        # queues
+        self.queue_index = {q.uid: i for i, q in enumerate(queues)}
+        qs = (_abi.kbg_queue * max(1, len(queues)))()
+        for i, q in enumerate(queues):
+            qs[i].uid = S(q.uid)
+            qs[i].weight = q.weight
+        # nodes
+        nd = np.zeros(len(nodes), dtype=np.dtype(_abi.kbg_node))
+        labels, taints = [], []
+        for i, n in enumerate(nodes):
+            obj = n.node or {}
+            r = nd[i]
+            r["name"] = S(n.name)
+            r["has_node"] = 1 if n.node is not None else 0
+            r["allocatable"] = n.allocatable.as_tuple()
+            r["idle"] = n.idle.as_tuple()
+            r["releasing"] = n.releasing.as_tuple()
+            r["max_task_num"] = n.allocatable.max_task_num
+            r["num_tasks"] = len(n.tasks)
+            r["unschedulable"] = 1 if obj.get("unschedulable") else 0
+            r["label_off"] = len(labels) // 2
+            for k, v in (obj.get("labels") or {}).items():
+                labels += [S(k), S(v)]
+            r["label_len"] = len(labels) // 2 - r["label_off"]
+            r["taint_off"] = len(taints)
+            for t in obj.get("taints") or []:
+                taints.append((S(t.get("key")), S(t.get("value")), S(t.get("effect"))))
+            r["taint_len"] = len(taints) - r["taint_off"]
+        self.node_names = [n.name for n in nodes]
+        # jobs + tasks + specs
+        jb = np.zeros(len(jobs), dtype=np.dtype(_abi.kbg_job))
+        task_rows, self.task_objs = [], []
+        spec_ids = {}
+        specs, terms, reqs, values, tols, selectors = [], [], [], [], [], []
+
+        def spec_of(pod):
+            key = _spec_key(pod)
+            sid = spec_ids.get(key)
+            if sid is not None:
+                return sid
+            sel_off = len(selectors) // 2
+            for k, v in (pod.get("nodeSelector") or {}).items():
+                selectors.extend((S(k), S(v)))
+            aff = pod.get("affinity") or {}
+            na = aff.get("nodeAffinity") if isinstance(aff, dict) else None
+            req = na.get("requiredDuringSchedulingIgnoredDuringExecution") if isinstance(na, dict) else None
+            term_off = len(terms)
+            if req is not None:
+                for t in req.get("nodeSelectorTerms") or []:
+                    row = []
+                    for part in ("matchExpressions", "matchFields"):
+                        off = len(reqs)
+                        for e in t.get(part) or []:
+                            voff = len(values)
+                            values.extend(S(v) for v in (e.get("values") or []))
+                            reqs.append((S(e.get("key")), S(e.get("operator")), voff, len(values) - voff))
+                        row += [off, len(reqs) - off]
+                    terms.append(tuple(row))
+            tol_off = len(tols)
+            for t in pod.get("tolerations") or []:
+                tols.append((S(t.get("key")), S(t.get("operator")), S(t.get("value")), S(t.get("effect"))))
+            has_ports = any((pt.get("hostPort") or 0) > 0
+                            for c in pod.get("containers", []) for pt in (c.get("ports") or []))
+            has_pa = isinstance(aff, dict) and (aff.get("podAffinity") is not None or aff.get("podAntiAffinity") is not None)
+            specs.append((sel_off, len(selectors) // 2 - sel_off, 1 if req is not None else 0, term_off,
+                          len(terms) - term_off, tol_off, len(tols) - tol_off, 1 if has_ports else 0,
+                          1 if has_pa else 0))
+            sid = len(specs) - 1
+            spec_ids[key] = sid
+            return sid
+
+        for j, job in enumerate(jobs):
+            r = jb[j]
+            r["uid"] = S(job.uid)
+            r["queue"] = self.queue_index[job.queue]
+            r["min_available"] = job.min_available
+            r["priority"] = job.priority
+            r["creation_ns"] = job.creation_timestamp
+            for t in job.tasks.values():
+                task_rows.append((S(t.uid), j, t.status, t.priority, t.resreq.as_tuple(), spec_of(t.pod), S(t.node_name)))
+                self.task_objs.append(t)
+        tk = np.zeros(len(task_rows), dtype=np.dtype(_abi.kbg_task))
+        for i, row in enumerate(task_rows):
+            tk[i] = row
+        self.pending_count = sum(1 for t in self.task_objs if t.status == PENDING and not t.resreq.is_empty())
+
+        def arr(ctype, rows):
+            a = (ctype * max(1, len(rows)))()
+            for i, row in enumerate(rows):
+                a[i] = ctype(*row)
+            return a
+
+        self._keep = []
+        oth = arr(_abi.kbg_resource, [t.resreq.as_tuple() for t in others])
+        plugin_rows, tier_sizes = [], []
+        for tier in tiers:
+            tier_sizes.append(len(tier.plugins))
+            for p in tier.plugins:
+                plugin_rows.append((S(p.name), p.flags()))
+        self.strings_c = (ctypes.c_char_p * max(1, len(S.strings)))(*[s.encode("utf-8") for s in S.strings])
+        self.arrays = dict(
+            nodes=nd, jobs=jb, tasks=tk, queues=qs, others=oth,
+            specs=arr(_abi.kbg_spec, specs), terms=arr(_abi.kbg_term, terms), reqs=arr(_abi.kbg_requirement, reqs),
+            values=np.asarray(values or [0], dtype=np.int32), tols=arr(_abi.kbg_toleration, tols),
+            labels=np.asarray(labels or [0, 0], dtype=np.int32), taints=arr(_abi.kbg_taint, taints),
+            selectors=np.asarray(selectors or [0, 0], dtype=np.int32),
+            plugins=arr(_abi.kbg_plugin_option, plugin_rows), tier_sizes=np.asarray(tier_sizes or [0], dtype=np.int32))
+        A = self.arrays
+
+        def ptr(a, ctype):
+            if isinstance(a, np.ndarray):
+                return a.ctypes.data_as(ctypes.POINTER(ctype))
+            return ctypes.cast(a, ctypes.POINTER(ctype))
+
+        snap = _abi.kbg_snapshot()
+        snap.strings = ctypes.cast(self.strings_c, ctypes.POINTER(ctypes.c_char_p))
+        snap.n_strings = len(S.strings)
+        snap.nodes, snap.n_nodes = ptr(A["nodes"], _abi.kbg_node), len(nodes)
+        snap.jobs, snap.n_jobs = ptr(A["jobs"], _abi.kbg_job), len(jobs)
+        snap.queues, snap.n_queues = ptr(A["queues"], _abi.kbg_queue), len(queues)
+        snap.tasks, snap.n_tasks = ptr(A["tasks"], _abi.kbg_task), len(task_rows)
+        snap.others, snap.n_others = ptr(A["others"], _abi.kbg_resource), len(others)
+        snap.specs, snap.n_specs = ptr(A["specs"], _abi.kbg_spec), len(specs)
+        snap.terms, snap.n_terms = ptr(A["terms"], _abi.kbg_term), len(terms)
+        snap.reqs, snap.n_reqs = ptr(A["reqs"], _abi.kbg_requirement), len(reqs)
+        snap.values, snap.n_values = ptr(A["values"], ctypes.c_int32), len(values)
+        snap.tolerations, snap.n_tolerations = ptr(A["tols"], _abi.kbg_toleration), len(tols)
+        snap.labels, snap.n_labels = ptr(A["labels"], ctypes.c_int32), len(labels) // 2
+        snap.taints, snap.n_taints = ptr(A["taints"], _abi.kbg_taint), len(taints)
+        snap.selectors, snap.n_selectors = ptr(A["selectors"], ctypes.c_int32), len(selectors) // 2
+        snap.plugins, snap.n_plugins = ptr(A["plugins"], _abi.kbg_plugin_option), len(plugin_rows)
+        snap.tier_sizes, snap.n_tiers = ptr(A["tier_sizes"], ctypes.c_int32), len(tier_sizes)
+        self.snap = snap

@@ -1,0 +1,231 @@
+"""Seeded synthetic sessions in the fixture schema (k8s-like objects).
+
+`config_fixture(cid)` builds BASELINE.json's configs C1-C4 as SURVEY §8(d)
+specifies them (seed 20261015 + config id); `random_fixture(seed)` builds
+small adversarial sessions for parity fuzzing (tight capacity, releasing
+pods, BestEffort pods, priorities, selectors/affinity/taints, gang minimums,
+several queues, random tiers and disable flags).
+The same dicts feed the kbref oracle (as JSON) and the device path.
+"""
+import random
+
+BASE_SEED = 20261015
+GI = 1024 ** 3
+
+CONFIGS = {
+    1: dict(nodes=100, jobs=20, tasks_per_job=50, mix="c1", queues=[("default", 1)],
+            tiers=[[{"name": "priority"}, {"name": "gang"}],
+                   [{"name": "drf"}, {"name": "predicates"}, {"name": "nodeorder"}]]),
+    2: dict(nodes=1000, jobs=200, tasks_per_job=50, mix="hetero", queues=[("q1", 1), ("q2", 1)], tiers=None),
+    3: dict(nodes=5000, jobs=2000, tasks_per_job=50, mix="hetero", queues=[("q1", 1), ("q2", 2), ("q3", 3), ("q4", 4)],
+            tiers=None),
+    4: dict(nodes=20000, jobs=10000, tasks_per_job=50, mix="hetero4", queues=[("q1", 1), ("q2", 2), ("q3", 3), ("q4", 4)],
+            tiers=None),
+}
+
+NODE_TYPES = {  # (type, cpu cores, memory GiB, gpus)
+    "cpu": (32, 128, 0),
+    "mem": (64, 256, 0),
+    "gpu": (96, 512, 8),
+}
+
+
+def _node(i, rng, mix):
+    name = f"node-{i:05d}"
+    if mix == "c1":
+        ntype, (cpu, mem, gpu) = "cpu", NODE_TYPES["cpu"]
+    else:
+        ntype = ("cpu", "mem", "gpu")[rng.randrange(3)]
+        cpu, mem, gpu = NODE_TYPES[ntype]
+        if mix == "hetero4":
+            mem = min(mem, 256)  # keep Σ memory < 2^53 at 20k nodes
+    alloc = {"cpu": str(cpu), "memory": f"{mem}Gi", "nvidia.com/gpu": str(gpu), "pods": "110"}
+    n = {"name": name, "allocatable": alloc,
+         "labels": {"zone": f"z{i % 4}", "type": ntype, "rack": f"r{i % 50}", "cores": str(cpu)}}
+    if mix != "c1":
+        taints = []
+        if ntype == "gpu":
+            taints.append({"key": "dedicated", "value": "gpu", "effect": "NoSchedule"})
+        if rng.random() < 0.05:
+            taints.append({"key": "maint", "value": "", "effect": "NoExecute"})
+        if taints:
+            n["taints"] = taints
+        if rng.random() < 0.02:
+            n["unschedulable"] = True
+    return n
+
+
+def config_fixture(cid):
+    """BASELINE config `cid` (1-4) as a fixture dict."""
+    c = CONFIGS[cid]
+    rng = random.Random(BASE_SEED + cid)
+    nodes = [_node(i, rng, c["mix"]) for i in range(c["nodes"])]
+    queues = [{"name": q, "weight": w} for q, w in c["queues"]]
+    pods, pgs = [], []
+    for j in range(c["jobs"]):
+        ns = f"ns{j % 8}"
+        pg = f"pg-{j:05d}"
+        q = queues[rng.randrange(len(queues))]["name"]
+        cpu = ("500m", "1", "2")[rng.randrange(3)]
+        mem = ("1Gi", "2Gi", "4Gi")[rng.randrange(3)]
+        req = {"cpu": cpu, "memory": mem}
+        spec = {}
+        if c["mix"] != "c1":
+            r = rng.random()
+            if r < 0.10:  # GPU job: 1 GPU + tolerate the dedicated taint
+                req["nvidia.com/gpu"] = "1"
+                spec["tolerations"] = [{"key": "dedicated", "operator": "Equal", "value": "gpu", "effect": "NoSchedule"}]
+            elif r < 0.40:  # 30%: node selector on zone or type
+                spec["nodeSelector"] = ({"zone": f"z{rng.randrange(4)}"} if rng.random() < 0.5
+                                        else {"type": ("cpu", "mem")[rng.randrange(2)]})
+            elif r < 0.45:  # 5%: required node affinity
+                k = rng.randrange(3)
+                if k == 0:
+                    expr = {"key": "rack", "operator": "In", "values": [f"r{x}" for x in rng.sample(range(50), 10)]}
+                elif k == 1:
+                    expr = {"key": "zone", "operator": "NotIn", "values": [f"z{rng.randrange(4)}"]}
+                else:
+                    expr = {"key": "cores", "operator": "Gt", "values": ["40"]}
+                spec["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+                    "nodeSelectorTerms": [{"matchExpressions": [expr]}]}}}
+        min_member = 50 if cid == 1 else (1, 25, 50)[rng.randrange(3)]
+        pgs.append({"namespace": ns, "name": pg, "minMember": min_member, "queue": q,
+                    "creationTimestamp": (1_700_000_000 + j) * 1_000_000_000})
+        for t in range(c["tasks_per_job"]):
+            p = {"uid": f"uid-{j:05d}-{t:03d}", "namespace": ns, "name": f"{pg}-{t:03d}", "phase": "Pending",
+                 "annotations": {"scheduling.k8s.io/group-name": pg}, "containers": [{"requests": dict(req)}]}
+            p.update(spec)
+            pods.append(p)
+    return {"name": f"C{cid}", "tiers": c["tiers"], "nodes": nodes, "pods": pods, "podGroups": pgs, "queues": queues}
+
+
+# ------------------------------------------------------------------ fuzz
+_OPS = ("In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt")
+
+
+def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8):
+    rng = random.Random(seed)
+    nn = rng.randint(1, max_nodes)
+    zones = ["a", "b", "c"]
+    nodes = []
+    for i in range(nn):
+        cpu = rng.choice([1, 2, 4, 8, 16])
+        mem = rng.choice([1, 2, 4, 8, 32])
+        gpu = rng.choice([0, 0, 0, 1, 4])
+        alloc = {"cpu": str(cpu), "memory": f"{mem}Gi", "nvidia.com/gpu": str(gpu)}
+        if rng.random() < 0.93:
+            alloc["pods"] = str(rng.choice([2, 3, 5, 110]))
+        labels = {"zone": rng.choice(zones), "size": str(cpu)}
+        if rng.random() < 0.3:
+            labels["ssd"] = "true"
+        if rng.random() < 0.1:
+            labels["size"] = "x12"  # non-integer: Gt/Lt must fail on it
+        n = {"name": f"n{i:02d}", "allocatable": alloc, "labels": labels}
+        if rng.random() < 0.2:
+            n["taints"] = [{"key": rng.choice(["dedicated", "maint"]), "value": rng.choice(["", "gpu"]),
+                            "effect": rng.choice(["NoSchedule", "NoExecute", "PreferNoSchedule"])}]
+        if rng.random() < 0.08:
+            n["unschedulable"] = True
+        nodes.append(n)
+    queues = [{"name": f"q{i}", "weight": rng.choice([1, 1, 2, 3])} for i in range(rng.randint(1, 3))]
+    pods, pgs = [], []
+    uid = 0
+
+    def mk_pod(ns, name, phase, node, req, group=None, controller=None):
+        nonlocal uid
+        uid += 1
+        p = {"uid": f"u{uid:04d}-{rng.randrange(100):02d}", "namespace": ns, "name": name, "phase": phase,
+             "nodeName": node, "containers": [{"requests": req}]}
+        if group:
+            p["annotations"] = {"scheduling.k8s.io/group-name": group}
+        if controller:
+            p["controller"] = controller
+        return p
+
+    def rand_req(best_effort_ok=True):
+        if best_effort_ok and rng.random() < 0.06:
+            return {"cpu": "5m"}  # BestEffort (all dims below the tolerance)
+        r = {"cpu": rng.choice(["100m", "500m", "1", "2", "3"]), "memory": rng.choice(["256Mi", "1Gi", "2Gi", "3Gi"])}
+        if rng.random() < 0.15:
+            r["nvidia.com/gpu"] = rng.choice(["1", "2"])
+        return r
+
+    # existing pods on nodes (Running / deleting -> Releasing)
+    for i in range(rng.randint(0, nn)):
+        node = rng.choice(nodes)
+        p = mk_pod("default", f"run{i}", "Running", node["name"], {"cpu": "500m", "memory": "512Mi"},
+                   group=None if rng.random() < 0.5 else "pg-run", controller="rc-1" if rng.random() < 0.5 else None)
+        if rng.random() < 0.35:
+            p["deletionTimestamp"] = "2026-01-01T00:00:00Z"
+        pods.append(p)
+    nj = rng.randint(1, max_jobs)
+    for j in range(nj):
+        ns = rng.choice(["c1", "c2"])
+        pg = f"pg{j}"
+        ntask = rng.randint(1, max_tasks)
+        pgs.append({"namespace": ns, "name": pg, "minMember": rng.randint(0, ntask + 1),
+                    "queue": rng.choice(queues)["name"] if rng.random() < 0.9 else "",
+                    "creationTimestamp": rng.choice([0, 100, 200, 300]) * 1_000_000_000})
+        job_req = rand_req()
+        spec = {}
+        r = rng.random()
+        if r < 0.25:
+            spec["nodeSelector"] = {"zone": rng.choice(zones)}
+            if rng.random() < 0.1:
+                spec["nodeSelector"]["bad key!"] = "x"  # invalid => selector matches everything
+        elif r < 0.5:
+            terms = []
+            for _ in range(rng.randint(0, 2)):
+                exprs = []
+                for _ in range(rng.randint(0, 2)):
+                    op = rng.choice(_OPS)
+                    if op in ("In", "NotIn"):
+                        vals = rng.sample(zones, rng.randint(1, 2))
+                        key = "zone"
+                    elif op in ("Gt", "Lt"):
+                        vals = [rng.choice(["2", "4", "x"])]
+                        key = "size"
+                    else:
+                        vals = []
+                        key = rng.choice(["ssd", "zone", "gpu"])
+                    exprs.append({"key": key, "operator": op, "values": vals})
+                term = {"matchExpressions": exprs}
+                if rng.random() < 0.3:
+                    term["matchFields"] = [{"key": "metadata.name", "operator": rng.choice(["In", "NotIn"]),
+                                            "values": [rng.choice(nodes)["name"]]}]
+                terms.append(term)
+            spec["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution":
+                                                 {"nodeSelectorTerms": terms}}}
+        if rng.random() < 0.3:
+            spec["tolerations"] = [{"key": rng.choice(["dedicated", "maint", ""]),
+                                    "operator": rng.choice(["Equal", "Exists", ""]),
+                                    "value": rng.choice(["", "gpu"]),
+                                    "effect": rng.choice(["", "NoSchedule", "NoExecute"])}]
+        for t in range(ntask):
+            req = job_req if rng.random() < 0.7 else rand_req()
+            phase, node = "Pending", ""
+            if rng.random() < 0.1:
+                phase, node = "Running", rng.choice(nodes)["name"]
+            p = mk_pod(ns, f"{pg}-t{t}", phase, node, req, group=pg)
+            if rng.random() < 0.25:
+                p["priority"] = rng.choice([1, 5, 10])
+            p.update(spec)
+            pods.append(p)
+    plugins = ["priority", "gang", "drf", "predicates", "proportion", "nodeorder"]
+    rng.shuffle(plugins)
+    keep = [p for p in plugins if rng.random() < 0.85]
+    cut = rng.randint(0, len(keep))
+    flags = ["disableJobOrder", "disableJobReady", "disableTaskOrder", "disableQueueOrder", "disablePredicate"]
+
+    def opt(name):
+        o = {"name": name}
+        if rng.random() < 0.1:
+            o[rng.choice(flags)] = True
+        return o
+
+    tiers = [[opt(p) for p in keep[:cut]], [opt(p) for p in keep[cut:]]]
+    tiers = [t for t in tiers if t]
+    fx = {"name": f"fuzz-{seed}", "tiers": tiers, "nodes": nodes, "pods": pods, "podGroups": pgs, "queues": queues}
+    if rng.random() < 0.2:
+        fx["namespaces"] = ["c1", "c2"]
+    return fx

@@ -1,0 +1,217 @@
+"""Hand-derived known-answer fixtures (KATs) for paths the reference's own
+tests do not pin. Each expected value below was derived by
+reading the cited reference code, not by running any implementation.
+
+Run: python tests/golden/make_kats.py   (rewrites tests/golden/kat_*.json)
+"""
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def pod(uid, name, req, ns="ns", group="pg1", phase="Pending", node="", **kw):
+    p = {"uid": uid, "namespace": ns, "name": name, "phase": phase, "nodeName": node,
+         "containers": [{"requests": req}]}
+    if group:
+        p["annotations"] = {"scheduling.k8s.io/group-name": group}
+    p.update(kw)
+    return p
+
+
+def node(name, cpu, mem="64Gi", pods="110", **kw):
+    alloc = {"cpu": cpu, "memory": mem}
+    if pods is not None:
+        alloc["pods"] = pods
+    n = {"name": name, "allocatable": alloc}
+    n.update(kw)
+    return n
+
+
+Q = [{"name": "q", "weight": 1}]
+
+
+def pg(name="pg1", ns="ns", minMember=0, created=0, queue="q"):
+    return {"namespace": ns, "name": name, "minMember": minMember, "queue": queue, "creationTimestamp": created}
+
+
+KATS = {
+    # resource_info.go:142-146: |idle - req| < 10 mCPU counts as a fit and
+    # drives Idle to -9 (Sub only panics beyond the tolerance, :100-110).
+    # Next task: LessEqual(1m, -9m) is false (|-9-1| = 10 is not < 10).
+    "kat_tolerance_edge": {
+        "tiers": [[{"name": "predicates"}]],
+        "nodes": [node("n1", "1", "1Gi"), node("n2", "1", "1Gi")],
+        "pods": [pod("a", "pa", {"cpu": "1009m", "memory": "1Mi"}),
+                 pod("b", "pb", {"cpu": "1m", "memory": "20Mi"}),
+                 pod("c", "pc", {"cpu": "1011m", "memory": "1Mi"})],
+        "podGroups": [pg()], "queues": Q,
+        "expected": {"decisions": [["a", "n1", "allocate"], ["b", "n2", "allocate"]],
+                     "binds": {"ns/pa": "n1", "ns/pb": "n2"}},
+    },
+    # allocate.go:131-161: Idle misses, Releasing fits -> Pipeline (no dispatch,
+    # session.go:205-241); gang counts Pipelined as ready (gang.go:44-55).
+    # The releasing pod (Running + deletionTimestamp) holds 2 CPU / 1Gi.
+    "kat_pipeline": {
+        "tiers": [[{"name": "gang"}], [{"name": "predicates"}]],
+        "nodes": [node("n1", "2", "4Gi")],
+        "pods": [pod("r", "old", {"cpu": "2", "memory": "1Gi"}, ns="other", group=None, phase="Running",
+                     node="n1", deletionTimestamp="2026-01-01T00:00:00Z"),
+                 pod("t1", "p1", {"cpu": "1", "memory": "512Mi"}),
+                 pod("t2", "p2", {"cpu": "1", "memory": "512Mi"}),
+                 pod("t3", "p3", {"cpu": "1", "memory": "512Mi"})],
+        "podGroups": [pg(minMember=2)], "queues": Q,
+        "expected": {"decisions": [["t1", "n1", "pipeline"], ["t2", "n1", "pipeline"]], "binds": {},
+                     "ready": {"ns/pg1": True}},
+    },
+    # gang.go:129-163 job order + session.go:283-290 dispatch: pg1 (older) goes
+    # first until ready (3 of 4), then non-ready pg2 ranks ahead of ready pg1;
+    # FitError (job_info.go:329-358) of pg1's failed last task a4: cpu only
+    # (FitDelta skips dims the task does not request, resource_info.go:116-129).
+    "kat_gang_dispatch": {
+        "tiers": [[{"name": "priority"}, {"name": "gang"}], [{"name": "drf"}, {"name": "predicates"}]],
+        "nodes": [node("n1", "4", "4Gi")],
+        "pods": [pod(f"a{i}", f"a{i}", {"cpu": "1"}, group="pg1") for i in range(1, 5)] +
+                [pod("b1", "b1", {"cpu": "1"}, group="pg2")],
+        "podGroups": [pg("pg1", minMember=3, created=0), pg("pg2", minMember=1, created=100)], "queues": Q,
+        "expected": {"decisions": [["a1", "n1", "allocate"], ["a2", "n1", "allocate"], ["a3", "n1", "allocate"],
+                                   ["b1", "n1", "allocate"]],
+                     "binds": {"ns/a1": "n1", "ns/a2": "n1", "ns/a3": "n1", "ns/b1": "n1"},
+                     "ready": {"ns/pg1": True, "ns/pg2": True},
+                     "fit_error": {"ns/pg1": "0/1 nodes are available, 1 insufficient cpu.",
+                                   "ns/pg2": "0 nodes are available"}},
+    },
+    # priority.go:37-53: higher pod priority first, default priority 1
+    # (job_info.go:79), ties by UID (session_plugins.go:266-276).
+    "kat_priority_order": {
+        "tiers": [[{"name": "priority"}], [{"name": "predicates"}]],
+        "nodes": [node("n1", "2")],
+        "pods": [pod("a", "pa", {"cpu": "1"}, priority=1), pod("b", "pb", {"cpu": "1"}, priority=10),
+                 pod("c", "pc", {"cpu": "1"}, priority=5), pod("d", "pd", {"cpu": "1"})],
+        "podGroups": [pg()], "queues": Q,
+        "expected": {"decisions": [["b", "n1", "allocate"], ["c", "n1", "allocate"]]},
+    },
+    # Static predicates: selector (labels/selector.go:849-866, invalid key =>
+    # match all), unschedulable (predicates.go:105-110), taints NoSchedule/
+    # NoExecute only (predicates.go:1489-1517), node affinity terms
+    # (helpers.go:302-331: empty term list matches nothing, a term with an
+    # invalid operator is skipped), Gt on a non-integer label fails, matchFields
+    # metadata.name, empty-key Exists toleration tolerates everything.
+    "kat_selector_taints": {
+        "tiers": [[{"name": "predicates"}]],
+        "nodes": [node("n1", "10", labels={"zone": "a", "size": "4"},
+                       taints=[{"key": "dedicated", "value": "gpu", "effect": "NoSchedule"}]),
+                  node("n2", "10", labels={"zone": "a", "size": "8"},
+                       taints=[{"key": "soft", "value": "", "effect": "PreferNoSchedule"}]),
+                  node("n3", "10", labels={"zone": "b"}, unschedulable=True),
+                  node("n4", "10", labels={"zone": "b", "size": "x"})],
+        "pods": [
+            pod("a", "pa", {"cpu": "1"}, nodeSelector={"zone": "b"}),
+            pod("b", "pb", {"cpu": "1"}, tolerations=[{"key": "dedicated", "operator": "Equal", "value": "gpu",
+                                                      "effect": "NoSchedule"}]),
+            pod("c", "pc", {"cpu": "1"}),
+            pod("d", "pd", {"cpu": "1"}, nodeSelector={"bad key!": "x"}),
+            pod("e", "pe", {"cpu": "1"}, affinity={"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+                "nodeSelectorTerms": [{"matchExpressions": [{"key": "zone", "operator": "NotIn", "values": ["a"]}]}]}}}),
+            pod("f", "pf", {"cpu": "1"}, affinity={"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+                "nodeSelectorTerms": [{"matchExpressions": [{"key": "size", "operator": "Gt", "values": ["5"]}]}]}}}),
+            pod("g", "pg", {"cpu": "1"}, affinity={"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+                "nodeSelectorTerms": []}}}),
+            pod("h", "ph", {"cpu": "1"}, affinity={"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+                "nodeSelectorTerms": [{"matchExpressions": [{"key": "zone", "operator": "in", "values": ["b"]}]},
+                                      {"matchExpressions": [{"key": "zone", "operator": "Exists"}]}]}}}),
+            pod("i", "pi", {"cpu": "1"}, affinity={"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+                "nodeSelectorTerms": [{"matchFields": [{"key": "metadata.name", "operator": "In",
+                                                        "values": ["n4"]}]}]}}}),
+            pod("j", "pj", {"cpu": "1"}, tolerations=[{"operator": "Exists"}]),
+        ],
+        "podGroups": [pg()], "queues": Q,
+        "expected": {"decisions": [["a", "n4", "allocate"], ["b", "n1", "allocate"], ["c", "n2", "allocate"],
+                                   ["d", "n2", "allocate"], ["e", "n4", "allocate"], ["f", "n2", "allocate"],
+                                   ["h", "n2", "allocate"], ["i", "n4", "allocate"], ["j", "n1", "allocate"]]},
+    },
+    # F10: without a "pods" allocatable MaxTaskNum is 0 and the cap rejects the
+    # node (predicates.go:125-127); with pods=1 the second task is rejected.
+    "kat_pod_cap": {
+        "tiers": [[{"name": "predicates"}]],
+        "nodes": [node("n1", "4", pods=None), node("n2", "4", pods="1")],
+        "pods": [pod("t1", "p1", {"cpu": "1"}), pod("t2", "p2", {"cpu": "1"})],
+        "podGroups": [pg()], "queues": Q,
+        "expected": {"decisions": [["t1", "n2", "allocate"]]},
+    },
+    # F9: a second water-fill round subtracts cumulative deserved
+    # (proportion.go:119-140): qb becomes met in round 2 with deserved 8 CPU
+    # while remaining is 4 CPU -> Resource.Sub panics.
+    "kat_proportion_panic": {
+        "tiers": [[{"name": "proportion"}]],
+        "nodes": [node("n1", "10", "10Gi")],
+        "pods": [pod("a", "pa", {"cpu": "1", "memory": "1Gi"}, group="pga"),
+                 pod("b", "pb", {"cpu": "8", "memory": "8Gi"}, group="pgb")],
+        "podGroups": [pg("pga", queue="qa"), pg("pgb", queue="qb")],
+        "queues": [{"name": "qa", "weight": 1}, {"name": "qb", "weight": 1}],
+        "expected": {"status": "ref_panic"},
+    },
+    # A pod bound to an unknown node creates a NodeInfo with Node == nil
+    # (event_handlers.go:51-54); the predicates closure dereferences it when
+    # the scan reaches it (predicates.go:122-123). n1 fails first because the
+    # same bound pod names a node outside ssn.NodeIndex (vendor
+    # predicates.go:1273-1282), so every predicate call errors.
+    "kat_nil_node_panic": {
+        "tiers": [[{"name": "predicates"}]],
+        "nodes": [node("n1", "4")],
+        "pods": [pod("r", "run", {"cpu": "1"}, group="pg1", phase="Running", node="ghost"),
+                 pod("t", "pt", {"cpu": "500m"})],
+        "podGroups": [pg()], "queues": Q,
+        "expected": {"status": "ref_panic"},
+    },
+    # Same cluster without predicates: the nil node is a zero-resource node.
+    "kat_nil_node_nopred": {
+        "tiers": [[{"name": "drf"}]],
+        "nodes": [node("n1", "4")],
+        "pods": [pod("r", "run", {"cpu": "1"}, group="pg1", phase="Running", node="ghost"),
+                 pod("t", "pt", {"cpu": "500m"})],
+        "podGroups": [pg()], "queues": Q,
+        "expected": {"decisions": [["t", "n1", "allocate"]], "binds": {"ns/pt": "n1"}},
+    },
+    # allocate.go:88-96: BestEffort pods are skipped; gang minMember 2 is then
+    # not reached, so nothing is dispatched (session.go:283-290).
+    "kat_besteffort": {
+        "tiers": [[{"name": "gang"}], [{"name": "predicates"}]],
+        "nodes": [node("n1", "4")],
+        "pods": [pod("a", "pa", {"cpu": "5m"}), pod("b", "pb", {"cpu": "1"})],
+        "podGroups": [pg(minMember=2)], "queues": Q,
+        "expected": {"decisions": [["b", "n1", "allocate"]], "binds": {}, "ready": {"ns/pg1": False}},
+    },
+    # proportion.go:146-159,188-193: queue order by share, overused queues are
+    # dropped from the queue heap (allocate.go:71-74).
+    "kat_overused": {
+        "tiers": [[{"name": "proportion"}]],
+        "nodes": [node("n1", "4", "4Gi")],
+        "pods": [pod(f"a{i}", f"a{i}", {"cpu": "1"}, group="pga") for i in range(1, 5)] +
+                [pod(f"b{i}", f"b{i}", {"cpu": "1"}, group="pgb") for i in range(1, 5)],
+        "podGroups": [pg("pga", queue="qa"), pg("pgb", queue="qb")],
+        "queues": [{"name": "qa", "weight": 1}, {"name": "qb", "weight": 3}],
+        "expected": {"decisions": [["a1", "n1", "allocate"], ["b1", "n1", "allocate"], ["b2", "n1", "allocate"],
+                                   ["b3", "n1", "allocate"]]},
+    },
+    # k8s Quantity -> (MilliValue, Value), both rounding up.
+    "kat_quantity": {
+        "kind": "quantity",
+        "quantities": ["1", "500m", "1.5", "1Gi", "1G", "100Mi", "1e3", "0.1m", "2.5Ki", "1n", "0"],
+        "expected": {"values": [[1000, 1], [500, 1], [1500, 2], [1073741824000, 1073741824],
+                                [1000000000000, 1000000000], [104857600000, 104857600], [1000000, 1000],
+                                [1, 1], [2560000, 2560], [1, 1], [0, 0]]},
+    },
+}
+
+
+def main():
+    for name, fx in KATS.items():
+        with open(os.path.join(HERE, name + ".json"), "w") as f:
+            json.dump(fx, f, indent=1)
+            f.write("\n")
+    print("wrote", len(KATS), "KATs")
+
+
+if __name__ == "__main__":
+    main()

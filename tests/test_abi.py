@@ -1,0 +1,86 @@
+"""The C-ABI library loads, exports every symbol include/kbgpu.h declares, and
+its struct layouts match the ctypes mirror (CPU; no compute calls)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from helpers import ROOT
+
+HEADER = os.path.join(ROOT, "include", "kbgpu.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:kbg_status|int32_t|const char\*|void)\s+(kbg_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_declares_functions():
+    fns = declared_functions()
+    assert "kbg_session_open" in fns and "kbg_allocate" in fns and len(fns) >= 12
+
+
+def test_library_exports_every_declared_symbol():
+    from kbgpu import _abi
+    L = _abi.lib()
+    for fn in declared_functions():
+        assert hasattr(L, fn), fn
+    assert set(declared_functions()) == set(_abi.SIGNATURES)
+    assert L.kbg_abi_version() == 1
+    assert L.kbg_device_count() >= 0
+
+
+STRUCTS = ["kbg_resource", "kbg_node", "kbg_taint", "kbg_job", "kbg_queue", "kbg_task", "kbg_spec", "kbg_term",
+           "kbg_requirement", "kbg_toleration", "kbg_plugin_option", "kbg_snapshot", "kbg_options", "kbg_decision",
+           "kbg_job_state", "kbg_queue_state", "kbg_node_state", "kbg_stats"]
+
+
+def test_struct_layouts_match_c(tmp_path):
+    from kbgpu import _abi
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "kbgpu.h"', "int main(void){"]
+    for s in STRUCTS:
+        cls = getattr(_abi, s)
+        lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
+        for fname, _ in cls._fields_:
+            lines.append(f'printf("{s}.{fname} %zu\\n", offsetof({s}, {fname}));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n") if l)
+    for s in STRUCTS:
+        cls = getattr(_abi, s)
+        assert int(got[s]) == ctypes.sizeof(cls), s
+        for fname, _ in cls._fields_:
+            assert int(got[f"{s}.{fname}"]) == getattr(cls, fname).offset, (s, fname)
+
+
+def test_open_without_device_fails_loudly():
+    from kbgpu import _abi
+    L = _abi.lib()
+    if L.kbg_device_count() > 0:
+        pytest.skip("a device is present")
+    h = ctypes.c_void_p()
+    snap = _abi.kbg_snapshot()
+    code = L.kbg_session_open(ctypes.byref(snap), None, ctypes.byref(h))
+    assert code == _abi.KBG_E_HIP
+    assert b"device" in L.kbg_last_error()
+    assert not h.value
+
+
+def test_invalid_snapshot_rejected():
+    from kbgpu import _abi
+    L = _abi.lib()
+    h = ctypes.c_void_p()
+    snap = _abi.kbg_snapshot()
+    jobs = (_abi.kbg_job * 1)()
+    jobs[0].queue = 5  # no queues
+    snap.jobs = ctypes.cast(jobs, ctypes.POINTER(_abi.kbg_job))
+    snap.n_jobs = 1
+    strs = (ctypes.c_char_p * 1)(b"j")
+    snap.strings = ctypes.cast(strs, ctypes.POINTER(ctypes.c_char_p))
+    snap.n_strings = 1
+    assert L.kbg_session_open(ctypes.byref(snap), None, ctypes.byref(h)) == _abi.KBG_E_INVALID

@@ -1,0 +1,49 @@
+"""The kbref oracle against the reference's own test expectations (CPU)."""
+import glob
+import json
+import os
+
+import pytest
+
+from helpers import GOLDEN, run_oracle
+
+REF = sorted(glob.glob(os.path.join(GOLDEN, "ref_*.json")))
+KAT = sorted(glob.glob(os.path.join(GOLDEN, "kat_*.json")))
+
+
+@pytest.mark.parametrize("path", REF, ids=[os.path.basename(p) for p in REF])
+def test_reference_tests(path):
+    fx = json.load(open(path))
+    out = run_oracle(fx)
+    assert out["status"] == "ok"
+    for k, v in fx["expected"].items():
+        assert out[k] == v, (k, out[k], v)
+
+
+@pytest.mark.parametrize("path", KAT, ids=[os.path.basename(p) for p in KAT])
+def test_kats(path):
+    fx = json.load(open(path))
+    out = run_oracle(fx)
+    exp = fx["expected"]
+    assert out["status"] == exp.get("status", "ok"), out
+    if "decisions" in exp:
+        got = [(d["task"], d["node"], d["kind"]) for d in out["decisions"]]
+        assert got == [tuple(x) for x in exp["decisions"]]
+    for k in ("binds", "values"):
+        if k in exp:
+            assert out[k] == exp[k]
+    if "ready" in exp:
+        assert {j["uid"]: j["ready"] for j in out["jobs"]} == exp["ready"]
+    if "fit_error" in exp:
+        assert {j["uid"]: j["fit_error"] for j in out["jobs"]} == exp["fit_error"]
+
+
+def test_faithful_scan_mode_agrees():
+    """The per-call podLister walk (F7, --faithful) changes cost, not decisions."""
+    from kbgpu import synth
+    fx = synth.config_fixture(1)
+    a = run_oracle(fx)
+    b = run_oracle(fx, "--faithful")
+    assert a["decisions"] == b["decisions"]
+    c = run_oracle(fx, "--no-cache")
+    assert a["decisions"] == c["decisions"]
