@@ -1251,7 +1251,7 @@ struct World {
 
 static Tiers parse_tiers(const Value* v) {
   Tiers t;
-  if (!v) {  // pkg/scheduler/util.go:30-40 default conf
+  if (!v || v->is_null()) {  // pkg/scheduler/util.go:30-40 default conf
     t = {{{"priority"}, {"gang"}}, {{"drf"}, {"predicates"}, {"proportion"}}};
     return t;
   }
