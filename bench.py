@@ -192,7 +192,9 @@ def main():
         "device_breakdown_ms_per_cycle": {"scan": scan_ms / args.steps, "select": sel_ms / args.steps,
                                           "launches": launches / args.steps,
                                           "batches": st.batches, "mispredictions": st.mispredictions,
-                                          "truncations": st.truncations},
+                                          "truncations": st.truncations, "replayed": st.replayed,
+                                          "host_engine": st.engine_ms, "host_resolve": st.resolve_ms,
+                                          "device_roundtrips": st.device_ms, "delta_writeback": st.delta_ms},
         "open_ms": st.open_ms,
     }
     if rank == 0 and not args.no_cpu_baseline:

@@ -225,6 +225,11 @@ typedef struct kbg_stats {
   double select_kernel_ms; /* summed HIP-event time of the candidate-select kernel */
   double allocate_ms;      /* wall time of the last kbg_allocate */
   double open_ms;          /* wall time of kbg_session_open */
+  double engine_ms;        /* host: queue/job/task ordering (prediction + replay) */
+  double resolve_ms;       /* host: in-order commit of the device candidates */
+  double device_ms;        /* host wall time spent in scan round trips (H2D, kernels, D2H) */
+  double delta_ms;         /* host wall time spent writing touched node rows back to HBM */
+  int64_t replayed;        /* engine steps replayed after a cut */
   int32_t n_classes;       /* static predicate classes on the device */
   int32_t reserved[5];
 } kbg_stats;

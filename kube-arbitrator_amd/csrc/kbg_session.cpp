@@ -829,6 +829,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   S.stats.batches = S.stats.mispredictions = S.stats.truncations = 0;
   S.stats.evaluations = S.stats.node_visits = S.stats.scan_launches = 0;
   S.stats.scan_kernel_ms = S.stats.select_kernel_ms = 0;
+  S.stats.engine_ms = S.stats.resolve_ms = S.stats.device_ms = S.stats.delta_ms = 0;
+  S.stats.replayed = 0;
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
 
   Engine E = S.init;
   Engine ckpt;
@@ -851,6 +855,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
 
   for (;;) {
     // 1. predict the next K evaluations
+    auto tp = clk::now();
     ckpt = E;
     bt.clear();
     bpred.clear();
@@ -862,12 +867,16 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       bpred.push_back(p);
       ops.apply(t, p);
     }
+    S.stats.engine_ms += ms_since(tp);
     if (bt.empty()) break;
     S.stats.batches++;
     // 2. device: feasibility scan + first-M candidates against the batch-start table
+    tp = clk::now();
     kbg_status st = device_scan(S, bt.data(), (int32_t)bt.size());
     if (st != KBG_OK) return st;
+    S.stats.device_ms += ms_since(tp);
     // 3. commit in order
+    tp = clk::now();
     ++stamp;
     touched.clear();
     bactual.assign(bt.size(), 0);
@@ -915,7 +924,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         break;
       }
     }
+    S.stats.resolve_ms += ms_since(tp);
+    tp = clk::now();
     if ((st = push_deltas(S, touched)) != KBG_OK) return st;
+    S.stats.delta_ms += ms_since(tp);
     if (panic) {
       result = fail(KBG_E_REF_PANIC, "allocate reached a node whose NodeInfo.Node is nil with the predicates plugin on "
                                      "(predicates.go:122-123)");
@@ -923,12 +935,15 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
     // 4. on a cut, rebuild the engine state at the cut from the checkpoint
     if (cut >= 0) {
+      tp = clk::now();
       E = ckpt;
       for (int32_t k = 0; k < cut; ++k) {
         const int32_t t = ops.next_task();
         if (t != bt[k]) return fail(KBG_E_INVALID, "internal: replay diverged");
         ops.apply(t, bactual[k]);
       }
+      S.stats.replayed += cut;
+      S.stats.engine_ms += ms_since(tp);
     }
   }
   S.fin = E;

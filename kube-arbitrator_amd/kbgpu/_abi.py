@@ -139,7 +139,8 @@ class kbg_node_state(ctypes.Structure):
 class kbg_stats(ctypes.Structure):
     _fields_ = [("evaluations", i64), ("node_visits", i64), ("batches", i64), ("mispredictions", i64),
                 ("truncations", i64), ("scan_launches", i64), ("scan_kernel_ms", f64), ("select_kernel_ms", f64),
-                ("allocate_ms", f64), ("open_ms", f64), ("n_classes", i32), ("reserved", i32 * 5)]
+                ("allocate_ms", f64), ("open_ms", f64), ("engine_ms", f64), ("resolve_ms", f64),
+                ("device_ms", f64), ("delta_ms", f64), ("replayed", i64), ("n_classes", i32), ("reserved", i32 * 5)]
 
 
 # Every symbol include/kbgpu.h declares, with its ctypes signature.
