@@ -108,8 +108,9 @@ hipError_t launch_build_class_mask(const StaticTables& t, int32_t n_classes, int
 hipError_t launch_scan(const NodeSoA& n, int32_t n_nodes, int32_t W, const uint64_t* class_mask, const TaskRec* tasks,
                        int32_t n_tasks, int32_t cap_check, uint64_t* out_feas, uint64_t* out_idle, hipStream_t stream);
 
-hipError_t launch_select(const uint64_t* feas, const uint64_t* idlem, int32_t W, int32_t n_tasks, int32_t M,
-                         uint32_t* out_cand, uint32_t* out_count, hipStream_t stream);
+// Row g gets cap_off[g+1]-cap_off[g] candidate slots at out_cand[cap_off[g]].
+hipError_t launch_select(const uint64_t* feas, const uint64_t* idlem, int32_t W, int32_t n_rows,
+                         const uint32_t* cap_off, uint32_t* out_cand, uint32_t* out_count, hipStream_t stream);
 
 hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream);
 

@@ -88,13 +88,16 @@ hipError_t launch_scan(const NodeSoA& n, int32_t n_nodes, int32_t W, const uint6
 // ---------------------------------------------------------------- select
 __global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restrict__ feas,
                                                          const uint64_t* __restrict__ idlem, int32_t W,
-                                                         int32_t n_tasks, int32_t M, uint32_t* __restrict__ out_cand,
+                                                         int32_t n_rows, const uint32_t* __restrict__ cap_off,
+                                                         uint32_t* __restrict__ out_cand,
                                                          uint32_t* __restrict__ out_count) {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= n_tasks) return;
+  if (t >= n_rows) return;
   const uint64_t* frow = feas + (size_t)t * W;
   const uint64_t* irow = idlem + (size_t)t * W;
+  const int M = (int)(cap_off[t + 1] - cap_off[t]);
+  uint32_t* cand = out_cand + cap_off[t];
   int found = 0;
   int base = 0;
   for (; base < W && found < M; base += 64) {
@@ -114,7 +117,7 @@ __global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restr
       const int b = __ffsll((unsigned long long)f) - 1;
       f &= f - 1ull;
       const uint32_t kind = ((iw >> b) & 1ull) ? 0u : kCandPipelineBit;
-      out_cand[(size_t)t * M + r] = (uint32_t)(c * 64 + b) | kind;
+      cand[r] = (uint32_t)(c * 64 + b) | kind;
       ++r;
     }
     found += total;
@@ -126,10 +129,10 @@ __global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restr
   }
 }
 
-hipError_t launch_select(const uint64_t* feas, const uint64_t* idlem, int32_t W, int32_t n_tasks, int32_t M,
-                         uint32_t* out_cand, uint32_t* out_count, hipStream_t stream) {
-  if (n_tasks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(kbg_select_kernel, dim3((n_tasks + 3) / 4), dim3(256), 0, stream, feas, idlem, W, n_tasks, M,
+hipError_t launch_select(const uint64_t* feas, const uint64_t* idlem, int32_t W, int32_t n_rows,
+                         const uint32_t* cap_off, uint32_t* out_cand, uint32_t* out_count, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kbg_select_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, stream, feas, idlem, W, n_rows, cap_off,
                      out_cand, out_count);
   return hipGetLastError();
 }

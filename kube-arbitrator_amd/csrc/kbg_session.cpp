@@ -295,6 +295,8 @@ void free_device(Session& S) {
   if (S.h_tasks) (void)hipHostFree(S.h_tasks);
   if (S.h_cand) (void)hipHostFree(S.h_cand);
   if (S.h_count) (void)hipHostFree(S.h_count);
+  if (S.h_capoff) (void)hipHostFree(S.h_capoff);
+  S.h_capoff = nullptr;
   if (S.h_deltas) (void)hipHostFree(S.h_deltas);
   S.h_tasks = nullptr;
   S.h_cand = S.h_count = nullptr;
@@ -350,26 +352,21 @@ kbg_status upload_nodes(Session& S) {
   return copy_soa(S, S.d_nodes, S.d_nodes0);
 }
 
-// Evaluates tasks[0..n) (n <= K) on the device against the current table.
-kbg_status device_scan(Session& S, const int32_t* tasks, int32_t n) {
-  for (int32_t i = 0; i < n; ++i) {
-    const int32_t t = tasks[i];
-    kbg::TaskRec& r = S.h_tasks[i];
-    r.req[0] = S.treq[t].c;
-    r.req[1] = S.treq[t].m;
-    r.req[2] = S.treq[t].g;
-    r.cls = S.task_class[t];
-    r.pad = 0;
-  }
-  HIP_TRY(hipMemcpyAsync(S.d_tasks, S.h_tasks, (size_t)n * sizeof(kbg::TaskRec), hipMemcpyHostToDevice, S.stream));
+// One device round trip for a batch: rows[0..G) are the distinct evaluation
+// rows (a task in full-scan mode, a (class, request) shape otherwise), each
+// given cap_off[g+1]-cap_off[g] candidate slots. Fills S.h_cand / S.h_count.
+kbg_status device_scan(Session& S, int32_t G) {
+  const uint32_t total = S.h_capoff[G];
+  HIP_TRY(hipMemcpyAsync(S.d_tasks, S.h_tasks, (size_t)G * sizeof(kbg::TaskRec), hipMemcpyHostToDevice, S.stream));
+  HIP_TRY(hipMemcpyAsync(S.d_capoff, S.h_capoff, (size_t)(G + 1) * 4, hipMemcpyHostToDevice, S.stream));
   HIP_TRY(hipEventRecord(S.ev[0], S.stream));
-  HIP_TRY(kbg::launch_scan(S.d_nodes, S.n_nodes, S.W, S.d_class_mask, S.d_tasks, n, S.pred_active ? 1 : 0, S.d_feas,
+  HIP_TRY(kbg::launch_scan(S.d_nodes, S.n_nodes, S.W, S.d_class_mask, S.d_tasks, G, S.pred_active ? 1 : 0, S.d_feas,
                            S.d_idlem, S.stream));
   HIP_TRY(hipEventRecord(S.ev[1], S.stream));
-  HIP_TRY(kbg::launch_select(S.d_feas, S.d_idlem, S.W, n, S.M, S.d_cand, S.d_count, S.stream));
+  HIP_TRY(kbg::launch_select(S.d_feas, S.d_idlem, S.W, G, S.d_capoff, S.d_cand, S.d_count, S.stream));
   HIP_TRY(hipEventRecord(S.ev[2], S.stream));
-  HIP_TRY(hipMemcpyAsync(S.h_count, S.d_count, (size_t)n * 4, hipMemcpyDeviceToHost, S.stream));
-  HIP_TRY(hipMemcpyAsync(S.h_cand, S.d_cand, (size_t)n * S.M * 4, hipMemcpyDeviceToHost, S.stream));
+  HIP_TRY(hipMemcpyAsync(S.h_count, S.d_count, (size_t)G * 4, hipMemcpyDeviceToHost, S.stream));
+  HIP_TRY(hipMemcpyAsync(S.h_cand, S.d_cand, (size_t)total * 4, hipMemcpyDeviceToHost, S.stream));
   HIP_TRY(hipStreamSynchronize(S.stream));
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, S.ev[0], S.ev[1]));
@@ -377,8 +374,8 @@ kbg_status device_scan(Session& S, const int32_t* tasks, int32_t n) {
   HIP_TRY(hipEventElapsedTime(&ms, S.ev[1], S.ev[2]));
   S.stats.select_kernel_ms += ms;
   S.stats.scan_launches++;
-  S.stats.evaluations += n;
-  S.stats.node_visits += (int64_t)n * S.n_nodes;
+  S.stats.evaluations += G;
+  S.stats.node_visits += (int64_t)G * S.n_nodes;
   return KBG_OK;
 }
 
@@ -402,18 +399,69 @@ kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
   return KBG_OK;
 }
 
-// Sequential commit of one task against its batch-start candidate list.
+// Groups the tasks of a batch into device rows and sizes their candidate
+// lists. Full-scan mode: one row per task with M slots (every evaluation
+// scans the whole table — the SURVEY §8(d) roofline rule). Grouped mode: one
+// row per distinct (class, request) shape with (tasks of the shape + M) slots;
+// tasks of a shape share one first-fit list and a cursor (Resolver).
+struct Grouper {
+  Session& S;
+  std::unordered_map<ShapeKey, int32_t, ShapeHash> index;
+  std::vector<int32_t> row_of;  // per batch entry
+  int32_t build(const std::vector<int32_t>& bt) {
+    index.clear();
+    row_of.assign(bt.size(), 0);
+    std::vector<int32_t> count;
+    int32_t G = 0;
+    for (size_t i = 0; i < bt.size(); ++i) {
+      const int32_t t = bt[i];
+      int32_t g;
+      if (S.opts.full_scan) {
+        g = G++;
+        count.push_back(0);
+      } else {
+        auto it = index.emplace(ShapeKey{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g}, G);
+        if (it.second) {
+          ++G;
+          count.push_back(0);
+        }
+        g = it.first->second;
+      }
+      row_of[i] = g;
+      if (count[g]++ == 0) {
+        kbg::TaskRec& r = S.h_tasks[g];
+        r.req[0] = S.treq[t].c;
+        r.req[1] = S.treq[t].m;
+        r.req[2] = S.treq[t].g;
+        r.cls = S.task_class[t];
+        r.pad = 0;
+      }
+    }
+    S.h_capoff[0] = 0;
+    for (int32_t g = 0; g < G; ++g) {
+      const uint32_t want = S.opts.full_scan ? (uint32_t)S.M : (uint32_t)std::min(count[g] + S.M, 4096);
+      S.h_capoff[g + 1] = S.h_capoff[g] + want;
+    }
+    return G;
+  }
+};
+
+// In-order commit against the batch-start candidate lists. A row's cursor
+// only moves forward: a candidate found infeasible for a (class, request)
+// shape stays infeasible for every later task of that shape (monotonicity).
 enum { RES_OK = 0, RES_TRUNC = 1, RES_PANIC = 2 };
 struct Resolver {
   Session& S;
   std::vector<int32_t>& mark;
   int32_t stamp;
-  int resolve(int32_t i, int32_t t, int32_t* node, int32_t* kind) {
-    const uint32_t cnt = S.h_count[i];
+  std::vector<int32_t> cursor;
+  void reset(int32_t G) { cursor.assign(G, 0); }
+  int resolve(int32_t g, int32_t t, int32_t* node, int32_t* kind) {
+    const uint32_t cnt = S.h_count[g];
     const int32_t n = (int32_t)(cnt & kbg::kCountMask);
-    const uint32_t* c = S.h_cand + (size_t)i * S.M;
+    const uint32_t* c = S.h_cand + S.h_capoff[g];
     const Res& r = S.treq[t];
-    for (int32_t k = 0; k < n; ++k) {
+    for (int32_t& k = cursor[g]; k < n; ++k) {
       const int32_t nd = (int32_t)(c[k] & ~kbg::kCandPipelineBit);
       if (S.nil_node[nd] && S.pred_active) return RES_PANIC;
       if (mark[nd] != stamp) {
@@ -449,7 +497,6 @@ void mirror_add(Session& S, int32_t t, int32_t nd, int32_t kind) {
   }
   S.ntasks[nd]++;
 }
-
 kbg_status validate(const kbg_snapshot* s) {
   if (!s) return fail(KBG_E_INVALID, "null snapshot");
   auto in = [](int32_t v, int32_t n) { return v >= 0 && v < n; };
@@ -540,6 +587,8 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.K = S.opts.batch_tasks > 0 ? S.opts.batch_tasks : 2048;
   S.M = S.opts.candidates > 0 ? S.opts.candidates : 32;
   if (S.M > 4096) return fail(KBG_E_INVALID, "candidates > 4096");
+  // full-scan: K rows x M slots; grouped: sum over shapes of min(n_s + M, 4096) <= K + K*M
+  S.cand_cap = (int64_t)S.K * S.M + (S.opts.full_scan ? 0 : S.K);
 
   S.strs.assign(snap->strings, snap->strings + snap->n_strings);
   {
@@ -777,11 +826,13 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   if ((st = alloc_soa(S, &S.d_nodes)) || (st = alloc_soa(S, &S.d_nodes0))) return st;
   if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) || (st = dalloc(S, &S.d_tasks, S.K)) ||
       (st = dalloc(S, &S.d_feas, (size_t)S.K * S.W)) || (st = dalloc(S, &S.d_idlem, (size_t)S.K * S.W)) ||
-      (st = dalloc(S, &S.d_cand, (size_t)S.K * S.M)) || (st = dalloc(S, &S.d_count, S.K)) ||
+      (st = dalloc(S, &S.d_cand, (size_t)S.cand_cap)) || (st = dalloc(S, &S.d_count, S.K)) ||
+      (st = dalloc(S, &S.d_capoff, (size_t)S.K + 1)) ||
       (st = dalloc(S, &S.d_deltas, S.K)))
     return st;
   HIP_TRY(hipHostMalloc((void**)&S.h_tasks, (size_t)S.K * sizeof(kbg::TaskRec), hipHostMallocDefault));
-  HIP_TRY(hipHostMalloc((void**)&S.h_cand, (size_t)S.K * S.M * 4, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&S.h_cand, (size_t)S.cand_cap * 4, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&S.h_capoff, ((size_t)S.K + 1) * 4, hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void**)&S.h_count, (size_t)S.K * 4, hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void**)&S.h_deltas, (size_t)S.K * sizeof(kbg::NodeDelta), hipHostMallocDefault));
   if ((st = upload_nodes(S))) return st;
@@ -825,14 +876,14 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
 
 kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
   if (S.allocated) return fail(KBG_E_INVALID, "kbg_allocate already ran on this session; call kbg_session_reset");
-  const auto t0 = std::chrono::steady_clock::now();
-  S.stats.batches = S.stats.mispredictions = S.stats.truncations = 0;
-  S.stats.evaluations = S.stats.node_visits = S.stats.scan_launches = 0;
-  S.stats.scan_kernel_ms = S.stats.select_kernel_ms = 0;
-  S.stats.engine_ms = S.stats.resolve_ms = S.stats.device_ms = S.stats.delta_ms = 0;
-  S.stats.replayed = 0;
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+  const auto t0 = clk::now();
+  const int32_t n_classes = S.stats.n_classes;
+  const double open_ms = S.stats.open_ms;
+  S.stats = kbg_stats{};
+  S.stats.n_classes = n_classes;
+  S.stats.open_ms = open_ms;
 
   Engine E = S.init;
   Engine ckpt;
@@ -847,6 +898,8 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   bt.reserve(S.K);
   int32_t stamp = 0;
   kbg_status result = KBG_OK;
+  Grouper grouper{S, {}, {}};
+  Resolver rs{S, mark, 0, {}};
 
   auto shape = [&](int32_t t) { return ShapeKey{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g}; };
   auto job_ready_committed = [&](int32_t j) {
@@ -854,7 +907,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   };
 
   for (;;) {
-    // 1. predict the next K evaluations
+    // 1. predict the next K evaluations (success unless the shape already failed)
     auto tp = clk::now();
     ckpt = E;
     bt.clear();
@@ -870,23 +923,24 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     S.stats.engine_ms += ms_since(tp);
     if (bt.empty()) break;
     S.stats.batches++;
-    // 2. device: feasibility scan + first-M candidates against the batch-start table
+    // 2. device: feasibility scan + first-fit candidate lists against the batch-start table
     tp = clk::now();
-    kbg_status st = device_scan(S, bt.data(), (int32_t)bt.size());
+    const int32_t G = grouper.build(bt);
+    kbg_status st = device_scan(S, G);
     if (st != KBG_OK) return st;
     S.stats.device_ms += ms_since(tp);
     // 3. commit in order
     tp = clk::now();
-    ++stamp;
+    rs.stamp = ++stamp;
+    rs.reset(G);
     touched.clear();
     bactual.assign(bt.size(), 0);
-    Resolver rs{S, mark, stamp};
     int32_t cut = -1;
     bool panic = false;
     for (int32_t i = 0; i < (int32_t)bt.size(); ++i) {
       const int32_t t = bt[i];
       int32_t node = -1, kind = 0;
-      const int r = rs.resolve(i, t, &node, &kind);
+      const int r = rs.resolve(grouper.row_of[i], t, &node, &kind);
       if (r == RES_TRUNC) {
         cut = i;
         S.stats.truncations++;
@@ -948,7 +1002,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   }
   S.fin = E;
   S.allocated = true;
-  S.stats.allocate_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  S.stats.allocate_ms = ms_since(t0);
   if (n_out) *n_out = (int32_t)dec.size();
   if ((int32_t)dec.size() > cap || (!out && !dec.empty())) {
     if (result == KBG_OK) result = fail(KBG_E_CAPACITY, "decision buffer too small: need " + std::to_string(dec.size()));
@@ -1023,20 +1077,26 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
   Session& S = s->s;
   HIP_TRY(hipSetDevice(S.device));
   for (int32_t i = 0; i < n; ++i)
-    if (tasks[i] < 0 || tasks[i] >= S.n_tasks) return fail(KBG_E_INVALID, "task index");
-  std::vector<int32_t> mark(S.n_nodes, -1), touched;
-  int32_t done = 0;
+    if (tasks[i] < 0 || tasks[i] >= S.n_tasks || !S.pending_candidate[tasks[i]])
+      return fail(KBG_E_INVALID, "task index (must be a Pending, non-BestEffort session task)");
+  std::vector<int32_t> mark(S.n_nodes, -1), touched, bt;
+  Grouper grouper{S, {}, {}};
+  Resolver rs{S, mark, 0, {}};
+  int32_t done = 0, stamp = 0;
   bool stop = false;
   while (done < n && !stop) {
     const int32_t cnt = std::min(n - done, S.K);
-    kbg_status st = device_scan(S, tasks + done, cnt);
+    bt.assign(tasks + done, tasks + done + cnt);
+    const int32_t G = grouper.build(bt);
+    kbg_status st = device_scan(S, G);
     if (st != KBG_OK) return st;
     touched.clear();
-    Resolver rs{S, mark, 1};
+    rs.stamp = ++stamp;
+    rs.reset(G);
     int32_t i = 0;
     for (; i < cnt; ++i) {
       int32_t node = -1, kind = 0;
-      const int r = rs.resolve(i, tasks[done + i], &node, &kind);
+      const int r = rs.resolve(grouper.row_of[i], bt[i], &node, &kind);
       if (r == RES_TRUNC) break;  // rescan from this task with the updated table
       if (r == RES_PANIC) {
         if ((st = push_deltas(S, touched)) != KBG_OK) return st;
@@ -1046,9 +1106,9 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
       out_node[done + i] = node;
       if (out_kind) out_kind[done + i] = kind;
       if (node >= 0) {
-        mirror_add(S, tasks[done + i], node, kind);
-        if (mark[node] != 1) {
-          mark[node] = 1;
+        mirror_add(S, bt[i], node, kind);
+        if (mark[node] != stamp) {
+          mark[node] = stamp;
           touched.push_back(node);
         }
         if (stop_at_first_success) {
@@ -1058,7 +1118,6 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
         }
       }
     }
-    for (int32_t nd : touched) mark[nd] = -1;
     if ((st = push_deltas(S, touched)) != KBG_OK) return st;
     done += i;
   }

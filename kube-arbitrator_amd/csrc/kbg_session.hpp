@@ -122,7 +122,8 @@ struct Session {
   hipStream_t stream = nullptr;
   int32_t W = 0;            // u64 words per node bitmap row
   int32_t n_classes = 0;
-  int32_t K = 0, M = 0;     // batch tasks, candidates per task
+  int32_t K = 0, M = 0;     // batch tasks, candidates per row (full-scan) / slack (grouped)
+  int64_t cand_cap = 0;     // candidate slots allocated
   NodeSoA d_nodes{};
   NodeSoA d_nodes0{};       // pristine copy for kbg_session_reset
   uint64_t* d_class_mask = nullptr;
@@ -131,6 +132,8 @@ struct Session {
   uint64_t* d_idlem = nullptr;
   uint32_t* d_cand = nullptr;
   uint32_t* d_count = nullptr;
+  uint32_t* d_capoff = nullptr;   // per-row candidate slot offsets
+  uint32_t* h_capoff = nullptr;   // pinned
   NodeDelta* d_deltas = nullptr;
   TaskRec* h_tasks = nullptr;    // pinned
   uint32_t* h_cand = nullptr;    // pinned

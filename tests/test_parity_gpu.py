@@ -81,6 +81,10 @@ def test_config_parity(cid):
     {"batch_tasks": 7, "candidates": 2},
     {"batch_tasks": 64, "candidates": 4},
     {"batch_tasks": 4096, "candidates": 256},
+    {"batch_tasks": 1, "candidates": 1, "full_scan": 1},
+    {"batch_tasks": 7, "candidates": 2, "full_scan": 1},
+    {"batch_tasks": 64, "candidates": 4, "full_scan": 1},
+    {"batch_tasks": 2048, "candidates": 32, "full_scan": 1},
 ])
 def test_batching_is_exact(opts):
     """Speculation, truncation and replay must not change any decision."""
@@ -94,7 +98,7 @@ def test_batching_is_exact(opts):
 def test_fuzz_parity(seed):
     fx = synth.random_fixture(seed)
     ref = run_oracle(fx)
-    got, ssn = run_fixture(fx, {"batch_tasks": 1 + seed % 9, "candidates": 1 + seed % 5})
+    got, ssn = run_fixture(fx, {"batch_tasks": 1 + seed % 9, "candidates": 1 + seed % 5, "full_scan": seed % 2})
     compare_outputs(ref, got)
     if ssn:
         ssn.close()
@@ -111,9 +115,16 @@ def test_fuzz_parity_heap_rule(seed):
 
 
 @pytest.mark.slow
-def test_config3_full_parity():
-    """C3 (5k nodes x 100k tasks) end to end, every decision."""
-    fx = synth.config_fixture(3)
-    got, ssn = run_fixture(fx)
-    compare_outputs(run_oracle(fx), got)
+@pytest.mark.parametrize("full_scan", [0, 1])
+def test_config3_full_parity(full_scan, c3_oracle):
+    """C3 (5k nodes x 100k tasks) end to end, every decision, both scan modes."""
+    fx, ref = c3_oracle
+    got, ssn = run_fixture(fx, {"full_scan": full_scan})
+    compare_outputs(ref, got)
     ssn.close()
+
+
+@pytest.fixture(scope="module")
+def c3_oracle():
+    fx = synth.config_fixture(3)
+    return fx, run_oracle(fx)
