@@ -22,6 +22,16 @@
 
 namespace kbg {
 
+// Wave-uniform broadcast of lane j's value (j must be uniform): v_readlane.
+__device__ __forceinline__ uint64_t bcast_u64(uint64_t v, int j) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ double bcast_f64(double v, int j) {
+  return __builtin_bit_cast(double, bcast_u64(__builtin_bit_cast(uint64_t, v), j));
+}
+
 __device__ __forceinline__ bool le(double r, double a, double mn) {
   // (r < a || |a - r| < min)  — resource_info.go:142-146, one dimension
   return r < a || fabs(a - r) < mn;
@@ -55,23 +65,39 @@ __global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, int32_t n_nod
   }
   const bool node_ok = valid && (!cap_check || nt < mt);
   const int t0 = blockIdx.y * kScanTasksPerBlock;
-  const int t1 = min(n_tasks, t0 + kScanTasksPerBlock);
-  for (int t = t0; t < t1; ++t) {
-    const double q0 = tasks[t].req[0];
-    const double q1 = tasks[t].req[1];
-    const double q2 = tasks[t].req[2];
-    const int32_t cls = tasks[t].cls;
-    const uint64_t mw = class_mask[(size_t)cls * W + chunk];
+  const int nt_blk = min(n_tasks - t0, kScanTasksPerBlock);
+  // Prefetch: lane j holds evaluation row t0+j (request + its class-mask word
+  // for this chunk), so the row loop below reads registers, not dependent
+  // scalar loads.
+  double pq0 = 0, pq1 = 0, pq2 = 0;
+  uint64_t pmw = 0;
+  if (lane < nt_blk) {
+    const TaskRec tr = tasks[t0 + lane];
+    pq0 = tr.req[0];
+    pq1 = tr.req[1];
+    pq2 = tr.req[2];
+    pmw = class_mask[(size_t)tr.cls * W + chunk];
+  }
+  uint64_t keep_f = 0, keep_i = 0;  // lane j keeps the ballots of row t0+j
+  for (int j = 0; j < nt_blk; ++j) {
+    const double q0 = bcast_f64(pq0, j);
+    const double q1 = bcast_f64(pq1, j);
+    const double q2 = bcast_f64(pq2, j);
+    const uint64_t mw = bcast_u64(pmw, j);
     const bool sbit = (mw >> lane) & 1ull;
     const bool ifit = le(q0, ic, kMinMilliCPU) && le(q1, im, kMinMemory) && le(q2, ig, kMinMilliGPU);
     const bool rfit = le(q0, rc, kMinMilliCPU) && le(q1, rm, kMinMemory) && le(q2, rg, kMinMilliGPU);
     const bool feas = node_ok && sbit && (ifit || rfit);
     const uint64_t fm = __ballot(feas);
     const uint64_t imk = __ballot(feas && ifit);
-    if (lane == 0) {
-      out_feas[(size_t)t * W + chunk] = fm;
-      out_idle[(size_t)t * W + chunk] = imk;
+    if (lane == j) {
+      keep_f = fm;
+      keep_i = imk;
     }
+  }
+  if (lane < nt_blk) {
+    out_feas[(size_t)(t0 + lane) * W + chunk] = keep_f;
+    out_idle[(size_t)(t0 + lane) * W + chunk] = keep_i;
   }
 }
 

@@ -117,36 +117,40 @@ inline void go_down(int32_t* h, int i0, int n, L less, bool go111) {
   }
 }
 
+void make_job_key(const Session& S, const Engine& E, int32_t j, kbg::JobKey* k) {
+  const kbg_job& jb = S.jobs_in[j];
+  int n = 0;
+  bool zero = false;
+  for (int32_t p : S.job_chain) {
+    double v;
+    if (p == kbg::JO_PRIORITY) {  // priority.go:58-74 (higher first)
+      v = -(double)jb.priority;
+    } else if (p == kbg::JO_GANG) {  // gang.go:129-163 (non-ready first)
+      const bool ready = E.jready[j] >= jb.min_available;
+      k->c[n++] = zero ? 0.0 : (ready ? 1.0 : 0.0);
+      if (!ready) zero = true;
+      continue;
+    } else {  // drf.go:109-125 (lower share first)
+      v = E.jshare[j];
+    }
+    k->c[n++] = zero ? 0.0 : v;
+  }
+  while (n < 3) k->c[n++] = 0.0;
+  k->creation = jb.creation_ns;
+  k->rank = S.job_rank[j];
+  k->pad = 0;
+}
+
 struct Ops {
   const Session& S;
   Engine& E;
 
   bool job_ready(int32_t j) const { return E.jready[j] >= S.jobs_in[j].min_available; }
 
-  // Session.JobOrderFn (session_plugins.go:196-221) over the configured tiers.
-  bool job_less(int32_t a, int32_t b) const {
-    const kbg_job& ja = S.jobs_in[a];
-    const kbg_job& jb = S.jobs_in[b];
-    for (int32_t p : S.job_chain) {
-      if (p == kbg::JO_PRIORITY) {  // priority.go:58-74
-        if (ja.priority > jb.priority) return true;
-        if (ja.priority < jb.priority) return false;
-      } else if (p == kbg::JO_GANG) {  // gang.go:129-163
-        const bool ra = job_ready(a), rb = job_ready(b);
-        if (ra && rb) continue;
-        if (ra) return false;
-        if (rb) return true;
-        if (ja.creation_ns == jb.creation_ns) return S.job_rank[a] < S.job_rank[b];
-        return ja.creation_ns < jb.creation_ns;
-      } else {  // drf.go:109-125
-        const double sa = E.jshare[a], sb = E.jshare[b];
-        if (sa == sb) continue;
-        return sa < sb;
-      }
-    }
-    if (ja.creation_ns == jb.creation_ns) return S.job_rank[a] < S.job_rank[b];
-    return ja.creation_ns < jb.creation_ns;
-  }
+  // Session.JobOrderFn (session_plugins.go:196-221) over the configured tiers,
+  // as a precomputed key (kbg_session.hpp JobKey).
+  bool job_less(int32_t a, int32_t b) const { return kbg::job_key_less(E.jkey[a], E.jkey[b]); }
+  void refresh_key(int32_t j) { make_job_key(S, E, j, &E.jkey[j]); }
   // Session.QueueOrderFn (session_plugins.go:223-245); proportion.go:146-159
   bool queue_less(int32_t a, int32_t b) const {
     if (S.queue_order_prop) {
@@ -223,6 +227,7 @@ struct Ops {
       E.qshare[jq] = share_of(E.qalloc[jq], S.q_deserved[jq]);
     }
     E.jready[j]++;
+    refresh_key(j);
     jpush(q, j);  // :164-168
     qpush(q);     // :174
     E.in_job = false;
@@ -292,10 +297,10 @@ kbg_status copy_soa(Session& S, const kbg::NodeSoA& dst, const kbg::NodeSoA& src
 }
 
 void free_device(Session& S) {
-  if (S.h_tasks) (void)hipHostFree(S.h_tasks);
-  if (S.h_cand) (void)hipHostFree(S.h_cand);
-  if (S.h_count) (void)hipHostFree(S.h_count);
-  if (S.h_capoff) (void)hipHostFree(S.h_capoff);
+  if (S.h_up) (void)hipHostFree(S.h_up);
+  if (S.h_down) (void)hipHostFree(S.h_down);
+  S.h_up = nullptr;
+  S.h_down = nullptr;
   S.h_capoff = nullptr;
   if (S.h_deltas) (void)hipHostFree(S.h_deltas);
   S.h_tasks = nullptr;
@@ -357,17 +362,20 @@ kbg_status upload_nodes(Session& S) {
 // given cap_off[g+1]-cap_off[g] candidate slots. Fills S.h_cand / S.h_count.
 kbg_status device_scan(Session& S, int32_t G) {
   const uint32_t total = S.h_capoff[G];
-  HIP_TRY(hipMemcpyAsync(S.d_tasks, S.h_tasks, (size_t)G * sizeof(kbg::TaskRec), hipMemcpyHostToDevice, S.stream));
-  HIP_TRY(hipMemcpyAsync(S.d_capoff, S.h_capoff, (size_t)(G + 1) * 4, hipMemcpyHostToDevice, S.stream));
+  const size_t up_bytes = (size_t)G * sizeof(kbg::TaskRec) + (size_t)(G + 1) * 4;
+  const kbg::TaskRec* d_tasks = (const kbg::TaskRec*)S.d_up;
+  const uint32_t* d_capoff = (const uint32_t*)(S.d_up + (size_t)G * sizeof(kbg::TaskRec));
+  HIP_TRY(hipMemcpyAsync(S.d_up, S.h_up, up_bytes, hipMemcpyHostToDevice, S.stream));
   HIP_TRY(hipEventRecord(S.ev[0], S.stream));
-  HIP_TRY(kbg::launch_scan(S.d_nodes, S.n_nodes, S.W, S.d_class_mask, S.d_tasks, G, S.pred_active ? 1 : 0, S.d_feas,
+  HIP_TRY(kbg::launch_scan(S.d_nodes, S.n_nodes, S.W, S.d_class_mask, d_tasks, G, S.pred_active ? 1 : 0, S.d_feas,
                            S.d_idlem, S.stream));
   HIP_TRY(hipEventRecord(S.ev[1], S.stream));
-  HIP_TRY(kbg::launch_select(S.d_feas, S.d_idlem, S.W, G, S.d_capoff, S.d_cand, S.d_count, S.stream));
+  HIP_TRY(kbg::launch_select(S.d_feas, S.d_idlem, S.W, G, d_capoff, S.d_down + G, S.d_down, S.stream));
   HIP_TRY(hipEventRecord(S.ev[2], S.stream));
-  HIP_TRY(hipMemcpyAsync(S.h_count, S.d_count, (size_t)G * 4, hipMemcpyDeviceToHost, S.stream));
-  HIP_TRY(hipMemcpyAsync(S.h_cand, S.d_cand, (size_t)total * 4, hipMemcpyDeviceToHost, S.stream));
+  HIP_TRY(hipMemcpyAsync(S.h_down, S.d_down, ((size_t)G + total) * 4, hipMemcpyDeviceToHost, S.stream));
   HIP_TRY(hipStreamSynchronize(S.stream));
+  S.h_count = S.h_down;
+  S.h_cand = S.h_down + G;
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, S.ev[0], S.ev[1]));
   S.stats.scan_kernel_ms += ms;
@@ -393,8 +401,10 @@ kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
     }
     HIP_TRY(hipMemcpyAsync(S.d_deltas, S.h_deltas, cnt * sizeof(kbg::NodeDelta), hipMemcpyHostToDevice, S.stream));
     HIP_TRY(kbg::launch_apply(S.d_nodes, S.d_deltas, (int32_t)cnt, S.stream));
-    HIP_TRY(hipStreamSynchronize(S.stream));  // the pinned staging buffer is reused
     done += cnt;
+    // The staging buffer is reused by the next chunk or the next batch; the
+    // next device_scan's synchronize (same stream) retires this copy first.
+    if (done < touched.size()) HIP_TRY(hipStreamSynchronize(S.stream));
   }
   return KBG_OK;
 }
@@ -404,11 +414,14 @@ kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
 // scans the whole table — the SURVEY §8(d) roofline rule). Grouped mode: one
 // row per distinct (class, request) shape with (tasks of the shape + M) slots;
 // tasks of a shape share one first-fit list and a cursor (Resolver).
+constexpr int32_t kGroupSlack = 512;  // extra candidate slots per shape row (grouped mode)
+
 struct Grouper {
   Session& S;
   std::unordered_map<ShapeKey, int32_t, ShapeHash> index;
   std::vector<int32_t> row_of;  // per batch entry
   int32_t build(const std::vector<int32_t>& bt) {
+    S.h_tasks = (kbg::TaskRec*)S.h_up;
     index.clear();
     row_of.assign(bt.size(), 0);
     std::vector<int32_t> count;
@@ -437,9 +450,10 @@ struct Grouper {
         r.pad = 0;
       }
     }
+    S.h_capoff = (uint32_t*)(S.h_up + (size_t)G * sizeof(kbg::TaskRec));
     S.h_capoff[0] = 0;
     for (int32_t g = 0; g < G; ++g) {
-      const uint32_t want = S.opts.full_scan ? (uint32_t)S.M : (uint32_t)std::min(count[g] + S.M, 4096);
+      const uint32_t want = S.opts.full_scan ? (uint32_t)S.M : (uint32_t)std::min(count[g] + kGroupSlack, 4096);
       S.h_capoff[g + 1] = S.h_capoff[g] + want;
     }
     return G;
@@ -587,8 +601,8 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.K = S.opts.batch_tasks > 0 ? S.opts.batch_tasks : 2048;
   S.M = S.opts.candidates > 0 ? S.opts.candidates : 32;
   if (S.M > 4096) return fail(KBG_E_INVALID, "candidates > 4096");
-  // full-scan: K rows x M slots; grouped: sum over shapes of min(n_s + M, 4096) <= K + K*M
-  S.cand_cap = (int64_t)S.K * S.M + (S.opts.full_scan ? 0 : S.K);
+  // full-scan: K rows x M slots; grouped: sum over shapes of min(n_s + slack, 4096)
+  S.cand_cap = S.opts.full_scan ? (int64_t)S.K * S.M : (int64_t)S.K * (512 + 1);
 
   S.strs.assign(snap->strings, snap->strings + snap->n_strings);
   {
@@ -801,6 +815,8 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   E.jlen.assign(S.n_queues, 0);
   E.qheap.clear();
   E.qheap.reserve(S.n_jobs);
+  E.jkey.assign(S.n_jobs, kbg::JobKey{});
+  for (int32_t j = 0; j < S.n_jobs; ++j) make_job_key(S, E, j, &E.jkey[j]);
   {
     Ops ops{S, E};
     for (int32_t j = 0; j < S.n_jobs; ++j) {
@@ -824,16 +840,14 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   HIP_TRY(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   for (auto& e : S.ev) HIP_TRY(hipEventCreate(&e));
   if ((st = alloc_soa(S, &S.d_nodes)) || (st = alloc_soa(S, &S.d_nodes0))) return st;
-  if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) || (st = dalloc(S, &S.d_tasks, S.K)) ||
+  const size_t up_cap = (size_t)S.K * sizeof(kbg::TaskRec) + ((size_t)S.K + 1) * 4;
+  const size_t down_cap = (size_t)S.K + (size_t)S.cand_cap;
+  if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) || (st = dalloc(S, &S.d_up, up_cap)) ||
       (st = dalloc(S, &S.d_feas, (size_t)S.K * S.W)) || (st = dalloc(S, &S.d_idlem, (size_t)S.K * S.W)) ||
-      (st = dalloc(S, &S.d_cand, (size_t)S.cand_cap)) || (st = dalloc(S, &S.d_count, S.K)) ||
-      (st = dalloc(S, &S.d_capoff, (size_t)S.K + 1)) ||
-      (st = dalloc(S, &S.d_deltas, S.K)))
+      (st = dalloc(S, &S.d_down, down_cap)) || (st = dalloc(S, &S.d_deltas, S.K)))
     return st;
-  HIP_TRY(hipHostMalloc((void**)&S.h_tasks, (size_t)S.K * sizeof(kbg::TaskRec), hipHostMallocDefault));
-  HIP_TRY(hipHostMalloc((void**)&S.h_cand, (size_t)S.cand_cap * 4, hipHostMallocDefault));
-  HIP_TRY(hipHostMalloc((void**)&S.h_capoff, ((size_t)S.K + 1) * 4, hipHostMallocDefault));
-  HIP_TRY(hipHostMalloc((void**)&S.h_count, (size_t)S.K * 4, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&S.h_up, up_cap, hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&S.h_down, down_cap * 4, hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void**)&S.h_deltas, (size_t)S.K * sizeof(kbg::NodeDelta), hipHostMallocDefault));
   if ((st = upload_nodes(S))) return st;
 
@@ -1000,6 +1014,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       S.stats.engine_ms += ms_since(tp);
     }
   }
+  HIP_TRY(hipStreamSynchronize(S.stream));  // last delta write-back
   S.fin = E;
   S.allocated = true;
   S.stats.allocate_ms = ms_since(t0);
@@ -1100,6 +1115,7 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
       if (r == RES_TRUNC) break;  // rescan from this task with the updated table
       if (r == RES_PANIC) {
         if ((st = push_deltas(S, touched)) != KBG_OK) return st;
+        HIP_TRY(hipStreamSynchronize(S.stream));
         if (n_evaluated) *n_evaluated = done + i;
         return fail(KBG_E_REF_PANIC, "node with nil Node reached (predicates.go:122-123)");
       }
@@ -1121,6 +1137,7 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
     if ((st = push_deltas(S, touched)) != KBG_OK) return st;
     done += i;
   }
+  HIP_TRY(hipStreamSynchronize(S.stream));
   if (n_evaluated) *n_evaluated = done;
   return KBG_OK;
 }
@@ -1136,7 +1153,10 @@ kbg_status kbg_apply(kbg_session* s, int32_t node, const kbg_resource* req, int3
     if (!kbg::res_sub(target, r)) return fail(KBG_E_REF_PANIC, "Resource.Sub underflow (resource_info.go:100-110)");
   }
   S.ntasks[node]++;
-  return push_deltas(S, std::vector<int32_t>{node});
+  kbg_status st = push_deltas(S, std::vector<int32_t>{node});
+  if (st != KBG_OK) return st;
+  HIP_TRY(hipStreamSynchronize(S.stream));
+  return KBG_OK;
 }
 
 kbg_status kbg_job_state_get(kbg_session* s, int32_t job, kbg_job_state* out) {

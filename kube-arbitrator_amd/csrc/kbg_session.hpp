@@ -50,6 +50,26 @@ struct StaticHost {
 
 enum JobOrderPlugin : int32_t { JO_PRIORITY = 1, JO_GANG = 2, JO_DRF = 3 };
 
+// Session.JobOrderFn flattened into a lexicographic key (exactly equivalent
+// for the configured tier order): one component per job-order plugin
+// (priority: -Priority, gang: ready ? 1 : 0, drf: share), components after
+// gang zeroed for a non-ready job (gang.go:148-160 decides non-ready pairs by
+// creation/UID without consulting later plugins), then the fallback
+// (CreationTimestamp, UID) of session_plugins.go:212-220.
+struct JobKey {
+  double c[3];
+  int64_t creation;
+  int32_t rank;
+  int32_t pad;
+};
+inline bool job_key_less(const JobKey& a, const JobKey& b) {
+  if (a.c[0] != b.c[0]) return a.c[0] < b.c[0];
+  if (a.c[1] != b.c[1]) return a.c[1] < b.c[1];
+  if (a.c[2] != b.c[2]) return a.c[2] < b.c[2];
+  if (a.creation != b.creation) return a.creation < b.creation;
+  return a.rank < b.rank;
+}
+
 // Mutable state of the ordering engine (queue/job/task priority queues and
 // the plugin state they read). Flat arrays so a batch checkpoint is a copy.
 struct Engine {
@@ -64,6 +84,7 @@ struct Engine {
   std::vector<int32_t> jready;  // gang readyTaskNum
   std::vector<Res> qalloc;      // proportion attr.allocated
   std::vector<double> qshare;   // proportion attr.share
+  std::vector<JobKey> jkey;     // job order key (derived from the fields above)
 };
 
 struct Session {
@@ -127,17 +148,17 @@ struct Session {
   NodeSoA d_nodes{};
   NodeSoA d_nodes0{};       // pristine copy for kbg_session_reset
   uint64_t* d_class_mask = nullptr;
-  TaskRec* d_tasks = nullptr;
   uint64_t* d_feas = nullptr;
   uint64_t* d_idlem = nullptr;
-  uint32_t* d_cand = nullptr;
-  uint32_t* d_count = nullptr;
-  uint32_t* d_capoff = nullptr;   // per-row candidate slot offsets
-  uint32_t* h_capoff = nullptr;   // pinned
+  uint32_t* h_capoff = nullptr;   // per-row candidate slot offsets (inside h_up)
+  char* h_up = nullptr;           // pinned upload staging: TaskRec[G] then capoff[G+1]
+  char* d_up = nullptr;
+  uint32_t* h_down = nullptr;     // pinned download staging: count[G] then candidates
+  uint32_t* d_down = nullptr;
   NodeDelta* d_deltas = nullptr;
-  TaskRec* h_tasks = nullptr;    // pinned
-  uint32_t* h_cand = nullptr;    // pinned
-  uint32_t* h_count = nullptr;   // pinned
+  TaskRec* h_tasks = nullptr;    // = h_up
+  uint32_t* h_cand = nullptr;    // = h_down + G (set per batch)
+  uint32_t* h_count = nullptr;   // = h_down
   NodeDelta* h_deltas = nullptr; // pinned
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<void*> d_allocs;

@@ -53,10 +53,13 @@ def compare_outputs(ref, got):
     assert [(j["uid"], j["ready_num"], j["ready"]) for j in ref["jobs"]] == \
            [(j["uid"], j["ready_num"], j["ready"]) for j in got["jobs"]]
     for a, b in zip(ref["jobs"], got["jobs"]):
+        assert a["allocated"] == b["allocated"], (a, b)
         if "drf_share" in a:
             assert close(a["drf_share"], b["drf_share"]), (a, b)
-    assert [q["uid"] for q in ref["queues"]] == [q["uid"] for q in got["queues"]]
-    for a, b in zip(ref["queues"], got["queues"]):
+    assert sorted(q["uid"] for q in ref["queues"]) == sorted(q["uid"] for q in got["queues"])
+    gq = {q["uid"]: q for q in got["queues"]}
+    for a in ref["queues"]:
+        b = gq[a["uid"]]
         assert close(a["share"], b["share"]), (a, b)
         for k in ("deserved", "allocated", "request"):
             assert all(close(x, y) for x, y in zip(a[k], b[k])), (k, a, b)
