@@ -197,7 +197,8 @@ typedef struct kbg_decision {
 
 typedef struct kbg_job_state {
   int32_t ready_num;     /* gang readyTaskNum (gang.go:44-55) */
-  int32_t ready;         /* ssn.JobReady(job) */
+  int32_t ready;         /* gang jobReady predicate: ready_num >= MinAvailable (gang.go:72-78),
+                            reported whether or not the gang plugin is configured */
   double drf_share;      /* drf attr.share (drf.go:152-166); 0 if drf is off */
   kbg_resource drf_allocated;
 } kbg_job_state;

@@ -1165,7 +1165,7 @@ kbg_status kbg_job_state_get(kbg_session* s, int32_t job, kbg_job_state* out) {
   if (job < 0 || job >= S.n_jobs) return fail(KBG_E_INVALID, "job index");
   const Engine& E = S.allocated ? S.fin : S.init;
   out->ready_num = S.allocated ? S.committed_ready[job] : S.job_ready0[job];
-  out->ready = (!S.ready_gang || out->ready_num >= S.jobs_in[job].min_available) ? 1 : 0;
+  out->ready = out->ready_num >= S.jobs_in[job].min_available ? 1 : 0;  // gang jobReady (gang.go:72-78)
   out->drf_share = S.has_drf ? E.jshare[job] : 0.0;
   out->drf_allocated = to_kres(E.jalloc[job]);
   return KBG_OK;
