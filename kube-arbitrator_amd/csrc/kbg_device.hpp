@@ -105,12 +105,16 @@ enum NodeFlag : uint8_t { NF_UNSCHED = 1, NF_NIL = 2, NF_DEAD = 4 };
 hipError_t launch_build_class_mask(const StaticTables& t, int32_t n_classes, int32_t W, uint64_t* class_mask,
                                    hipStream_t stream);
 
+// `start`/`stop` (optional) are stamped at the kernel's own start and end
+// (hipExtLaunchKernelGGL), so their elapsed time is the kernel duration.
 hipError_t launch_scan(const NodeSoA& n, int32_t n_nodes, int32_t W, const uint64_t* class_mask, const TaskRec* tasks,
-                       int32_t n_tasks, int32_t cap_check, uint64_t* out_feas, uint64_t* out_idle, hipStream_t stream);
+                       int32_t n_tasks, int32_t cap_check, uint64_t* out_feas, uint64_t* out_idle, hipStream_t stream,
+                       hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
 // Row g gets cap_off[g+1]-cap_off[g] candidate slots at out_cand[cap_off[g]].
 hipError_t launch_select(const uint64_t* feas, const uint64_t* idlem, int32_t W, int32_t n_rows,
-                         const uint32_t* cap_off, uint32_t* out_cand, uint32_t* out_count, hipStream_t stream);
+                         const uint32_t* cap_off, uint32_t* out_cand, uint32_t* out_count, hipStream_t stream,
+                         hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
 hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream);
 

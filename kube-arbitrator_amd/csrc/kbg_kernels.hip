@@ -18,6 +18,8 @@
 //
 // fp64 is compared with the reference's own expression; the file is compiled
 // with -ffp-contract=off so nothing is fused.
+#include <hip/hip_ext.h>
+
 #include "kbg_device.hpp"
 
 namespace kbg {
@@ -103,11 +105,11 @@ __global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, int32_t n_nod
 
 hipError_t launch_scan(const NodeSoA& n, int32_t n_nodes, int32_t W, const uint64_t* class_mask, const TaskRec* tasks,
                        int32_t n_tasks, int32_t cap_check, uint64_t* out_feas, uint64_t* out_idle,
-                       hipStream_t stream) {
+                       hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
   if (n_tasks <= 0 || W <= 0) return hipSuccess;
   dim3 grid((W + kScanWaves - 1) / kScanWaves, (n_tasks + kScanTasksPerBlock - 1) / kScanTasksPerBlock);
-  hipLaunchKernelGGL(kbg_scan_kernel, grid, dim3(64 * kScanWaves), 0, stream, n, n_nodes, W, class_mask, tasks,
-                     n_tasks, cap_check, out_feas, out_idle);
+  hipExtLaunchKernelGGL(kbg_scan_kernel, grid, dim3(64 * kScanWaves), 0, stream, start, stop, 0, n, n_nodes, W,
+                        class_mask, tasks, n_tasks, cap_check, out_feas, out_idle);
   return hipGetLastError();
 }
 
@@ -156,10 +158,11 @@ __global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restr
 }
 
 hipError_t launch_select(const uint64_t* feas, const uint64_t* idlem, int32_t W, int32_t n_rows,
-                         const uint32_t* cap_off, uint32_t* out_cand, uint32_t* out_count, hipStream_t stream) {
+                         const uint32_t* cap_off, uint32_t* out_cand, uint32_t* out_count, hipStream_t stream,
+                         hipEvent_t start, hipEvent_t stop) {
   if (n_rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(kbg_select_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, stream, feas, idlem, W, n_rows, cap_off,
-                     out_cand, out_count);
+  hipExtLaunchKernelGGL(kbg_select_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, stream, start, stop, 0, feas, idlem, W,
+                        n_rows, cap_off, out_cand, out_count);
   return hipGetLastError();
 }
 

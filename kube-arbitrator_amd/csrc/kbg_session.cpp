@@ -151,19 +151,40 @@ struct Ops {
   // as a precomputed key (kbg_session.hpp JobKey).
   bool job_less(int32_t a, int32_t b) const { return kbg::job_key_less(E.jkey[a], E.jkey[b]); }
   void refresh_key(int32_t j) { make_job_key(S, E, j, &E.jkey[j]); }
-  // Session.QueueOrderFn (session_plugins.go:223-245); proportion.go:146-159
-  bool queue_less(int32_t a, int32_t b) const {
+  // Session.QueueOrderFn (session_plugins.go:223-245; proportion.go:146-159):
+  // share, then UID. With proportion on, E.qrank holds every queue's position
+  // in that order (maintained by reorder_queue), so a compare is two loads.
+  bool queue_less_slow(int32_t a, int32_t b) const {
     if (S.queue_order_prop) {
       const double sa = E.qshare[a], sb = E.qshare[b];
       if (sa != sb) return sa < sb;
     }
     return S.queue_rank[a] < S.queue_rank[b];
   }
+  bool queue_less(int32_t a, int32_t b) const { return E.qrank[a] < E.qrank[b]; }
+  void reorder_queue(int32_t q) {  // q's share changed: move it to its new position
+    int32_t pos = E.qrank[q];
+    const int32_t Q = (int32_t)E.qorder.size();
+    while (pos + 1 < Q && queue_less_slow(E.qorder[pos + 1], q)) {
+      E.qorder[pos] = E.qorder[pos + 1];
+      E.qrank[E.qorder[pos]] = pos;
+      ++pos;
+    }
+    while (pos > 0 && queue_less_slow(q, E.qorder[pos - 1])) {
+      E.qorder[pos] = E.qorder[pos - 1];
+      E.qrank[E.qorder[pos]] = pos;
+      --pos;
+    }
+    E.qorder[pos] = q;
+    E.qrank[q] = pos;
+  }
   // proportion.go:188-193
   bool overused(int32_t q) const {
     if (!S.has_prop || !S.q_has_attr[q]) return false;
     return kbg::res_le(S.q_deserved[q], E.qalloc[q]);
   }
+  // The queue heap is a literal container/heap: it holds one entry per job
+  // and entries keep stale keys, so its layout decides the order.
   void qpush(int32_t q) {
     E.qheap.push_back(q);
     go_up(E.qheap.data(), (int)E.qheap.size() - 1, [this](int32_t x, int32_t y) { return queue_less(x, y); });
@@ -176,18 +197,26 @@ struct Ops {
     E.qheap.pop_back();
     return q;
   }
+  // Per-queue job heaps. A job's key changes only while it is popped (drf and
+  // gang update the allocated job, drf.go:131-139, gang.go:44-55), so keys in
+  // a heap are static, the order is strict (UID tie-break) and the pop
+  // sequence does not depend on the heap layout. allocate.go pops
+  // the job, runs its tasks and pushes it back; here the job stays at the
+  // root meanwhile and is re-sifted (success) or removed (no task fitted).
   void jpush(int32_t q, int32_t j) {
     int32_t* h = E.jheap.data() + S.joff[q];
     const int n = E.jlen[q]++;
     h[n] = j;
     go_up(h, n, [this](int32_t x, int32_t y) { return job_less(x, y); });
   }
-  int32_t jpop(int32_t q) {
+  void jfix_top(int32_t q) {
+    go_down(E.jheap.data() + S.joff[q], 0, E.jlen[q], [this](int32_t x, int32_t y) { return job_less(x, y); }, false);
+  }
+  void jremove_top(int32_t q) {
     int32_t* h = E.jheap.data() + S.joff[q];
     const int n = --E.jlen[q];
     std::swap(h[0], h[n]);
-    go_down(h, 0, n, [this](int32_t x, int32_t y) { return job_less(x, y); }, S.heap_go111);
-    return h[n];
+    go_down(h, 0, n, [this](int32_t x, int32_t y) { return job_less(x, y); }, false);
   }
 
   // allocate.go:65-112: advance the control flow to the next task whose node
@@ -197,7 +226,8 @@ struct Ops {
       if (E.in_job) {
         const int32_t j = E.cur_j;
         if (E.cursor[j] < S.pend_len[j]) return S.pend[S.pend_off[j] + E.cursor[j]++];
-        qpush(E.cur_q);  // no task of the job fitted: allocate.go:173-174
+        jremove_top(E.cur_q);  // no task of the job fitted: the job is not pushed back
+        qpush(E.cur_q);        // allocate.go:173-174
         E.in_job = false;
         continue;
       }
@@ -205,7 +235,7 @@ struct Ops {
       const int32_t q = qpop();
       if (overused(q)) continue;     // :71-74
       if (E.jlen[q] == 0) continue;  // :78-81
-      E.cur_j = jpop(q);             // :85
+      E.cur_j = E.jheap[S.joff[q]];  // :85 jobs.Pop()
       E.cur_q = q;
       E.in_job = true;
     }
@@ -225,10 +255,11 @@ struct Ops {
       const int32_t jq = S.job_queue[j];
       kbg::res_add(E.qalloc[jq], r);
       E.qshare[jq] = share_of(E.qalloc[jq], S.q_deserved[jq]);
+      if (S.queue_order_prop) reorder_queue(jq);
     }
     E.jready[j]++;
     refresh_key(j);
-    jpush(q, j);  // :164-168
+    jfix_top(q);  // :164-168 jobs.Push(job)
     qpush(q);     // :174
     E.in_job = false;
   }
@@ -360,31 +391,39 @@ kbg_status upload_nodes(Session& S) {
 // One device round trip for a batch: rows[0..G) are the distinct evaluation
 // rows (a task in full-scan mode, a (class, request) shape otherwise), each
 // given cap_off[g+1]-cap_off[g] candidate slots. Fills S.h_cand / S.h_count.
-kbg_status device_scan(Session& S, int32_t G) {
+kbg_status device_launch(Session& S, int32_t G) {
   const uint32_t total = S.h_capoff[G];
   const size_t up_bytes = (size_t)G * sizeof(kbg::TaskRec) + (size_t)(G + 1) * 4;
   const kbg::TaskRec* d_tasks = (const kbg::TaskRec*)S.d_up;
   const uint32_t* d_capoff = (const uint32_t*)(S.d_up + (size_t)G * sizeof(kbg::TaskRec));
   HIP_TRY(hipMemcpyAsync(S.d_up, S.h_up, up_bytes, hipMemcpyHostToDevice, S.stream));
-  HIP_TRY(hipEventRecord(S.ev[0], S.stream));
   HIP_TRY(kbg::launch_scan(S.d_nodes, S.n_nodes, S.W, S.d_class_mask, d_tasks, G, S.pred_active ? 1 : 0, S.d_feas,
-                           S.d_idlem, S.stream));
-  HIP_TRY(hipEventRecord(S.ev[1], S.stream));
-  HIP_TRY(kbg::launch_select(S.d_feas, S.d_idlem, S.W, G, d_capoff, S.d_down + G, S.d_down, S.stream));
-  HIP_TRY(hipEventRecord(S.ev[2], S.stream));
+                           S.d_idlem, S.stream, S.ev[0], S.ev[1]));
+  HIP_TRY(kbg::launch_select(S.d_feas, S.d_idlem, S.W, G, d_capoff, S.d_down + G, S.d_down, S.stream, S.ev[2],
+                             S.ev[3]));
   HIP_TRY(hipMemcpyAsync(S.h_down, S.d_down, ((size_t)G + total) * 4, hipMemcpyDeviceToHost, S.stream));
+  return KBG_OK;
+}
+
+kbg_status device_wait(Session& S, int32_t G) {
   HIP_TRY(hipStreamSynchronize(S.stream));
   S.h_count = S.h_down;
   S.h_cand = S.h_down + G;
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, S.ev[0], S.ev[1]));
   S.stats.scan_kernel_ms += ms;
-  HIP_TRY(hipEventElapsedTime(&ms, S.ev[1], S.ev[2]));
+  HIP_TRY(hipEventElapsedTime(&ms, S.ev[2], S.ev[3]));
   S.stats.select_kernel_ms += ms;
   S.stats.scan_launches++;
   S.stats.evaluations += G;
   S.stats.node_visits += (int64_t)G * S.n_nodes;
   return KBG_OK;
+}
+
+// One synchronous device round trip (kbg_select path).
+kbg_status device_scan(Session& S, int32_t G) {
+  kbg_status st = device_launch(S, G);
+  return st != KBG_OK ? st : device_wait(S, G);
 }
 
 // Writes the rows of the nodes touched by the last commits back to HBM.
@@ -418,30 +457,27 @@ constexpr int32_t kGroupSlack = 512;  // extra candidate slots per shape row (gr
 
 struct Grouper {
   Session& S;
-  std::unordered_map<ShapeKey, int32_t, ShapeHash> index;
+  std::vector<int32_t> shape_row, shape_stamp, count;
   std::vector<int32_t> row_of;  // per batch entry
+  int32_t stamp = 0;
+  explicit Grouper(Session& s) : S(s), shape_row(s.n_shapes, -1), shape_stamp(s.n_shapes, -1) {}
   int32_t build(const std::vector<int32_t>& bt) {
     S.h_tasks = (kbg::TaskRec*)S.h_up;
-    index.clear();
-    row_of.assign(bt.size(), 0);
-    std::vector<int32_t> count;
+    ++stamp;
+    row_of.resize(bt.size());
+    count.clear();
     int32_t G = 0;
     for (size_t i = 0; i < bt.size(); ++i) {
       const int32_t t = bt[i];
       int32_t g;
-      if (S.opts.full_scan) {
+      const int32_t sh = S.task_shape[t];
+      if (!S.opts.full_scan && shape_stamp[sh] == stamp) {
+        g = shape_row[sh];
+      } else {
         g = G++;
         count.push_back(0);
-      } else {
-        auto it = index.emplace(ShapeKey{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g}, G);
-        if (it.second) {
-          ++G;
-          count.push_back(0);
-        }
-        g = it.first->second;
-      }
-      row_of[i] = g;
-      if (count[g]++ == 0) {
+        shape_stamp[sh] = stamp;
+        shape_row[sh] = g;
         kbg::TaskRec& r = S.h_tasks[g];
         r.req[0] = S.treq[t].c;
         r.req[1] = S.treq[t].m;
@@ -449,6 +485,8 @@ struct Grouper {
         r.cls = S.task_class[t];
         r.pad = 0;
       }
+      row_of[i] = g;
+      count[g]++;
     }
     S.h_capoff = (uint32_t*)(S.h_up + (size_t)G * sizeof(kbg::TaskRec));
     S.h_capoff[0] = 0;
@@ -819,6 +857,11 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   for (int32_t j = 0; j < S.n_jobs; ++j) make_job_key(S, E, j, &E.jkey[j]);
   {
     Ops ops{S, E};
+    E.qorder.resize(S.n_queues);
+    std::iota(E.qorder.begin(), E.qorder.end(), 0);
+    std::sort(E.qorder.begin(), E.qorder.end(), [&](int32_t a, int32_t b) { return ops.queue_less_slow(a, b); });
+    E.qrank.assign(S.n_queues, 0);
+    for (int32_t i = 0; i < S.n_queues; ++i) E.qrank[E.qorder[i]] = i;
     for (int32_t j = 0; j < S.n_jobs; ++j) {
       ops.qpush(S.job_queue[j]);
       ops.jpush(S.job_queue[j], j);
@@ -830,6 +873,16 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   compile_static_predicates(S, &sh);
   S.n_classes = sh.n_classes;
   S.W = (N + 63) / 64;
+  {
+    std::unordered_map<ShapeKey, int32_t, ShapeHash> ids;
+    S.task_shape.assign(S.n_tasks, -1);
+    for (int32_t t = 0; t < S.n_tasks; ++t) {
+      if (!S.pending_candidate[t]) continue;
+      auto it = ids.emplace(ShapeKey{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g}, (int32_t)ids.size());
+      S.task_shape[t] = it.first->second;
+    }
+    S.n_shapes = (int32_t)ids.size();
+  }
 
   // ---- device
   int ndev = 0;
@@ -906,42 +959,69 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   dec.reserve(S.pend.size());
   std::vector<std::vector<int32_t>> undispatched(S.n_jobs);
   S.committed_ready = S.job_ready0;
-  std::unordered_set<ShapeKey, ShapeHash> failed;
+  std::vector<char> failed(S.n_shapes, 0);  // shapes known to fit nowhere (monotone)
   std::vector<int32_t> bt, mark(S.n_nodes, -1), touched;
   std::vector<char> bpred, bactual;
   bt.reserve(S.K);
   int32_t stamp = 0;
   kbg_status result = KBG_OK;
-  Grouper grouper{S, {}, {}};
+  Grouper grouper(S);
   Resolver rs{S, mark, 0, {}};
 
-  auto shape = [&](int32_t t) { return ShapeKey{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g}; };
   auto job_ready_committed = [&](int32_t j) {
     return !S.ready_gang || S.committed_ready[j] >= S.jobs_in[j].min_available;
   };
 
-  for (;;) {
-    // 1. predict the next K evaluations (success unless the shape already failed)
-    auto tp = clk::now();
-    ckpt = E;
-    bt.clear();
-    bpred.clear();
-    while ((int32_t)bt.size() < S.K) {
+  // Predicts up to K evaluations from the current engine state (success
+  // unless the shape is known to fail) into (out, pred).
+  auto generate = [&](std::vector<int32_t>& out, std::vector<char>& pred) {
+    out.clear();
+    pred.clear();
+    while ((int32_t)out.size() < S.K) {
       const int32_t t = ops.next_task();
       if (t < 0) break;
-      const bool p = !failed.count(shape(t));
-      bt.push_back(t);
-      bpred.push_back(p);
+      const bool p = !failed[S.task_shape[t]];
+      out.push_back(t);
+      pred.push_back(p);
       ops.apply(t, p);
+    }
+  };
+  std::vector<int32_t> bt_next;
+  std::vector<char> bpred_next;
+  Engine ckpt_next;
+  bool have_next = false;
+
+  for (;;) {
+    // 1. the batch to evaluate: the one predicted while the previous batch was
+    //    on the device, or a fresh prediction from the engine state
+    auto tp = clk::now();
+    if (have_next) {
+      std::swap(bt, bt_next);
+      std::swap(bpred, bpred_next);
+      std::swap(ckpt, ckpt_next);
+      have_next = false;
+    } else {
+      ckpt = E;
+      generate(bt, bpred);
     }
     S.stats.engine_ms += ms_since(tp);
     if (bt.empty()) break;
     S.stats.batches++;
-    // 2. device: feasibility scan + first-fit candidate lists against the batch-start table
+    // 2. device: feasibility scan + first-fit candidate lists against the
+    //    batch-start table; meanwhile predict the following batch assuming
+    //    this one goes as predicted (discarded on a cut)
     tp = clk::now();
     const int32_t G = grouper.build(bt);
-    kbg_status st = device_scan(S, G);
+    kbg_status st = device_launch(S, G);
     if (st != KBG_OK) return st;
+    S.stats.device_ms += ms_since(tp);
+    tp = clk::now();
+    ckpt_next = E;
+    generate(bt_next, bpred_next);
+    have_next = !bt_next.empty();
+    S.stats.engine_ms += ms_since(tp);
+    tp = clk::now();
+    if ((st = device_wait(S, G)) != KBG_OK) return st;
     S.stats.device_ms += ms_since(tp);
     // 3. commit in order
     tp = clk::now();
@@ -984,7 +1064,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
           }
         }
       } else {
-        failed.insert(shape(t));
+        failed[S.task_shape[t]] = 1;
       }
       if (ok != (bool)bpred[i]) {
         cut = i + 1;
@@ -1001,9 +1081,11 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
                                      "(predicates.go:122-123)");
       break;
     }
-    // 4. on a cut, rebuild the engine state at the cut from the checkpoint
+    // 4. on a cut, drop the speculative next batch and rebuild the engine
+    //    state at the cut from this batch's checkpoint
     if (cut >= 0) {
       tp = clk::now();
+      have_next = false;
       E = ckpt;
       for (int32_t k = 0; k < cut; ++k) {
         const int32_t t = ops.next_task();
@@ -1095,7 +1177,7 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
     if (tasks[i] < 0 || tasks[i] >= S.n_tasks || !S.pending_candidate[tasks[i]])
       return fail(KBG_E_INVALID, "task index (must be a Pending, non-BestEffort session task)");
   std::vector<int32_t> mark(S.n_nodes, -1), touched, bt;
-  Grouper grouper{S, {}, {}};
+  Grouper grouper(S);
   Resolver rs{S, mark, 0, {}};
   int32_t done = 0, stamp = 0;
   bool stop = false;

@@ -85,6 +85,8 @@ struct Engine {
   std::vector<Res> qalloc;      // proportion attr.allocated
   std::vector<double> qshare;   // proportion attr.share
   std::vector<JobKey> jkey;     // job order key (derived from the fields above)
+  std::vector<int32_t> qorder;  // queues sorted by QueueOrderFn
+  std::vector<int32_t> qrank;   // position of each queue in qorder
 };
 
 struct Session {
@@ -120,6 +122,8 @@ struct Session {
   std::vector<int32_t> pend, pend_off, pend_len;         // per-job pending tasks in TaskOrderFn order
   std::vector<char> pending_candidate;                   // task is Pending and not BestEffort
   std::vector<int32_t> task_class;
+  std::vector<int32_t> task_shape;                       // (class, request) shape id of a pending task
+  int32_t n_shapes = 0;
   std::vector<Res> treq;
   Res drf_total, prop_total;
   std::vector<char> q_has_attr;
