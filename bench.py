@@ -80,20 +80,16 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--candidates", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on MI355X; gloo to rehearse on one GPU")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-
     import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", init_method="env://")
-        torch.cuda.set_device(local_rank)
-    else:
-        torch.cuda.set_device(0)
+    from kbgpu import dist as kdist
+    rank, world, local_rank = kdist.env_rank()
+    # KBG_BENCH_DEVICE pins every rank to one device (rehearsal on a 1-GPU box only)
+    device = int(os.environ.get("KBG_BENCH_DEVICE", local_rank))
+    torch.cuda.set_device(device)
+    kdist.init(args.dist_backend)
 
     from kbgpu import _abi, actions, synth  # noqa: F401
     from kbgpu.cache import cache_from_fixture
@@ -107,7 +103,7 @@ def main():
         # weak scaling: each rank schedules its own replica cluster
         fx["name"] += f"-replica{rank}"
     cache = cache_from_fixture(fx)
-    base_opts = {"device": local_rank}
+    base_opts = {"device": device}
     if args.batch:
         base_opts["batch_tasks"] = args.batch
     if args.candidates:
@@ -128,8 +124,8 @@ def main():
         for _ in range(warmup):
             step()
         agg = {"cycle_ms": [], "decisions": 0, "evals": 0, "scan_ms": 0.0, "sel_ms": 0.0, "launches": 0}
-        if barrier and dist:
-            dist.barrier()
+        if barrier:
+            kdist.barrier()
         torch.cuda.synchronize()
         t_start = time.perf_counter()
         for _ in range(steps):
@@ -142,9 +138,9 @@ def main():
             agg["sel_ms"] += st.select_kernel_ms
             agg["launches"] += st.scan_launches
         torch.cuda.synchronize()
-        if barrier and dist:
-            dist.barrier()
         agg["elapsed"] = time.perf_counter() - t_start
+        if barrier:
+            kdist.barrier()
         agg["stats"] = ssn.stats()
         agg["n_nodes"] = len(ssn.nodes)
         agg["pending"] = ssn.flat.pending_count
@@ -165,16 +161,8 @@ def main():
     log(f"[rank {rank}] C{cid} setup {time.time() - t0:.1f}s")
     prod = run_mode(0, args.steps, args.warmup, True)      # production: grouped shapes
     full = run_mode(1, max(1, min(3, args.steps)), 1, False)  # SURVEY roofline rule: every task scans all N
-    elapsed = prod["elapsed"]
     decisions = prod["decisions"]
-    total_decisions = decisions
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        d = torch.tensor([decisions], dtype=torch.float64, device="cuda")
-        dist.all_reduce(d, op=dist.ReduceOp.SUM)
-        total_decisions = int(d.item())
+    elapsed, total_decisions = kdist.aggregate(prod["elapsed"], decisions)
     st = prod["stats"]
     n_nodes = prod["n_nodes"]
 
@@ -218,8 +206,7 @@ def main():
         line["cpu_baseline"] = cpu_baseline(fx, f"C{cid}")
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    kdist.shutdown()
 
 
 if __name__ == "__main__":

@@ -24,16 +24,6 @@
 
 namespace kbg {
 
-// Wave-uniform broadcast of lane j's value (j must be uniform): v_readlane.
-__device__ __forceinline__ uint64_t bcast_u64(uint64_t v, int j) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ double bcast_f64(double v, int j) {
-  return __builtin_bit_cast(double, bcast_u64(__builtin_bit_cast(uint64_t, v), j));
-}
-
 __device__ __forceinline__ bool le(double r, double a, double mn) {
   // (r < a || |a - r| < min)  — resource_info.go:142-146, one dimension
   return r < a || fabs(a - r) < mn;
@@ -43,14 +33,65 @@ __device__ __forceinline__ bool le(double r, double a, double mn) {
 constexpr int kScanWaves = 4;          // waves per workgroup (256 threads)
 constexpr int kScanTasksPerBlock = 64; // task evaluations per workgroup
 
+// The row loop: lane = node, rows broadcast from LDS; REL_ZERO selects the
+// per-row precomputed Releasing fit (all nodes of the wave have Releasing 0).
+template <bool REL_ZERO>
+__device__ __forceinline__ void scan_rows(const double (*s_req)[4], const uint64_t* s_mask, int nt_blk, int lane,
+                                          int node_ok, double ic, double im, double ig, double rc, double rm,
+                                          double rg, uint64_t rz_rows, uint64_t* keep_f, uint64_t* keep_i) {
+  // Rows are processed 4 at a time with no remainder loop (ballots are
+  // convergent, so a runtime-count remainder would block unrolling); rows past
+  // nt_blk read stale LDS and their ballots are never stored.
+  for (int j0 = 0; j0 < nt_blk; j0 += 4) {
+#pragma unroll
+  for (int j = j0; j < j0 + 4; ++j) {
+    const double q0 = s_req[j][0];
+    const double q1 = s_req[j][1];
+    const double q2 = s_req[j][2];
+    const uint64_t mw = s_mask[j];
+    const int sbit = (int)((mw >> lane) & 1ull);
+    const int ifit = (int)le(q0, ic, kMinMilliCPU) & (int)le(q1, im, kMinMemory) & (int)le(q2, ig, kMinMilliGPU);
+    int rfit;
+    if (REL_ZERO) {
+      rfit = (int)((rz_rows >> j) & 1ull);
+    } else {
+      rfit = (int)le(q0, rc, kMinMilliCPU) & (int)le(q1, rm, kMinMemory) & (int)le(q2, rg, kMinMilliGPU);
+    }
+    const int ok = node_ok & sbit;
+    const uint64_t fm = __ballot((ok & (ifit | rfit)) != 0);
+    const uint64_t imk = __ballot((ok & ifit) != 0);
+    if (lane == j) {
+      *keep_f = fm;
+      *keep_i = imk;
+    }
+  }
+  }
+}
+
 __global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, int32_t n_nodes, int32_t W,
                                                        const uint64_t* __restrict__ class_mask,
                                                        const TaskRec* __restrict__ tasks, int32_t n_tasks,
                                                        int32_t cap_check, uint64_t* __restrict__ out_feas,
                                                        uint64_t* __restrict__ out_idle) {
+  // Evaluation rows of this workgroup, staged once in LDS and read back as
+  // same-address broadcasts; per wave, the class-mask word of each row for
+  // the wave's 64-node chunk.
+  __shared__ double s_req[kScanTasksPerBlock][4];
+  __shared__ uint64_t s_mask[kScanWaves][kScanTasksPerBlock];
   const int lane = threadIdx.x & 63;
-  const int chunk = blockIdx.x * kScanWaves + (threadIdx.x >> 6);
-  if (chunk >= W) return;  // wave-uniform exit
+  const int wave = threadIdx.x >> 6;
+  const int chunk = blockIdx.x * kScanWaves + wave;
+  const int t0 = blockIdx.y * kScanTasksPerBlock;
+  const int nt_blk = min(n_tasks - t0, kScanTasksPerBlock);
+  if (threadIdx.x < nt_blk) {
+    const TaskRec tr = tasks[t0 + threadIdx.x];
+    s_req[threadIdx.x][0] = tr.req[0];
+    s_req[threadIdx.x][1] = tr.req[1];
+    s_req[threadIdx.x][2] = tr.req[2];
+  }
+  if (lane < nt_blk && chunk < W) s_mask[wave][lane] = class_mask[(size_t)tasks[t0 + lane].cls * W + chunk];
+  __syncthreads();
+  if (chunk >= W) return;  // wave-uniform exit (after the barrier)
   const int node = chunk * 64 + lane;
   const bool valid = node < n_nodes;
   double ic = 0, im = 0, ig = 0, rc = 0, rm = 0, rg = 0;
@@ -65,38 +106,25 @@ __global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, int32_t n_nod
     nt = nd.ntasks[node];
     mt = nd.maxtasks[node];
   }
-  const bool node_ok = valid && (!cap_check || nt < mt);
-  const int t0 = blockIdx.y * kScanTasksPerBlock;
-  const int nt_blk = min(n_tasks - t0, kScanTasksPerBlock);
-  // Prefetch: lane j holds evaluation row t0+j (request + its class-mask word
-  // for this chunk), so the row loop below reads registers, not dependent
-  // scalar loads.
-  double pq0 = 0, pq1 = 0, pq2 = 0;
-  uint64_t pmw = 0;
-  if (lane < nt_blk) {
-    const TaskRec tr = tasks[t0 + lane];
-    pq0 = tr.req[0];
-    pq1 = tr.req[1];
-    pq2 = tr.req[2];
-    pmw = class_mask[(size_t)tr.cls * W + chunk];
+  const int node_ok = (int)valid & ((int)!cap_check | (int)(nt < mt));
+  // Releasing is usually zero on every node of the wave; then the Releasing
+  // fit of a row is LessEqual(req, 0) for every lane — the same expression,
+  // evaluated once per row (lane j for row j) instead of once per node.
+  const bool rel_zero_wave = __ballot(!(rc == 0.0 && rm == 0.0 && rg == 0.0)) == 0ull;
+  uint64_t rz_rows = 0;
+  if (rel_zero_wave) {
+    bool rz = false;
+    if (lane < nt_blk) {
+      const double q0 = s_req[lane][0], q1 = s_req[lane][1], q2 = s_req[lane][2];
+      rz = ((int)le(q0, 0.0, kMinMilliCPU) & (int)le(q1, 0.0, kMinMemory) & (int)le(q2, 0.0, kMinMilliGPU)) != 0;
+    }
+    rz_rows = __ballot(rz);
   }
   uint64_t keep_f = 0, keep_i = 0;  // lane j keeps the ballots of row t0+j
-  for (int j = 0; j < nt_blk; ++j) {
-    const double q0 = bcast_f64(pq0, j);
-    const double q1 = bcast_f64(pq1, j);
-    const double q2 = bcast_f64(pq2, j);
-    const uint64_t mw = bcast_u64(pmw, j);
-    const bool sbit = (mw >> lane) & 1ull;
-    const bool ifit = le(q0, ic, kMinMilliCPU) && le(q1, im, kMinMemory) && le(q2, ig, kMinMilliGPU);
-    const bool rfit = le(q0, rc, kMinMilliCPU) && le(q1, rm, kMinMemory) && le(q2, rg, kMinMilliGPU);
-    const bool feas = node_ok && sbit && (ifit || rfit);
-    const uint64_t fm = __ballot(feas);
-    const uint64_t imk = __ballot(feas && ifit);
-    if (lane == j) {
-      keep_f = fm;
-      keep_i = imk;
-    }
-  }
+  if (rel_zero_wave)
+    scan_rows<true>(s_req, s_mask[wave], nt_blk, lane, node_ok, ic, im, ig, rc, rm, rg, rz_rows, &keep_f, &keep_i);
+  else
+    scan_rows<false>(s_req, s_mask[wave], nt_blk, lane, node_ok, ic, im, ig, rc, rm, rg, rz_rows, &keep_f, &keep_i);
   if (lane < nt_blk) {
     out_feas[(size_t)(t0 + lane) * W + chunk] = keep_f;
     out_idle[(size_t)(t0 + lane) * W + chunk] = keep_i;
