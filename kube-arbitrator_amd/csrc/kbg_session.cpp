@@ -26,7 +26,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -941,6 +947,37 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   return KBG_OK;
 }
 
+// The host side of one allocate cycle runs on two threads:
+//   predictor (std::thread) — the ordering engine: predicts batches of K task
+//                             evaluations ahead, each with a checkpoint of the
+//                             engine state it started from;
+//   committer (caller)      — per batch: device scan, in-order commit against
+//                             the candidates, node-row write-back.
+// When a batch is cut (an unpredicted outcome or an exhausted candidate list)
+// the committer bumps the epoch and hands the predictor the batch's
+// checkpoint plus the actual outcomes up to the cut; the predictor restores,
+// replays them and continues; batches of an older epoch are dropped.
+struct Batch {
+  std::vector<int32_t> bt;
+  std::vector<char> bpred;
+  Engine ckpt;
+  int64_t epoch = 0;
+};
+
+struct Pipe {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<Batch*> ready;    // predicted, waiting for the committer
+  std::vector<Batch*> free;    // recycled buffers
+  int64_t epoch = 0;           // current epoch (committer-owned, read by predictor under mu)
+  bool rollback = false;       // predictor must restore `rb_ckpt` and replay
+  Engine rb_ckpt;
+  std::vector<int32_t> rb_tasks;
+  std::vector<char> rb_actual;
+  bool stop = false;
+  static constexpr size_t kDepth = 3;
+};
+
 kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
   if (S.allocated) return fail(KBG_E_INVALID, "kbg_allocate already ran on this session; call kbg_session_reset");
   using clk = std::chrono::steady_clock;
@@ -952,78 +989,142 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   S.stats.n_classes = n_classes;
   S.stats.open_ms = open_ms;
 
-  Engine E = S.init;
-  Engine ckpt;
-  Ops ops{S, E};
   std::vector<kbg_decision> dec;
   dec.reserve(S.pend.size());
   std::vector<std::vector<int32_t>> undispatched(S.n_jobs);
   S.committed_ready = S.job_ready0;
-  std::vector<char> failed(S.n_shapes, 0);  // shapes known to fit nowhere (monotone)
-  std::vector<int32_t> bt, mark(S.n_nodes, -1), touched;
-  std::vector<char> bpred, bactual;
-  bt.reserve(S.K);
+  // shapes known to fit nowhere (monotone): written by the committer, read by the predictor
+  std::unique_ptr<std::atomic<uint8_t>[]> failed(new std::atomic<uint8_t>[std::max(1, S.n_shapes)]);
+  for (int32_t i = 0; i < S.n_shapes; ++i) failed[i].store(0, std::memory_order_relaxed);
+  std::vector<int32_t> mark(S.n_nodes, -1), touched;
+  std::vector<char> bactual;
   int32_t stamp = 0;
   kbg_status result = KBG_OK;
   Grouper grouper(S);
   Resolver rs{S, mark, 0, {}};
-
   auto job_ready_committed = [&](int32_t j) {
     return !S.ready_gang || S.committed_ready[j] >= S.jobs_in[j].min_available;
   };
 
-  // Predicts up to K evaluations from the current engine state (success
-  // unless the shape is known to fail) into (out, pred).
-  auto generate = [&](std::vector<int32_t>& out, std::vector<char>& pred) {
-    out.clear();
-    pred.clear();
-    while ((int32_t)out.size() < S.K) {
-      const int32_t t = ops.next_task();
-      if (t < 0) break;
-      const bool p = !failed[S.task_shape[t]];
-      out.push_back(t);
-      pred.push_back(p);
-      ops.apply(t, p);
+  // ------------------------------------------------------------ predictor
+  Pipe P;
+  Engine E = S.init;
+  double engine_ms = 0;
+  int64_t replayed = 0;
+  std::string pred_error;
+  std::thread predictor([&]() {
+    Ops ops{S, E};
+    bool exhausted = false;
+    for (;;) {
+      Batch* b = nullptr;
+      int64_t my_epoch;
+      {
+        std::unique_lock<std::mutex> lk(P.mu);
+        P.cv.wait(lk, [&] { return P.stop || P.rollback || (!exhausted && P.ready.size() < Pipe::kDepth); });
+        if (P.stop) return;
+        if (P.rollback) {
+          const auto tp = clk::now();
+          E = P.rb_ckpt;
+          for (size_t k = 0; k < P.rb_tasks.size(); ++k) {
+            const int32_t t = ops.next_task();
+            if (t != P.rb_tasks[k]) {
+              pred_error = "internal: replay diverged";
+              P.stop = true;
+              P.ready.push_back(nullptr);
+              P.cv.notify_all();
+              return;
+            }
+            ops.apply(t, P.rb_actual[k]);
+          }
+          replayed += (int64_t)P.rb_tasks.size();
+          engine_ms += ms_since(tp);
+          P.rollback = false;
+          exhausted = false;
+        }
+        my_epoch = P.epoch;
+        if (!P.free.empty()) {
+          b = P.free.back();
+          P.free.pop_back();
+        }
+      }
+      if (!b) b = new Batch();
+      const auto tp = clk::now();
+      b->ckpt = E;
+      b->epoch = my_epoch;
+      b->bt.clear();
+      b->bpred.clear();
+      while ((int32_t)b->bt.size() < S.K) {
+        const int32_t t = ops.next_task();
+        if (t < 0) break;
+        const bool p = !failed[S.task_shape[t]].load(std::memory_order_relaxed);
+        b->bt.push_back(t);
+        b->bpred.push_back(p);
+        ops.apply(t, p);
+      }
+      engine_ms += ms_since(tp);
+      if (b->bt.empty()) exhausted = true;  // the empty batch marks the end of this epoch
+      std::lock_guard<std::mutex> lk(P.mu);
+      P.ready.push_back(b);
+      P.cv.notify_all();
     }
-  };
-  std::vector<int32_t> bt_next;
-  std::vector<char> bpred_next;
-  Engine ckpt_next;
-  bool have_next = false;
+  });
 
-  for (;;) {
-    // 1. the batch to evaluate: the one predicted while the previous batch was
-    //    on the device, or a fresh prediction from the engine state
-    auto tp = clk::now();
-    if (have_next) {
-      std::swap(bt, bt_next);
-      std::swap(bpred, bpred_next);
-      std::swap(ckpt, ckpt_next);
-      have_next = false;
-    } else {
-      ckpt = E;
-      generate(bt, bpred);
+  auto take = [&]() -> Batch* {
+    std::unique_lock<std::mutex> lk(P.mu);
+    P.cv.wait(lk, [&] { return !P.ready.empty(); });
+    Batch* b = P.ready.front();
+    P.ready.pop_front();
+    P.cv.notify_all();
+    return b;
+  };
+  auto recycle = [&](Batch* b) {
+    if (!b) return;
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.free.push_back(b);
+  };
+  auto finish = [&]() {
+    {
+      std::lock_guard<std::mutex> lk(P.mu);
+      P.stop = true;
+      P.cv.notify_all();
     }
-    S.stats.engine_ms += ms_since(tp);
-    if (bt.empty()) break;
+    predictor.join();
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (Batch* b : P.ready) delete b;
+    for (Batch* b : P.free) delete b;
+    P.ready.clear();
+    P.free.clear();
+  };
+
+  // ------------------------------------------------------------ committer
+  int64_t cur_epoch = 0;
+  for (;;) {
+    Batch* b = take();
+    if (!b) {  // predictor failed
+      finish();
+      return fail(KBG_E_INVALID, pred_error);
+    }
+    if (b->epoch != cur_epoch) {  // predicted before the last cut
+      recycle(b);
+      continue;
+    }
+    if (b->bt.empty()) {  // engine exhausted in the current epoch: the cycle is over
+      recycle(b);
+      break;
+    }
+    const std::vector<int32_t>& bt = b->bt;
     S.stats.batches++;
-    // 2. device: feasibility scan + first-fit candidate lists against the
-    //    batch-start table; meanwhile predict the following batch assuming
-    //    this one goes as predicted (discarded on a cut)
-    tp = clk::now();
+    // device: feasibility scan + first-fit candidate lists against the batch-start table
+    auto tp = clk::now();
     const int32_t G = grouper.build(bt);
     kbg_status st = device_launch(S, G);
-    if (st != KBG_OK) return st;
+    if (st == KBG_OK) st = device_wait(S, G);
+    if (st != KBG_OK) {
+      finish();
+      return st;
+    }
     S.stats.device_ms += ms_since(tp);
-    tp = clk::now();
-    ckpt_next = E;
-    generate(bt_next, bpred_next);
-    have_next = !bt_next.empty();
-    S.stats.engine_ms += ms_since(tp);
-    tp = clk::now();
-    if ((st = device_wait(S, G)) != KBG_OK) return st;
-    S.stats.device_ms += ms_since(tp);
-    // 3. commit in order
+    // commit in order
     tp = clk::now();
     rs.stamp = ++stamp;
     rs.reset(G);
@@ -1064,9 +1165,9 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
           }
         }
       } else {
-        failed[S.task_shape[t]] = 1;
+        failed[S.task_shape[t]].store(1, std::memory_order_relaxed);
       }
-      if (ok != (bool)bpred[i]) {
+      if (ok != (bool)b->bpred[i]) {
         cut = i + 1;
         S.stats.mispredictions++;
         break;
@@ -1074,30 +1175,35 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
     S.stats.resolve_ms += ms_since(tp);
     tp = clk::now();
-    if ((st = push_deltas(S, touched)) != KBG_OK) return st;
+    if ((st = push_deltas(S, touched)) != KBG_OK) {
+      finish();
+      return st;
+    }
     S.stats.delta_ms += ms_since(tp);
     if (panic) {
+      recycle(b);
       result = fail(KBG_E_REF_PANIC, "allocate reached a node whose NodeInfo.Node is nil with the predicates plugin on "
                                      "(predicates.go:122-123)");
       break;
     }
-    // 4. on a cut, drop the speculative next batch and rebuild the engine
-    //    state at the cut from this batch's checkpoint
-    if (cut >= 0) {
-      tp = clk::now();
-      have_next = false;
-      E = ckpt;
-      for (int32_t k = 0; k < cut; ++k) {
-        const int32_t t = ops.next_task();
-        if (t != bt[k]) return fail(KBG_E_INVALID, "internal: replay diverged");
-        ops.apply(t, bactual[k]);
-      }
-      S.stats.replayed += cut;
-      S.stats.engine_ms += ms_since(tp);
+    if (cut >= 0) {  // roll the predictor back to this batch's checkpoint + the actual prefix
+      std::lock_guard<std::mutex> lk(P.mu);
+      P.epoch = ++cur_epoch;
+      P.rollback = true;
+      P.rb_ckpt = b->ckpt;
+      P.rb_tasks.assign(bt.begin(), bt.begin() + cut);
+      P.rb_actual.assign(bactual.begin(), bactual.begin() + cut);
+      P.free.push_back(b);
+      P.cv.notify_all();
+    } else {
+      recycle(b);
     }
   }
+  finish();
   HIP_TRY(hipStreamSynchronize(S.stream));  // last delta write-back
   S.fin = E;
+  S.stats.engine_ms = engine_ms;
+  S.stats.replayed = replayed;
   S.allocated = true;
   S.stats.allocate_ms = ms_since(t0);
   if (n_out) *n_out = (int32_t)dec.size();
