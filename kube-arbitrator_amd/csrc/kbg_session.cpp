@@ -147,6 +147,46 @@ void make_job_key(const Session& S, const Engine& E, int32_t j, kbg::JobKey* k) 
   k->pad = 0;
 }
 
+// container/heap on queue ids compared through a rank table (rk[q] = position
+// of q in QueueOrderFn order). Hole-based sifting is the same algorithm as
+// Go's swap-based up/down: the element being moved is one side of every
+// compare, so swapping it step by step or writing it once at the end gives
+// the same array.
+inline void rank_heap_up(int32_t* h, int j, const int32_t* rk) {
+  const int32_t x = h[j];
+  const int32_t rx = rk[x];
+  while (j > 0) {
+    const int p = (j - 1) / 2;
+    if (!(rx < rk[h[p]])) break;
+    h[j] = h[p];
+    j = p;
+  }
+  h[j] = x;
+}
+inline void rank_heap_down(int32_t* h, int n, const int32_t* rk, bool go111) {
+  if (n <= 1) return;
+  const int32_t x = h[0];
+  const int32_t rx = rk[x];
+  int i = 0;
+  for (;;) {
+    const int j1 = 2 * i + 1;
+    if (j1 >= n) break;
+    int j = j1;
+    int32_t rj = rk[h[j1]];
+    if (j1 + 1 < n) {
+      const int32_t r2 = rk[h[j1 + 1]];
+      // go1.11: right child when !Less(j1, j2) (r2 <= r1); later: when Less(j2, j1)
+      const bool right = go111 ? (r2 <= rj) : (r2 < rj);
+      j += right ? 1 : 0;
+      rj = right ? r2 : rj;
+    }
+    if (!(rj < rx)) break;
+    h[i] = h[j];
+    i = j;
+  }
+  h[i] = x;
+}
+
 struct Ops {
   const Session& S;
   Engine& E;
@@ -193,12 +233,12 @@ struct Ops {
   // and entries keep stale keys, so its layout decides the order.
   void qpush(int32_t q) {
     E.qheap.push_back(q);
-    go_up(E.qheap.data(), (int)E.qheap.size() - 1, [this](int32_t x, int32_t y) { return queue_less(x, y); });
+    rank_heap_up(E.qheap.data(), (int)E.qheap.size() - 1, E.qrank.data());
   }
   int32_t qpop() {
     const int n = (int)E.qheap.size() - 1;
     std::swap(E.qheap[0], E.qheap[n]);
-    go_down(E.qheap.data(), 0, n, [this](int32_t x, int32_t y) { return queue_less(x, y); }, S.heap_go111);
+    rank_heap_down(E.qheap.data(), n, E.qrank.data(), S.heap_go111);
     const int32_t q = E.qheap.back();
     E.qheap.pop_back();
     return q;
