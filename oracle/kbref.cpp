@@ -739,6 +739,7 @@ struct Session {  // framework/session.go:35-61
   std::unordered_map<TaskInfo*, int> decisionOf;
   std::vector<std::pair<std::string, std::string>> binds;  // (ns/name, node) in dispatch order
   int64_t predicate_calls = 0;
+  std::vector<TaskInfo*> evaluated;  // every task whose node loop ran, in order
 
   // session_plugins.go:142-156
   bool Overused(QueueInfo* q) {
@@ -1215,6 +1216,7 @@ static void allocate_execute(Session* ssn) {
     PriorityQueue<TaskInfo>* tasks = pendingTasks[job->uid];
     while (!tasks->Empty()) {
       TaskInfo* task = tasks->Pop();
+      ssn->evaluated.push_back(task);
       bool assigned = false;
       if (!job->nodesFitDelta.empty()) job->nodesFitDelta.clear();
       for (NodeInfo* node : ssn->nodes) {
@@ -1432,6 +1434,8 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache) {
          ",\"node\":" + kbjson::quote(d.node) + ",\"kind\":\"" + (d.kind == KIND_ALLOCATE ? "allocate" : "pipeline") +
          "\",\"dispatched_at\":" + std::to_string(d.dispatched_at) + "}";
   }
+  o += "],\"evaluated\":[";
+  for (size_t i = 0; i < ssn->evaluated.size(); i++) o += (i ? "," : "") + kbjson::quote(ssn->evaluated[i]->uid);
   o += "],\"binds\":{";
   for (size_t i = 0; i < ssn->binds.size(); i++)
     o += (i ? "," : "") + kbjson::quote(ssn->binds[i].first) + ":" + kbjson::quote(ssn->binds[i].second);

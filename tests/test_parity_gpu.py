@@ -128,3 +128,82 @@ def test_config3_full_parity(full_scan, c3_oracle):
 def c3_oracle():
     fx = synth.config_fixture(3)
     return fx, run_oracle(fx)
+
+
+def _open(fx, opts=None):
+    from kbgpu.cache import FakeBinder, cache_from_fixture
+    from kbgpu.fixture import _OrderedCache, fixture_tiers
+    from kbgpu.framework import open_session
+    return open_session(_OrderedCache(cache_from_fixture(fx, FakeBinder()), fx), fixture_tiers(fx), opts or {})
+
+
+@pytest.mark.parametrize("seed", list(range(0, 60, 3)) + ["c1"])
+def test_select_replays_reference_node_loop(seed):
+    """kbg_select (the node loop of allocate.go:119-162) on the oracle's own
+    evaluation sequence, one task per call, reproduces every outcome."""
+    import ctypes
+    from kbgpu import _abi
+    fx = synth.config_fixture(1) if seed == "c1" else synth.random_fixture(seed)
+    ref = run_oracle(fx)
+    if ref["status"] != "ok":
+        pytest.skip(ref["status"])
+    ssn = _open(fx)
+    idx = {t.uid: i for i, t in enumerate(ssn.flat.task_objs)}
+    decided = {d["task"]: (d["node"], d["kind"]) for d in ref["decisions"]}
+    L = _abi.lib()
+    node, kind, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    for uid in ref["evaluated"]:
+        arr = (ctypes.c_int32 * 1)(idx[uid])
+        _abi.check(L.kbg_select(ssn.handle, arr, 1, 1, ctypes.byref(node), ctypes.byref(kind), ctypes.byref(n)))
+        assert n.value == 1
+        if uid in decided:
+            want_node, want_kind = decided[uid]
+            assert ssn.flat.node_names[node.value] == want_node, uid
+            assert ("allocate" if kind.value == _abi.KIND_ALLOCATE else "pipeline") == want_kind, uid
+        else:
+            assert node.value == -1, uid
+    for i, nref in enumerate(ref["nodes"]):
+        st = ssn.node_state(i)
+        assert [st.idle.milli_cpu, st.idle.memory, st.idle.milli_gpu] == nref["idle"]
+        assert st.num_tasks == nref["ntasks"]
+    ssn.close()
+
+
+def test_select_batch_stops_at_first_success():
+    """One job pop: tasks tried in order until one is placed (allocate.go:105-171)."""
+    import ctypes
+    from kbgpu import _abi
+    fx = load_golden("kat_tolerance_edge.json")  # a -> n1 (tolerance), b -> n2, c fits nowhere
+    ssn = _open(fx)
+    idx = {t.uid: i for i, t in enumerate(ssn.flat.task_objs)}
+    L = _abi.lib()
+    order = [idx["c"], idx["a"], idx["b"]]
+    arr = (ctypes.c_int32 * 3)(*order)
+    nodes, kinds, n = (ctypes.c_int32 * 3)(), (ctypes.c_int32 * 3)(), ctypes.c_int32()
+    _abi.check(L.kbg_select(ssn.handle, arr, 3, 1, nodes, kinds, ctypes.byref(n)))
+    assert n.value == 2  # c failed, a placed, b not evaluated
+    assert nodes[0] == -1 and ssn.flat.node_names[nodes[1]] == "n1"
+    ssn.close()
+
+
+def test_apply_matches_node_accounting():
+    """kbg_apply = NodeInfo.AddTask (node_info.go:101-129) on the device table."""
+    import ctypes
+    from kbgpu import _abi
+    fx = synth.config_fixture(1)
+    ref = run_oracle(fx)
+    ssn = _open(fx)
+    tasks = {t.uid: t for t in ssn.flat.task_objs}
+    names = {n: i for i, n in enumerate(ssn.flat.node_names)}
+    L = _abi.lib()
+    for d in ref["decisions"]:
+        r = tasks[d["task"]].resreq
+        res = _abi.kbg_resource(r.milli_cpu, r.memory, r.milli_gpu)
+        _abi.check(L.kbg_apply(ssn.handle, names[d["node"]], ctypes.byref(res),
+                               _abi.KIND_ALLOCATE if d["kind"] == "allocate" else _abi.KIND_PIPELINE))
+    for i, nref in enumerate(ref["nodes"]):
+        st = ssn.node_state(i)
+        assert [st.idle.milli_cpu, st.idle.memory, st.idle.milli_gpu] == nref["idle"]
+        assert st.num_tasks == nref["ntasks"]
+    # the device table must agree with the host mirror: every further task now fits nowhere it should not
+    ssn.close()
