@@ -201,6 +201,13 @@ typedef struct kbg_job_state {
                             reported whether or not the gang plugin is configured */
   double drf_share;      /* drf attr.share (drf.go:152-166); 0 if drf is off */
   kbg_resource drf_allocated;
+  /* JobInfo.NodesFitDelta of the job's last evaluated task (allocate.go:116-144),
+     summarised as JobInfo.FitError counts it (job_info.go:329-358); filled after
+     kbg_allocate for jobs that are not ready (what gang.go:169-190 reports). */
+  int32_t fit_valid;     /* 1 when the counts below were computed */
+  int32_t fit_nodes;     /* len(NodesFitDelta) */
+  int32_t fit_cpu, fit_memory, fit_gpu; /* entries with a negative cpu / memory / GPU delta */
+  int32_t reserved[3];
 } kbg_job_state;
 
 typedef struct kbg_queue_state {

@@ -980,6 +980,9 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     t.terms = tm;
     t.classes = cl;
     HIP_TRY(kbg::launch_build_class_mask(t, S.n_classes, S.W, S.d_class_mask, S.stream));
+    S.h_class_mask.resize((size_t)S.n_classes * S.W);
+    HIP_TRY(hipMemcpyAsync(S.h_class_mask.data(), S.d_class_mask, S.h_class_mask.size() * 8, hipMemcpyDeviceToHost,
+                           S.stream));
     HIP_TRY(hipStreamSynchronize(S.stream));  // sh's host vectors end with this scope
   }
   S.stats.n_classes = S.n_classes;
@@ -1018,6 +1021,72 @@ struct Pipe {
   static constexpr size_t kDepth = 3;
 };
 
+// Last node-loop run of a job: the task, how many decisions preceded it and
+// where it ended (node -1 = fitted nowhere).
+struct LastEval {
+  int32_t task = -1, before = 0, node = -1, kind = 0;
+};
+
+// JobInfo.NodesFitDelta of each not-ready job's last evaluated task
+// (allocate.go:116-144; reset per task, so only the last one survives), as
+// the counts JobInfo.FitError prints (job_info.go:329-358). The node states
+// at each job's evaluation point are rebuilt by undoing the decision log
+// backwards from the final mirror (exact: the pre-commit values are logged).
+void compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, const std::vector<Res>& dec_old,
+                        const std::vector<LastEval>& last) {
+  S.fit.assign(S.n_jobs, Session::FitCounts{});
+  std::vector<int32_t> jobs;
+  for (int32_t j = 0; j < S.n_jobs; ++j)
+    if (S.committed_ready[j] < S.jobs_in[j].min_available) jobs.push_back(j);
+  if (jobs.empty()) return;
+  std::sort(jobs.begin(), jobs.end(), [&](int32_t a, int32_t b) { return last[a].before > last[b].before; });
+  std::vector<Res> idle = S.idle, rel = S.rel;
+  std::vector<int32_t> ntasks = S.ntasks;
+  int32_t k = (int32_t)dec.size();
+  for (int32_t j : jobs) {
+    Session::FitCounts& fc = S.fit[j];
+    fc.valid = 1;
+    const LastEval& le = last[j];
+    if (le.task < 0) continue;  // never evaluated: empty map, "0 nodes are available"
+    while (k > le.before) {
+      --k;
+      const int32_t n = dec[k].node;
+      if (!S.nil_node[n]) (dec[k].kind == KBG_KIND_ALLOCATE ? idle[n] : rel[n]) = dec_old[k];
+      ntasks[n]--;
+    }
+    const int32_t t = le.task;
+    const Res& r = S.treq[t];
+    const uint64_t* cm = S.h_class_mask.data() + (size_t)S.task_class[t] * S.W;
+    const int32_t end = le.node < 0 ? S.n_nodes : le.node + (le.kind == KBG_KIND_PIPELINE ? 1 : 0);
+    bool nil_seen = false;
+    Res nil_delta{};
+    for (int32_t n = 0; n < end; ++n) {
+      if (!((cm[n >> 6] >> (n & 63)) & 1ull)) continue;                 // static predicate
+      if (S.pred_active && ntasks[n] >= S.maxtasks[n]) continue;       // pod cap
+      if (n != le.node && kbg::res_le(r, idle[n])) continue;           // would have been chosen
+      Res d = idle[n];                                                 // Resource.FitDelta
+      if (r.c > 0) d.c -= r.c + kbg::kMinMilliCPU;
+      if (r.m > 0) d.m -= r.m + kbg::kMinMemory;
+      if (r.g > 0) d.g -= r.g + kbg::kMinMilliGPU;
+      if (S.nil_node[n]) {  // every nil Node is named "": one map entry, the last one wins
+        nil_seen = true;
+        nil_delta = d;
+        continue;
+      }
+      fc.nodes++;
+      fc.cpu += d.c < 0;
+      fc.mem += d.m < 0;
+      fc.gpu += d.g < 0;
+    }
+    if (nil_seen) {
+      fc.nodes++;
+      fc.cpu += nil_delta.c < 0;
+      fc.mem += nil_delta.m < 0;
+      fc.gpu += nil_delta.g < 0;
+    }
+  }
+}
+
 kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
   if (S.allocated) return fail(KBG_E_INVALID, "kbg_allocate already ran on this session; call kbg_session_reset");
   using clk = std::chrono::steady_clock;
@@ -1030,7 +1099,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   S.stats.open_ms = open_ms;
 
   std::vector<kbg_decision> dec;
+  std::vector<Res> dec_old;  // the Idle (Allocate) or Releasing (Pipeline) row before each decision
   dec.reserve(S.pend.size());
+  dec_old.reserve(S.pend.size());
+  std::vector<LastEval> last(S.n_jobs);
   std::vector<std::vector<int32_t>> undispatched(S.n_jobs);
   S.committed_ready = S.job_ready0;
   // shapes known to fit nowhere (monotone): written by the committer, read by the predictor
@@ -1187,7 +1259,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       }
       const bool ok = node >= 0;
       bactual[i] = ok;
+      const int32_t j = S.tasks_in[t].job;
+      last[j] = LastEval{t, (int32_t)dec.size(), node, kind};
       if (ok) {
+        dec_old.push_back(kind == KBG_KIND_ALLOCATE ? S.idle[node] : S.rel[node]);
         mirror_add(S, t, node, kind);
         if (mark[node] != stamp) {
           mark[node] = stamp;
@@ -1195,7 +1270,6 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         }
         const int32_t di = (int32_t)dec.size();
         dec.push_back(kbg_decision{t, node, kind, -1});
-        const int32_t j = S.tasks_in[t].job;
         S.committed_ready[j]++;
         if (kind == KBG_KIND_ALLOCATE) {  // session.go:283-290
           undispatched[j].push_back(di);
@@ -1241,6 +1315,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   }
   finish();
   HIP_TRY(hipStreamSynchronize(S.stream));  // last delta write-back
+  compute_fit_deltas(S, dec, dec_old, last);
   S.fin = E;
   S.stats.engine_ms = engine_ms;
   S.stats.replayed = replayed;
@@ -1396,6 +1471,14 @@ kbg_status kbg_job_state_get(kbg_session* s, int32_t job, kbg_job_state* out) {
   out->ready = out->ready_num >= S.jobs_in[job].min_available ? 1 : 0;  // gang jobReady (gang.go:72-78)
   out->drf_share = S.has_drf ? E.jshare[job] : 0.0;
   out->drf_allocated = to_kres(E.jalloc[job]);
+  out->fit_valid = out->fit_nodes = out->fit_cpu = out->fit_memory = out->fit_gpu = 0;
+  if (S.allocated && (size_t)job < S.fit.size() && S.fit[job].valid) {
+    out->fit_valid = 1;
+    out->fit_nodes = S.fit[job].nodes;
+    out->fit_cpu = S.fit[job].cpu;
+    out->fit_memory = S.fit[job].mem;
+    out->fit_gpu = S.fit[job].gpu;
+  }
   return KBG_OK;
 }
 

@@ -141,6 +141,9 @@ struct Session {
   Engine fin;
   bool allocated = false;
   std::vector<int32_t> committed_ready;
+  struct FitCounts { int32_t valid = 0, nodes = 0, cpu = 0, mem = 0, gpu = 0; };
+  std::vector<FitCounts> fit;               // per job (A17)
+  std::vector<uint64_t> h_class_mask;       // host copy of the static predicate bits
 
   // ---- device
   int32_t device = 0;

@@ -124,7 +124,9 @@ class kbg_decision(ctypes.Structure):
 
 
 class kbg_job_state(ctypes.Structure):
-    _fields_ = [("ready_num", i32), ("ready", i32), ("drf_share", f64), ("drf_allocated", kbg_resource)]
+    _fields_ = [("ready_num", i32), ("ready", i32), ("drf_share", f64), ("drf_allocated", kbg_resource),
+                ("fit_valid", i32), ("fit_nodes", i32), ("fit_cpu", i32), ("fit_memory", i32), ("fit_gpu", i32),
+                ("reserved", i32 * 3)]
 
 
 class kbg_queue_state(ctypes.Structure):

@@ -45,6 +45,14 @@ class _OrderedCache:
         return s
 
 
+def fit_error(nodes, cpu, memory, gpu):
+    """JobInfo.FitError (job_info.go:329-358) from NodesFitDelta counts."""
+    if nodes == 0:
+        return "0 nodes are available"
+    reasons = [f"{v} insufficient {k}" for k, v in (("cpu", cpu), ("memory", memory), ("GPU", gpu)) if v > 0]
+    return f"0/{nodes} nodes are available, {', '.join(sorted(reasons))}."
+
+
 def run_fixture(fx, options=None):
     """Returns (result dict in the oracle's output schema, session)."""
     opts = dict(options or {})
@@ -78,6 +86,8 @@ def run_fixture(fx, options=None):
                "ready": bool(st.ready), "allocated": list(job.allocated.as_tuple())}
         if has_drf:
             row["drf_share"] = st.drf_share
+        if st.fit_valid:
+            row["fit_error"] = fit_error(st.fit_nodes, st.fit_cpu, st.fit_memory, st.fit_gpu)
         out["jobs"].append(row)
     for q, queue in enumerate(ssn.queues):
         st = ssn.queue_state(q)

@@ -150,9 +150,28 @@ def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8):
             r["nvidia.com/gpu"] = rng.choice(["1", "2"])
         return r
 
+    # remaining capacity per node, so that bound pods rarely overcommit a node
+    # (an overcommitted node makes the reference panic in AddPod; ~3% keep that path)
+    free = {n["name"]: [int(n["allocatable"]["cpu"]) * 1000, int(n["allocatable"]["memory"][:-2]) * 1024]
+            for n in nodes}
+
+    def fits(node_name, req):
+        cpu = req.get("cpu", "0")
+        mc = int(float(cpu[:-1])) if cpu.endswith("m") else int(float(cpu) * 1000)
+        mem = req.get("memory", "0")
+        mm = int(mem[:-2]) if mem.endswith("Mi") else (int(mem[:-2]) * 1024 if mem.endswith("Gi") else 0)
+        f = free[node_name]
+        if (f[0] >= mc and f[1] >= mm) or rng.random() < 0.03:
+            f[0] -= mc
+            f[1] -= mm
+            return True
+        return False
+
     # existing pods on nodes (Running / deleting -> Releasing)
     for i in range(rng.randint(0, nn)):
         node = rng.choice(nodes)
+        if not fits(node["name"], {"cpu": "500m", "memory": "512Mi"}):
+            continue
         p = mk_pod("default", f"run{i}", "Running", node["name"], {"cpu": "500m", "memory": "512Mi"},
                    group=None if rng.random() < 0.5 else "pg-run", controller="rc-1" if rng.random() < 0.5 else None)
         if rng.random() < 0.35:
@@ -205,7 +224,9 @@ def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8):
             req = job_req if rng.random() < 0.7 else rand_req()
             phase, node = "Pending", ""
             if rng.random() < 0.1:
-                phase, node = "Running", rng.choice(nodes)["name"]
+                cand = rng.choice(nodes)["name"]
+                if fits(cand, req):
+                    phase, node = "Running", cand
             p = mk_pod(ns, f"{pg}-t{t}", phase, node, req, group=pg)
             if rng.random() < 0.25:
                 p["priority"] = rng.choice([1, 5, 10])

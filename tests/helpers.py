@@ -54,6 +54,8 @@ def compare_outputs(ref, got):
            [(j["uid"], j["ready_num"], j["ready"]) for j in got["jobs"]]
     for a, b in zip(ref["jobs"], got["jobs"]):
         assert a["allocated"] == b["allocated"], (a, b)
+        if not a["ready"]:  # gang reports FitError for jobs that are not ready (gang.go:169-190)
+            assert b.get("fit_error") == a["fit_error"], (a, b)
         if "drf_share" in a:
             assert close(a["drf_share"], b["drf_share"]), (a, b)
     assert sorted(q["uid"] for q in ref["queues"]) == sorted(q["uid"] for q in got["queues"])
