@@ -191,7 +191,7 @@ def main():
         "config": {"workload": f"C{cid}: {n_nodes} nodes x {prod['pending']} pending tasks, "
                                f"{prod['jobs']} gang PodGroups, {prod['queues']} proportion queues, default tiers",
                    "parallelism": "replicas" if world > 1 else "single-gpu",
-                   "batch_tasks": base_opts.get("batch_tasks", 2048),
+                   "batch_tasks": base_opts.get("batch_tasks", 8192),
                    "candidates": base_opts.get("candidates", 32)},
         "roofline": roofline(full),
         "roofline_note": "scan kernel in full-scan mode (every task evaluation scans all N nodes, SURVEY 8d rule); "

@@ -36,6 +36,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -187,9 +188,17 @@ inline void rank_heap_down(int32_t* h, int n, const int32_t* rk, bool go111) {
   h[i] = x;
 }
 
+// Opt-in cycle counters of the ordering engine (KBG_PROFILE_ENGINE=1).
+struct EngineProfile {
+  bool on = false;
+  uint64_t qpop = 0, qpush = 0, jtop = 0, apply = 0, steps = 0;
+};
+inline uint64_t cycles() { return __builtin_readcyclecounter(); }
+
 struct Ops {
   const Session& S;
   Engine& E;
+  EngineProfile* prof = nullptr;
 
   bool job_ready(int32_t j) const { return E.jready[j] >= S.jobs_in[j].min_available; }
 
@@ -278,7 +287,9 @@ struct Ops {
         continue;
       }
       if (E.qheap.empty()) return -1;
+      uint64_t c0 = prof ? cycles() : 0;
       const int32_t q = qpop();
+      if (prof) prof->qpop += cycles() - c0;
       if (overused(q)) continue;     // :71-74
       if (E.jlen[q] == 0) continue;  // :78-81
       E.cur_j = E.jheap[S.joff[q]];  // :85 jobs.Pop()
@@ -291,6 +302,7 @@ struct Ops {
   // (drf.go:131-139, proportion.go:197-206), then jobs.Push / queues.Push.
   void apply(int32_t t, bool success) {
     if (!success) return;
+    uint64_t c0 = prof ? cycles() : 0;
     const int32_t j = E.cur_j, q = E.cur_q;
     const Res& r = S.treq[t];
     if (S.has_drf) {
@@ -305,9 +317,18 @@ struct Ops {
     }
     E.jready[j]++;
     refresh_key(j);
+    uint64_t c1 = prof ? cycles() : 0;
     jfix_top(q);  // :164-168 jobs.Push(job)
+    uint64_t c2 = prof ? cycles() : 0;
     qpush(q);     // :174
     E.in_job = false;
+    if (prof) {
+      const uint64_t c3 = cycles();
+      prof->apply += c1 - c0;
+      prof->jtop += c2 - c1;
+      prof->qpush += c3 - c2;
+      prof->steps++;
+    }
   }
 };
 
@@ -682,7 +703,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   if (st != KBG_OK) return st;
   if (o) S.opts = *o;
   S.heap_go111 = S.opts.heap_rule == 0;
-  S.K = S.opts.batch_tasks > 0 ? S.opts.batch_tasks : 2048;
+  S.K = S.opts.batch_tasks > 0 ? S.opts.batch_tasks : 8192;
   S.M = S.opts.candidates > 0 ? S.opts.candidates : 32;
   if (S.M > 4096) return fail(KBG_E_INVALID, "candidates > 4096");
   // full-scan: K rows x M slots; grouped: sum over shapes of min(n_s + slack, 4096)
@@ -1124,8 +1145,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   double engine_ms = 0;
   int64_t replayed = 0;
   std::string pred_error;
+  EngineProfile eprof;
+  eprof.on = getenv("KBG_PROFILE_ENGINE") != nullptr;
   std::thread predictor([&]() {
-    Ops ops{S, E};
+    Ops ops{S, E, eprof.on ? &eprof : nullptr};
     bool exhausted = false;
     for (;;) {
       Batch* b = nullptr;
@@ -1319,6 +1342,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   S.fin = E;
   S.stats.engine_ms = engine_ms;
   S.stats.replayed = replayed;
+  if (eprof.on && eprof.steps)
+    fprintf(stderr, "[kbg engine] steps %llu cycles/step: qpop %.1f apply %.1f jfix %.1f qpush %.1f (engine %.3f ms)\n",
+            (unsigned long long)eprof.steps, (double)eprof.qpop / eprof.steps, (double)eprof.apply / eprof.steps,
+            (double)eprof.jtop / eprof.steps, (double)eprof.qpush / eprof.steps, engine_ms);
   S.allocated = true;
   S.stats.allocate_ms = ms_since(t0);
   if (n_out) *n_out = (int32_t)dec.size();
