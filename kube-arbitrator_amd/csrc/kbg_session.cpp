@@ -143,8 +143,7 @@ void make_job_key(const Session& S, const Engine& E, int32_t j, kbg::JobKey* k) 
     k->c[n++] = zero ? 0.0 : v;
   }
   while (n < 3) k->c[n++] = 0.0;
-  k->creation = jb.creation_ns;
-  k->rank = S.job_rank[j];
+  k->frank = S.job_frank[j];
   k->pad = 0;
 }
 
@@ -316,9 +315,12 @@ struct Ops {
       if (S.queue_order_prop) reorder_queue(jq);
     }
     E.jready[j]++;
+    const kbg::JobKey before = E.jkey[j];
     refresh_key(j);
     uint64_t c1 = prof ? cycles() : 0;
-    jfix_top(q);  // :164-168 jobs.Push(job)
+    // :164-168 jobs.Push(job): an unchanged key (e.g. a gang job still short
+    // of MinAvailable) leaves the heap as it is
+    if (!kbg::job_key_same(before, E.jkey[j])) jfix_top(q);
     uint64_t c2 = prof ? cycles() : 0;
     qpush(q);     // :174
     E.in_job = false;
@@ -772,6 +774,16 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     ids.resize(S.n_tasks);
     for (int32_t t = 0; t < S.n_tasks; ++t) ids[t] = S.tasks_in[t].uid;
     S.task_rank = ranks_of(S, ids);
+  }
+  {
+    std::vector<int32_t> order(S.n_jobs);
+    std::iota(order.begin(), order.end(), 0);
+    std::sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+      if (S.jobs_in[a].creation_ns != S.jobs_in[b].creation_ns) return S.jobs_in[a].creation_ns < S.jobs_in[b].creation_ns;
+      return S.job_rank[a] < S.job_rank[b];
+    });
+    S.job_frank.assign(S.n_jobs, 0);
+    for (int32_t i = 0; i < S.n_jobs; ++i) S.job_frank[order[i]] = i;
   }
   S.treq.resize(S.n_tasks);
   S.pending_candidate.assign(S.n_tasks, 0);

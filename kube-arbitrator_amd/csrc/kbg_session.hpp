@@ -58,16 +58,17 @@ enum JobOrderPlugin : int32_t { JO_PRIORITY = 1, JO_GANG = 2, JO_DRF = 3 };
 // (CreationTimestamp, UID) of session_plugins.go:212-220.
 struct JobKey {
   double c[3];
-  int64_t creation;
-  int32_t rank;
+  int32_t frank;  // position of the job in (CreationTimestamp, UID) order
   int32_t pad;
 };
 inline bool job_key_less(const JobKey& a, const JobKey& b) {
   if (a.c[0] != b.c[0]) return a.c[0] < b.c[0];
   if (a.c[1] != b.c[1]) return a.c[1] < b.c[1];
   if (a.c[2] != b.c[2]) return a.c[2] < b.c[2];
-  if (a.creation != b.creation) return a.creation < b.creation;
-  return a.rank < b.rank;
+  return a.frank < b.frank;
+}
+inline bool job_key_same(const JobKey& a, const JobKey& b) {
+  return a.c[0] == b.c[0] && a.c[1] == b.c[1] && a.c[2] == b.c[2] && a.frank == b.frank;
 }
 
 // Mutable state of the ordering engine (queue/job/task priority queues and
@@ -117,6 +118,7 @@ struct Session {
 
   // ---- derived, immutable after open
   std::vector<int32_t> job_rank, queue_rank, task_rank;  // bytewise UID order
+  std::vector<int32_t> job_frank;                        // (CreationTimestamp, UID) order
   std::vector<int32_t> job_queue;                        // job -> queue index
   std::vector<int32_t> joff, jcap;                       // per-queue job-heap segment
   std::vector<int32_t> pend, pend_off, pend_len;         // per-job pending tasks in TaskOrderFn order
