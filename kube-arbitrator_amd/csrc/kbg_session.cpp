@@ -251,50 +251,26 @@ struct Ops {
     E.qheap.pop_back();
     return q;
   }
-  // Per-queue job priority queues. A job's key changes only while it is
-  // popped (drf and gang update the allocated job, drf.go:131-139,
-  // gang.go:44-55), so keys in a queue are static, the order is strict (UID
-  // tie-break) and the pop sequence does not depend on the container
-  // (SURVEY H2). Each queue's jobs are kept sorted in a circular buffer of
-  // capacity = its job count: jobs.Pop() reads the head; allocate.go's
-  // push-back of the popped job is a reinsertion by binary search that shifts
-  // the shorter side (O(1) when it becomes the largest, as in drf
-  // round-robin); a job whose tasks are exhausted is dropped from the head.
-  int32_t* jslot(int32_t q, int32_t i) {
-    const int32_t c = S.jcap[q];
-    int32_t k = E.jhead[q] + i;
-    if (k >= c) k -= c;
-    return &E.jheap[S.joff[q] + k];
+  // Per-queue job heaps. A job's key changes only while it is popped (drf and
+  // gang update the allocated job, drf.go:131-139, gang.go:44-55), so keys in
+  // a heap are static, the order is strict (UID tie-break) and the pop
+  // sequence does not depend on the heap layout. allocate.go pops
+  // the job, runs its tasks and pushes it back; here the job stays at the
+  // root meanwhile and is re-sifted (success) or removed (no task fitted).
+  void jpush(int32_t q, int32_t j) {
+    int32_t* h = E.jheap.data() + S.joff[q];
+    const int n = E.jlen[q]++;
+    h[n] = j;
+    go_up(h, n, [this](int32_t x, int32_t y) { return job_less(x, y); });
   }
-  int32_t jtop(int32_t q) { return *jslot(q, 0); }
+  void jfix_top(int32_t q) {
+    go_down(E.jheap.data() + S.joff[q], 0, E.jlen[q], [this](int32_t x, int32_t y) { return job_less(x, y); }, false);
+  }
   void jremove_top(int32_t q) {
-    if (++E.jhead[q] == S.jcap[q]) E.jhead[q] = 0;
-    --E.jlen[q];
-  }
-  void jfix_top(int32_t q) {  // the head's key grew: move it to its place
-    const int32_t n = E.jlen[q];
-    const int32_t x = jtop(q);
-    int32_t p;
-    if (n <= 1 || job_less(x, *jslot(q, 1))) return;  // still the smallest
-    if (job_less(*jslot(q, n - 1), x)) {
-      p = n;
-    } else {
-      int32_t lo = 1, hi = n - 1;  // first index in [1, n) whose job is greater than x
-      while (lo < hi) {
-        const int32_t mid = (lo + hi) >> 1;
-        if (job_less(*jslot(q, mid), x)) lo = mid + 1;
-        else hi = mid;
-      }
-      p = lo;
-    }
-    if (p - 1 <= n - p) {  // shift [1, p) one slot towards the head
-      for (int32_t i = 1; i < p; ++i) *jslot(q, i - 1) = *jslot(q, i);
-      *jslot(q, p - 1) = x;
-    } else {  // shift [p, n) one slot towards the tail (the freed head slot is the spare one)
-      for (int32_t i = n - 1; i >= p; --i) *jslot(q, i + 1) = *jslot(q, i);
-      *jslot(q, p) = x;
-      if (++E.jhead[q] == S.jcap[q]) E.jhead[q] = 0;
-    }
+    int32_t* h = E.jheap.data() + S.joff[q];
+    const int n = --E.jlen[q];
+    std::swap(h[0], h[n]);
+    go_down(h, 0, n, [this](int32_t x, int32_t y) { return job_less(x, y); }, false);
   }
 
   // allocate.go:65-112: advance the control flow to the next task whose node
@@ -315,7 +291,7 @@ struct Ops {
       if (prof) prof->qpop += cycles() - c0;
       if (overused(q)) continue;     // :71-74
       if (E.jlen[q] == 0) continue;  // :78-81
-      E.cur_j = jtop(q);             // :85 jobs.Pop()
+      E.cur_j = E.jheap[S.joff[q]];  // :85 jobs.Pop()
       E.cur_q = q;
       E.in_job = true;
     }
@@ -954,7 +930,6 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   for (int32_t q = 1; q < S.n_queues; ++q) S.joff[q] = S.joff[q - 1] + S.jcap[q - 1];
   E.jheap.assign(S.n_jobs, -1);
   E.jlen.assign(S.n_queues, 0);
-  E.jhead.assign(S.n_queues, 0);
   E.qheap.clear();
   E.qheap.reserve(S.n_jobs);
   E.jkey.assign(S.n_jobs, kbg::JobKey{});
@@ -967,13 +942,9 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     E.qrank.assign(S.n_queues, 0);
     for (int32_t i = 0; i < S.n_queues; ++i) E.qrank[E.qorder[i]] = i;
     for (int32_t j = 0; j < S.n_jobs; ++j) {
-      ops.qpush(S.job_queue[j]);  // allocate.go:48-59: one queue entry per job
-      const int32_t q = S.job_queue[j];
-      E.jheap[S.joff[q] + E.jlen[q]++] = j;
+      ops.qpush(S.job_queue[j]);
+      ops.jpush(S.job_queue[j], j);
     }
-    for (int32_t q = 0; q < S.n_queues; ++q)
-      std::sort(E.jheap.begin() + S.joff[q], E.jheap.begin() + S.joff[q] + E.jlen[q],
-                [&](int32_t a, int32_t b) { return ops.job_less(a, b); });
   }
 
   // ---- static predicates

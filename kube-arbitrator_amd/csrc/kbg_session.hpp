@@ -75,9 +75,8 @@ inline bool job_key_same(const JobKey& a, const JobKey& b) {
 // the plugin state they read). Flat arrays so a batch checkpoint is a copy.
 struct Engine {
   std::vector<int32_t> qheap;   // queue heap items (queue index), util.PriorityQueue
-  std::vector<int32_t> jheap;   // per-queue sorted circular job buffers, flat at joff[q]
-  std::vector<int32_t> jlen;    // live length of each per-queue buffer
-  std::vector<int32_t> jhead;   // head slot of each per-queue buffer
+  std::vector<int32_t> jheap;   // per-queue job heaps, flat at joff[q]
+  std::vector<int32_t> jlen;    // live length of each per-queue heap
   std::vector<int32_t> cursor;  // per job: next position in its sorted pending list
   int32_t cur_q = -1, cur_j = -1;
   bool in_job = false;
