@@ -124,8 +124,9 @@ inline void go_down(int32_t* h, int i0, int n, L less, bool go111) {
   }
 }
 
-void make_job_key(const Session& S, const Engine& E, int32_t j, kbg::JobKey* k) {
+kbg::JobEnt make_job_ent(const Session& S, const Engine& E, int32_t j) {
   const kbg_job& jb = S.jobs_in[j];
+  double c[3] = {0.0, 0.0, 0.0};
   int n = 0;
   bool zero = false;
   for (int32_t p : S.job_chain) {
@@ -134,17 +135,32 @@ void make_job_key(const Session& S, const Engine& E, int32_t j, kbg::JobKey* k) 
       v = -(double)jb.priority;
     } else if (p == kbg::JO_GANG) {  // gang.go:129-163 (non-ready first)
       const bool ready = E.jready[j] >= jb.min_available;
-      k->c[n++] = zero ? 0.0 : (ready ? 1.0 : 0.0);
+      c[n++] = zero ? 0.0 : (ready ? 1.0 : 0.0);
       if (!ready) zero = true;
       continue;
     } else {  // drf.go:109-125 (lower share first)
       v = E.jshare[j];
     }
-    k->c[n++] = zero ? 0.0 : v;
+    c[n++] = zero ? 0.0 : v;
   }
-  while (n < 3) k->c[n++] = 0.0;
-  k->frank = S.job_frank[j];
-  k->pad = 0;
+  kbg::JobEnt e;
+  e.a = ((unsigned __int128)kbg::ordered_bits(c[0]) << 64) | kbg::ordered_bits(c[1]);
+  e.b = ((unsigned __int128)kbg::ordered_bits(c[2]) << 64) | ((uint64_t)(uint32_t)S.job_frank[j] << 32) | (uint32_t)j;
+  return e;
+}
+
+// Min-heap sift of `x` from the root over h[0..n) (hole-based).
+inline void job_heap_down(kbg::JobEnt* h, int n, const kbg::JobEnt& x) {
+  int i = 0;
+  for (;;) {
+    int j = 2 * i + 1;
+    if (j >= n) break;
+    if (j + 1 < n && kbg::job_ent_less(h[j + 1], h[j])) ++j;
+    if (!kbg::job_ent_less(h[j], x)) break;
+    h[i] = h[j];
+    i = j;
+  }
+  h[i] = x;
 }
 
 // container/heap on queue ids compared through a rank table (rk[q] = position
@@ -201,10 +217,8 @@ struct Ops {
 
   bool job_ready(int32_t j) const { return E.jready[j] >= S.jobs_in[j].min_available; }
 
-  // Session.JobOrderFn (session_plugins.go:196-221) over the configured tiers,
-  // as a precomputed key (kbg_session.hpp JobKey).
-  bool job_less(int32_t a, int32_t b) const { return kbg::job_key_less(E.jkey[a], E.jkey[b]); }
-  void refresh_key(int32_t j) { make_job_key(S, E, j, &E.jkey[j]); }
+  // Session.JobOrderFn (session_plugins.go:196-221) over the configured tiers
+  // is the order of kbg_session.hpp JobEnt keys, built by make_job_ent.
   // Session.QueueOrderFn (session_plugins.go:223-245; proportion.go:146-159):
   // share, then UID. With proportion on, E.qrank holds every queue's position
   // in that order (maintained by reorder_queue), so a compare is two loads.
@@ -257,20 +271,13 @@ struct Ops {
   // sequence does not depend on the heap layout. allocate.go pops
   // the job, runs its tasks and pushes it back; here the job stays at the
   // root meanwhile and is re-sifted (success) or removed (no task fitted).
-  void jpush(int32_t q, int32_t j) {
-    int32_t* h = E.jheap.data() + S.joff[q];
-    const int n = E.jlen[q]++;
-    h[n] = j;
-    go_up(h, n, [this](int32_t x, int32_t y) { return job_less(x, y); });
-  }
-  void jfix_top(int32_t q) {
-    go_down(E.jheap.data() + S.joff[q], 0, E.jlen[q], [this](int32_t x, int32_t y) { return job_less(x, y); }, false);
+  void jfix_top(int32_t q, const kbg::JobEnt& x) {
+    job_heap_down(E.jheap.data() + S.joff[q], E.jlen[q], x);
   }
   void jremove_top(int32_t q) {
-    int32_t* h = E.jheap.data() + S.joff[q];
+    kbg::JobEnt* h = E.jheap.data() + S.joff[q];
     const int n = --E.jlen[q];
-    std::swap(h[0], h[n]);
-    go_down(h, 0, n, [this](int32_t x, int32_t y) { return job_less(x, y); }, false);
+    if (n > 0) job_heap_down(h, n, h[n]);
   }
 
   // allocate.go:65-112: advance the control flow to the next task whose node
@@ -291,7 +298,7 @@ struct Ops {
       if (prof) prof->qpop += cycles() - c0;
       if (overused(q)) continue;     // :71-74
       if (E.jlen[q] == 0) continue;  // :78-81
-      E.cur_j = E.jheap[S.joff[q]];  // :85 jobs.Pop()
+      E.cur_j = kbg::job_ent_job(E.jheap[S.joff[q]]);  // :85 jobs.Pop()
       E.cur_q = q;
       E.in_job = true;
     }
@@ -315,12 +322,11 @@ struct Ops {
       if (S.queue_order_prop) reorder_queue(jq);
     }
     E.jready[j]++;
-    const kbg::JobKey before = E.jkey[j];
-    refresh_key(j);
+    const kbg::JobEnt key = make_job_ent(S, E, j);
     uint64_t c1 = prof ? cycles() : 0;
-    // :164-168 jobs.Push(job): an unchanged key (e.g. a gang job still short
-    // of MinAvailable) leaves the heap as it is
-    if (!kbg::job_key_same(before, E.jkey[j])) jfix_top(q);
+    // :164-168 jobs.Push(job): the popped job is still the root here; an
+    // unchanged key (e.g. a gang job short of MinAvailable) leaves the heap as is
+    if (!kbg::job_ent_same(key, E.jheap[S.joff[q]])) jfix_top(q, key);
     uint64_t c2 = prof ? cycles() : 0;
     qpush(q);     // :174
     E.in_job = false;
@@ -928,12 +934,10 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.jcap.assign(S.n_queues, 0);
   for (int32_t j = 0; j < S.n_jobs; ++j) S.jcap[S.job_queue[j]]++;
   for (int32_t q = 1; q < S.n_queues; ++q) S.joff[q] = S.joff[q - 1] + S.jcap[q - 1];
-  E.jheap.assign(S.n_jobs, -1);
+  E.jheap.assign(S.n_jobs, kbg::JobEnt{});
   E.jlen.assign(S.n_queues, 0);
   E.qheap.clear();
   E.qheap.reserve(S.n_jobs);
-  E.jkey.assign(S.n_jobs, kbg::JobKey{});
-  for (int32_t j = 0; j < S.n_jobs; ++j) make_job_key(S, E, j, &E.jkey[j]);
   {
     Ops ops{S, E};
     E.qorder.resize(S.n_queues);
@@ -942,9 +946,12 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     E.qrank.assign(S.n_queues, 0);
     for (int32_t i = 0; i < S.n_queues; ++i) E.qrank[E.qorder[i]] = i;
     for (int32_t j = 0; j < S.n_jobs; ++j) {
-      ops.qpush(S.job_queue[j]);
-      ops.jpush(S.job_queue[j], j);
+      ops.qpush(S.job_queue[j]);  // allocate.go:48-59: one queue entry per job
+      const int32_t q = S.job_queue[j];
+      E.jheap[S.joff[q] + E.jlen[q]++] = make_job_ent(S, E, j);
     }
+    for (int32_t q = 0; q < S.n_queues; ++q)  // a sorted array is a valid min-heap
+      std::sort(E.jheap.begin() + S.joff[q], E.jheap.begin() + S.joff[q] + E.jlen[q], kbg::job_ent_less);
   }
 
   // ---- static predicates

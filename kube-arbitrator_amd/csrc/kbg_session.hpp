@@ -55,27 +55,28 @@ enum JobOrderPlugin : int32_t { JO_PRIORITY = 1, JO_GANG = 2, JO_DRF = 3 };
 // (priority: -Priority, gang: ready ? 1 : 0, drf: share), components after
 // gang zeroed for a non-ready job (gang.go:148-160 decides non-ready pairs by
 // creation/UID without consulting later plugins), then the fallback
-// (CreationTimestamp, UID) of session_plugins.go:212-220.
-struct JobKey {
-  double c[3];
-  int32_t frank;  // position of the job in (CreationTimestamp, UID) order
-  int32_t pad;
+// (CreationTimestamp, UID) of session_plugins.go:212-220 as one dense rank.
+// Stored inline in the job heaps as two 128-bit words of order-preserving
+// integers: a = (c0, c1), b = (c2, frank, job).
+struct JobEnt {
+  unsigned __int128 a, b;
 };
-inline bool job_key_less(const JobKey& a, const JobKey& b) {
-  if (a.c[0] != b.c[0]) return a.c[0] < b.c[0];
-  if (a.c[1] != b.c[1]) return a.c[1] < b.c[1];
-  if (a.c[2] != b.c[2]) return a.c[2] < b.c[2];
-  return a.frank < b.frank;
-}
-inline bool job_key_same(const JobKey& a, const JobKey& b) {
-  return a.c[0] == b.c[0] && a.c[1] == b.c[1] && a.c[2] == b.c[2] && a.frank == b.frank;
+inline bool job_ent_less(const JobEnt& x, const JobEnt& y) { return x.a < y.a || (x.a == y.a && x.b < y.b); }
+inline bool job_ent_same(const JobEnt& x, const JobEnt& y) { return x.a == y.a && x.b == y.b; }
+inline int32_t job_ent_job(const JobEnt& x) { return (int32_t)(uint32_t)(uint64_t)x.b; }
+// double -> uint64 with the same order (-0.0 folded onto +0.0: they compare equal)
+inline uint64_t ordered_bits(double v) {
+  if (v == 0.0) v = 0.0;
+  uint64_t u;
+  __builtin_memcpy(&u, &v, 8);
+  return (u >> 63) ? ~u : (u | (1ull << 63));
 }
 
 // Mutable state of the ordering engine (queue/job/task priority queues and
 // the plugin state they read). Flat arrays so a batch checkpoint is a copy.
 struct Engine {
   std::vector<int32_t> qheap;   // queue heap items (queue index), util.PriorityQueue
-  std::vector<int32_t> jheap;   // per-queue job heaps, flat at joff[q]
+  std::vector<JobEnt> jheap;    // per-queue job heaps (binary, inline keys), flat at joff[q]
   std::vector<int32_t> jlen;    // live length of each per-queue heap
   std::vector<int32_t> cursor;  // per job: next position in its sorted pending list
   int32_t cur_q = -1, cur_j = -1;
@@ -85,7 +86,6 @@ struct Engine {
   std::vector<int32_t> jready;  // gang readyTaskNum
   std::vector<Res> qalloc;      // proportion attr.allocated
   std::vector<double> qshare;   // proportion attr.share
-  std::vector<JobKey> jkey;     // job order key (derived from the fields above)
   std::vector<int32_t> qorder;  // queues sorted by QueueOrderFn
   std::vector<int32_t> qrank;   // position of each queue in qorder
 };
