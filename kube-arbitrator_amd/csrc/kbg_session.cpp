@@ -124,39 +124,34 @@ inline void go_down(int32_t* h, int i0, int n, L less, bool go111) {
   }
 }
 
-kbg::JobEnt make_job_ent(const Session& S, const Engine& E, int32_t j) {
-  const kbg_job& jb = S.jobs_in[j];
-  double c[3] = {0.0, 0.0, 0.0};
-  int n = 0;
+kbg::JobKey make_job_key(const Session& S, const Engine& E, int32_t j) {
+  kbg::JobKey k = 0;
   bool zero = false;
   for (int32_t p : S.job_chain) {
-    double v;
     if (p == kbg::JO_PRIORITY) {  // priority.go:58-74 (higher first)
-      v = -(double)jb.priority;
+      k = (k << 32) | (zero ? 0u : S.job_prank[j]);
     } else if (p == kbg::JO_GANG) {  // gang.go:129-163 (non-ready first)
-      const bool ready = E.jready[j] >= jb.min_available;
-      c[n++] = zero ? 0.0 : (ready ? 1.0 : 0.0);
+      const bool ready = E.jready[j] >= S.jobs_in[j].min_available;
+      k = (k << 1) | (zero ? 0u : (ready ? 1u : 0u));
       if (!ready) zero = true;
-      continue;
     } else {  // drf.go:109-125 (lower share first)
-      v = E.jshare[j];
+      uint64_t u;
+      __builtin_memcpy(&u, &E.jshare[j], 8);
+      k = (k << 63) | (zero ? 0 : (u & ~(1ull << 63)));
     }
-    c[n++] = zero ? 0.0 : v;
   }
-  kbg::JobEnt e;
-  e.a = ((unsigned __int128)kbg::ordered_bits(c[0]) << 64) | kbg::ordered_bits(c[1]);
-  e.b = ((unsigned __int128)kbg::ordered_bits(c[2]) << 64) | ((uint64_t)(uint32_t)S.job_frank[j] << 32) | (uint32_t)j;
-  return e;
+  return (k << 32) | (uint32_t)S.job_frank[j];
 }
 
-// Min-heap sift of `x` from the root over h[0..n) (hole-based).
-inline void job_heap_down(kbg::JobEnt* h, int n, const kbg::JobEnt& x) {
+// Min-heap sift of `x` from the root over h[0..n); h[n] holds the sentinel,
+// so the right-child probe needs no bounds test (hole-based).
+inline void job_heap_down(kbg::JobKey* h, int n, kbg::JobKey x) {
   int i = 0;
   for (;;) {
     int j = 2 * i + 1;
     if (j >= n) break;
-    if (j + 1 < n && kbg::job_ent_less(h[j + 1], h[j])) ++j;
-    if (!kbg::job_ent_less(h[j], x)) break;
+    j += h[j + 1] < h[j] ? 1 : 0;
+    if (!(h[j] < x)) break;
     h[i] = h[j];
     i = j;
   }
@@ -179,6 +174,7 @@ inline void rank_heap_up(int32_t* h, int j, const int32_t* rk) {
   }
   h[j] = x;
 }
+// h[n] holds the sentinel queue id (rank INT32_MAX): never chosen as a child.
 inline void rank_heap_down(int32_t* h, int n, const int32_t* rk, bool go111) {
   if (n <= 1) return;
   const int32_t x = h[0];
@@ -187,15 +183,11 @@ inline void rank_heap_down(int32_t* h, int n, const int32_t* rk, bool go111) {
   for (;;) {
     const int j1 = 2 * i + 1;
     if (j1 >= n) break;
-    int j = j1;
-    int32_t rj = rk[h[j1]];
-    if (j1 + 1 < n) {
-      const int32_t r2 = rk[h[j1 + 1]];
-      // go1.11: right child when !Less(j1, j2) (r2 <= r1); later: when Less(j2, j1)
-      const bool right = go111 ? (r2 <= rj) : (r2 < rj);
-      j += right ? 1 : 0;
-      rj = right ? r2 : rj;
-    }
+    const int32_t r1 = rk[h[j1]], r2 = rk[h[j1 + 1]];
+    // go1.11: right child when !Less(j1, j2) (r2 <= r1); later: when Less(j2, j1)
+    const bool right = go111 ? (r2 <= r1) : (r2 < r1);
+    const int j = j1 + (right ? 1 : 0);
+    const int32_t rj = right ? r2 : r1;
     if (!(rj < rx)) break;
     h[i] = h[j];
     i = j;
@@ -218,7 +210,7 @@ struct Ops {
   bool job_ready(int32_t j) const { return E.jready[j] >= S.jobs_in[j].min_available; }
 
   // Session.JobOrderFn (session_plugins.go:196-221) over the configured tiers
-  // is the order of kbg_session.hpp JobEnt keys, built by make_job_ent.
+  // is the order of kbg_session.hpp JobKey keys, built by make_job_key.
   // Session.QueueOrderFn (session_plugins.go:223-245; proportion.go:146-159):
   // share, then UID. With proportion on, E.qrank holds every queue's position
   // in that order (maintained by reorder_queue), so a compare is two loads.
@@ -253,16 +245,23 @@ struct Ops {
   }
   // The queue heap is a literal container/heap: it holds one entry per job
   // and entries keep stale keys, so its layout decides the order.
+  // Fixed capacity (one entry per job at most, allocate.go:48-59 pushes one
+  // per job and every pop is followed by at most one push); qheap[qlen] is the
+  // sentinel id n_queues.
   void qpush(int32_t q) {
-    E.qheap.push_back(q);
-    rank_heap_up(E.qheap.data(), (int)E.qheap.size() - 1, E.qrank.data());
+    int32_t* h = E.qheap.data();
+    const int n = E.qlen++;
+    h[n] = q;
+    h[n + 1] = S.n_queues;
+    rank_heap_up(h, n, E.qrank.data());
   }
-  int32_t qpop() {
-    const int n = (int)E.qheap.size() - 1;
-    std::swap(E.qheap[0], E.qheap[n]);
-    rank_heap_down(E.qheap.data(), n, E.qrank.data(), S.heap_go111);
-    const int32_t q = E.qheap.back();
-    E.qheap.pop_back();
+  int32_t qpop() {  // Pop: swap(0, n-1), down(0, n-1), take h[n-1]
+    int32_t* h = E.qheap.data();
+    const int n = --E.qlen;
+    const int32_t q = h[0];
+    h[0] = h[n];
+    h[n] = S.n_queues;
+    rank_heap_down(h, n, E.qrank.data(), S.heap_go111);
     return q;
   }
   // Per-queue job heaps. A job's key changes only while it is popped (drf and
@@ -271,13 +270,13 @@ struct Ops {
   // sequence does not depend on the heap layout. allocate.go pops
   // the job, runs its tasks and pushes it back; here the job stays at the
   // root meanwhile and is re-sifted (success) or removed (no task fitted).
-  void jfix_top(int32_t q, const kbg::JobEnt& x) {
-    job_heap_down(E.jheap.data() + S.joff[q], E.jlen[q], x);
-  }
+  void jfix_top(int32_t q, kbg::JobKey x) { job_heap_down(E.jheap.data() + S.joff[q], E.jlen[q], x); }
   void jremove_top(int32_t q) {
-    kbg::JobEnt* h = E.jheap.data() + S.joff[q];
+    kbg::JobKey* h = E.jheap.data() + S.joff[q];
     const int n = --E.jlen[q];
-    if (n > 0) job_heap_down(h, n, h[n]);
+    const kbg::JobKey x = h[n];
+    h[n] = kbg::kJobKeySentinel;
+    if (n > 0) job_heap_down(h, n, x);
   }
 
   // allocate.go:65-112: advance the control flow to the next task whose node
@@ -292,13 +291,13 @@ struct Ops {
         E.in_job = false;
         continue;
       }
-      if (E.qheap.empty()) return -1;
+      if (E.qlen == 0) return -1;
       uint64_t c0 = prof ? cycles() : 0;
       const int32_t q = qpop();
       if (prof) prof->qpop += cycles() - c0;
       if (overused(q)) continue;     // :71-74
       if (E.jlen[q] == 0) continue;  // :78-81
-      E.cur_j = kbg::job_ent_job(E.jheap[S.joff[q]]);  // :85 jobs.Pop()
+      E.cur_j = S.job_by_frank[kbg::job_key_frank(E.jheap[S.joff[q]])];  // :85 jobs.Pop()
       E.cur_q = q;
       E.in_job = true;
     }
@@ -322,11 +321,11 @@ struct Ops {
       if (S.queue_order_prop) reorder_queue(jq);
     }
     E.jready[j]++;
-    const kbg::JobEnt key = make_job_ent(S, E, j);
+    const kbg::JobKey key = make_job_key(S, E, j);
     uint64_t c1 = prof ? cycles() : 0;
     // :164-168 jobs.Push(job): the popped job is still the root here; an
     // unchanged key (e.g. a gang job short of MinAvailable) leaves the heap as is
-    if (!kbg::job_ent_same(key, E.jheap[S.joff[q]])) jfix_top(q, key);
+    if (key != E.jheap[S.joff[q]]) jfix_top(q, key);
     uint64_t c2 = prof ? cycles() : 0;
     qpush(q);     // :174
     E.in_job = false;
@@ -590,7 +589,7 @@ struct Resolver {
     const Res& r = S.treq[t];
     for (int32_t& k = cursor[g]; k < n; ++k) {
       const int32_t nd = (int32_t)(c[k] & ~kbg::kCandPipelineBit);
-      if (S.nil_node[nd] && S.pred_active) return RES_PANIC;
+      if (S.panic_node[nd]) return RES_PANIC;
       if (mark[nd] != stamp) {
         *node = nd;
         *kind = (c[k] & kbg::kCandPipelineBit) ? KBG_KIND_PIPELINE : KBG_KIND_ALLOCATE;
@@ -790,6 +789,15 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     });
     S.job_frank.assign(S.n_jobs, 0);
     for (int32_t i = 0; i < S.n_jobs; ++i) S.job_frank[order[i]] = i;
+    S.job_by_frank = order;
+    std::vector<int32_t> prios(S.n_jobs);
+    for (int32_t j = 0; j < S.n_jobs; ++j) prios[j] = S.jobs_in[j].priority;
+    std::sort(prios.begin(), prios.end(), std::greater<int32_t>());
+    prios.erase(std::unique(prios.begin(), prios.end()), prios.end());
+    S.job_prank.resize(S.n_jobs);
+    for (int32_t j = 0; j < S.n_jobs; ++j)
+      S.job_prank[j] = (uint32_t)(std::lower_bound(prios.begin(), prios.end(), S.jobs_in[j].priority,
+                                                   std::greater<int32_t>()) - prios.begin());
   }
   S.treq.resize(S.n_tasks);
   S.pending_candidate.assign(S.n_tasks, 0);
@@ -798,6 +806,8 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     // allocate.go:88-96: only Pending, non-BestEffort tasks enter the node loop
     S.pending_candidate[t] = S.tasks_in[t].status == KBG_PENDING && !kbg::res_empty(S.treq[t]);
   }
+  S.task_job.resize(S.n_tasks);
+  for (int32_t t = 0; t < S.n_tasks; ++t) S.task_job[t] = S.tasks_in[t].job;
   S.job_queue.resize(S.n_jobs);
   for (int32_t j = 0; j < S.n_jobs; ++j) S.job_queue[j] = S.jobs_in[j].queue;
 
@@ -815,6 +825,9 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     S.maxtasks[n] = S.nodes_in[n].max_task_num;
     S.nil_node[n] = S.nodes_in[n].has_node ? 0 : 1;
   }
+  S.panic_node.assign(N, 0);
+  if (S.pred_active)
+    for (int32_t n = 0; n < N; ++n) S.panic_node[n] = S.nil_node[n];
   S.idle0 = S.idle;
   S.rel0 = S.rel;
   S.ntasks0 = S.ntasks;
@@ -933,25 +946,25 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.joff.assign(S.n_queues, 0);
   S.jcap.assign(S.n_queues, 0);
   for (int32_t j = 0; j < S.n_jobs; ++j) S.jcap[S.job_queue[j]]++;
-  for (int32_t q = 1; q < S.n_queues; ++q) S.joff[q] = S.joff[q - 1] + S.jcap[q - 1];
-  E.jheap.assign(S.n_jobs, kbg::JobEnt{});
+  for (int32_t q = 1; q < S.n_queues; ++q) S.joff[q] = S.joff[q - 1] + S.jcap[q - 1] + 1;
+  E.jheap.assign((size_t)S.n_jobs + S.n_queues, kbg::kJobKeySentinel);
   E.jlen.assign(S.n_queues, 0);
-  E.qheap.clear();
-  E.qheap.reserve(S.n_jobs);
+  E.qheap.assign((size_t)S.n_jobs + 1, S.n_queues);
+  E.qlen = 0;
   {
     Ops ops{S, E};
     E.qorder.resize(S.n_queues);
     std::iota(E.qorder.begin(), E.qorder.end(), 0);
     std::sort(E.qorder.begin(), E.qorder.end(), [&](int32_t a, int32_t b) { return ops.queue_less_slow(a, b); });
-    E.qrank.assign(S.n_queues, 0);
+    E.qrank.assign(S.n_queues + 1, INT32_MAX);  // [n_queues]: the heap sentinel
     for (int32_t i = 0; i < S.n_queues; ++i) E.qrank[E.qorder[i]] = i;
     for (int32_t j = 0; j < S.n_jobs; ++j) {
       ops.qpush(S.job_queue[j]);  // allocate.go:48-59: one queue entry per job
       const int32_t q = S.job_queue[j];
-      E.jheap[S.joff[q] + E.jlen[q]++] = make_job_ent(S, E, j);
+      E.jheap[S.joff[q] + E.jlen[q]++] = make_job_key(S, E, j);
     }
     for (int32_t q = 0; q < S.n_queues; ++q)  // a sorted array is a valid min-heap
-      std::sort(E.jheap.begin() + S.joff[q], E.jheap.begin() + S.joff[q] + E.jlen[q], kbg::job_ent_less);
+      std::sort(E.jheap.begin() + S.joff[q], E.jheap.begin() + S.joff[q] + E.jlen[q]);
   }
 
   // ---- static predicates
@@ -1143,7 +1156,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   dec.reserve(S.pend.size());
   dec_old.reserve(S.pend.size());
   std::vector<LastEval> last(S.n_jobs);
-  std::vector<std::vector<int32_t>> undispatched(S.n_jobs);
+  // Allocate decisions of a job not yet dispatched (gang short of MinAvailable):
+  // a per-job list threaded through decision indices
+  std::vector<int32_t> undisp_head(S.n_jobs, -1), undisp_next;
+  undisp_next.reserve(S.pend.size());
   S.committed_ready = S.job_ready0;
   // shapes known to fit nowhere (monotone): written by the committer, read by the predictor
   std::unique_ptr<std::atomic<uint8_t>[]> failed(new std::atomic<uint8_t>[std::max(1, S.n_shapes)]);
@@ -1301,7 +1317,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       }
       const bool ok = node >= 0;
       bactual[i] = ok;
-      const int32_t j = S.tasks_in[t].job;
+      const int32_t j = S.task_job[t];
       last[j] = LastEval{t, (int32_t)dec.size(), node, kind};
       if (ok) {
         dec_old.push_back(kind == KBG_KIND_ALLOCATE ? S.idle[node] : S.rel[node]);
@@ -1312,12 +1328,14 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         }
         const int32_t di = (int32_t)dec.size();
         dec.push_back(kbg_decision{t, node, kind, -1});
+        undisp_next.push_back(-1);
         S.committed_ready[j]++;
         if (kind == KBG_KIND_ALLOCATE) {  // session.go:283-290
-          undispatched[j].push_back(di);
+          undisp_next[di] = undisp_head[j];
+          undisp_head[j] = di;
           if (job_ready_committed(j)) {
-            for (int32_t d : undispatched[j]) dec[d].dispatched_at = di;
-            undispatched[j].clear();
+            for (int32_t d = undisp_head[j]; d >= 0; d = undisp_next[d]) dec[d].dispatched_at = di;
+            undisp_head[j] = -1;
           }
         }
       } else {

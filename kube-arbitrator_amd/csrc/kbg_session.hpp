@@ -50,33 +50,25 @@ struct StaticHost {
 
 enum JobOrderPlugin : int32_t { JO_PRIORITY = 1, JO_GANG = 2, JO_DRF = 3 };
 
-// Session.JobOrderFn flattened into a lexicographic key (exactly equivalent
-// for the configured tier order): one component per job-order plugin
-// (priority: -Priority, gang: ready ? 1 : 0, drf: share), components after
-// gang zeroed for a non-ready job (gang.go:148-160 decides non-ready pairs by
-// creation/UID without consulting later plugins), then the fallback
-// (CreationTimestamp, UID) of session_plugins.go:212-220 as one dense rank.
-// Stored inline in the job heaps as two 128-bit words of order-preserving
-// integers: a = (c0, c1), b = (c2, frank, job).
-struct JobEnt {
-  unsigned __int128 a, b;
-};
-inline bool job_ent_less(const JobEnt& x, const JobEnt& y) { return x.a < y.a || (x.a == y.a && x.b < y.b); }
-inline bool job_ent_same(const JobEnt& x, const JobEnt& y) { return x.a == y.a && x.b == y.b; }
-inline int32_t job_ent_job(const JobEnt& x) { return (int32_t)(uint32_t)(uint64_t)x.b; }
-// double -> uint64 with the same order (-0.0 folded onto +0.0: they compare equal)
-inline uint64_t ordered_bits(double v) {
-  if (v == 0.0) v = 0.0;
-  uint64_t u;
-  __builtin_memcpy(&u, &v, 8);
-  return (u >> 63) ? ~u : (u | (1ull << 63));
-}
+// Session.JobOrderFn flattened into one 128-bit order-preserving integer
+// (exactly equivalent for the configured tier order). One field per
+// job-order plugin in tier order — priority: dense rank of -Priority (32
+// bits); gang: ready ? 1 : 0 (1 bit); drf: the share's IEEE bits (63 bits,
+// shares are >= +0 so the sign bit is always clear and the bits order like
+// the values) — fields after gang zeroed for a non-ready job (gang.go:148-160
+// decides non-ready pairs by creation/UID without consulting later plugins),
+// then the fallback (CreationTimestamp, UID) of session_plugins.go:212-220 as
+// one dense rank in the low 32 bits. 32 + 1 + 63 + 32 = 128: every chain fits.
+typedef unsigned __int128 JobKey;
+constexpr JobKey kJobKeySentinel = ~(JobKey)0;  // above every real key (frank < 2^32 - 1)
+inline uint32_t job_key_frank(JobKey k) { return (uint32_t)(uint64_t)k; }
 
 // Mutable state of the ordering engine (queue/job/task priority queues and
 // the plugin state they read). Flat arrays so a batch checkpoint is a copy.
 struct Engine {
-  std::vector<int32_t> qheap;   // queue heap items (queue index), util.PriorityQueue
-  std::vector<JobEnt> jheap;    // per-queue job heaps (binary, inline keys), flat at joff[q]
+  std::vector<int32_t> qheap;   // queue heap items (queue index), util.PriorityQueue; qheap[qlen] = sentinel
+  int32_t qlen = 0;
+  std::vector<JobKey> jheap;    // per-queue job heaps (binary, inline keys), flat at joff[q]; [jlen] = sentinel
   std::vector<int32_t> jlen;    // live length of each per-queue heap
   std::vector<int32_t> cursor;  // per job: next position in its sorted pending list
   int32_t cur_q = -1, cur_j = -1;
@@ -87,7 +79,7 @@ struct Engine {
   std::vector<Res> qalloc;      // proportion attr.allocated
   std::vector<double> qshare;   // proportion attr.share
   std::vector<int32_t> qorder;  // queues sorted by QueueOrderFn
-  std::vector<int32_t> qrank;   // position of each queue in qorder
+  std::vector<int32_t> qrank;   // position of each queue in qorder; qrank[n_queues] = INT32_MAX (sentinel id)
 };
 
 struct Session {
@@ -119,8 +111,11 @@ struct Session {
   // ---- derived, immutable after open
   std::vector<int32_t> job_rank, queue_rank, task_rank;  // bytewise UID order
   std::vector<int32_t> job_frank;                        // (CreationTimestamp, UID) order
+  std::vector<int32_t> job_by_frank;                     // inverse of job_frank
+  std::vector<uint32_t> job_prank;                       // dense rank of -Priority
   std::vector<int32_t> job_queue;                        // job -> queue index
-  std::vector<int32_t> joff, jcap;                       // per-queue job-heap segment
+  std::vector<int32_t> task_job;                         // task -> job index
+  std::vector<int32_t> joff, jcap;                       // per-queue job-heap segment (jcap + 1 slots)
   std::vector<int32_t> pend, pend_off, pend_len;         // per-job pending tasks in TaskOrderFn order
   std::vector<char> pending_candidate;                   // task is Pending and not BestEffort
   std::vector<int32_t> task_class;
@@ -138,6 +133,7 @@ struct Session {
   std::vector<Res> idle0, rel0, idle, rel;
   std::vector<int32_t> ntasks0, ntasks, maxtasks;
   std::vector<char> nil_node;
+  std::vector<char> panic_node;  // nil Node under an active predicates plugin (predicates.go:122-123)
 
   // ---- results of the last allocate
   Engine fin;

@@ -1,0 +1,40 @@
+// Developer tool (not part of libkbgpu.so): times the host ordering engine of
+// the allocate path alone, on a CPU-only machine. It includes the session
+// source to reach the engine, runs open_session (which builds all host state
+// and then stops at the missing device) and drives the predictor with every
+// outcome = placed, i.e. the engine work of a cycle where everything fits.
+#include "../csrc/kbg_session.cpp"
+
+extern "C" double kbg_tool_engine_ns_per_step(const kbg_snapshot* snap, const kbg_options* o, int32_t reps,
+                                              int64_t* steps_out, double* checksum, int32_t profile) {
+  kbg::Session S;
+  open_session(S, snap, o);  // returns KBG_E_HIP on a machine without a device; host state is complete
+  if (S.init.qlen == 0) return -1.0;
+  double best = 1e30;
+  int64_t steps = 0;
+  uint64_t sum = 0;
+  EngineProfile prof;
+  for (int32_t r = 0; r < reps; ++r) {
+    Engine E = S.init;
+    prof = EngineProfile{};
+    Ops ops{S, E, profile ? &prof : nullptr};
+    steps = 0;
+    sum = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const int32_t t = ops.next_task();
+      if (t < 0) break;
+      ops.apply(t, true);
+      sum = (sum * 1000003u) ^ (uint64_t)t;  // order-sensitive
+      ++steps;
+    }
+    const double ns = std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0).count();
+    best = std::min(best, ns / std::max<int64_t>(1, steps));
+  }
+  if (steps_out) *steps_out = steps;
+  if (checksum) *checksum = (double)(sum >> 11);
+  if (profile && prof.steps)
+    fprintf(stderr, "cycles/step: qpop %.1f apply %.1f jfix %.1f qpush %.1f\n", (double)prof.qpop / prof.steps,
+            (double)prof.apply / prof.steps, (double)prof.jtop / prof.steps, (double)prof.qpush / prof.steps);
+  return best;
+}

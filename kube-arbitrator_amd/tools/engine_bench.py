@@ -1,0 +1,33 @@
+"""Times the host ordering engine alone (CPU): python kube-arbitrator_amd/tools/engine_bench.py [config]"""
+import ctypes
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+sys.path.insert(0, PKG)
+
+
+def main():
+    cid = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    lib = os.path.join(HERE, "libkbg_tools.so")
+    subprocess.run(["make", "-s", "-C", PKG, "tools"], check=True)
+    from kbgpu import _abi, synth
+    from kbgpu.cache import cache_from_fixture
+    from kbgpu.fixture import fixture_tiers
+    from kbgpu.snapshot import FlatSnapshot
+    fx = synth.config_fixture(cid)
+    s = cache_from_fixture(fx).snapshot()
+    flat = FlatSnapshot(s.nodes, s.jobs, s.queues, s.others, fixture_tiers(fx))
+    L = ctypes.CDLL(lib)
+    L.kbg_tool_engine_ns_per_step.restype = ctypes.c_double
+    opts = _abi.kbg_options()
+    steps, chk = ctypes.c_int64(), ctypes.c_double()
+    ns = L.kbg_tool_engine_ns_per_step(ctypes.byref(flat.snap), ctypes.byref(opts), 5, ctypes.byref(steps),
+                                       ctypes.byref(chk), int(os.environ.get("PROF", "0")))
+    print(f"C{cid}: {steps.value} steps, {ns:.1f} ns/step, engine {ns * steps.value / 1e6:.2f} ms, checksum {chk.value:.0f}")
+
+
+if __name__ == "__main__":
+    main()
