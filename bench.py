@@ -14,7 +14,11 @@ roofline    = the scan kernel (dominant device kernel): algorithmic bytes per
               time of the launch, against 8 TB/s HBM3E
 cpu_baseline= the kbref oracle (single-threaded C++ restatement of the Go
               allocate path) on one full C3 cycle on this host
-N > 1       = independent replicas, one cluster per rank (weak scaling); see DESIGN.md
+N > 1       = ONE cluster with its node axis sharded over the N GPUs:
+              each rank scans its node rows, an RCCL all-gather over xGMI
+              publishes the per-shard feasibility bitmaps every batch, every
+              rank resolves the identical decision sequence (strong scaling;
+              the whole job places decisions_per_cycle per step)
 """
 import argparse
 import ctypes
@@ -80,6 +84,8 @@ def main():
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--candidates", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--comm", action="store_true",
+                    help="open the session through the RCCL sharded entry point even at N=1 (rehearsal)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on MI355X; gloo to rehearse on one GPU")
     args = ap.parse_args()
 
@@ -98,12 +104,13 @@ def main():
 
     cid = args.config
     t0 = time.time()
-    fx = synth.config_fixture(cid)
-    if world > 1 and rank > 0:
-        # weak scaling: each rank schedules its own replica cluster
-        fx["name"] += f"-replica{rank}"
+    fx = synth.config_fixture(cid)  # every rank: the same cluster
     cache = cache_from_fixture(fx)
     base_opts = {"device": device}
+    comm = None
+    if world > 1 or args.comm:
+        comm = kdist.ShardComm(device)
+        base_opts["comm"] = comm
     if args.batch:
         base_opts["batch_tasks"] = args.batch
     if args.candidates:
@@ -123,7 +130,8 @@ def main():
 
         for _ in range(warmup):
             step()
-        agg = {"cycle_ms": [], "decisions": 0, "evals": 0, "scan_ms": 0.0, "sel_ms": 0.0, "launches": 0}
+        agg = {"cycle_ms": [], "decisions": 0, "evals": 0, "visits": 0, "scan_ms": 0.0, "sel_ms": 0.0,
+               "launches": 0}
         if barrier:
             kdist.barrier()
         torch.cuda.synchronize()
@@ -134,6 +142,7 @@ def main():
             agg["cycle_ms"].append((time.perf_counter() - t1) * 1e3)
             st = ssn.stats()
             agg["evals"] += st.evaluations
+            agg["visits"] += st.node_visits
             agg["scan_ms"] += st.scan_kernel_ms
             agg["sel_ms"] += st.select_kernel_ms
             agg["launches"] += st.scan_launches
@@ -150,10 +159,11 @@ def main():
         return agg
 
     def roofline(agg):
-        algo = agg["evals"] * (agg["n_nodes"] * NODE_RECORD_B + TASK_RECORD_B)
+        # per rank: every evaluation row streams this shard's node records (N/R x 64 B) + its 32 B task record
+        algo = agg["visits"] * NODE_RECORD_B + agg["evals"] * TASK_RECORD_B
         ach = algo / (agg["scan_ms"] * 1e-3) / 1e9 if agg["scan_ms"] > 0 else 0.0
         return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                "traffic": load_pmc_traffic(agg["n_nodes"]), "kernel": "kbg_scan_kernel",
+                "traffic": load_pmc_traffic(agg["n_nodes"]) if comm is None else None, "kernel": "kbg_scan_kernel",
                 "avg_launch_us": agg["scan_ms"] * 1e3 / max(1, agg["launches"]),
                 "algo_bytes_per_launch": algo / max(1, agg["launches"]),
                 "evaluations_per_launch": agg["evals"] / max(1, agg["launches"])}
@@ -162,7 +172,7 @@ def main():
     prod = run_mode(0, args.steps, args.warmup, True)      # production: grouped shapes
     full = run_mode(1, max(1, min(3, args.steps)), 1, False)  # SURVEY roofline rule: every task scans all N
     decisions = prod["decisions"]
-    elapsed, total_decisions = kdist.aggregate(prod["elapsed"], decisions)
+    elapsed, total_decisions = kdist.aggregate(prod["elapsed"], decisions, sharded=world > 1)
     st = prod["stats"]
     n_nodes = prod["n_nodes"]
 
@@ -172,7 +182,8 @@ def main():
                 "evaluations": s2.evaluations, "batches": s2.batches, "mispredictions": s2.mispredictions,
                 "truncations": s2.truncations, "replayed": s2.replayed, "host_engine_ms": s2.engine_ms,
                 "host_resolve_ms": s2.resolve_ms, "device_roundtrip_ms": s2.device_ms,
-                "delta_writeback_ms": s2.delta_ms, "cycle_ms": s2.allocate_ms}
+                "delta_writeback_ms": s2.delta_ms, "exchange_ms": s2.exchange_ms, "shards": s2.shards,
+                "cycle_ms": s2.allocate_ms}
 
     line = {
         "metric": "task placements/sec + p50 allocate-cycle latency, 5k nodes x 100k pending tasks",
@@ -184,13 +195,13 @@ def main():
         "ms_per_step": elapsed / args.steps * 1e3,
         "p50_cycle_ms": statistics.median(prod["cycle_ms"]),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded BASELINE config generator, kbgpu/synth.py)",
         "config": {"workload": f"C{cid}: {n_nodes} nodes x {prod['pending']} pending tasks, "
                                f"{prod['jobs']} gang PodGroups, {prod['queues']} proportion queues, default tiers",
-                   "parallelism": "replicas" if world > 1 else "single-gpu",
+                   "parallelism": f"node-axis shards x{world} (RCCL all-gather)" if world > 1 else "single-gpu",
                    "batch_tasks": base_opts.get("batch_tasks", 8192),
                    "candidates": base_opts.get("candidates", 32)},
         "roofline": roofline(full),
@@ -206,6 +217,8 @@ def main():
         line["cpu_baseline"] = cpu_baseline(fx, f"C{cid}")
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     kdist.shutdown()
 
 

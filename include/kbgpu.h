@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KBG_ABI_VERSION 1
+#define KBG_ABI_VERSION 2
 
 typedef enum kbg_status {
   KBG_OK = 0,
@@ -183,7 +183,11 @@ typedef struct kbg_options {
   int32_t batch_tasks;  /* speculative batch size K (0 = default) */
   int32_t candidates;   /* first-M feasible nodes kept per task (0 = default) */
   int32_t full_scan;    /* 1 = every task evaluation scans the full node table */
-  int32_t reserved[7];
+  int32_t shards;       /* node-axis shards (0/1 = unsharded). Without a communicator every
+                           shard lives in this process (same layout and exchange buffer as the
+                           multi-GPU path, for single-device parity runs); with one (see
+                           kbg_session_open_sharded) it must equal the communicator size. */
+  int32_t reserved[6];
 } kbg_options;
 
 /* One placement decision, in reference order. */
@@ -239,10 +243,30 @@ typedef struct kbg_stats {
   double delta_ms;         /* host wall time spent writing touched node rows back to HBM */
   int64_t replayed;        /* engine steps replayed after a cut */
   int32_t n_classes;       /* static predicate classes on the device */
-  int32_t reserved[5];
+  int32_t shards;          /* node-axis shards of the session (1 = unsharded) */
+  int32_t shard_index;     /* the shard this process holds; -1 = every shard is local */
+  int32_t reserved0;
+  double exchange_ms;      /* summed HIP-event time of the per-batch RCCL all-gather */
+  int32_t reserved[2];
 } kbg_stats;
 
 typedef struct kbg_session kbg_session;
+
+/* Node-axis sharding across GPUs. A communicator is an RCCL
+ * clique, one rank per GPU, created collectively from one unique id that the
+ * caller distributes (rank 0 calls kbg_comm_unique_id; any side channel
+ * carries the bytes). Shard r holds the node-table rows of 64-node words
+ * [r*Wl, (r+1)*Wl), Wl = ceil(ceil(N/64)/R); per batch every rank scans its
+ * rows and an RCCL all-gather over xGMI publishes the feasibility bitmaps, so
+ * every rank resolves the identical decision sequence; each rank writes back
+ * only the node rows it owns. All ranks must call kbg_session_open_sharded
+ * and kbg_allocate with the same snapshot and options, in lockstep. */
+#define KBG_COMM_ID_BYTES 128
+typedef struct kbg_comm kbg_comm;
+kbg_status kbg_comm_unique_id(uint8_t out[KBG_COMM_ID_BYTES]);
+kbg_status kbg_comm_init(const uint8_t id[KBG_COMM_ID_BYTES], int32_t n_ranks, int32_t rank, int32_t device,
+                         kbg_comm** out);
+void kbg_comm_destroy(kbg_comm* c);
 
 /* ABI version and the last error message of this thread. */
 int32_t kbg_abi_version(void);
@@ -255,6 +279,13 @@ int32_t kbg_device_count(void);
  * gang.go:80-166, priority.go:36-77, predicates.go:112-202) on the host, uploads
  * the node table to HBM and builds the static predicate masks on the device. */
 kbg_status kbg_session_open(const kbg_snapshot* snap, const kbg_options* opts, kbg_session** out);
+
+/* kbg_session_open for rank `comm` of a node-axis sharded session: this
+ * process holds shard kbg_comm rank of opts->shards (= the communicator size);
+ * the session runs on the communicator's device. The communicator must
+ * outlive the session. */
+kbg_status kbg_session_open_sharded(const kbg_snapshot* snap, const kbg_options* opts, kbg_comm* comm,
+                                    kbg_session** out);
 
 /* allocateAction.Execute (allocate.go:41-176). Writes at most `cap` decisions.
  * Can be called once per opened or reset session. */

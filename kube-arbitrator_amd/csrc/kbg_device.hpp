@@ -105,16 +105,32 @@ enum NodeFlag : uint8_t { NF_UNSCHED = 1, NF_NIL = 2, NF_DEAD = 4 };
 hipError_t launch_build_class_mask(const StaticTables& t, int32_t n_classes, int32_t W, uint64_t* class_mask,
                                    hipStream_t stream);
 
+// Feasibility bitmaps of a batch of G evaluation rows live in one buffer laid
+// out [slot][plane][row][Wl] (u64 words; plane 0 = Idle-or-Releasing fit,
+// plane 1 = Idle fit; slot = node-axis shard, Wl = 64-node words per shard).
+// Unsharded, slot count 1 and Wl = W. Sharded, the per-shard slots are exactly
+// an all-gather's receive layout, so the select kernel reads the same buffer
+// whether the slots were written locally or gathered over RCCL.
+struct ScanGeom {
+  int32_t n_nodes;   // global node count N
+  int32_t W;         // global 64-node words, ceil(N/64)
+  int32_t Wl;        // words per shard slot
+  int32_t chunk_lo;  // first global word this launch covers
+  int32_t n_chunks;  // words this launch covers (Wl for one shard; slots*Wl for all local shards)
+  int32_t tab_lo;    // first global node held by the node table (rows are node - tab_lo)
+};
+
 // `start`/`stop` (optional) are stamped at the kernel's own start and end
 // (hipExtLaunchKernelGGL), so their elapsed time is the kernel duration.
-hipError_t launch_scan(const NodeSoA& n, int32_t n_nodes, int32_t W, const uint64_t* class_mask, const TaskRec* tasks,
-                       int32_t n_tasks, int32_t cap_check, uint64_t* out_feas, uint64_t* out_idle, hipStream_t stream,
+// `out` points at the slot of chunk_lo.
+hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* class_mask, const TaskRec* tasks,
+                       int32_t n_tasks, int32_t cap_check, uint64_t* out, hipStream_t stream,
                        hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
 // Row g gets cap_off[g+1]-cap_off[g] candidate slots at out_cand[cap_off[g]].
-hipError_t launch_select(const uint64_t* feas, const uint64_t* idlem, int32_t W, int32_t n_rows,
-                         const uint32_t* cap_off, uint32_t* out_cand, uint32_t* out_count, hipStream_t stream,
-                         hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+hipError_t launch_select(const uint64_t* bits, int32_t W, int32_t Wl, int32_t n_rows, const uint32_t* cap_off,
+                         uint32_t* out_cand, uint32_t* out_count, hipStream_t stream, hipEvent_t start = nullptr,
+                         hipEvent_t stop = nullptr);
 
 hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream);
 

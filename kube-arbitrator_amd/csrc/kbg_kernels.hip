@@ -68,11 +68,10 @@ __device__ __forceinline__ void scan_rows(const double (*s_req)[4], const uint64
   }
 }
 
-__global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, int32_t n_nodes, int32_t W,
+__global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, ScanGeom geo,
                                                        const uint64_t* __restrict__ class_mask,
                                                        const TaskRec* __restrict__ tasks, int32_t n_tasks,
-                                                       int32_t cap_check, uint64_t* __restrict__ out_feas,
-                                                       uint64_t* __restrict__ out_idle) {
+                                                       int32_t cap_check, uint64_t* __restrict__ out) {
   // Evaluation rows of this workgroup, staged once in LDS and read back as
   // same-address broadcasts; per wave, the class-mask word of each row for
   // the wave's 64-node chunk.
@@ -80,7 +79,9 @@ __global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, int32_t n_nod
   __shared__ uint64_t s_mask[kScanWaves][kScanTasksPerBlock];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int chunk = blockIdx.x * kScanWaves + wave;
+  const int rel = blockIdx.x * kScanWaves + wave;  // word relative to chunk_lo
+  const int chunk = geo.chunk_lo + rel;            // global 64-node word
+  const bool live = rel < geo.n_chunks && chunk < geo.W;
   const int t0 = blockIdx.y * kScanTasksPerBlock;
   const int nt_blk = min(n_tasks - t0, kScanTasksPerBlock);
   if (threadIdx.x < nt_blk) {
@@ -89,22 +90,23 @@ __global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, int32_t n_nod
     s_req[threadIdx.x][1] = tr.req[1];
     s_req[threadIdx.x][2] = tr.req[2];
   }
-  if (lane < nt_blk && chunk < W) s_mask[wave][lane] = class_mask[(size_t)tasks[t0 + lane].cls * W + chunk];
+  if (lane < nt_blk && live) s_mask[wave][lane] = class_mask[(size_t)tasks[t0 + lane].cls * geo.W + chunk];
   __syncthreads();
-  if (chunk >= W) return;  // wave-uniform exit (after the barrier)
+  if (!live) return;  // wave-uniform exit (after the barrier); words past W are never read
   const int node = chunk * 64 + lane;
-  const bool valid = node < n_nodes;
+  const bool valid = node < geo.n_nodes;
+  const int row = node - geo.tab_lo;
   double ic = 0, im = 0, ig = 0, rc = 0, rm = 0, rg = 0;
   int32_t nt = 0, mt = 0;
   if (valid) {
-    ic = nd.idle_cpu[node];
-    im = nd.idle_mem[node];
-    ig = nd.idle_gpu[node];
-    rc = nd.rel_cpu[node];
-    rm = nd.rel_mem[node];
-    rg = nd.rel_gpu[node];
-    nt = nd.ntasks[node];
-    mt = nd.maxtasks[node];
+    ic = nd.idle_cpu[row];
+    im = nd.idle_mem[row];
+    ig = nd.idle_gpu[row];
+    rc = nd.rel_cpu[row];
+    rm = nd.rel_mem[row];
+    rg = nd.rel_gpu[row];
+    nt = nd.ntasks[row];
+    mt = nd.maxtasks[row];
   }
   const int node_ok = (int)valid & ((int)!cap_check | (int)(nt < mt));
   // Releasing is usually zero on every node of the wave; then the Releasing
@@ -126,40 +128,50 @@ __global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, int32_t n_nod
   else
     scan_rows<false>(s_req, s_mask[wave], nt_blk, lane, node_ok, ic, im, ig, rc, rm, rg, rz_rows, &keep_f, &keep_i);
   if (lane < nt_blk) {
-    out_feas[(size_t)(t0 + lane) * W + chunk] = keep_f;
-    out_idle[(size_t)(t0 + lane) * W + chunk] = keep_i;
+    // [slot][plane][row][Wl] (kbg_device.hpp ScanGeom)
+    const int slot = rel / geo.Wl, w = rel - slot * geo.Wl;
+    const size_t plane = (size_t)n_tasks * geo.Wl;
+    uint64_t* o = out + (size_t)slot * 2 * plane + (size_t)(t0 + lane) * geo.Wl + w;
+    o[0] = keep_f;
+    o[plane] = keep_i;
   }
 }
 
-hipError_t launch_scan(const NodeSoA& n, int32_t n_nodes, int32_t W, const uint64_t* class_mask, const TaskRec* tasks,
-                       int32_t n_tasks, int32_t cap_check, uint64_t* out_feas, uint64_t* out_idle,
-                       hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
-  if (n_tasks <= 0 || W <= 0) return hipSuccess;
-  dim3 grid((W + kScanWaves - 1) / kScanWaves, (n_tasks + kScanTasksPerBlock - 1) / kScanTasksPerBlock);
-  hipExtLaunchKernelGGL(kbg_scan_kernel, grid, dim3(64 * kScanWaves), 0, stream, start, stop, 0, n, n_nodes, W,
-                        class_mask, tasks, n_tasks, cap_check, out_feas, out_idle);
+hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* class_mask, const TaskRec* tasks,
+                       int32_t n_tasks, int32_t cap_check, uint64_t* out, hipStream_t stream, hipEvent_t start,
+                       hipEvent_t stop) {
+  if (n_tasks <= 0 || g.n_chunks <= 0) return hipSuccess;
+  dim3 grid((g.n_chunks + kScanWaves - 1) / kScanWaves, (n_tasks + kScanTasksPerBlock - 1) / kScanTasksPerBlock);
+  hipExtLaunchKernelGGL(kbg_scan_kernel, grid, dim3(64 * kScanWaves), 0, stream, start, stop, 0, n, g, class_mask,
+                        tasks, n_tasks, cap_check, out);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- select
-__global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restrict__ feas,
-                                                         const uint64_t* __restrict__ idlem, int32_t W,
+// One wave per row walks the row's words in global node order (shard slots in
+// rank order = ascending node index), so the candidates come out first-fit.
+__global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restrict__ bits, int32_t W, int32_t Wl,
                                                          int32_t n_rows, const uint32_t* __restrict__ cap_off,
                                                          uint32_t* __restrict__ out_cand,
                                                          uint32_t* __restrict__ out_count) {
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= n_rows) return;
-  const uint64_t* frow = feas + (size_t)t * W;
-  const uint64_t* irow = idlem + (size_t)t * W;
+  const size_t plane = (size_t)n_rows * Wl;
+  const uint64_t* row = bits + (size_t)t * Wl;
   const int M = (int)(cap_off[t + 1] - cap_off[t]);
   uint32_t* cand = out_cand + cap_off[t];
   int found = 0;
   int base = 0;
   for (; base < W && found < M; base += 64) {
     const int c = base + lane;
-    uint64_t f = c < W ? frow[c] : 0ull;
-    const uint64_t iw = c < W ? irow[c] : 0ull;
+    uint64_t f = 0ull, iw = 0ull;
+    if (c < W) {
+      const int slot = c / Wl;
+      const uint64_t* p = row + (size_t)slot * 2 * plane + (c - slot * Wl);
+      f = p[0];
+      iw = p[plane];
+    }
     const int pc = __popcll(f);
     int incl = pc;
 #pragma unroll
@@ -185,11 +197,11 @@ __global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restr
   }
 }
 
-hipError_t launch_select(const uint64_t* feas, const uint64_t* idlem, int32_t W, int32_t n_rows,
-                         const uint32_t* cap_off, uint32_t* out_cand, uint32_t* out_count, hipStream_t stream,
-                         hipEvent_t start, hipEvent_t stop) {
+hipError_t launch_select(const uint64_t* bits, int32_t W, int32_t Wl, int32_t n_rows, const uint32_t* cap_off,
+                         uint32_t* out_cand, uint32_t* out_count, hipStream_t stream, hipEvent_t start,
+                         hipEvent_t stop) {
   if (n_rows <= 0) return hipSuccess;
-  hipExtLaunchKernelGGL(kbg_select_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, stream, start, stop, 0, feas, idlem, W,
+  hipExtLaunchKernelGGL(kbg_select_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, stream, start, stop, 0, bits, W, Wl,
                         n_rows, cap_off, out_cand, out_count);
   return hipGetLastError();
 }

@@ -24,6 +24,7 @@
 // mirror. An unpredicted outcome or an exhausted candidate list cuts the
 // batch; the engine is restored from a checkpoint and replayed to the cut.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -45,6 +46,12 @@
 #include <vector>
 
 #include "kbg_session.hpp"
+
+// An RCCL clique of node-axis shards, one rank per GPU (kbgpu.h).
+struct kbg_comm {
+  ncclComm_t nccl = nullptr;
+  int32_t n_ranks = 1, rank = 0, device = 0;
+};
 
 namespace {
 
@@ -379,7 +386,7 @@ kbg_status hupload(Session& S, T** p, const std::vector<T>& v) {
 }
 
 kbg_status alloc_soa(Session& S, kbg::NodeSoA* soa) {
-  const size_t N = (size_t)S.n_nodes;
+  const size_t N = (size_t)S.tab_n;
   kbg_status st;
   if ((st = dalloc(S, &soa->idle_cpu, N)) || (st = dalloc(S, &soa->idle_mem, N)) || (st = dalloc(S, &soa->idle_gpu, N)) ||
       (st = dalloc(S, &soa->rel_cpu, N)) || (st = dalloc(S, &soa->rel_mem, N)) || (st = dalloc(S, &soa->rel_gpu, N)) ||
@@ -389,7 +396,8 @@ kbg_status alloc_soa(Session& S, kbg::NodeSoA* soa) {
 }
 
 kbg_status copy_soa(Session& S, const kbg::NodeSoA& dst, const kbg::NodeSoA& src) {
-  const size_t N = (size_t)S.n_nodes;
+  const size_t N = (size_t)S.tab_n;
+  if (N == 0) return KBG_OK;
   HIP_TRY(hipMemcpyAsync(dst.idle_cpu, src.idle_cpu, N * 8, hipMemcpyDeviceToDevice, S.stream));
   HIP_TRY(hipMemcpyAsync(dst.idle_mem, src.idle_mem, N * 8, hipMemcpyDeviceToDevice, S.stream));
   HIP_TRY(hipMemcpyAsync(dst.idle_gpu, src.idle_gpu, N * 8, hipMemcpyDeviceToDevice, S.stream));
@@ -444,11 +452,14 @@ void device_row(const Session& S, int32_t n, double* ic, double* im, double* ig,
   *mt = S.maxtasks[n];
 }
 
+// Uploads the node rows this process holds (global nodes [tab_lo, tab_lo + tab_n)).
 kbg_status upload_nodes(Session& S) {
-  const int32_t N = S.n_nodes;
+  const int32_t N = S.tab_n;
+  if (N == 0) return KBG_OK;
   std::vector<double> ic(N), im(N), ig(N), rc(N), rm(N), rg(N);
   std::vector<int32_t> nt(N), mt(N);
-  for (int32_t n = 0; n < N; ++n) device_row(S, n, &ic[n], &im[n], &ig[n], &rc[n], &rm[n], &rg[n], &nt[n], &mt[n]);
+  for (int32_t i = 0; i < N; ++i)
+    device_row(S, S.tab_lo + i, &ic[i], &im[i], &ig[i], &rc[i], &rm[i], &rg[i], &nt[i], &mt[i]);
   auto up = [&](void* d, const void* h, size_t b) { return hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, S.stream); };
   HIP_TRY(up(S.d_nodes0.idle_cpu, ic.data(), N * 8));
   HIP_TRY(up(S.d_nodes0.idle_mem, im.data(), N * 8));
@@ -471,10 +482,24 @@ kbg_status device_launch(Session& S, int32_t G) {
   const kbg::TaskRec* d_tasks = (const kbg::TaskRec*)S.d_up;
   const uint32_t* d_capoff = (const uint32_t*)(S.d_up + (size_t)G * sizeof(kbg::TaskRec));
   HIP_TRY(hipMemcpyAsync(S.d_up, S.h_up, up_bytes, hipMemcpyHostToDevice, S.stream));
-  HIP_TRY(kbg::launch_scan(S.d_nodes, S.n_nodes, S.W, S.d_class_mask, d_tasks, G, S.pred_active ? 1 : 0, S.d_feas,
-                           S.d_idlem, S.stream, S.ev[0], S.ev[1]));
-  HIP_TRY(kbg::launch_select(S.d_feas, S.d_idlem, S.W, G, d_capoff, S.d_down + G, S.d_down, S.stream, S.ev[2],
-                             S.ev[3]));
+  // this process scans its shard (or every shard when they are all local)
+  kbg::ScanGeom geo{S.n_nodes, S.W, S.Wl, 0, S.R * S.Wl, S.tab_lo};
+  const size_t slot_words = (size_t)2 * G * S.Wl;
+  uint64_t* out = S.d_bits;
+  if (S.comm) {
+    geo.chunk_lo = S.shard * S.Wl;
+    geo.n_chunks = S.Wl;
+    out = S.d_bits + (size_t)S.shard * slot_words;
+  }
+  HIP_TRY(kbg::launch_scan(S.d_nodes, geo, S.d_class_mask, d_tasks, G, S.pred_active ? 1 : 0, out, S.stream, S.ev[0],
+                           S.ev[1]));
+  if (S.comm) {  // in-place all-gather: every rank receives every shard's slot, in rank (= node) order
+    HIP_TRY(hipEventRecord(S.ev[4], S.stream));
+    const ncclResult_t nr = ncclAllGather(out, S.d_bits, slot_words, ncclUint64, S.comm->nccl, S.stream);
+    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
+    HIP_TRY(hipEventRecord(S.ev[5], S.stream));
+  }
+  HIP_TRY(kbg::launch_select(S.d_bits, S.W, S.Wl, G, d_capoff, S.d_down + G, S.d_down, S.stream, S.ev[2], S.ev[3]));
   HIP_TRY(hipMemcpyAsync(S.h_down, S.d_down, ((size_t)G + total) * 4, hipMemcpyDeviceToHost, S.stream));
   return KBG_OK;
 }
@@ -488,9 +513,13 @@ kbg_status device_wait(Session& S, int32_t G) {
   S.stats.scan_kernel_ms += ms;
   HIP_TRY(hipEventElapsedTime(&ms, S.ev[2], S.ev[3]));
   S.stats.select_kernel_ms += ms;
+  if (S.comm) {
+    HIP_TRY(hipEventElapsedTime(&ms, S.ev[4], S.ev[5]));
+    S.stats.exchange_ms += ms;
+  }
   S.stats.scan_launches++;
   S.stats.evaluations += G;
-  S.stats.node_visits += (int64_t)G * S.n_nodes;
+  S.stats.node_visits += (int64_t)G * (S.comm ? S.tab_n : S.n_nodes);
   return KBG_OK;
 }
 
@@ -500,24 +529,26 @@ kbg_status device_scan(Session& S, int32_t G) {
   return st != KBG_OK ? st : device_wait(S, G);
 }
 
-// Writes the rows of the nodes touched by the last commits back to HBM.
+// Writes the rows of the nodes touched by the last commits back to HBM (only
+// the rows this process holds; every shard's host mirror saw every commit).
 kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
-  size_t done = 0;
-  while (done < touched.size()) {
-    const size_t cnt = std::min<size_t>(touched.size() - done, (size_t)S.K);
-    for (size_t i = 0; i < cnt; ++i) {
-      const int32_t n = touched[done + i];
-      kbg::NodeDelta& d = S.h_deltas[i];
+  size_t i = 0;
+  while (i < touched.size()) {
+    int32_t cnt = 0;
+    for (; i < touched.size() && cnt < S.K; ++i) {
+      const int32_t n = touched[i];
+      if (n < S.tab_lo || n >= S.tab_lo + S.tab_n) continue;
+      kbg::NodeDelta& d = S.h_deltas[cnt++];
       int32_t mt;
-      d.node = n;
+      d.node = n - S.tab_lo;
       device_row(S, n, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &mt);
     }
+    if (cnt == 0) break;
     HIP_TRY(hipMemcpyAsync(S.d_deltas, S.h_deltas, cnt * sizeof(kbg::NodeDelta), hipMemcpyHostToDevice, S.stream));
-    HIP_TRY(kbg::launch_apply(S.d_nodes, S.d_deltas, (int32_t)cnt, S.stream));
-    done += cnt;
+    HIP_TRY(kbg::launch_apply(S.d_nodes, S.d_deltas, cnt, S.stream));
     // The staging buffer is reused by the next chunk or the next batch; the
     // next device_scan's synchronize (same stream) retires this copy first.
-    if (done < touched.size()) HIP_TRY(hipStreamSynchronize(S.stream));
+    if (i < touched.size()) HIP_TRY(hipStreamSynchronize(S.stream));
   }
   return KBG_OK;
 }
@@ -704,7 +735,7 @@ std::vector<int32_t> ranks_of(const Session& S, const std::vector<int32_t>& ids)
   return rank;
 }
 
-kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
+kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options* o, kbg_comm* comm) {
   const auto t_open = std::chrono::steady_clock::now();
   kbg_status st = validate(snap);
   if (st != KBG_OK) return st;
@@ -972,6 +1003,25 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   compile_static_predicates(S, &sh);
   S.n_classes = sh.n_classes;
   S.W = (N + 63) / 64;
+  // ---- node-axis shards: contiguous 64-node word ranges, so
+  // rank order is node order and first-fit survives the split
+  S.comm = comm;
+  S.R = std::max(1, S.opts.shards);
+  if (comm) {
+    if (S.opts.shards > 0 && S.opts.shards != comm->n_ranks)
+      return fail(KBG_E_INVALID, "options.shards differs from the communicator size");
+    S.R = comm->n_ranks;
+    S.shard = comm->rank;
+  }
+  if (S.R > 1024) return fail(KBG_E_INVALID, "shards > 1024");
+  S.Wl = std::max(1, (S.W + S.R - 1) / S.R);
+  if (S.comm) {
+    S.tab_lo = std::min(N, S.shard * S.Wl * 64);
+    S.tab_n = std::min(N, (S.shard + 1) * S.Wl * 64) - S.tab_lo;
+  } else {
+    S.tab_lo = 0;
+    S.tab_n = N;
+  }
   {
     std::unordered_map<ShapeKey, int32_t, ShapeHash> ids;
     S.task_shape.assign(S.n_tasks, -1);
@@ -988,6 +1038,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(KBG_E_HIP, "no HIP device visible");
   S.device = S.opts.device >= 0 ? S.opts.device : 0;
   if (S.opts.device < 0) HIP_TRY(hipGetDevice(&S.device));
+  if (comm) S.device = comm->device;
   HIP_TRY(hipSetDevice(S.device));
   HIP_TRY(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   for (auto& e : S.ev) HIP_TRY(hipEventCreate(&e));
@@ -995,7 +1046,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   const size_t up_cap = (size_t)S.K * sizeof(kbg::TaskRec) + ((size_t)S.K + 1) * 4;
   const size_t down_cap = (size_t)S.K + (size_t)S.cand_cap;
   if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) || (st = dalloc(S, &S.d_up, up_cap)) ||
-      (st = dalloc(S, &S.d_feas, (size_t)S.K * S.W)) || (st = dalloc(S, &S.d_idlem, (size_t)S.K * S.W)) ||
+      (st = dalloc(S, &S.d_bits, (size_t)S.R * 2 * S.K * S.Wl)) ||
       (st = dalloc(S, &S.d_down, down_cap)) || (st = dalloc(S, &S.d_deltas, S.K)))
     return st;
   HIP_TRY(hipHostMalloc((void**)&S.h_up, up_cap, hipHostMallocDefault));
@@ -1039,6 +1090,8 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     HIP_TRY(hipStreamSynchronize(S.stream));  // sh's host vectors end with this scope
   }
   S.stats.n_classes = S.n_classes;
+  S.stats.shards = S.R;
+  S.stats.shard_index = S.comm ? S.shard : -1;
   S.stats.open_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_open).count();
   return KBG_OK;
 }
@@ -1145,11 +1198,12 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   const auto t0 = clk::now();
-  const int32_t n_classes = S.stats.n_classes;
-  const double open_ms = S.stats.open_ms;
+  const kbg_stats prev = S.stats;
   S.stats = kbg_stats{};
-  S.stats.n_classes = n_classes;
-  S.stats.open_ms = open_ms;
+  S.stats.n_classes = prev.n_classes;
+  S.stats.shards = prev.shards;
+  S.stats.shard_index = prev.shard_index;
+  S.stats.open_ms = prev.open_ms;
 
   std::vector<kbg_decision> dec;
   std::vector<Res> dec_old;  // the Idle (Allocate) or Releasing (Pipeline) row before each decision
@@ -1409,14 +1463,14 @@ int32_t kbg_device_count(void) {
   return n;
 }
 
-kbg_status kbg_session_open(const kbg_snapshot* snap, const kbg_options* opts, kbg_session** out) {
+static kbg_status session_open(const kbg_snapshot* snap, const kbg_options* opts, kbg_comm* comm, kbg_session** out) {
   if (!out) return fail(KBG_E_INVALID, "null out");
   *out = nullptr;
   kbg_session* s = new (std::nothrow) kbg_session();
   if (!s) return fail(KBG_E_NOMEM, "session");
   kbg_status st;
   try {
-    st = open_session(s->s, snap, opts);
+    st = open_session(s->s, snap, opts, comm);
   } catch (const std::bad_alloc&) {
     st = fail(KBG_E_NOMEM, "host allocation failed");
   }
@@ -1427,6 +1481,55 @@ kbg_status kbg_session_open(const kbg_snapshot* snap, const kbg_options* opts, k
   }
   *out = s;
   return KBG_OK;
+}
+
+kbg_status kbg_session_open(const kbg_snapshot* snap, const kbg_options* opts, kbg_session** out) {
+  return session_open(snap, opts, nullptr, out);
+}
+
+kbg_status kbg_session_open_sharded(const kbg_snapshot* snap, const kbg_options* opts, kbg_comm* comm,
+                                    kbg_session** out) {
+  if (!comm) return fail(KBG_E_INVALID, "null communicator");
+  return session_open(snap, opts, comm, out);
+}
+
+kbg_status kbg_comm_unique_id(uint8_t out[KBG_COMM_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) == KBG_COMM_ID_BYTES, "ncclUniqueId size");
+  if (!out) return fail(KBG_E_INVALID, "null out");
+  ncclUniqueId id;
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::memcpy(out, &id, sizeof(id));
+  return KBG_OK;
+}
+
+kbg_status kbg_comm_init(const uint8_t id[KBG_COMM_ID_BYTES], int32_t n_ranks, int32_t rank, int32_t device,
+                         kbg_comm** out) {
+  if (!id || !out) return fail(KBG_E_INVALID, "null argument");
+  *out = nullptr;
+  if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(KBG_E_INVALID, "rank / n_ranks");
+  HIP_TRY(hipSetDevice(device));
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  kbg_comm* c = new (std::nothrow) kbg_comm();
+  if (!c) return fail(KBG_E_NOMEM, "comm");
+  const ncclResult_t r = ncclCommInitRank(&c->nccl, n_ranks, uid, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return fail(KBG_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  c->n_ranks = n_ranks;
+  c->rank = rank;
+  c->device = device;
+  *out = c;
+  return KBG_OK;
+}
+
+void kbg_comm_destroy(kbg_comm* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->nccl) (void)ncclCommDestroy(c->nccl);
+  delete c;
 }
 
 kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out) {

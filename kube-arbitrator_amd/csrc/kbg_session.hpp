@@ -147,14 +147,18 @@ struct Session {
   int32_t device = 0;
   hipStream_t stream = nullptr;
   int32_t W = 0;            // u64 words per node bitmap row
+  // node-axis sharding: R shards of Wl words; this process holds
+  // shard `shard` (comm != null) or every shard (shard = -1)
+  int32_t R = 1, Wl = 0, shard = -1;
+  int32_t tab_lo = 0, tab_n = 0;  // global node range of the device node table
+  kbg_comm* comm = nullptr;
   int32_t n_classes = 0;
   int32_t K = 0, M = 0;     // batch tasks, candidates per row (full-scan) / slack (grouped)
   int64_t cand_cap = 0;     // candidate slots allocated
   NodeSoA d_nodes{};
   NodeSoA d_nodes0{};       // pristine copy for kbg_session_reset
   uint64_t* d_class_mask = nullptr;
-  uint64_t* d_feas = nullptr;
-  uint64_t* d_idlem = nullptr;
+  uint64_t* d_bits = nullptr;     // feasibility bitmaps [slot][plane][row][Wl] (ScanGeom)
   uint32_t* h_capoff = nullptr;   // per-row candidate slot offsets (inside h_up)
   char* h_up = nullptr;           // pinned upload staging: TaskRec[G] then capoff[G+1]
   char* d_up = nullptr;
@@ -165,7 +169,7 @@ struct Session {
   uint32_t* h_cand = nullptr;    // = h_down + G (set per batch)
   uint32_t* h_count = nullptr;   // = h_down
   NodeDelta* h_deltas = nullptr; // pinned
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   std::vector<void*> d_allocs;
 
   kbg_stats stats{};

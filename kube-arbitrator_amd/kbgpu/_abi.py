@@ -35,6 +35,9 @@ DISABLE_RECLAIMABLE = 1 << 4
 DISABLE_QUEUE_ORDER = 1 << 5
 DISABLE_PREDICATE = 1 << 6
 
+ABI_VERSION = 2
+COMM_ID_BYTES = 128
+
 KIND_ALLOCATE = 0
 KIND_PIPELINE = 1
 
@@ -116,7 +119,7 @@ class kbg_snapshot(ctypes.Structure):
 
 class kbg_options(ctypes.Structure):
     _fields_ = [("device", i32), ("heap_rule", i32), ("batch_tasks", i32), ("candidates", i32),
-                ("full_scan", i32), ("reserved", i32 * 7)]
+                ("full_scan", i32), ("shards", i32), ("reserved", i32 * 6)]
 
 
 class kbg_decision(ctypes.Structure):
@@ -142,7 +145,8 @@ class kbg_stats(ctypes.Structure):
     _fields_ = [("evaluations", i64), ("node_visits", i64), ("batches", i64), ("mispredictions", i64),
                 ("truncations", i64), ("scan_launches", i64), ("scan_kernel_ms", f64), ("select_kernel_ms", f64),
                 ("allocate_ms", f64), ("open_ms", f64), ("engine_ms", f64), ("resolve_ms", f64),
-                ("device_ms", f64), ("delta_ms", f64), ("replayed", i64), ("n_classes", i32), ("reserved", i32 * 5)]
+                ("device_ms", f64), ("delta_ms", f64), ("replayed", i64), ("n_classes", i32), ("shards", i32), ("shard_index", i32),
+                ("reserved0", i32), ("exchange_ms", f64), ("reserved", i32 * 2)]
 
 
 # Every symbol include/kbgpu.h declares, with its ctypes signature.
@@ -151,6 +155,10 @@ SIGNATURES = {
     "kbg_last_error": (ctypes.c_char_p, []),
     "kbg_device_count": (i32, []),
     "kbg_session_open": (i32, [P(kbg_snapshot), P(kbg_options), P(ctypes.c_void_p)]),
+    "kbg_session_open_sharded": (i32, [P(kbg_snapshot), P(kbg_options), ctypes.c_void_p, P(ctypes.c_void_p)]),
+    "kbg_comm_unique_id": (i32, [P(ctypes.c_uint8)]),
+    "kbg_comm_init": (i32, [P(ctypes.c_uint8), i32, i32, i32, P(ctypes.c_void_p)]),
+    "kbg_comm_destroy": (None, [ctypes.c_void_p]),
     "kbg_allocate": (i32, [ctypes.c_void_p, P(kbg_decision), i32, P(i32)]),
     "kbg_session_reset": (i32, [ctypes.c_void_p]),
     "kbg_select": (i32, [ctypes.c_void_p, P(i32), i32, i32, P(i32), P(i32), P(i32)]),
@@ -186,7 +194,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.kbg_abi_version() != 1:
+        if L.kbg_abi_version() != ABI_VERSION:
             raise ImportError("libkbgpu ABI version mismatch")
         _lib = L
     return _lib

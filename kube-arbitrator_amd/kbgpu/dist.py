@@ -1,10 +1,13 @@
 """Multi-process plumbing for `bench.py --gpus N` (one process per GPU).
 
-This round N > 1 runs independent replicas (one cluster per rank, weak
-scaling): the only cross-rank traffic is the bench's own barrier and the
-max-over-ranks wall time / sum-over-ranks placements reduction below.
-Works with "nccl" (RCCL over xGMI) on MI355X and with "gloo" on CPU.
+N > 1 shards ONE cluster's node axis across the ranks: every
+rank opens the same snapshot through `kbg_session_open_sharded` on an RCCL
+communicator (`ShardComm`) and the library all-gathers the per-shard
+feasibility bitmaps of each batch over xGMI. torch.distributed ("nccl" =
+RCCL on MI355X, "gloo" on CPU) only carries the communicator's unique id, the
+bench's barriers and the max-over-ranks wall time.
 """
+import ctypes
 import os
 
 import torch
@@ -30,15 +33,50 @@ def barrier():
         dist.barrier()
 
 
-def aggregate(elapsed_s, decisions):
-    """(max elapsed over ranks, total placements over ranks)."""
+def broadcast_bytes(data, src=0):
+    """Rank `src`'s bytes on every rank (the communicator id's side channel)."""
+    if not dist.is_initialized():
+        return data
+    box = [data]
+    dist.broadcast_object_list(box, src=src)
+    return box[0]
+
+
+class ShardComm:
+    """kbg_comm: the RCCL clique of the node-axis shards, one rank per GPU."""
+
+    def __init__(self, device, rank=None, world=None):
+        from . import _abi
+        L = _abi.lib()
+        if rank is None:
+            rank, world = (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
+        uid = (ctypes.c_uint8 * _abi.COMM_ID_BYTES)()
+        if rank == 0:
+            _abi.check(L.kbg_comm_unique_id(uid))
+        uid_bytes = broadcast_bytes(bytes(uid))
+        uid = (ctypes.c_uint8 * _abi.COMM_ID_BYTES).from_buffer_copy(uid_bytes)
+        self.handle = ctypes.c_void_p()
+        _abi.check(L.kbg_comm_init(uid, world, rank, device, ctypes.byref(self.handle)))
+        self.rank, self.world, self.device = rank, world, device
+
+    def close(self):
+        if self.handle:
+            from . import _abi
+            _abi.lib().kbg_comm_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+
+def aggregate(elapsed_s, decisions, sharded=False):
+    """(max elapsed over ranks, placements of the whole job). Sharded ranks
+    produce the same decisions for one cluster, so they count once;
+    independent clusters (replicas) add up."""
     if not dist.is_initialized():
         return elapsed_s, decisions
     dev = torch.device("cuda") if dist.get_backend() == "nccl" else torch.device("cpu")
     t = torch.tensor([elapsed_s], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     d = torch.tensor([float(decisions)], dtype=torch.float64, device=dev)
-    dist.all_reduce(d, op=dist.ReduceOp.SUM)
+    dist.all_reduce(d, op=dist.ReduceOp.MAX if sharded else dist.ReduceOp.SUM)
     return float(t.item()), int(d.item())
 
 

@@ -60,10 +60,17 @@ class Session:
         self.handle = ctypes.c_void_p()
         opts = _abi.kbg_options()
         opts.device = -1
-        for k, v in (options or {}).items():
+        options = dict(options or {})
+        comm = options.pop("comm", None)  # dist.ShardComm: node-axis shard of an RCCL clique
+        for k, v in options.items():
             setattr(opts, k, v)
         L = _abi.lib()
-        _abi.check(L.kbg_session_open(ctypes.byref(self.flat.snap), ctypes.byref(opts), ctypes.byref(self.handle)))
+        if comm is not None:
+            _abi.check(L.kbg_session_open_sharded(ctypes.byref(self.flat.snap), ctypes.byref(opts), comm.handle,
+                                                  ctypes.byref(self.handle)))
+        else:
+            _abi.check(L.kbg_session_open(ctypes.byref(self.flat.snap), ctypes.byref(opts),
+                                          ctypes.byref(self.handle)))
         self.decisions = []
 
     def _active_tiers(self):

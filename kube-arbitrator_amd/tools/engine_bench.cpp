@@ -8,7 +8,7 @@
 extern "C" double kbg_tool_engine_ns_per_step(const kbg_snapshot* snap, const kbg_options* o, int32_t reps,
                                               int64_t* steps_out, double* checksum, int32_t profile) {
   kbg::Session S;
-  open_session(S, snap, o);  // returns KBG_E_HIP on a machine without a device; host state is complete
+  open_session(S, snap, o, nullptr);  // returns KBG_E_HIP on a machine without a device; host state is complete
   if (S.init.qlen == 0) return -1.0;
   double best = 1e30;
   int64_t steps = 0;

@@ -23,7 +23,12 @@ def _worker(rank, world, port, q):
     assert dist.init("gloo")
     dist.barrier()
     # rank r "placed" 1000*(r+1) tasks in (r+1) seconds
-    q.put((rank, dist.aggregate(float(rank + 1), 1000 * (rank + 1))))
+    replicas = dist.aggregate(float(rank + 1), 1000 * (rank + 1))
+    # node-axis shards of one cluster: every rank reports the same decisions
+    sharded = dist.aggregate(float(rank + 1), 5000, sharded=True)
+    # the communicator id travels from rank 0 (kbg_comm_unique_id) to every rank
+    uid = dist.broadcast_bytes(bytes(range(128)) if rank == 0 else b"")
+    q.put((rank, (replicas, sharded, uid)))
     dist.shutdown()
 
 
@@ -40,4 +45,21 @@ def test_gloo_aggregate(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     for r in range(world):
-        assert got[r] == (float(world), 1000 * world * (world + 1) // 2)
+        replicas, sharded, uid = got[r]
+        assert replicas == (float(world), 1000 * world * (world + 1) // 2)
+        assert sharded == (float(world), 5000)
+        assert uid == bytes(range(128))
+
+
+def test_comm_fails_loudly_without_device():
+    """No silent single-process fallback when RCCL / HIP cannot start."""
+    import ctypes
+    from kbgpu import _abi
+    L = _abi.lib()
+    if L.kbg_device_count() > 0:
+        pytest.skip("a device is present")
+    h = ctypes.c_void_p()
+    uid = (ctypes.c_uint8 * _abi.COMM_ID_BYTES)()
+    assert L.kbg_comm_init(uid, 1, 0, 0, ctypes.byref(h)) == _abi.KBG_E_HIP
+    assert not h.value
+    assert L.kbg_comm_init(uid, 2, 2, 0, ctypes.byref(h)) == _abi.KBG_E_INVALID

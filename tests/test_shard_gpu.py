@@ -1,0 +1,94 @@
+"""Node-axis sharding against the kbref oracle, on the GPU box.
+
+`shards=R` without a communicator keeps all R shards in one process: the
+same scan geometry, slot layout and select walk as R GPUs exchanging their
+slots over RCCL, with the slots written locally instead of all-gathered. A
+one-rank RCCL communicator runs the all-gather itself. Decisions must stay
+bit-exact for every shard count, including shards that hold no node.
+"""
+import pytest
+
+from helpers import compare_outputs, run_oracle
+
+pytestmark = pytest.mark.gpu
+
+kbgpu = pytest.importorskip("kbgpu")
+from kbgpu import synth  # noqa: E402
+from kbgpu.fixture import run_fixture  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_device():
+    from kbgpu import _abi
+    if _abi.lib().kbg_device_count() < 1:
+        pytest.fail("no HIP device: the gpu tests must run on an MI355X (no CPU fallback)")
+
+
+@pytest.mark.parametrize("shards", [2, 3, 8, 64])
+@pytest.mark.parametrize("cid", [1, 2])
+def test_local_shards_config_parity(cid, shards):
+    fx = synth.config_fixture(cid)
+    got, ssn = run_fixture(fx, {"shards": shards})
+    assert ssn.stats().shards == shards and ssn.stats().shard_index == -1
+    compare_outputs(run_oracle(fx), got)
+    ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 120, 2))
+def test_local_shards_fuzz_parity(seed):
+    fx = synth.random_fixture(seed)
+    opts = {"shards": 2 + seed % 7, "batch_tasks": 1 + seed % 9, "candidates": 1 + seed % 5, "full_scan": seed % 4 == 0}
+    opts["full_scan"] = int(opts["full_scan"])
+    got, ssn = run_fixture(fx, opts)
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
+@pytest.mark.slow
+def test_local_shards_config3(c3_ref):
+    fx, ref = c3_ref
+    got, ssn = run_fixture(fx, {"shards": 8})
+    compare_outputs(ref, got)
+    ssn.close()
+
+
+@pytest.fixture(scope="module")
+def c3_ref():
+    fx = synth.config_fixture(3)
+    return fx, run_oracle(fx)
+
+
+@pytest.fixture(scope="module")
+def comm1():
+    from kbgpu.dist import ShardComm
+    c = ShardComm(device=0, rank=0, world=1)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("cid", [1, 2])
+def test_rccl_one_rank_parity(cid, comm1):
+    """The sharded entry point end to end: scan of the own slot, ncclAllGather
+    in place, select over the gathered slots."""
+    fx = synth.config_fixture(cid)
+    got, ssn = run_fixture(fx, {"comm": comm1})
+    st = ssn.stats()
+    assert st.shards == 1 and st.shard_index == 0 and st.exchange_ms > 0.0
+    compare_outputs(run_oracle(fx), got)
+    ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 40, 5))
+def test_rccl_one_rank_fuzz(seed, comm1):
+    fx = synth.random_fixture(seed)
+    got, ssn = run_fixture(fx, {"comm": comm1, "batch_tasks": 1 + seed % 9, "candidates": 1 + seed % 5})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
+def test_rccl_shard_count_must_match(comm1):
+    fx = synth.config_fixture(1)
+    got, ssn = run_fixture(fx, {"comm": comm1, "shards": 2})
+    assert got["status"] == "invalid" and ssn is None
