@@ -231,7 +231,7 @@ typedef struct kbg_stats {
   int64_t node_visits;     /* (task,node) pairs evaluated on the device */
   int64_t batches;
   int64_t mispredictions;  /* batches cut by an unpredicted failure */
-  int64_t truncations;     /* batches cut by an exhausted candidate list */
+  int64_t truncations;     /* rescans of a batch remainder after an exhausted candidate list */
   int64_t scan_launches;
   double scan_kernel_ms;   /* summed HIP-event time of the scan kernel */
   double select_kernel_ms; /* summed HIP-event time of the candidate-select kernel */

@@ -566,13 +566,13 @@ struct Grouper {
   std::vector<int32_t> row_of;  // per batch entry
   int32_t stamp = 0;
   explicit Grouper(Session& s) : S(s), shape_row(s.n_shapes, -1), shape_stamp(s.n_shapes, -1) {}
-  int32_t build(const std::vector<int32_t>& bt) {
+  int32_t build(const int32_t* bt, int32_t n) {
     S.h_tasks = (kbg::TaskRec*)S.h_up;
     ++stamp;
-    row_of.resize(bt.size());
+    row_of.resize(n);
     count.clear();
     int32_t G = 0;
-    for (size_t i = 0; i < bt.size(); ++i) {
+    for (int32_t i = 0; i < n; ++i) {
       const int32_t t = bt[i];
       int32_t g;
       const int32_t sh = S.task_shape[t];
@@ -1340,7 +1340,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     S.stats.batches++;
     // device: feasibility scan + first-fit candidate lists against the batch-start table
     auto tp = clk::now();
-    const int32_t G = grouper.build(bt);
+    int32_t G = grouper.build(bt.data(), (int32_t)bt.size());
     kbg_status st = device_launch(S, G);
     if (st == KBG_OK) st = device_wait(S, G);
     if (st != KBG_OK) {
@@ -1355,15 +1355,37 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     touched.clear();
     bactual.assign(bt.size(), 0);
     int32_t cut = -1;
+    int32_t seg = 0;  // first batch entry covered by the current device scan
     bool panic = false;
     for (int32_t i = 0; i < (int32_t)bt.size(); ++i) {
       const int32_t t = bt[i];
       int32_t node = -1, kind = 0;
-      const int r = rs.resolve(grouper.row_of[i], t, &node, &kind);
+      int r = rs.resolve(grouper.row_of[i - seg], t, &node, &kind);
       if (r == RES_TRUNC) {
-        cut = i;
+        // A candidate list ran out before the table did. The predictions
+        // still hold (no outcome differed), so instead of cutting the batch
+        // and replaying the engine, write the commits so far back to HBM and
+        // rescan the rest of the batch against the updated table.
+        S.stats.resolve_ms += ms_since(tp);
+        tp = clk::now();
         S.stats.truncations++;
-        break;
+        st = push_deltas(S, touched);
+        if (st == KBG_OK) {
+          G = grouper.build(bt.data() + i, (int32_t)bt.size() - i);
+          st = device_launch(S, G);
+        }
+        if (st == KBG_OK) st = device_wait(S, G);
+        if (st != KBG_OK) {
+          finish();
+          return st;
+        }
+        S.stats.device_ms += ms_since(tp);
+        tp = clk::now();
+        seg = i;
+        rs.stamp = ++stamp;  // the device table now holds every commit so far
+        rs.reset(G);
+        touched.clear();
+        r = rs.resolve(grouper.row_of[0], t, &node, &kind);  // a fresh list always decides its first task
       }
       if (r == RES_PANIC) {
         panic = true;
@@ -1572,7 +1594,7 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
   while (done < n && !stop) {
     const int32_t cnt = std::min(n - done, S.K);
     bt.assign(tasks + done, tasks + done + cnt);
-    const int32_t G = grouper.build(bt);
+    const int32_t G = grouper.build(bt.data(), cnt);
     kbg_status st = device_scan(S, G);
     if (st != KBG_OK) return st;
     touched.clear();
