@@ -245,7 +245,8 @@ typedef struct kbg_stats {
   int32_t n_classes;       /* static predicate classes on the device */
   int32_t shards;          /* node-axis shards of the session (1 = unsharded) */
   int32_t shard_index;     /* the shard this process holds; -1 = every shard is local */
-  int32_t reserved0;
+  int32_t int_scan;        /* 1 = the scan compares exact-integer thresholds (every value an
+                              integer <= 2^51); 0 = the reference's LessEqual expression */
   double exchange_ms;      /* summed HIP-event time of the per-batch RCCL all-gather */
   int32_t reserved[2];
 } kbg_stats;

@@ -34,11 +34,26 @@ struct NodeSoA {
 };
 
 // One task evaluation request (32 B, SURVEY §8(d) task record).
+// General mode: req = Resreq and the kernel evaluates LessEqual with the
+// reference's expression `r < a || |a - r| < min` per dimension.
+// Integer mode (the session proved every node value and request an exact
+// integer of magnitude <= 2^51, with the pending requests' sum <= 2^51 so the
+// values stay exact integers for the whole cycle): req = Resreq - min, and
+// `r <= a` is exactly `a > req`: if r < a then a > r - min; if |a - r| < min
+// then a - r > -min; conversely a > r - min gives r < a or r - min < a <= r,
+// i.e. |a - r| < min — every operation exact on such integers.
 struct TaskRec {
   double req[3];
   int32_t cls;
-  int32_t pad;
+  int32_t flags;  // kRowRelZeroFits: LessEqual(Resreq, 0) (the Releasing fit on a zero-Releasing node)
 };
+constexpr int32_t kRowRelZeroFits = 1;
+
+// Scan rows per workgroup (one per lane for the write-out). The host pads
+// every batch's rows to a multiple of this with copies of a real row, so the
+// kernel's row loop has no bound checks (kbg_pad_rows).
+constexpr int kScanRowsPerBlock = 64;
+inline int32_t kbg_pad_rows(int32_t g) { return (g + kScanRowsPerBlock - 1) / kScanRowsPerBlock * kScanRowsPerBlock; }
 
 // Node row written back after the host commits placements (AddTask delta).
 struct NodeDelta {
@@ -124,7 +139,7 @@ struct ScanGeom {
 // (hipExtLaunchKernelGGL), so their elapsed time is the kernel duration.
 // `out` points at the slot of chunk_lo.
 hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* class_mask, const TaskRec* tasks,
-                       int32_t n_tasks, int32_t cap_check, uint64_t* out, hipStream_t stream,
+                       int32_t n_tasks, int32_t cap_check, int32_t int_mode, uint64_t* out, hipStream_t stream,
                        hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
 // Row g gets cap_off[g+1]-cap_off[g] candidate slots at out_cand[cap_off[g]].

@@ -8,8 +8,8 @@
 //                       predicates.go:125-127)
 //                     && (Resreq.LessEqual(Idle) || Resreq.LessEqual(Releasing))
 //                     (resource_info.go:142-146). One wave = 64 consecutive
-//                     nodes held in registers; tasks are wave-uniform (scalar
-//                     loads); results leave as 64-bit ballots.
+//                     nodes held in registers; task rows are wave-uniform
+//                     (scalar loads); results leave as 64-bit ballots.
 // kbg_select_kernel — per task, the first M feasible node indices in
 //                     ssn.Nodes order (first-fit = min index), with
 //                     the Allocate/Pipeline kind of each.
@@ -19,6 +19,8 @@
 // fp64 is compared with the reference's own expression; the file is compiled
 // with -ffp-contract=off so nothing is fused.
 #include <hip/hip_ext.h>
+
+#include <utility>
 
 #include "kbg_device.hpp"
 
@@ -31,68 +33,97 @@ __device__ __forceinline__ bool le(double r, double a, double mn) {
 
 // ------------------------------------------------------------------ scan
 constexpr int kScanWaves = 4;          // waves per workgroup (256 threads)
-constexpr int kScanTasksPerBlock = 64; // task evaluations per workgroup
 
-// The row loop: lane = node, rows broadcast from LDS; REL_ZERO selects the
-// per-row precomputed Releasing fit (all nodes of the wave have Releasing 0).
-template <bool REL_ZERO>
-__device__ __forceinline__ void scan_rows(const double (*s_req)[4], const uint64_t* s_mask, int nt_blk, int lane,
-                                          int node_ok, double ic, double im, double ig, double rc, double rm,
-                                          double rg, uint64_t rz_rows, uint64_t* keep_f, uint64_t* keep_i) {
-  // Rows are processed 4 at a time with no remainder loop (ballots are
-  // convergent, so a runtime-count remainder would block unrolling); rows past
-  // nt_blk read stale LDS and their ballots are never stored.
-  for (int j0 = 0; j0 < nt_blk; j0 += 4) {
-#pragma unroll
-  for (int j = j0; j < j0 + 4; ++j) {
-    const double q0 = s_req[j][0];
-    const double q1 = s_req[j][1];
-    const double q2 = s_req[j][2];
-    const uint64_t mw = s_mask[j];
-    const int sbit = (int)((mw >> lane) & 1ull);
-    const int ifit = (int)le(q0, ic, kMinMilliCPU) & (int)le(q1, im, kMinMemory) & (int)le(q2, ig, kMinMilliGPU);
-    int rfit;
-    if (REL_ZERO) {
-      rfit = (int)((rz_rows >> j) & 1ull);
-    } else {
-      rfit = (int)le(q0, rc, kMinMilliCPU) & (int)le(q1, rm, kMinMemory) & (int)le(q2, rg, kMinMilliGPU);
-    }
-    const int ok = node_ok & sbit;
-    const uint64_t fm = __ballot((ok & (ifit | rfit)) != 0);
-    const uint64_t imk = __ballot((ok & ifit) != 0);
-    if (lane == j) {
-      *keep_f = fm;
-      *keep_i = imk;
-    }
-  }
-  }
+// Lane mask of the nodes of this wave on which a row's request fits
+// (Resource.LessEqual, one ballot per dimension, ANDed on the scalar unit).
+// INT_MODE: the row carries thr = req - min and every value is an exact
+// integer (kbg_device.hpp TaskRec), where `req <= a` is exactly `a > thr`.
+template <bool INT_MODE>
+__device__ __forceinline__ uint64_t fit_mask(double a0, double a1, double a2, double q0, double q1, double q2) {
+  if (INT_MODE) return __ballot(a0 > q0) & __ballot(a1 > q1) & __ballot(a2 > q2);
+  return __ballot(le(q0, a0, kMinMilliCPU)) & __ballot(le(q1, a1, kMinMemory)) & __ballot(le(q2, a2, kMinMilliGPU));
 }
 
+// One row J of the workgroup's 64: its request (q, read from LDS as a
+// same-address broadcast by the caller), its class-mask word for this wave's
+// 64 nodes from lane J (v_readlane); lane J keeps the row's two masks
+// (v_writelane_b32 with an inline-constant lane select: one scalar operand
+// per VALU op on gfx9).
+template <bool INT_MODE, bool REL_ZERO, int J>
+__device__ __forceinline__ void scan_row(double q0, double q1, double q2, uint64_t lane_mw, uint64_t rzm,
+                                         uint64_t okm, double ic, double im, double ig, double rc, double rm,
+                                         double rg, uint32_t (&keep)[4]) {
+  // (the builtin returns int: go through uint32_t so the low word is not sign-extended)
+  const uint32_t mw_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lane_mw, J);
+  const uint32_t mw_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lane_mw >> 32), J);
+  const uint64_t mw = (((uint64_t)mw_hi << 32) | (uint64_t)mw_lo) & okm;
+  const uint64_t mi = fit_mask<INT_MODE>(ic, im, ig, q0, q1, q2) & mw;
+  uint64_t mr;
+  if (REL_ZERO) mr = ((rzm >> J) & 1ull) ? mw : 0ull;  // LessEqual(req, 0) on every lane
+  else mr = fit_mask<INT_MODE>(rc, rm, rg, q0, q1, q2) & mw;
+  const uint64_t mf = mi | mr;
+  asm("v_writelane_b32 %0, %4, %8\n\t"
+      "v_writelane_b32 %1, %5, %8\n\t"
+      "v_writelane_b32 %2, %6, %8\n\t"
+      "v_writelane_b32 %3, %7, %8"
+      : "+v"(keep[0]), "+v"(keep[1]), "+v"(keep[2]), "+v"(keep[3])
+      : "s"((uint32_t)mf), "s"((uint32_t)(mf >> 32)), "s"((uint32_t)mi), "s"((uint32_t)(mi >> 32)), "i"(J));
+}
+
+// All ROWS rows of the workgroup, unrolled at compile time in groups of
+// kRowGroup whose LDS reads are issued together (one wave per SIMD is common
+// in production launches, so the LDS latency must overlap within the wave).
+// The host pads every batch to whole blocks with copies of a real row, so no
+// row needs a bound check.
+constexpr int kRowGroup = 8;
+#ifndef KBG_SMALL_BATCH_ROWS
+#define KBG_SMALL_BATCH_ROWS 1024
+#endif
+constexpr int kSmallBatchRows = KBG_SMALL_BATCH_ROWS;  // launch_scan: batches up to this many rows use 16-row workgroups
+template <bool INT_MODE, bool REL_ZERO, int ROWS, int J = 0>
+__device__ __forceinline__ void scan_rows(const double (*s_req)[3], uint64_t lane_mw, uint64_t rzm, uint64_t okm,
+                                          double ic, double im, double ig, double rc, double rm, double rg,
+                                          uint32_t (&keep)[4]) {
+  double q[kRowGroup][3];
+#pragma unroll
+  for (int u = 0; u < kRowGroup; ++u) {
+    q[u][0] = s_req[J + u][0];
+    q[u][1] = s_req[J + u][1];
+    q[u][2] = s_req[J + u][2];
+  }
+  [&]<int... U>(std::integer_sequence<int, U...>) {
+    (scan_row<INT_MODE, REL_ZERO, J + U>(q[U][0], q[U][1], q[U][2], lane_mw, rzm, okm, ic, im, ig, rc, rm, rg, keep),
+     ...);
+  }(std::make_integer_sequence<int, kRowGroup>{});
+  if constexpr (J + kRowGroup < ROWS)
+    scan_rows<INT_MODE, REL_ZERO, ROWS, J + kRowGroup>(s_req, lane_mw, rzm, okm, ic, im, ig, rc, rm, rg, keep);
+}
+
+template <bool INT_MODE, int ROWS>
 __global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, ScanGeom geo,
                                                        const uint64_t* __restrict__ class_mask,
                                                        const TaskRec* __restrict__ tasks, int32_t n_tasks,
                                                        int32_t cap_check, uint64_t* __restrict__ out) {
-  // Evaluation rows of this workgroup, staged once in LDS and read back as
-  // same-address broadcasts; per wave, the class-mask word of each row for
-  // the wave's 64-node chunk.
-  __shared__ double s_req[kScanTasksPerBlock][4];
-  __shared__ uint64_t s_mask[kScanWaves][kScanTasksPerBlock];
+  __shared__ double s_req[ROWS][3];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int rel = blockIdx.x * kScanWaves + wave;  // word relative to chunk_lo
   const int chunk = geo.chunk_lo + rel;            // global 64-node word
-  const bool live = rel < geo.n_chunks && chunk < geo.W;
-  const int t0 = blockIdx.y * kScanTasksPerBlock;
-  const int nt_blk = min(n_tasks - t0, kScanTasksPerBlock);
-  if (threadIdx.x < nt_blk) {
-    const TaskRec tr = tasks[t0 + threadIdx.x];
-    s_req[threadIdx.x][0] = tr.req[0];
-    s_req[threadIdx.x][1] = tr.req[1];
-    s_req[threadIdx.x][2] = tr.req[2];
+  const bool live = rel < geo.n_chunks && chunk < geo.W;  // words past W are never read
+  const int t0 = blockIdx.y * ROWS;
+  const int nt_blk = min(n_tasks - t0, ROWS);
+  // Rows are padded to whole kScanRowsPerBlock blocks: every lane j < ROWS
+  // has a real row t0 + j.
+  const TaskRec tr = tasks[t0 + (lane & (ROWS - 1))];
+  if (wave == 0 && lane < ROWS) {
+    s_req[lane][0] = tr.req[0];
+    s_req[lane][1] = tr.req[1];
+    s_req[lane][2] = tr.req[2];
   }
-  if (lane < nt_blk && live) s_mask[wave][lane] = class_mask[(size_t)tasks[t0 + lane].cls * geo.W + chunk];
+  const uint64_t lane_mw = live ? class_mask[(size_t)tr.cls * geo.W + chunk] : 0ull;  // row `lane`, this chunk
+  const uint64_t rzm = __ballot((tr.flags & kRowRelZeroFits) != 0);  // bits >= ROWS are never read
   __syncthreads();
-  if (!live) return;  // wave-uniform exit (after the barrier); words past W are never read
+  if (!live) return;  // wave-uniform, after the barrier
   const int node = chunk * 64 + lane;
   const bool valid = node < geo.n_nodes;
   const int row = node - geo.tab_lo;
@@ -108,42 +139,49 @@ __global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, ScanGeom geo,
     nt = nd.ntasks[row];
     mt = nd.maxtasks[row];
   }
-  const int node_ok = (int)valid & ((int)!cap_check | (int)(nt < mt));
-  // Releasing is usually zero on every node of the wave; then the Releasing
-  // fit of a row is LessEqual(req, 0) for every lane — the same expression,
-  // evaluated once per row (lane j for row j) instead of once per node.
+  const uint64_t okm = __ballot(valid && (!cap_check || nt < mt));  // predicates.go:125-127 pod cap
+  // Releasing is usually zero on every node of the wave; then a row's
+  // Releasing fit is LessEqual(req, 0) on every lane, precomputed per row.
   const bool rel_zero_wave = __ballot(!(rc == 0.0 && rm == 0.0 && rg == 0.0)) == 0ull;
-  uint64_t rz_rows = 0;
-  if (rel_zero_wave) {
-    bool rz = false;
-    if (lane < nt_blk) {
-      const double q0 = s_req[lane][0], q1 = s_req[lane][1], q2 = s_req[lane][2];
-      rz = ((int)le(q0, 0.0, kMinMilliCPU) & (int)le(q1, 0.0, kMinMemory) & (int)le(q2, 0.0, kMinMilliGPU)) != 0;
-    }
-    rz_rows = __ballot(rz);
-  }
-  uint64_t keep_f = 0, keep_i = 0;  // lane j keeps the ballots of row t0+j
+  uint32_t keep[4] = {0u, 0u, 0u, 0u};  // lane j: (feasible, idle-fit) masks of row t0+j
   if (rel_zero_wave)
-    scan_rows<true>(s_req, s_mask[wave], nt_blk, lane, node_ok, ic, im, ig, rc, rm, rg, rz_rows, &keep_f, &keep_i);
+    scan_rows<INT_MODE, true, ROWS>(s_req, lane_mw, rzm, okm, ic, im, ig, rc, rm, rg, keep);
   else
-    scan_rows<false>(s_req, s_mask[wave], nt_blk, lane, node_ok, ic, im, ig, rc, rm, rg, rz_rows, &keep_f, &keep_i);
+    scan_rows<INT_MODE, false, ROWS>(s_req, lane_mw, rzm, okm, ic, im, ig, rc, rm, rg, keep);
   if (lane < nt_blk) {
     // [slot][plane][row][Wl] (kbg_device.hpp ScanGeom)
     const int slot = rel / geo.Wl, w = rel - slot * geo.Wl;
     const size_t plane = (size_t)n_tasks * geo.Wl;
     uint64_t* o = out + (size_t)slot * 2 * plane + (size_t)(t0 + lane) * geo.Wl + w;
-    o[0] = keep_f;
-    o[plane] = keep_i;
+    o[0] = (uint64_t)keep[0] | ((uint64_t)keep[1] << 32);
+    o[plane] = (uint64_t)keep[2] | ((uint64_t)keep[3] << 32);
   }
 }
 
 hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* class_mask, const TaskRec* tasks,
-                       int32_t n_tasks, int32_t cap_check, uint64_t* out, hipStream_t stream, hipEvent_t start,
-                       hipEvent_t stop) {
+                       int32_t n_tasks, int32_t cap_check, int32_t int_mode, uint64_t* out, hipStream_t stream,
+                       hipEvent_t start, hipEvent_t stop) {
   if (n_tasks <= 0 || g.n_chunks <= 0) return hipSuccess;
-  dim3 grid((g.n_chunks + kScanWaves - 1) / kScanWaves, (n_tasks + kScanTasksPerBlock - 1) / kScanTasksPerBlock);
-  hipExtLaunchKernelGGL(kbg_scan_kernel, grid, dim3(64 * kScanWaves), 0, stream, start, stop, 0, n, g, class_mask,
-                        tasks, n_tasks, cap_check, out);
+  // Rows per workgroup: a wave's rows run back to back, so short batches
+  // (grouped mode: tens of rows) get more, shorter waves.
+  const int rows = (n_tasks <= kSmallBatchRows) ? 16 : 64;
+  dim3 grid((g.n_chunks + kScanWaves - 1) / kScanWaves, (n_tasks + rows - 1) / rows);
+  dim3 block(64 * kScanWaves);
+  if (int_mode) {
+    if (rows == 16)
+      hipExtLaunchKernelGGL((kbg_scan_kernel<true, 16>), grid, block, 0, stream, start, stop, 0, n, g, class_mask, tasks,
+                            n_tasks, cap_check, out);
+    else
+      hipExtLaunchKernelGGL((kbg_scan_kernel<true, 64>), grid, block, 0, stream, start, stop, 0, n, g, class_mask, tasks,
+                            n_tasks, cap_check, out);
+  } else {
+    if (rows == 16)
+      hipExtLaunchKernelGGL((kbg_scan_kernel<false, 16>), grid, block, 0, stream, start, stop, 0, n, g, class_mask,
+                            tasks, n_tasks, cap_check, out);
+    else
+      hipExtLaunchKernelGGL((kbg_scan_kernel<false, 64>), grid, block, 0, stream, start, stop, 0, n, g, class_mask,
+                            tasks, n_tasks, cap_check, out);
+  }
   return hipGetLastError();
 }
 

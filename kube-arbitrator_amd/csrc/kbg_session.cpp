@@ -478,9 +478,10 @@ kbg_status upload_nodes(Session& S) {
 // given cap_off[g+1]-cap_off[g] candidate slots. Fills S.h_cand / S.h_count.
 kbg_status device_launch(Session& S, int32_t G) {
   const uint32_t total = S.h_capoff[G];
-  const size_t up_bytes = (size_t)G * sizeof(kbg::TaskRec) + (size_t)(G + 1) * 4;
+  const int32_t Gp = kbg::kbg_pad_rows(G);  // Grouper::build padded the rows
+  const size_t up_bytes = (size_t)Gp * sizeof(kbg::TaskRec) + (size_t)(G + 1) * 4;
   const kbg::TaskRec* d_tasks = (const kbg::TaskRec*)S.d_up;
-  const uint32_t* d_capoff = (const uint32_t*)(S.d_up + (size_t)G * sizeof(kbg::TaskRec));
+  const uint32_t* d_capoff = (const uint32_t*)(S.d_up + (size_t)Gp * sizeof(kbg::TaskRec));
   HIP_TRY(hipMemcpyAsync(S.d_up, S.h_up, up_bytes, hipMemcpyHostToDevice, S.stream));
   // this process scans its shard (or every shard when they are all local)
   kbg::ScanGeom geo{S.n_nodes, S.W, S.Wl, 0, S.R * S.Wl, S.tab_lo};
@@ -491,8 +492,8 @@ kbg_status device_launch(Session& S, int32_t G) {
     geo.n_chunks = S.Wl;
     out = S.d_bits + (size_t)S.shard * slot_words;
   }
-  HIP_TRY(kbg::launch_scan(S.d_nodes, geo, S.d_class_mask, d_tasks, G, S.pred_active ? 1 : 0, out, S.stream, S.ev[0],
-                           S.ev[1]));
+  HIP_TRY(kbg::launch_scan(S.d_nodes, geo, S.d_class_mask, d_tasks, G, S.pred_active ? 1 : 0, S.int_mode ? 1 : 0, out,
+                           S.stream, S.ev[0], S.ev[1]));
   if (S.comm) {  // in-place all-gather: every rank receives every shard's slot, in rank (= node) order
     HIP_TRY(hipEventRecord(S.ev[4], S.stream));
     const ncclResult_t nr = ncclAllGather(out, S.d_bits, slot_words, ncclUint64, S.comm->nccl, S.stream);
@@ -584,16 +585,25 @@ struct Grouper {
         shape_stamp[sh] = stamp;
         shape_row[sh] = g;
         kbg::TaskRec& r = S.h_tasks[g];
-        r.req[0] = S.treq[t].c;
-        r.req[1] = S.treq[t].m;
-        r.req[2] = S.treq[t].g;
+        const Res& q = S.treq[t];
+        if (S.int_mode) {  // thresholds: LessEqual(q, a) == (a > q - min), exact (kbg_device.hpp)
+          r.req[0] = q.c - kbg::kMinMilliCPU;
+          r.req[1] = q.m - kbg::kMinMemory;
+          r.req[2] = q.g - kbg::kMinMilliGPU;
+        } else {
+          r.req[0] = q.c;
+          r.req[1] = q.m;
+          r.req[2] = q.g;
+        }
         r.cls = S.task_class[t];
-        r.pad = 0;
+        r.flags = kbg::res_le(q, Res{}) ? kbg::kRowRelZeroFits : 0;
       }
       row_of[i] = g;
       count[g]++;
     }
-    S.h_capoff = (uint32_t*)(S.h_up + (size_t)G * sizeof(kbg::TaskRec));
+    const int32_t Gp = kbg::kbg_pad_rows(G);
+    for (int32_t g = G; g < Gp; ++g) S.h_tasks[g] = S.h_tasks[0];  // padding rows: scanned, never stored
+    S.h_capoff = (uint32_t*)(S.h_up + (size_t)Gp * sizeof(kbg::TaskRec));
     S.h_capoff[0] = 0;
     for (int32_t g = 0; g < G; ++g) {
       const uint32_t want = S.opts.full_scan ? (uint32_t)S.M : (uint32_t)std::min(count[g] + kGroupSlack, 4096);
@@ -1003,6 +1013,27 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   compile_static_predicates(S, &sh);
   S.n_classes = sh.n_classes;
   S.W = (N + 63) / 64;
+  // ---- integer scan mode (kbg_device.hpp TaskRec): every value the scan
+  // compares is an exact integer and stays one through the cycle
+  {
+    constexpr double kLim = 2251799813685248.0;  // 2^51
+    auto exact = [&](double v) { return std::isfinite(v) && std::fabs(v) <= kLim && v == std::floor(v); };
+    bool ok = true;
+    for (int32_t n = 0; n < N && ok; ++n)
+      ok = exact(S.idle[n].c) && exact(S.idle[n].m) && exact(S.idle[n].g) && exact(S.rel[n].c) &&
+           exact(S.rel[n].m) && exact(S.rel[n].g);
+    double sum_c = 0, sum_m = 0, sum_g = 0;
+    for (int32_t t = 0; t < S.n_tasks && ok; ++t) {
+      if (!S.pending_candidate[t]) continue;
+      const Res& q = S.treq[t];
+      ok = exact(q.c) && exact(q.m) && exact(q.g) && q.c >= 0 && q.m >= 0 && q.g >= 0;
+      sum_c += q.c;
+      sum_m += q.m;
+      sum_g += q.g;
+    }
+    S.int_mode = ok && sum_c <= kLim && sum_m <= kLim && sum_g <= kLim &&
+                 getenv("KBG_FORCE_GENERAL_SCAN") == nullptr;
+  }
   // ---- node-axis shards: contiguous 64-node word ranges, so
   // rank order is node order and first-fit survives the split
   S.comm = comm;
@@ -1043,7 +1074,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   HIP_TRY(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   for (auto& e : S.ev) HIP_TRY(hipEventCreate(&e));
   if ((st = alloc_soa(S, &S.d_nodes)) || (st = alloc_soa(S, &S.d_nodes0))) return st;
-  const size_t up_cap = (size_t)S.K * sizeof(kbg::TaskRec) + ((size_t)S.K + 1) * 4;
+  const size_t up_cap = (size_t)kbg::kbg_pad_rows(S.K) * sizeof(kbg::TaskRec) + ((size_t)S.K + 1) * 4;
   const size_t down_cap = (size_t)S.K + (size_t)S.cand_cap;
   if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) || (st = dalloc(S, &S.d_up, up_cap)) ||
       (st = dalloc(S, &S.d_bits, (size_t)S.R * 2 * S.K * S.Wl)) ||
@@ -1092,6 +1123,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.stats.n_classes = S.n_classes;
   S.stats.shards = S.R;
   S.stats.shard_index = S.comm ? S.shard : -1;
+  S.stats.int_scan = S.int_mode ? 1 : 0;
   S.stats.open_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_open).count();
   return KBG_OK;
 }
@@ -1203,6 +1235,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   S.stats.n_classes = prev.n_classes;
   S.stats.shards = prev.shards;
   S.stats.shard_index = prev.shard_index;
+  S.stats.int_scan = prev.int_scan;
   S.stats.open_ms = prev.open_ms;
 
   std::vector<kbg_decision> dec;

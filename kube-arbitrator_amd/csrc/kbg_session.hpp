@@ -147,6 +147,7 @@ struct Session {
   int32_t device = 0;
   hipStream_t stream = nullptr;
   int32_t W = 0;            // u64 words per node bitmap row
+  bool int_mode = false;    // scan rows carry integer thresholds (kbg_device.hpp TaskRec)
   // node-axis sharding: R shards of Wl words; this process holds
   // shard `shard` (comm != null) or every shard (shard = -1)
   int32_t R = 1, Wl = 0, shard = -1;

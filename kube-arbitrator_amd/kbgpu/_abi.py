@@ -146,7 +146,7 @@ class kbg_stats(ctypes.Structure):
                 ("truncations", i64), ("scan_launches", i64), ("scan_kernel_ms", f64), ("select_kernel_ms", f64),
                 ("allocate_ms", f64), ("open_ms", f64), ("engine_ms", f64), ("resolve_ms", f64),
                 ("device_ms", f64), ("delta_ms", f64), ("replayed", i64), ("n_classes", i32), ("shards", i32), ("shard_index", i32),
-                ("reserved0", i32), ("exchange_ms", f64), ("reserved", i32 * 2)]
+                ("int_scan", i32), ("exchange_ms", f64), ("reserved", i32 * 2)]
 
 
 # Every symbol include/kbgpu.h declares, with its ctypes signature.

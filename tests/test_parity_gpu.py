@@ -207,3 +207,35 @@ def test_apply_matches_node_accounting():
         assert st.num_tasks == nref["ntasks"]
     # the device table must agree with the host mirror: every further task now fits nowhere it should not
     ssn.close()
+
+
+@pytest.fixture
+def general_scan(monkeypatch):
+    """Sessions opened under this fixture use the reference's LessEqual
+    expression on the device instead of integer thresholds."""
+    monkeypatch.setenv("KBG_FORCE_GENERAL_SCAN", "1")
+
+
+@pytest.mark.parametrize("cid", [1, 2])
+def test_general_scan_config_parity(cid, general_scan):
+    fx = synth.config_fixture(cid)
+    got, ssn = run_fixture(fx)
+    assert ssn.stats().int_scan == 0
+    compare_outputs(run_oracle(fx), got)
+    ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 100, 3))
+def test_general_scan_fuzz_parity(seed, general_scan):
+    fx = synth.random_fixture(seed)
+    got, ssn = run_fixture(fx, {"batch_tasks": 1 + seed % 9, "candidates": 1 + seed % 5, "full_scan": seed % 2})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
+def test_int_scan_is_the_default_on_integer_sessions():
+    fx = synth.config_fixture(2)
+    got, ssn = run_fixture(fx)
+    assert ssn.stats().int_scan == 1
+    ssn.close()
