@@ -61,15 +61,17 @@ def cpu_baseline(fx, budget_note):
                       f"{out['stats']['predicate_calls']} predicate calls), kbref C++ port, 1 thread"}
 
 
-def load_pmc_traffic(n_nodes):
-    """Per-launch HBM bytes of the scan kernel from the committed PMC profile, if any."""
+def load_pmc_traffic(n_nodes, mode):
+    """Per-launch HBM bytes (read + write) of the scan kernel in `mode`
+    ("full_scan" / "grouped") from the committed rocprofv3 PMC summary of this
+    same bench command (profiles/pmc_scan.json), if it matches the workload."""
     p = os.path.join(ROOT, "profiles", "pmc_scan.json")
     if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
         if d.get("n_nodes") == n_nodes:
-            return d.get("hbm_bytes_per_launch")
+            return (d.get(mode) or {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
     return None
@@ -158,12 +160,12 @@ def main():
         ssn.close()
         return agg
 
-    def roofline(agg):
+    def roofline(agg, mode):
         # per rank: every evaluation row streams this shard's node records (N/R x 64 B) + its 32 B task record
         algo = agg["visits"] * NODE_RECORD_B + agg["evals"] * TASK_RECORD_B
         ach = algo / (agg["scan_ms"] * 1e-3) / 1e9 if agg["scan_ms"] > 0 else 0.0
         return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                "traffic": load_pmc_traffic(agg["n_nodes"]) if comm is None else None, "kernel": "kbg_scan_kernel",
+                "traffic": load_pmc_traffic(agg["n_nodes"], mode) if comm is None else None, "kernel": "kbg_scan_kernel",
                 "avg_launch_us": agg["scan_ms"] * 1e3 / max(1, agg["launches"]),
                 "algo_bytes_per_launch": algo / max(1, agg["launches"]),
                 "evaluations_per_launch": agg["evals"] / max(1, agg["launches"])}
@@ -204,12 +206,12 @@ def main():
                    "parallelism": f"node-axis shards x{world} (RCCL all-gather)" if world > 1 else "single-gpu",
                    "batch_tasks": base_opts.get("batch_tasks", 8192),
                    "candidates": base_opts.get("candidates", 32)},
-        "roofline": roofline(full),
+        "roofline": roofline(full, "full_scan"),
         "roofline_note": "scan kernel in full-scan mode (every task evaluation scans all N nodes, SURVEY 8d rule); "
                          "the production mode groups identical (class, request) shapes per batch",
         "full_scan_mode": {"placements_per_s": full["decisions"] / full["elapsed"],
                            "p50_cycle_ms": statistics.median(full["cycle_ms"]), "breakdown": breakdown(full)},
-        "production_mode": {"roofline": roofline(prod), "breakdown": breakdown(prod)},
+        "production_mode": {"roofline": roofline(prod, "grouped"), "breakdown": breakdown(prod)},
         "decisions_per_cycle": decisions // max(1, args.steps),
         "open_ms": st.open_ms,
     }
