@@ -248,7 +248,7 @@ typedef struct kbg_stats {
   int32_t int_scan;        /* 1 = the scan compares exact-integer thresholds (every value an
                               integer <= 2^51); 0 = the reference's LessEqual expression */
   double exchange_ms;      /* summed HIP-event time of the per-batch RCCL all-gather */
-  int32_t reserved[2];
+  double backfill_ms;      /* wall time of the last kbg_backfill */
 } kbg_stats;
 
 typedef struct kbg_session kbg_session;
@@ -291,6 +291,16 @@ kbg_status kbg_session_open_sharded(const kbg_snapshot* snap, const kbg_options*
 /* allocateAction.Execute (allocate.go:41-176). Writes at most `cap` decisions.
  * Can be called once per opened or reset session. */
 kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out);
+
+/* backfillAction.Execute (backfill.go:40-71), run after kbg_allocate on the
+ * same cycle (the reference's default conf runs "allocate, backfill",
+ * util.go:30-40) or alone: every Pending task requesting nothing (BestEffort)
+ * of every job, in ssn.Jobs and status-index order, goes to the first node
+ * whose PredicateFn passes (static predicate + pod cap, no resource fit)
+ * through ssn.Allocate — so it counts toward gang readiness and may dispatch
+ * earlier Allocate decisions of its job. Writes the cycle's whole decision
+ * log (allocate's decisions first, dispatched_at updated) to `out`. */
+kbg_status kbg_backfill(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out);
 
 /* Restores the state captured at kbg_session_open (device-side copy); used to
  * re-run a cycle on the same snapshot without re-uploading it. */

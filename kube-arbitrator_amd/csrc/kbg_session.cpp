@@ -586,7 +586,9 @@ struct Grouper {
         shape_row[sh] = g;
         kbg::TaskRec& r = S.h_tasks[g];
         const Res& q = S.treq[t];
-        if (S.int_mode) {  // thresholds: LessEqual(q, a) == (a > q - min), exact (kbg_device.hpp)
+        if (S.be_task[t]) {  // backfill: PredicateFn only — every node fits (a > -inf in both modes)
+          r.req[0] = r.req[1] = r.req[2] = -INFINITY;
+        } else if (S.int_mode) {  // thresholds: LessEqual(q, a) == (a > q - min), exact (kbg_device.hpp)
           r.req[0] = q.c - kbg::kMinMilliCPU;
           r.req[1] = q.m - kbg::kMinMemory;
           r.req[2] = q.g - kbg::kMinMilliGPU;
@@ -596,7 +598,7 @@ struct Grouper {
           r.req[2] = q.g;
         }
         r.cls = S.task_class[t];
-        r.flags = kbg::res_le(q, Res{}) ? kbg::kRowRelZeroFits : 0;
+        r.flags = (S.be_task[t] || kbg::res_le(q, Res{})) ? kbg::kRowRelZeroFits : 0;
       }
       row_of[i] = g;
       count[g]++;
@@ -638,6 +640,11 @@ struct Resolver {
       }
       // touched by an earlier commit of this batch: re-check on the host mirror
       if (S.pred_active && S.ntasks[nd] >= S.maxtasks[nd]) continue;
+      if (S.be_task[t]) {  // backfill: PredicateFn only, always ssn.Allocate
+        *node = nd;
+        *kind = KBG_KIND_ALLOCATE;
+        return RES_OK;
+      }
       if (kbg::res_le(r, S.idle[nd])) {
         *node = nd;
         *kind = KBG_KIND_ALLOCATE;
@@ -842,10 +849,12 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   }
   S.treq.resize(S.n_tasks);
   S.pending_candidate.assign(S.n_tasks, 0);
+  S.be_task.assign(S.n_tasks, 0);
   for (int32_t t = 0; t < S.n_tasks; ++t) {
     S.treq[t] = to_res(S.tasks_in[t].resreq);
     // allocate.go:88-96: only Pending, non-BestEffort tasks enter the node loop
     S.pending_candidate[t] = S.tasks_in[t].status == KBG_PENDING && !kbg::res_empty(S.treq[t]);
+    S.be_task[t] = S.tasks_in[t].status == KBG_PENDING && kbg::res_empty(S.treq[t]);
   }
   S.task_job.resize(S.n_tasks);
   for (int32_t t = 0; t < S.n_tasks; ++t) S.task_job[t] = S.tasks_in[t].job;
@@ -887,6 +896,12 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
 
   std::vector<std::vector<int32_t>> job_tasks(S.n_jobs);
   for (int32_t t = 0; t < S.n_tasks; ++t) job_tasks[S.tasks_in[t].job].push_back(t);
+  S.jt_off.assign(S.n_jobs + 1, 0);
+  S.jt.clear();
+  for (int32_t j = 0; j < S.n_jobs; ++j) {
+    S.jt.insert(S.jt.end(), job_tasks[j].begin(), job_tasks[j].end());
+    S.jt_off[j + 1] = (int32_t)S.jt.size();
+  }
   for (int32_t j = 0; j < S.n_jobs; ++j)
     for (int32_t t : job_tasks[j])
       if (ready_status(S.tasks_in[t].status)) E.jready[j]++;
@@ -1062,6 +1077,14 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
       S.task_shape[t] = it.first->second;
     }
     S.n_shapes = (int32_t)ids.size();
+    // backfill rows: one grouping id per class (the request does not matter)
+    S.be_shape.assign(std::max(1, S.n_classes), -1);
+    for (int32_t t = 0; t < S.n_tasks; ++t) {
+      if (!S.be_task[t]) continue;
+      int32_t& b = S.be_shape[S.task_class[t]];
+      if (b < 0) b = S.n_shapes++;
+      S.task_shape[t] = b;
+    }
   }
 
   // ---- device
@@ -1225,8 +1248,54 @@ void compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, const 
   }
 }
 
+// State of a cycle's first action: the decision log, gang dispatch lists,
+// committed readiness and the plugin state start from the session snapshot.
+void begin_cycle(Session& S) {
+  S.dec.clear();
+  S.dec.reserve(S.pend.size());
+  S.undisp_head.assign(S.n_jobs, -1);
+  S.undisp_next.clear();
+  S.undisp_next.reserve(S.pend.size());
+  S.committed_ready = S.job_ready0;
+  S.fin = S.init;
+  S.fit.assign(S.n_jobs, Session::FitCounts{});
+  S.cycle_started = true;
+}
+
+// Appends one committed decision to the log and runs the gang part of
+// ssn.Allocate (session.go:283-290): every Allocated task of the job is
+// dispatched when this decision makes the job ready. Pipelined tasks count
+// toward readiness (gang.go:44-55) but never dispatch.
+void record_decision(Session& S, int32_t t, int32_t node, int32_t kind) {
+  const int32_t j = S.task_job[t];
+  const int32_t di = (int32_t)S.dec.size();
+  S.dec.push_back(kbg_decision{t, node, kind, -1});
+  S.undisp_next.push_back(-1);
+  S.committed_ready[j]++;
+  if (kind == KBG_KIND_ALLOCATE) {
+    S.undisp_next[di] = S.undisp_head[j];
+    S.undisp_head[j] = di;
+    if (!S.ready_gang || S.committed_ready[j] >= S.jobs_in[j].min_available) {
+      for (int32_t d = S.undisp_head[j]; d >= 0; d = S.undisp_next[d]) S.dec[d].dispatched_at = di;
+      S.undisp_head[j] = -1;
+    }
+  }
+}
+
+kbg_status copy_log(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out, kbg_status result) {
+  if (n_out) *n_out = (int32_t)S.dec.size();
+  if ((int32_t)S.dec.size() > cap || (!out && !S.dec.empty())) {
+    if (result == KBG_OK) result = fail(KBG_E_CAPACITY, "decision buffer too small: need " + std::to_string(S.dec.size()));
+    return result;
+  }
+  if (!S.dec.empty()) std::memcpy(out, S.dec.data(), S.dec.size() * sizeof(kbg_decision));
+  return result;
+}
+
 kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
-  if (S.allocated) return fail(KBG_E_INVALID, "kbg_allocate already ran on this session; call kbg_session_reset");
+  if (S.cycle_started)
+    return fail(KBG_E_INVALID, "an action already ran on this session (allocate runs first); call kbg_session_reset");
+  begin_cycle(S);
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   const auto t0 = clk::now();
@@ -1238,16 +1307,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   S.stats.int_scan = prev.int_scan;
   S.stats.open_ms = prev.open_ms;
 
-  std::vector<kbg_decision> dec;
+  std::vector<kbg_decision>& dec = S.dec;
   std::vector<Res> dec_old;  // the Idle (Allocate) or Releasing (Pipeline) row before each decision
-  dec.reserve(S.pend.size());
   dec_old.reserve(S.pend.size());
   std::vector<LastEval> last(S.n_jobs);
-  // Allocate decisions of a job not yet dispatched (gang short of MinAvailable):
-  // a per-job list threaded through decision indices
-  std::vector<int32_t> undisp_head(S.n_jobs, -1), undisp_next;
-  undisp_next.reserve(S.pend.size());
-  S.committed_ready = S.job_ready0;
   // shapes known to fit nowhere (monotone): written by the committer, read by the predictor
   std::unique_ptr<std::atomic<uint8_t>[]> failed(new std::atomic<uint8_t>[std::max(1, S.n_shapes)]);
   for (int32_t i = 0; i < S.n_shapes; ++i) failed[i].store(0, std::memory_order_relaxed);
@@ -1257,9 +1320,6 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   kbg_status result = KBG_OK;
   Grouper grouper(S);
   Resolver rs{S, mark, 0, {}};
-  auto job_ready_committed = [&](int32_t j) {
-    return !S.ready_gang || S.committed_ready[j] >= S.jobs_in[j].min_available;
-  };
 
   // ------------------------------------------------------------ predictor
   Pipe P;
@@ -1435,18 +1495,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
           mark[node] = stamp;
           touched.push_back(node);
         }
-        const int32_t di = (int32_t)dec.size();
-        dec.push_back(kbg_decision{t, node, kind, -1});
-        undisp_next.push_back(-1);
-        S.committed_ready[j]++;
-        if (kind == KBG_KIND_ALLOCATE) {  // session.go:283-290
-          undisp_next[di] = undisp_head[j];
-          undisp_head[j] = di;
-          if (job_ready_committed(j)) {
-            for (int32_t d = undisp_head[j]; d >= 0; d = undisp_next[d]) dec[d].dispatched_at = di;
-            undisp_head[j] = -1;
-          }
-        }
+        record_decision(S, t, node, kind);
       } else {
         failed[S.task_shape[t]].store(1, std::memory_order_relaxed);
       }
@@ -1494,13 +1543,98 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
             (double)eprof.jtop / eprof.steps, (double)eprof.qpush / eprof.steps, engine_ms);
   S.allocated = true;
   S.stats.allocate_ms = ms_since(t0);
-  if (n_out) *n_out = (int32_t)dec.size();
-  if ((int32_t)dec.size() > cap || (!out && !dec.empty())) {
-    if (result == KBG_OK) result = fail(KBG_E_CAPACITY, "decision buffer too small: need " + std::to_string(dec.size()));
-    return result;
+  return copy_log(S, out, cap, n_out, result);
+}
+
+// backfillAction.Execute (backfill.go:40-71). The order of the BestEffort
+// tasks is fixed (ssn.Jobs, then each job's status index) and does not depend
+// on outcomes, and a node only loses feasibility (its pod count grows), so
+// the whole list is scanned in batches of K against the batch-start table and
+// resolved in order exactly like allocate's rows, with no prediction.
+kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
+  using clk = std::chrono::steady_clock;
+  if (S.backfilled) return fail(KBG_E_INVALID, "kbg_backfill already ran on this session; call kbg_session_reset");
+  if (S.pred_active)
+    for (int32_t t = 0; t < S.n_tasks; ++t) {
+      const int32_t sp = S.tasks_in[t].spec;
+      if (S.be_task[t] && sp >= 0 && S.specs_in[sp].has_host_ports)
+        return fail(KBG_E_UNSUPPORTED, "BestEffort pending task declares hostPort: run the reference predicate path");
+    }
+  const auto t0 = clk::now();
+  if (!S.cycle_started) begin_cycle(S);
+  S.backfilled = true;
+  std::vector<int32_t> be;
+  for (int32_t j = 0; j < S.n_jobs; ++j)
+    for (int32_t k = S.jt_off[j]; k < S.jt_off[j + 1]; ++k)
+      if (S.be_task[S.jt[k]]) be.push_back(S.jt[k]);
+  std::vector<int32_t> mark(S.n_nodes, -1), touched;
+  int32_t stamp = 0;
+  Grouper grouper(S);
+  Resolver rs{S, mark, 0, {}};
+  kbg_status result = KBG_OK, st = KBG_OK;
+  Engine& E = S.fin;
+  for (size_t done = 0; done < be.size() && result == KBG_OK;) {
+    const int32_t cnt = (int32_t)std::min<size_t>(be.size() - done, (size_t)S.K);
+    const int32_t* bt = be.data() + done;
+    int32_t G = grouper.build(bt, cnt);
+    if ((st = device_scan(S, G)) != KBG_OK) return st;
+    rs.stamp = ++stamp;
+    rs.reset(G);
+    touched.clear();
+    int32_t seg = 0;
+    for (int32_t i = 0; i < cnt; ++i) {
+      const int32_t t = bt[i];
+      int32_t node = -1, kind = 0;
+      int r = rs.resolve(grouper.row_of[i - seg], t, &node, &kind);
+      if (r == RES_TRUNC) {  // list exhausted: write back, rescan the rest of the batch
+        S.stats.truncations++;
+        if ((st = push_deltas(S, touched)) != KBG_OK) return st;
+        G = grouper.build(bt + i, cnt - i);
+        if ((st = device_scan(S, G)) != KBG_OK) return st;
+        seg = i;
+        rs.stamp = ++stamp;
+        rs.reset(G);
+        touched.clear();
+        r = rs.resolve(grouper.row_of[0], t, &node, &kind);
+      }
+      if (r == RES_PANIC) {
+        result = fail(KBG_E_REF_PANIC, "backfill reached a node whose NodeInfo.Node is nil with the predicates plugin on "
+                                       "(predicates.go:122-123)");
+        break;
+      }
+      if (node < 0) continue;  // no node passes the predicates: the task stays Pending
+      // ssn.Allocate -> NodeInfo.AddTask -> Idle.Sub panics when even the
+      // tolerance does not cover the request (resource_info.go:100-110)
+      if (!S.nil_node[node] && !kbg::res_le(S.treq[t], S.idle[node])) {
+        result = fail(KBG_E_REF_PANIC, "backfill: Resource.Sub underflow on the node's Idle (resource_info.go:100-110)");
+        break;
+      }
+      mirror_add(S, t, node, KBG_KIND_ALLOCATE);
+      if (mark[node] != stamp) {
+        mark[node] = stamp;
+        touched.push_back(node);
+      }
+      // drf / proportion AllocateFunc (drf.go:130-139, proportion.go:196-206)
+      const int32_t j = S.task_job[t];
+      const Res& q = S.treq[t];
+      if (S.has_drf) {
+        kbg::res_add(E.jalloc[j], q);
+        E.jshare[j] = share_of(E.jalloc[j], S.drf_total);
+      }
+      if (S.has_prop) {
+        const int32_t jq = S.job_queue[j];
+        kbg::res_add(E.qalloc[jq], q);
+        E.qshare[jq] = share_of(E.qalloc[jq], S.q_deserved[jq]);
+      }
+      E.jready[j]++;
+      record_decision(S, t, node, KBG_KIND_ALLOCATE);
+    }
+    if ((st = push_deltas(S, touched)) != KBG_OK) return st;
+    done += cnt;
   }
-  if (!dec.empty()) std::memcpy(out, dec.data(), dec.size() * sizeof(kbg_decision));
-  return result;
+  HIP_TRY(hipStreamSynchronize(S.stream));
+  S.stats.backfill_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  return copy_log(S, out, cap, n_out, result);
 }
 
 }  // namespace
@@ -1597,6 +1731,16 @@ kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t*
   }
 }
 
+kbg_status kbg_backfill(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out) {
+  if (!s) return fail(KBG_E_INVALID, "null session");
+  HIP_TRY(hipSetDevice(s->s.device));
+  try {
+    return backfill_cycle(s->s, out, cap, n_out);
+  } catch (const std::bad_alloc&) {
+    return fail(KBG_E_NOMEM, "host allocation failed");
+  }
+}
+
 kbg_status kbg_session_reset(kbg_session* s) {
   if (!s) return fail(KBG_E_INVALID, "null session");
   Session& S = s->s;
@@ -1604,7 +1748,7 @@ kbg_status kbg_session_reset(kbg_session* s) {
   S.idle = S.idle0;
   S.rel = S.rel0;
   S.ntasks = S.ntasks0;
-  S.allocated = false;
+  S.allocated = S.backfilled = S.cycle_started = false;
   kbg_status st = copy_soa(S, S.d_nodes, S.d_nodes0);
   if (st != KBG_OK) return st;
   HIP_TRY(hipStreamSynchronize(S.stream));
@@ -1688,13 +1832,15 @@ kbg_status kbg_job_state_get(kbg_session* s, int32_t job, kbg_job_state* out) {
   if (!s || !out) return fail(KBG_E_INVALID, "null argument");
   Session& S = s->s;
   if (job < 0 || job >= S.n_jobs) return fail(KBG_E_INVALID, "job index");
-  const Engine& E = S.allocated ? S.fin : S.init;
-  out->ready_num = S.allocated ? S.committed_ready[job] : S.job_ready0[job];
+  const Engine& E = S.cycle_started ? S.fin : S.init;
+  out->ready_num = S.cycle_started ? S.committed_ready[job] : S.job_ready0[job];
   out->ready = out->ready_num >= S.jobs_in[job].min_available ? 1 : 0;  // gang jobReady (gang.go:72-78)
   out->drf_share = S.has_drf ? E.jshare[job] : 0.0;
   out->drf_allocated = to_kres(E.jalloc[job]);
   out->fit_valid = out->fit_nodes = out->fit_cpu = out->fit_memory = out->fit_gpu = 0;
-  if (S.allocated && (size_t)job < S.fit.size() && S.fit[job].valid) {
+  // gang reports FitError for jobs not ready at session close (gang.go:169-190);
+  // NodesFitDelta comes from allocate only (empty when it did not run)
+  if (S.cycle_started && out->ready_num < S.jobs_in[job].min_available && (size_t)job < S.fit.size()) {
     out->fit_valid = 1;
     out->fit_nodes = S.fit[job].nodes;
     out->fit_cpu = S.fit[job].cpu;
@@ -1708,7 +1854,7 @@ kbg_status kbg_queue_state_get(kbg_session* s, int32_t queue, kbg_queue_state* o
   if (!s || !out) return fail(KBG_E_INVALID, "null argument");
   Session& S = s->s;
   if (queue < 0 || queue >= S.n_queues) return fail(KBG_E_INVALID, "queue index");
-  const Engine& E = S.allocated ? S.fin : S.init;
+  const Engine& E = S.cycle_started ? S.fin : S.init;
   out->has_attr = S.has_prop && S.q_has_attr[queue];
   out->share = E.qshare[queue];
   out->deserved = to_kres(S.q_deserved[queue]);

@@ -118,6 +118,7 @@ struct Session {
   std::vector<int32_t> joff, jcap;                       // per-queue job-heap segment (jcap + 1 slots)
   std::vector<int32_t> pend, pend_off, pend_len;         // per-job pending tasks in TaskOrderFn order
   std::vector<char> pending_candidate;                   // task is Pending and not BestEffort
+  std::vector<char> be_task;                             // task is Pending and BestEffort (backfill.go:48-50)
   std::vector<int32_t> task_class;
   std::vector<int32_t> task_shape;                       // (class, request) shape id of a pending task
   int32_t n_shapes = 0;
@@ -135,9 +136,14 @@ struct Session {
   std::vector<char> nil_node;
   std::vector<char> panic_node;  // nil Node under an active predicates plugin (predicates.go:122-123)
 
-  // ---- results of the last allocate
-  Engine fin;
-  bool allocated = false;
+  // ---- the cycle's actions (allocate, then backfill) on this snapshot
+  Engine fin;                 // plugin/ordering state after the last action
+  bool cycle_started = false; // an action ran since open / reset
+  bool allocated = false, backfilled = false;
+  std::vector<kbg_decision> dec;              // decision log of the cycle
+  std::vector<int32_t> undisp_head, undisp_next;  // Allocate decisions not yet dispatched, per job
+  std::vector<int32_t> jt_off, jt;            // tasks of each job in snapshot (status-index) order
+  std::vector<int32_t> be_shape;              // per pod-spec class: grouping id of its BestEffort tasks
   std::vector<int32_t> committed_ready;
   struct FitCounts { int32_t valid = 0, nodes = 0, cpu = 0, mem = 0, gpu = 0; };
   std::vector<FitCounts> fit;               // per job (A17)

@@ -273,7 +273,7 @@ std::string spec_key(const Session& S, const kbg_spec* sp) {
 
 }  // namespace
 
-// Builds classes for every pending task, the node bitsets and the device
+// Builds classes for every pending task (allocate and backfill candidates), the node bitsets and the device
 // programs; fills S.task_class and S.static_host (uploaded by the caller).
 void compile_static_predicates(Session& S, StaticHost* out) {
   Compiler C(S);
@@ -288,7 +288,7 @@ void compile_static_predicates(Session& S, StaticHost* out) {
     std::unordered_map<std::string, int32_t> class_of_key;
     std::vector<int32_t> class_spec;
     for (int32_t t = 0; t < S.n_tasks; ++t) {
-      if (!S.pending_candidate[t]) continue;
+      if (!S.pending_candidate[t] && !S.be_task[t]) continue;  // allocate and backfill candidates
       const int32_t sp = S.tasks_in[t].spec;
       const kbg_spec* spec = sp >= 0 ? &S.specs_in[sp] : nullptr;
       std::string key = spec_key(S, spec);

@@ -146,7 +146,7 @@ class kbg_stats(ctypes.Structure):
                 ("truncations", i64), ("scan_launches", i64), ("scan_kernel_ms", f64), ("select_kernel_ms", f64),
                 ("allocate_ms", f64), ("open_ms", f64), ("engine_ms", f64), ("resolve_ms", f64),
                 ("device_ms", f64), ("delta_ms", f64), ("replayed", i64), ("n_classes", i32), ("shards", i32), ("shard_index", i32),
-                ("int_scan", i32), ("exchange_ms", f64), ("reserved", i32 * 2)]
+                ("int_scan", i32), ("exchange_ms", f64), ("backfill_ms", f64)]
 
 
 # Every symbol include/kbgpu.h declares, with its ctypes signature.
@@ -160,6 +160,7 @@ SIGNATURES = {
     "kbg_comm_init": (i32, [P(ctypes.c_uint8), i32, i32, i32, P(ctypes.c_void_p)]),
     "kbg_comm_destroy": (None, [ctypes.c_void_p]),
     "kbg_allocate": (i32, [ctypes.c_void_p, P(kbg_decision), i32, P(i32)]),
+    "kbg_backfill": (i32, [ctypes.c_void_p, P(kbg_decision), i32, P(i32)]),
     "kbg_session_reset": (i32, [ctypes.c_void_p]),
     "kbg_select": (i32, [ctypes.c_void_p, P(i32), i32, i32, P(i32), P(i32), P(i32)]),
     "kbg_apply": (i32, [ctypes.c_void_p, i32, P(kbg_resource), i32]),

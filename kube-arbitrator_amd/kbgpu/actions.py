@@ -1,9 +1,12 @@
-"""The allocate action (pkg/scheduler/actions/allocate/allocate.go:27-178).
+"""The allocate and backfill actions (pkg/scheduler/actions/allocate/allocate.go:27-178,
+pkg/scheduler/actions/backfill/backfill.go:26-73).
 
-`AllocateAction.execute(ssn)` runs allocateAction.Execute on the MI355X path
-(kbg_allocate) and replays its decision log through the session in reference
-order: ssn.Allocate / ssn.Pipeline per decision, then ssn.dispatch for every
-task the decision's JobReady check bound (session.go:283-290).
+`execute(ssn)` runs the action's Execute on the MI355X path (kbg_allocate /
+kbg_backfill) and replays the new part of the cycle's decision log through
+the session in reference order: ssn.Allocate / ssn.Pipeline per decision,
+then ssn.dispatch for every task the decision's JobReady check bound
+(session.go:283-290) — a backfill decision can dispatch Allocate decisions of
+its job made by the allocate action earlier in the cycle.
 """
 import ctypes
 
@@ -11,16 +14,18 @@ from . import _abi
 from .framework import register_action
 
 
-class AllocateResult:
+class ActionResult:
     def __init__(self, decisions, status, error):
-        self.decisions = decisions  # list of (task_index, node_index, kind, dispatched_at)
+        self.decisions = decisions  # the cycle's log: (task_index, node_index, kind, dispatched_at)
         self.status = status
         self.error = error
 
 
-class AllocateAction:
-    def name(self):
-        return "allocate"
+AllocateResult = ActionResult
+
+
+class _DeviceAction:
+    _entry = None
 
     def initialize(self):
         pass
@@ -30,32 +35,49 @@ class AllocateAction:
 
     def execute(self, ssn):
         L = _abi.lib()
-        cap = max(1, ssn.flat.pending_count)
+        cap = max(1, ssn.flat.pending_all)
         buf = (_abi.kbg_decision * cap)()
         n = ctypes.c_int32(0)
-        code = L.kbg_allocate(ssn.handle, buf, cap, ctypes.byref(n))
+        code = getattr(L, self._entry)(ssn.handle, buf, cap, ctypes.byref(n))
         err = L.kbg_last_error().decode() if code != _abi.KBG_OK else ""
         if code not in (_abi.KBG_OK, _abi.KBG_E_REF_PANIC):
             _abi.check(code)
         decs = [(buf[i].task, buf[i].node, buf[i].kind, buf[i].dispatched_at) for i in range(n.value)]
+        start = len(ssn.decisions)
         tasks = ssn.flat.task_objs
         names = ssn.flat.node_names
         bound_at = {}
-        for i, (t, nd, kind, disp) in enumerate(decs):
-            task = tasks[t]
+        for t, _, _, disp in decs:
+            if disp >= start:
+                bound_at.setdefault(disp, []).append(tasks[t])
+        for i in range(start, len(decs)):
+            t, nd, kind, _ = decs[i]
             if kind == _abi.KIND_ALLOCATE:
-                ssn.allocate(task, names[nd])
+                ssn.allocate(tasks[t], names[nd])
             else:
-                ssn.pipeline(task, names[nd])
-            if disp >= 0:
-                bound_at.setdefault(disp, []).append(task)
+                ssn.pipeline(tasks[t], names[nd])
             for bt in bound_at.pop(i, []):
                 ssn.dispatch(bt)
         ssn.decisions = decs
-        result = AllocateResult(decs, _abi.STATUS_NAMES[code], err)
+        ssn.action_of.extend([self.name()] * (len(decs) - start))
+        result = ActionResult(decs, _abi.STATUS_NAMES[code], err)
         if code == _abi.KBG_E_REF_PANIC:
             raise _abi.KbgError(code, err)
         return result
+
+
+class AllocateAction(_DeviceAction):
+    _entry = "kbg_allocate"
+
+    def name(self):
+        return "allocate"
+
+
+class BackfillAction(_DeviceAction):
+    _entry = "kbg_backfill"
+
+    def name(self):
+        return "backfill"
 
 
 def new():
@@ -63,3 +85,4 @@ def new():
 
 
 register_action(AllocateAction())
+register_action(BackfillAction())

@@ -4,7 +4,7 @@ from . import _abi, actions
 from .api import RefPanic
 from .cache import FakeBinder, cache_from_fixture
 from .conf import tiers_from_list, load_scheduler_conf
-from .framework import open_session
+from .framework import get_action, open_session
 
 
 def fixture_tiers(fx):
@@ -66,19 +66,27 @@ def run_fixture(fx, options=None):
         return {"status": "ref_panic", "error": str(e)}, None
     except _abi.KbgError as e:
         return {"status": e.status, "error": str(e)}, None
+    status = "ok"
     try:
-        res = actions.new().execute(ssn)
-        status = res.status
+        for name in fx.get("actions") or ["allocate"]:  # conf "actions" (util.go:30-61)
+            action = get_action(name)
+            if action is None:
+                return {"status": "bad_input", "error": f"unsupported action {name}"}, ssn
+            status = action.execute(ssn).status
     except _abi.KbgError as e:
+        if e.status == "unsupported":
+            return {"status": "unsupported", "error": str(e)}, ssn
         if e.status != "ref_panic":
             raise
         return {"status": "ref_panic", "error": str(e)}, ssn
     tasks, names = ssn.flat.task_objs, ssn.flat.node_names
     out = {"status": status, "decisions": [], "binds": dict(binder.binds), "jobs": [], "queues": [], "nodes": []}
-    for t, nd, kind, disp in ssn.decisions:
-        out["decisions"].append({"task": tasks[t].uid, "job": tasks[t].job, "node": names[nd],
-                                 "kind": "allocate" if kind == _abi.KIND_ALLOCATE else "pipeline",
-                                 "dispatched_at": disp})
+    for (t, nd, kind, disp), act in zip(ssn.decisions, ssn.action_of):
+        d = {"task": tasks[t].uid, "job": tasks[t].job, "node": names[nd],
+             "kind": "allocate" if kind == _abi.KIND_ALLOCATE else "pipeline", "dispatched_at": disp}
+        if act == "backfill":
+            d["action"] = "backfill"
+        out["decisions"].append(d)
     has_drf = any(p.name == "drf" for t in ssn.tiers for p in t.plugins)
     for j, job in enumerate(ssn.jobs):
         st = ssn.job_state(j)

@@ -72,6 +72,7 @@ class Session:
             _abi.check(L.kbg_session_open(ctypes.byref(self.flat.snap), ctypes.byref(opts),
                                           ctypes.byref(self.handle)))
         self.decisions = []
+        self.action_of = []  # action name of each decision of the cycle
 
     def _active_tiers(self):
         from .conf import Tier

@@ -125,6 +125,7 @@ class FlatSnapshot:
         for i, row in enumerate(task_rows):
             tk[i] = row
         self.pending_count = sum(1 for t in self.task_objs if t.status == PENDING and not t.resreq.is_empty())
+        self.pending_all = sum(1 for t in self.task_objs if t.status == PENDING)
 
         def arr(ctype, rows):
             a = (ctype * max(1, len(rows)))()

@@ -103,7 +103,7 @@ def config_fixture(cid):
 _OPS = ("In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt")
 
 
-def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8):
+def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8, be_frac=0.06):
     rng = random.Random(seed)
     nn = rng.randint(1, max_nodes)
     zones = ["a", "b", "c"]
@@ -143,7 +143,7 @@ def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8):
         return p
 
     def rand_req(best_effort_ok=True):
-        if best_effort_ok and rng.random() < 0.06:
+        if best_effort_ok and rng.random() < be_frac:
             return {"cpu": "5m"}  # BestEffort (all dims below the tolerance)
         r = {"cpu": rng.choice(["100m", "500m", "1", "2", "3"]), "memory": rng.choice(["256Mi", "1Gi", "2Gi", "3Gi"])}
         if rng.random() < 0.15:
@@ -249,4 +249,9 @@ def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8):
     fx = {"name": f"fuzz-{seed}", "tiers": tiers, "nodes": nodes, "pods": pods, "podGroups": pgs, "queues": queues}
     if rng.random() < 0.2:
         fx["namespaces"] = ["c1", "c2"]
+    r = rng.random()  # conf actions (util.go:30-61): the default "allocate, backfill", or one of them
+    if r < 0.5:
+        fx["actions"] = ["allocate", "backfill"]
+    elif r < 0.6:
+        fx["actions"] = ["backfill"]
     return fx

@@ -14,6 +14,7 @@
 //   pkg/scheduler/api/{resource_info.go, node_info.go, job_info.go, helpers.go, helpers/helpers.go}
 //   pkg/scheduler/plugins/{drf,proportion,gang,priority,predicates}
 //   pkg/scheduler/actions/allocate/allocate.go:41-176
+//   pkg/scheduler/actions/backfill/backfill.go:40-71 (fixture "actions": [..., "backfill"])
 //   vendor/k8s.io/kubernetes/pkg/scheduler/algorithm/predicates/predicates.go:797-862,1489-1517
 //   vendor/k8s.io/kubernetes/pkg/apis/core/v1/helper/helpers.go:222-331,412-441
 //   vendor/k8s.io/api/core/v1/toleration.go:37-56
@@ -710,7 +711,7 @@ struct PluginOption {
 };
 typedef std::vector<std::vector<PluginOption>> Tiers;
 
-struct Decision { TaskInfo* task; std::string node; int kind; int dispatched_at = -1; };
+struct Decision { TaskInfo* task; std::string node; int kind; int dispatched_at = -1; bool backfill = false; };
 enum { KIND_ALLOCATE = 0, KIND_PIPELINE = 1 };
 
 struct Session;
@@ -740,6 +741,7 @@ struct Session {  // framework/session.go:35-61
   std::vector<std::pair<std::string, std::string>> binds;  // (ns/name, node) in dispatch order
   int64_t predicate_calls = 0;
   std::vector<TaskInfo*> evaluated;  // every task whose node loop ran, in order
+  bool be_host_port = false;         // a BestEffort Pending pod declares hostPort (predicates active)
 
   // session_plugins.go:142-156
   bool Overused(QueueInfo* q) {
@@ -1169,6 +1171,7 @@ struct Predicates {
           throw Unsupported("pod (anti)affinity present: inter-pod affinity predicate not restated");
         if (t->status == Pending && !t->resreq.IsEmpty() && t->pod->has_host_port)
           throw Unsupported("pending pod declares hostPort: host-port predicate not restated");
+        if (t->status == Pending && t->resreq.IsEmpty() && t->pod->has_host_port) s->be_host_port = true;
         if (AllocatedStatus(t->status) && !s->nodeIndex.count(t->nodeName)) ghost = true;
       }
     s->predicateFns["predicates"] = [this](TaskInfo* task, NodeInfo* node) -> bool {
@@ -1239,6 +1242,31 @@ static void allocate_execute(Session* ssn) {
       if (assigned) { jobs->Push(job); break; }
     }
     queues.Push(queue);
+  }
+}
+
+// backfill.go:40-71: every Pending task of every job (ssn.Jobs order, status
+// index order) that requests nothing goes to the first node whose PredicateFn
+// passes, through ssn.Allocate. Go ranges over the live Pending map while
+// Allocate removes the current task from it; removing the entry being visited
+// does not change which entries the range yields, so a copy is equivalent.
+static void backfill_execute(Session* ssn) {
+  if (ssn->be_host_port) throw Unsupported("BestEffort pending pod declares hostPort: host-port predicate not restated");
+  for (JobInfo* job : ssn->jobs) {
+    auto it = job->statusIndex.find(Pending);
+    if (it == job->statusIndex.end()) continue;
+    std::vector<TaskInfo*> pending;
+    for (auto& kv : it->second.items) pending.push_back(kv.second);
+    for (TaskInfo* task : pending) {
+      if (!task->resreq.IsEmpty()) continue;  // "backfill for other case" is a TODO in v0.4
+      for (NodeInfo* node : ssn->nodes) {
+        if (!ssn->PredicateFn(task, node)) continue;
+        const size_t before = ssn->decisions.size();
+        ssn->Allocate(task, node);
+        ssn->decisions[before].backfill = true;
+        break;
+      }
+    }
   }
 }
 
@@ -1420,8 +1448,18 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache) {
       // unknown plugin names are skipped (framework.go:30-35 logs an error)
     }
 
+  // conf "actions" (util.go:30-61); fixtures without the field run allocate only
+  std::vector<std::string> actions = {"allocate"};
+  if (const Value* a = fx.get("actions")) {
+    actions.clear();
+    for (auto& x : a->arr) actions.push_back(x.s);
+  }
   auto t0 = std::chrono::steady_clock::now();
-  allocate_execute(ssn);
+  for (auto& a : actions) {
+    if (a == "allocate") allocate_execute(ssn);
+    else if (a == "backfill") backfill_execute(ssn);
+    else throw BadInput("unsupported action " + a);
+  }
   auto t1 = std::chrono::steady_clock::now();
   double secs = std::chrono::duration<double>(t1 - t0).count();
 
@@ -1432,7 +1470,7 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache) {
     if (i) o += ",";
     o += "{\"task\":" + kbjson::quote(d.task->uid) + ",\"job\":" + kbjson::quote(d.task->job) +
          ",\"node\":" + kbjson::quote(d.node) + ",\"kind\":\"" + (d.kind == KIND_ALLOCATE ? "allocate" : "pipeline") +
-         "\",\"dispatched_at\":" + std::to_string(d.dispatched_at) + "}";
+         "\",\"dispatched_at\":" + std::to_string(d.dispatched_at) + (d.backfill ? ",\"action\":\"backfill\"" : "") + "}";
   }
   o += "],\"evaluated\":[";
   for (size_t i = 0; i < ssn->evaluated.size(); i++) o += (i ? "," : "") + kbjson::quote(ssn->evaluated[i]->uid);

@@ -144,6 +144,7 @@ def test_select_replays_reference_node_loop(seed):
     import ctypes
     from kbgpu import _abi
     fx = synth.config_fixture(1) if seed == "c1" else synth.random_fixture(seed)
+    fx.pop("actions", None)  # the node loop of allocate only
     ref = run_oracle(fx)
     if ref["status"] != "ok":
         pytest.skip(ref["status"])
@@ -239,3 +240,37 @@ def test_int_scan_is_the_default_on_integer_sessions():
     got, ssn = run_fixture(fx)
     assert ssn.stats().int_scan == 1
     ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_backfill_parity(seed):
+    """backfill.go:40-71 after (or without) allocate: first node whose PredicateFn
+    passes, pod caps 2-5 on most nodes, panics on overcommitted Idle."""
+    fx = synth.random_fixture(2000 + seed, max_nodes=10, max_jobs=12, max_tasks=12, be_frac=0.6)
+    fx["actions"] = ["allocate", "backfill"] if seed % 4 else ["backfill"]
+    got, ssn = run_fixture(fx, {"batch_tasks": 1 + seed % 7, "candidates": 1 + seed % 3, "full_scan": seed % 2})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+@pytest.mark.parametrize("be_req", [{}, {"cpu": "5m"}])
+def test_backfill_config2(shards, be_req):
+    """C2 with every 7th pod BestEffort: allocate then backfill over 1k nodes.
+    Requests of 5m drive a full node's Idle below the tolerance on the second
+    BestEffort pod, where Resource.Sub panics (resource_info.go:100-110)."""
+    fx = synth.config_fixture(2)
+    for i, p in enumerate(fx["pods"]):
+        if i % 7 == 3:
+            p["containers"] = [{"requests": dict(be_req)}]
+    fx["actions"] = ["allocate", "backfill"]
+    ref = run_oracle(fx)
+    if be_req:
+        assert ref["status"] == "ref_panic"
+    else:
+        assert sum(1 for d in ref["decisions"] if d.get("action") == "backfill") > 1000
+    got, ssn = run_fixture(fx, {"shards": shards})
+    compare_outputs(ref, got)
+    if ssn:
+        ssn.close()
