@@ -30,14 +30,14 @@
 extern "C" {
 #endif
 
-#define KBG_ABI_VERSION 2
+#define KBG_ABI_VERSION 3
 
 typedef enum kbg_status {
   KBG_OK = 0,
   KBG_E_INVALID = 1,     /* malformed snapshot / arguments */
   KBG_E_UNSUPPORTED = 2, /* session uses a predicate the device path does not run
-                            (pending hostPort, pod (anti)affinity): run the
-                            reference path instead. Never a silent fallback. */
+                            (pod (anti)affinity): run the reference path
+                            instead. Never a silent fallback. */
   KBG_E_REF_PANIC = 3,   /* the reference would panic here (Resource.Sub underflow
                             resource_info.go:100-110, proportion water-fill F9
                             proportion.go:119-140, nil-Node predicate
@@ -95,7 +95,17 @@ typedef struct kbg_node {
   int32_t unschedulable;   /* Node.Spec.Unschedulable */
   int32_t label_off, label_len; /* Node.Labels: pairs (key,value) at labels[2*i] */
   int32_t taint_off, taint_len; /* Node.Spec.Taints: taints[taint_off ..] */
+  int32_t port_off, port_len;   /* NodeInfo.UsedPorts(): every container port of the pods on the
+                                   node (node.Pods(), node_info.go:181-187 -> vendor
+                                   cache/node_info.go:593-605), ports[port_off ..] */
 } kbg_node;
+
+/* One v1.ContainerPort as HostPortInfo sees it (vendor cache/host_ports.go). */
+typedef struct kbg_host_port {
+  int32_t host_ip;   /* string id of HostIP ("" means 0.0.0.0) */
+  int32_t protocol;  /* string id of Protocol ("" means TCP) */
+  int32_t host_port; /* HostPort; <= 0 never conflicts and is never recorded */
+} kbg_host_port;
 
 typedef struct kbg_taint {
   int32_t key, value, effect; /* string ids */
@@ -135,6 +145,7 @@ typedef struct kbg_spec {
   int32_t toleration_off, toleration_len;
   int32_t has_host_ports;             /* some container port has hostPort > 0 */
   int32_t has_pod_affinity;           /* Affinity.PodAffinity or PodAntiAffinity set */
+  int32_t port_off, port_len;         /* GetContainerPorts(pod): ports[port_off ..] */
 } kbg_spec;
 
 typedef struct kbg_term {
@@ -175,6 +186,7 @@ typedef struct kbg_snapshot {
   const int32_t* selectors;        int32_t n_selectors; /* 2*n_selectors ints */
   const kbg_plugin_option* plugins; int32_t n_plugins;
   const int32_t* tier_sizes;       int32_t n_tiers;     /* plugins grouped by tier, in order */
+  const kbg_host_port* ports;      int32_t n_ports;
 } kbg_snapshot;
 
 typedef struct kbg_options {

@@ -63,6 +63,14 @@ struct NodeDelta {
   double rel[3];
 };
 
+// One class-mask word rewritten by the host (host-port conflicts).
+struct MaskDelta {
+  uint32_t index;
+  uint32_t pad;
+  uint64_t value;
+};
+constexpr int32_t kMaskDeltaCap = 8192;
+
 // ---- static predicate programs (built on host, evaluated on device) ----
 enum ReqKind : int32_t {
   REQ_FALSE = 0,
@@ -148,5 +156,6 @@ hipError_t launch_select(const uint64_t* bits, int32_t W, int32_t Wl, int32_t n_
                          hipEvent_t stop = nullptr);
 
 hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream);
+hipError_t launch_mask_apply(uint64_t* class_mask, const MaskDelta* deltas, int32_t n_deltas, hipStream_t stream);
 
 }  // namespace kbg

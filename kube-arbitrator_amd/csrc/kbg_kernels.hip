@@ -264,6 +264,19 @@ hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_del
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void kbg_mask_apply_kernel(uint64_t* __restrict__ class_mask,
+                                                             const MaskDelta* __restrict__ d, int32_t n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) class_mask[d[i].index] = d[i].value;
+}
+
+hipError_t launch_mask_apply(uint64_t* class_mask, const MaskDelta* deltas, int32_t n_deltas, hipStream_t stream) {
+  if (n_deltas <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kbg_mask_apply_kernel, dim3((n_deltas + 255) / 256), dim3(256), 0, stream, class_mask, deltas,
+                     n_deltas);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------- static mask
 // One lane = one (class, node) pair; vendor predicates.go:807-850 (selector +
 // required node affinity), predicates.go:105-110 (unschedulable),

@@ -39,7 +39,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <numeric>
+#include <tuple>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -416,6 +418,8 @@ void free_device(Session& S) {
   S.h_down = nullptr;
   S.h_capoff = nullptr;
   if (S.h_deltas) (void)hipHostFree(S.h_deltas);
+  if (S.h_mdeltas) (void)hipHostFree(S.h_mdeltas);
+  S.h_mdeltas = nullptr;
   S.h_tasks = nullptr;
   S.h_cand = S.h_count = nullptr;
   S.h_deltas = nullptr;
@@ -533,6 +537,21 @@ kbg_status device_scan(Session& S, int32_t G) {
 // Writes the rows of the nodes touched by the last commits back to HBM (only
 // the rows this process holds; every shard's host mirror saw every commit).
 kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
+  // class-mask words cleared by host-port conflicts (every shard holds the whole mask)
+  for (size_t m = 0; m < S.mask_dirty.size();) {
+    const int32_t cnt = (int32_t)std::min<size_t>(S.mask_dirty.size() - m, (size_t)kbg::kMaskDeltaCap);
+    for (int32_t k = 0; k < cnt; ++k) {
+      const uint32_t idx = S.mask_dirty[m + k];
+      S.h_mdeltas[k] = kbg::MaskDelta{idx, 0u, S.h_class_mask[idx]};
+      S.mask_dirty_flag[idx] = 0;
+    }
+    HIP_TRY(hipMemcpyAsync(S.d_mdeltas, S.h_mdeltas, cnt * sizeof(kbg::MaskDelta), hipMemcpyHostToDevice, S.stream));
+    HIP_TRY(kbg::launch_mask_apply(S.d_class_mask, S.d_mdeltas, cnt, S.stream));
+    m += cnt;
+    if (m < S.mask_dirty.size()) HIP_TRY(hipStreamSynchronize(S.stream));  // staging reuse
+  }
+  // (the last chunk's copy is retired by the next device round trip's synchronize)
+  S.mask_dirty.clear();
   size_t i = 0;
   while (i < touched.size()) {
     int32_t cnt = 0;
@@ -640,6 +659,7 @@ struct Resolver {
       }
       // touched by an earlier commit of this batch: re-check on the host mirror
       if (S.pred_active && S.ntasks[nd] >= S.maxtasks[nd]) continue;
+      if (S.has_ports && !((S.h_class_mask[(size_t)S.task_class[t] * S.W + (nd >> 6)] >> (nd & 63)) & 1ull)) continue;
       if (S.be_task[t]) {  // backfill: PredicateFn only, always ssn.Allocate
         *node = nd;
         *kind = KBG_KIND_ALLOCATE;
@@ -664,12 +684,122 @@ struct Resolver {
 
 // NodeInfo.AddTask on the host mirror (node_info.go:101-129): Allocated ->
 // Idle -= req; Pipelined -> Releasing -= req; both add a task.
+void clear_mask_bit(Session& S, int32_t c, int32_t nd) {
+  const uint32_t idx = (uint32_t)((size_t)c * S.W + (nd >> 6));
+  const uint64_t bit = 1ull << (nd & 63);
+  if (!(S.h_class_mask[idx] & bit)) return;
+  S.h_class_mask[idx] &= ~bit;
+  if (!S.mask_dirty_flag[idx]) {
+    S.mask_dirty_flag[idx] = 1;
+    S.mask_dirty.push_back(idx);
+  }
+}
+
+// The pod joins node.Pods(), so its ports join the node's HostPortInfo
+// (vendor cache/node_info.go:593-605): every class that conflicts with a newly
+// used (ip, protocol, port) loses the node.
+void add_ports(Session& S, int32_t c, int32_t nd) {
+  uint64_t* np = &S.node_ports[(size_t)nd * S.PW];
+  const uint64_t* add = &S.cls_add[(size_t)c * S.PW];
+  for (int32_t w = 0; w < S.PW; ++w) {
+    uint64_t nb = add[w] & ~np[w];
+    np[w] |= nb;
+    while (nb) {
+      const int32_t a = w * 64 + __builtin_ctzll(nb);
+      nb &= nb - 1;
+      for (int32_t c2 : S.atom_cls[a]) clear_mask_bit(S, c2, nd);
+    }
+  }
+}
+
 void mirror_add(Session& S, int32_t t, int32_t nd, int32_t kind) {
   if (!S.nil_node[nd]) {
     if (kind == KBG_KIND_ALLOCATE) kbg::res_sub(S.idle[nd], S.treq[t]);
     else kbg::res_sub(S.rel[nd], S.treq[t]);
   }
   S.ntasks[nd]++;
+  if (S.has_ports) add_ports(S, S.task_class[t], nd);
+}
+
+// Builds the port-atom dictionary (distinct sanitized (ip, protocol, port)
+// with port > 0 over the nodes' used ports and the candidate classes' wanted
+// ports), each class's conflict set (host_ports.go CheckConflict: same
+// protocol and port, and either side 0.0.0.0 or the same ip) and folds the
+// nodes' current conflicts into the class masks.
+void setup_host_ports(Session& S) {
+  S.has_ports = false;
+  if (!S.pred_active) return;
+  const int32_t C = (int32_t)S.class_spec.size();
+  auto ip_of = [&](int32_t id) { return S.strs[id].empty() ? std::string("0.0.0.0") : S.strs[id]; };
+  auto proto_of = [&](int32_t id) { return S.strs[id].empty() ? std::string("TCP") : S.strs[id]; };
+  typedef std::tuple<std::string, std::string, int32_t> Atom;
+  std::map<Atom, int32_t> atoms;
+  std::vector<Atom> atom_list;
+  auto atom = [&](const kbg_host_port& hp) {
+    Atom a{ip_of(hp.host_ip), proto_of(hp.protocol), hp.host_port};
+    auto it = atoms.find(a);
+    if (it != atoms.end()) return it->second;
+    const int32_t id = (int32_t)atom_list.size();
+    atoms.emplace(a, id);
+    atom_list.push_back(a);
+    return id;
+  };
+  std::vector<std::vector<int32_t>> want(C);
+  bool any = false;
+  for (int32_t c = 0; c < C; ++c) {
+    const int32_t sp = S.class_spec[c];
+    if (sp < 0) continue;
+    const kbg_spec& spec = S.specs_in[sp];
+    for (int32_t i = 0; i < spec.port_len; ++i) {
+      const kbg_host_port& hp = S.ports_in[spec.port_off + i];
+      if (hp.host_port <= 0) continue;
+      want[c].push_back(atom(hp));
+      any = true;
+    }
+  }
+  if (!any) return;
+  std::vector<std::vector<int32_t>> used(S.n_nodes);
+  for (int32_t n = 0; n < S.n_nodes; ++n) {
+    const kbg_node& nd = S.nodes_in[n];
+    for (int32_t i = 0; i < nd.port_len; ++i) {
+      const kbg_host_port& hp = S.ports_in[nd.port_off + i];
+      if (hp.host_port > 0) used[n].push_back(atom(hp));
+    }
+  }
+  S.has_ports = true;
+  const int32_t A = (int32_t)atom_list.size();
+  S.PW = (A + 63) / 64;
+  S.cls_conf.assign((size_t)C * S.PW, 0);
+  S.cls_add.assign((size_t)C * S.PW, 0);
+  S.atom_cls.assign(A, {});
+  for (int32_t c = 0; c < C; ++c)
+    for (int32_t w : want[c]) {
+      S.cls_add[(size_t)c * S.PW + w / 64] |= 1ull << (w % 64);
+      const Atom& wa = atom_list[w];
+      for (int32_t a = 0; a < A; ++a) {
+        const Atom& ea = atom_list[a];
+        if (std::get<1>(ea) != std::get<1>(wa) || std::get<2>(ea) != std::get<2>(wa)) continue;
+        if (std::get<0>(wa) == "0.0.0.0" || std::get<0>(ea) == "0.0.0.0" || std::get<0>(ea) == std::get<0>(wa))
+          S.cls_conf[(size_t)c * S.PW + a / 64] |= 1ull << (a % 64);
+      }
+    }
+  for (int32_t c = 0; c < C; ++c)
+    for (int32_t a = 0; a < A; ++a)
+      if ((S.cls_conf[(size_t)c * S.PW + a / 64] >> (a % 64)) & 1ull) S.atom_cls[a].push_back(c);
+  S.node_ports.assign((size_t)S.n_nodes * S.PW, 0);
+  S.mask_dirty_flag.assign(S.h_class_mask.size(), 0);
+  S.mask_dirty.clear();
+  for (int32_t n = 0; n < S.n_nodes; ++n) {
+    for (int32_t a : used[n]) S.node_ports[(size_t)n * S.PW + a / 64] |= 1ull << (a % 64);
+    if (S.panic_node[n]) continue;  // SetNode(nil) panics before any check: keep the node reachable
+    for (int32_t c = 0; c < C; ++c) {
+      bool conflict = false;
+      for (int32_t w = 0; w < S.PW && !conflict; ++w)
+        conflict = (S.node_ports[(size_t)n * S.PW + w] & S.cls_conf[(size_t)c * S.PW + w]) != 0;
+      if (conflict) S.h_class_mask[(size_t)c * S.W + (n >> 6)] &= ~(1ull << (n & 63));
+    }
+  }
+  S.node_ports0 = S.node_ports;
 }
 kbg_status validate(const kbg_snapshot* s) {
   if (!s) return fail(KBG_E_INVALID, "null snapshot");
@@ -681,7 +811,8 @@ kbg_status validate(const kbg_snapshot* s) {
   const int32_t NS = s->n_strings;
   for (int32_t i = 0; i < s->n_nodes; ++i) {
     const kbg_node& n = s->nodes[i];
-    if (!in(n.name, NS) || !range(n.label_off, n.label_len, s->n_labels) || !range(n.taint_off, n.taint_len, s->n_taints))
+    if (!in(n.name, NS) || !range(n.label_off, n.label_len, s->n_labels) || !range(n.taint_off, n.taint_len, s->n_taints) ||
+        !range(n.port_off, n.port_len, s->n_ports))
       return fail(KBG_E_INVALID, "node " + std::to_string(i));
   }
   for (int32_t i = 0; i < s->n_labels * 2; ++i)
@@ -705,7 +836,7 @@ kbg_status validate(const kbg_snapshot* s) {
   for (int32_t i = 0; i < s->n_specs; ++i) {
     const kbg_spec& p = s->specs[i];
     if (!range(p.selector_off, p.selector_len, s->n_selectors) || !range(p.term_off, p.term_len, s->n_terms) ||
-        !range(p.toleration_off, p.toleration_len, s->n_tolerations))
+        !range(p.toleration_off, p.toleration_len, s->n_tolerations) || !range(p.port_off, p.port_len, s->n_ports))
       return fail(KBG_E_INVALID, "spec " + std::to_string(i));
   }
   for (int32_t i = 0; i < s->n_terms; ++i) {
@@ -719,6 +850,9 @@ kbg_status validate(const kbg_snapshot* s) {
   }
   for (int32_t i = 0; i < s->n_values; ++i)
     if (!in(s->values[i], NS)) return fail(KBG_E_INVALID, "value");
+  if (s->n_ports < 0 || (s->n_ports > 0 && !s->ports)) return fail(KBG_E_INVALID, "ports");
+  for (int32_t i = 0; i < s->n_ports; ++i)
+    if (!in(s->ports[i].host_ip, NS) || !in(s->ports[i].protocol, NS)) return fail(KBG_E_INVALID, "port");
   for (int32_t i = 0; i < s->n_tolerations; ++i) {
     const kbg_toleration& t = s->tolerations[i];
     if (!in(t.key, NS) || !in(t.op, NS) || !in(t.value, NS) || !in(t.effect, NS)) return fail(KBG_E_INVALID, "toleration");
@@ -786,6 +920,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.selectors_in = copy_arr(snap->selectors, 2 * snap->n_selectors);
   S.tols_in = copy_arr(snap->tolerations, snap->n_tolerations);
   S.taints_in = copy_arr(snap->taints, snap->n_taints);
+  S.ports_in = copy_arr(snap->ports, snap->n_ports);
 
   // ---- plugins (framework.go:26-46; unknown names ignored)
   {
@@ -975,8 +1110,6 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
       const kbg_spec* sp = tk.spec >= 0 ? &S.specs_in[tk.spec] : nullptr;
       if (sp && sp->has_pod_affinity)
         return fail(KBG_E_UNSUPPORTED, "inter-pod (anti)affinity present: run the reference predicate path");
-      if (sp && sp->has_host_ports && S.pending_candidate[t])
-        return fail(KBG_E_UNSUPPORTED, "pending task declares hostPort: run the reference predicate path");
       if (allocated_status(tk.status) && !names.count(S.canon[tk.node_name])) S.ghost = true;
     }
   }
@@ -1143,6 +1276,15 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
                            S.stream));
     HIP_TRY(hipStreamSynchronize(S.stream));  // sh's host vectors end with this scope
   }
+  // host ports: the port fit is folded into the class masks (setup_host_ports)
+  S.h_class_mask_static = S.h_class_mask;
+  setup_host_ports(S);
+  if (S.has_ports) {
+    HIP_TRY(hipMemcpy(S.d_class_mask, S.h_class_mask.data(), S.h_class_mask.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipHostMalloc((void**)&S.h_mdeltas, (size_t)kbg::kMaskDeltaCap * sizeof(kbg::MaskDelta), hipHostMallocDefault));
+    if ((st = dalloc(S, &S.d_mdeltas, kbg::kMaskDeltaCap))) return st;
+  }
+  S.h_class_mask0 = S.h_class_mask;
   S.stats.n_classes = S.n_classes;
   S.stats.shards = S.R;
   S.stats.shard_index = S.comm ? S.shard : -1;
@@ -1194,7 +1336,7 @@ struct LastEval {
 // at each job's evaluation point are rebuilt by undoing the decision log
 // backwards from the final mirror (exact: the pre-commit values are logged).
 void compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, const std::vector<Res>& dec_old,
-                        const std::vector<LastEval>& last) {
+                        const std::vector<uint64_t>& dec_oldp, const std::vector<LastEval>& last) {
   S.fit.assign(S.n_jobs, Session::FitCounts{});
   std::vector<int32_t> jobs;
   for (int32_t j = 0; j < S.n_jobs; ++j)
@@ -1203,6 +1345,8 @@ void compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, const 
   std::sort(jobs.begin(), jobs.end(), [&](int32_t a, int32_t b) { return last[a].before > last[b].before; });
   std::vector<Res> idle = S.idle, rel = S.rel;
   std::vector<int32_t> ntasks = S.ntasks;
+  std::vector<uint64_t> ports = S.node_ports;  // host ports: [N][PW]
+  const int32_t PW = S.PW;
   int32_t k = (int32_t)dec.size();
   for (int32_t j : jobs) {
     Session::FitCounts& fc = S.fit[j];
@@ -1214,16 +1358,25 @@ void compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, const 
       const int32_t n = dec[k].node;
       if (!S.nil_node[n]) (dec[k].kind == KBG_KIND_ALLOCATE ? idle[n] : rel[n]) = dec_old[k];
       ntasks[n]--;
+      if (S.has_ports)
+        std::copy(dec_oldp.begin() + (size_t)k * PW, dec_oldp.begin() + (size_t)(k + 1) * PW,
+                  ports.begin() + (size_t)n * PW);
     }
     const int32_t t = le.task;
     const Res& r = S.treq[t];
-    const uint64_t* cm = S.h_class_mask.data() + (size_t)S.task_class[t] * S.W;
+    const uint64_t* cm = S.h_class_mask_static.data() + (size_t)S.task_class[t] * S.W;
+    const uint64_t* conf = S.has_ports ? S.cls_conf.data() + (size_t)S.task_class[t] * PW : nullptr;
     const int32_t end = le.node < 0 ? S.n_nodes : le.node + (le.kind == KBG_KIND_PIPELINE ? 1 : 0);
     bool nil_seen = false;
     Res nil_delta{};
     for (int32_t n = 0; n < end; ++n) {
       if (!((cm[n >> 6] >> (n & 63)) & 1ull)) continue;                 // static predicate
       if (S.pred_active && ntasks[n] >= S.maxtasks[n]) continue;       // pod cap
+      if (conf && !S.panic_node[n]) {                                  // host ports
+        bool clash = false;
+        for (int32_t w = 0; w < PW && !clash; ++w) clash = (ports[(size_t)n * PW + w] & conf[w]) != 0;
+        if (clash) continue;
+      }
       if (n != le.node && kbg::res_le(r, idle[n])) continue;           // would have been chosen
       Res d = idle[n];                                                 // Resource.FitDelta
       if (r.c > 0) d.c -= r.c + kbg::kMinMilliCPU;
@@ -1310,6 +1463,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   std::vector<kbg_decision>& dec = S.dec;
   std::vector<Res> dec_old;  // the Idle (Allocate) or Releasing (Pipeline) row before each decision
   dec_old.reserve(S.pend.size());
+  std::vector<uint64_t> dec_oldp;  // host ports: the node's used-port atoms before each decision
   std::vector<LastEval> last(S.n_jobs);
   // shapes known to fit nowhere (monotone): written by the committer, read by the predictor
   std::unique_ptr<std::atomic<uint8_t>[]> failed(new std::atomic<uint8_t>[std::max(1, S.n_shapes)]);
@@ -1490,6 +1644,9 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       last[j] = LastEval{t, (int32_t)dec.size(), node, kind};
       if (ok) {
         dec_old.push_back(kind == KBG_KIND_ALLOCATE ? S.idle[node] : S.rel[node]);
+        if (S.has_ports)
+          dec_oldp.insert(dec_oldp.end(), S.node_ports.begin() + (size_t)node * S.PW,
+                          S.node_ports.begin() + (size_t)(node + 1) * S.PW);
         mirror_add(S, t, node, kind);
         if (mark[node] != stamp) {
           mark[node] = stamp;
@@ -1533,7 +1690,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   }
   finish();
   HIP_TRY(hipStreamSynchronize(S.stream));  // last delta write-back
-  compute_fit_deltas(S, dec, dec_old, last);
+  compute_fit_deltas(S, dec, dec_old, dec_oldp, last);
   S.fin = E;
   S.stats.engine_ms = engine_ms;
   S.stats.replayed = replayed;
@@ -1554,12 +1711,6 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
 kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
   using clk = std::chrono::steady_clock;
   if (S.backfilled) return fail(KBG_E_INVALID, "kbg_backfill already ran on this session; call kbg_session_reset");
-  if (S.pred_active)
-    for (int32_t t = 0; t < S.n_tasks; ++t) {
-      const int32_t sp = S.tasks_in[t].spec;
-      if (S.be_task[t] && sp >= 0 && S.specs_in[sp].has_host_ports)
-        return fail(KBG_E_UNSUPPORTED, "BestEffort pending task declares hostPort: run the reference predicate path");
-    }
   const auto t0 = clk::now();
   if (!S.cycle_started) begin_cycle(S);
   S.backfilled = true;
@@ -1749,6 +1900,14 @@ kbg_status kbg_session_reset(kbg_session* s) {
   S.rel = S.rel0;
   S.ntasks = S.ntasks0;
   S.allocated = S.backfilled = S.cycle_started = false;
+  if (S.has_ports) {  // the class masks carry the port fit: back to the snapshot's
+    S.node_ports = S.node_ports0;
+    S.h_class_mask = S.h_class_mask0;
+    S.mask_dirty.clear();
+    std::fill(S.mask_dirty_flag.begin(), S.mask_dirty_flag.end(), 0);
+    HIP_TRY(hipMemcpyAsync(S.d_class_mask, S.h_class_mask.data(), S.h_class_mask.size() * 8, hipMemcpyHostToDevice,
+                           S.stream));
+  }
   kbg_status st = copy_soa(S, S.d_nodes, S.d_nodes0);
   if (st != KBG_OK) return st;
   HIP_TRY(hipStreamSynchronize(S.stream));

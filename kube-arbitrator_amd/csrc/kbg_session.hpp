@@ -97,6 +97,7 @@ struct Session {
   std::vector<int32_t> values_in, labels_in, selectors_in;
   std::vector<kbg_toleration> tols_in;
   std::vector<kbg_taint> taints_in;
+  std::vector<kbg_host_port> ports_in;
   kbg_options opts{};
 
   // ---- plugin configuration (session_plugins.go tier walks, flattened)
@@ -120,6 +121,7 @@ struct Session {
   std::vector<char> pending_candidate;                   // task is Pending and not BestEffort
   std::vector<char> be_task;                             // task is Pending and BestEffort (backfill.go:48-50)
   std::vector<int32_t> task_class;
+  std::vector<int32_t> class_spec;                       // spec of each static class (-1: none)
   std::vector<int32_t> task_shape;                       // (class, request) shape id of a pending task
   int32_t n_shapes = 0;
   std::vector<Res> treq;
@@ -147,7 +149,22 @@ struct Session {
   std::vector<int32_t> committed_ready;
   struct FitCounts { int32_t valid = 0, nodes = 0, cpu = 0, mem = 0, gpu = 0; };
   std::vector<FitCounts> fit;               // per job (A17)
-  std::vector<uint64_t> h_class_mask;       // host copy of the static predicate bits
+  std::vector<uint64_t> h_class_mask;       // host copy of the class masks the scan reads (static predicate,
+                                            // and with host ports the dynamic port fit)
+  // ---- host ports (vendor predicates.go:1031-1051). A node's used ports only
+  // grow during a cycle, so a (class, node) pair only ever loses feasibility:
+  // the port fit is folded into the class masks and kept current by clearing
+  // bits as placements record ports (monotone, like the pod cap).
+  bool has_ports = false;
+  int32_t PW = 0;                              // u64 words per port-atom set
+  std::vector<uint64_t> node_ports, node_ports0;  // [N][PW] used (ip, protocol, port) atoms
+  std::vector<uint64_t> cls_conf, cls_add;     // [class][PW] atoms a class conflicts with / records
+  std::vector<std::vector<int32_t>> atom_cls;  // classes that conflict with each atom
+  std::vector<uint64_t> h_class_mask0, h_class_mask_static;  // at open (ports applied) / static predicate only
+  std::vector<uint32_t> mask_dirty;            // class-mask words changed since the last write-back
+  std::vector<uint8_t> mask_dirty_flag;
+  MaskDelta* h_mdeltas = nullptr;              // pinned staging
+  MaskDelta* d_mdeltas = nullptr;
 
   // ---- device
   int32_t device = 0;

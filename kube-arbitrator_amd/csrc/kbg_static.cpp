@@ -268,6 +268,14 @@ std::string spec_key(const Session& S, const kbg_spec* sp) {
     add(t.value);
     add(t.effect);
   }
+  k += "P";  // host ports (vendor predicates.go:1031-1051): part of the class, checked dynamically
+  for (int32_t i = 0; i < sp->port_len; ++i) {
+    const kbg_host_port& hp = S.ports_in[sp->port_off + i];
+    k += "p";
+    add(hp.host_ip);
+    add(hp.protocol);
+    k += std::to_string(hp.host_port);
+  }
   return k;
 }
 
@@ -279,6 +287,7 @@ void compile_static_predicates(Session& S, StaticHost* out) {
   Compiler C(S);
   out->n_classes = 0;
   S.task_class.assign(S.n_tasks, 0);
+  S.class_spec.assign(1, -1);
   if (!S.pred_active) {
     ClassProg c{};
     c.sel_req = -1;
@@ -303,6 +312,7 @@ void compile_static_predicates(Session& S, StaticHost* out) {
       }
     }
     if (class_spec.empty()) class_spec.push_back(-1);
+    S.class_spec = class_spec;
     for (int32_t sp : class_spec) C.classes.push_back(C.compile_spec(sp >= 0 ? &S.specs_in[sp] : nullptr));
 
     // taint dictionary over NoSchedule/NoExecute taints of the session nodes

@@ -35,7 +35,7 @@ DISABLE_RECLAIMABLE = 1 << 4
 DISABLE_QUEUE_ORDER = 1 << 5
 DISABLE_PREDICATE = 1 << 6
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 COMM_ID_BYTES = 128
 
 KIND_ALLOCATE = 0
@@ -54,7 +54,12 @@ class kbg_resource(ctypes.Structure):
 class kbg_node(ctypes.Structure):
     _fields_ = [("name", i32), ("has_node", i32), ("allocatable", kbg_resource), ("idle", kbg_resource),
                 ("releasing", kbg_resource), ("max_task_num", i32), ("num_tasks", i32), ("unschedulable", i32),
-                ("label_off", i32), ("label_len", i32), ("taint_off", i32), ("taint_len", i32)]
+                ("label_off", i32), ("label_len", i32), ("taint_off", i32), ("taint_len", i32),
+                ("port_off", i32), ("port_len", i32)]
+
+
+class kbg_host_port(ctypes.Structure):
+    _fields_ = [("host_ip", i32), ("protocol", i32), ("host_port", i32)]
 
 
 class kbg_taint(ctypes.Structure):
@@ -77,7 +82,7 @@ class kbg_task(ctypes.Structure):
 class kbg_spec(ctypes.Structure):
     _fields_ = [("selector_off", i32), ("selector_len", i32), ("has_required_affinity", i32), ("term_off", i32),
                 ("term_len", i32), ("toleration_off", i32), ("toleration_len", i32), ("has_host_ports", i32),
-                ("has_pod_affinity", i32)]
+                ("has_pod_affinity", i32), ("port_off", i32), ("port_len", i32)]
 
 
 class kbg_term(ctypes.Structure):
@@ -114,6 +119,7 @@ class kbg_snapshot(ctypes.Structure):
         ("selectors", P(i32)), ("n_selectors", i32),
         ("plugins", P(kbg_plugin_option)), ("n_plugins", i32),
         ("tier_sizes", P(i32)), ("n_tiers", i32),
+        ("ports", P(kbg_host_port)), ("n_ports", i32),
     ]
 
 

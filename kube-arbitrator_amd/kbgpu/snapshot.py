@@ -28,10 +28,16 @@ class Interner:
         return i
 
 
+def container_ports(pod):
+    """GetContainerPorts(pod) (vendor scheduler/util/utils.go:30-41) as (hostIP, protocol, hostPort)."""
+    return [(pt.get("hostIP") or "", pt.get("protocol") or "", int(pt.get("hostPort") or 0))
+            for c in pod.get("containers", []) for pt in (c.get("ports") or [])]
+
+
 def _spec_key(pod):
     aff = pod.get("affinity") or None
-    has_ports = any((pt.get("hostPort") or 0) > 0 for c in pod.get("containers", []) for pt in (c.get("ports") or []))
-    return json.dumps([pod.get("nodeSelector") or {}, aff, pod.get("tolerations") or [], has_ports], sort_keys=True)
+    return json.dumps([pod.get("nodeSelector") or {}, aff, pod.get("tolerations") or [], container_ports(pod)],
+                      sort_keys=True)
 
 
 class FlatSnapshot:
@@ -48,7 +54,7 @@ class FlatSnapshot:
             qs[i].weight = q.weight
         # nodes
         nd = np.zeros(len(nodes), dtype=np.dtype(_abi.kbg_node))
-        labels, taints = [], []
+        labels, taints, ports = [], [], []
         for i, n in enumerate(nodes):
             obj = n.node or {}
             r = nd[i]
@@ -68,6 +74,16 @@ class FlatSnapshot:
             for t in obj.get("taints") or []:
                 taints.append((S(t.get("key")), S(t.get("value")), S(t.get("effect"))))
             r["taint_len"] = len(taints) - r["taint_off"]
+            # NodeInfo.UsedPorts over node.Pods(): a set, only hostPort > 0 is recorded (host_ports.go Add)
+            r["port_off"] = len(ports)
+            used = {}
+            for t in n.tasks.values():
+                for ip, proto, port in container_ports(t.pod):
+                    if port > 0:
+                        used.setdefault((ip or "0.0.0.0", proto or "TCP", port), None)
+            for ip, proto, port in used:
+                ports.append((S(ip), S(proto), port))
+            r["port_len"] = len(ports) - r["port_off"]
         self.node_names = [n.name for n in nodes]
         # jobs + tasks + specs
         jb = np.zeros(len(jobs), dtype=np.dtype(_abi.kbg_job))
@@ -101,12 +117,15 @@ class FlatSnapshot:
             tol_off = len(tols)
             for t in pod.get("tolerations") or []:
                 tols.append((S(t.get("key")), S(t.get("operator")), S(t.get("value")), S(t.get("effect"))))
-            has_ports = any((pt.get("hostPort") or 0) > 0
-                            for c in pod.get("containers", []) for pt in (c.get("ports") or []))
+            cports = container_ports(pod)
+            has_ports = any(port > 0 for _, _, port in cports)
+            port_off = len(ports)
+            for ip, proto, port in cports:
+                ports.append((S(ip), S(proto), port))
             has_pa = isinstance(aff, dict) and (aff.get("podAffinity") is not None or aff.get("podAntiAffinity") is not None)
             specs.append((sel_off, len(selectors) // 2 - sel_off, 1 if req is not None else 0, term_off,
                           len(terms) - term_off, tol_off, len(tols) - tol_off, 1 if has_ports else 0,
-                          1 if has_pa else 0))
+                          1 if has_pa else 0, port_off, len(ports) - port_off))
             sid = len(specs) - 1
             spec_ids[key] = sid
             return sid
@@ -147,7 +166,8 @@ class FlatSnapshot:
             values=np.asarray(values or [0], dtype=np.int32), tols=arr(_abi.kbg_toleration, tols),
             labels=np.asarray(labels or [0, 0], dtype=np.int32), taints=arr(_abi.kbg_taint, taints),
             selectors=np.asarray(selectors or [0, 0], dtype=np.int32),
-            plugins=arr(_abi.kbg_plugin_option, plugin_rows), tier_sizes=np.asarray(tier_sizes or [0], dtype=np.int32))
+            plugins=arr(_abi.kbg_plugin_option, plugin_rows), tier_sizes=np.asarray(tier_sizes or [0], dtype=np.int32),
+            ports=arr(_abi.kbg_host_port, ports))
         A = self.arrays
 
         def ptr(a, ctype):
@@ -173,4 +193,5 @@ class FlatSnapshot:
         snap.selectors, snap.n_selectors = ptr(A["selectors"], ctypes.c_int32), len(selectors) // 2
         snap.plugins, snap.n_plugins = ptr(A["plugins"], _abi.kbg_plugin_option), len(plugin_rows)
         snap.tier_sizes, snap.n_tiers = ptr(A["tier_sizes"], ctypes.c_int32), len(tier_sizes)
+        snap.ports, snap.n_ports = ptr(A["ports"], _abi.kbg_host_port), len(ports)
         self.snap = snap

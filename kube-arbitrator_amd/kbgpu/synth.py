@@ -150,6 +150,10 @@ def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8, be_frac=0.06):
             r["nvidia.com/gpu"] = rng.choice(["1", "2"])
         return r
 
+    def rand_ports():  # v1.ContainerPort host ports (vendor cache/host_ports.go semantics)
+        return [{"hostPort": rng.choice([80, 443, 0]), "protocol": rng.choice(["", "TCP", "UDP"]),
+                 "hostIP": rng.choice(["", "0.0.0.0", "10.0.0.1", "10.0.0.2"])} for _ in range(rng.randint(1, 2))]
+
     # remaining capacity per node, so that bound pods rarely overcommit a node
     # (an overcommitted node makes the reference panic in AddPod; ~3% keep that path)
     free = {n["name"]: [int(n["allocatable"]["cpu"]) * 1000, int(n["allocatable"]["memory"][:-2]) * 1024]
@@ -176,6 +180,8 @@ def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8, be_frac=0.06):
                    group=None if rng.random() < 0.5 else "pg-run", controller="rc-1" if rng.random() < 0.5 else None)
         if rng.random() < 0.35:
             p["deletionTimestamp"] = "2026-01-01T00:00:00Z"
+        if rng.random() < 0.2:
+            p["containers"][0]["ports"] = rand_ports()
         pods.append(p)
     nj = rng.randint(1, max_jobs)
     for j in range(nj):
@@ -220,6 +226,7 @@ def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8, be_frac=0.06):
                                     "operator": rng.choice(["Equal", "Exists", ""]),
                                     "value": rng.choice(["", "gpu"]),
                                     "effect": rng.choice(["", "NoSchedule", "NoExecute"])}]
+        ports = rand_ports() if rng.random() < 0.2 else None
         for t in range(ntask):
             req = job_req if rng.random() < 0.7 else rand_req()
             phase, node = "Pending", ""
@@ -231,6 +238,8 @@ def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8, be_frac=0.06):
             if rng.random() < 0.25:
                 p["priority"] = rng.choice([1, 5, 10])
             p.update(spec)
+            if ports:
+                p["containers"][0]["ports"] = ports
             pods.append(p)
     plugins = ["priority", "gang", "drf", "predicates", "proportion", "nodeorder"]
     rng.shuffle(plugins)

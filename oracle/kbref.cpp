@@ -15,7 +15,8 @@
 //   pkg/scheduler/plugins/{drf,proportion,gang,priority,predicates}
 //   pkg/scheduler/actions/allocate/allocate.go:41-176
 //   pkg/scheduler/actions/backfill/backfill.go:40-71 (fixture "actions": [..., "backfill"])
-//   vendor/k8s.io/kubernetes/pkg/scheduler/algorithm/predicates/predicates.go:797-862,1489-1517
+//   vendor/k8s.io/kubernetes/pkg/scheduler/algorithm/predicates/predicates.go:797-862,1031-1051,1489-1517
+//   vendor/k8s.io/kubernetes/pkg/scheduler/cache/host_ports.go:29-135, node_info.go:593-605 (host ports)
 //   vendor/k8s.io/kubernetes/pkg/apis/core/v1/helper/helpers.go:222-331,412-441
 //   vendor/k8s.io/api/core/v1/toleration.go:37-56
 //   vendor/k8s.io/apimachinery/pkg/labels/selector.go:134-236,849-866
@@ -33,8 +34,8 @@
 // order everywhere; SURVEY F4 makes that order an input of both sides.
 //
 // Not supported (the session is rejected with status "unsupported", the same
-// boundary the device path draws): pending pods with hostPort > 0, any pod
-// with PodAffinity/PodAntiAffinity while the predicates plugin is enabled.
+// boundary the device path draws): any pod with PodAffinity/PodAntiAffinity
+// while the predicates plugin is enabled.
 
 #include <algorithm>
 #include <chrono>
@@ -299,6 +300,8 @@ struct Pod {
   std::vector<Toleration> tolerations;
   std::vector<Value> containers_requests;
   bool has_host_port = false;
+  struct Port { std::string ip, protocol; int64_t port; };
+  std::vector<Port> ports;  // GetContainerPorts(pod) (vendor scheduler/util/utils.go:30-41)
   Resource resreq;
 };
 
@@ -365,8 +368,10 @@ static Pod parse_pod(const Value& v) {
     for (auto& c : cs->arr) {
       p.resreq.Add(new_resource(c.get("requests")));
       if (const Value* ports = c.get("ports"); ports && ports->is_arr())
-        for (auto& pt : ports->arr)
+        for (auto& pt : ports->arr) {
+          p.ports.push_back({pt.str("hostIP"), pt.str("protocol"), pt.integer("hostPort")});
           if (pt.integer("hostPort") > 0) p.has_host_port = true;
+        }
     }
   }
   return p;
@@ -741,7 +746,6 @@ struct Session {  // framework/session.go:35-61
   std::vector<std::pair<std::string, std::string>> binds;  // (ns/name, node) in dispatch order
   int64_t predicate_calls = 0;
   std::vector<TaskInfo*> evaluated;  // every task whose node loop ran, in order
-  bool be_host_port = false;         // a BestEffort Pending pod declares hostPort (predicates active)
 
   // session_plugins.go:142-156
   bool Overused(QueueInfo* q) {
@@ -1158,6 +1162,28 @@ struct Predicates {
     return r;
   }
   std::unordered_map<NodeInfo*, size_t> pos;
+  // PodFitsHostPorts(task.Pod, nil, NewNodeInfo(node.Pods()...)) — vendor
+  // predicates.go:1031-1051: every wanted port checked against the HostPortInfo
+  // of the pods on the node (host_ports.go CheckConflict; sanitize "" -> 0.0.0.0
+  // and TCP; port <= 0 is never recorded and never conflicts).
+  static bool fits_host_ports(TaskInfo* task, NodeInfo* node) {
+    const auto& want = task->pod->ports;
+    if (want.empty()) return true;
+    auto ip_of = [](const std::string& ip) { return ip.empty() ? std::string("0.0.0.0") : ip; };
+    auto proto_of = [](const std::string& p) { return p.empty() ? std::string("TCP") : p; };
+    for (auto& w : want) {
+      if (w.port <= 0) continue;
+      const std::string wip = ip_of(w.ip), wproto = proto_of(w.protocol);
+      for (auto& kv : node->tasks.items)
+        for (auto& e : kv.second->pod->ports) {
+          if (e.port <= 0 || e.port != w.port || proto_of(e.protocol) != wproto) continue;
+          const std::string eip = ip_of(e.ip);
+          if (wip == "0.0.0.0" || eip == "0.0.0.0" || eip == wip) return false;
+        }
+    }
+    return true;
+  }
+
   void open(Session* s, bool active) {
     ssn = s;
     for (size_t i = 0; i < s->nodes.size(); i++) pos[s->nodes[i]] = i;
@@ -1169,16 +1195,14 @@ struct Predicates {
         TaskInfo* t = kv.second;
         if (t->pod->has_pod_affinity || t->pod->has_pod_anti_affinity)
           throw Unsupported("pod (anti)affinity present: inter-pod affinity predicate not restated");
-        if (t->status == Pending && !t->resreq.IsEmpty() && t->pod->has_host_port)
-          throw Unsupported("pending pod declares hostPort: host-port predicate not restated");
-        if (t->status == Pending && t->resreq.IsEmpty() && t->pod->has_host_port) s->be_host_port = true;
         if (AllocatedStatus(t->status) && !s->nodeIndex.count(t->nodeName)) ghost = true;
       }
     s->predicateFns["predicates"] = [this](TaskInfo* task, NodeInfo* node) -> bool {
       // cache.NewNodeInfo(node.Pods()...).SetNode(node.Node): nil node => nil dereference
       if (!node->node) throw RefPanic("predicate on a NodeInfo without Node (nil dereference)");
       if (node->allocatable.MaxTaskNum <= (int)node->tasks.size()) return false;  // :125-127
-      if (!static_ok(task, node, pos[node])) return false;                       // :130-183
+      if (!static_ok(task, node, pos[node])) return false;                       // :130-141,158-183
+      if (!fits_host_ports(task, node)) return false;                            // :144-155
       if (faithful_scan) return affinity_ok_faithful(node);                       // :186-198
       return !ghost;
     };
@@ -1251,7 +1275,6 @@ static void allocate_execute(Session* ssn) {
 // Allocate removes the current task from it; removing the entry being visited
 // does not change which entries the range yields, so a copy is equivalent.
 static void backfill_execute(Session* ssn) {
-  if (ssn->be_host_port) throw Unsupported("BestEffort pending pod declares hostPort: host-port predicate not restated");
   for (JobInfo* job : ssn->jobs) {
     auto it = job->statusIndex.find(Pending);
     if (it == job->statusIndex.end()) continue;

@@ -202,6 +202,57 @@ KATS = {
                                 [1000000000000, 1000000000], [104857600000, 104857600], [1000000, 1000],
                                 [1, 1], [2560000, 2560], [1, 1], [0, 0]]},
     },
+    # vendor predicates.go:1031-1051 PodFitsHostPorts over NewNodeInfo(node.Pods()...),
+    # host_ports.go CheckConflict: "" ip = 0.0.0.0 and "" protocol = TCP (sanitize);
+    # a 0.0.0.0 side conflicts with every ip of the same (protocol, port), two
+    # concrete ips only when equal; hostPort <= 0 never conflicts. The pods on
+    # a node include pods outside any session job (web, dns: no PodGroup).
+    #   a 10.0.0.2:80/TCP  -> n1 (only 10.0.0.1:80 there)
+    #   b 0.0.0.0:80/TCP   -> n1 has TCP 80 -> n2
+    #   c 10.0.0.1:53/UDP  -> n1 (no UDP 53 on n1)
+    #   d 10.0.0.3:80/TCP  -> n1 (no 0.0.0.0:80 or 10.0.0.3:80 there)
+    #   e 10.0.0.1:53/UDP  -> n1 has it (c), n2 has 0.0.0.0:53/UDP -> n3
+    #   f :0 + 10.0.0.1:80 -> n1 has it, n2 has 0.0.0.0:80 (b) -> n3 (e is UDP)
+    #   g 0.0.0.0:80/UDP   -> n1
+    "kat_host_ports": {
+        "tiers": [[{"name": "predicates"}]],
+        "nodes": [node("n1", "8"), node("n2", "8"), node("n3", "8")],
+        "pods": [pod("web", "web", {"cpu": "1"}, ns="sys", group=None, phase="Running", node="n1",
+                     containers=[{"requests": {"cpu": "1"},
+                                  "ports": [{"hostIP": "10.0.0.1", "hostPort": 80, "protocol": "TCP"}]}]),
+                 pod("dns", "dns", {"cpu": "1"}, ns="sys", group=None, phase="Running", node="n2",
+                     containers=[{"requests": {"cpu": "1"}, "ports": [{"hostPort": 53, "protocol": "UDP"}]}])]
+                + [pod(u, "p" + u, {"cpu": "1"}, containers=[{"requests": {"cpu": "1"}, "ports": ports}])
+                   for u, ports in (("a", [{"hostIP": "10.0.0.2", "hostPort": 80}]),
+                                    ("b", [{"hostPort": 80}]),
+                                    ("c", [{"hostIP": "10.0.0.1", "hostPort": 53, "protocol": "UDP"}]),
+                                    ("d", [{"hostIP": "10.0.0.3", "hostPort": 80, "protocol": "TCP"}]),
+                                    ("e", [{"hostIP": "10.0.0.1", "hostPort": 53, "protocol": "UDP"}]),
+                                    ("f", [{"hostPort": 0}, {"hostIP": "10.0.0.1", "hostPort": 80}]),
+                                    ("g", [{"hostIP": "0.0.0.0", "hostPort": 80, "protocol": "UDP"}]))],
+        "podGroups": [pg()], "queues": Q,
+        "expected": {"decisions": [["a", "n1", "allocate"], ["b", "n2", "allocate"], ["c", "n1", "allocate"],
+                                   ["d", "n1", "allocate"], ["e", "n3", "allocate"], ["f", "n3", "allocate"],
+                                   ["g", "n1", "allocate"]]},
+    },
+    # backfill.go:40-71 after allocate (conf "allocate, backfill"): w (1 CPU)
+    # takes n1's last pod slot (cap 2 with the running pod) but pg1 needs 2
+    # (gang.go:72-78), so it is not dispatched; backfill puts BestEffort x
+    # (pg1) on n2 (n1 is at its pod cap, predicates.go:125-127) through
+    # ssn.Allocate, pg1 becomes ready and both are bound (session.go:283-290);
+    # y, z (pg2) follow on n2.
+    "kat_backfill": {
+        "actions": ["allocate", "backfill"],
+        "tiers": [[{"name": "gang"}], [{"name": "predicates"}]],
+        "nodes": [node("n1", "4", pods="2"), node("n2", "4")],
+        "pods": [pod("r", "run", {"cpu": "1"}, ns="sys", group=None, phase="Running", node="n1"),
+                 pod("w", "pw", {"cpu": "1"}), pod("x", "px", {}),
+                 pod("y", "py", {}, group="pg2"), pod("z", "pz", {}, group="pg2")],
+        "podGroups": [pg(minMember=2), pg("pg2")], "queues": Q,
+        "expected": {"decisions": [["w", "n1", "allocate"], ["x", "n2", "allocate"], ["y", "n2", "allocate"],
+                                   ["z", "n2", "allocate"]],
+                     "binds": {"ns/pw": "n1", "ns/px": "n2", "ns/py": "n2", "ns/pz": "n2"}},
+    },
 }
 
 

@@ -4,10 +4,12 @@ Decisions must be bit-exact (task -> node, Allocate/Pipeline kind, order,
 gang dispatch); drf/proportion shares within 1e-12 relative.
 """
 import copy
+import glob
+import os
 
 import pytest
 
-from helpers import compare_outputs, load_golden, run_oracle
+from helpers import GOLDEN, compare_outputs, load_golden, run_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -36,6 +38,25 @@ def test_reference_allocate_cases(case):
     assert got["binds"] == fx["expected"]["binds"]
     compare_outputs(run_oracle(fx), got)
     ssn.close()
+
+
+KATS = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "kat_*.json")))
+
+
+@pytest.mark.parametrize("name", KATS)
+def test_kats_through_device(name):
+    """Every hand-derived KAT session through the device path, against the
+    oracle (which tests/test_oracle_golden.py pins to the KAT's expectations)."""
+    fx = load_golden(name)
+    if fx.get("kind", "session") != "session":
+        pytest.skip("data-model KAT")
+    got, ssn = run_fixture(fx)
+    compare_outputs(run_oracle(fx), got)
+    if "decisions" in fx.get("expected", {}) and got["status"] == "ok":
+        assert [(d["task"], d["node"], d["kind"]) for d in got["decisions"]] \
+            == [tuple(x) for x in fx["expected"]["decisions"]]
+    if ssn:
+        ssn.close()
 
 
 def test_allocate_like_reference_test():
