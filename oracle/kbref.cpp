@@ -85,6 +85,9 @@ struct Resource {
     MilliGPU += rr.MilliGPU;
     return *this;
   }
+  bool Less(const Resource& rr) const {  // :138-140 (every dimension strictly less)
+    return MilliCPU < rr.MilliCPU && Memory < rr.Memory && MilliGPU < rr.MilliGPU;
+  }
   bool LessEqual(const Resource& rr) const {  // :142-146
     return (MilliCPU < rr.MilliCPU || std::fabs(rr.MilliCPU - MilliCPU) < kMinMilliCPU) &&
            (Memory < rr.Memory || std::fabs(rr.Memory - Memory) < kMinMemory) &&
@@ -716,7 +719,9 @@ struct PluginOption {
 };
 typedef std::vector<std::vector<PluginOption>> Tiers;
 
-struct Decision { TaskInfo* task; std::string node; int kind; int dispatched_at = -1; bool backfill = false; };
+struct Decision { TaskInfo* task; std::string node; int kind; int dispatched_at = -1; const char* action = ""; };
+// One committed eviction (cache.Evict), in commit order.
+struct Eviction { std::string task, by, action; };
 enum { KIND_ALLOCATE = 0, KIND_PIPELINE = 1 };
 
 struct Session;
@@ -739,6 +744,10 @@ struct Session {  // framework/session.go:35-61
   std::map<std::string, CompareFn> jobOrderFns, queueOrderFns, taskOrderFns;
   std::map<std::string, PredFn> predicateFns;
   std::map<std::string, ValidateFn> overusedFns, jobReadyFns;
+  typedef std::function<std::vector<TaskInfo*>(TaskInfo*, const std::vector<TaskInfo*>&)> VictimFn;
+  std::map<std::string, VictimFn> preemptableFns, reclaimableFns;
+  std::vector<Eviction> evictions;
+  const char* action = "";  // the action whose decisions are being logged
 
   // run-time bookkeeping for the decision log
   std::vector<Decision> decisions;
@@ -818,6 +827,53 @@ struct Session {  // framework/session.go:35-61
     return true;
   }
 
+  // session_plugins.go:59-140: the first tier with a registered, enabled fn
+  // decides; its fns' candidate lists are intersected in plugin order (Go nil
+  // slices: an empty result falls through to the next tier, where it stays empty).
+  std::vector<TaskInfo*> victims_of(bool preempt, TaskInfo* t, const std::vector<TaskInfo*>& tasks) {
+    std::vector<TaskInfo*> victims;
+    bool init = false;
+    for (auto& tier : tiers) {
+      for (auto& p : tier) {
+        if (preempt ? p.preemptableDisabled : p.reclaimableDisabled) continue;
+        auto& fns = preempt ? preemptableFns : reclaimableFns;
+        auto it = fns.find(p.name);
+        if (it == fns.end()) continue;
+        std::vector<TaskInfo*> cand = it->second(t, tasks);
+        if (!init) {
+          victims = cand;
+          init = true;
+        } else {
+          std::vector<TaskInfo*> inter;
+          for (TaskInfo* v : victims)
+            for (TaskInfo* c : cand)
+              if (v->uid == c->uid) inter.push_back(v);
+          victims = inter;
+        }
+      }
+      if (!victims.empty()) return victims;
+    }
+    return victims;
+  }
+  // job/node side of an eviction (session.go:323-349, statement.go:36-59):
+  // Releasing in the job, NodeInfo.UpdateTask on the node, DeallocateFunc
+  void evict_state(TaskInfo* reclaimee) {
+    auto jit = jobIndex.find(reclaimee->job);
+    if (jit != jobIndex.end()) jit->second->UpdateTaskStatus(reclaimee, Releasing);
+    auto nit = nodeIndex.find(reclaimee->nodeName);
+    if (nit != nodeIndex.end()) {
+      nit->second->RemoveTask(reclaimee);  // node_info.go:159-165
+      nit->second->AddTask(reclaimee);
+    }
+    for (auto& eh : eventHandlers)
+      if (eh.deallocate) eh.deallocate(reclaimee);
+  }
+  // session.go:318-352 (the fake cache's Evict succeeds and is recorded)
+  void Evict(TaskInfo* reclaimee, const std::string& by) {
+    evictions.push_back({reclaimee->uid, by, action});
+    evict_state(reclaimee);
+  }
+
   // session.go:295-316
   void dispatch(TaskInfo* task) {
     binds.emplace_back(pod_key(task->pod), task->nodeName);
@@ -834,7 +890,7 @@ struct Session {  // framework/session.go:35-61
     auto nit = nodeIndex.find(nodeHint->name);
     if (nit != nodeIndex.end()) nit->second->AddTask(task);
     decisionOf[task] = (int)decisions.size();
-    decisions.push_back({task, nodeHint->name, KIND_PIPELINE, -1});
+    decisions.push_back({task, nodeHint->name, KIND_PIPELINE, -1, action});
     for (auto& eh : eventHandlers)
       if (eh.allocate) eh.allocate(task);
   }
@@ -847,7 +903,7 @@ struct Session {  // framework/session.go:35-61
     auto nit = nodeIndex.find(nodeHint->name);
     if (nit != nodeIndex.end()) nit->second->AddTask(task);
     decisionOf[task] = (int)decisions.size();
-    decisions.push_back({task, nodeHint->name, KIND_ALLOCATE, -1});
+    decisions.push_back({task, nodeHint->name, KIND_ALLOCATE, -1, action});
     for (auto& eh : eventHandlers)
       if (eh.allocate) eh.allocate(task);
     if (!job) throw RefPanic("JobReady on nil job");
@@ -890,11 +946,38 @@ struct DRF {
       if (ls < rs) return -1;
       return 1;
     };
+    // drf.go:80-105: a preemptee is a victim when the preemptor job's share
+    // with the preemptor placed does not exceed the preemptee job's share with
+    // this and the earlier preemptees of that job removed (within 1e-6).
+    ssn->preemptableFns["drf"] = [this](TaskInfo* preemptor, const std::vector<TaskInfo*>& preemptees) {
+      std::vector<TaskInfo*> victims;
+      auto lit = opts.find(preemptor->job);
+      if (lit == opts.end()) throw RefPanic("drf: preemptor job has no attributes (nil dereference)");
+      Resource lalloc = lit->second.first;
+      lalloc.Add(preemptor->resreq);
+      const double ls = calc(lalloc);
+      std::map<std::string, Resource> allocations;
+      for (TaskInfo* p : preemptees) {
+        auto al = allocations.find(p->job);
+        if (al == allocations.end()) {
+          auto rit = opts.find(p->job);
+          if (rit == opts.end()) throw RefPanic("drf: preemptee job has no attributes (nil dereference)");
+          al = allocations.emplace(p->job, rit->second.first).first;
+        }
+        const double rs = calc(al->second.Sub(p->resreq));
+        if (ls < rs || std::fabs(ls - rs) <= 0.000001) victims.push_back(p);  // shareDelta drf.go:29
+      }
+      return victims;
+    };
     ssn->eventHandlers.push_back({[this](TaskInfo* t) {
       auto& a = opts[t->job];
       a.first.Add(t->resreq);
       a.second = calc(a.first);
-    }, nullptr});
+    }, [this](TaskInfo* t) {  // drf.go:140-148
+      auto& a = opts[t->job];
+      a.first.Sub(t->resreq);
+      a.second = calc(a.first);
+    }});
   }
 };
 
@@ -962,12 +1045,36 @@ struct Proportion {
       QueueAttr* a = *opts.find(((QueueInfo*)q)->uid);
       return a->deserved.LessEqual(a->allocated);
     };
+    // proportion.go:161-186: reclaimees of a queue are victims while the
+    // queue's allocation with them removed (cumulatively, in list order)
+    // still covers its deserved share; one the allocation cannot cover
+    // (Less: every dimension short) is skipped.
+    ssn->reclaimableFns["proportion"] = [this, ssn](TaskInfo*, const std::vector<TaskInfo*>& reclaimees) {
+      std::vector<TaskInfo*> victims;
+      std::map<std::string, Resource> allocations;
+      for (TaskInfo* r : reclaimees) {
+        JobInfo* job = ssn->jobIndex[r->job];
+        QueueAttr** ap = opts.find(job->queue);
+        if (!ap) throw RefPanic("proportion: reclaimee queue has no attributes (nil dereference)");
+        auto al = allocations.find(job->queue);
+        if (al == allocations.end()) al = allocations.emplace(job->queue, (*ap)->allocated).first;
+        if (al->second.Less(r->resreq)) continue;
+        al->second.Sub(r->resreq);
+        if ((*ap)->deserved.LessEqual(al->second)) victims.push_back(r);
+      }
+      return victims;
+    };
     ssn->eventHandlers.push_back({[this, ssn](TaskInfo* t) {
       JobInfo* job = ssn->jobIndex[t->job];
       QueueAttr* a = *opts.find(job->queue);
       a->allocated.Add(t->resreq);
       update_share(a);
-    }, nullptr});
+    }, [this, ssn](TaskInfo* t) {  // proportion.go:207-216
+      JobInfo* job = ssn->jobIndex[t->job];
+      QueueAttr* a = *opts.find(job->queue);
+      a->allocated.Sub(t->resreq);
+      update_share(a);
+    }});
   }
 };
 
@@ -995,6 +1102,19 @@ static void gang_open(Session* ssn) {
     return 1;
   };
   ssn->jobReadyFns["gang"] = [](void* j) { return jobReady((JobInfo*)j); };
+  // gang.go:104-127: a preemptee is a victim when its job stays at or above
+  // MinAvailable without it (registered for both preempt and reclaim)
+  Session::VictimFn fn = [ssn](TaskInfo*, const std::vector<TaskInfo*>& preemptees) {
+    std::vector<TaskInfo*> victims;
+    for (TaskInfo* p : preemptees) {
+      auto it = ssn->jobIndex.find(p->job);
+      if (it == ssn->jobIndex.end()) throw RefPanic("gang: preemptee job not in session (nil dereference)");
+      if (it->second->minAvailable <= readyTaskNum(it->second) - 1) victims.push_back(p);
+    }
+    return victims;
+  };
+  ssn->reclaimableFns["gang"] = fn;
+  ssn->preemptableFns["gang"] = fn;
 }
 
 // priority: pkg/scheduler/plugins/priority/priority.go:36-77
@@ -1284,12 +1404,213 @@ static void backfill_execute(Session* ssn) {
       if (!task->resreq.IsEmpty()) continue;  // "backfill for other case" is a TODO in v0.4
       for (NodeInfo* node : ssn->nodes) {
         if (!ssn->PredicateFn(task, node)) continue;
-        const size_t before = ssn->decisions.size();
         ssn->Allocate(task, node);
-        ssn->decisions[before].backfill = true;
         break;
       }
     }
+  }
+}
+
+// framework/statement.go:35-217. Evict/Pipeline change the session at once
+// and are recorded; Commit sends the evictions to the cache (recorded here);
+// Discard undoes in reverse order — unevict's node.AddTask finds the task
+// still on the node (it was re-added as Releasing) and fails, so the node
+// keeps it as Releasing while the job and the plugins see it Running again.
+struct Statement {
+  Session* ssn;
+  struct Op { bool evict; TaskInfo* task; std::string by; };
+  std::vector<Op> ops;
+  explicit Statement(Session* s) : ssn(s) {}
+  void Evict(TaskInfo* reclaimee, const std::string& by) {  // :35-67
+    ssn->evict_state(reclaimee);
+    ops.push_back({true, reclaimee, by});
+  }
+  void Pipeline(TaskInfo* task, NodeInfo* node) {  // :110-151
+    auto jit = ssn->jobIndex.find(task->job);
+    if (jit != ssn->jobIndex.end()) jit->second->UpdateTaskStatus(task, Pipelined);
+    task->nodeName = node->name;
+    auto nit = ssn->nodeIndex.find(node->name);
+    if (nit != ssn->nodeIndex.end()) nit->second->AddTask(task);
+    for (auto& eh : ssn->eventHandlers)
+      if (eh.allocate) eh.allocate(task);
+    ops.push_back({false, task, ""});
+  }
+  void Discard() {  // :194-205
+    for (size_t k = ops.size(); k-- > 0;) {
+      TaskInfo* t = ops[k].task;
+      auto jit = ssn->jobIndex.find(t->job);
+      auto nit = ssn->nodeIndex.find(t->nodeName);
+      if (ops[k].evict) {  // unevict :81-108
+        if (jit != ssn->jobIndex.end()) jit->second->UpdateTaskStatus(t, Running);
+        if (nit != ssn->nodeIndex.end()) nit->second->AddTask(t);  // already on the node: error, no change
+        for (auto& eh : ssn->eventHandlers)
+          if (eh.allocate) eh.allocate(t);
+      } else {  // unpipeline :156-192
+        if (jit != ssn->jobIndex.end()) jit->second->UpdateTaskStatus(t, Pending);
+        if (nit != ssn->nodeIndex.end()) nit->second->RemoveTask(t);
+        for (auto& eh : ssn->eventHandlers)
+          if (eh.deallocate) eh.deallocate(t);
+      }
+    }
+  }
+  void Commit() {  // :207-217
+    for (auto& op : ops) {
+      if (op.evict) ssn->evictions.push_back({op.task->uid, op.by, ssn->action});
+      else ssn->decisions.push_back({op.task, op.task->nodeName, KIND_PIPELINE, -1, ssn->action});
+    }
+  }
+};
+
+// preempt.go:182-240: the first node (ssn.Nodes order) whose PredicateFn
+// passes and whose filtered tasks yield validated victims; victims are evicted
+// in order until the request is covered, then the preemptor is pipelined.
+// Clones of the node's tasks are evicted (node.Tasks order = insertion order).
+static bool preempt_one(Session* ssn, Statement& stmt, TaskInfo* preemptor,
+                        const std::function<bool(TaskInfo*)>& filter) {
+  Resource resreq = preemptor->resreq;
+  for (NodeInfo* node : ssn->nodes) {
+    if (!ssn->PredicateFn(preemptor, node)) continue;
+    std::vector<TaskInfo*> preemptees;
+    for (auto& kv : node->tasks.items)
+      if (filter(kv.second)) preemptees.push_back(new TaskInfo(*kv.second));
+    std::vector<TaskInfo*> victims = ssn->victims_of(true, preemptor, preemptees);
+    if (victims.empty()) continue;  // validateVictims :242-253
+    Resource all;
+    for (TaskInfo* v : victims) all.Add(v->resreq);
+    if (all.Less(resreq)) continue;
+    for (TaskInfo* v : victims) {
+      stmt.Evict(v, preemptor->uid);
+      if (resreq.LessEqual(v->resreq)) break;
+      resreq.Sub(v->resreq);
+    }
+    stmt.Pipeline(preemptor, node);
+    return true;
+  }
+  return false;
+}
+
+static void preempt_execute(Session* ssn) {  // preempt.go:43-171
+  OMap<PriorityQueue<JobInfo>*> preemptorsMap;
+  std::unordered_map<std::string, PriorityQueue<TaskInfo>*> preemptorTasks;
+  std::vector<JobInfo*> underRequest;
+  std::vector<QueueInfo*> queues;
+  auto job_less = [ssn](JobInfo* l, JobInfo* r) { return ssn->JobOrderFn(l, r); };
+  auto task_less = [ssn](TaskInfo* l, TaskInfo* r) { return ssn->TaskOrderFn(l, r); };
+  for (JobInfo* job : ssn->jobs) {
+    auto q = ssn->queueIndex.find(job->queue);
+    if (q == ssn->queueIndex.end()) continue;
+    queues.push_back(q->second);
+    auto pit = job->statusIndex.find(Pending);
+    if (pit != job->statusIndex.end() && pit->second.size() != 0) {
+      if (!preemptorsMap.find(job->queue)) preemptorsMap.set(job->queue, new PriorityQueue<JobInfo>(job_less));
+      (*preemptorsMap.find(job->queue))->Push(job);
+      underRequest.push_back(job);
+      auto* tasks = new PriorityQueue<TaskInfo>(task_less);
+      for (auto& kv : pit->second.items) tasks->Push(kv.second);
+      preemptorTasks[job->uid] = tasks;
+    }
+  }
+  for (QueueInfo* queue : queues) {
+    for (;;) {  // preemption between jobs within the queue
+      PriorityQueue<JobInfo>** pp = preemptorsMap.find(queue->uid);
+      if (!pp || (*pp)->Empty()) break;
+      JobInfo* preemptorJob = (*pp)->Pop();
+      Statement stmt(ssn);
+      bool assigned = false;
+      for (;;) {
+        PriorityQueue<TaskInfo>* tasks = preemptorTasks[preemptorJob->uid];
+        if (tasks->Empty()) break;
+        TaskInfo* preemptor = tasks->Pop();
+        if (preempt_one(ssn, stmt, preemptor, [&](TaskInfo* t) {
+              if (t->status != Running) return false;
+              auto jit = ssn->jobIndex.find(t->job);
+              if (jit == ssn->jobIndex.end()) return false;
+              return jit->second->queue == preemptorJob->queue && preemptor->job != t->job;
+            }))
+          assigned = true;
+        if (ssn->JobReady(preemptorJob)) {
+          stmt.Commit();
+          break;
+        }
+      }
+      if (!ssn->JobReady(preemptorJob)) {
+        stmt.Discard();
+        continue;
+      }
+      if (assigned) (*pp)->Push(preemptorJob);
+    }
+    for (JobInfo* job : underRequest) {  // preemption between tasks within a job
+      for (;;) {
+        auto it = preemptorTasks.find(job->uid);
+        if (it == preemptorTasks.end() || it->second->Empty()) break;
+        TaskInfo* preemptor = it->second->Pop();
+        Statement stmt(ssn);
+        const bool assigned = preempt_one(ssn, stmt, preemptor, [&](TaskInfo* t) {
+          return t->status == Running && preemptor->job == t->job;
+        });
+        stmt.Commit();
+        if (!assigned) break;
+      }
+    }
+  }
+}
+
+static void reclaim_execute(Session* ssn) {  // reclaim.go:41-188
+  PriorityQueue<QueueInfo> queues([ssn](QueueInfo* l, QueueInfo* r) { return ssn->QueueOrderFn(l, r); });
+  OMap<PriorityQueue<JobInfo>*> preemptorsMap;
+  std::unordered_map<std::string, PriorityQueue<TaskInfo>*> preemptorTasks;
+  auto job_less = [ssn](JobInfo* l, JobInfo* r) { return ssn->JobOrderFn(l, r); };
+  auto task_less = [ssn](TaskInfo* l, TaskInfo* r) { return ssn->TaskOrderFn(l, r); };
+  for (JobInfo* job : ssn->jobs) {
+    auto q = ssn->queueIndex.find(job->queue);
+    if (q == ssn->queueIndex.end()) continue;
+    queues.Push(q->second);
+    auto pit = job->statusIndex.find(Pending);
+    if (pit != job->statusIndex.end() && pit->second.size() != 0) {
+      if (!preemptorsMap.find(job->queue)) preemptorsMap.set(job->queue, new PriorityQueue<JobInfo>(job_less));
+      (*preemptorsMap.find(job->queue))->Push(job);
+      auto* tasks = new PriorityQueue<TaskInfo>(task_less);
+      for (auto& kv : pit->second.items) tasks->Push(kv.second);
+      preemptorTasks[job->uid] = tasks;
+    }
+  }
+  for (;;) {
+    if (queues.Empty()) break;
+    QueueInfo* queue = queues.Pop();
+    if (ssn->Overused(queue)) continue;
+    PriorityQueue<JobInfo>** jp = preemptorsMap.find(queue->uid);
+    if (!jp || (*jp)->Empty()) continue;
+    JobInfo* job = (*jp)->Pop();
+    auto tit = preemptorTasks.find(job->uid);
+    if (tit == preemptorTasks.end() || tit->second->Empty()) continue;
+    TaskInfo* task = tit->second->Pop();
+    Resource resreq = task->resreq;
+    bool assigned = false;
+    for (NodeInfo* n : ssn->nodes) {
+      if (!ssn->PredicateFn(task, n)) continue;
+      std::vector<TaskInfo*> reclaimees;
+      for (auto& kv : n->tasks.items) {
+        TaskInfo* t = kv.second;
+        if (t->status != Running) continue;
+        auto jit = ssn->jobIndex.find(t->job);
+        if (jit == ssn->jobIndex.end()) continue;
+        if (jit->second->queue != job->queue) reclaimees.push_back(new TaskInfo(*t));
+      }
+      std::vector<TaskInfo*> victims = ssn->victims_of(false, task, reclaimees);
+      if (victims.empty()) continue;
+      Resource all;
+      for (TaskInfo* v : victims) all.Add(v->resreq);
+      if (all.Less(resreq)) continue;
+      for (TaskInfo* v : victims) {
+        ssn->Evict(v, task->uid);
+        if (resreq.LessEqual(v->resreq)) break;
+        resreq.Sub(v->resreq);
+      }
+      ssn->Pipeline(task, n);
+      assigned = true;
+      break;
+    }
+    if (assigned) queues.Push(queue);
   }
 }
 
@@ -1479,8 +1800,10 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache) {
   }
   auto t0 = std::chrono::steady_clock::now();
   for (auto& a : actions) {
-    if (a == "allocate") allocate_execute(ssn);
-    else if (a == "backfill") backfill_execute(ssn);
+    if (a == "allocate") { ssn->action = ""; allocate_execute(ssn); }
+    else if (a == "backfill") { ssn->action = "backfill"; backfill_execute(ssn); }
+    else if (a == "reclaim") { ssn->action = "reclaim"; reclaim_execute(ssn); }
+    else if (a == "preempt") { ssn->action = "preempt"; preempt_execute(ssn); }
     else throw BadInput("unsupported action " + a);
   }
   auto t1 = std::chrono::steady_clock::now();
@@ -1493,14 +1816,20 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache) {
     if (i) o += ",";
     o += "{\"task\":" + kbjson::quote(d.task->uid) + ",\"job\":" + kbjson::quote(d.task->job) +
          ",\"node\":" + kbjson::quote(d.node) + ",\"kind\":\"" + (d.kind == KIND_ALLOCATE ? "allocate" : "pipeline") +
-         "\",\"dispatched_at\":" + std::to_string(d.dispatched_at) + (d.backfill ? ",\"action\":\"backfill\"" : "") + "}";
+         "\",\"dispatched_at\":" + std::to_string(d.dispatched_at) + (*d.action ? ",\"action\":\"" + std::string(d.action) + "\"" : std::string()) + "}";
   }
   o += "],\"evaluated\":[";
   for (size_t i = 0; i < ssn->evaluated.size(); i++) o += (i ? "," : "") + kbjson::quote(ssn->evaluated[i]->uid);
   o += "],\"binds\":{";
   for (size_t i = 0; i < ssn->binds.size(); i++)
     o += (i ? "," : "") + kbjson::quote(ssn->binds[i].first) + ":" + kbjson::quote(ssn->binds[i].second);
-  o += "},\"jobs\":[";
+  o += "},\"evictions\":[";
+  for (size_t i = 0; i < ssn->evictions.size(); i++) {
+    auto& e = ssn->evictions[i];
+    o += (i ? "," : "") + std::string("{\"task\":") + kbjson::quote(e.task) + ",\"by\":" + kbjson::quote(e.by) +
+         ",\"action\":" + kbjson::quote(e.action) + "}";
+  }
+  o += "],\"jobs\":[";
   for (size_t i = 0; i < ssn->jobs.size(); i++) {
     JobInfo* j = ssn->jobs[i];
     o += (i ? "," : "");

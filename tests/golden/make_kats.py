@@ -29,6 +29,7 @@ def node(name, cpu, mem="64Gi", pods="110", **kw):
 
 
 Q = [{"name": "q", "weight": 1}]
+GI = 1024 ** 3
 
 
 def pg(name="pg1", ns="ns", minMember=0, created=0, queue="q"):
@@ -252,6 +253,62 @@ KATS = {
         "expected": {"decisions": [["w", "n1", "allocate"], ["x", "n2", "allocate"], ["y", "n2", "allocate"],
                                    ["z", "n2", "allocate"]],
                      "binds": {"ns/pw": "n1", "ns/px": "n2", "ns/py": "n2", "ns/pz": "n2"}},
+    },
+    # reclaim.go:41-188 with gang + proportion in one tier (session_plugins.go:59-98
+    # intersects them). CPU-only requests, so memory shares are Share(0,0)=0.
+    # proportion.go:102-144: total 4 CPU, q1 requests 4, q2 requests 2 -> both
+    # met in round 1 at 2 CPU deserved; q1 holds 4 (share 2, overused), q2 0.
+    # q2 pops first; b1 (1 CPU) on n1: gang keeps all of a1..a4 (A ready 4,
+    # MinMember 1); proportion's running allocation 4000 -> 3000 (victim: 2000
+    # <= 3000), 2000 (victim), 1000 (no), 0 (no) -> victims [a1, a2]; a1 covers
+    # the request (LessEqual), so only a1 is evicted and b1 is pipelined onto
+    # n1 (session.go:205-241). Job B is not pushed back (reclaim.go:96-101).
+    "kat_reclaim": {
+        "actions": ["reclaim"],
+        "tiers": [[{"name": "gang"}, {"name": "proportion"}, {"name": "predicates"}]],
+        "nodes": [node("n1", "4", "8Gi")],
+        "pods": [pod(u, "p" + u, {"cpu": "1"}, group="pgA", ns="na", phase="Running", node="n1")
+                 for u in ("a1", "a2", "a3", "a4")]
+                + [pod(u, "p" + u, {"cpu": "1"}, group="pgB", ns="nb") for u in ("b1", "b2")],
+        "podGroups": [pg("pgA", ns="na", minMember=1, queue="q1"), pg("pgB", ns="nb", minMember=1, queue="q2")],
+        "queues": [{"name": "q1", "weight": 1}, {"name": "q2", "weight": 1}],
+        "expected": {"decisions": [["b1", "n1", "pipeline"]], "evictions": [["a1", "b1"]],
+                     "nodes": {"n1": [[0, 8 * GI, 0], [0, 0, 0], 5]}},
+    },
+    # preempt.go:43-171, within one queue: P (MinMember 2) preempts V
+    # (MinMember 2, 4 running on the full node). gang decides in tier 1
+    # (priority has no preemptable fn): V stays >= 2 without the victim while
+    # it has 4 then 3 ready tasks. p1 evicts v1 (one victim covers 1 CPU) and
+    # is pipelined; P is not ready (1 < 2) so p2 goes next and evicts v2; P is
+    # ready, the statement commits (statement.go:207-217).
+    "kat_preempt": {
+        "actions": ["preempt"],
+        "tiers": [[{"name": "priority"}, {"name": "gang"}], [{"name": "drf"}, {"name": "predicates"}]],
+        "nodes": [node("n1", "4", "8Gi")],
+        "pods": [pod(u, "p" + u, {"cpu": "1"}, group="pgV", phase="Running", node="n1")
+                 for u in ("v1", "v2", "v3", "v4")]
+                + [pod(u, "p" + u, {"cpu": "1"}, group="pgP") for u in ("p1", "p2")],
+        "podGroups": [pg("pgV", minMember=2), pg("pgP", minMember=2)], "queues": Q,
+        "expected": {"decisions": [["p1", "n1", "pipeline"], ["p2", "n1", "pipeline"]],
+                     "evictions": [["v1", "p1"], ["v2", "p2"]],
+                     "nodes": {"n1": [[0, 8 * GI, 0], [0, 0, 0], 6]}},
+    },
+    # The same with P needing 3: after p1, p2 P is still short, the statement
+    # is discarded (statement.go:194-205). unpipeline removes p1, p2 from the
+    # node (Releasing += 1 CPU each, node_info.go:131-157); unevict's
+    # node.AddTask finds v1, v2 still there as Releasing and fails
+    # (node_info.go:101-106), so the node keeps 2 CPU Releasing while the job
+    # sees them Running again. Nothing is committed.
+    "kat_preempt_discard": {
+        "actions": ["preempt"],
+        "tiers": [[{"name": "priority"}, {"name": "gang"}], [{"name": "drf"}, {"name": "predicates"}]],
+        "nodes": [node("n1", "4", "8Gi")],
+        "pods": [pod(u, "p" + u, {"cpu": "1"}, group="pgV", phase="Running", node="n1")
+                 for u in ("v1", "v2", "v3", "v4")]
+                + [pod(u, "p" + u, {"cpu": "1"}, group="pgP") for u in ("p1", "p2")],
+        "podGroups": [pg("pgV", minMember=2), pg("pgP", minMember=3)], "queues": Q,
+        "expected": {"decisions": [], "evictions": [],
+                     "nodes": {"n1": [[0, 8 * GI, 0], [2000, 0, 0], 4]}},
     },
 }
 

@@ -36,6 +36,11 @@ def test_kats(path):
         assert {j["uid"]: j["ready"] for j in out["jobs"]} == exp["ready"]
     if "fit_error" in exp:
         assert {j["uid"]: j["fit_error"] for j in out["jobs"]} == exp["fit_error"]
+    if "evictions" in exp:
+        assert [[e["task"], e["by"]] for e in out["evictions"]] == exp["evictions"]
+    if "nodes" in exp:
+        got = {n["name"]: [n["idle"], n["releasing"], n["ntasks"]] for n in out["nodes"]}
+        assert {k: got[k] for k in exp["nodes"]} == exp["nodes"]
 
 
 def test_faithful_scan_mode_agrees():
