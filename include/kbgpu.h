@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KBG_ABI_VERSION 3
+#define KBG_ABI_VERSION 4
 
 typedef enum kbg_status {
   KBG_OK = 0,
@@ -98,6 +98,9 @@ typedef struct kbg_node {
   int32_t port_off, port_len;   /* NodeInfo.UsedPorts(): every container port of the pods on the
                                    node (node.Pods(), node_info.go:181-187 -> vendor
                                    cache/node_info.go:593-605), ports[port_off ..] */
+  int32_t task_off, task_len;   /* the session-job tasks in NodeInfo.Tasks, in its (insertion) order:
+                                   node_tasks[task_off ..] are indices into tasks. preempt/reclaim
+                                   take victims in this order (preempt.go:199-206, reclaim.go:113-126) */
 } kbg_node;
 
 /* One v1.ContainerPort as HostPortInfo sees it (vendor cache/host_ports.go). */
@@ -187,6 +190,7 @@ typedef struct kbg_snapshot {
   const kbg_plugin_option* plugins; int32_t n_plugins;
   const int32_t* tier_sizes;       int32_t n_tiers;     /* plugins grouped by tier, in order */
   const kbg_host_port* ports;      int32_t n_ports;
+  const int32_t* node_tasks;       int32_t n_node_tasks;
 } kbg_snapshot;
 
 typedef struct kbg_options {
@@ -261,6 +265,10 @@ typedef struct kbg_stats {
                               integer <= 2^51); 0 = the reference's LessEqual expression */
   double exchange_ms;      /* summed HIP-event time of the per-batch RCCL all-gather */
   double backfill_ms;      /* wall time of the last kbg_backfill */
+  double reclaim_ms;       /* wall time of the last kbg_reclaim */
+  double preempt_ms;       /* wall time of the last kbg_preempt */
+  int64_t victim_scans;    /* victim-scan kernel launches (one per preemptor / reclaimer tried) */
+  double victim_kernel_ms; /* summed HIP-event time of the victim-scan kernel */
 } kbg_stats;
 
 typedef struct kbg_session kbg_session;
@@ -313,6 +321,35 @@ kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t*
  * earlier Allocate decisions of its job. Writes the cycle's whole decision
  * log (allocate's decisions first, dispatched_at updated) to `out`. */
 kbg_status kbg_backfill(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out);
+
+/* reclaimAction.Execute (reclaim.go:41-188) and preemptAction.Execute
+ * (preempt.go:43-253) on the same cycle, in the conf's action order (the
+ * reference's full conf is "reclaim, allocate, backfill, preempt"). Every
+ * node a reclaimer / preemptor is tried on is evaluated on the device in one
+ * victim-scan launch: PredicateFn, the filtered Running tasks of the node in
+ * NodeInfo.Tasks order, the victim fns of the deciding tier
+ * (session_plugins.go:59-140: gang, drf / gang, proportion) and
+ * validateVictims; the host then evicts on the first such node exactly as the
+ * reference does and pipelines the task. Statements (preempt) commit or
+ * discard as statement.go does, including the node-side quirk of unevict.
+ * Both write the cycle's decision log (pipelines carry the action); the
+ * evictions are read with kbg_evictions_get. Sessions with host ports or
+ * node-axis shards are refused (KBG_E_UNSUPPORTED). */
+kbg_status kbg_reclaim(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out);
+kbg_status kbg_preempt(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out);
+
+/* One committed eviction (cache.Evict), in commit order. */
+typedef struct kbg_eviction {
+  int32_t task;   /* the evicted task (index into tasks) */
+  int32_t by;     /* the reclaimer / preemptor task */
+  int32_t action; /* KBG_ACTION_RECLAIM or KBG_ACTION_PREEMPT */
+  int32_t reserved;
+} kbg_eviction;
+enum { KBG_ACTION_ALLOCATE = 0, KBG_ACTION_BACKFILL = 1, KBG_ACTION_RECLAIM = 2, KBG_ACTION_PREEMPT = 3 };
+/* out == NULL with cap == 0 only reports the count in *n_out. */
+kbg_status kbg_evictions_get(kbg_session* s, kbg_eviction* out, int32_t cap, int32_t* n_out);
+/* The action that produced decision i of the cycle's log (KBG_ACTION_*). */
+kbg_status kbg_decision_actions_get(kbg_session* s, int32_t* out, int32_t cap, int32_t* n_out);
 
 /* Restores the state captured at kbg_session_open (device-side copy); used to
  * re-run a cycle on the same snapshot without re-uploading it. */

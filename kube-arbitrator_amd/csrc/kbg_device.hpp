@@ -71,6 +71,51 @@ struct MaskDelta {
 };
 constexpr int32_t kMaskDeltaCap = 8192;
 
+// ---- preempt / reclaim victim scan (preempt.go:182-240, reclaim.go:106-135)
+enum VictimPlugin : int32_t { VP_GANG = 1, VP_DRF = 2, VP_PROP = 4 };
+enum VictimMode : int32_t { VM_PREEMPT_JOBS = 0, VM_PREEMPT_TASKS = 1, VM_RECLAIM = 2 };
+constexpr int kMaxVictimTiers = 8;
+constexpr int kMaxNodeCandidates = 128;  // victim candidates per node (two 64-bit masks)
+
+// One reclaimer / preemptor against every node.
+struct VictimScan {
+  int32_t n_nodes, W, cls, cap_check;  // n_nodes: global N
+  int32_t node_lo, node_n;             // node range this launch covers (the shard's node table, tab_lo based)
+  int32_t mode;                        // VictimMode
+  int32_t n_tiers;                     // tiers holding an enabled victim fn, in order
+  int32_t tier_fns[kMaxVictimTiers];   // VictimPlugin bits of each (every fn keeps the preemptee order,
+                                       // so the intersection does not depend on the fns' order)
+  int32_t job, queue;                  // the preemptor's
+  double req[3];                       // its Resreq
+  double ls;                           // drf: its job's share with it placed
+};
+
+struct VictimTables {
+  const int32_t* ntasks;        // node table rows (node - VictimScan.node_lo)
+  const int32_t* maxtasks;
+  const uint8_t* panic_node;    // nil Node under an active predicates plugin
+  const uint64_t* class_mask;
+  const int32_t* nt_off;        // [N+1] candidate lists: session tasks Running on the node at open
+  const int32_t* nt_task;       //       in NodeInfo.Tasks order
+  const int32_t* t_job;         // per task
+  const double* t_req;          // [T][3]
+  uint8_t* t_run;               // node-side status still Running
+  const int32_t* j_queue;       // per job
+  const int32_t* j_min;
+  int32_t* j_ready;             // gang readyTaskNum
+  double* j_alloc;              // [J][3] drf attr.allocated
+  double* q_alloc;              // [Q][3] proportion attr.allocated
+  const double* q_deserved;     // [Q][3]
+  double drf_total[3];
+};
+
+// A host-side change to the victim tables.
+struct StateDelta {
+  int32_t kind;   // 0 task running flag, 1 job ready, 2 job drf alloc, 3 queue alloc
+  int32_t index;
+  double v[3];
+};
+
 // ---- static predicate programs (built on host, evaluated on device) ----
 enum ReqKind : int32_t {
   REQ_FALSE = 0,
@@ -157,5 +202,12 @@ hipError_t launch_select(const uint64_t* bits, int32_t W, int32_t Wl, int32_t n_
 
 hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream);
 hipError_t launch_mask_apply(uint64_t* class_mask, const MaskDelta* deltas, int32_t n_deltas, hipStream_t stream);
+
+// Writes min over nodes of (node << 1 | panic) for the nodes where the
+// reference would stop (validated victims, or a panic) into *out (preset to
+// UINT32_MAX by the caller's memset on the same stream).
+hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* out, hipStream_t stream,
+                              hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+hipError_t launch_state_apply(const VictimTables& t, const StateDelta* d, int32_t n, hipStream_t stream);
 
 }  // namespace kbg

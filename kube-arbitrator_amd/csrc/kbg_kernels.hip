@@ -277,6 +277,170 @@ hipError_t launch_mask_apply(uint64_t* class_mask, const MaskDelta* deltas, int3
   return hipGetLastError();
 }
 
+// --------------------------------------------------------- victim scan
+// resource_info.go:138-146 on [3] arrays
+__device__ __forceinline__ bool res_le3(const double* r, const double* a) {
+  return le(r[0], a[0], kMinMilliCPU) && le(r[1], a[1], kMinMemory) && le(r[2], a[2], kMinMilliGPU);
+}
+__device__ __forceinline__ bool res_less3(const double* r, const double* a) {
+  return r[0] < a[0] && r[1] < a[1] && r[2] < a[2];
+}
+// drf.go:156-166 with helpers.Share
+__device__ __forceinline__ double share3(const double* a, const double* tot) {
+  double res = 0;
+  for (int d = 0; d < 3; ++d) {
+    const double s = tot[d] == 0 ? (a[d] == 0 ? 0.0 : 1.0) : a[d] / tot[d];
+    if (s > res) res = s;
+  }
+  return res;
+}
+
+// One thread per node, in ssn.Nodes order; the lowest node where the
+// reference stops (validated victims, or a panic inside PredicateFn or a
+// victim fn) wins. Candidates are the session tasks Running on the node at
+// open, in NodeInfo.Tasks order (at most kMaxNodeCandidates; the host checks).
+// Cumulative per-job (drf.go:87-100) / per-queue (proportion.go:166-183)
+// allocations are replayed from the node's list head for every candidate, so
+// each subtraction happens in the reference's order.
+__global__ __launch_bounds__(256) void kbg_victim_kernel(VictimScan p, VictimTables t, uint32_t* __restrict__ out) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= p.node_n) return;
+  const int n = p.node_lo + row;
+  if (!((t.class_mask[(size_t)p.cls * p.W + (n >> 6)] >> (n & 63)) & 1ull)) return;  // static predicate
+  if (t.panic_node[n]) {  // SetNode(nil) inside PredicateFn (predicates.go:122-123)
+    atomicMin(out, ((uint32_t)n << 1) | 1u);
+    return;
+  }
+  if (p.cap_check && t.ntasks[row] >= t.maxtasks[row]) return;  // predicates.go:125-127
+  const int off = t.nt_off[n];
+  const int L = t.nt_off[n + 1] - off;
+  uint64_t pm[2] = {0ull, 0ull};  // preemptees: filtered Running tasks
+  for (int k = 0; k < L; ++k) {
+    const int task = t.nt_task[off + k];
+    if (!t.t_run[task]) continue;
+    const int jv = t.t_job[task];
+    bool f;
+    if (p.mode == VM_PREEMPT_JOBS) f = t.j_queue[jv] == p.queue && jv != p.job;  // preempt.go:100-112
+    else if (p.mode == VM_PREEMPT_TASKS) f = jv == p.job;                      // :146-154
+    else f = t.j_queue[jv] != p.queue;                                          // reclaim.go:113-126
+    if (f) pm[k >> 6] |= 1ull << (k & 63);
+  }
+  if (!(pm[0] | pm[1])) return;  // no preemptee: every fn returns nil
+  bool panic = false;
+  uint64_t vm[2] = {0ull, 0ull};
+  for (int ti = 0; ti < p.n_tiers && !panic; ++ti) {
+    const int fns = p.tier_fns[ti];
+    uint64_t tm[2] = {pm[0], pm[1]};
+    if (fns & VP_GANG) {  // gang.go:104-124
+      uint64_t c[2] = {0ull, 0ull};
+      for (int k = 0; k < L; ++k) {
+        if (!((pm[k >> 6] >> (k & 63)) & 1ull)) continue;
+        const int jv = t.t_job[t.nt_task[off + k]];
+        if (t.j_min[jv] <= t.j_ready[jv] - 1) c[k >> 6] |= 1ull << (k & 63);
+      }
+      tm[0] &= c[0];
+      tm[1] &= c[1];
+    }
+    if (fns & VP_DRF) {  // drf.go:80-105
+      uint64_t c[2] = {0ull, 0ull};
+      for (int k = 0; k < L && !panic; ++k) {
+        if (!((pm[k >> 6] >> (k & 63)) & 1ull)) continue;
+        const int jv = t.t_job[t.nt_task[off + k]];
+        double x[3] = {t.j_alloc[3 * jv], t.j_alloc[3 * jv + 1], t.j_alloc[3 * jv + 2]};
+        for (int k2 = 0; k2 <= k && !panic; ++k2) {
+          if (!((pm[k2 >> 6] >> (k2 & 63)) & 1ull)) continue;
+          const int t2 = t.nt_task[off + k2];
+          if (t.t_job[t2] != jv) continue;
+          const double* r = t.t_req + 3 * (size_t)t2;
+          if (!res_le3(r, x)) panic = true;  // Resource.Sub (resource_info.go:100-110)
+          x[0] -= r[0];
+          x[1] -= r[1];
+          x[2] -= r[2];
+        }
+        const double rs = share3(x, t.drf_total);
+        if (p.ls < rs || fabs(p.ls - rs) <= 0.000001) c[k >> 6] |= 1ull << (k & 63);
+      }
+      tm[0] &= c[0];
+      tm[1] &= c[1];
+    }
+    if (fns & VP_PROP) {  // proportion.go:161-186
+      uint64_t c[2] = {0ull, 0ull};
+      for (int k = 0; k < L && !panic; ++k) {
+        if (!((pm[k >> 6] >> (k & 63)) & 1ull)) continue;
+        const int q = t.j_queue[t.t_job[t.nt_task[off + k]]];
+        double x[3] = {t.q_alloc[3 * q], t.q_alloc[3 * q + 1], t.q_alloc[3 * q + 2]};
+        bool victim = false;
+        for (int k2 = 0; k2 <= k && !panic; ++k2) {
+          if (!((pm[k2 >> 6] >> (k2 & 63)) & 1ull)) continue;
+          const int t2 = t.nt_task[off + k2];
+          if (t.j_queue[t.t_job[t2]] != q) continue;
+          const double* r = t.t_req + 3 * (size_t)t2;
+          if (res_less3(x, r)) continue;  // skipped, allocation untouched
+          if (!res_le3(r, x)) panic = true;
+          x[0] -= r[0];
+          x[1] -= r[1];
+          x[2] -= r[2];
+          if (k2 == k) victim = res_le3(t.q_deserved + 3 * q, x);
+        }
+        if (victim) c[k >> 6] |= 1ull << (k & 63);
+      }
+      tm[0] &= c[0];
+      tm[1] &= c[1];
+    }
+    if (tm[0] | tm[1]) {  // the host passes only the deciding tier (session_plugins.go:59-98)
+      vm[0] = tm[0];
+      vm[1] = tm[1];
+      break;
+    }
+  }
+  if (panic) {
+    atomicMin(out, ((uint32_t)n << 1) | 1u);
+    return;
+  }
+  if (!(vm[0] | vm[1])) return;
+  double all[3] = {0.0, 0.0, 0.0};  // validateVictims (preempt.go:242-253)
+  for (int k = 0; k < L; ++k) {
+    if (!((vm[k >> 6] >> (k & 63)) & 1ull)) continue;
+    const double* r = t.t_req + 3 * (size_t)t.nt_task[off + k];
+    all[0] += r[0];
+    all[1] += r[1];
+    all[2] += r[2];
+  }
+  if (res_less3(all, p.req)) return;
+  atomicMin(out, (uint32_t)n << 1);
+}
+
+hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* out, hipStream_t stream,
+                              hipEvent_t start, hipEvent_t stop) {
+  if (p.node_n <= 0) return hipSuccess;
+  hipExtLaunchKernelGGL(kbg_victim_kernel, dim3((p.node_n + 255) / 256), dim3(256), 0, stream, start, stop, 0, p, t,
+                        out);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void kbg_state_apply_kernel(VictimTables t, const StateDelta* __restrict__ d,
+                                                              int32_t n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const StateDelta x = d[i];
+  switch (x.kind) {
+    case 0: t.t_run[x.index] = (uint8_t)(x.v[0] != 0.0); break;
+    case 1: t.j_ready[x.index] = (int32_t)x.v[0]; break;
+    case 2:
+      for (int k = 0; k < 3; ++k) t.j_alloc[3 * (size_t)x.index + k] = x.v[k];
+      break;
+    case 3:
+      for (int k = 0; k < 3; ++k) t.q_alloc[3 * (size_t)x.index + k] = x.v[k];
+      break;
+  }
+}
+
+hipError_t launch_state_apply(const VictimTables& t, const StateDelta* d, int32_t n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kbg_state_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, t, d, n);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------- static mask
 // One lane = one (class, node) pair; vendor predicates.go:807-850 (selector +
 // required node affinity), predicates.go:105-110 (unschedulable),

@@ -348,6 +348,28 @@ struct Ops {
   }
 };
 
+// allocate.go:45-59: one queue entry per job (queue heap) and every job in
+// its queue's job heap, keyed from E's plugin state.
+void build_heaps(const Session& S, Engine& E) {
+  E.jheap.assign((size_t)S.n_jobs + S.n_queues, kbg::kJobKeySentinel);
+  E.jlen.assign(S.n_queues, 0);
+  E.qheap.assign((size_t)S.n_jobs + 1, S.n_queues);
+  E.qlen = 0;
+  Ops ops{S, E};
+  E.qorder.resize(S.n_queues);
+  std::iota(E.qorder.begin(), E.qorder.end(), 0);
+  std::sort(E.qorder.begin(), E.qorder.end(), [&](int32_t a, int32_t b) { return ops.queue_less_slow(a, b); });
+  E.qrank.assign(S.n_queues + 1, INT32_MAX);  // [n_queues]: the heap sentinel
+  for (int32_t i = 0; i < S.n_queues; ++i) E.qrank[E.qorder[i]] = i;
+  for (int32_t j = 0; j < S.n_jobs; ++j) {
+    ops.qpush(S.job_queue[j]);
+    const int32_t q = S.job_queue[j];
+    E.jheap[S.joff[q] + E.jlen[q]++] = make_job_key(S, E, j);
+  }
+  for (int32_t q = 0; q < S.n_queues; ++q)  // a sorted array is a valid min-heap
+    std::sort(E.jheap.begin() + S.joff[q], E.jheap.begin() + S.joff[q] + E.jlen[q]);
+}
+
 struct ShapeKey {
   int32_t cls;
   double c, m, g;
@@ -420,6 +442,11 @@ void free_device(Session& S) {
   if (S.h_deltas) (void)hipHostFree(S.h_deltas);
   if (S.h_mdeltas) (void)hipHostFree(S.h_mdeltas);
   S.h_mdeltas = nullptr;
+  if (S.h_vout) (void)hipHostFree(S.h_vout);
+  if (S.h_sdeltas) (void)hipHostFree(S.h_sdeltas);
+  S.h_vout = nullptr;
+  S.h_sdeltas = nullptr;
+  S.vt_ready = false;
   S.h_tasks = nullptr;
   S.h_cand = S.h_count = nullptr;
   S.h_deltas = nullptr;
@@ -851,6 +878,12 @@ kbg_status validate(const kbg_snapshot* s) {
   for (int32_t i = 0; i < s->n_values; ++i)
     if (!in(s->values[i], NS)) return fail(KBG_E_INVALID, "value");
   if (s->n_ports < 0 || (s->n_ports > 0 && !s->ports)) return fail(KBG_E_INVALID, "ports");
+  if (s->n_node_tasks < 0 || (s->n_node_tasks > 0 && !s->node_tasks)) return fail(KBG_E_INVALID, "node_tasks");
+  for (int32_t i = 0; i < s->n_nodes; ++i)
+    if (!range(s->nodes[i].task_off, s->nodes[i].task_len, s->n_node_tasks))
+      return fail(KBG_E_INVALID, "node task list " + std::to_string(i));
+  for (int32_t i = 0; i < s->n_node_tasks; ++i)
+    if (!in(s->node_tasks[i], s->n_tasks)) return fail(KBG_E_INVALID, "node task index");
   for (int32_t i = 0; i < s->n_ports; ++i)
     if (!in(s->ports[i].host_ip, NS) || !in(s->ports[i].protocol, NS)) return fail(KBG_E_INVALID, "port");
   for (int32_t i = 0; i < s->n_tolerations; ++i) {
@@ -949,6 +982,26 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
           if (!(f & KBG_DISABLE_PREDICATE)) S.pred_active = true;
         }
       }
+    // victim fns per tier (session_plugins.go:59-140): gang and drf register
+    // preemptable fns, gang and proportion reclaimable ones (gang.go:104-127,
+    // drf.go:80-107, proportion.go:161-186)
+    p = 0;
+    for (int32_t ti = 0; ti < snap->n_tiers; ++ti) {
+      int32_t pre = 0, rec = 0;
+      for (int32_t k = 0; k < snap->tier_sizes[ti]; ++k, ++p) {
+        const std::string& name = S.strs[snap->plugins[p].name];
+        const uint32_t f = snap->plugins[p].flags;
+        if (name == "gang" && !(f & KBG_DISABLE_PREEMPTABLE)) pre |= kbg::VP_GANG;
+        if (name == "drf" && !(f & KBG_DISABLE_PREEMPTABLE)) pre |= kbg::VP_DRF;
+        if (name == "gang" && !(f & KBG_DISABLE_RECLAIMABLE)) rec |= kbg::VP_GANG;
+        if (name == "proportion" && !(f & KBG_DISABLE_RECLAIMABLE)) rec |= kbg::VP_PROP;
+      }
+      // `init` outlives the tier loop (session_plugins.go:60-61, 115-131):
+      // once a tier has run a fn, later tiers intersect with its result, so
+      // an empty result stays empty and the first tier with a fn decides alone
+      if (pre && S.tier_preempt.empty()) S.tier_preempt.push_back(pre);
+      if (rec && S.tier_reclaim.empty()) S.tier_reclaim.push_back(rec);
+    }
   }
 
   // ---- ranks, tasks
@@ -1016,6 +1069,29 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.idle0 = S.idle;
   S.rel0 = S.rel;
   S.ntasks0 = S.ntasks;
+  // victim candidates (preempt/reclaim): session tasks Running on each node,
+  // in NodeInfo.Tasks order; a task's node by NodeName (ssn.NodeIndex)
+  {
+    std::unordered_map<int32_t, int32_t> node_of;
+    for (int32_t n = 0; n < N; ++n) node_of[S.canon[S.nodes_in[n].name]] = n;
+    S.task_node.assign(S.n_tasks, -1);
+    for (int32_t t = 0; t < S.n_tasks; ++t) {
+      auto it = node_of.find(S.canon[S.tasks_in[t].node_name]);
+      if (it != node_of.end()) S.task_node[t] = it->second;
+    }
+    S.nt_off.assign(N + 1, 0);
+    S.nt_task.clear();
+    S.max_candidates = 0;
+    for (int32_t n = 0; n < N; ++n) {
+      const kbg_node& nd = S.nodes_in[n];
+      for (int32_t i = 0; i < nd.task_len; ++i) {
+        const int32_t t = snap->node_tasks[nd.task_off + i];
+        if (S.tasks_in[t].status == KBG_RUNNING) S.nt_task.push_back(t);
+      }
+      S.nt_off[n + 1] = (int32_t)S.nt_task.size();
+      S.max_candidates = std::max(S.max_candidates, S.nt_off[n + 1] - S.nt_off[n]);
+    }
+  }
 
   // ---- engine initial state
   Engine& E = S.init;
@@ -1136,25 +1212,10 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.jcap.assign(S.n_queues, 0);
   for (int32_t j = 0; j < S.n_jobs; ++j) S.jcap[S.job_queue[j]]++;
   for (int32_t q = 1; q < S.n_queues; ++q) S.joff[q] = S.joff[q - 1] + S.jcap[q - 1] + 1;
-  E.jheap.assign((size_t)S.n_jobs + S.n_queues, kbg::kJobKeySentinel);
-  E.jlen.assign(S.n_queues, 0);
-  E.qheap.assign((size_t)S.n_jobs + 1, S.n_queues);
-  E.qlen = 0;
-  {
-    Ops ops{S, E};
-    E.qorder.resize(S.n_queues);
-    std::iota(E.qorder.begin(), E.qorder.end(), 0);
-    std::sort(E.qorder.begin(), E.qorder.end(), [&](int32_t a, int32_t b) { return ops.queue_less_slow(a, b); });
-    E.qrank.assign(S.n_queues + 1, INT32_MAX);  // [n_queues]: the heap sentinel
-    for (int32_t i = 0; i < S.n_queues; ++i) E.qrank[E.qorder[i]] = i;
-    for (int32_t j = 0; j < S.n_jobs; ++j) {
-      ops.qpush(S.job_queue[j]);  // allocate.go:48-59: one queue entry per job
-      const int32_t q = S.job_queue[j];
-      E.jheap[S.joff[q] + E.jlen[q]++] = make_job_key(S, E, j);
-    }
-    for (int32_t q = 0; q < S.n_queues; ++q)  // a sorted array is a valid min-heap
-      std::sort(E.jheap.begin() + S.joff[q], E.jheap.begin() + S.joff[q] + E.jlen[q]);
-  }
+  S.pend_all = S.pend;
+  S.pend_off_all = S.pend_off;
+  S.pend_len_all = S.pend_len;
+  build_heaps(S, E);
 
   // ---- static predicates
   kbg::StaticHost sh;
@@ -1412,7 +1473,54 @@ void begin_cycle(Session& S) {
   S.committed_ready = S.job_ready0;
   S.fin = S.init;
   S.fit.assign(S.n_jobs, Session::FitCounts{});
+  const kbg_stats prev = S.stats;
+  S.stats = kbg_stats{};
+  S.stats.n_classes = prev.n_classes;
+  S.stats.shards = prev.shards;
+  S.stats.shard_index = prev.shard_index;
+  S.stats.int_scan = prev.int_scan;
+  S.stats.open_ms = prev.open_ms;
+  S.dec_action.clear();
+  S.evictions.clear();
+  S.tstat.resize(S.n_tasks);
+  for (int32_t t = 0; t < S.n_tasks; ++t) S.tstat[t] = S.tasks_in[t].status;
+  S.trun.assign(S.n_tasks, 0);
+  for (int32_t t : S.nt_task) S.trun[t] = 1;
+  S.pend = S.pend_all;
+  S.pend_off = S.pend_off_all;
+  S.pend_len = S.pend_len_all;
   S.cycle_started = true;
+}
+
+// The allocate engine's starting state when an earlier action of the cycle
+// (reclaim) changed the session: plugin state and readiness as they are now,
+// the pending lists without the tasks that left Pending, fresh heaps.
+Engine live_engine(Session& S) {
+  Engine E;
+  E.jalloc = S.fin.jalloc;
+  E.jshare = S.fin.jshare;
+  E.jready = S.committed_ready;
+  E.qalloc = S.fin.qalloc;
+  E.qshare = S.fin.qshare;
+  E.cursor.assign(S.n_jobs, 0);
+  S.pend.clear();
+  for (int32_t j = 0; j < S.n_jobs; ++j) {
+    S.pend_off[j] = (int32_t)S.pend.size();
+    for (int32_t k = 0; k < S.pend_len_all[j]; ++k) {
+      const int32_t t = S.pend_all[S.pend_off_all[j] + k];
+      if (S.tstat[t] == KBG_PENDING) S.pend.push_back(t);
+    }
+    S.pend_len[j] = (int32_t)S.pend.size() - S.pend_off[j];
+  }
+  build_heaps(S, E);
+  return E;
+}
+
+// Appends a decision to the cycle's log (no gang bookkeeping).
+void append_log(Session& S, int32_t t, int32_t node, int32_t kind) {
+  S.dec.push_back(kbg_decision{t, node, kind, -1});
+  S.undisp_next.push_back(-1);
+  S.dec_action.push_back(S.action);
 }
 
 // Appends one committed decision to the log and runs the gang part of
@@ -1422,14 +1530,17 @@ void begin_cycle(Session& S) {
 void record_decision(Session& S, int32_t t, int32_t node, int32_t kind) {
   const int32_t j = S.task_job[t];
   const int32_t di = (int32_t)S.dec.size();
-  S.dec.push_back(kbg_decision{t, node, kind, -1});
-  S.undisp_next.push_back(-1);
+  append_log(S, t, node, kind);
   S.committed_ready[j]++;
+  S.tstat[t] = kind == KBG_KIND_ALLOCATE ? KBG_ALLOCATED : KBG_PIPELINED;
   if (kind == KBG_KIND_ALLOCATE) {
     S.undisp_next[di] = S.undisp_head[j];
     S.undisp_head[j] = di;
     if (!S.ready_gang || S.committed_ready[j] >= S.jobs_in[j].min_available) {
-      for (int32_t d = S.undisp_head[j]; d >= 0; d = S.undisp_next[d]) S.dec[d].dispatched_at = di;
+      for (int32_t d = S.undisp_head[j]; d >= 0; d = S.undisp_next[d]) {
+        S.dec[d].dispatched_at = di;
+        S.tstat[S.dec[d].task] = KBG_BINDING;  // dispatch (session.go:295-316)
+      }
       S.undisp_head[j] = -1;
     }
   }
@@ -1446,24 +1557,21 @@ kbg_status copy_log(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out, 
 }
 
 kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
-  if (S.cycle_started)
-    return fail(KBG_E_INVALID, "an action already ran on this session (allocate runs first); call kbg_session_reset");
-  begin_cycle(S);
+  if (S.allocated || S.backfilled || S.preempted)
+    return fail(KBG_E_INVALID, "allocate runs once per cycle, before backfill and preempt; call kbg_session_reset");
+  const bool first = !S.cycle_started;  // else reclaim ran first: start from the live state
+  if (first) begin_cycle(S);
+  S.action = KBG_ACTION_ALLOCATE;
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   const auto t0 = clk::now();
-  const kbg_stats prev = S.stats;
-  S.stats = kbg_stats{};
-  S.stats.n_classes = prev.n_classes;
-  S.stats.shards = prev.shards;
-  S.stats.shard_index = prev.shard_index;
-  S.stats.int_scan = prev.int_scan;
-  S.stats.open_ms = prev.open_ms;
 
   std::vector<kbg_decision>& dec = S.dec;
-  std::vector<Res> dec_old;  // the Idle (Allocate) or Releasing (Pipeline) row before each decision
-  dec_old.reserve(S.pend.size());
-  std::vector<uint64_t> dec_oldp;  // host ports: the node's used-port atoms before each decision
+  // the Idle (Allocate) or Releasing (Pipeline) row before each decision
+  // (indexed by decision; earlier actions' decisions are never undone)
+  std::vector<Res> dec_old(dec.size());
+  dec_old.reserve(dec.size() + S.pend.size());
+  std::vector<uint64_t> dec_oldp(dec.size() * (size_t)S.PW);  // host ports: used-port atoms before each decision
   std::vector<LastEval> last(S.n_jobs);
   // shapes known to fit nowhere (monotone): written by the committer, read by the predictor
   std::unique_ptr<std::atomic<uint8_t>[]> failed(new std::atomic<uint8_t>[std::max(1, S.n_shapes)]);
@@ -1477,7 +1585,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
 
   // ------------------------------------------------------------ predictor
   Pipe P;
-  Engine E = S.init;
+  Engine E = first ? S.init : live_engine(S);
   double engine_ms = 0;
   int64_t replayed = 0;
   std::string pred_error;
@@ -1710,14 +1818,16 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
 // resolved in order exactly like allocate's rows, with no prediction.
 kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
   using clk = std::chrono::steady_clock;
-  if (S.backfilled) return fail(KBG_E_INVALID, "kbg_backfill already ran on this session; call kbg_session_reset");
+  if (S.backfilled || S.preempted)
+    return fail(KBG_E_INVALID, "backfill runs once per cycle, before preempt; call kbg_session_reset");
   const auto t0 = clk::now();
   if (!S.cycle_started) begin_cycle(S);
   S.backfilled = true;
+  S.action = KBG_ACTION_BACKFILL;
   std::vector<int32_t> be;
   for (int32_t j = 0; j < S.n_jobs; ++j)
     for (int32_t k = S.jt_off[j]; k < S.jt_off[j + 1]; ++k)
-      if (S.be_task[S.jt[k]]) be.push_back(S.jt[k]);
+      if (S.be_task[S.jt[k]] && S.tstat[S.jt[k]] == KBG_PENDING) be.push_back(S.jt[k]);
   std::vector<int32_t> mark(S.n_nodes, -1), touched;
   int32_t stamp = 0;
   Grouper grouper(S);
@@ -1785,6 +1895,563 @@ kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   }
   HIP_TRY(hipStreamSynchronize(S.stream));
   S.stats.backfill_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  return copy_log(S, out, cap, n_out, result);
+}
+
+// ====================================================== preempt / reclaim
+// preempt.go:43-253, reclaim.go:41-188, statement.go:35-217, session.go:318-352.
+// The node loop of every reclaimer / preemptor runs on the device (one
+// victim-scan launch over all nodes); the host replays the reference's
+// control flow and, on the node the device names, its exact victim
+// selection, eviction loop and pipeline.
+
+void vt_delta(Session& S, int32_t kind, int32_t index, double a, double b, double c) {
+  S.sdeltas.push_back(kbg::StateDelta{kind, index, {a, b, c}});
+}
+
+// Applies the queued state changes. Each carries the entry's new value, so
+// only the last one of an entry is kept (the apply kernel writes in parallel).
+kbg_status vt_flush(Session& S) {
+  if (S.sdeltas.empty()) return KBG_OK;
+  {
+    std::unordered_set<int64_t> seen;
+    std::vector<kbg::StateDelta> uniq;
+    for (size_t i = S.sdeltas.size(); i-- > 0;)
+      if (seen.insert(((int64_t)S.sdeltas[i].kind << 32) | (uint32_t)S.sdeltas[i].index).second)
+        uniq.push_back(S.sdeltas[i]);
+    S.sdeltas.swap(uniq);
+  }
+  for (size_t m = 0; m < S.sdeltas.size();) {
+    const int32_t cnt = (int32_t)std::min<size_t>(S.sdeltas.size() - m, (size_t)kbg::kMaskDeltaCap);
+    std::memcpy(S.h_sdeltas, S.sdeltas.data() + m, (size_t)cnt * sizeof(kbg::StateDelta));
+    HIP_TRY(hipMemcpyAsync(S.d_sdeltas, S.h_sdeltas, (size_t)cnt * sizeof(kbg::StateDelta), hipMemcpyHostToDevice,
+                           S.stream));
+    HIP_TRY(kbg::launch_state_apply(S.vt, S.d_sdeltas, cnt, S.stream));
+    HIP_TRY(hipStreamSynchronize(S.stream));  // the staging buffer is reused next
+    m += cnt;
+  }
+  S.sdeltas.clear();
+  return KBG_OK;
+}
+
+// Device copies of the victim tables; the live parts (running flags, gang
+// readiness, drf / proportion allocations) are re-uploaded at every action.
+kbg_status vt_setup(Session& S) {
+  const size_t T = (size_t)std::max(1, S.n_tasks), J = (size_t)std::max(1, S.n_jobs),
+               Q = (size_t)std::max(1, S.n_queues);
+  kbg_status st;
+  if (!S.vt_ready) {
+    kbg::VictimTables& v = S.vt;
+    v.ntasks = S.d_nodes.ntasks;
+    v.maxtasks = S.d_nodes.maxtasks;
+    v.class_mask = S.d_class_mask;
+    std::vector<uint8_t> pn(S.panic_node.begin(), S.panic_node.end());
+    std::vector<int32_t> jq(S.job_queue), jm(S.n_jobs);
+    for (int32_t j = 0; j < S.n_jobs; ++j) jm[j] = S.jobs_in[j].min_available;
+    std::vector<double> tr(3 * T, 0.0), qd(3 * Q, 0.0);
+    for (int32_t t = 0; t < S.n_tasks; ++t) {
+      tr[3 * t] = S.treq[t].c;
+      tr[3 * t + 1] = S.treq[t].m;
+      tr[3 * t + 2] = S.treq[t].g;
+    }
+    for (int32_t q = 0; q < S.n_queues; ++q) {
+      qd[3 * q] = S.q_deserved[q].c;
+      qd[3 * q + 1] = S.q_deserved[q].m;
+      qd[3 * q + 2] = S.q_deserved[q].g;
+    }
+    uint8_t *dpn, *drun;
+    int32_t *doff, *dtask, *djob, *djq, *djm, *djr;
+    double *dtr, *dja, *dqa, *dqd;
+    std::vector<int32_t> tj(S.task_job);
+    if ((st = hupload(S, &dpn, pn)) || (st = hupload(S, &doff, S.nt_off)) || (st = hupload(S, &dtask, S.nt_task)) ||
+        (st = hupload(S, &djob, tj)) || (st = hupload(S, &dtr, tr)) || (st = dalloc(S, &drun, T)) ||
+        (st = hupload(S, &djq, jq)) || (st = hupload(S, &djm, jm)) || (st = dalloc(S, &djr, J)) ||
+        (st = dalloc(S, &dja, 3 * J)) || (st = dalloc(S, &dqa, 3 * Q)) || (st = hupload(S, &dqd, qd)) ||
+        (st = dalloc(S, &S.d_vout, 1)) || (st = dalloc(S, &S.d_sdeltas, kbg::kMaskDeltaCap)))
+      return st;
+    HIP_TRY(hipHostMalloc((void**)&S.h_vout, sizeof(uint32_t), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&S.h_sdeltas, (size_t)kbg::kMaskDeltaCap * sizeof(kbg::StateDelta),
+                          hipHostMallocDefault));
+    v.panic_node = dpn;
+    v.nt_off = doff;
+    v.nt_task = dtask;
+    v.t_job = djob;
+    v.t_req = dtr;
+    v.t_run = drun;
+    v.j_queue = djq;
+    v.j_min = djm;
+    v.j_ready = djr;
+    v.j_alloc = dja;
+    v.q_alloc = dqa;
+    v.q_deserved = dqd;
+    v.drf_total[0] = S.drf_total.c;
+    v.drf_total[1] = S.drf_total.m;
+    v.drf_total[2] = S.drf_total.g;
+    S.vt_ready = true;
+    HIP_TRY(hipStreamSynchronize(S.stream));  // host vectors end here
+  }
+  // live state
+  std::vector<double> ja(3 * J, 0.0), qa(3 * Q, 0.0);
+  for (int32_t j = 0; j < S.n_jobs; ++j) {
+    ja[3 * j] = S.fin.jalloc[j].c;
+    ja[3 * j + 1] = S.fin.jalloc[j].m;
+    ja[3 * j + 2] = S.fin.jalloc[j].g;
+  }
+  for (int32_t q = 0; q < S.n_queues; ++q) {
+    qa[3 * q] = S.fin.qalloc[q].c;
+    qa[3 * q + 1] = S.fin.qalloc[q].m;
+    qa[3 * q + 2] = S.fin.qalloc[q].g;
+  }
+  HIP_TRY(hipMemcpyAsync(S.vt.t_run, S.trun.data(), S.trun.size(), hipMemcpyHostToDevice, S.stream));
+  HIP_TRY(hipMemcpyAsync(S.vt.j_ready, S.committed_ready.data(), (size_t)S.n_jobs * 4, hipMemcpyHostToDevice,
+                         S.stream));
+  HIP_TRY(hipMemcpyAsync(S.vt.j_alloc, ja.data(), ja.size() * 8, hipMemcpyHostToDevice, S.stream));
+  HIP_TRY(hipMemcpyAsync(S.vt.q_alloc, qa.data(), qa.size() * 8, hipMemcpyHostToDevice, S.stream));
+  HIP_TRY(hipStreamSynchronize(S.stream));
+  S.sdeltas.clear();
+  S.fin.jready = S.committed_ready;  // the job order keys read the live readiness
+  return KBG_OK;
+}
+
+// The plugin and gang state an event changes (drf.go:130-148,
+// proportion.go:196-216, gang readiness), mirrored to the victim tables.
+struct Live {
+  Session& S;
+  std::vector<int32_t>& touched;
+  std::vector<int32_t>& mark;
+  int32_t stamp;
+  void touch(int32_t n) {
+    if (n >= 0 && mark[n] != stamp) {
+      mark[n] = stamp;
+      touched.push_back(n);
+    }
+  }
+  void ready(int32_t j, int32_t d) {
+    S.committed_ready[j] += d;
+    S.fin.jready[j] = S.committed_ready[j];
+    vt_delta(S, 1, j, (double)S.committed_ready[j], 0, 0);
+  }
+  // AllocateFunc (+) / DeallocateFunc (-); false when Sub would panic
+  bool plugins(int32_t t, bool add) {
+    const int32_t j = S.task_job[t];
+    const Res& r = S.treq[t];
+    if (S.has_drf) {
+      Res& a = S.fin.jalloc[j];
+      if (add) kbg::res_add(a, r);
+      else if (!kbg::res_sub(a, r)) return false;
+      S.fin.jshare[j] = share_of(a, S.drf_total);
+      vt_delta(S, 2, j, a.c, a.m, a.g);
+    }
+    if (S.has_prop) {
+      const int32_t q = S.job_queue[j];
+      Res& a = S.fin.qalloc[q];
+      if (add) kbg::res_add(a, r);
+      else if (!kbg::res_sub(a, r)) return false;
+      S.fin.qshare[q] = share_of(a, S.q_deserved[q]);
+      vt_delta(S, 3, q, a.c, a.m, a.g);
+    }
+    return true;
+  }
+  // job Releasing, NodeInfo.UpdateTask (Running copy out, Releasing copy
+  // in), DeallocateFunc (session.go:323-349, statement.go:36-59)
+  bool evict(int32_t v) {
+    const int32_t j = S.task_job[v];
+    if (ready_status(S.tstat[v])) ready(j, -1);
+    S.tstat[v] = KBG_RELEASING;
+    const int32_t n = S.task_node[v];
+    if (n >= 0) {
+      if (!S.nil_node[n]) {
+        const Res& r = S.treq[v];
+        kbg::res_add(S.idle[n], r);                    // RemoveTask (node_info.go:148)
+        kbg::res_add(S.rel[n], r);                     // AddTask as Releasing (:115-116)
+        if (!kbg::res_sub(S.idle[n], r)) return false;
+      }
+      touch(n);
+    }
+    S.trun[v] = 0;
+    vt_delta(S, 0, v, 0, 0, 0);
+    return plugins(v, false);
+  }
+  // job Pipelined, NodeInfo.AddTask as Pipelined, AllocateFunc (session.go:205-241, statement.go:110-151)
+  bool pipeline(int32_t t, int32_t n) {
+    const int32_t j = S.task_job[t];
+    if (!ready_status(S.tstat[t])) ready(j, +1);
+    S.tstat[t] = KBG_PIPELINED;
+    if (!S.nil_node[n] && !kbg::res_sub(S.rel[n], S.treq[t])) return false;  // node_info.go:117-118
+    S.ntasks[n]++;
+    touch(n);
+    return plugins(t, true);
+  }
+  // statement.go:81-108: job Running again; node.AddTask fails (the task is
+  // still there, as Releasing), so the node is unchanged; AllocateFunc
+  void unevict(int32_t v) {
+    const int32_t j = S.task_job[v];
+    S.tstat[v] = KBG_RUNNING;
+    ready(j, +1);
+    plugins(v, true);
+  }
+  // statement.go:156-192: job Pending; node.RemoveTask; DeallocateFunc
+  bool unpipeline(int32_t t, int32_t n) {
+    const int32_t j = S.task_job[t];
+    ready(j, -1);
+    S.tstat[t] = KBG_PENDING;
+    if (!S.nil_node[n]) kbg::res_add(S.rel[n], S.treq[t]);  // node_info.go:145-146
+    S.ntasks[n]--;
+    touch(n);
+    return plugins(t, false);
+  }
+};
+
+// Victims of `t` on node n, exactly as the reference builds them: the
+// filtered Running tasks in NodeInfo.Tasks order, then the victim fns of the
+// deciding tier (session_plugins.go:59-140). false = a fn would panic.
+bool host_victims(Session& S, int32_t mode, int32_t t, int32_t n, std::vector<int32_t>* victims) {
+  const int32_t pj = S.task_job[t], pq = S.job_queue[pj];
+  std::vector<int32_t> pre;
+  for (int32_t k = S.nt_off[n]; k < S.nt_off[n + 1]; ++k) {
+    const int32_t v = S.nt_task[k];
+    if (!S.trun[v]) continue;
+    const int32_t jv = S.task_job[v];
+    bool f;
+    if (mode == kbg::VM_PREEMPT_JOBS) f = S.job_queue[jv] == pq && jv != pj;
+    else if (mode == kbg::VM_PREEMPT_TASKS) f = jv == pj;
+    else f = S.job_queue[jv] != pq;
+    if (f) pre.push_back(v);
+  }
+  victims->clear();
+  if (pre.empty()) return true;
+  const std::vector<int32_t>& tiers = mode == kbg::VM_RECLAIM ? S.tier_reclaim : S.tier_preempt;
+  for (int32_t fns : tiers) {
+    std::vector<char> keep(pre.size(), 1);
+    if (fns & kbg::VP_GANG)  // gang.go:104-124
+      for (size_t i = 0; i < pre.size(); ++i) {
+        const int32_t jv = S.task_job[pre[i]];
+        if (!(S.jobs_in[jv].min_available <= S.committed_ready[jv] - 1)) keep[i] = 0;
+      }
+    if (fns & kbg::VP_DRF) {  // drf.go:80-105
+      Res la = S.fin.jalloc[pj];
+      kbg::res_add(la, S.treq[t]);
+      const double ls = share_of(la, S.drf_total);
+      std::unordered_map<int32_t, Res> alloc;
+      for (size_t i = 0; i < pre.size(); ++i) {
+        const int32_t jv = S.task_job[pre[i]];
+        auto it = alloc.emplace(jv, S.fin.jalloc[jv]).first;
+        if (!kbg::res_sub(it->second, S.treq[pre[i]])) return false;
+        const double rs = share_of(it->second, S.drf_total);
+        if (!(ls < rs || std::fabs(ls - rs) <= 0.000001)) keep[i] = 0;
+      }
+    }
+    if (fns & kbg::VP_PROP) {  // proportion.go:161-186
+      std::unordered_map<int32_t, Res> alloc;
+      for (size_t i = 0; i < pre.size(); ++i) {
+        const int32_t q = S.job_queue[S.task_job[pre[i]]];
+        auto it = alloc.emplace(q, S.fin.qalloc[q]).first;
+        const Res& r = S.treq[pre[i]];
+        Res& a = it->second;
+        if (a.c < r.c && a.m < r.m && a.g < r.g) {  // Resource.Less: skipped
+          keep[i] = 0;
+          continue;
+        }
+        if (!kbg::res_sub(a, r)) return false;
+        if (!kbg::res_le(S.q_deserved[q], a)) keep[i] = 0;
+      }
+    }
+    for (size_t i = 0; i < pre.size(); ++i)
+      if (keep[i]) victims->push_back(pre[i]);
+    if (!victims->empty()) return true;
+  }
+  return true;
+}
+
+// One statement (statement.go); a null statement is the session itself
+// (reclaim uses ssn.Evict / ssn.Pipeline directly).
+struct Stmt {
+  struct Op {
+    bool evict;
+    int32_t task, node, by;
+  };
+  std::vector<Op> ops;
+};
+
+enum { TRY_NONE = 0, TRY_ASSIGNED = 1 };
+
+// preempt.go:174-240 / reclaim.go:106-176 for one task: the device finds the
+// first node where the reference stops; the host evicts there and pipelines.
+kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, int32_t* outcome) {
+  using clk = std::chrono::steady_clock;
+  *outcome = TRY_NONE;
+  kbg::VictimScan p{};
+  p.n_nodes = S.n_nodes;
+  p.node_lo = S.tab_lo;  // a node-axis shard scans its own nodes; the lowest stop is min-reduced over ranks
+  p.node_n = S.tab_n;
+  p.W = S.W;
+  p.cls = S.task_class[t];
+  p.cap_check = S.pred_active ? 1 : 0;
+  p.mode = mode;
+  const std::vector<int32_t>& tiers = mode == kbg::VM_RECLAIM ? S.tier_reclaim : S.tier_preempt;
+  p.n_tiers = (int32_t)tiers.size();
+  for (int32_t i = 0; i < p.n_tiers; ++i) p.tier_fns[i] = tiers[i];
+  const int32_t pj = S.task_job[t];
+  p.job = pj;
+  p.queue = S.job_queue[pj];
+  p.req[0] = S.treq[t].c;
+  p.req[1] = S.treq[t].m;
+  p.req[2] = S.treq[t].g;
+  Res la = S.fin.jalloc[pj];
+  kbg::res_add(la, S.treq[t]);
+  p.ls = share_of(la, S.drf_total);
+  kbg_status st = vt_flush(S);
+  if (st != KBG_OK) return st;
+  HIP_TRY(hipMemsetAsync(S.d_vout, 0xff, sizeof(uint32_t), S.stream));
+  HIP_TRY(kbg::launch_victim_scan(p, S.vt, S.d_vout, S.stream, S.ev[0], S.ev[1]));
+  if (S.comm) {
+    const ncclResult_t nr = ncclAllReduce(S.d_vout, S.d_vout, 1, ncclUint32, ncclMin, S.comm->nccl, S.stream);
+    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+  }
+  HIP_TRY(hipMemcpyAsync(S.h_vout, S.d_vout, sizeof(uint32_t), hipMemcpyDeviceToHost, S.stream));
+  HIP_TRY(hipStreamSynchronize(S.stream));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, S.ev[0], S.ev[1]));
+  S.stats.victim_kernel_ms += ms;
+  S.stats.victim_scans++;
+  const uint32_t key = *S.h_vout;
+  if (key == UINT32_MAX) return KBG_OK;  // no node: the task stays Pending
+  const int32_t n = (int32_t)(key >> 1);
+  if (key & 1u)
+    return fail(KBG_E_REF_PANIC, "victim selection panics on node " + S.strs[S.nodes_in[n].name] +
+                                     " (nil Node or Resource.Sub underflow in a victim fn)");
+  std::vector<int32_t> victims;
+  if (!host_victims(S, mode, t, n, &victims) || victims.empty())
+    return fail(KBG_E_INVALID, "internal: device and host victim selection disagree");
+  Res all{};
+  for (int32_t v : victims) kbg::res_add(all, S.treq[v]);
+  const Res& req = S.treq[t];
+  if (all.c < req.c && all.m < req.m && all.g < req.g)
+    return fail(KBG_E_INVALID, "internal: device and host victim validation disagree");
+  Res resreq = req;
+  for (int32_t v : victims) {
+    if (stmt) stmt->ops.push_back({true, v, -1, t});
+    else S.evictions.push_back(kbg_eviction{v, t, S.action, 0});
+    if (!L.evict(v)) return fail(KBG_E_REF_PANIC, "eviction: Resource.Sub underflow (resource_info.go:100-110)");
+    if (kbg::res_le(resreq, S.treq[v])) break;  // preempt.go:221-224
+    if (!kbg::res_sub(resreq, S.treq[v])) return fail(KBG_E_REF_PANIC, "preempt: resreq.Sub underflow (preempt.go:225)");
+  }
+  if (!L.pipeline(t, n)) return fail(KBG_E_REF_PANIC, "pipeline: Releasing.Sub underflow (node_info.go:117-118)");
+  if (stmt) stmt->ops.push_back({false, t, n, -1});
+  else append_log(S, t, n, KBG_KIND_PIPELINE);
+  (void)clk::now();
+  *outcome = TRY_ASSIGNED;
+  return KBG_OK;
+}
+
+void stmt_commit(Session& S, Stmt& stmt) {  // statement.go:207-217
+  for (auto& op : stmt.ops) {
+    if (op.evict) S.evictions.push_back(kbg_eviction{op.task, op.by, S.action, 0});
+    else append_log(S, op.task, op.node, KBG_KIND_PIPELINE);
+  }
+  stmt.ops.clear();
+}
+
+bool stmt_discard(Session& S, Live& L, Stmt& stmt) {  // statement.go:194-205
+  bool ok = true;
+  for (size_t k = stmt.ops.size(); k-- > 0;) {
+    const Stmt::Op& op = stmt.ops[k];
+    if (op.evict) L.unevict(op.task);
+    else ok = L.unpipeline(op.task, op.node) && ok;
+  }
+  stmt.ops.clear();
+  return ok;
+}
+
+// Per job, its Pending tasks in TaskOrderFn order (a strict order, so the
+// util.PriorityQueue pop sequence is this sorted order).
+std::vector<std::vector<int32_t>> pending_by_job(const Session& S) {
+  std::vector<std::vector<int32_t>> out(S.n_jobs);
+  for (int32_t j = 0; j < S.n_jobs; ++j) {
+    for (int32_t k = S.jt_off[j]; k < S.jt_off[j + 1]; ++k)
+      if (S.tstat[S.jt[k]] == KBG_PENDING) out[j].push_back(S.jt[k]);
+    std::sort(out[j].begin(), out[j].end(), [&](int32_t a, int32_t c) {
+      if (S.task_order_prio && S.tasks_in[a].priority != S.tasks_in[c].priority)
+        return S.tasks_in[a].priority > S.tasks_in[c].priority;
+      return S.task_rank[a] < S.task_rank[c];
+    });
+  }
+  return out;
+}
+
+kbg_status victim_action_check(Session& S) {
+  if (S.has_ports) return fail(KBG_E_UNSUPPORTED, "preempt/reclaim with host ports: run the reference path");
+  if (S.max_candidates > kbg::kMaxNodeCandidates)
+    return fail(KBG_E_UNSUPPORTED, "a node holds more than 128 running session tasks");
+  return KBG_OK;
+}
+
+struct VictimRun {
+  Session& S;
+  std::vector<int32_t> mark, touched;
+  Live L;
+  explicit VictimRun(Session& s) : S(s), mark(s.n_nodes, -1), L{s, touched, mark, 0} {}
+  kbg_status sync() {  // node rows + plugin state to the device before the next scan
+    kbg_status st = push_deltas(S, touched);
+    touched.clear();
+    ++L.stamp;
+    return st;
+  }
+};
+
+kbg_status reclaim_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
+  if (S.reclaimed || S.allocated || S.backfilled || S.preempted)
+    return fail(KBG_E_INVALID, "reclaim runs once per cycle, first; call kbg_session_reset");
+  kbg_status st = victim_action_check(S);
+  if (st != KBG_OK) return st;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (!S.cycle_started) begin_cycle(S);
+  S.reclaimed = true;
+  S.action = KBG_ACTION_RECLAIM;
+  if ((st = vt_setup(S)) != KBG_OK) return st;
+  VictimRun R(S);
+  auto queue_less = [&](int32_t a, int32_t b) {  // QueueOrderFn (proportion share, then UID)
+    if (S.queue_order_prop && S.fin.qshare[a] != S.fin.qshare[b]) return S.fin.qshare[a] < S.fin.qshare[b];
+    return S.queue_rank[a] < S.queue_rank[b];
+  };
+  auto job_less = [&](int32_t a, int32_t b) { return make_job_key(S, S.fin, a) < make_job_key(S, S.fin, b); };
+  std::vector<int32_t> qheap;
+  std::vector<std::vector<int32_t>> jheap(S.n_queues);
+  std::vector<char> has_jobs(S.n_queues, 0);
+  auto pending = pending_by_job(S);
+  std::vector<size_t> next(S.n_jobs, 0);
+  auto push = [&](std::vector<int32_t>& h, int32_t x, auto less) {
+    h.push_back(x);
+    go_up(h.data(), (int)h.size() - 1, less);
+  };
+  auto pop = [&](std::vector<int32_t>& h, auto less) {
+    const int n = (int)h.size() - 1;
+    std::swap(h[0], h[n]);
+    go_down(h.data(), 0, n, less, S.heap_go111);
+    const int32_t x = h.back();
+    h.pop_back();
+    return x;
+  };
+  for (int32_t j = 0; j < S.n_jobs; ++j) {  // reclaim.go:53-76
+    const int32_t q = S.job_queue[j];
+    push(qheap, q, queue_less);
+    if (!pending[j].empty()) {
+      has_jobs[q] = 1;
+      push(jheap[q], j, job_less);
+    }
+  }
+  kbg_status result = KBG_OK;
+  while (!qheap.empty()) {  // reclaim.go:78-183
+    const int32_t q = pop(qheap, queue_less);
+    if (S.has_prop && S.q_has_attr[q] && kbg::res_le(S.q_deserved[q], S.fin.qalloc[q])) continue;  // Overused
+    if (!has_jobs[q] || jheap[q].empty()) continue;
+    const int32_t j = pop(jheap[q], job_less);
+    if (next[j] >= pending[j].size()) continue;
+    const int32_t t = pending[j][next[j]++];
+    int32_t outcome;
+    if ((result = try_task(S, R.L, kbg::VM_RECLAIM, t, nullptr, &outcome)) != KBG_OK) break;
+    if ((result = R.sync()) != KBG_OK) break;
+    if (outcome == TRY_ASSIGNED) push(qheap, q, queue_less);
+  }
+  if (result == KBG_OK || result == KBG_E_REF_PANIC) {
+    kbg_status s2 = R.sync();
+    if (s2 == KBG_OK) s2 = vt_flush(S);
+    if (s2 != KBG_OK) return s2;
+  }
+  HIP_TRY(hipStreamSynchronize(S.stream));
+  S.stats.reclaim_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return copy_log(S, out, cap, n_out, result);
+}
+
+kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
+  if (S.preempted) return fail(KBG_E_INVALID, "preempt runs once per cycle, last; call kbg_session_reset");
+  kbg_status st = victim_action_check(S);
+  if (st != KBG_OK) return st;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (!S.cycle_started) begin_cycle(S);
+  S.preempted = true;
+  S.action = KBG_ACTION_PREEMPT;
+  if ((st = vt_setup(S)) != KBG_OK) return st;
+  VictimRun R(S);
+  auto job_less = [&](int32_t a, int32_t b) { return make_job_key(S, S.fin, a) < make_job_key(S, S.fin, b); };
+  auto job_ready = [&](int32_t j) { return !S.ready_gang || S.committed_ready[j] >= S.jobs_in[j].min_available; };
+  std::vector<std::vector<int32_t>> jheap(S.n_queues);
+  std::vector<char> has_jobs(S.n_queues, 0);
+  std::vector<int32_t> queues, under;
+  auto pending = pending_by_job(S);
+  std::vector<size_t> next(S.n_jobs, 0);
+  auto push = [&](std::vector<int32_t>& h, int32_t x) {
+    h.push_back(x);
+    go_up(h.data(), (int)h.size() - 1, job_less);
+  };
+  auto pop = [&](std::vector<int32_t>& h) {
+    const int n = (int)h.size() - 1;
+    std::swap(h[0], h[n]);
+    go_down(h.data(), 0, n, job_less, S.heap_go111);
+    const int32_t x = h.back();
+    h.pop_back();
+    return x;
+  };
+  for (int32_t j = 0; j < S.n_jobs; ++j) {  // preempt.go:54-77
+    const int32_t q = S.job_queue[j];
+    queues.push_back(q);
+    if (!pending[j].empty()) {
+      has_jobs[q] = 1;
+      push(jheap[q], j);
+      under.push_back(j);
+    }
+  }
+  kbg_status result = KBG_OK;
+  auto run = [&]() -> kbg_status {
+    kbg_status s2;
+    int32_t outcome;
+    for (int32_t q : queues) {
+      for (;;) {  // preempt.go:81-130: between jobs of the queue
+        if (!has_jobs[q] || jheap[q].empty()) break;
+        const int32_t pj = pop(jheap[q]);
+        Stmt stmt;
+        bool assigned = false;
+        for (;;) {
+          if (next[pj] >= pending[pj].size()) break;
+          const int32_t t = pending[pj][next[pj]++];
+          if ((s2 = try_task(S, R.L, kbg::VM_PREEMPT_JOBS, t, &stmt, &outcome)) != KBG_OK) return s2;
+          if ((s2 = R.sync()) != KBG_OK) return s2;
+          if (outcome == TRY_ASSIGNED) assigned = true;
+          if (job_ready(pj)) {
+            stmt_commit(S, stmt);
+            break;
+          }
+        }
+        if (!job_ready(pj)) {
+          if (!stmt_discard(S, R.L, stmt))
+            return fail(KBG_E_REF_PANIC, "statement discard: DeallocateFunc Sub underflow (resource_info.go:100-110)");
+          if ((s2 = R.sync()) != KBG_OK) return s2;
+          continue;
+        }
+        if (assigned) push(jheap[q], pj);
+      }
+      for (int32_t j : under) {  // preempt.go:132-166: between tasks of a job
+        for (;;) {
+          if (next[j] >= pending[j].size()) break;
+          const int32_t t = pending[j][next[j]++];
+          Stmt stmt;
+          if ((s2 = try_task(S, R.L, kbg::VM_PREEMPT_TASKS, t, &stmt, &outcome)) != KBG_OK) return s2;
+          stmt_commit(S, stmt);
+          if ((s2 = R.sync()) != KBG_OK) return s2;
+          if (outcome != TRY_ASSIGNED) break;
+        }
+      }
+    }
+    return KBG_OK;
+  };
+  result = run();
+  if (result == KBG_OK || result == KBG_E_REF_PANIC) {
+    kbg_status s2 = R.sync();
+    if (s2 == KBG_OK) s2 = vt_flush(S);
+    if (s2 != KBG_OK) return s2;
+  }
+  HIP_TRY(hipStreamSynchronize(S.stream));
+  S.stats.preempt_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return copy_log(S, out, cap, n_out, result);
 }
 
@@ -1892,6 +2559,48 @@ kbg_status kbg_backfill(kbg_session* s, kbg_decision* out, int32_t cap, int32_t*
   }
 }
 
+kbg_status kbg_reclaim(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out) {
+  if (!s) return fail(KBG_E_INVALID, "null session");
+  HIP_TRY(hipSetDevice(s->s.device));
+  try {
+    return reclaim_cycle(s->s, out, cap, n_out);
+  } catch (const std::bad_alloc&) {
+    return fail(KBG_E_NOMEM, "host allocation failed");
+  }
+}
+
+kbg_status kbg_preempt(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out) {
+  if (!s) return fail(KBG_E_INVALID, "null session");
+  HIP_TRY(hipSetDevice(s->s.device));
+  try {
+    return preempt_cycle(s->s, out, cap, n_out);
+  } catch (const std::bad_alloc&) {
+    return fail(KBG_E_NOMEM, "host allocation failed");
+  }
+}
+
+kbg_status kbg_evictions_get(kbg_session* s, kbg_eviction* out, int32_t cap, int32_t* n_out) {
+  if (!s) return fail(KBG_E_INVALID, "null session");
+  const auto& ev = s->s.evictions;
+  if (n_out) *n_out = (int32_t)ev.size();
+  if (!out && cap == 0) return KBG_OK;  // size query
+  if ((int32_t)ev.size() > cap || (!out && !ev.empty()))
+    return fail(KBG_E_CAPACITY, "eviction buffer too small: need " + std::to_string(ev.size()));
+  if (!ev.empty()) std::memcpy(out, ev.data(), ev.size() * sizeof(kbg_eviction));
+  return KBG_OK;
+}
+
+kbg_status kbg_decision_actions_get(kbg_session* s, int32_t* out, int32_t cap, int32_t* n_out) {
+  if (!s) return fail(KBG_E_INVALID, "null session");
+  const auto& a = s->s.dec_action;
+  if (n_out) *n_out = (int32_t)a.size();
+  if (!out && cap == 0) return KBG_OK;  // size query
+  if ((int32_t)a.size() > cap || (!out && !a.empty()))
+    return fail(KBG_E_CAPACITY, "action buffer too small: need " + std::to_string(a.size()));
+  if (!a.empty()) std::memcpy(out, a.data(), a.size() * sizeof(int32_t));
+  return KBG_OK;
+}
+
 kbg_status kbg_session_reset(kbg_session* s) {
   if (!s) return fail(KBG_E_INVALID, "null session");
   Session& S = s->s;
@@ -1899,7 +2608,7 @@ kbg_status kbg_session_reset(kbg_session* s) {
   S.idle = S.idle0;
   S.rel = S.rel0;
   S.ntasks = S.ntasks0;
-  S.allocated = S.backfilled = S.cycle_started = false;
+  S.allocated = S.backfilled = S.reclaimed = S.preempted = S.cycle_started = false;
   if (S.has_ports) {  // the class masks carry the port fit: back to the snapshot's
     S.node_ports = S.node_ports0;
     S.h_class_mask = S.h_class_mask0;

@@ -117,7 +117,8 @@ struct Session {
   std::vector<int32_t> job_queue;                        // job -> queue index
   std::vector<int32_t> task_job;                         // task -> job index
   std::vector<int32_t> joff, jcap;                       // per-queue job-heap segment (jcap + 1 slots)
-  std::vector<int32_t> pend, pend_off, pend_len;         // per-job pending tasks in TaskOrderFn order
+  std::vector<int32_t> pend, pend_off, pend_len;         // per-job pending tasks in TaskOrderFn order (this cycle)
+  std::vector<int32_t> pend_all, pend_off_all, pend_len_all;  // the same at open
   std::vector<char> pending_candidate;                   // task is Pending and not BestEffort
   std::vector<char> be_task;                             // task is Pending and BestEffort (backfill.go:48-50)
   std::vector<int32_t> task_class;
@@ -141,10 +142,29 @@ struct Session {
   // ---- the cycle's actions (allocate, then backfill) on this snapshot
   Engine fin;                 // plugin/ordering state after the last action
   bool cycle_started = false; // an action ran since open / reset
-  bool allocated = false, backfilled = false;
+  bool allocated = false, backfilled = false, reclaimed = false, preempted = false;
   std::vector<kbg_decision> dec;              // decision log of the cycle
   std::vector<int32_t> undisp_head, undisp_next;  // Allocate decisions not yet dispatched, per job
   std::vector<int32_t> jt_off, jt;            // tasks of each job in snapshot (status-index) order
+  int32_t action = KBG_ACTION_ALLOCATE;       // the action whose decisions are being logged
+  std::vector<int32_t> dec_action;            // KBG_ACTION_* of each decision
+  std::vector<int32_t> tstat;                 // job-side status of each task in the cycle
+  // ---- preempt / reclaim (preempt.go, reclaim.go, statement.go)
+  std::vector<int32_t> nt_off, nt_task;       // victim candidates per node: session tasks Running there at
+                                              // open, in NodeInfo.Tasks order
+  std::vector<uint8_t> trun;                  // node-side copy still Running (an eviction makes it Releasing
+                                              // for good: unevict's AddTask fails, node_info.go:101-106)
+  std::vector<int32_t> task_node;             // node index of a task's NodeName (-1: not a session node)
+  std::vector<kbg_eviction> evictions;        // committed cache.Evict calls
+  std::vector<int32_t> tier_preempt, tier_reclaim;  // VictimPlugin bits per tier holding an enabled victim fn
+  int32_t max_candidates = 0;
+  kbg::VictimTables vt{};                     // device copies (allocated at the first victim action)
+  bool vt_ready = false;
+  uint32_t* d_vout = nullptr;
+  uint32_t* h_vout = nullptr;                 // pinned
+  kbg::StateDelta* d_sdeltas = nullptr;
+  kbg::StateDelta* h_sdeltas = nullptr;       // pinned
+  std::vector<kbg::StateDelta> sdeltas;       // queued victim-table changes
   std::vector<int32_t> be_shape;              // per pod-spec class: grouping id of its BestEffort tasks
   std::vector<int32_t> committed_ready;
   struct FitCounts { int32_t valid = 0, nodes = 0, cpu = 0, mem = 0, gpu = 0; };

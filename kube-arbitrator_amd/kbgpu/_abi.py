@@ -35,7 +35,7 @@ DISABLE_RECLAIMABLE = 1 << 4
 DISABLE_QUEUE_ORDER = 1 << 5
 DISABLE_PREDICATE = 1 << 6
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 COMM_ID_BYTES = 128
 
 KIND_ALLOCATE = 0
@@ -55,7 +55,7 @@ class kbg_node(ctypes.Structure):
     _fields_ = [("name", i32), ("has_node", i32), ("allocatable", kbg_resource), ("idle", kbg_resource),
                 ("releasing", kbg_resource), ("max_task_num", i32), ("num_tasks", i32), ("unschedulable", i32),
                 ("label_off", i32), ("label_len", i32), ("taint_off", i32), ("taint_len", i32),
-                ("port_off", i32), ("port_len", i32)]
+                ("port_off", i32), ("port_len", i32), ("task_off", i32), ("task_len", i32)]
 
 
 class kbg_host_port(ctypes.Structure):
@@ -120,6 +120,7 @@ class kbg_snapshot(ctypes.Structure):
         ("plugins", P(kbg_plugin_option)), ("n_plugins", i32),
         ("tier_sizes", P(i32)), ("n_tiers", i32),
         ("ports", P(kbg_host_port)), ("n_ports", i32),
+        ("node_tasks", P(i32)), ("n_node_tasks", i32),
     ]
 
 
@@ -152,7 +153,15 @@ class kbg_stats(ctypes.Structure):
                 ("truncations", i64), ("scan_launches", i64), ("scan_kernel_ms", f64), ("select_kernel_ms", f64),
                 ("allocate_ms", f64), ("open_ms", f64), ("engine_ms", f64), ("resolve_ms", f64),
                 ("device_ms", f64), ("delta_ms", f64), ("replayed", i64), ("n_classes", i32), ("shards", i32), ("shard_index", i32),
-                ("int_scan", i32), ("exchange_ms", f64), ("backfill_ms", f64)]
+                ("int_scan", i32), ("exchange_ms", f64), ("backfill_ms", f64),
+                ("reclaim_ms", f64), ("preempt_ms", f64), ("victim_scans", i64), ("victim_kernel_ms", f64)]
+
+
+class kbg_eviction(ctypes.Structure):
+    _fields_ = [("task", i32), ("by", i32), ("action", i32), ("reserved", i32)]
+
+
+ACTION_NAMES = {0: "allocate", 1: "backfill", 2: "reclaim", 3: "preempt"}
 
 
 # Every symbol include/kbgpu.h declares, with its ctypes signature.
@@ -167,6 +176,10 @@ SIGNATURES = {
     "kbg_comm_destroy": (None, [ctypes.c_void_p]),
     "kbg_allocate": (i32, [ctypes.c_void_p, P(kbg_decision), i32, P(i32)]),
     "kbg_backfill": (i32, [ctypes.c_void_p, P(kbg_decision), i32, P(i32)]),
+    "kbg_reclaim": (i32, [ctypes.c_void_p, P(kbg_decision), i32, P(i32)]),
+    "kbg_preempt": (i32, [ctypes.c_void_p, P(kbg_decision), i32, P(i32)]),
+    "kbg_evictions_get": (i32, [ctypes.c_void_p, P(kbg_eviction), i32, P(i32)]),
+    "kbg_decision_actions_get": (i32, [ctypes.c_void_p, P(i32), i32, P(i32)]),
     "kbg_session_reset": (i32, [ctypes.c_void_p]),
     "kbg_select": (i32, [ctypes.c_void_p, P(i32), i32, i32, P(i32), P(i32), P(i32)]),
     "kbg_apply": (i32, [ctypes.c_void_p, i32, P(kbg_resource), i32]),

@@ -1,5 +1,6 @@
-"""The allocate and backfill actions (pkg/scheduler/actions/allocate/allocate.go:27-178,
-pkg/scheduler/actions/backfill/backfill.go:26-73).
+"""The allocate, backfill, reclaim and preempt actions
+(pkg/scheduler/actions/{allocate/allocate.go:27-178, backfill/backfill.go:26-73,
+reclaim/reclaim.go:27-191, preempt/preempt.go:30-253}).
 
 `execute(ssn)` runs the action's Execute on the MI355X path (kbg_allocate /
 kbg_backfill) and replays the new part of the cycle's decision log through
@@ -26,6 +27,7 @@ AllocateResult = ActionResult
 
 class _DeviceAction:
     _entry = None
+    _evicting = False
 
     def initialize(self):
         pass
@@ -54,6 +56,8 @@ class _DeviceAction:
             t, nd, kind, _ = decs[i]
             if kind == _abi.KIND_ALLOCATE:
                 ssn.allocate(tasks[t], names[nd])
+            elif self._evicting:
+                ssn.pipeline_replay(tasks[t], names[nd])
             else:
                 ssn.pipeline(tasks[t], names[nd])
             for bt in bound_at.pop(i, []):
@@ -80,9 +84,52 @@ class BackfillAction(_DeviceAction):
         return "backfill"
 
 
+class _EvictingAction(_DeviceAction):
+    """reclaim / preempt: pipelines and committed evictions replay as statuses
+    (framework.Session.pipeline_replay / evict); the committed evictions go
+    through the cache's evictor (cache.Evict). Node Idle / Releasing (which a
+    discarded statement also changes, statement.go:81-108) are then taken from
+    the device session, so the actions after this one replay from them."""
+
+    _evicting = True
+
+    def execute(self, ssn):
+        seen = len(ssn.evictions)
+        try:
+            return super().execute(ssn)
+        finally:
+            L = _abi.lib()
+            n = ctypes.c_int32(0)
+            _abi.check(L.kbg_evictions_get(ssn.handle, None, 0, ctypes.byref(n)))
+            buf = (_abi.kbg_eviction * max(1, n.value))()
+            _abi.check(L.kbg_evictions_get(ssn.handle, buf, n.value, ctypes.byref(n)))
+            tasks = ssn.flat.task_objs
+            for i in range(seen, n.value):
+                ev = (tasks[buf[i].task], tasks[buf[i].by], _abi.ACTION_NAMES[buf[i].action])
+                ssn.evictions.append(ev)
+                ssn.evict(ev[0], ev[2])
+            ssn.sync_node_resources()
+
+
+class ReclaimAction(_EvictingAction):
+    _entry = "kbg_reclaim"
+
+    def name(self):
+        return "reclaim"
+
+
+class PreemptAction(_EvictingAction):
+    _entry = "kbg_preempt"
+
+    def name(self):
+        return "preempt"
+
+
 def new():
     return AllocateAction()
 
 
 register_action(AllocateAction())
 register_action(BackfillAction())
+register_action(ReclaimAction())
+register_action(PreemptAction())

@@ -24,11 +24,15 @@ class FakeBinder:
     def __init__(self):
         self.binds = {}
         self.order = []
+        self.evicts = []
 
     def bind(self, pod, hostname):
         key = f"{pod.get('namespace', '')}/{pod['name']}"
         self.binds[key] = hostname
         self.order.append(key)
+
+    def evict(self, pod, reason):  # the fake Evictor: records (pod key, reason)
+        self.evicts.append((f"{pod.get('namespace', '')}/{pod['name']}", reason))
 
 
 class SchedulerCache:
@@ -80,6 +84,9 @@ class SchedulerCache:
 
     def bind(self, task, hostname):  # cache.go:408-444 (session-visible part)
         self.binder.bind(task.pod, hostname)
+
+    def evict(self, task, reason):  # cache.go:369-405 (the evictor side)
+        self.binder.evict(task.pod, reason)
 
     def snapshot(self):  # cache.go:549-597
         s = ClusterInfo()

@@ -80,12 +80,13 @@ def run_fixture(fx, options=None):
             raise
         return {"status": "ref_panic", "error": str(e)}, ssn
     tasks, names = ssn.flat.task_objs, ssn.flat.node_names
-    out = {"status": status, "decisions": [], "binds": dict(binder.binds), "jobs": [], "queues": [], "nodes": []}
+    out = {"status": status, "decisions": [], "binds": dict(binder.binds), "jobs": [], "queues": [], "nodes": [],
+           "evictions": [{"task": t.uid, "by": by.uid, "action": act} for t, by, act in ssn.evictions]}
     for (t, nd, kind, disp), act in zip(ssn.decisions, ssn.action_of):
         d = {"task": tasks[t].uid, "job": tasks[t].job, "node": names[nd],
              "kind": "allocate" if kind == _abi.KIND_ALLOCATE else "pipeline", "dispatched_at": disp}
-        if act == "backfill":
-            d["action"] = "backfill"
+        if act != "allocate":
+            d["action"] = act
         out["decisions"].append(d)
     has_drf = any(p.name == "drf" for t in ssn.tiers for p in t.plugins)
     for j, job in enumerate(ssn.jobs):

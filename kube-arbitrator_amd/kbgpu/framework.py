@@ -12,7 +12,7 @@ reference's bookkeeping (session.go:205-316).
 import ctypes
 
 from . import _abi
-from .api import ALLOCATED, BINDING, PIPELINED
+from .api import ALLOCATED, BINDING, PIPELINED, RELEASING, pod_key
 from .snapshot import FlatSnapshot
 
 KNOWN_PLUGINS = ("priority", "gang", "drf", "predicates", "proportion")
@@ -73,6 +73,7 @@ class Session:
                                           ctypes.byref(self.handle)))
         self.decisions = []
         self.action_of = []  # action name of each decision of the cycle
+        self.evictions = []  # (task, by, action) committed evictions (cache.Evict)
 
     def _active_tiers(self):
         from .conf import Tier
@@ -104,6 +105,42 @@ class Session:
         job = self.job_index.get(task.job)
         if job is not None:
             job.update_task_status(task, BINDING)
+
+    # ---- session.go:318-352 / statement.go: the resource side of evictions and of
+    # the pipelines that follow them lives in the device session (node Idle /
+    # Releasing, including what discarded statements leave behind); the host
+    # objects record the statuses, the node membership and the cache's Evict.
+    def evict(self, task, reason):
+        job = self.job_index.get(task.job)
+        if job is not None:
+            job.update_task_status(task, RELEASING)
+        node = self.node_index.get(task.node_name)
+        if node is not None:
+            held = node.tasks.get(pod_key(task.pod))
+            if held is not None:
+                held.status = RELEASING
+        self.cache.evict(task, reason)
+
+    def pipeline_replay(self, task, hostname):
+        job = self.job_index.get(task.job)
+        if job is not None:
+            job.update_task_status(task, PIPELINED)
+        task.node_name = hostname
+        node = self.node_index.get(hostname)
+        if node is not None and pod_key(task.pod) not in node.tasks:
+            node.tasks[pod_key(task.pod)] = task.clone()
+
+    def sync_node_resources(self):
+        """Idle / Releasing of every host NodeInfo from the device session,
+        after an action whose statements changed them (reclaim, preempt), so
+        later actions' replays account from the same values."""
+        for i, name in enumerate(self.flat.node_names):
+            node = self.node_index.get(name)
+            if node is None or node.node is None:
+                continue
+            st = self.node_state(i)
+            for mine, dev in ((node.idle, st.idle), (node.releasing, st.releasing)):
+                mine.milli_cpu, mine.memory, mine.milli_gpu = dev.milli_cpu, dev.memory, dev.milli_gpu
 
     def job_state(self, j):
         st = _abi.kbg_job_state()

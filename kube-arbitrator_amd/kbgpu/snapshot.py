@@ -85,7 +85,7 @@ class FlatSnapshot:
                 ports.append((S(ip), S(proto), port))
             r["port_len"] = len(ports) - r["port_off"]
         self.node_names = [n.name for n in nodes]
-        # jobs + tasks + specs
+        # jobs + tasks + specs (node task lists are filled once task indices exist)
         jb = np.zeros(len(jobs), dtype=np.dtype(_abi.kbg_job))
         task_rows, self.task_objs = [], []
         spec_ids = {}
@@ -140,6 +140,13 @@ class FlatSnapshot:
             for t in job.tasks.values():
                 task_rows.append((S(t.uid), j, t.status, t.priority, t.resreq.as_tuple(), spec_of(t.pod), S(t.node_name)))
                 self.task_objs.append(t)
+        # NodeInfo.Tasks order of the session-job tasks on each node (preempt/reclaim victims)
+        task_index = {t.uid: i for i, t in enumerate(self.task_objs)}
+        node_tasks = []
+        for i, n in enumerate(nodes):
+            nd[i]["task_off"] = len(node_tasks)
+            node_tasks.extend(task_index[t.uid] for t in n.tasks.values() if t.uid in task_index)
+            nd[i]["task_len"] = len(node_tasks) - nd[i]["task_off"]
         tk = np.zeros(len(task_rows), dtype=np.dtype(_abi.kbg_task))
         for i, row in enumerate(task_rows):
             tk[i] = row
@@ -167,7 +174,7 @@ class FlatSnapshot:
             labels=np.asarray(labels or [0, 0], dtype=np.int32), taints=arr(_abi.kbg_taint, taints),
             selectors=np.asarray(selectors or [0, 0], dtype=np.int32),
             plugins=arr(_abi.kbg_plugin_option, plugin_rows), tier_sizes=np.asarray(tier_sizes or [0], dtype=np.int32),
-            ports=arr(_abi.kbg_host_port, ports))
+            ports=arr(_abi.kbg_host_port, ports), node_tasks=np.asarray(node_tasks or [0], dtype=np.int32))
         A = self.arrays
 
         def ptr(a, ctype):
@@ -194,4 +201,5 @@ class FlatSnapshot:
         snap.plugins, snap.n_plugins = ptr(A["plugins"], _abi.kbg_plugin_option), len(plugin_rows)
         snap.tier_sizes, snap.n_tiers = ptr(A["tier_sizes"], ctypes.c_int32), len(tier_sizes)
         snap.ports, snap.n_ports = ptr(A["ports"], _abi.kbg_host_port), len(ports)
+        snap.node_tasks, snap.n_node_tasks = ptr(A["node_tasks"], ctypes.c_int32), len(node_tasks)
         self.snap = snap

@@ -258,9 +258,79 @@ def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8, be_frac=0.06):
     fx = {"name": f"fuzz-{seed}", "tiers": tiers, "nodes": nodes, "pods": pods, "podGroups": pgs, "queues": queues}
     if rng.random() < 0.2:
         fx["namespaces"] = ["c1", "c2"]
-    r = rng.random()  # conf actions (util.go:30-61): the default "allocate, backfill", or one of them
-    if r < 0.5:
+    r = rng.random()  # conf actions (util.go:30-61): the default "allocate, backfill", the full set, or one
+    if r < 0.4:
         fx["actions"] = ["allocate", "backfill"]
-    elif r < 0.6:
+    elif r < 0.5:
         fx["actions"] = ["backfill"]
+    elif r < 0.7:
+        fx["actions"] = ["reclaim", "allocate", "backfill", "preempt"]
+    elif r < 0.8:
+        fx["actions"] = ["preempt"]
+    elif r < 0.9:
+        fx["actions"] = ["reclaim"]
     return fx
+
+
+def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3):
+    """A cluster already full of Running gang jobs in several queues, with
+    Pending jobs of every queue: the regime of reclaim and preempt
+    (BASELINE config 5 in miniature). Tasks of a job share one request so the
+    reference's eviction loop (preempt.go:214-226) stays panic-free most of
+    the time; mixed sizes still occur."""
+    rng = random.Random(seed)
+    qs = [{"name": f"q{i}", "weight": rng.choice([1, 2, 3])} for i in range(queues)]
+    nds = []
+    for i in range(nodes):
+        alloc = {"cpu": str(rng.choice([4, 8])), "memory": f"{rng.choice([8, 16])}Gi",
+                 "pods": str(rng.choice([4, 8, 110]))}
+        nds.append({"name": f"n{i:02d}", "allocatable": alloc, "labels": {"zone": rng.choice(["a", "b"])}})
+    free = {n["name"]: [int(n["allocatable"]["cpu"]) * 1000, int(n["allocatable"]["pods"])] for n in nds}
+    pods, pgs = [], []
+    uid = 0
+    uniform = rng.random() < 0.7  # one request size for every job: evictions free exactly what a pipeline needs
+    base = (rng.choice([500, 1000, 2000]), rng.choice(["0", "512Mi", "1Gi"]))
+    for j in range(jobs):
+        ns = rng.choice(["c1", "c2"])
+        pg = f"pg{j}"
+        q = rng.choice(qs)["name"]
+        n_t = rng.randint(1, tasks)
+        pgs.append({"namespace": ns, "name": pg, "minMember": rng.randint(0, n_t), "queue": q,
+                    "creationTimestamp": rng.choice([0, 100, 200]) * 1_000_000_000})
+        cpu, mem = base if uniform else (rng.choice([500, 1000, 2000]), rng.choice(["0", "512Mi", "1Gi"]))
+        req = {"cpu": f"{cpu}m", "memory": mem}
+        running = rng.random() < 0.6
+        for t in range(n_t):
+            uid += 1
+            phase, node = "Pending", ""
+            if running:
+                cands = [n["name"] for n in nds if free[n["name"]][0] >= cpu and free[n["name"]][1] > 0]
+                if cands:
+                    node = rng.choice(cands)
+                    free[node][0] -= cpu
+                    free[node][1] -= 1
+                    phase = "Running"
+            p = {"uid": f"u{uid:04d}", "namespace": ns, "name": f"{pg}-t{t}", "phase": phase, "nodeName": node,
+                 "annotations": {"scheduling.k8s.io/group-name": pg},
+                 "containers": [{"requests": dict(req) if rng.random() < 0.95 or not uniform else {"cpu": "5m"}}]}
+            if rng.random() < 0.3:
+                p["priority"] = rng.choice([1, 5, 10])
+            if rng.random() < 0.15:
+                p["nodeSelector"] = {"zone": rng.choice(["a", "b"])}
+            pods.append(p)
+    plugins = ["priority", "gang", "drf", "predicates", "proportion"]
+    rng.shuffle(plugins)
+    cut = rng.randint(0, len(plugins))
+    flags = ["disablePreemptable", "disableReclaimable", "disableJobOrder", "disableJobReady"]
+
+    def opt(name):
+        o = {"name": name}
+        if rng.random() < 0.1:
+            o[rng.choice(flags)] = True
+        return o
+
+    tiers = [t for t in ([opt(p) for p in plugins[:cut]], [opt(p) for p in plugins[cut:]]) if t]
+    acts = rng.choice([["reclaim"], ["preempt"], ["reclaim", "allocate", "backfill", "preempt"],
+                       ["allocate", "preempt"]])
+    return {"name": f"contended-{seed}", "tiers": tiers, "nodes": nds, "pods": pods, "podGroups": pgs,
+            "queues": qs, "actions": acts}

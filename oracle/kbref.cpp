@@ -748,6 +748,10 @@ struct Session {  // framework/session.go:35-61
   std::map<std::string, VictimFn> preemptableFns, reclaimableFns;
   std::vector<Eviction> evictions;
   const char* action = "";  // the action whose decisions are being logged
+  // A pending pod declares hostPort under an active predicates plugin: the
+  // device path refuses reclaim/preempt for such sessions (kbgpu.h), so the
+  // oracle draws the same boundary there.
+  bool pending_host_ports = false;
 
   // run-time bookkeeping for the decision log
   std::vector<Decision> decisions;
@@ -1316,6 +1320,7 @@ struct Predicates {
         if (t->pod->has_pod_affinity || t->pod->has_pod_anti_affinity)
           throw Unsupported("pod (anti)affinity present: inter-pod affinity predicate not restated");
         if (AllocatedStatus(t->status) && !s->nodeIndex.count(t->nodeName)) ghost = true;
+        if (t->status == Pending && t->pod->has_host_port) s->pending_host_ports = true;
       }
     s->predicateFns["predicates"] = [this](TaskInfo* task, NodeInfo* node) -> bool {
       // cache.NewNodeInfo(node.Pods()...).SetNode(node.Node): nil node => nil dereference
@@ -1802,6 +1807,8 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache) {
   for (auto& a : actions) {
     if (a == "allocate") { ssn->action = ""; allocate_execute(ssn); }
     else if (a == "backfill") { ssn->action = "backfill"; backfill_execute(ssn); }
+    else if ((a == "reclaim" || a == "preempt") && ssn->pending_host_ports)
+      throw Unsupported("reclaim/preempt with pending host ports: not on the device path");
     else if (a == "reclaim") { ssn->action = "reclaim"; reclaim_execute(ssn); }
     else if (a == "preempt") { ssn->action = "preempt"; preempt_execute(ssn); }
     else throw BadInput("unsupported action " + a);

@@ -50,6 +50,7 @@ def compare_outputs(ref, got):
         assert a == b, f"decision {i}: oracle {a} != device {b}"
     assert len(rd) == len(gd)
     assert ref["binds"] == got["binds"]
+    assert ref.get("evictions", []) == got.get("evictions", [])
     assert [(j["uid"], j["ready_num"], j["ready"]) for j in ref["jobs"]] == \
            [(j["uid"], j["ready_num"], j["ready"]) for j in got["jobs"]]
     for a, b in zip(ref["jobs"], got["jobs"]):

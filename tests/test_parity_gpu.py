@@ -295,3 +295,15 @@ def test_backfill_config2(shards, be_req):
     compare_outputs(ref, got)
     if ssn:
         ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(150))
+def test_contended_reclaim_preempt_parity(seed):
+    """reclaim.go / preempt.go / statement.go on clusters full of running gang
+    jobs: evictions (order, preemptor), pipelines, discarded statements'
+    node-side residue, shares and readiness against the oracle."""
+    fx = synth.contended_fixture(seed)
+    got, ssn = run_fixture(fx)
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()

@@ -88,6 +88,25 @@ def test_rccl_one_rank_fuzz(seed, comm1):
         ssn.close()
 
 
+@pytest.mark.parametrize("seed", range(0, 60, 6))
+def test_rccl_one_rank_reclaim_preempt(seed, comm1):
+    """Victim scans of a comm session: the shard's nodes, then ncclAllReduce(min)."""
+    fx = synth.contended_fixture(seed)
+    got, ssn = run_fixture(fx, {"comm": comm1})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(1, 60, 4))
+def test_local_shards_reclaim_preempt(seed):
+    fx = synth.contended_fixture(seed)
+    got, ssn = run_fixture(fx, {"shards": 2 + seed % 5})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
 def test_rccl_shard_count_must_match(comm1):
     fx = synth.config_fixture(1)
     got, ssn = run_fixture(fx, {"comm": comm1, "shards": 2})
