@@ -171,6 +171,9 @@ def main():
                 "evaluations_per_launch": agg["evals"] / max(1, agg["launches"])}
 
     log(f"[rank {rank}] C{cid} setup {time.time() - t0:.1f}s")
+    if fx.get("actions"):
+        contended_bench(args, fx, cache, base_opts, comm, rank, world, cid)
+        return
     prod = run_mode(0, args.steps, args.warmup, True)      # production: grouped shapes
     full = run_mode(1, max(1, min(3, args.steps)), 1, False)  # SURVEY roofline rule: every task scans all N
     decisions = prod["decisions"]
@@ -217,6 +220,107 @@ def main():
     }
     if rank == 0 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(fx, f"C{cid}")
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
+    kdist.shutdown()
+
+
+def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid):
+    """C5: one step = one scheduling cycle of the fixture's actions ("reclaim,
+    allocate, backfill, preempt") through the C ABI on a session reset to the
+    snapshot. value = (pipelines + allocations) / s; evictions are reported
+    beside them. The dominant device kernel is the victim scan (one launch per
+    reclaimer / preemptor task, one thread per node); its algorithmic bytes per
+    launch are N x 64 B (node record) + R x 32 B (the Running task records the
+    scan walks, R = running session tasks), DESIGN.md §5."""
+    import torch
+    from kbgpu import _abi
+    from kbgpu import dist as kdist
+    from kbgpu.api import RUNNING
+    from kbgpu.fixture import fixture_tiers
+    from kbgpu.framework import open_session
+
+    L = _abi.lib()
+    ssn = open_session(cache, fixture_tiers(fx), dict(base_opts))
+    cap = max(1, ssn.flat.pending_all)
+    buf = (_abi.kbg_decision * cap)()
+    nout = ctypes.c_int32(0)
+    nev = ctypes.c_int32(0)
+    entries = {"reclaim": L.kbg_reclaim, "allocate": L.kbg_allocate, "backfill": L.kbg_backfill,
+               "preempt": L.kbg_preempt}
+    acts = [entries[a] for a in fx["actions"]]
+    phase = {"reclaim_ms": [], "allocate_ms": [], "backfill_ms": [], "preempt_ms": []}
+
+    def step():
+        _abi.check(L.kbg_session_reset(ssn.handle))
+        for fn in acts:
+            _abi.check(fn(ssn.handle, buf, cap, ctypes.byref(nout)))
+        _abi.check(L.kbg_evictions_get(ssn.handle, None, 0, ctypes.byref(nev)))
+        return nout.value, nev.value
+
+    for _ in range(args.warmup):
+        step()
+    cyc, dec, ev, vscans, vms = [], 0, 0, 0, 0.0
+    kdist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        t1 = time.perf_counter()
+        d, e = step()
+        cyc.append((time.perf_counter() - t1) * 1e3)
+        dec += d
+        ev += e
+        st = ssn.stats()
+        vscans += st.victim_scans
+        vms += st.victim_kernel_ms
+        for k in phase:
+            phase[k].append(getattr(st, k))
+    torch.cuda.synchronize()
+    elapsed_local = time.perf_counter() - t_start
+    kdist.barrier()
+    st = ssn.stats()
+    n_nodes = len(ssn.nodes)
+    running = sum(1 for t in ssn.flat.task_objs if t.status == RUNNING)
+    pending = ssn.flat.pending_all
+    ssn.close()
+    elapsed, total = kdist.aggregate(elapsed_local, dec, sharded=world > 1)
+    nodes_per_rank = n_nodes / max(1, world)
+    algo = nodes_per_rank * NODE_RECORD_B + running / max(1, world) * TASK_RECORD_B
+    launch_us = vms * 1e3 / max(1, vscans)
+    ach = algo / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
+    line = {
+        "metric": "task placements/sec + p50 scheduling-cycle latency, contended cluster (reclaim/preempt)",
+        "value": total / elapsed,
+        "unit": "placements/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "p50_cycle_ms": statistics.median(cyc),
+        "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded BASELINE config generator, kbgpu/synth.py contended_config)",
+        "config": {"workload": f"C{cid}: {n_nodes} nodes, {running} running + {pending} pending tasks "
+                               f"(~95% CPU), actions {', '.join(fx['actions'])}, default tiers",
+                   "parallelism": f"node-axis shards x{world} (RCCL min-reduce of the victim-scan stop node)"
+                                  if world > 1 else "single-gpu"},
+        "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": "kbg_victim_kernel",
+                     "avg_launch_us": launch_us, "algo_bytes_per_launch": algo},
+        "decisions_per_cycle": dec // max(1, args.steps),
+        "evictions_per_cycle": ev // max(1, args.steps),
+        "victim_scans_per_cycle": vscans // max(1, args.steps),
+        "phase_ms_p50": {k: statistics.median(v) for k, v in phase.items()},
+        "open_ms": st.open_ms,
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(fx, f"C{cid}")
+        line["cpu_baseline"]["sample"] = line["cpu_baseline"]["sample"].replace("allocate cycle", "cycle (" +
+                                                                                ", ".join(fx["actions"]) + ")")
     if rank == 0:
         print(json.dumps(line), flush=True)
     if comm is not None:

@@ -268,7 +268,7 @@ typedef struct kbg_stats {
   double reclaim_ms;       /* wall time of the last kbg_reclaim */
   double preempt_ms;       /* wall time of the last kbg_preempt */
   int64_t victim_scans;    /* victim-scan kernel launches (one per preemptor / reclaimer tried) */
-  double victim_kernel_ms; /* summed HIP-event time of the victim-scan kernel */
+  double victim_kernel_ms; /* victim-scan kernel time: HIP-event time of every 16th launch x launches / timed */
 } kbg_stats;
 
 typedef struct kbg_session kbg_session;

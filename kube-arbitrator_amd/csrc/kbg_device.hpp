@@ -203,11 +203,37 @@ hipError_t launch_select(const uint64_t* bits, int32_t W, int32_t Wl, int32_t n_
 hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream);
 hipError_t launch_mask_apply(uint64_t* class_mask, const MaskDelta* deltas, int32_t n_deltas, hipStream_t stream);
 
-// Writes min over nodes of (node << 1 | panic) for the nodes where the
-// reference would stop (validated victims, or a panic) into *out (preset to
-// UINT32_MAX by the caller's memset on the same stream).
-hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* out, hipStream_t stream,
+// One victim scan. The reference stops at the first node (ssn.Nodes order)
+// with validated victims or a panic; its key is (node << 1 | panic). Waves
+// walk the node range grid-strided, each keeping its first stop (rows ascend,
+// so that is its minimum), and workgroup b writes the min of its waves to
+// blk_min[b] (UINT32_MAX for none). The caller takes the min over the
+// kbg_victim_blocks(node_n) entries: on the host straight from host-mapped
+// memory, or — sharded — after an element-wise ncclAllReduce(min) of the
+// kMaxVictimBlocks-entry array (entries past a rank's grid stay UINT32_MAX).
+constexpr int kVictimWaves = 4;          // waves per workgroup
+constexpr int kMaxVictimBlocks = 1024;
+inline int32_t kbg_victim_blocks(int32_t node_n) {
+  const int32_t b = (node_n + kVictimWaves - 1) / kVictimWaves;
+  return b < 1 ? 1 : (b > kMaxVictimBlocks ? kMaxVictimBlocks : b);
+}
+hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* blk_min, hipStream_t stream,
                               hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
-hipError_t launch_state_apply(const VictimTables& t, const StateDelta* d, int32_t n, hipStream_t stream);
+// Host-side changes before a scan, read in place from host-mapped memory:
+// node rows (NodeInfo.Tasks count / Idle / Releasing) and victim-table
+// entries, in one launch.
+hipError_t launch_victim_prep(const NodeSoA& n, const VictimTables& t, const NodeDelta* nd, int32_t n_nodes,
+                              const StateDelta* sd, int32_t n_state, hipStream_t stream);
+// The common case (a try evicted a few tasks) carried in the kernel arguments:
+// no PCIe reads on the critical path.
+constexpr int kArgNodeDeltas = 16;
+constexpr int kArgStateDeltas = 48;
+struct VictimPrepArgs {
+  int32_t nn, ns;
+  NodeDelta nd[kArgNodeDeltas];
+  StateDelta sd[kArgStateDeltas];
+};
+hipError_t launch_victim_prep_inline(const NodeSoA& n, const VictimTables& t, const VictimPrepArgs& a,
+                                     hipStream_t stream);
 
 }  // namespace kbg

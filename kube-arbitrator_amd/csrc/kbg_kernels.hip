@@ -295,97 +295,131 @@ __device__ __forceinline__ double share3(const double* a, const double* tot) {
   return res;
 }
 
-// One thread per node, in ssn.Nodes order; the lowest node where the
-// reference stops (validated victims, or a panic inside PredicateFn or a
-// victim fn) wins. Candidates are the session tasks Running on the node at
-// open, in NodeInfo.Tasks order (at most kMaxNodeCandidates; the host checks).
-// Cumulative per-job (drf.go:87-100) / per-queue (proportion.go:166-183)
-// allocations are replayed from the node's list head for every candidate, so
-// each subtraction happens in the reference's order.
-__global__ __launch_bounds__(256) void kbg_victim_kernel(VictimScan p, VictimTables t, uint32_t* __restrict__ out) {
-  const int row = blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= p.node_n) return;
+// One wave per node, in ssn.Nodes order; the lowest node where the reference
+// stops (validated victims, or a panic inside PredicateFn or a victim fn)
+// wins. The node's candidates — the session tasks Running on it at open, in
+// NodeInfo.Tasks order, at most kMaxNodeCandidates (the host checks) — sit
+// one per lane (k = h * 64 + lane, h = 0, 1). The victim fns that accumulate
+// per job (drf.go:87-100) or per queue (proportion.go:166-183) walk the
+// preemptees in order as a wave-uniform loop: candidate k2's job, queue and
+// request come to every lane through v_readlane, and lane k applies it while
+// k2 <= k, so each lane sees exactly the subtractions the reference has made
+// when it reaches its candidate.
+
+__device__ __forceinline__ int32_t rl_i(int32_t v, int32_t l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ double rl_d(double v, int32_t l) {
+  const uint64_t u = __double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)(u >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// The stop key of one node (wave-uniform), UINT32_MAX when the reference
+// moves on to the next node.
+__device__ uint32_t victim_node(const VictimScan& p, const VictimTables& t, int row, int lane) {
+  constexpr uint32_t kNone = 0xffffffffu;
   const int n = p.node_lo + row;
-  if (!((t.class_mask[(size_t)p.cls * p.W + (n >> 6)] >> (n & 63)) & 1ull)) return;  // static predicate
-  if (t.panic_node[n]) {  // SetNode(nil) inside PredicateFn (predicates.go:122-123)
-    atomicMin(out, ((uint32_t)n << 1) | 1u);
-    return;
-  }
-  if (p.cap_check && t.ntasks[row] >= t.maxtasks[row]) return;  // predicates.go:125-127
+  if (!((t.class_mask[(size_t)p.cls * p.W + (n >> 6)] >> (n & 63)) & 1ull)) return kNone;  // static predicate
+  if (t.panic_node[n]) return ((uint32_t)n << 1) | 1u;  // SetNode(nil) inside PredicateFn (predicates.go:122-123)
+  if (p.cap_check && t.ntasks[row] >= t.maxtasks[row]) return kNone;  // predicates.go:125-127
   const int off = t.nt_off[n];
   const int L = t.nt_off[n + 1] - off;
-  uint64_t pm[2] = {0ull, 0ull};  // preemptees: filtered Running tasks
-  for (int k = 0; k < L; ++k) {
-    const int task = t.nt_task[off + k];
-    if (!t.t_run[task]) continue;
-    const int jv = t.t_job[task];
-    bool f;
-    if (p.mode == VM_PREEMPT_JOBS) f = t.j_queue[jv] == p.queue && jv != p.job;  // preempt.go:100-112
-    else if (p.mode == VM_PREEMPT_TASKS) f = jv == p.job;                      // :146-154
-    else f = t.j_queue[jv] != p.queue;                                          // reclaim.go:113-126
-    if (f) pm[k >> 6] |= 1ull << (k & 63);
+  // this lane's two candidates: job, queue, request, preemptee filter
+  int32_t jv[2], qv[2];
+  double rq[2][3];
+  uint64_t pm[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = h * 64 + lane;
+    bool f = false;
+    jv[h] = -1;
+    qv[h] = -1;
+    rq[h][0] = rq[h][1] = rq[h][2] = 0.0;
+    if (k < L) {
+      const int task = t.nt_task[off + k];
+      jv[h] = t.t_job[task];
+      qv[h] = t.j_queue[jv[h]];
+      rq[h][0] = t.t_req[3 * (size_t)task];
+      rq[h][1] = t.t_req[3 * (size_t)task + 1];
+      rq[h][2] = t.t_req[3 * (size_t)task + 2];
+      if (t.t_run[task]) {
+        if (p.mode == VM_PREEMPT_JOBS) f = qv[h] == p.queue && jv[h] != p.job;  // preempt.go:100-112
+        else if (p.mode == VM_PREEMPT_TASKS) f = jv[h] == p.job;              // :146-154
+        else f = qv[h] != p.queue;                                              // reclaim.go:113-126
+      }
+    }
+    pm[h] = __ballot(f);
   }
-  if (!(pm[0] | pm[1])) return;  // no preemptee: every fn returns nil
+  if (!(pm[0] | pm[1])) return kNone;  // no preemptee: every fn returns nil
+  const int nh = L > 64 ? 2 : 1;
   bool panic = false;
   uint64_t vm[2] = {0ull, 0ull};
-  for (int ti = 0; ti < p.n_tiers && !panic; ++ti) {
+  for (int ti = 0; ti < p.n_tiers; ++ti) {
     const int fns = p.tier_fns[ti];
     uint64_t tm[2] = {pm[0], pm[1]};
     if (fns & VP_GANG) {  // gang.go:104-124
-      uint64_t c[2] = {0ull, 0ull};
-      for (int k = 0; k < L; ++k) {
-        if (!((pm[k >> 6] >> (k & 63)) & 1ull)) continue;
-        const int jv = t.t_job[t.nt_task[off + k]];
-        if (t.j_min[jv] <= t.j_ready[jv] - 1) c[k >> 6] |= 1ull << (k & 63);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const bool c = jv[h] >= 0 && t.j_min[jv[h]] <= t.j_ready[jv[h]] - 1;
+        tm[h] &= __ballot(c);
       }
-      tm[0] &= c[0];
-      tm[1] &= c[1];
     }
-    if (fns & VP_DRF) {  // drf.go:80-105
-      uint64_t c[2] = {0ull, 0ull};
-      for (int k = 0; k < L && !panic; ++k) {
-        if (!((pm[k >> 6] >> (k & 63)) & 1ull)) continue;
-        const int jv = t.t_job[t.nt_task[off + k]];
-        double x[3] = {t.j_alloc[3 * jv], t.j_alloc[3 * jv + 1], t.j_alloc[3 * jv + 2]};
-        for (int k2 = 0; k2 <= k && !panic; ++k2) {
-          if (!((pm[k2 >> 6] >> (k2 & 63)) & 1ull)) continue;
-          const int t2 = t.nt_task[off + k2];
-          if (t.t_job[t2] != jv) continue;
-          const double* r = t.t_req + 3 * (size_t)t2;
-          if (!res_le3(r, x)) panic = true;  // Resource.Sub (resource_info.go:100-110)
-          x[0] -= r[0];
-          x[1] -= r[1];
-          x[2] -= r[2];
+    if (fns & (VP_DRF | VP_PROP)) {
+      // running per-lane allocation: drf per job, proportion per queue
+      double xd[2][3], xp[2][3];
+      bool vd[2] = {false, false}, vp[2] = {false, false};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const bool on = (pm[h] >> lane) & 1ull;
+        for (int d = 0; d < 3; ++d) {
+          xd[h][d] = on && (fns & VP_DRF) ? t.j_alloc[3 * (size_t)jv[h] + d] : 0.0;
+          xp[h][d] = on && (fns & VP_PROP) ? t.q_alloc[3 * (size_t)qv[h] + d] : 0.0;
         }
-        const double rs = share3(x, t.drf_total);
-        if (p.ls < rs || fabs(p.ls - rs) <= 0.000001) c[k >> 6] |= 1ull << (k & 63);
       }
-      tm[0] &= c[0];
-      tm[1] &= c[1];
-    }
-    if (fns & VP_PROP) {  // proportion.go:161-186
-      uint64_t c[2] = {0ull, 0ull};
-      for (int k = 0; k < L && !panic; ++k) {
-        if (!((pm[k >> 6] >> (k & 63)) & 1ull)) continue;
-        const int q = t.j_queue[t.t_job[t.nt_task[off + k]]];
-        double x[3] = {t.q_alloc[3 * q], t.q_alloc[3 * q + 1], t.q_alloc[3 * q + 2]};
-        bool victim = false;
-        for (int k2 = 0; k2 <= k && !panic; ++k2) {
-          if (!((pm[k2 >> 6] >> (k2 & 63)) & 1ull)) continue;
-          const int t2 = t.nt_task[off + k2];
-          if (t.j_queue[t.t_job[t2]] != q) continue;
-          const double* r = t.t_req + 3 * (size_t)t2;
-          if (res_less3(x, r)) continue;  // skipped, allocation untouched
-          if (!res_le3(r, x)) panic = true;
-          x[0] -= r[0];
-          x[1] -= r[1];
-          x[2] -= r[2];
-          if (k2 == k) victim = res_le3(t.q_deserved + 3 * q, x);
+      bool lpanic = false;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        if (h2 >= nh) break;
+        const uint64_t bits = pm[h2];
+        for (uint64_t b = bits; b; b &= b - 1) {  // preemptees k2 in order (wave-uniform)
+          const int l2 = __builtin_ctzll(b);
+          const int k2 = h2 * 64 + l2;
+          const int32_t j2 = rl_i(jv[h2], l2);
+          const int32_t q2 = rl_i(qv[h2], l2);
+          const double r2[3] = {rl_d(rq[h2][0], l2), rl_d(rq[h2][1], l2), rl_d(rq[h2][2], l2)};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int k = h * 64 + lane;
+            if (!((pm[h] >> lane) & 1ull) || k2 > k) continue;
+            if ((fns & VP_DRF) && j2 == jv[h]) {
+              if (!res_le3(r2, xd[h])) lpanic = true;  // Resource.Sub (resource_info.go:100-110)
+              xd[h][0] -= r2[0];
+              xd[h][1] -= r2[1];
+              xd[h][2] -= r2[2];
+            }
+            if ((fns & VP_PROP) && q2 == qv[h]) {
+              if (!res_less3(xp[h], r2)) {  // Less: skipped, allocation untouched
+                if (!res_le3(r2, xp[h])) lpanic = true;
+                xp[h][0] -= r2[0];
+                xp[h][1] -= r2[1];
+                xp[h][2] -= r2[2];
+                if (k2 == k) vp[h] = res_le3(t.q_deserved + 3 * (size_t)qv[h], xp[h]);
+              }
+            }
+          }
         }
-        if (victim) c[k >> 6] |= 1ull << (k & 63);
       }
-      tm[0] &= c[0];
-      tm[1] &= c[1];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if ((fns & VP_DRF) && ((pm[h] >> lane) & 1ull)) {
+          const double rs = share3(xd[h], t.drf_total);
+          vd[h] = p.ls < rs || fabs(p.ls - rs) <= 0.000001;
+        }
+        if (fns & VP_DRF) tm[h] &= __ballot(vd[h]);
+        if (fns & VP_PROP) tm[h] &= __ballot(vp[h]);
+      }
+      panic = __ballot(lpanic) != 0ull;
+      if (panic) break;
     }
     if (tm[0] | tm[1]) {  // the host passes only the deciding tier (session_plugins.go:59-98)
       vm[0] = tm[0];
@@ -393,36 +427,61 @@ __global__ __launch_bounds__(256) void kbg_victim_kernel(VictimScan p, VictimTab
       break;
     }
   }
-  if (panic) {
-    atomicMin(out, ((uint32_t)n << 1) | 1u);
-    return;
-  }
-  if (!(vm[0] | vm[1])) return;
-  double all[3] = {0.0, 0.0, 0.0};  // validateVictims (preempt.go:242-253)
-  for (int k = 0; k < L; ++k) {
-    if (!((vm[k >> 6] >> (k & 63)) & 1ull)) continue;
-    const double* r = t.t_req + 3 * (size_t)t.nt_task[off + k];
-    all[0] += r[0];
-    all[1] += r[1];
-    all[2] += r[2];
-  }
-  if (res_less3(all, p.req)) return;
-  atomicMin(out, (uint32_t)n << 1);
+  if (panic) return ((uint32_t)n << 1) | 1u;
+  if (!(vm[0] | vm[1])) return kNone;
+  double all[3] = {0.0, 0.0, 0.0};  // validateVictims (preempt.go:242-253), in victims order
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2)
+    for (uint64_t b = vm[h2]; b; b &= b - 1) {
+      const int l2 = __builtin_ctzll(b);
+      all[0] += rl_d(rq[h2][0], l2);
+      all[1] += rl_d(rq[h2][1], l2);
+      all[2] += rl_d(rq[h2][2], l2);
+    }
+  if (res_less3(all, p.req)) return kNone;
+  return (uint32_t)n << 1;
 }
 
-hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* out, hipStream_t stream,
+__global__ __launch_bounds__(256) void kbg_victim_kernel(VictimScan p, VictimTables t, uint32_t* __restrict__ blk_min) {
+  __shared__ uint32_t s_key[kVictimWaves];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  uint32_t best = 0xffffffffu;
+  for (int row = blockIdx.x * kVictimWaves + w; row < p.node_n; row += gridDim.x * kVictimWaves) {
+    const uint32_t key = victim_node(p, t, row, lane);  // wave-uniform
+    if (key != 0xffffffffu) {
+      best = key;  // rows ascend: the wave's first stop is its minimum
+      break;
+    }
+  }
+  if (lane == 0) s_key[w] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t m = s_key[0];
+#pragma unroll
+    for (int i = 1; i < kVictimWaves; ++i) m = min(m, s_key[i]);
+    *(volatile uint32_t*)(blk_min + blockIdx.x) = m;
+  }
+}
+
+hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* blk_min, hipStream_t stream,
                               hipEvent_t start, hipEvent_t stop) {
-  if (p.node_n <= 0) return hipSuccess;
-  hipExtLaunchKernelGGL(kbg_victim_kernel, dim3((p.node_n + 255) / 256), dim3(256), 0, stream, start, stop, 0, p, t,
-                        out);
+  hipExtLaunchKernelGGL(kbg_victim_kernel, dim3(kbg_victim_blocks(p.node_n)), dim3(64 * kVictimWaves), 0, stream,
+                        start, stop, 0, p, t, blk_min);
   return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void kbg_state_apply_kernel(VictimTables t, const StateDelta* __restrict__ d,
-                                                              int32_t n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const StateDelta x = d[i];
+__device__ __forceinline__ void apply_node_delta(const NodeSoA& nd, const NodeDelta& x) {
+  nd.idle_cpu[x.node] = x.idle[0];
+  nd.idle_mem[x.node] = x.idle[1];
+  nd.idle_gpu[x.node] = x.idle[2];
+  nd.rel_cpu[x.node] = x.rel[0];
+  nd.rel_mem[x.node] = x.rel[1];
+  nd.rel_gpu[x.node] = x.rel[2];
+  nd.ntasks[x.node] = x.ntasks;
+}
+
+__device__ __forceinline__ void apply_state_delta(const VictimTables& t, const StateDelta& x) {
   switch (x.kind) {
     case 0: t.t_run[x.index] = (uint8_t)(x.v[0] != 0.0); break;
     case 1: t.j_ready[x.index] = (int32_t)x.v[0]; break;
@@ -435,9 +494,34 @@ __global__ __launch_bounds__(256) void kbg_state_apply_kernel(VictimTables t, co
   }
 }
 
-hipError_t launch_state_apply(const VictimTables& t, const StateDelta* d, int32_t n, hipStream_t stream) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(kbg_state_apply_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, t, d, n);
+__global__ __launch_bounds__(256) void kbg_victim_prep_kernel(NodeSoA nd, VictimTables t,
+                                                              const NodeDelta* __restrict__ d, int32_t nn,
+                                                              const StateDelta* __restrict__ sd, int32_t ns) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nn) apply_node_delta(nd, d[i]);
+  else if (i < nn + ns) apply_state_delta(t, sd[i - nn]);
+}
+
+__global__ __launch_bounds__(64) void kbg_victim_prep_inline_kernel(NodeSoA nd, VictimTables t, VictimPrepArgs a) {
+  for (int i = threadIdx.x; i < a.nn + a.ns; i += 64) {
+    if (i < a.nn) apply_node_delta(nd, a.nd[i]);
+    else apply_state_delta(t, a.sd[i - a.nn]);
+  }
+}
+
+hipError_t launch_victim_prep_inline(const NodeSoA& n, const VictimTables& t, const VictimPrepArgs& a,
+                                     hipStream_t stream) {
+  if (a.nn + a.ns <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kbg_victim_prep_inline_kernel, dim3(1), dim3(64), 0, stream, n, t, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_victim_prep(const NodeSoA& n, const VictimTables& t, const NodeDelta* nd, int32_t n_nodes,
+                              const StateDelta* sd, int32_t n_state, hipStream_t stream) {
+  const int32_t tot = n_nodes + n_state;
+  if (tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kbg_victim_prep_kernel, dim3((tot + 255) / 256), dim3(256), 0, stream, n, t, nd, n_nodes, sd,
+                     n_state);
   return hipGetLastError();
 }
 

@@ -442,9 +442,9 @@ void free_device(Session& S) {
   if (S.h_deltas) (void)hipHostFree(S.h_deltas);
   if (S.h_mdeltas) (void)hipHostFree(S.h_mdeltas);
   S.h_mdeltas = nullptr;
-  if (S.h_vout) (void)hipHostFree(S.h_vout);
+  if (S.h_vblk) (void)hipHostFree(S.h_vblk);
   if (S.h_sdeltas) (void)hipHostFree(S.h_sdeltas);
-  S.h_vout = nullptr;
+  S.h_vblk = nullptr;
   S.h_sdeltas = nullptr;
   S.vt_ready = false;
   S.h_tasks = nullptr;
@@ -1475,6 +1475,8 @@ void begin_cycle(Session& S) {
   S.fit.assign(S.n_jobs, Session::FitCounts{});
   const kbg_stats prev = S.stats;
   S.stats = kbg_stats{};
+  S.vk_timed_ms = 0;
+  S.vk_timed = 0;
   S.stats.n_classes = prev.n_classes;
   S.stats.shards = prev.shards;
   S.stats.shard_index = prev.shard_index;
@@ -1911,9 +1913,12 @@ void vt_delta(Session& S, int32_t kind, int32_t index, double a, double b, doubl
 
 // Applies the queued state changes. Each carries the entry's new value, so
 // only the last one of an entry is kept (the apply kernel writes in parallel).
-kbg_status vt_flush(Session& S) {
-  if (S.sdeltas.empty()) return KBG_OK;
-  {
+// Node rows and victim-table entries changed by the host since the last
+// scan, in one launch that reads them in place from host-mapped staging. The
+// staging buffers are rewritten only once the previous launch has retired
+// (the victim scan's synchronize, or an explicit one here).
+kbg_status victim_push(Session& S, const std::vector<int32_t>& touched) {
+  if (!S.sdeltas.empty()) {  // last write of each entry wins
     std::unordered_set<int64_t> seen;
     std::vector<kbg::StateDelta> uniq;
     for (size_t i = S.sdeltas.size(); i-- > 0;)
@@ -1921,14 +1926,44 @@ kbg_status vt_flush(Session& S) {
         uniq.push_back(S.sdeltas[i]);
     S.sdeltas.swap(uniq);
   }
-  for (size_t m = 0; m < S.sdeltas.size();) {
-    const int32_t cnt = (int32_t)std::min<size_t>(S.sdeltas.size() - m, (size_t)kbg::kMaskDeltaCap);
-    std::memcpy(S.h_sdeltas, S.sdeltas.data() + m, (size_t)cnt * sizeof(kbg::StateDelta));
-    HIP_TRY(hipMemcpyAsync(S.d_sdeltas, S.h_sdeltas, (size_t)cnt * sizeof(kbg::StateDelta), hipMemcpyHostToDevice,
-                           S.stream));
-    HIP_TRY(kbg::launch_state_apply(S.vt, S.d_sdeltas, cnt, S.stream));
-    HIP_TRY(hipStreamSynchronize(S.stream));  // the staging buffer is reused next
-    m += cnt;
+  {  // few changes: in the kernel arguments
+    int32_t nn = 0;
+    for (int32_t n : touched) nn += n >= S.tab_lo && n < S.tab_lo + S.tab_n;
+    if (nn <= kbg::kArgNodeDeltas && S.sdeltas.size() <= (size_t)kbg::kArgStateDeltas) {
+      kbg::VictimPrepArgs a;
+      a.nn = 0;
+      for (int32_t n : touched) {
+        if (n < S.tab_lo || n >= S.tab_lo + S.tab_n) continue;
+        kbg::NodeDelta& d = a.nd[a.nn++];
+        int32_t mt;
+        d.node = n - S.tab_lo;
+        device_row(S, n, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &mt);
+      }
+      a.ns = (int32_t)S.sdeltas.size();
+      if (a.ns) std::memcpy(a.sd, S.sdeltas.data(), (size_t)a.ns * sizeof(kbg::StateDelta));
+      S.sdeltas.clear();
+      HIP_TRY(kbg::launch_victim_prep_inline(S.d_nodes, S.vt, a, S.stream));
+      return KBG_OK;
+    }
+  }
+  size_t ti = 0, si = 0;
+  while (ti < touched.size() || si < S.sdeltas.size()) {
+    if (S.vstage_busy) HIP_TRY(hipStreamSynchronize(S.stream));
+    int32_t nn = 0;
+    for (; ti < touched.size() && nn < S.K; ++ti) {
+      const int32_t n = touched[ti];
+      if (n < S.tab_lo || n >= S.tab_lo + S.tab_n) continue;  // another rank's row
+      kbg::NodeDelta& d = S.h_deltas[nn++];
+      int32_t mt;
+      d.node = n - S.tab_lo;
+      device_row(S, n, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &mt);
+    }
+    const int32_t ns = (int32_t)std::min<size_t>(S.sdeltas.size() - si, (size_t)kbg::kMaskDeltaCap);
+    if (ns > 0) std::memcpy(S.h_sdeltas, S.sdeltas.data() + si, (size_t)ns * sizeof(kbg::StateDelta));
+    si += ns;
+    if (nn + ns == 0) break;
+    HIP_TRY(kbg::launch_victim_prep(S.d_nodes, S.vt, S.h_deltas_dev, nn, S.h_sdeltas_dev, ns, S.stream));
+    S.vstage_busy = true;
   }
   S.sdeltas.clear();
   return KBG_OK;
@@ -1967,11 +2002,17 @@ kbg_status vt_setup(Session& S) {
         (st = hupload(S, &djob, tj)) || (st = hupload(S, &dtr, tr)) || (st = dalloc(S, &drun, T)) ||
         (st = hupload(S, &djq, jq)) || (st = hupload(S, &djm, jm)) || (st = dalloc(S, &djr, J)) ||
         (st = dalloc(S, &dja, 3 * J)) || (st = dalloc(S, &dqa, 3 * Q)) || (st = hupload(S, &dqd, qd)) ||
-        (st = dalloc(S, &S.d_vout, 1)) || (st = dalloc(S, &S.d_sdeltas, kbg::kMaskDeltaCap)))
+        (st = dalloc(S, &S.d_vblk, kbg::kMaxVictimBlocks)) ||
+        (st = dalloc(S, &S.d_vblk_red, kbg::kMaxVictimBlocks)))
       return st;
-    HIP_TRY(hipHostMalloc((void**)&S.h_vout, sizeof(uint32_t), hipHostMallocDefault));
+    HIP_TRY(hipMemset(S.d_vblk, 0xff, kbg::kMaxVictimBlocks * sizeof(uint32_t)));  // entries past the grid
+    HIP_TRY(hipHostMalloc((void**)&S.h_vblk, kbg::kMaxVictimBlocks * sizeof(uint32_t),
+                          hipHostMallocCoherent | hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void**)&S.h_vblk_dev, S.h_vblk, 0));
+    HIP_TRY(hipHostGetDevicePointer((void**)&S.h_deltas_dev, S.h_deltas, 0));
     HIP_TRY(hipHostMalloc((void**)&S.h_sdeltas, (size_t)kbg::kMaskDeltaCap * sizeof(kbg::StateDelta),
-                          hipHostMallocDefault));
+                          hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void**)&S.h_sdeltas_dev, S.h_sdeltas, 0));
     v.panic_node = dpn;
     v.nt_off = doff;
     v.nt_task = dtask;
@@ -2200,21 +2241,39 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
   Res la = S.fin.jalloc[pj];
   kbg::res_add(la, S.treq[t]);
   p.ls = share_of(la, S.drf_total);
-  kbg_status st = vt_flush(S);
+  kbg_status st = victim_push(S, L.touched);
   if (st != KBG_OK) return st;
-  HIP_TRY(hipMemsetAsync(S.d_vout, 0xff, sizeof(uint32_t), S.stream));
-  HIP_TRY(kbg::launch_victim_scan(p, S.vt, S.d_vout, S.stream, S.ev[0], S.ev[1]));
+  L.touched.clear();
+  ++L.stamp;
+  // unsharded: the workgroup minima land straight in host memory; sharded:
+  // in device memory, min-reduced element-wise over the ranks, copied back
+  int32_t nblk = kbg::kbg_victim_blocks(p.node_n);
+  const bool timed = (S.stats.victim_scans & 15) == 0;  // HIP-event time of every 16th launch
+  HIP_TRY(kbg::launch_victim_scan(p, S.vt, S.comm ? S.d_vblk : S.h_vblk_dev, S.stream, timed ? S.ev[0] : nullptr,
+                                  timed ? S.ev[1] : nullptr));
   if (S.comm) {
-    const ncclResult_t nr = ncclAllReduce(S.d_vout, S.d_vout, 1, ncclUint32, ncclMin, S.comm->nccl, S.stream);
+    nblk = kbg::kMaxVictimBlocks;
+    const ncclResult_t nr =
+        ncclAllReduce(S.d_vblk, S.d_vblk_red, nblk, ncclUint32, ncclMin, S.comm->nccl, S.stream);
     if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+    HIP_TRY(hipMemcpyAsync(S.h_vblk, S.d_vblk_red, nblk * sizeof(uint32_t), hipMemcpyDeviceToHost, S.stream));
   }
-  HIP_TRY(hipMemcpyAsync(S.h_vout, S.d_vout, sizeof(uint32_t), hipMemcpyDeviceToHost, S.stream));
   HIP_TRY(hipStreamSynchronize(S.stream));
-  float ms = 0;
-  HIP_TRY(hipEventElapsedTime(&ms, S.ev[0], S.ev[1]));
-  S.stats.victim_kernel_ms += ms;
+  S.vstage_busy = false;
+  if (timed) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, S.ev[0], S.ev[1]));
+    S.vk_timed_ms += ms;
+    S.vk_timed++;
+  }
   S.stats.victim_scans++;
-  const uint32_t key = *S.h_vout;
+  S.stats.victim_kernel_ms = S.vk_timed_ms / S.vk_timed * (double)S.stats.victim_scans;
+  uint32_t key = UINT32_MAX;
+  const volatile uint32_t* blk = S.h_vblk;
+  for (int32_t b = 0; b < nblk; ++b) {
+    const uint32_t v = blk[b];
+    if (v < key) key = v;
+  }
   if (key == UINT32_MAX) return KBG_OK;  // no node: the task stays Pending
   const int32_t n = (int32_t)(key >> 1);
   if (key & 1u)
@@ -2292,7 +2351,7 @@ struct VictimRun {
   Live L;
   explicit VictimRun(Session& s) : S(s), mark(s.n_nodes, -1), L{s, touched, mark, 0} {}
   kbg_status sync() {  // node rows + plugin state to the device before the next scan
-    kbg_status st = push_deltas(S, touched);
+    kbg_status st = victim_push(S, touched);
     touched.clear();
     ++L.stamp;
     return st;
@@ -2355,10 +2414,10 @@ kbg_status reclaim_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
   }
   if (result == KBG_OK || result == KBG_E_REF_PANIC) {
     kbg_status s2 = R.sync();
-    if (s2 == KBG_OK) s2 = vt_flush(S);
     if (s2 != KBG_OK) return s2;
   }
   HIP_TRY(hipStreamSynchronize(S.stream));
+  S.vstage_busy = false;
   S.stats.reclaim_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return copy_log(S, out, cap, n_out, result);
 }
@@ -2447,10 +2506,10 @@ kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
   result = run();
   if (result == KBG_OK || result == KBG_E_REF_PANIC) {
     kbg_status s2 = R.sync();
-    if (s2 == KBG_OK) s2 = vt_flush(S);
     if (s2 != KBG_OK) return s2;
   }
   HIP_TRY(hipStreamSynchronize(S.stream));
+  S.vstage_busy = false;
   S.stats.preempt_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return copy_log(S, out, cap, n_out, result);
 }

@@ -160,10 +160,16 @@ struct Session {
   int32_t max_candidates = 0;
   kbg::VictimTables vt{};                     // device copies (allocated at the first victim action)
   bool vt_ready = false;
-  uint32_t* d_vout = nullptr;
-  uint32_t* h_vout = nullptr;                 // pinned
-  kbg::StateDelta* d_sdeltas = nullptr;
-  kbg::StateDelta* h_sdeltas = nullptr;       // pinned
+  uint32_t* d_vblk = nullptr;                 // sharded: per-workgroup scan minima [kMaxVictimBlocks], and
+  uint32_t* d_vblk_red = nullptr;             //   their element-wise min over the ranks
+  uint32_t* h_vblk = nullptr;                 // pinned, coherent, device-mapped per-workgroup minima
+  uint32_t* h_vblk_dev = nullptr;
+  kbg::StateDelta* h_sdeltas = nullptr;       // pinned, device-mapped (the prep kernel reads it in place)
+  kbg::StateDelta* h_sdeltas_dev = nullptr;
+  kbg::NodeDelta* h_deltas_dev = nullptr;     // device address of h_deltas
+  bool vstage_busy = false;                   // a prep launch may still read the staging buffers
+  double vk_timed_ms = 0;                     // sampled victim-scan kernel time (this cycle)
+  int64_t vk_timed = 0;
   std::vector<kbg::StateDelta> sdeltas;       // queued victim-table changes
   std::vector<int32_t> be_shape;              // per pod-spec class: grouping id of its BestEffort tasks
   std::vector<int32_t> committed_ready;

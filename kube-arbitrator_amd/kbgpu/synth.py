@@ -23,6 +23,10 @@ CONFIGS = {
             tiers=None),
 }
 
+# C5: contended cluster at ~95% CPU utilisation (reclaim, allocate, backfill, preempt)
+C5 = dict(nodes=10000, jobs=4000, tasks_per_job=50, pending_jobs=200, util=0.95,
+          queues=[("q1", 1), ("q2", 2), ("q3", 3), ("q4", 4)])
+
 NODE_TYPES = {  # (type, cpu cores, memory GiB, gpus)
     "cpu": (32, 128, 0),
     "mem": (64, 256, 0),
@@ -56,7 +60,9 @@ def _node(i, rng, mix):
 
 
 def config_fixture(cid):
-    """BASELINE config `cid` (1-4) as a fixture dict."""
+    """BASELINE config `cid` (1-5) as a fixture dict."""
+    if cid == 5:
+        return contended_config()
     c = CONFIGS[cid]
     rng = random.Random(BASE_SEED + cid)
     nodes = [_node(i, rng, c["mix"]) for i in range(c["nodes"])]
@@ -334,3 +340,52 @@ def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3):
                        ["allocate", "preempt"]])
     return {"name": f"contended-{seed}", "tiers": tiers, "nodes": nds, "pods": pods, "podGroups": pgs,
             "queues": qs, "actions": acts}
+
+
+def contended_config(**over):
+    """BASELINE config 5: 10k nodes x 200k tasks, the cluster ~95% full (CPU)
+    of Running gang jobs spread round-robin over the nodes, most of them in the
+    two low-weight queues (which therefore exceed their proportion share), and
+    200 Pending jobs (10k tasks, pod priority 10 against 1) spread over all four
+    queues. Every task requests the same 3200m / 6Gi, so the reference's
+    eviction loop never underflows (preempt.go:221-226, reclaim.go:152-165) and
+    a pipelined task always fits the Releasing its victim freed. Runs the
+    actions "reclaim, allocate, backfill, preempt" under the default tiers
+    (util.go:30-40), so gang's victim fns (tier 1) decide both actions."""
+    c = dict(C5, **over)  # smaller instances of the same generator for parity tests
+    rng = random.Random(BASE_SEED + 5)
+    nodes = [_node(i, rng, "hetero4") for i in range(c["nodes"])]
+    for n in nodes:  # keep every node usable: the packer below ignores taints and selectors
+        n.pop("taints", None)
+        n.pop("unschedulable", None)
+    queues = [{"name": q, "weight": w} for q, w in c["queues"]]
+    cpu, req = 3200, {"cpu": "3200m", "memory": "6Gi"}
+    room = [int(n["allocatable"]["cpu"]) * 1000 // cpu for n in nodes]
+    cursor = 0
+    n_run = c["jobs"] - c["pending_jobs"]
+    pods, pgs = [], []
+    for j in range(c["jobs"]):
+        ns = f"ns{j % 8}"
+        pg = f"pg-{j:05d}"
+        running = j < n_run
+        if running:
+            q = ("q1", "q1", "q2", "q2", "q2", "q3", "q4")[rng.randrange(7)]
+        else:
+            q = queues[rng.randrange(4)]["name"]
+        pgs.append({"namespace": ns, "name": pg, "minMember": (1, 25, 50)[rng.randrange(3)], "queue": q,
+                    "creationTimestamp": (1_700_000_000 + j) * 1_000_000_000})
+        for t in range(c["tasks_per_job"]):
+            p = {"uid": f"uid-{j:05d}-{t:03d}", "namespace": ns, "name": f"{pg}-{t:03d}", "phase": "Pending",
+                 "annotations": {"scheduling.k8s.io/group-name": pg}, "containers": [{"requests": dict(req)}],
+                 "priority": 1 if running else 10}
+            if running:
+                for _ in range(len(nodes)):  # round-robin over the nodes with room
+                    k = cursor
+                    cursor = (cursor + 1) % len(nodes)
+                    if room[k] > 0:
+                        room[k] -= 1
+                        p["phase"], p["nodeName"] = "Running", nodes[k]["name"]
+                        break
+            pods.append(p)
+    return {"name": "C5", "tiers": None, "nodes": nodes, "pods": pods, "podGroups": pgs, "queues": queues,
+            "actions": ["reclaim", "allocate", "backfill", "preempt"]}

@@ -307,3 +307,24 @@ def test_contended_reclaim_preempt_parity(seed):
     compare_outputs(run_oracle(fx), got)
     if ssn:
         ssn.close()
+
+
+@pytest.mark.parametrize("nodes,jobs,pending", [(300, 120, 8), (1000, 400, 20)])
+def test_config5_scaled_parity(nodes, jobs, pending):
+    """The C5 generator (95% full cluster, reclaim, allocate, backfill,
+    preempt) at reduced size: evictions, pipelines and allocations exact."""
+    fx = synth.contended_config(nodes=nodes, jobs=jobs, pending_jobs=pending)
+    ref = run_oracle(fx)
+    assert ref["status"] == "ok" and ref["evictions"], ref.get("error")
+    got, ssn = run_fixture(fx)
+    compare_outputs(ref, got)
+    ssn.close()
+
+
+@pytest.mark.slow
+def test_config5_full_parity():
+    """C5 (10k nodes x 200k tasks) end to end against the oracle."""
+    fx = synth.config_fixture(5)
+    got, ssn = run_fixture(fx)
+    compare_outputs(run_oracle(fx), got)
+    ssn.close()
