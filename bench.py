@@ -262,7 +262,7 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid):
 
     for _ in range(args.warmup):
         step()
-    cyc, dec, ev, vscans, vms = [], 0, 0, 0, 0.0
+    cyc, dec, ev, vscans, vms, vtries, vevals = [], 0, 0, 0, 0.0, 0, 0
     kdist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
@@ -275,6 +275,8 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid):
         st = ssn.stats()
         vscans += st.victim_scans
         vms += st.victim_kernel_ms
+        vtries += st.victim_tries
+        vevals += st.victim_host_evals
         for k in phase:
             phase[k].append(getattr(st, k))
     torch.cuda.synchronize()
@@ -314,6 +316,8 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid):
         "decisions_per_cycle": dec // max(1, args.steps),
         "evictions_per_cycle": ev // max(1, args.steps),
         "victim_scans_per_cycle": vscans // max(1, args.steps),
+        "victim_tries_per_cycle": vtries // max(1, args.steps),
+        "victim_host_evals_per_cycle": vevals // max(1, args.steps),
         "phase_ms_p50": {k: statistics.median(v) for k, v in phase.items()},
         "open_ms": st.open_ms,
     }

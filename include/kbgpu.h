@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KBG_ABI_VERSION 4
+#define KBG_ABI_VERSION 5
 
 typedef enum kbg_status {
   KBG_OK = 0,
@@ -269,6 +269,8 @@ typedef struct kbg_stats {
   double preempt_ms;       /* wall time of the last kbg_preempt */
   int64_t victim_scans;    /* victim-scan kernel launches (one per preemptor / reclaimer tried) */
   double victim_kernel_ms; /* victim-scan kernel time: HIP-event time of every 16th launch x launches / timed */
+  int64_t victim_tries;    /* reclaimer / preemptor tasks tried (a scan, or the kept stop maps) */
+  int64_t victim_host_evals; /* nodes re-evaluated on the host after a change since the last scan */
 } kbg_stats;
 
 typedef struct kbg_session kbg_session;

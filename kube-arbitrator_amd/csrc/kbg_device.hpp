@@ -203,22 +203,21 @@ hipError_t launch_select(const uint64_t* bits, int32_t W, int32_t Wl, int32_t n_
 hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream);
 hipError_t launch_mask_apply(uint64_t* class_mask, const MaskDelta* deltas, int32_t n_deltas, hipStream_t stream);
 
-// One victim scan. The reference stops at the first node (ssn.Nodes order)
-// with validated victims or a panic; its key is (node << 1 | panic). Waves
-// walk the node range grid-strided, each keeping its first stop (rows ascend,
-// so that is its minimum), and workgroup b writes the min of its waves to
-// blk_min[b] (UINT32_MAX for none). The caller takes the min over the
-// kbg_victim_blocks(node_n) entries: on the host straight from host-mapped
-// memory, or — sharded — after an element-wise ncclAllReduce(min) of the
-// kMaxVictimBlocks-entry array (entries past a rank's grid stay UINT32_MAX).
-constexpr int kVictimWaves = 4;          // waves per workgroup
-constexpr int kMaxVictimBlocks = 1024;
-inline int32_t kbg_victim_blocks(int32_t node_n) {
-  const int32_t b = (node_n + kVictimWaves - 1) / kVictimWaves;
-  return b < 1 ? 1 : (b > kMaxVictimBlocks ? kMaxVictimBlocks : b);
-}
-hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* blk_min, hipStream_t stream,
-                              hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+// One victim scan evaluates every node of the range for one (preemptor,
+// state) and writes two bitmaps of 32-node words, indexed by global node:
+// stop[n] — the reference would stop at node n (validated victims, or a
+// panic), panic[n] — that stop is a panic. The reference's answer is the
+// lowest stop; the host keeps the maps and, as later tries of the same
+// preemptor shape change the state, re-evaluates only the nodes those changes
+// touched (kbg_session.cpp VictimCache). A workgroup (16 waves) covers 32
+// consecutive nodes, two per wave, and writes its two words; sharded, each
+// rank writes the words of its node range (64-node aligned) into zeroed
+// arrays and an element-wise ncclAllReduce(max) of disjoint words is their OR.
+constexpr int kVictimNodesPerBlock = 32;
+constexpr int kVictimBlockWaves = 16;
+inline int32_t kbg_victim_words(int32_t n_nodes) { return (n_nodes + 31) / 32; }
+hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* stop_bits, uint32_t* panic_bits,
+                              hipStream_t stream, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 // Host-side changes before a scan, read in place from host-mapped memory:
 // node rows (NodeInfo.Tasks count / Idle / Releasing) and victim-table
 // entries, in one launch.

@@ -442,32 +442,40 @@ __device__ uint32_t victim_node(const VictimScan& p, const VictimTables& t, int 
   return (uint32_t)n << 1;
 }
 
-__global__ __launch_bounds__(256) void kbg_victim_kernel(VictimScan p, VictimTables t, uint32_t* __restrict__ blk_min) {
-  __shared__ uint32_t s_key[kVictimWaves];
+__global__ __launch_bounds__(64 * kVictimBlockWaves) void kbg_victim_kernel(VictimScan p, VictimTables t,
+                                                                           uint32_t* __restrict__ stop_bits,
+                                                                           uint32_t* __restrict__ panic_bits) {
+  __shared__ uint32_t s_stop, s_panic;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  uint32_t best = 0xffffffffu;
-  for (int row = blockIdx.x * kVictimWaves + w; row < p.node_n; row += gridDim.x * kVictimWaves) {
-    const uint32_t key = victim_node(p, t, row, lane);  // wave-uniform
-    if (key != 0xffffffffu) {
-      best = key;  // rows ascend: the wave's first stop is its minimum
-      break;
+  if (threadIdx.x == 0) s_stop = s_panic = 0u;
+  __syncthreads();
+  const int base = blockIdx.x * kVictimNodesPerBlock;  // rows of this workgroup
+#pragma unroll
+  for (int k = 0; k < kVictimNodesPerBlock / kVictimBlockWaves; ++k) {
+    const int off = w + k * kVictimBlockWaves;
+    const int row = base + off;
+    if (row < p.node_n) {
+      const uint32_t key = victim_node(p, t, row, lane);  // wave-uniform
+      if (key != 0xffffffffu && lane == 0) {
+        atomicOr(&s_stop, 1u << off);
+        if (key & 1u) atomicOr(&s_panic, 1u << off);
+      }
     }
   }
-  if (lane == 0) s_key[w] = best;
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t m = s_key[0];
-#pragma unroll
-    for (int i = 1; i < kVictimWaves; ++i) m = min(m, s_key[i]);
-    *(volatile uint32_t*)(blk_min + blockIdx.x) = m;
+    const int word = (p.node_lo >> 5) + blockIdx.x;  // node_lo is 64-node aligned
+    *(volatile uint32_t*)(stop_bits + word) = s_stop;
+    *(volatile uint32_t*)(panic_bits + word) = s_panic;
   }
 }
 
-hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* blk_min, hipStream_t stream,
-                              hipEvent_t start, hipEvent_t stop) {
-  hipExtLaunchKernelGGL(kbg_victim_kernel, dim3(kbg_victim_blocks(p.node_n)), dim3(64 * kVictimWaves), 0, stream,
-                        start, stop, 0, p, t, blk_min);
+hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* stop_bits, uint32_t* panic_bits,
+                              hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
+  if (p.node_n <= 0) return hipSuccess;
+  hipExtLaunchKernelGGL(kbg_victim_kernel, dim3((p.node_n + kVictimNodesPerBlock - 1) / kVictimNodesPerBlock),
+                        dim3(64 * kVictimBlockWaves), 0, stream, start, stop, 0, p, t, stop_bits, panic_bits);
   return hipGetLastError();
 }
 

@@ -442,9 +442,9 @@ void free_device(Session& S) {
   if (S.h_deltas) (void)hipHostFree(S.h_deltas);
   if (S.h_mdeltas) (void)hipHostFree(S.h_mdeltas);
   S.h_mdeltas = nullptr;
-  if (S.h_vblk) (void)hipHostFree(S.h_vblk);
+  if (S.h_vbits) (void)hipHostFree(S.h_vbits);
   if (S.h_sdeltas) (void)hipHostFree(S.h_sdeltas);
-  S.h_vblk = nullptr;
+  S.h_vbits = nullptr;
   S.h_sdeltas = nullptr;
   S.vt_ready = false;
   S.h_tasks = nullptr;
@@ -1976,6 +1976,7 @@ kbg_status vt_setup(Session& S) {
                Q = (size_t)std::max(1, S.n_queues);
   kbg_status st;
   if (!S.vt_ready) {
+    S.W32 = kbg::kbg_victim_words(S.n_nodes);
     kbg::VictimTables& v = S.vt;
     v.ntasks = S.d_nodes.ntasks;
     v.maxtasks = S.d_nodes.maxtasks;
@@ -2002,13 +2003,29 @@ kbg_status vt_setup(Session& S) {
         (st = hupload(S, &djob, tj)) || (st = hupload(S, &dtr, tr)) || (st = dalloc(S, &drun, T)) ||
         (st = hupload(S, &djq, jq)) || (st = hupload(S, &djm, jm)) || (st = dalloc(S, &djr, J)) ||
         (st = dalloc(S, &dja, 3 * J)) || (st = dalloc(S, &dqa, 3 * Q)) || (st = hupload(S, &dqd, qd)) ||
-        (st = dalloc(S, &S.d_vblk, kbg::kMaxVictimBlocks)) ||
-        (st = dalloc(S, &S.d_vblk_red, kbg::kMaxVictimBlocks)))
+        (st = dalloc(S, &S.d_vbits, 2 * (size_t)S.W32)) || (st = dalloc(S, &S.d_vbits_red, 2 * (size_t)S.W32)))
       return st;
-    HIP_TRY(hipMemset(S.d_vblk, 0xff, kbg::kMaxVictimBlocks * sizeof(uint32_t)));  // entries past the grid
-    HIP_TRY(hipHostMalloc((void**)&S.h_vblk, kbg::kMaxVictimBlocks * sizeof(uint32_t),
+    HIP_TRY(hipMemset(S.d_vbits, 0, 2 * (size_t)S.W32 * sizeof(uint32_t)));  // other ranks' words stay 0
+    HIP_TRY(hipHostMalloc((void**)&S.h_vbits, 2 * (size_t)S.W32 * sizeof(uint32_t),
                           hipHostMallocCoherent | hipHostMallocMapped));
-    HIP_TRY(hipHostGetDevicePointer((void**)&S.h_vblk_dev, S.h_vblk, 0));
+    HIP_TRY(hipHostGetDevicePointer((void**)&S.h_vbits_dev, S.h_vbits, 0));
+    // per job, the nodes holding its tasks Running at open (the only tasks a
+    // victim fn can see; their job's readiness / allocation feed the fns)
+    std::vector<std::vector<int32_t>> jn(S.n_jobs);
+    for (int32_t n = 0; n < S.n_nodes; ++n)
+      for (int32_t k = S.nt_off[n]; k < S.nt_off[n + 1]; ++k) {
+        std::vector<int32_t>& l = jn[S.task_job[S.nt_task[k]]];
+        if (l.empty() || l.back() != n) l.push_back(n);
+      }
+    S.jn_off.assign(S.n_jobs + 1, 0);
+    S.jn_node.clear();
+    for (int32_t j = 0; j < S.n_jobs; ++j) {
+      S.jn_node.insert(S.jn_node.end(), jn[j].begin(), jn[j].end());
+      S.jn_off[j + 1] = (int32_t)S.jn_node.size();
+    }
+    S.vc.stop.assign(S.W32, 0u);
+    S.vc.panic.assign(S.W32, 0u);
+    S.vc.unk.assign(S.W32, 0u);
     HIP_TRY(hipHostGetDevicePointer((void**)&S.h_deltas_dev, S.h_deltas, 0));
     HIP_TRY(hipHostMalloc((void**)&S.h_sdeltas, (size_t)kbg::kMaskDeltaCap * sizeof(kbg::StateDelta),
                           hipHostMallocMapped));
@@ -2054,6 +2071,21 @@ kbg_status vt_setup(Session& S) {
   return KBG_OK;
 }
 
+// ---- victim-scan stop maps kept current on the host (Session::VictimCache).
+// A node's stop status for a preemptor depends on the node (static predicate,
+// pod count, its Running tasks) and, through the victim fns, on the gang
+// readiness and drf allocation of the jobs of those tasks and on the
+// proportion allocation of their queues. Every change marks what it can
+// affect unknown; a queue allocation change under a proportion fn affects
+// every node and drops the maps.
+void vc_dirty_node(Session& S, int32_t n) {
+  if (S.vc.valid && n >= 0) S.vc.unk[n >> 5] |= 1u << (n & 31);
+}
+void vc_dirty_job(Session& S, int32_t j) {
+  if (!S.vc.valid) return;
+  for (int32_t k = S.jn_off[j]; k < S.jn_off[j + 1]; ++k) vc_dirty_node(S, S.jn_node[k]);
+}
+
 // The plugin and gang state an event changes (drf.go:130-148,
 // proportion.go:196-216, gang readiness), mirrored to the victim tables.
 struct Live {
@@ -2062,12 +2094,14 @@ struct Live {
   std::vector<int32_t>& mark;
   int32_t stamp;
   void touch(int32_t n) {
+    vc_dirty_node(S, n);
     if (n >= 0 && mark[n] != stamp) {
       mark[n] = stamp;
       touched.push_back(n);
     }
   }
   void ready(int32_t j, int32_t d) {
+    vc_dirty_job(S, j);
     S.committed_ready[j] += d;
     S.fin.jready[j] = S.committed_ready[j];
     vt_delta(S, 1, j, (double)S.committed_ready[j], 0, 0);
@@ -2082,8 +2116,10 @@ struct Live {
       else if (!kbg::res_sub(a, r)) return false;
       S.fin.jshare[j] = share_of(a, S.drf_total);
       vt_delta(S, 2, j, a.c, a.m, a.g);
+      if (S.vc.fns & kbg::VP_DRF) vc_dirty_job(S, j);
     }
     if (S.has_prop) {
+      if (S.vc.fns & kbg::VP_PROP) S.vc.valid = false;
       const int32_t q = S.job_queue[j];
       Res& a = S.fin.qalloc[q];
       if (add) kbg::res_add(a, r);
@@ -2204,6 +2240,22 @@ bool host_victims(Session& S, int32_t mode, int32_t t, int32_t n, std::vector<in
   return true;
 }
 
+// host_victims plus the rest of the reference's per-node test, for node n
+// against the current host state: 0 the scan moves on, 1 stop, 2 panic.
+int host_stop(Session& S, int32_t mode, int32_t t, int32_t n) {
+  const int32_t cls = S.task_class[t];
+  if (!((S.h_class_mask[(size_t)cls * S.W + (n >> 6)] >> (n & 63)) & 1ull)) return 0;  // static predicate
+  if (S.panic_node[n]) return 2;                                                      // predicates.go:122-123
+  if (S.pred_active && S.ntasks[n] >= S.maxtasks[n]) return 0;                        // :125-127
+  thread_local std::vector<int32_t> v;
+  if (!host_victims(S, mode, t, n, &v)) return 2;
+  if (v.empty()) return 0;
+  Res all{};
+  for (int32_t x : v) kbg::res_add(all, S.treq[x]);  // validateVictims (preempt.go:242-253)
+  const Res& req = S.treq[t];
+  return (all.c < req.c && all.m < req.m && all.g < req.g) ? 0 : 1;
+}
+
 // One statement (statement.go); a null statement is the session itself
 // (reclaim uses ssn.Evict / ssn.Pipeline directly).
 struct Stmt {
@@ -2241,42 +2293,75 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
   Res la = S.fin.jalloc[pj];
   kbg::res_add(la, S.treq[t]);
   p.ls = share_of(la, S.drf_total);
-  kbg_status st = victim_push(S, L.touched);
-  if (st != KBG_OK) return st;
-  L.touched.clear();
-  ++L.stamp;
-  // unsharded: the workgroup minima land straight in host memory; sharded:
-  // in device memory, min-reduced element-wise over the ranks, copied back
-  int32_t nblk = kbg::kbg_victim_blocks(p.node_n);
-  const bool timed = (S.stats.victim_scans & 15) == 0;  // HIP-event time of every 16th launch
-  HIP_TRY(kbg::launch_victim_scan(p, S.vt, S.comm ? S.d_vblk : S.h_vblk_dev, S.stream, timed ? S.ev[0] : nullptr,
-                                  timed ? S.ev[1] : nullptr));
-  if (S.comm) {
-    nblk = kbg::kMaxVictimBlocks;
-    const ncclResult_t nr =
-        ncclAllReduce(S.d_vblk, S.d_vblk_red, nblk, ncclUint32, ncclMin, S.comm->nccl, S.stream);
-    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
-    HIP_TRY(hipMemcpyAsync(S.h_vblk, S.d_vblk_red, nblk * sizeof(uint32_t), hipMemcpyDeviceToHost, S.stream));
+  S.stats.victim_tries++;
+  const int32_t dfns = p.n_tiers ? p.tier_fns[0] : 0;
+  // ls matters only to a drf fn in the deciding tier
+  // the preemptor's job enters the preemptee filter only through its tasks
+  // Running at open (reclaim filters by queue alone)
+  const int32_t kjob = mode != kbg::VM_RECLAIM && S.jn_off[pj + 1] > S.jn_off[pj] ? pj : -1;
+  const kbg::VictimKey key{mode, kjob, p.cls, p.queue, {p.req[0], p.req[1], p.req[2]}, (dfns & kbg::VP_DRF) ? p.ls : 0.0};
+  Session::VictimCache& vc = S.vc;
+  if (!(vc.valid && vc.key == key)) {
+    // device scan of every node against the current state
+    kbg_status st = victim_push(S, L.touched);
+    if (st != KBG_OK) return st;
+    L.touched.clear();
+    ++L.stamp;
+    uint32_t* bits = S.comm ? S.d_vbits : S.h_vbits_dev;
+    const bool timed = (S.stats.victim_scans & 15) == 0 && p.node_n > 0;  // HIP-event time of every 16th launch
+    HIP_TRY(kbg::launch_victim_scan(p, S.vt, bits, bits + S.W32, S.stream, timed ? S.ev[0] : nullptr,
+                                    timed ? S.ev[1] : nullptr));
+    if (S.comm) {  // disjoint words of the ranks: element-wise max is their OR
+      const ncclResult_t nr =
+          ncclAllReduce(S.d_vbits, S.d_vbits_red, 2 * (size_t)S.W32, ncclUint32, ncclMax, S.comm->nccl, S.stream);
+      if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+      HIP_TRY(hipMemcpyAsync(S.h_vbits, S.d_vbits_red, 2 * (size_t)S.W32 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                             S.stream));
+    }
+    HIP_TRY(hipStreamSynchronize(S.stream));
+    S.vstage_busy = false;
+    if (timed) {
+      float ms = 0;
+      HIP_TRY(hipEventElapsedTime(&ms, S.ev[0], S.ev[1]));
+      S.vk_timed_ms += ms;
+      S.vk_timed++;
+    }
+    S.stats.victim_scans++;
+    if (S.vk_timed) S.stats.victim_kernel_ms = S.vk_timed_ms / S.vk_timed * (double)S.stats.victim_scans;
+    const volatile uint32_t* hb = S.h_vbits;
+    for (int32_t w = 0; w < S.W32; ++w) {
+      vc.stop[w] = hb[w];
+      vc.panic[w] = hb[S.W32 + w];
+    }
+    std::fill(vc.unk.begin(), vc.unk.end(), 0u);
+    vc.key = key;
+    vc.fns = dfns;
+    vc.valid = true;
   }
-  HIP_TRY(hipStreamSynchronize(S.stream));
-  S.vstage_busy = false;
-  if (timed) {
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, S.ev[0], S.ev[1]));
-    S.vk_timed_ms += ms;
-    S.vk_timed++;
+  // the first stop in node order: a node changed since the scan is
+  // re-evaluated on the host (host_stop) when the search reaches it
+  int32_t n = -1;
+  bool pan = false;
+  for (int32_t w = 0; w < S.W32 && n < 0; ++w) {
+    for (uint32_t cand = vc.stop[w] | vc.unk[w]; cand; cand &= cand - 1) {
+      const int b = __builtin_ctz(cand);
+      const uint32_t bit = 1u << b;
+      const int32_t node = w * 32 + b;
+      if (vc.unk[w] & bit) {
+        vc.unk[w] &= ~bit;
+        const int r = host_stop(S, mode, t, node);
+        S.stats.victim_host_evals++;
+        vc.stop[w] = r ? (vc.stop[w] | bit) : (vc.stop[w] & ~bit);
+        vc.panic[w] = r == 2 ? (vc.panic[w] | bit) : (vc.panic[w] & ~bit);
+        if (!r) continue;
+      }
+      n = node;
+      pan = (vc.panic[w] & bit) != 0;
+      break;
+    }
   }
-  S.stats.victim_scans++;
-  S.stats.victim_kernel_ms = S.vk_timed_ms / S.vk_timed * (double)S.stats.victim_scans;
-  uint32_t key = UINT32_MAX;
-  const volatile uint32_t* blk = S.h_vblk;
-  for (int32_t b = 0; b < nblk; ++b) {
-    const uint32_t v = blk[b];
-    if (v < key) key = v;
-  }
-  if (key == UINT32_MAX) return KBG_OK;  // no node: the task stays Pending
-  const int32_t n = (int32_t)(key >> 1);
-  if (key & 1u)
+  if (n < 0) return KBG_OK;  // no node: the task stays Pending
+  if (pan)
     return fail(KBG_E_REF_PANIC, "victim selection panics on node " + S.strs[S.nodes_in[n].name] +
                                      " (nil Node or Resource.Sub underflow in a victim fn)");
   std::vector<int32_t> victims;
@@ -2350,7 +2435,11 @@ struct VictimRun {
   std::vector<int32_t> mark, touched;
   Live L;
   explicit VictimRun(Session& s) : S(s), mark(s.n_nodes, -1), L{s, touched, mark, 0} {}
-  kbg_status sync() {  // node rows + plugin state to the device before the next scan
+  // Node rows and plugin state reach the device before the next scan
+  // (try_task) or at the end of the action (flush); between scans the host
+  // stop maps carry the changes.
+  kbg_status sync() { return KBG_OK; }
+  kbg_status flush() {
     kbg_status st = victim_push(S, touched);
     touched.clear();
     ++L.stamp;
@@ -2367,6 +2456,7 @@ kbg_status reclaim_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
   if (!S.cycle_started) begin_cycle(S);
   S.reclaimed = true;
   S.action = KBG_ACTION_RECLAIM;
+  S.vc.valid = false;  // other actions changed the session since any earlier scan
   if ((st = vt_setup(S)) != KBG_OK) return st;
   VictimRun R(S);
   auto queue_less = [&](int32_t a, int32_t b) {  // QueueOrderFn (proportion share, then UID)
@@ -2413,7 +2503,7 @@ kbg_status reclaim_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
     if (outcome == TRY_ASSIGNED) push(qheap, q, queue_less);
   }
   if (result == KBG_OK || result == KBG_E_REF_PANIC) {
-    kbg_status s2 = R.sync();
+    kbg_status s2 = R.flush();
     if (s2 != KBG_OK) return s2;
   }
   HIP_TRY(hipStreamSynchronize(S.stream));
@@ -2430,6 +2520,7 @@ kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
   if (!S.cycle_started) begin_cycle(S);
   S.preempted = true;
   S.action = KBG_ACTION_PREEMPT;
+  S.vc.valid = false;  // other actions changed the session since any earlier scan
   if ((st = vt_setup(S)) != KBG_OK) return st;
   VictimRun R(S);
   auto job_less = [&](int32_t a, int32_t b) { return make_job_key(S, S.fin, a) < make_job_key(S, S.fin, b); };
@@ -2505,7 +2596,7 @@ kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
   };
   result = run();
   if (result == KBG_OK || result == KBG_E_REF_PANIC) {
-    kbg_status s2 = R.sync();
+    kbg_status s2 = R.flush();
     if (s2 != KBG_OK) return s2;
   }
   HIP_TRY(hipStreamSynchronize(S.stream));

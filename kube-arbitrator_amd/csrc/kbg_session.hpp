@@ -82,6 +82,19 @@ struct Engine {
   std::vector<int32_t> qrank;   // position of each queue in qorder; qrank[n_queues] = INT32_MAX (sentinel id)
 };
 
+// What a node's stop status depends on besides the session state: the
+// scan's mode, the preemptor's job, pod-spec class, queue, request and (drf)
+// its job's share with it placed.
+struct VictimKey {
+  int32_t mode = -1, job = -1, cls = -1, queue = -1;
+  double req[3] = {0, 0, 0};
+  double ls = 0;
+  bool operator==(const VictimKey& o) const {
+    return mode == o.mode && job == o.job && cls == o.cls && queue == o.queue && req[0] == o.req[0] &&
+           req[1] == o.req[1] && req[2] == o.req[2] && ls == o.ls;
+  }
+};
+
 struct Session {
   // ---- copied snapshot
   std::vector<std::string> strs;
@@ -160,10 +173,22 @@ struct Session {
   int32_t max_candidates = 0;
   kbg::VictimTables vt{};                     // device copies (allocated at the first victim action)
   bool vt_ready = false;
-  uint32_t* d_vblk = nullptr;                 // sharded: per-workgroup scan minima [kMaxVictimBlocks], and
-  uint32_t* d_vblk_red = nullptr;             //   their element-wise min over the ranks
-  uint32_t* h_vblk = nullptr;                 // pinned, coherent, device-mapped per-workgroup minima
-  uint32_t* h_vblk_dev = nullptr;
+  uint32_t* d_vbits = nullptr;                // sharded: [2][W32] stop / panic words of this rank's nodes, and
+  uint32_t* d_vbits_red = nullptr;            //   their OR over the ranks (element-wise max of disjoint words)
+  uint32_t* h_vbits = nullptr;                // pinned, coherent, device-mapped [2][W32] stop / panic words
+  uint32_t* h_vbits_dev = nullptr;
+  int32_t W32 = 0;                            // 32-node words over all N nodes
+  // Stop maps of the last victim scan, kept current on the host between
+  // scans (kbg_session.cpp VictimCache): valid for one preemptor shape; a
+  // node whose inputs changed since the scan is marked unknown and
+  // re-evaluated on the host when a search reaches it.
+  struct VictimCache {
+    bool valid = false;
+    VictimKey key;                            // the preemptor shape the maps are for
+    int32_t fns = 0;                          // victim fns of the deciding tier
+    std::vector<uint32_t> stop, panic, unk;   // [W32]
+  } vc;
+  std::vector<int32_t> jn_off, jn_node;       // per job: the nodes holding its tasks Running at open
   kbg::StateDelta* h_sdeltas = nullptr;       // pinned, device-mapped (the prep kernel reads it in place)
   kbg::StateDelta* h_sdeltas_dev = nullptr;
   kbg::NodeDelta* h_deltas_dev = nullptr;     // device address of h_deltas

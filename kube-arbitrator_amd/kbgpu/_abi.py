@@ -35,7 +35,7 @@ DISABLE_RECLAIMABLE = 1 << 4
 DISABLE_QUEUE_ORDER = 1 << 5
 DISABLE_PREDICATE = 1 << 6
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 COMM_ID_BYTES = 128
 
 KIND_ALLOCATE = 0
@@ -154,7 +154,8 @@ class kbg_stats(ctypes.Structure):
                 ("allocate_ms", f64), ("open_ms", f64), ("engine_ms", f64), ("resolve_ms", f64),
                 ("device_ms", f64), ("delta_ms", f64), ("replayed", i64), ("n_classes", i32), ("shards", i32), ("shard_index", i32),
                 ("int_scan", i32), ("exchange_ms", f64), ("backfill_ms", f64),
-                ("reclaim_ms", f64), ("preempt_ms", f64), ("victim_scans", i64), ("victim_kernel_ms", f64)]
+                ("reclaim_ms", f64), ("preempt_ms", f64), ("victim_scans", i64), ("victim_kernel_ms", f64),
+                ("victim_tries", i64), ("victim_host_evals", i64)]
 
 
 class kbg_eviction(ctypes.Structure):
