@@ -11,7 +11,7 @@ sys.path.insert(0, PKG)
 
 def main():
     cid = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-    lib = os.path.join(HERE, "libkbg_tools.so")
+    lib = os.environ.get("TOOLS_LIB", os.path.join(HERE, "libkbg_tools.so"))
     subprocess.run(["make", "-s", "-C", PKG, "tools"], check=True)
     from kbgpu import _abi, synth
     from kbgpu.cache import cache_from_fixture
@@ -24,7 +24,7 @@ def main():
     L.kbg_tool_engine_ns_per_step.restype = ctypes.c_double
     opts = _abi.kbg_options()
     steps, chk = ctypes.c_int64(), ctypes.c_double()
-    ns = L.kbg_tool_engine_ns_per_step(ctypes.byref(flat.snap), ctypes.byref(opts), 5, ctypes.byref(steps),
+    ns = L.kbg_tool_engine_ns_per_step(ctypes.byref(flat.snap), ctypes.byref(opts), int(os.environ.get("REPS", "5")), ctypes.byref(steps),
                                        ctypes.byref(chk), int(os.environ.get("PROF", "0")))
     print(f"C{cid}: {steps.value} steps, {ns:.1f} ns/step, engine {ns * steps.value / 1e6:.2f} ms, checksum {chk.value:.0f}")
 

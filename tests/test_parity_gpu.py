@@ -328,3 +328,15 @@ def test_config5_full_parity():
     got, ssn = run_fixture(fx)
     compare_outputs(run_oracle(fx), got)
     ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_contended_large_parity(seed):
+    """Bigger contended clusters: many tries per preemptor shape, so the host
+    keeps the victim scan's stop maps across evictions, pipelines and
+    discarded statements before the next scan."""
+    fx = synth.contended_fixture(5000 + seed, nodes=40, jobs=30, tasks=10, queues=3)
+    got, ssn = run_fixture(fx)
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
