@@ -300,6 +300,17 @@ struct Pod {
   bool has_affinity = false, has_node_affinity = false, has_required = false;
   std::vector<NodeSelectorTerm> terms;
   bool has_pod_affinity = false, has_pod_anti_affinity = false;
+  struct LabelSelector {  // metav1.LabelSelector; absent = nil (selects nothing)
+    bool present = false;
+    StrMap matchLabels;
+    std::vector<NodeSelectorRequirement> exprs;
+  };
+  struct AffinityTerm {  // v1.PodAffinityTerm
+    LabelSelector selector;
+    std::vector<std::string> namespaces;
+    std::string topologyKey;
+  };
+  std::vector<AffinityTerm> aff_terms, anti_terms;  // RequiredDuringSchedulingIgnoredDuringExecution
   std::vector<Toleration> tolerations;
   std::vector<Value> containers_requests;
   bool has_host_port = false;
@@ -361,8 +372,30 @@ static Pod parse_pod(const Value& v) {
           }
       }
     }
-    if (const Value* pa = aff->get("podAffinity"); pa && !pa->is_null()) p.has_pod_affinity = true;
-    if (const Value* pa = aff->get("podAntiAffinity"); pa && !pa->is_null()) p.has_pod_anti_affinity = true;
+    auto parse_terms = [](const Value* pa, std::vector<Pod::AffinityTerm>* out) {
+      const Value* rq = pa->get("requiredDuringSchedulingIgnoredDuringExecution");
+      if (!rq || !rq->is_arr()) return;
+      for (auto& t : rq->arr) {
+        Pod::AffinityTerm term;
+        if (const Value* ls = t.get("labelSelector"); ls && ls->is_obj()) {
+          term.selector.present = true;
+          term.selector.matchLabels = parse_strmap(ls->get("matchLabels"));
+          term.selector.exprs = parse_reqs(ls->get("matchExpressions"));
+        }
+        if (const Value* ns = t.get("namespaces"); ns && ns->is_arr())
+          for (auto& x : ns->arr) term.namespaces.push_back(x.s);
+        term.topologyKey = t.str("topologyKey");
+        out->push_back(term);
+      }
+    };
+    if (const Value* pa = aff->get("podAffinity"); pa && pa->is_obj()) {
+      p.has_pod_affinity = true;
+      parse_terms(pa, &p.aff_terms);
+    }
+    if (const Value* pa = aff->get("podAntiAffinity"); pa && pa->is_obj()) {
+      p.has_pod_anti_affinity = true;
+      parse_terms(pa, &p.anti_terms);
+    }
   }
   if (const Value* ts = v.get("tolerations"); ts && ts->is_arr())
     for (auto& t : ts->arr) p.tolerations.push_back({t.str("key"), t.str("operator"), t.str("value"), t.str("effect")});
@@ -752,6 +785,7 @@ struct Session {  // framework/session.go:35-61
   // device path refuses reclaim/preempt for such sessions (kbgpu.h), so the
   // oracle draws the same boundary there.
   bool pending_host_ports = false;
+  bool pod_affinity_terms = false;  // some task of the session carries a required pod (anti)affinity term
 
   // run-time bookkeeping for the decision log
   std::vector<Decision> decisions;
@@ -1251,23 +1285,148 @@ struct Predicates {
   bool ghost = false;          // some allocated-status pod names a node outside the session
   std::unordered_map<int64_t, char> static_cache;
 
-  // predicates.go:45-89 FilteredList + vendor predicates.go:1273-1282 GetNodeInfo errors
-  bool affinity_ok_faithful(NodeInfo* node) {
+  // ---- PodAffinityChecker.InterPodAffinityMatches with meta == nil (vendor
+  // predicates.go:1155-1182), the slow path kube-batch takes
+  // (pkg/scheduler/plugins/predicates/predicates.go:185-198).
+  // podLister.FilteredList(nodeInfo.Filter, Everything()) (predicates.go:67-89,
+  // vendor cache/node_info.go:692-702): every AllocatedStatus task of every job
+  // as a pod whose Spec.NodeName is the task's NodeName, minus the pods that
+  // name this node but are missing from it.
+  std::vector<TaskInfo*> filtered_pods(NodeInfo* node) {
+    std::vector<TaskInfo*> out;
     for (JobInfo* job : ssn->jobs)
       for (auto& kv : job->statusIndex) {
         if (!AllocatedStatus(kv.first)) continue;
         for (auto& t : kv.second.items) {
           TaskInfo* task = t.second;
           bool keep;
-          if (task->pod->nodeName != node->node->name) keep = true;
+          if (task->nodeName != node->node->name) keep = true;
           else {
             keep = false;
             for (auto& nt : node->tasks.items)
               if (nt.second->pod->name == task->pod->name && nt.second->pod->ns == task->pod->ns) { keep = true; break; }
           }
-          if (keep && !ssn->nodeIndex.count(task->nodeName)) return false;
+          if (keep) out.push_back(task);
         }
       }
+    return out;
+  }
+  // metav1.LabelSelectorAsSelector (apimachinery/pkg/apis/meta/v1/helpers.go:31-67)
+  struct Selector { bool err = false, nothing = false, everything = false; std::vector<Req> reqs; };
+  static Selector as_selector(const Pod::LabelSelector& ls) {
+    Selector s;
+    if (!ls.present) { s.nothing = true; return s; }
+    if (ls.matchLabels.empty() && ls.exprs.empty()) { s.everything = true; return s; }
+    for (auto& kv : ls.matchLabels) {
+      Req r = make_requirement(kv.first, "=", {kv.second});
+      if (!r.ok) { s.err = true; return s; }
+      s.reqs.push_back(r);
+    }
+    for (auto& e : ls.exprs) {
+      if (e.op != "In" && e.op != "NotIn" && e.op != "Exists" && e.op != "DoesNotExist") { s.err = true; return s; }
+      Req r = make_requirement(e.key, e.op, e.values);
+      if (!r.ok) { s.err = true; return s; }
+      s.reqs.push_back(r);
+    }
+    return s;
+  }
+  static bool selector_matches(const Selector& s, const StrMap& labels) {
+    if (s.nothing) return false;
+    if (s.everything) return true;
+    for (auto& r : s.reqs)
+      if (!req_matches(r, labels)) return false;
+    return true;
+  }
+  // priorities/util/topologies.go:28-48 (namespaces default to the term owner's)
+  static bool ns_and_selector_match(const Pod* owner, const Pod::AffinityTerm& term, const Selector& sel,
+                                    const Pod* target) {
+    bool in = false;
+    if (term.namespaces.empty()) in = target->ns == owner->ns;
+    else
+      for (auto& n : term.namespaces)
+        if (n == target->ns) { in = true; break; }
+    return in && selector_matches(sel, target->labels);
+  }
+  // topologies.go:52-71
+  static bool same_topology(const Node* a, const Node* b, const std::string& key) {
+    if (key.empty()) return false;
+    const std::string* va = map_get(a->labels, key);
+    const std::string* vb = map_get(b->labels, key);
+    return va && vb && *va == *vb;
+  }
+  // podMatchesPodAffinityTerms (vendor predicates.go:1189-1214): {match, selector match, error}.
+  // getAffinityTermProperties builds every term's selector before any match,
+  // so a selector error in any term is returned first.
+  struct TermsMatch { bool match = false, sel = false, err = false; };
+  TermsMatch pod_matches_terms(const Pod* pod, TaskInfo* target, NodeInfo* node,
+                               const std::vector<Pod::AffinityTerm>& terms) {
+    TermsMatch r;
+    std::vector<Selector> sels;
+    for (auto& t : terms) {
+      sels.push_back(as_selector(t.selector));
+      if (sels.back().err) { r.err = true; return r; }
+    }
+    for (size_t i = 0; i < terms.size(); ++i)  // podMatchesAllAffinityTermProperties
+      if (!ns_and_selector_match(pod, terms[i], sels[i], target->pod)) return r;
+    auto it = ssn->nodeIndex.find(target->nodeName);  // c.info.GetNodeInfo
+    if (it == ssn->nodeIndex.end() || !it->second->node) { r.err = true; return r; }
+    for (auto& t : terms) {
+      if (t.topologyKey.empty()) { r.err = true; return r; }
+      if (!same_topology(node->node, it->second->node, t.topologyKey)) { r.sel = true; return r; }
+    }
+    r.match = r.sel = true;
+    return r;
+  }
+  // targetPodMatchesAffinityOfPod(pod, pod) (vendor predicates/metadata.go)
+  static bool pod_matches_own_affinity(const Pod* pod) {
+    if (pod->aff_terms.empty()) return false;
+    std::vector<Selector> sels;
+    for (auto& t : pod->aff_terms) {
+      sels.push_back(as_selector(t.selector));
+      if (sels.back().err) return false;
+    }
+    for (size_t i = 0; i < pod->aff_terms.size(); ++i)
+      if (!ns_and_selector_match(pod, pod->aff_terms[i], sels[i], pod)) return false;
+    return true;
+  }
+  bool inter_pod_affinity_ok(TaskInfo* task, NodeInfo* node) {
+    const Pod* pod = task->pod;
+    std::vector<TaskInfo*> pods = filtered_pods(node);
+    // satisfiesExistingPodsAntiAffinity (:1293-1332) via
+    // getMatchingAntiAffinityTopologyPairsOfPods (:1270-1289)
+    std::set<std::pair<std::string, std::string>> pairs;
+    for (TaskInfo* e : pods) {
+      auto it = ssn->nodeIndex.find(e->nodeName);
+      if (it == ssn->nodeIndex.end() || !it->second->node) return false;  // GetNodeInfo error (not IsNotFound)
+      const Node* enode = it->second->node;
+      for (auto& term : e->pod->anti_terms) {  // :1247-1268
+        Selector sel = as_selector(term.selector);
+        if (sel.err) return false;
+        if (!ns_and_selector_match(e->pod, term, sel, pod)) continue;
+        if (const std::string* v = map_get(enode->labels, term.topologyKey)) pairs.insert({term.topologyKey, *v});
+      }
+    }
+    for (auto& kv : node->node->labels)
+      if (pairs.count({kv.first, kv.second})) return false;
+    if (pod->aff_terms.empty() && pod->anti_terms.empty()) return true;
+    // satisfiesPodsAffinityAntiAffinity, slow path (:1402-1457)
+    bool matchFound = false, termsSelectorMatchFound = false;
+    for (TaskInfo* e : pods) {
+      if (!matchFound && !pod->aff_terms.empty()) {
+        TermsMatch m = pod_matches_terms(pod, e, node, pod->aff_terms);
+        if (m.err) return false;
+        if (m.sel) termsSelectorMatchFound = true;
+        if (m.match) matchFound = true;
+      }
+      if (!pod->anti_terms.empty()) {
+        TermsMatch m = pod_matches_terms(pod, e, node, pod->anti_terms);
+        if (m.err || m.match) return false;
+      }
+    }
+    if (!matchFound && !pod->aff_terms.empty()) {
+      if (termsSelectorMatchFound) return false;
+      if (!pod_matches_own_affinity(pod)) return false;
+    }
     return true;
   }
   bool static_ok(TaskInfo* task, NodeInfo* node, size_t node_pos) {
@@ -1311,14 +1470,14 @@ struct Predicates {
   void open(Session* s, bool active) {
     ssn = s;
     for (size_t i = 0; i < s->nodes.size(); i++) pos[s->nodes[i]] = i;
-    // Preconditions of the proven-true InterPodAffinity path and A8,
-    // checked only when the predicate will actually be evaluated.
+    // Without any pod (anti)affinity term in the session the inter-pod
+    // predicate reduces to the GetNodeInfo errors of allocated pods whose node
+    // is outside the session (SURVEY A10 "ghost" pods); otherwise it runs in full.
     if (active)
     for (JobInfo* job : s->jobs)
       for (auto& kv : job->tasks.items) {
         TaskInfo* t = kv.second;
-        if (t->pod->has_pod_affinity || t->pod->has_pod_anti_affinity)
-          throw Unsupported("pod (anti)affinity present: inter-pod affinity predicate not restated");
+        if (!t->pod->aff_terms.empty() || !t->pod->anti_terms.empty()) s->pod_affinity_terms = true;
         if (AllocatedStatus(t->status) && !s->nodeIndex.count(t->nodeName)) ghost = true;
         if (t->status == Pending && t->pod->has_host_port) s->pending_host_ports = true;
       }
@@ -1328,7 +1487,7 @@ struct Predicates {
       if (node->allocatable.MaxTaskNum <= (int)node->tasks.size()) return false;  // :125-127
       if (!static_ok(task, node, pos[node])) return false;                       // :130-141,158-183
       if (!fits_host_ports(task, node)) return false;                            // :144-155
-      if (faithful_scan) return affinity_ok_faithful(node);                       // :186-198
+      if (faithful_scan || ssn->pod_affinity_terms) return inter_pod_affinity_ok(task, node);  // :186-198
       return !ghost;
     };
   }
@@ -1807,7 +1966,7 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache) {
   for (auto& a : actions) {
     if (a == "allocate") { ssn->action = ""; allocate_execute(ssn); }
     else if (a == "backfill") { ssn->action = "backfill"; backfill_execute(ssn); }
-    else if ((a == "reclaim" || a == "preempt") && ssn->pending_host_ports)
+    else if ((a == "reclaim" || a == "preempt") && (ssn->pending_host_ports || ssn->pod_affinity_terms))
       throw Unsupported("reclaim/preempt with pending host ports: not on the device path");
     else if (a == "reclaim") { ssn->action = "reclaim"; reclaim_execute(ssn); }
     else if (a == "preempt") { ssn->action = "preempt"; preempt_execute(ssn); }

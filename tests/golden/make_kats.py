@@ -310,6 +310,94 @@ KATS = {
         "expected": {"decisions": [], "evictions": [],
                      "nodes": {"n1": [[0, 8 * GI, 0], [2000, 0, 0], 4]}},
     },
+    # Inter-pod anti-affinity of an existing pod (vendor predicates.go:1244-1332,
+    # kube-batch predicates.go:185-198 with meta == nil). Running e (ns, app=db,
+    # job pg0 of the session, so the podLister sees it, predicates.go:45-65)
+    # forbids (zone, a) to pods its term selects: app=web in e's own namespace
+    # (GetNamespacesFromPodAffinityTerm, topologies.go:28-37). w1 skips n1, n2
+    # (zone a) for n3; w2 (app=other) and w3 (namespace other) are not selected.
+    "kat_pod_anti_affinity_existing": {
+        "tiers": [[{"name": "predicates"}]],
+        "nodes": [node("n1", "4", labels={"zone": "a"}), node("n2", "4", labels={"zone": "a"}),
+                  node("n3", "4", labels={"zone": "b"})],
+        "pods": [pod("e", "e", {"cpu": "1"}, group="pg0", phase="Running", node="n1", labels={"app": "db"},
+                     affinity={"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                         {"labelSelector": {"matchLabels": {"app": "web"}}, "topologyKey": "zone"}]}}),
+                 pod("w1", "w1", {"cpu": "1"}, labels={"app": "web"}),
+                 pod("w2", "w2", {"cpu": "1"}, labels={"app": "other"}),
+                 pod("w3", "w3", {"cpu": "1"}, ns="other", group="pg2", labels={"app": "web"})],
+        "podGroups": [pg("pg0"), pg(), pg("pg2", ns="other", created=100)], "queues": Q,
+        "expected": {"decisions": [["w1", "n3", "allocate"], ["w2", "n1", "allocate"], ["w3", "n1", "allocate"]],
+                     "binds": {"ns/w1": "n3", "ns/w2": "n1", "other/w3": "n1"}},
+    },
+    # The pod's own affinity (vendor predicates.go:1402-1456). a1: no allocated
+    # pod matches the term's selector and a1 matches its own term, so it may go
+    # anywhere (the "first pod of a series" rule) -> n1, which it fills. a2: a1
+    # now matches, so the node must share a1's zone: n2 (zone b) fails, n3
+    # (zone a) takes it. c1's term selects nothing and c1 does not match it
+    # itself (targetPodMatchesAffinityOfPod): it fits nowhere.
+    "kat_pod_affinity_first_pod": {
+        "tiers": [[{"name": "predicates"}]],
+        "nodes": [node("n1", "1", labels={"zone": "a"}), node("n2", "4", labels={"zone": "b"}),
+                  node("n3", "4", labels={"zone": "a"})],
+        "pods": [pod(u, u, {"cpu": "1"}, labels={"app": "cache"},
+                     affinity={"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                         {"labelSelector": {"matchLabels": {"app": "cache"}}, "topologyKey": "zone"}]}})
+                 for u in ("a1", "a2")]
+                + [pod("c1", "c1", {"cpu": "1"}, group="pg2", labels={"app": "other"},
+                       affinity={"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                           {"labelSelector": {"matchLabels": {"app": "nothing"}}, "topologyKey": "zone"}]}})],
+        "podGroups": [pg(), pg("pg2", created=100)], "queues": Q,
+        "expected": {"decisions": [["a1", "n1", "allocate"], ["a2", "n3", "allocate"]],
+                     "binds": {"ns/a1": "n1", "ns/a2": "n3"}},
+    },
+    # Own anti-affinity on a per-node topology key: one app=spread pod per
+    # node. s2 sees s1 on n1 (both as s1's existing anti term, :1244-1332, and
+    # as its own, :1428-1436); s3 finds both nodes taken.
+    "kat_pod_anti_affinity_spread": {
+        "tiers": [[{"name": "predicates"}]],
+        "nodes": [node("n1", "4", labels={"host": "n1"}), node("n2", "4", labels={"host": "n2"})],
+        "pods": [pod(u, u, {"cpu": "1"}, labels={"app": "spread"},
+                     affinity={"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                         {"labelSelector": {"matchLabels": {"app": "spread"}}, "topologyKey": "host"}]}})
+                 for u in ("s1", "s2", "s3")],
+        "podGroups": [pg()], "queues": Q,
+        "expected": {"decisions": [["s1", "n1", "allocate"], ["s2", "n2", "allocate"]],
+                     "binds": {"ns/s1": "n1", "ns/s2": "n2"}},
+    },
+    # Errors fail the predicate. x1's anti term has an invalid operator
+    # (LabelSelectorAsSelector, helpers.go:46-59): with any allocated pod in
+    # the podLister the error is reached (:1428-1435). y1's affinity term has an
+    # empty topologyKey: the running e matches its selector, so
+    # podMatchesPodAffinityTerms returns the error (:1205-1208). z1 is plain.
+    "kat_pod_affinity_errors": {
+        "tiers": [[{"name": "predicates"}]],
+        "nodes": [node("n1", "4", labels={"zone": "a"})],
+        "pods": [pod("e", "e", {"cpu": "1"}, group="pg0", phase="Running", node="n1", labels={"app": "db"}),
+                 pod("x1", "x1", {"cpu": "1"}, affinity={"podAntiAffinity": {
+                     "requiredDuringSchedulingIgnoredDuringExecution": [
+                         {"labelSelector": {"matchExpressions": [{"key": "app", "operator": "Foo", "values": ["a"]}]},
+                          "topologyKey": "zone"}]}}),
+                 pod("y1", "y1", {"cpu": "1"}, affinity={"podAffinity": {
+                     "requiredDuringSchedulingIgnoredDuringExecution": [
+                         {"labelSelector": {"matchLabels": {"app": "db"}}, "topologyKey": ""}]}}),
+                 pod("z1", "z1", {"cpu": "1"})],
+        "podGroups": [pg("pg0"), pg()], "queues": Q,
+        "expected": {"decisions": [["z1", "n1", "allocate"]], "binds": {"ns/z1": "n1"}},
+    },
+    # An allocated pod whose anti term fails to build its selector makes
+    # getMatchingAntiAffinityTopologyPairsOfPods return the error for every
+    # incoming pod on every node (:1270-1289, :1310-1314): nothing is placed.
+    "kat_pod_anti_affinity_poison": {
+        "tiers": [[{"name": "predicates"}]],
+        "nodes": [node("n1", "4", labels={"zone": "a"}), node("n2", "4", labels={"zone": "b"})],
+        "pods": [pod("e", "e", {"cpu": "1"}, group="pg0", phase="Running", node="n1",
+                     affinity={"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                         {"labelSelector": {"matchLabels": {"bad key!": "x"}}, "topologyKey": "zone"}]}}),
+                 pod("p1", "p1", {"cpu": "1"})],
+        "podGroups": [pg("pg0"), pg()], "queues": Q,
+        "expected": {"decisions": [], "binds": {}},
+    },
 }
 
 
