@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KBG_ABI_VERSION 5
+#define KBG_ABI_VERSION 6
 
 typedef enum kbg_status {
   KBG_OK = 0,
@@ -147,9 +147,25 @@ typedef struct kbg_spec {
   int32_t term_off, term_len;         /* its NodeSelectorTerms */
   int32_t toleration_off, toleration_len;
   int32_t has_host_ports;             /* some container port has hostPort > 0 */
-  int32_t has_pod_affinity;           /* Affinity.PodAffinity or PodAntiAffinity set */
+  int32_t has_pod_affinity;           /* some required pod (anti)affinity term */
   int32_t port_off, port_len;         /* GetContainerPorts(pod): ports[port_off ..] */
+  /* inter-pod (anti)affinity (vendor predicates.go:1155-1466): the pod's
+     namespace and labels (what other pods' terms select) and its own
+     RequiredDuringSchedulingIgnoredDuringExecution terms */
+  int32_t ns;                         /* string id of the pod namespace */
+  int32_t pod_label_off, pod_label_len; /* pod labels, pairs at pod_labels[2*i] */
+  int32_t aff_off, aff_len;           /* PodAffinity terms: pod_terms[aff_off ..] */
+  int32_t anti_off, anti_len;         /* PodAntiAffinity terms */
 } kbg_spec;
+
+/* v1.PodAffinityTerm */
+typedef struct kbg_pod_term {
+  int32_t has_selector;               /* LabelSelector != nil (nil selects nothing) */
+  int32_t match_off, match_len;       /* MatchLabels pairs at selectors[2*i] */
+  int32_t expr_off, expr_len;         /* MatchExpressions: reqs[expr_off ..] */
+  int32_t ns_off, ns_len;             /* Namespaces: values[ns_off ..] string ids (empty: the pod's own) */
+  int32_t topology_key;               /* string id */
+} kbg_pod_term;
 
 typedef struct kbg_term {
   int32_t expr_off, expr_len;   /* MatchExpressions: reqs[expr_off ..] */
@@ -191,6 +207,8 @@ typedef struct kbg_snapshot {
   const int32_t* tier_sizes;       int32_t n_tiers;     /* plugins grouped by tier, in order */
   const kbg_host_port* ports;      int32_t n_ports;
   const int32_t* node_tasks;       int32_t n_node_tasks;
+  const kbg_pod_term* pod_terms;   int32_t n_pod_terms;
+  const int32_t* pod_labels;       int32_t n_pod_labels;  /* 2*n_pod_labels ints */
 } kbg_snapshot;
 
 typedef struct kbg_options {

@@ -679,14 +679,17 @@ struct Resolver {
     for (int32_t& k = cursor[g]; k < n; ++k) {
       const int32_t nd = (int32_t)(c[k] & ~kbg::kCandPipelineBit);
       if (S.panic_node[nd]) return RES_PANIC;
-      if (mark[nd] != stamp) {
+      if (mark[nd] != stamp && (!S.has_aff || S.mmark[nd] != S.mstamp)) {
         *node = nd;
         *kind = (c[k] & kbg::kCandPipelineBit) ? KBG_KIND_PIPELINE : KBG_KIND_ALLOCATE;
         return RES_OK;
       }
-      // touched by an earlier commit of this batch: re-check on the host mirror
+      // touched by an earlier commit of this batch (resources, or a class-mask
+      // bit it lost): re-check on the host mirror
       if (S.pred_active && S.ntasks[nd] >= S.maxtasks[nd]) continue;
-      if (S.has_ports && !((S.h_class_mask[(size_t)S.task_class[t] * S.W + (nd >> 6)] >> (nd & 63)) & 1ull)) continue;
+      if ((S.has_ports || S.has_aff) &&
+          !((S.h_class_mask[(size_t)S.task_class[t] * S.W + (nd >> 6)] >> (nd & 63)) & 1ull))
+        continue;
       if (S.be_task[t]) {  // backfill: PredicateFn only, always ssn.Allocate
         *node = nd;
         *kind = KBG_KIND_ALLOCATE;
@@ -746,6 +749,8 @@ void mirror_add(Session& S, int32_t t, int32_t nd, int32_t kind) {
   }
   S.ntasks[nd]++;
   if (S.has_ports) add_ports(S, S.task_class[t], nd);
+  // an Allocated pod joins the podLister (api/helpers.go:63-70); Pipelined does not
+  if (S.has_aff && kind == KBG_KIND_ALLOCATE) kbg::aff_place(S, t, nd, +1, S.affm->st, true);
 }
 
 // Builds the port-atom dictionary (distinct sanitized (ip, protocol, port)
@@ -860,11 +865,23 @@ kbg_status validate(const kbg_snapshot* s) {
       return fail(KBG_E_INVALID, "task " + std::to_string(i));
     if (t.status <= 0 || t.status > KBG_UNKNOWN || (t.status & (t.status - 1))) return fail(KBG_E_INVALID, "task status");
   }
+  if (s->n_pod_terms < 0 || (s->n_pod_terms > 0 && !s->pod_terms)) return fail(KBG_E_INVALID, "pod_terms");
+  if (s->n_pod_labels < 0 || (s->n_pod_labels > 0 && !s->pod_labels)) return fail(KBG_E_INVALID, "pod_labels");
   for (int32_t i = 0; i < s->n_specs; ++i) {
     const kbg_spec& p = s->specs[i];
     if (!range(p.selector_off, p.selector_len, s->n_selectors) || !range(p.term_off, p.term_len, s->n_terms) ||
-        !range(p.toleration_off, p.toleration_len, s->n_tolerations) || !range(p.port_off, p.port_len, s->n_ports))
+        !range(p.toleration_off, p.toleration_len, s->n_tolerations) || !range(p.port_off, p.port_len, s->n_ports) ||
+        !in(p.ns, NS) || !range(p.pod_label_off, p.pod_label_len, s->n_pod_labels) ||
+        !range(p.aff_off, p.aff_len, s->n_pod_terms) || !range(p.anti_off, p.anti_len, s->n_pod_terms))
       return fail(KBG_E_INVALID, "spec " + std::to_string(i));
+  }
+  for (int32_t i = 0; i < s->n_pod_labels * 2; ++i)
+    if (!in(s->pod_labels[i], NS)) return fail(KBG_E_INVALID, "pod label string");
+  for (int32_t i = 0; i < s->n_pod_terms; ++i) {
+    const kbg_pod_term& t = s->pod_terms[i];
+    if (!range(t.match_off, t.match_len, s->n_selectors) || !range(t.expr_off, t.expr_len, s->n_reqs) ||
+        !range(t.ns_off, t.ns_len, s->n_values) || !in(t.topology_key, NS))
+      return fail(KBG_E_INVALID, "pod term " + std::to_string(i));
   }
   for (int32_t i = 0; i < s->n_terms; ++i) {
     const kbg_term& t = s->terms[i];
@@ -954,6 +971,8 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.tols_in = copy_arr(snap->tolerations, snap->n_tolerations);
   S.taints_in = copy_arr(snap->taints, snap->n_taints);
   S.ports_in = copy_arr(snap->ports, snap->n_ports);
+  S.pod_terms_in = copy_arr(snap->pod_terms, snap->n_pod_terms);
+  S.pod_labels_in = copy_arr(snap->pod_labels, 2 * snap->n_pod_labels);
 
   // ---- plugins (framework.go:26-46; unknown names ignored)
   {
@@ -1184,8 +1203,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     for (int32_t t = 0; t < S.n_tasks; ++t) {
       const kbg_task& tk = S.tasks_in[t];
       const kbg_spec* sp = tk.spec >= 0 ? &S.specs_in[tk.spec] : nullptr;
-      if (sp && sp->has_pod_affinity)
-        return fail(KBG_E_UNSUPPORTED, "inter-pod (anti)affinity present: run the reference predicate path");
+      if (sp && (sp->aff_len > 0 || sp->anti_len > 0)) S.has_aff = true;  // kbg_affinity.cpp
       if (allocated_status(tk.status) && !names.count(S.canon[tk.node_name])) S.ghost = true;
     }
   }
@@ -1340,7 +1358,8 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   // host ports: the port fit is folded into the class masks (setup_host_ports)
   S.h_class_mask_static = S.h_class_mask;
   setup_host_ports(S);
-  if (S.has_ports) {
+  setup_affinity(S);  // inter-pod (anti)affinity: folded in the same way (kbg_affinity.cpp)
+  if (S.has_ports || S.has_aff) {
     HIP_TRY(hipMemcpy(S.d_class_mask, S.h_class_mask.data(), S.h_class_mask.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipHostMalloc((void**)&S.h_mdeltas, (size_t)kbg::kMaskDeltaCap * sizeof(kbg::MaskDelta), hipHostMallocDefault));
     if ((st = dalloc(S, &S.d_mdeltas, kbg::kMaskDeltaCap))) return st;
@@ -1408,6 +1427,8 @@ void compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, const 
   std::vector<int32_t> ntasks = S.ntasks;
   std::vector<uint64_t> ports = S.node_ports;  // host ports: [N][PW]
   const int32_t PW = S.PW;
+  kbg::AffState aff;  // pod affinity counts, rewound with the decisions
+  if (S.has_aff) aff = S.affm->st;
   int32_t k = (int32_t)dec.size();
   for (int32_t j : jobs) {
     Session::FitCounts& fc = S.fit[j];
@@ -1422,6 +1443,7 @@ void compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, const 
       if (S.has_ports)
         std::copy(dec_oldp.begin() + (size_t)k * PW, dec_oldp.begin() + (size_t)(k + 1) * PW,
                   ports.begin() + (size_t)n * PW);
+      if (S.has_aff && dec[k].kind == KBG_KIND_ALLOCATE) kbg::aff_place(S, dec[k].task, n, -1, aff, false);
     }
     const int32_t t = le.task;
     const Res& r = S.treq[t];
@@ -1438,6 +1460,7 @@ void compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, const 
         for (int32_t w = 0; w < PW && !clash; ++w) clash = (ports[(size_t)n * PW + w] & conf[w]) != 0;
         if (clash) continue;
       }
+      if (S.has_aff && !S.panic_node[n] && !kbg::aff_ok(S, aff, S.task_class[t], n)) continue;  // pod affinity
       if (n != le.node && kbg::res_le(r, idle[n])) continue;           // would have been chosen
       Res d = idle[n];                                                 // Resource.FitDelta
       if (r.c > 0) d.c -= r.c + kbg::kMinMilliCPU;
@@ -1491,6 +1514,11 @@ void begin_cycle(Session& S) {
   S.pend = S.pend_all;
   S.pend_off = S.pend_off_all;
   S.pend_len = S.pend_len_all;
+  if (S.has_aff) {
+    S.affm->st = S.affm->st0;
+    std::fill(S.aff_gain_flag.begin(), S.aff_gain_flag.end(), 0);
+    S.aff_gain_classes.clear();
+  }
   S.cycle_started = true;
 }
 
@@ -1708,6 +1736,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     // commit in order
     tp = clk::now();
     rs.stamp = ++stamp;
+    S.mstamp = stamp;
     rs.reset(G);
     touched.clear();
     bactual.assign(bt.size(), 0);
@@ -1740,6 +1769,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         tp = clk::now();
         seg = i;
         rs.stamp = ++stamp;  // the device table now holds every commit so far
+        S.mstamp = stamp;
         rs.reset(G);
         touched.clear();
         r = rs.resolve(grouper.row_of[0], t, &node, &kind);  // a fresh list always decides its first task
@@ -1767,6 +1797,20 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         failed[S.task_shape[t]].store(1, std::memory_order_relaxed);
       }
       if (ok != (bool)b->bpred[i]) {
+        cut = i + 1;
+        S.stats.mispredictions++;
+        break;
+      }
+      if (!S.aff_gain_classes.empty()) {
+        // pod affinity: a class gained nodes (kbg_affinity.cpp). The rest of
+        // the batch was scanned against the old masks and shapes of the class
+        // marked failed may fit again: cut here, the predictor replays to this
+        // point and the next batch is scanned against the new masks.
+        for (int32_t c : S.aff_gain_classes) {
+          S.aff_gain_flag[c] = 0;
+          for (int32_t sh : S.affm->class_shapes[c]) failed[sh].store(0, std::memory_order_relaxed);
+        }
+        S.aff_gain_classes.clear();
         cut = i + 1;
         S.stats.mispredictions++;
         break;
@@ -1842,6 +1886,7 @@ kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     int32_t G = grouper.build(bt, cnt);
     if ((st = device_scan(S, G)) != KBG_OK) return st;
     rs.stamp = ++stamp;
+    S.mstamp = stamp;
     rs.reset(G);
     touched.clear();
     int32_t seg = 0;
@@ -1856,6 +1901,7 @@ kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         if ((st = device_scan(S, G)) != KBG_OK) return st;
         seg = i;
         rs.stamp = ++stamp;
+        S.mstamp = stamp;
         rs.reset(G);
         touched.clear();
         r = rs.resolve(grouper.row_of[0], t, &node, &kind);
@@ -1891,6 +1937,19 @@ kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       }
       E.jready[j]++;
       record_decision(S, t, node, KBG_KIND_ALLOCATE);
+      if (!S.aff_gain_classes.empty() && i + 1 < cnt) {
+        // pod affinity gave a class new nodes: rescan the rest of the batch
+        for (int32_t c : S.aff_gain_classes) S.aff_gain_flag[c] = 0;
+        S.aff_gain_classes.clear();
+        if ((st = push_deltas(S, touched)) != KBG_OK) return st;
+        G = grouper.build(bt + i + 1, cnt - i - 1);
+        if ((st = device_scan(S, G)) != KBG_OK) return st;
+        seg = i + 1;
+        rs.stamp = ++stamp;
+        S.mstamp = stamp;
+        rs.reset(G);
+        touched.clear();
+      }
     }
     if ((st = push_deltas(S, touched)) != KBG_OK) return st;
     done += cnt;
@@ -2425,6 +2484,7 @@ std::vector<std::vector<int32_t>> pending_by_job(const Session& S) {
 
 kbg_status victim_action_check(Session& S) {
   if (S.has_ports) return fail(KBG_E_UNSUPPORTED, "preempt/reclaim with host ports: run the reference path");
+  if (S.has_aff) return fail(KBG_E_UNSUPPORTED, "preempt/reclaim with pod (anti)affinity: run the reference path");
   if (S.max_candidates > kbg::kMaxNodeCandidates)
     return fail(KBG_E_UNSUPPORTED, "a node holds more than 128 running session tasks");
   return KBG_OK;
@@ -2759,7 +2819,7 @@ kbg_status kbg_session_reset(kbg_session* s) {
   S.rel = S.rel0;
   S.ntasks = S.ntasks0;
   S.allocated = S.backfilled = S.reclaimed = S.preempted = S.cycle_started = false;
-  if (S.has_ports) {  // the class masks carry the port fit: back to the snapshot's
+  if (S.has_ports || S.has_aff) {  // the class masks carry the port fit / affinity: back to the snapshot's
     S.node_ports = S.node_ports0;
     S.h_class_mask = S.h_class_mask0;
     S.mask_dirty.clear();
@@ -2781,6 +2841,7 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
   for (int32_t i = 0; i < n; ++i)
     if (tasks[i] < 0 || tasks[i] >= S.n_tasks || !S.pending_candidate[tasks[i]])
       return fail(KBG_E_INVALID, "task index (must be a Pending, non-BestEffort session task)");
+  if (S.has_aff) return fail(KBG_E_UNSUPPORTED, "kbg_select with pod (anti)affinity: use kbg_allocate");
   std::vector<int32_t> mark(S.n_nodes, -1), touched, bt;
   Grouper grouper(S);
   Resolver rs{S, mark, 0, {}};

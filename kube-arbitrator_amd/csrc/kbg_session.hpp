@@ -2,7 +2,9 @@
 #pragma once
 #include <stdint.h>
 
+#include <memory>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/kbgpu.h"
@@ -80,6 +82,49 @@ struct Engine {
   std::vector<double> qshare;   // proportion attr.share
   std::vector<int32_t> qorder;  // queues sorted by QueueOrderFn
   std::vector<int32_t> qrank;   // position of each queue in qorder; qrank[n_queues] = INT32_MAX (sentinel id)
+};
+
+// ---- inter-pod (anti)affinity (kbg_affinity.cpp)
+struct AffSelReq { int32_t key; int32_t op; std::vector<int32_t> vals; };  // op: 0 In/=, 1 NotIn, 2 Exists, 3 DoesNotExist
+struct AffSel { bool err = false, nothing = false, everything = false; std::vector<AffSelReq> reqs; };
+struct AffTerm {
+  AffSel sel;
+  std::vector<int32_t> ns;  // canonical ids; empty = the owner's namespace
+  int32_t key = -1;         // canonical id of the topology key
+  bool key_empty = false;
+};
+struct AffSpec {
+  int32_t ns = -1;
+  std::vector<std::pair<int32_t, int32_t>> labels;  // sorted by key (labels.Set)
+  std::vector<AffTerm> aff, anti;
+  bool aff_err = false, anti_err = false;  // a term's selector fails to build
+};
+struct AffClass {  // per static class
+  bool hasB = false, b_err = false, b_empty_key = false, b_self = false;
+  std::vector<int32_t> b_keys, sigB;                // node signature over the affinity terms' keys (-1: a key missing)
+  std::vector<std::vector<int32_t>> b_nodes;        // nodes of each signature
+  bool hasC = false, c_err = false;
+  std::vector<int32_t> c_keys, sigC;                // over the anti terms' keys before the first empty one
+  std::vector<std::vector<int32_t>> c_nodes;
+};
+struct AffState {  // counts over the AllocatedStatus pods
+  int32_t poison = 0;     // pods whose anti term fails to build its selector
+  int32_t allocated = 0;  // all of them (the podLister is not empty)
+  std::vector<int32_t> nB;
+  std::vector<std::vector<int32_t>> cntB, cntC;
+  std::vector<std::unordered_map<int64_t, int32_t>> cntA;
+};
+struct AffinityModel {
+  std::vector<AffSpec> specs;                                  // per kbg_spec
+  std::vector<AffClass> cls;                                   // per class
+  std::vector<std::vector<std::vector<int32_t>>> anti_match;   // [spec][anti term] -> classes it selects
+  std::vector<std::vector<int32_t>> matchB, matchC;            // [spec] -> classes whose terms select it
+  std::vector<char> spec_poison;
+  std::vector<int32_t> c_err_classes;
+  std::vector<std::vector<std::pair<int32_t, int32_t>>> node_labels;
+  std::unordered_map<int64_t, std::vector<int32_t>> pair_nodes;  // (topology key, value) -> nodes
+  std::vector<std::vector<int32_t>> class_shapes;
+  AffState st0, st;  // at open / now
 };
 
 // What a node's stop status depends on besides the session state: the
@@ -216,6 +261,15 @@ struct Session {
   std::vector<uint8_t> mask_dirty_flag;
   MaskDelta* h_mdeltas = nullptr;              // pinned staging
   MaskDelta* d_mdeltas = nullptr;
+  // ---- inter-pod (anti)affinity folded into the class masks (kbg_affinity.cpp)
+  bool has_aff = false;                        // some task carries a required pod (anti)affinity term
+  std::shared_ptr<AffinityModel> affm;
+  std::vector<kbg_pod_term> pod_terms_in;
+  std::vector<int32_t> pod_labels_in;
+  std::vector<int32_t> mmark;                  // per node: batch stamp of the last class-mask bit it lost
+  int32_t mstamp = 0;                          // the current batch stamp
+  std::vector<uint8_t> aff_gain_flag;          // per class: gained nodes since the last cut
+  std::vector<int32_t> aff_gain_classes;
 
   // ---- device
   int32_t device = 0;
@@ -251,7 +305,13 @@ struct Session {
 };
 
 bool parse_go_int64(const std::string& s, int64_t* out);
+bool label_key_valid(const std::string& k);    // IsQualifiedName (validation.go:42-70)
+bool label_value_valid(const std::string& v);  // IsValidLabelValue (validation.go:97-106)
 void compile_static_predicates(Session& S, StaticHost* out);
+// kbg_affinity.cpp
+void setup_affinity(Session& S);
+void aff_place(Session& S, int32_t t, int32_t n, int32_t sign, AffState& st, bool update_bits);
+bool aff_ok(const Session& S, const AffState& st, int32_t c, int32_t n);
 
 }  // namespace kbg
 

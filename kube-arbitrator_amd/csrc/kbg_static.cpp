@@ -70,6 +70,9 @@ bool valid_label_value(const std::string& v) { return v.size() <= 63 && (v.empty
 
 }  // namespace
 
+bool label_key_valid(const std::string& k) { return valid_label_key(k); }
+bool label_value_valid(const std::string& v) { return valid_label_value(v); }
+
 // strconv.ParseInt(s, 10, 64)
 bool parse_go_int64(const std::string& s, int64_t* out) {
   if (s.empty()) return false;
@@ -275,6 +278,44 @@ std::string spec_key(const Session& S, const kbg_spec* sp) {
     add(hp.host_ip);
     add(hp.protocol);
     k += std::to_string(hp.host_port);
+  }
+  if (S.has_aff) {  // inter-pod (anti)affinity: what other pods' terms select, and the pod's own terms
+    k += "N";
+    add(sp->ns);
+    std::vector<std::pair<std::string, std::string>> lab;
+    for (int32_t i = 0; i < sp->pod_label_len; ++i)
+      lab.emplace_back(S.strs[S.pod_labels_in[2 * (sp->pod_label_off + i)]],
+                       S.strs[S.pod_labels_in[2 * (sp->pod_label_off + i) + 1]]);
+    std::stable_sort(lab.begin(), lab.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    for (size_t i = 0; i < lab.size(); ++i) {
+      if (i + 1 < lab.size() && lab[i + 1].first == lab[i].first) continue;  // the last value of a key wins
+      k += "l" + std::to_string(lab[i].first.size()) + ":" + lab[i].first + std::to_string(lab[i].second.size()) +
+           ":" + lab[i].second;
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+      const int32_t off = pass ? sp->anti_off : sp->aff_off, len = pass ? sp->anti_len : sp->aff_len;
+      k += pass ? "X" : "Y";
+      for (int32_t i = 0; i < len; ++i) {
+        const kbg_pod_term& t = S.pod_terms_in[off + i];
+        k += "q" + std::to_string(t.has_selector);
+        for (int32_t m = 0; m < t.match_len; ++m) {
+          add(S.selectors_in[2 * (t.match_off + m)]);
+          add(S.selectors_in[2 * (t.match_off + m) + 1]);
+        }
+        k += "e";
+        for (int32_t m = 0; m < t.expr_len; ++m) {
+          const kbg_requirement& r = S.reqs_in[t.expr_off + m];
+          k += "R";
+          add(r.key);
+          add(r.op);
+          for (int32_t v = 0; v < r.value_len; ++v) add(S.values_in[r.value_off + v]);
+        }
+        k += "n";
+        for (int32_t m = 0; m < t.ns_len; ++m) add(S.values_in[t.ns_off + m]);
+        k += "k";
+        add(t.topology_key);
+      }
+    }
   }
   return k;
 }

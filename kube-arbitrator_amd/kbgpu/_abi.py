@@ -35,7 +35,7 @@ DISABLE_RECLAIMABLE = 1 << 4
 DISABLE_QUEUE_ORDER = 1 << 5
 DISABLE_PREDICATE = 1 << 6
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 COMM_ID_BYTES = 128
 
 KIND_ALLOCATE = 0
@@ -82,7 +82,14 @@ class kbg_task(ctypes.Structure):
 class kbg_spec(ctypes.Structure):
     _fields_ = [("selector_off", i32), ("selector_len", i32), ("has_required_affinity", i32), ("term_off", i32),
                 ("term_len", i32), ("toleration_off", i32), ("toleration_len", i32), ("has_host_ports", i32),
-                ("has_pod_affinity", i32), ("port_off", i32), ("port_len", i32)]
+                ("has_pod_affinity", i32), ("port_off", i32), ("port_len", i32), ("ns", i32),
+                ("pod_label_off", i32), ("pod_label_len", i32), ("aff_off", i32), ("aff_len", i32),
+                ("anti_off", i32), ("anti_len", i32)]
+
+
+class kbg_pod_term(ctypes.Structure):
+    _fields_ = [("has_selector", i32), ("match_off", i32), ("match_len", i32), ("expr_off", i32), ("expr_len", i32),
+                ("ns_off", i32), ("ns_len", i32), ("topology_key", i32)]
 
 
 class kbg_term(ctypes.Structure):
@@ -121,6 +128,8 @@ class kbg_snapshot(ctypes.Structure):
         ("tier_sizes", P(i32)), ("n_tiers", i32),
         ("ports", P(kbg_host_port)), ("n_ports", i32),
         ("node_tasks", P(i32)), ("n_node_tasks", i32),
+        ("pod_terms", P(kbg_pod_term)), ("n_pod_terms", i32),
+        ("pod_labels", P(i32)), ("n_pod_labels", i32),
     ]
 
 

@@ -34,10 +34,20 @@ def container_ports(pod):
             for c in pod.get("containers", []) for pt in (c.get("ports") or [])]
 
 
-def _spec_key(pod):
+def pod_terms(pod, kind):
+    """RequiredDuringSchedulingIgnoredDuringExecution terms of the pod's
+    podAffinity / podAntiAffinity (vendor predicates.go:1216-1242)."""
+    aff = pod.get("affinity") or {}
+    pa = aff.get(kind) if isinstance(aff, dict) else None
+    return list((pa or {}).get("requiredDuringSchedulingIgnoredDuringExecution") or []) if isinstance(pa, dict) else []
+
+
+def _spec_key(pod, with_identity):
     aff = pod.get("affinity") or None
-    return json.dumps([pod.get("nodeSelector") or {}, aff, pod.get("tolerations") or [], container_ports(pod)],
-                      sort_keys=True)
+    key = [pod.get("nodeSelector") or {}, aff, pod.get("tolerations") or [], container_ports(pod)]
+    if with_identity:  # other pods' affinity terms select by namespace and labels
+        key += [pod.get("namespace") or "", pod.get("labels") or {}]
+    return json.dumps(key, sort_keys=True)
 
 
 class FlatSnapshot:
@@ -90,15 +100,43 @@ class FlatSnapshot:
         task_rows, self.task_objs = [], []
         spec_ids = {}
         specs, terms, reqs, values, tols, selectors = [], [], [], [], [], []
+        pterms, plabels = [], []
+        any_terms = any(pod_terms(t.pod, "podAffinity") or pod_terms(t.pod, "podAntiAffinity")
+                        for job in jobs for t in job.tasks.values())
+
+        def add_reqs(exprs):
+            off = len(reqs)
+            for e in exprs or []:
+                voff = len(values)
+                values.extend(S(v) for v in (e.get("values") or []))
+                reqs.append((S(e.get("key")), S(e.get("operator")), voff, len(values) - voff))
+            return off, len(reqs) - off
+
+        def add_pod_terms(pod, kind):
+            off = len(pterms)
+            for t in pod_terms(pod, kind):
+                ls = t.get("labelSelector")
+                moff = len(selectors) // 2
+                eoff, elen = len(reqs), 0
+                if isinstance(ls, dict):
+                    for k, v in (ls.get("matchLabels") or {}).items():
+                        selectors.extend((S(k), S(v)))
+                    eoff, elen = add_reqs(ls.get("matchExpressions"))
+                noff = len(values)
+                values.extend(S(n) for n in (t.get("namespaces") or []))
+                pterms.append((1 if isinstance(ls, dict) else 0, moff, len(selectors) // 2 - moff, eoff, elen,
+                               noff, len(values) - noff, S(t.get("topologyKey"))))
+            return off, len(pterms) - off
 
         def spec_of(pod):
-            key = _spec_key(pod)
+            key = _spec_key(pod, any_terms)
             sid = spec_ids.get(key)
             if sid is not None:
                 return sid
             sel_off = len(selectors) // 2
             for k, v in (pod.get("nodeSelector") or {}).items():
                 selectors.extend((S(k), S(v)))
+            sel_len = len(selectors) // 2 - sel_off  # (pod terms append matchLabels pairs to the same array)
             aff = pod.get("affinity") or {}
             na = aff.get("nodeAffinity") if isinstance(aff, dict) else None
             req = na.get("requiredDuringSchedulingIgnoredDuringExecution") if isinstance(na, dict) else None
@@ -107,12 +145,7 @@ class FlatSnapshot:
                 for t in req.get("nodeSelectorTerms") or []:
                     row = []
                     for part in ("matchExpressions", "matchFields"):
-                        off = len(reqs)
-                        for e in t.get(part) or []:
-                            voff = len(values)
-                            values.extend(S(v) for v in (e.get("values") or []))
-                            reqs.append((S(e.get("key")), S(e.get("operator")), voff, len(values) - voff))
-                        row += [off, len(reqs) - off]
+                        row += list(add_reqs(t.get(part)))
                     terms.append(tuple(row))
             tol_off = len(tols)
             for t in pod.get("tolerations") or []:
@@ -122,10 +155,17 @@ class FlatSnapshot:
             port_off = len(ports)
             for ip, proto, port in cports:
                 ports.append((S(ip), S(proto), port))
-            has_pa = isinstance(aff, dict) and (aff.get("podAffinity") is not None or aff.get("podAntiAffinity") is not None)
-            specs.append((sel_off, len(selectors) // 2 - sel_off, 1 if req is not None else 0, term_off,
+            aff_off, aff_len = add_pod_terms(pod, "podAffinity")
+            anti_off, anti_len = add_pod_terms(pod, "podAntiAffinity")
+            lab_off = len(plabels) // 2
+            if any_terms:
+                for k, v in (pod.get("labels") or {}).items():
+                    plabels.extend((S(k), S(v)))
+            specs.append((sel_off, sel_len, 1 if req is not None else 0, term_off,
                           len(terms) - term_off, tol_off, len(tols) - tol_off, 1 if has_ports else 0,
-                          1 if has_pa else 0, port_off, len(ports) - port_off))
+                          1 if aff_len or anti_len else 0, port_off, len(ports) - port_off,
+                          S(pod.get("namespace") or ""), lab_off, len(plabels) // 2 - lab_off,
+                          aff_off, aff_len, anti_off, anti_len))
             sid = len(specs) - 1
             spec_ids[key] = sid
             return sid
@@ -174,7 +214,8 @@ class FlatSnapshot:
             labels=np.asarray(labels or [0, 0], dtype=np.int32), taints=arr(_abi.kbg_taint, taints),
             selectors=np.asarray(selectors or [0, 0], dtype=np.int32),
             plugins=arr(_abi.kbg_plugin_option, plugin_rows), tier_sizes=np.asarray(tier_sizes or [0], dtype=np.int32),
-            ports=arr(_abi.kbg_host_port, ports), node_tasks=np.asarray(node_tasks or [0], dtype=np.int32))
+            ports=arr(_abi.kbg_host_port, ports), node_tasks=np.asarray(node_tasks or [0], dtype=np.int32),
+            pod_terms=arr(_abi.kbg_pod_term, pterms), pod_labels=np.asarray(plabels or [0, 0], dtype=np.int32))
         A = self.arrays
 
         def ptr(a, ctype):
@@ -202,4 +243,6 @@ class FlatSnapshot:
         snap.tier_sizes, snap.n_tiers = ptr(A["tier_sizes"], ctypes.c_int32), len(tier_sizes)
         snap.ports, snap.n_ports = ptr(A["ports"], _abi.kbg_host_port), len(ports)
         snap.node_tasks, snap.n_node_tasks = ptr(A["node_tasks"], ctypes.c_int32), len(node_tasks)
+        snap.pod_terms, snap.n_pod_terms = ptr(A["pod_terms"], _abi.kbg_pod_term), len(pterms)
+        snap.pod_labels, snap.n_pod_labels = ptr(A["pod_labels"], ctypes.c_int32), len(plabels) // 2
         self.snap = snap

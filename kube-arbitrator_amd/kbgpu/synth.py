@@ -389,3 +389,112 @@ def contended_config(**over):
             pods.append(p)
     return {"name": "C5", "tiers": None, "nodes": nodes, "pods": pods, "podGroups": pgs, "queues": queues,
             "actions": ["reclaim", "allocate", "backfill", "preempt"]}
+
+
+def affinity_fixture(seed, max_nodes=16, max_jobs=8, max_tasks=6):
+    """Small sessions exercising inter-pod (anti)affinity (vendor
+    predicates.go:1155-1466): pod labels over a few apps and namespaces,
+    required pod affinity / anti-affinity terms with matchLabels,
+    matchExpressions, nil and empty selectors, explicit namespaces, zone / rack
+    / host topology keys (some nodes lack them), the occasional empty
+    topologyKey or invalid selector, running pods that carry terms, and
+    allocate or allocate + backfill."""
+    rng = random.Random(seed)
+    nn = rng.randint(2, max_nodes)
+    nodes = []
+    for i in range(nn):
+        labels = {"host": f"n{i:02d}"}
+        if rng.random() < 0.9:
+            labels["zone"] = rng.choice(["a", "b", "c"])
+        if rng.random() < 0.7:
+            labels["rack"] = f"r{rng.randrange(4)}"
+        nodes.append({"name": f"n{i:02d}", "labels": labels,
+                      "allocatable": {"cpu": str(rng.choice([2, 4, 8])), "memory": "16Gi",
+                                      "pods": str(rng.choice([3, 110]))}})
+    apps = ["web", "db", "cache"]
+    nss = ["c1", "c2"]
+
+    def selector():
+        r = rng.random()
+        if r < 0.08:
+            return None  # nil: selects nothing
+        if r < 0.14:
+            return {}  # empty: selects everything
+        if r < 0.18:
+            return {"matchExpressions": [{"key": "app", "operator": "Foo", "values": ["web"]}]}  # build error
+        if r < 0.6:
+            return {"matchLabels": {"app": rng.choice(apps)}}
+        op = rng.choice(["In", "NotIn", "Exists", "DoesNotExist"])
+        e = {"key": rng.choice(["app", "tier"]), "operator": op}
+        if op in ("In", "NotIn"):
+            e["values"] = rng.sample(apps, rng.randint(1, 2))
+        return {"matchExpressions": [e]}
+
+    def terms():
+        out = []
+        for _ in range(rng.choice([1, 1, 1, 2])):
+            t = {"topologyKey": rng.choice(["zone", "zone", "rack", "host", "nokey", ""] if rng.random() < 0.15
+                                           else ["zone", "rack", "host"])}
+            sel = selector()
+            if sel is not None:
+                t["labelSelector"] = sel
+            if rng.random() < 0.25:
+                t["namespaces"] = rng.sample(nss, rng.randint(1, 2))
+            out.append(t)
+        return out
+
+    def affinity():
+        r = rng.random()
+        a = {}
+        if r < 0.45:
+            a["podAffinity"] = {"requiredDuringSchedulingIgnoredDuringExecution": terms()}
+        if 0.3 < r < 0.8:
+            a["podAntiAffinity"] = {"requiredDuringSchedulingIgnoredDuringExecution": terms()}
+        return a or None
+
+    pods, pgs = [], []
+    uid = 0
+
+    def mk(ns, name, group, phase="Pending", node="", app=None, aff=None, req=None):
+        nonlocal uid
+        uid += 1
+        p = {"uid": f"u{uid:04d}", "namespace": ns, "name": name, "phase": phase, "nodeName": node,
+             "annotations": {"scheduling.k8s.io/group-name": group},
+             "containers": [{"requests": req or {"cpu": rng.choice(["500m", "1"]), "memory": "1Gi"}}]}
+        labels = {}
+        if app:
+            labels["app"] = app
+        if rng.random() < 0.3:
+            labels["tier"] = rng.choice(["front", "back"])
+        if labels:
+            p["labels"] = labels
+        if aff:
+            p["affinity"] = aff
+        return p
+
+    pgs.append({"namespace": "c1", "name": "pg-run", "minMember": 0, "queue": "q1"})
+    for i in range(rng.randint(0, nn)):
+        node = rng.choice(nodes)["name"]
+        pods.append(mk("c1", f"run{i}", "pg-run", "Running", node, rng.choice(apps + [None]),
+                       affinity() if rng.random() < 0.3 else None, {"cpu": "500m", "memory": "512Mi"}))
+    for j in range(rng.randint(1, max_jobs)):
+        ns = rng.choice(nss)
+        nt = rng.randint(1, max_tasks)
+        pgs.append({"namespace": ns, "name": f"pg{j}", "minMember": rng.randint(0, nt), "queue": "q1",
+                    "creationTimestamp": rng.choice([0, 100, 200]) * 1_000_000_000})
+        app = rng.choice(apps + [None])
+        aff = affinity() if rng.random() < 0.7 else None
+        be = rng.random() < 0.1
+        for t in range(nt):
+            pods.append(mk(ns, f"pg{j}-{t}", f"pg{j}", app=app if rng.random() < 0.9 else rng.choice(apps),
+                           aff=aff, req={"cpu": "5m"} if be else None))
+    plugins = [{"name": "predicates"}] + [{"name": p} for p in rng.sample(["gang", "drf", "priority", "proportion"],
+                                                                            rng.randint(0, 3))]
+    rng.shuffle(plugins)
+    cut = rng.randint(1, len(plugins))
+    tiers = [t for t in (plugins[:cut], plugins[cut:]) if t]
+    fx = {"name": f"affinity-{seed}", "tiers": tiers, "nodes": nodes, "pods": pods, "podGroups": pgs,
+          "queues": [{"name": "q1", "weight": 1}]}
+    if rng.random() < 0.4:
+        fx["actions"] = ["allocate", "backfill"]
+    return fx

@@ -28,11 +28,11 @@ def test_library_exports_every_declared_symbol():
     for fn in declared_functions():
         assert hasattr(L, fn), fn
     assert set(declared_functions()) == set(_abi.SIGNATURES)
-    assert L.kbg_abi_version() == _abi.ABI_VERSION == 5
+    assert L.kbg_abi_version() == _abi.ABI_VERSION == 6
     assert L.kbg_device_count() >= 0
 
 
-STRUCTS = ["kbg_resource", "kbg_node", "kbg_host_port", "kbg_taint", "kbg_job", "kbg_queue", "kbg_task", "kbg_spec", "kbg_term",
+STRUCTS = ["kbg_resource", "kbg_node", "kbg_host_port", "kbg_taint", "kbg_job", "kbg_queue", "kbg_task", "kbg_spec", "kbg_pod_term", "kbg_term",
            "kbg_requirement", "kbg_toleration", "kbg_plugin_option", "kbg_snapshot", "kbg_options", "kbg_decision",
            "kbg_job_state", "kbg_queue_state", "kbg_node_state", "kbg_stats", "kbg_eviction"]
 

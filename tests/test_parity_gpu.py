@@ -340,3 +340,16 @@ def test_contended_large_parity(seed):
     compare_outputs(run_oracle(fx), got)
     if ssn:
         ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(300))
+def test_affinity_fuzz_parity(seed):
+    """Inter-pod (anti)affinity folded into the class masks (kbg_affinity.cpp):
+    monotone losses re-checked by the resolver, affinity gains cutting the
+    batch, FitError counts rewound with the counts, across batch sizes and
+    both scan modes."""
+    fx = synth.affinity_fixture(seed)
+    got, ssn = run_fixture(fx, {"batch_tasks": 1 + seed % 9, "candidates": 1 + seed % 5, "full_scan": seed % 2})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
