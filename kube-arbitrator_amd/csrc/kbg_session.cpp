@@ -938,6 +938,15 @@ std::vector<int32_t> ranks_of(const Session& S, const std::vector<int32_t>& ids)
 
 kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options* o, kbg_comm* comm) {
   const auto t_open = std::chrono::steady_clock::now();
+  // opt-in phase timing of the session open (KBG_PROFILE_OPEN=1)
+  const bool prof = getenv("KBG_PROFILE_OPEN") != nullptr;
+  auto t_last = t_open;
+  auto phase = [&](const char* name) {
+    if (!prof) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[kbg open] %-24s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(now - t_last).count());
+    t_last = now;
+  };
   kbg_status st = validate(snap);
   if (st != KBG_OK) return st;
   if (o) S.opts = *o;
@@ -973,6 +982,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.ports_in = copy_arr(snap->ports, snap->n_ports);
   S.pod_terms_in = copy_arr(snap->pod_terms, snap->n_pod_terms);
   S.pod_labels_in = copy_arr(snap->pod_labels, 2 * snap->n_pod_labels);
+  phase("validate+copy+strings");
 
   // ---- plugins (framework.go:26-46; unknown names ignored)
   {
@@ -1236,8 +1246,10 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   build_heaps(S, E);
 
   // ---- static predicates
+  phase("plugins+ranks+engine");
   kbg::StaticHost sh;
   compile_static_predicates(S, &sh);
+  phase("static predicates");
   S.n_classes = sh.n_classes;
   S.W = (N + 63) / 64;
   // ---- integer scan mode (kbg_device.hpp TaskRec): every value the scan
@@ -1300,6 +1312,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   }
 
   // ---- device
+  phase("int mode+shapes");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(KBG_E_HIP, "no HIP device visible");
   S.device = S.opts.device >= 0 ? S.opts.device : 0;
@@ -1319,6 +1332,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   HIP_TRY(hipHostMalloc((void**)&S.h_down, down_cap * 4, hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void**)&S.h_deltas, (size_t)S.K * sizeof(kbg::NodeDelta), hipHostMallocDefault));
   if ((st = upload_nodes(S))) return st;
+  phase("device alloc+nodes");
 
   {
     kbg::StaticTables t{};
@@ -1355,6 +1369,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
                            S.stream));
     HIP_TRY(hipStreamSynchronize(S.stream));  // sh's host vectors end with this scope
   }
+  phase("class-mask kernel");
   // host ports: the port fit is folded into the class masks (setup_host_ports)
   S.h_class_mask_static = S.h_class_mask;
   setup_host_ports(S);
@@ -1365,6 +1380,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     if ((st = dalloc(S, &S.d_mdeltas, kbg::kMaskDeltaCap))) return st;
   }
   S.h_class_mask0 = S.h_class_mask;
+  phase("ports+affinity");
   S.stats.n_classes = S.n_classes;
   S.stats.shards = S.R;
   S.stats.shard_index = S.comm ? S.shard : -1;

@@ -111,3 +111,22 @@ def test_rccl_shard_count_must_match(comm1):
     fx = synth.config_fixture(1)
     got, ssn = run_fixture(fx, {"comm": comm1, "shards": 2})
     assert got["status"] == "invalid" and ssn is None
+
+
+@pytest.mark.parametrize("seed", range(0, 60, 3))
+def test_local_shards_affinity_parity(seed):
+    """Pod-affinity mask deltas reach every shard's copy of the class masks."""
+    fx = synth.affinity_fixture(seed)
+    got, ssn = run_fixture(fx, {"shards": 2 + seed % 5, "batch_tasks": 1 + seed % 7})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 40, 4))
+def test_rccl_one_rank_affinity(seed, comm1):
+    fx = synth.affinity_fixture(seed)
+    got, ssn = run_fixture(fx, {"comm": comm1, "batch_tasks": 1 + seed % 5})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
