@@ -42,8 +42,12 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(fx, budget_note):
-    """kbref oracle on the same workload, single thread (kind "port")."""
+def cpu_baseline(fx, budget_note, threads=1):
+    """kbref oracle on the same workload (kind "port"): 1 thread (SURVEY 8(d)
+    B-ref, the Go allocate loop is single-goroutine), or `threads` threads
+    evaluating each task's node loop in parallel blocks with the FitDelta map
+    built once per job (B-omp, the fair multi-core CPU baseline); both return
+    the same decisions."""
     ref = os.path.join(ROOT, "oracle", "build", "kbref")
     if not os.path.exists(ref):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
@@ -51,14 +55,20 @@ def cpu_baseline(fx, budget_note):
         src, dst = os.path.join(d, "fx.json"), os.path.join(d, "out.json")
         with open(src, "w") as f:
             json.dump(fx, f)
-        subprocess.run(["taskset", "-c", "0", ref, src, "-o", dst], check=True)
+        cpus = ",".join(str(c) for c in range(threads))
+        subprocess.run(["taskset", "-c", cpus, ref, "--threads", str(threads), src, "-o", dst], check=True)
         with open(dst) as f:
             out = json.load(f)
     secs = out["stats"]["seconds"]
     n = out["stats"]["decisions"]
-    return {"value": n / secs, "unit": "placements/s", "cores": 1, "kind": "port",
+    how = "1 thread" if threads == 1 else f"{threads} threads (OpenMP node loop)"
+    return {"value": n / secs, "unit": "placements/s", "cores": threads, "kind": "port",
             "sample": f"one full {budget_note} allocate cycle ({n} placements, {secs:.2f} s, "
-                      f"{out['stats']['predicate_calls']} predicate calls), kbref C++ port, 1 thread"}
+                      f"{out['stats']['predicate_calls']} predicate calls), kbref C++ port, {how}"}
+
+
+def omp_threads():
+    return max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
 
 
 def load_pmc_traffic(n_nodes, mode):
@@ -226,6 +236,7 @@ def main():
     }
     if rank == 0 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(fx, f"C{cid}")
+        line["cpu_baseline_omp"] = cpu_baseline(fx, f"C{cid}", omp_threads())
     if rank == 0:
         print(json.dumps(line), flush=True)
     if comm is not None:

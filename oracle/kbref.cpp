@@ -38,12 +38,14 @@
 // while the predicates plugin is enabled.
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <cmath>
 #include <functional>
 #include <list>
 #include <map>
+#include <memory>
 #include <set>
 #include <string>
 #include <unordered_map>
@@ -529,6 +531,10 @@ struct JobInfo {  // api/job_info.go:118-145
   int priority = 0;
   int32_t minAvailable = 0;
   std::map<std::string, Resource> nodesFitDelta;
+  // B-omp only: the last evaluated task's FitDelta entries in node order,
+  // turned into nodesFitDelta when allocate ends (same map, built once)
+  std::vector<std::pair<const NodeInfo*, Resource>> fit_log;
+  bool fit_log_pending = false;
   std::map<int, OMap<TaskInfo*>> statusIndex;
   OMap<TaskInfo*> tasks;
   Resource allocated, totalRequest;
@@ -792,6 +798,7 @@ struct Session {  // framework/session.go:35-61
   std::unordered_map<TaskInfo*, int> decisionOf;
   std::vector<std::pair<std::string, std::string>> binds;  // (ns/name, node) in dispatch order
   int64_t predicate_calls = 0;
+  int threads = 1;  // > 1: allocate's node loop evaluated in parallel blocks (B-omp CPU baseline only)
   std::vector<TaskInfo*> evaluated;  // every task whose node loop ran, in order
 
   // session_plugins.go:142-156
@@ -853,8 +860,8 @@ struct Session {  // framework/session.go:35-61
     return l->uid < r->uid;
   }
   // :278-295
-  bool PredicateFn(TaskInfo* t, NodeInfo* n) {
-    predicate_calls++;
+  bool PredicateFn(TaskInfo* t, NodeInfo* n, bool count = true) {
+    if (count) predicate_calls++;
     for (auto& tier : tiers)
       for (auto& p : tier) {
         if (p.predicateDisabled) continue;
@@ -1283,7 +1290,8 @@ struct Predicates {
   Session* ssn = nullptr;
   bool faithful_scan = false;  // replay the podLister's per-call O(allocated pods) walk (F7)
   bool ghost = false;          // some allocated-status pod names a node outside the session
-  std::unordered_map<int64_t, char> static_cache;
+  std::unique_ptr<std::atomic<int8_t>[]> static_cache;  // [class][node]: -1 unknown
+  size_t static_nodes = 0;
 
   // ---- PodAffinityChecker.InterPodAffinityMatches with meta == nil (vendor
   // predicates.go:1155-1182), the slow path kube-batch takes
@@ -1436,12 +1444,12 @@ struct Predicates {
       if (!pod_tolerates_node_taints(task->pod, node->node)) return false;
       return true;
     };
-    if (faithful_scan || task->spec_class < 0) return calc();
-    int64_t key = (int64_t)task->spec_class * (int64_t)(1 << 30) + (int64_t)node_pos;
-    auto it = static_cache.find(key);
-    if (it != static_cache.end()) return it->second;
+    if (faithful_scan || task->spec_class < 0 || !static_cache) return calc();
+    std::atomic<int8_t>& slot = static_cache[(size_t)task->spec_class * static_nodes + node_pos];
+    const int8_t known = slot.load(std::memory_order_relaxed);
+    if (known >= 0) return known != 0;
     bool r = calc();
-    static_cache[key] = r;
+    slot.store(r ? 1 : 0, std::memory_order_relaxed);
     return r;
   }
   std::unordered_map<NodeInfo*, size_t> pos;
@@ -1467,9 +1475,15 @@ struct Predicates {
     return true;
   }
 
-  void open(Session* s, bool active) {
+  void open(Session* s, bool active, int n_classes) {
     ssn = s;
     for (size_t i = 0; i < s->nodes.size(); i++) pos[s->nodes[i]] = i;
+    static_nodes = s->nodes.size();
+    if (n_classes > 0) {
+      const size_t n = (size_t)n_classes * static_nodes;
+      static_cache.reset(new std::atomic<int8_t>[n]);
+      for (size_t i = 0; i < n; ++i) static_cache[i].store(-1, std::memory_order_relaxed);
+    }
     // Without any pod (anti)affinity term in the session the inter-pod
     // predicate reduces to the GetNodeInfo errors of allocated pods whose node
     // is outside the session (SURVEY A10 "ghost" pods); otherwise it runs in full.
@@ -1494,6 +1508,56 @@ struct Predicates {
 };
 
 // ---------------------------------------------------------------- allocate
+// allocate.go:119-162 for one task with the predicates of a block of nodes
+// evaluated on ssn->threads threads (PredicateFn reads the session only), then
+// the block walked in node order exactly like the sequential loop: the first
+// node whose Idle or Releasing fits wins; NodesFitDelta gets the
+// predicate-passing nodes before it. A panic inside PredicateFn is rethrown
+// when the walk reaches its node. Used for the B-omp CPU baseline only.
+static bool threaded_node_loop(Session* ssn, JobInfo* job, TaskInfo* task) {
+  const size_t N = ssn->nodes.size();
+  const size_t B = (size_t)ssn->threads * 64;
+  // per node of a block: 0 predicates fail, 1 Idle fits, 2 Releasing fits, 3 neither; 4 PredicateFn panics
+  std::vector<int8_t> st(std::min(N, B));
+  std::vector<std::string> panic(st.size());
+  job->fit_log.clear();
+  job->fit_log_pending = true;
+  for (size_t base = 0; base < N; base += B) {
+    const size_t n = std::min(N, base + B) - base;
+#pragma omp parallel for num_threads(ssn->threads) schedule(static)
+    for (size_t i = 0; i < n; ++i) {
+      NodeInfo* node = ssn->nodes[base + i];
+      try {
+        if (!ssn->PredicateFn(task, node, false)) st[i] = 0;
+        else if (task->resreq.LessEqual(node->idle)) st[i] = 1;
+        else if (task->resreq.LessEqual(node->releasing)) st[i] = 2;
+        else st[i] = 3;
+      } catch (const RefPanic& e) {
+        st[i] = 4;
+        panic[i] = e.what();
+      }
+    }
+    for (size_t i = 0; i < n; ++i) {
+      ssn->predicate_calls++;
+      if (st[i] == 4) throw RefPanic(panic[i]);
+      if (st[i] == 0) continue;
+      NodeInfo* node = ssn->nodes[base + i];
+      if (st[i] == 1) {
+        ssn->Allocate(task, node);
+        return true;
+      }
+      Resource fd = node->idle;
+      fd.FitDelta(task->resreq);
+      job->fit_log.emplace_back(node, fd);
+      if (st[i] == 2) {
+        ssn->Pipeline(task, node);
+        return true;
+      }
+    }
+  }
+  return false;
+}
+
 // pkg/scheduler/actions/allocate/allocate.go:41-176
 static void allocate_execute(Session* ssn) {
   PriorityQueue<QueueInfo> queues([ssn](QueueInfo* l, QueueInfo* r) { return ssn->QueueOrderFn(l, r); });
@@ -1530,6 +1594,10 @@ static void allocate_execute(Session* ssn) {
       ssn->evaluated.push_back(task);
       bool assigned = false;
       if (!job->nodesFitDelta.empty()) job->nodesFitDelta.clear();
+      if (ssn->threads > 1) {  // B-omp: the same loop, predicates evaluated in parallel blocks
+        if (threaded_node_loop(ssn, job, task)) { jobs->Push(job); break; }
+        continue;
+      }
       for (NodeInfo* node : ssn->nodes) {
         if (!ssn->PredicateFn(task, node)) continue;
         if (task->resreq.LessEqual(node->idle)) {
@@ -1551,6 +1619,13 @@ static void allocate_execute(Session* ssn) {
     }
     queues.Push(queue);
   }
+  for (JobInfo* job : ssn->jobs)
+    if (job->fit_log_pending) {
+      job->nodesFitDelta.clear();
+      for (auto& e : job->fit_log) job->nodesFitDelta[e.first->name] = e.second;
+      job->fit_log.clear();
+      job->fit_log_pending = false;
+    }
 }
 
 // backfill.go:40-71: every Pending task of every job (ssn.Jobs order, status
@@ -1832,7 +1907,7 @@ static void reorder(std::vector<T*>& v, const Value* order, std::function<std::s
   v = out;
 }
 
-static std::string run_session(const Value& fx, bool faithful, bool no_cache) {
+static std::string run_session(const Value& fx, bool faithful, bool no_cache, int threads) {
   World w;
   std::string defaultQueue;
   if (const Value* o = fx.get("options")) {
@@ -1894,6 +1969,8 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache) {
       w.pod_class.push_back(no_cache ? -1 : id);
     }
 
+  int n_pod_classes = 0;
+  for (int c : w.pod_class) n_pod_classes = std::max(n_pod_classes, c + 1);
   SchedulerCache cache;
   cache.defaultQueue = defaultQueue;
   for (auto& n : w.nodes) cache.addNode(&n);
@@ -1936,6 +2013,7 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache) {
   Proportion prop;
   Predicates preds;
   preds.faithful_scan = faithful;
+  ssn->threads = std::max(1, threads);
   // OnSessionOpen in plugin registration (tier) order; the plugins touch disjoint state.
   std::set<std::string> opened;
   for (auto& tier : ssn->tiers)
@@ -1951,7 +2029,7 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache) {
         for (auto& t2 : ssn->tiers)
           for (auto& p2 : t2)
             if (p2.name == "predicates" && !p2.predicateDisabled) active = true;
-        preds.open(ssn, active);
+        preds.open(ssn, active, n_pod_classes);
       }
       // unknown plugin names are skipped (framework.go:30-35 logs an error)
     }
@@ -2102,15 +2180,17 @@ static std::string run_ops(const Value& fx) {
 int main(int argc, char** argv) {
   std::string in, out;
   bool faithful = false, no_cache = false;
+  int threads = 1;
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
     if (a == "--faithful") faithful = true;
     else if (a == "--no-cache") no_cache = true;
+    else if (a == "--threads" && i + 1 < argc) threads = std::atoi(argv[++i]);
     else if (a == "-o" && i + 1 < argc) out = argv[++i];
     else in = a;
   }
   if (in.empty()) {
-    fprintf(stderr, "usage: kbref [--faithful] [--no-cache] fixture.json [-o out.json]\n");
+    fprintf(stderr, "usage: kbref [--faithful] [--no-cache] [--threads N] fixture.json [-o out.json]\n");
     return 2;
   }
   std::string result;
@@ -2118,7 +2198,7 @@ int main(int argc, char** argv) {
   try {
     Value fx = kbjson::parse_file(in);
     std::string kind = fx.str("kind", "session");
-    result = kind == "session" ? ref::run_session(fx, faithful, no_cache) : ref::run_ops(fx);
+    result = kind == "session" ? ref::run_session(fx, faithful, no_cache, threads) : ref::run_ops(fx);
   } catch (const ref::RefPanic& e) {
     result = std::string("{\"status\":\"ref_panic\",\"error\":") + kbjson::quote(e.what()) + "}";
   } catch (const ref::Unsupported& e) {
