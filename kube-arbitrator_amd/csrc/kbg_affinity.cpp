@@ -43,6 +43,29 @@ bool allocated_status(int32_t s) {  // api/helpers.go:63-70 (the podLister's pod
   return s == KBG_BOUND || s == KBG_BINDING || s == KBG_RUNNING || s == KBG_ALLOCATED;
 }
 
+// A class's forbidden pairs: a handful (one per distinct topology value of
+// the pods that forbid them), so a flat list beats a hash map.
+template <class K>
+int32_t count_of(const std::vector<std::pair<K, int32_t>>& v, K k) {
+  for (const auto& e : v)
+    if (e.first == k) return e.second;
+  return 0;
+}
+// adds d to k's count; returns {before, after}; drops entries that reach 0
+template <class K>
+std::pair<int32_t, int32_t> count_add(std::vector<std::pair<K, int32_t>>& v, K k, int32_t d) {
+  size_t i = 0;
+  while (i < v.size() && v[i].first != k) ++i;
+  if (i == v.size()) v.emplace_back(k, 0);
+  const int32_t b = v[i].second;
+  const int32_t a = v[i].second += d;
+  if (a == 0) {
+    v[i] = v.back();
+    v.pop_back();
+  }
+  return {b, a};
+}
+
 const int32_t* find_label(const std::vector<std::pair<int32_t, int32_t>>& ls, int32_t key) {
   auto it = std::lower_bound(ls.begin(), ls.end(), std::make_pair(key, INT32_MIN));
   return it != ls.end() && it->first == key ? &it->second : nullptr;
@@ -135,6 +158,7 @@ bool ports_ok(const Session& S, int32_t c, int32_t n) {
 // The class-mask bit of (c, n) from the static predicate, the port fit and
 // the affinity counts; a change is queued for the device and reported.
 void recompute_bit(Session& S, int32_t c, int32_t n) {
+  S.affm->prof_recomputes++;
   const size_t idx = (size_t)c * S.W + (n >> 6);
   const uint64_t bit = 1ull << (n & 63);
   bool v = (S.h_class_mask_static[idx] & bit) != 0;
@@ -149,7 +173,7 @@ void recompute_bit(Session& S, int32_t c, int32_t n) {
     }
   } else {
     S.h_class_mask[idx] &= ~bit;
-    S.mmark[n] = S.mstamp;  // a candidate list of this batch may hold the node: the resolver re-checks it
+    S.mwmark[idx] = S.mstamp;  // a candidate list of this batch may hold the node: the resolver re-checks it
   }
   if (!S.mask_dirty_flag[idx]) {
     S.mask_dirty_flag[idx] = 1;
@@ -168,10 +192,8 @@ bool aff_ok(const Session& S, const AffState& st, int32_t c, int32_t n) {
   if (st.poison) return false;
   const auto& ca = st.cntA[c];
   if (!ca.empty())
-    for (const auto& kv : M.node_labels[n]) {
-      auto it = ca.find(pair_key(kv.first, kv.second));
-      if (it != ca.end() && it->second > 0) return false;
-    }
+    for (const auto& kv : M.node_labels[n])
+      if (count_of(ca, pair_key(kv.first, kv.second)) > 0) return false;
   const AffClass& a = M.cls[c];
   if (a.hasB) {
     if (a.b_err) return false;
@@ -179,16 +201,16 @@ bool aff_ok(const Session& S, const AffState& st, int32_t c, int32_t n) {
       if (!a.b_self) return false;
     } else {
       if (a.b_empty_key) return false;
-      const int32_t sg = a.sigB[n];
-      if (sg < 0 || st.cntB[c][sg] == 0) return false;
+      const int32_t sg = M.sigtabs[a.b_tab].sig[n];
+      if (sg < 0 || count_of(st.cntB[c], sg) == 0) return false;
     }
   }
   if (a.hasC) {
     if (a.c_err) {
       if (st.allocated > 0) return false;
     } else {
-      const int32_t sg = a.sigC[n];
-      if (sg >= 0 && st.cntC[c][sg] > 0) return false;
+      const int32_t sg = M.sigtabs[a.c_tab].sig[n];
+      if (sg >= 0 && count_of(st.cntC[c], sg) > 0) return false;
     }
   }
   return true;
@@ -199,6 +221,10 @@ bool aff_ok(const Session& S, const AffState& st, int32_t c, int32_t n) {
 void aff_place(Session& S, int32_t t, int32_t n, int32_t sign, AffState& st, bool update_bits) {
   const AffinityModel& M = *S.affm;
   const int32_t s = S.tasks_in[t].spec;
+  if (s >= 0 && !M.spec_effect[s] && M.c_err_classes.empty()) {  // selects and is selected by nothing
+    st.allocated += sign;
+    return;
+  }
   std::vector<int32_t> full;  // classes to recompute on every node
   auto crossed = [](int32_t before, int32_t after) { return (before == 0) != (after == 0); };
   {
@@ -224,12 +250,8 @@ void aff_place(Session& S, int32_t t, int32_t n, int32_t sign, AffState& st, boo
       if (!v) continue;
       const int64_t pk = pair_key(term.key, *v);
       for (int32_t c : M.anti_match[s][k]) {
-        int32_t& cnt = st.cntA[c][pk];
-        const int32_t b = cnt;
-        cnt += sign;
-        const bool cross = crossed(b, cnt);
-        if (cnt == 0) st.cntA[c].erase(pk);
-        if (update_bits && cross) {
+        const auto ba = count_add(st.cntA[c], pk, sign);
+        if (update_bits && crossed(ba.first, ba.second)) {
           auto it = M.pair_nodes.find(pk);
           if (it != M.pair_nodes.end())
             for (int32_t m : it->second) recompute_bit(S, c, m);
@@ -241,25 +263,49 @@ void aff_place(Session& S, int32_t t, int32_t n, int32_t sign, AffState& st, boo
       const AffClass& a = M.cls[c];
       const int32_t b = st.nB[c];
       st.nB[c] += sign;
-      const bool all = update_bits && crossed(b, st.nB[c]);
-      const int32_t sg = a.sigB[n];
+      const bool first = update_bits && crossed(b, st.nB[c]);
+      const AffSigTable* tb = a.b_tab >= 0 ? &M.sigtabs[a.b_tab] : nullptr;
+      const int32_t sg = tb ? tb->sig[n] : -1;
       if (sg >= 0) {
-        const int32_t b2 = st.cntB[c][sg];
-        st.cntB[c][sg] += sign;
-        if (update_bits && !all && crossed(b2, st.cntB[c][sg]))
-          for (int32_t m : a.b_nodes[sg]) recompute_bit(S, c, m);
+        const auto ba = count_add(st.cntB[c], sg, sign);
+        if (update_bits && !first && crossed(ba.first, ba.second))
+          for (int32_t m : tb->nodes[sg]) recompute_bit(S, c, m);
       }
-      if (all) full.push_back(c);
+      if (!first) continue;
+      if (sign > 0 && a.b_self) {
+        // the first matching pod ends the "first pod of a series" pass: only
+        // its topology domain stays (nothing with an empty key or without the
+        // keys); every other constraint is unchanged, so the class mask is
+        // ANDed with the domain (nil-Node nodes stay reachable)
+        std::vector<uint64_t> keep(M.panic_words);
+        if (!a.b_empty_key && sg >= 0)
+          for (int32_t m : tb->nodes[sg]) keep[m >> 6] |= 1ull << (m & 63);
+        for (int32_t w = 0; w < S.W; ++w) {
+          const size_t idx = (size_t)c * S.W + w;
+          const uint64_t old = S.h_class_mask[idx], nw = old & keep[w];
+          if (nw == old) continue;
+          S.h_class_mask[idx] = nw;
+          S.mwmark[idx] = S.mstamp;
+          if (!S.mask_dirty_flag[idx]) {
+            S.mask_dirty_flag[idx] = 1;
+            S.mask_dirty.push_back((uint32_t)idx);
+          }
+        }
+      } else if (sign > 0 && !a.b_empty_key && sg >= 0) {
+        for (int32_t m : tb->nodes[sg]) recompute_bit(S, c, m);  // nothing passed before: its domain opens
+      } else {
+        full.push_back(c);
+      }
     }
     // (C) ... and of the anti terms of these
     for (int32_t c : M.matchC[s]) {
       const AffClass& a = M.cls[c];
-      const int32_t sg = a.sigC[n];
+      const AffSigTable& tc = M.sigtabs[a.c_tab];
+      const int32_t sg = tc.sig[n];
       if (sg < 0) continue;
-      const int32_t b = st.cntC[c][sg];
-      st.cntC[c][sg] += sign;
-      if (update_bits && crossed(b, st.cntC[c][sg]))
-        for (int32_t m : a.c_nodes[sg]) recompute_bit(S, c, m);
+      const auto ba = count_add(st.cntC[c], sg, sign);
+      if (update_bits && crossed(ba.first, ba.second))
+        for (int32_t m : tc.nodes[sg]) recompute_bit(S, c, m);
     }
   }
   if (!update_bits) return;
@@ -314,10 +360,17 @@ void setup_affinity(Session& S) {
   }
   // per class: (B) and (C) keys and node signatures
   M->cls.resize(C);
-  auto signatures = [&](const std::vector<int32_t>& keys, std::vector<int32_t>* sig,
-                        std::vector<std::vector<int32_t>>* nodes) {
+  std::map<std::vector<int32_t>, int32_t> tab_of;
+  auto sig_table = [&](const std::vector<int32_t>& keys) -> int32_t {
+    auto found = tab_of.find(keys);
+    if (found != tab_of.end()) return found->second;
+    const int32_t id = (int32_t)M->sigtabs.size();
+    tab_of.emplace(keys, id);
+    M->sigtabs.emplace_back();
+    AffSigTable& tab = M->sigtabs.back();
+    tab.keys = keys;
+    tab.sig.assign(N, -1);
     std::map<std::vector<int32_t>, int32_t> ids;
-    sig->assign(N, -1);
     for (int32_t n = 0; n < N; ++n) {
       std::vector<int32_t> vals;
       bool all = true;
@@ -331,17 +384,18 @@ void setup_affinity(Session& S) {
       }
       if (!all) continue;
       auto it = ids.find(vals);
-      int32_t id;
+      int32_t sg;
       if (it != ids.end()) {
-        id = it->second;
+        sg = it->second;
       } else {
-        id = (int32_t)ids.size();
-        ids.emplace(vals, id);
-        nodes->emplace_back();
+        sg = (int32_t)ids.size();
+        ids.emplace(vals, sg);
+        tab.nodes.emplace_back();
       }
-      (*sig)[n] = id;
-      (*nodes)[id].push_back(n);
+      tab.sig[n] = sg;
+      tab.nodes[sg].push_back(n);
     }
+    return id;
   };
   for (int32_t c = 0; c < C; ++c) {
     AffClass& a = M->cls[c];
@@ -351,24 +405,24 @@ void setup_affinity(Session& S) {
     if (!sp.aff.empty()) {
       a.hasB = true;
       a.b_err = sp.aff_err;
+      std::vector<int32_t> keys;
       for (const AffTerm& t : sp.aff) {
         if (t.key_empty) a.b_empty_key = true;
-        a.b_keys.push_back(t.key);
+        keys.push_back(t.key);
       }
       a.b_self = !a.b_err && all_terms_match(sp.aff, sp.ns, sp);  // targetPodMatchesAffinityOfPod(pod, pod)
-      if (!a.b_err && !a.b_empty_key) signatures(a.b_keys, &a.sigB, &a.b_nodes);
-      else a.sigB.assign(N, -1);
+      if (!a.b_err && !a.b_empty_key) a.b_tab = sig_table(keys);
     }
     if (!sp.anti.empty()) {
       a.hasC = true;
       a.c_err = sp.anti_err;
       if (a.c_err) M->c_err_classes.push_back(c);
+      std::vector<int32_t> keys;
       for (const AffTerm& t : sp.anti) {
         if (t.key_empty) break;  // the error is reached once every earlier key matched
-        a.c_keys.push_back(t.key);
+        keys.push_back(t.key);
       }
-      if (!a.c_err) signatures(a.c_keys, &a.sigC, &a.c_nodes);
-      else a.sigC.assign(N, -1);
+      if (!a.c_err) a.c_tab = sig_table(keys);
     }
   }
   // which classes each spec's pods select: as the owner of anti terms (A), as a target (B, C)
@@ -398,16 +452,18 @@ void setup_affinity(Session& S) {
   for (int32_t n = 0; n < N; ++n)
     for (const auto& kv : M->node_labels[n])
       if (anti_keys.count(kv.first)) M->pair_nodes[pair_key(kv.first, kv.second)].push_back(n);
+  M->spec_effect.assign(NS, 0);
+  for (int32_t s = 0; s < NS; ++s) {
+    bool e = M->spec_poison[s] || !M->matchB[s].empty() || !M->matchC[s].empty();
+    for (const auto& l : M->anti_match[s]) e = e || !l.empty();
+    M->spec_effect[s] = e ? 1 : 0;
+  }
   // counts of the pods allocated at open
   AffState& st = M->st0;
   st.nB.assign(C, 0);
   st.cntA.assign(C, {});
-  st.cntB.resize(C);
-  st.cntC.resize(C);
-  for (int32_t c = 0; c < C; ++c) {
-    st.cntB[c].assign(M->cls[c].b_nodes.size(), 0);
-    st.cntC[c].assign(M->cls[c].c_nodes.size(), 0);
-  }
+  st.cntB.assign(C, {});
+  st.cntC.assign(C, {});
   for (int32_t t = 0; t < S.n_tasks; ++t)
     if (allocated_status(S.tasks_in[t].status)) aff_place(S, t, S.task_node[t], +1, st, false);
   M->st = st;
@@ -433,7 +489,10 @@ void setup_affinity(Session& S) {
   }
   // fold into the class masks
   if (S.mask_dirty_flag.size() != S.h_class_mask.size()) S.mask_dirty_flag.assign(S.h_class_mask.size(), 0);
-  S.mmark.assign(N, -1);
+  S.mwmark.assign((size_t)C * S.W, -1);
+  M->panic_words.assign(S.W, 0);
+  for (int32_t n = 0; n < N; ++n)
+    if (S.panic_node[n]) M->panic_words[n >> 6] |= 1ull << (n & 63);
   S.aff_gain_flag.assign(C, 0);
   S.aff_gain_classes.clear();
   for (int32_t c = 0; c < C; ++c)

@@ -679,7 +679,8 @@ struct Resolver {
     for (int32_t& k = cursor[g]; k < n; ++k) {
       const int32_t nd = (int32_t)(c[k] & ~kbg::kCandPipelineBit);
       if (S.panic_node[nd]) return RES_PANIC;
-      if (mark[nd] != stamp && (!S.has_aff || S.mmark[nd] != S.mstamp)) {
+      if (mark[nd] != stamp &&
+          (!S.has_aff || S.mwmark[(size_t)S.task_class[t] * S.W + (nd >> 6)] != S.mstamp)) {
         *node = nd;
         *kind = (c[k] & kbg::kCandPipelineBit) ? KBG_KIND_PIPELINE : KBG_KIND_ALLOCATE;
         return RES_OK;
@@ -750,7 +751,15 @@ void mirror_add(Session& S, int32_t t, int32_t nd, int32_t kind) {
   S.ntasks[nd]++;
   if (S.has_ports) add_ports(S, S.task_class[t], nd);
   // an Allocated pod joins the podLister (api/helpers.go:63-70); Pipelined does not
-  if (S.has_aff && kind == KBG_KIND_ALLOCATE) kbg::aff_place(S, t, nd, +1, S.affm->st, true);
+  if (S.has_aff && kind == KBG_KIND_ALLOCATE) {
+    static const bool prof = getenv("KBG_PROFILE_AFF") != nullptr;
+    const uint64_t c0 = prof ? __builtin_readcyclecounter() : 0;
+    kbg::aff_place(S, t, nd, +1, S.affm->st, true);
+    if (prof) {
+      S.affm->prof_cycles += __builtin_readcyclecounter() - c0;
+      S.affm->prof_calls++;
+    }
+  }
 }
 
 // Builds the port-atom dictionary (distinct sanitized (ip, protocol, port)
@@ -1861,6 +1870,11 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   finish();
   HIP_TRY(hipStreamSynchronize(S.stream));  // last delta write-back
   compute_fit_deltas(S, dec, dec_old, dec_oldp, last);
+  if (S.has_aff && getenv("KBG_PROFILE_AFF"))
+    fprintf(stderr, "[kbg aff] aff_place %llu calls, %.1f cycles/call, %llu bit recomputes, mask words dirty %zu\n",
+            (unsigned long long)S.affm->prof_calls,
+            S.affm->prof_calls ? (double)S.affm->prof_cycles / S.affm->prof_calls : 0.0,
+            (unsigned long long)S.affm->prof_recomputes, S.mask_dirty.size());
   S.fin = E;
   S.stats.engine_ms = engine_ms;
   S.stats.replayed = replayed;

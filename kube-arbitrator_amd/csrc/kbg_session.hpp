@@ -99,31 +99,40 @@ struct AffSpec {
   std::vector<AffTerm> aff, anti;
   bool aff_err = false, anti_err = false;  // a term's selector fails to build
 };
+// Node signatures over a list of topology keys (the values of those keys;
+// -1 where a key is missing), shared by every class with the same key list.
+struct AffSigTable {
+  std::vector<int32_t> keys;
+  std::vector<int32_t> sig;                  // per node
+  std::vector<std::vector<int32_t>> nodes;   // per signature
+};
 struct AffClass {  // per static class
   bool hasB = false, b_err = false, b_empty_key = false, b_self = false;
-  std::vector<int32_t> b_keys, sigB;                // node signature over the affinity terms' keys (-1: a key missing)
-  std::vector<std::vector<int32_t>> b_nodes;        // nodes of each signature
+  int32_t b_tab = -1;   // signatures over the affinity terms' keys
   bool hasC = false, c_err = false;
-  std::vector<int32_t> c_keys, sigC;                // over the anti terms' keys before the first empty one
-  std::vector<std::vector<int32_t>> c_nodes;
+  int32_t c_tab = -1;   // over the anti terms' keys before the first empty one
 };
 struct AffState {  // counts over the AllocatedStatus pods
   int32_t poison = 0;     // pods whose anti term fails to build its selector
   int32_t allocated = 0;  // all of them (the podLister is not empty)
   std::vector<int32_t> nB;
-  std::vector<std::vector<int32_t>> cntB, cntC;
-  std::vector<std::unordered_map<int64_t, int32_t>> cntA;
+  std::vector<std::vector<std::pair<int32_t, int32_t>>> cntB, cntC;  // per class: (signature, count), sparse
+  std::vector<std::vector<std::pair<int64_t, int32_t>>> cntA;  // per class: (pair, count), few entries
 };
 struct AffinityModel {
   std::vector<AffSpec> specs;                                  // per kbg_spec
   std::vector<AffClass> cls;                                   // per class
+  std::vector<AffSigTable> sigtabs;
   std::vector<std::vector<std::vector<int32_t>>> anti_match;   // [spec][anti term] -> classes it selects
   std::vector<std::vector<int32_t>> matchB, matchC;            // [spec] -> classes whose terms select it
   std::vector<char> spec_poison;
+  std::vector<char> spec_effect;                               // [spec]: its allocation changes some count
   std::vector<int32_t> c_err_classes;
   std::vector<std::vector<std::pair<int32_t, int32_t>>> node_labels;
   std::unordered_map<int64_t, std::vector<int32_t>> pair_nodes;  // (topology key, value) -> nodes
   std::vector<std::vector<int32_t>> class_shapes;
+  std::vector<uint64_t> panic_words;  // nil-Node nodes (kept reachable in every mask)
+  uint64_t prof_cycles = 0, prof_calls = 0, prof_recomputes = 0;  // KBG_PROFILE_AFF
   AffState st0, st;  // at open / now
 };
 
@@ -266,7 +275,7 @@ struct Session {
   std::shared_ptr<AffinityModel> affm;
   std::vector<kbg_pod_term> pod_terms_in;
   std::vector<int32_t> pod_labels_in;
-  std::vector<int32_t> mmark;                  // per node: batch stamp of the last class-mask bit it lost
+  std::vector<int32_t> mwmark;                 // per class-mask word: batch stamp of the last bit it lost
   int32_t mstamp = 0;                          // the current batch stamp
   std::vector<uint8_t> aff_gain_flag;          // per class: gained nodes since the last cut
   std::vector<int32_t> aff_gain_classes;

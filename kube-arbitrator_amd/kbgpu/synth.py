@@ -63,6 +63,8 @@ def config_fixture(cid):
     """BASELINE config `cid` (1-5) as a fixture dict."""
     if cid == 5:
         return contended_config()
+    if cid == 6:  # not a BASELINE config: C3 with inter-pod (anti)affinity (scale check)
+        return affinity_config()
     c = CONFIGS[cid]
     rng = random.Random(BASE_SEED + cid)
     nodes = [_node(i, rng, c["mix"]) for i in range(c["nodes"])]
@@ -497,4 +499,37 @@ def affinity_fixture(seed, max_nodes=16, max_jobs=8, max_tasks=6):
           "queues": [{"name": "q1", "weight": 1}]}
     if rng.random() < 0.4:
         fx["actions"] = ["allocate", "backfill"]
+    return fx
+
+
+def affinity_config(nodes=5000, jobs=2000, tasks_per_job=50, seed=6):
+    """C3's cluster and jobs with inter-pod (anti)affinity on top (not a
+    BASELINE config; a scale check of kbg_affinity.cpp): every pod is labelled
+    with its job; 40% of the jobs spread over hosts (required anti-affinity to
+    their own pods on the node's name label), 20% co-locate in one zone
+    (required affinity to their own pods on the zone label), the rest plain."""
+    fx = config_fixture(3)
+    rng = random.Random(BASE_SEED + 100 + seed)
+    fx = dict(fx, name="C3-affinity")
+    fx["nodes"] = fx["nodes"][:nodes]
+    for n in fx["nodes"]:
+        n["labels"] = dict(n["labels"], host=n["name"])
+    pods = [p for p in fx["pods"] if int(p["uid"].split("-")[1]) < jobs and int(p["uid"].split("-")[2]) < tasks_per_job]
+    kind = {}
+    for p in pods:
+        j = p["annotations"]["scheduling.k8s.io/group-name"]
+        if j not in kind:
+            r = rng.random()
+            kind[j] = "spread" if r < 0.4 else ("colocate" if r < 0.6 else "plain")
+        p["labels"] = {"job": j}
+        term = {"labelSelector": {"matchLabels": {"job": j}}}
+        if kind[j] == "spread":
+            p["affinity"] = dict(p.get("affinity") or {}, podAntiAffinity={
+                "requiredDuringSchedulingIgnoredDuringExecution": [dict(term, topologyKey="host")]})
+        elif kind[j] == "colocate":
+            p["affinity"] = dict(p.get("affinity") or {}, podAffinity={
+                "requiredDuringSchedulingIgnoredDuringExecution": [dict(term, topologyKey="zone")]})
+    fx["pods"] = pods
+    names = {p["annotations"]["scheduling.k8s.io/group-name"] for p in pods}
+    fx["podGroups"] = [g for g in fx["podGroups"] if g["name"] in names]
     return fx

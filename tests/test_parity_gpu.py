@@ -353,3 +353,13 @@ def test_affinity_fuzz_parity(seed):
     compare_outputs(run_oracle(fx), got)
     if ssn:
         ssn.close()
+
+
+@pytest.mark.parametrize("nodes,jobs,tasks", [(300, 60, 20), (600, 100, 20)])
+def test_affinity_config_scaled_parity(nodes, jobs, tasks):
+    """C3's generator with spread (host anti-affinity) and co-located (zone
+    affinity) jobs, at a size the oracle's per-pair podLister walk finishes."""
+    fx = synth.affinity_config(nodes=nodes, jobs=jobs, tasks_per_job=tasks)
+    got, ssn = run_fixture(fx)
+    compare_outputs(run_oracle(fx), got)
+    ssn.close()
