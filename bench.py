@@ -42,6 +42,29 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# The contract is ONE JSON line on stdout. Libraries write there too (RCCL
+# prints a version banner when a communicator comes up), so file descriptor 1
+# is pointed at stderr for the whole run and the result line goes to a
+# duplicate of the original stdout.
+_RESULT_FD = None
+
+
+def _capture_stdout():
+    global _RESULT_FD
+    sys.stdout.flush()
+    _RESULT_FD = os.dup(1)
+    os.dup2(2, 1)
+
+
+def emit(line):
+    data = (json.dumps(line) + "\n").encode()
+    if _RESULT_FD is None:
+        sys.stdout.write(data.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_RESULT_FD, data)
+
+
 def cpu_baseline(fx, budget_note, threads=1):
     """kbref oracle on the same workload (kind "port"): 1 thread (SURVEY 8(d)
     B-ref, the Go allocate loop is single-goroutine), or `threads` threads
@@ -88,6 +111,7 @@ def load_pmc_traffic(n_nodes, mode):
 
 
 def main():
+    _capture_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -238,7 +262,7 @@ def main():
         line["cpu_baseline"] = cpu_baseline(fx, f"C{cid}")
         line["cpu_baseline_omp"] = cpu_baseline(fx, f"C{cid}", omp_threads())
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        emit(line)
     if comm is not None:
         comm.close()
     kdist.shutdown()
@@ -344,7 +368,7 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid, open_ms_
         line["cpu_baseline"]["sample"] = line["cpu_baseline"]["sample"].replace("allocate cycle", "cycle (" +
                                                                                 ", ".join(fx["actions"]) + ")")
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        emit(line)
     if comm is not None:
         comm.close()
     kdist.shutdown()
