@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KBG_ABI_VERSION 6
+#define KBG_ABI_VERSION 7
 
 typedef enum kbg_status {
   KBG_OK = 0,
@@ -392,6 +392,24 @@ kbg_status kbg_node_state_get(kbg_session* s, int32_t node, kbg_node_state* out)
 kbg_status kbg_stats_get(kbg_session* s, kbg_stats* out);
 
 void kbg_session_close(kbg_session* s);
+
+/* Snapshot wire format: the flat kbg_snapshot as one
+ * little-endian byte string — the header "KBGS", format version, ABI
+ * version, the 20 counts of kbg_snapshot in declaration order, then every
+ * string as (uint32 length, bytes) and every array as its raw struct bytes in
+ * declaration order. A cache adapter builds it once per scheduling cycle (or a
+ * recorder keeps it for replay); decoding rebuilds the arrays in library-owned
+ * memory, validates them as kbg_session_open does, and the snapshot it hands
+ * back opens sessions unchanged.
+ * kbg_snapshot_encode with out == NULL / cap == 0 stores the size in *n_out. */
+typedef struct kbg_snapshot_blob kbg_snapshot_blob;
+#define KBG_SNAPSHOT_FORMAT 1
+kbg_status kbg_snapshot_encode(const kbg_snapshot* snap, uint8_t* out, int64_t cap, int64_t* n_out);
+kbg_status kbg_snapshot_decode(const uint8_t* data, int64_t n, kbg_snapshot_blob** out);
+kbg_status kbg_snapshot_save(const kbg_snapshot* snap, const char* path);
+kbg_status kbg_snapshot_load(const char* path, kbg_snapshot_blob** out);
+const kbg_snapshot* kbg_snapshot_blob_get(const kbg_snapshot_blob* b);
+void kbg_snapshot_blob_free(kbg_snapshot_blob* b);
 
 #ifdef __cplusplus
 }

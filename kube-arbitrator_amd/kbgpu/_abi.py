@@ -35,7 +35,7 @@ DISABLE_RECLAIMABLE = 1 << 4
 DISABLE_QUEUE_ORDER = 1 << 5
 DISABLE_PREDICATE = 1 << 6
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 COMM_ID_BYTES = 128
 
 KIND_ALLOCATE = 0
@@ -198,6 +198,12 @@ SIGNATURES = {
     "kbg_node_state_get": (i32, [ctypes.c_void_p, i32, P(kbg_node_state)]),
     "kbg_stats_get": (i32, [ctypes.c_void_p, P(kbg_stats)]),
     "kbg_session_close": (None, [ctypes.c_void_p]),
+    "kbg_snapshot_encode": (i32, [P(kbg_snapshot), ctypes.c_void_p, i64, P(i64)]),
+    "kbg_snapshot_decode": (i32, [ctypes.c_void_p, i64, P(ctypes.c_void_p)]),
+    "kbg_snapshot_save": (i32, [P(kbg_snapshot), ctypes.c_char_p]),
+    "kbg_snapshot_load": (i32, [ctypes.c_char_p, P(ctypes.c_void_p)]),
+    "kbg_snapshot_blob_get": (P(kbg_snapshot), [ctypes.c_void_p]),
+    "kbg_snapshot_blob_free": (None, [ctypes.c_void_p]),
 }
 
 _lib = None

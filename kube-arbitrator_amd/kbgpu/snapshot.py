@@ -246,3 +246,44 @@ class FlatSnapshot:
         snap.pod_terms, snap.n_pod_terms = ptr(A["pod_terms"], _abi.kbg_pod_term), len(pterms)
         snap.pod_labels, snap.n_pod_labels = ptr(A["pod_labels"], ctypes.c_int32), len(plabels) // 2
         self.snap = snap
+
+
+# ---- wire format (include/kbgpu.h "Snapshot wire format")
+def encode(snap):
+    """The kbg_snapshot `snap` as the library's wire-format bytes."""
+    L = _abi.lib()
+    n = ctypes.c_int64(0)
+    _abi.check(L.kbg_snapshot_encode(ctypes.byref(snap), None, 0, ctypes.byref(n)))
+    buf = (ctypes.c_uint8 * max(1, n.value))()
+    _abi.check(L.kbg_snapshot_encode(ctypes.byref(snap), buf, n.value, ctypes.byref(n)))
+    return bytes(buf[:n.value])
+
+
+class SnapshotBlob:
+    """A decoded wire-format snapshot owned by the library; .snap is the
+    kbg_snapshot to hand to kbg_session_open."""
+
+    def __init__(self, handle):
+        self.handle = handle
+        self.snap = _abi.lib().kbg_snapshot_blob_get(handle).contents
+
+    @classmethod
+    def decode(cls, data):
+        h = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+        _abi.check(_abi.lib().kbg_snapshot_decode(buf, len(data), ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def load(cls, path):
+        h = ctypes.c_void_p()
+        _abi.check(_abi.lib().kbg_snapshot_load(str(path).encode(), ctypes.byref(h)))
+        return cls(h)
+
+    def close(self):
+        if self.handle:
+            _abi.lib().kbg_snapshot_blob_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()

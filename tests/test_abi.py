@@ -14,7 +14,8 @@ HEADER = os.path.join(ROOT, "include", "kbgpu.h")
 
 def declared_functions():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:kbg_status|int32_t|const char\*|void)\s+(kbg_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:kbg_status|int32_t|const char\*|const kbg_snapshot\*|void)\s+(kbg_\w+)\s*\(",
+                                 txt, re.M)))
 
 
 def test_header_declares_functions():
@@ -28,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for fn in declared_functions():
         assert hasattr(L, fn), fn
     assert set(declared_functions()) == set(_abi.SIGNATURES)
-    assert L.kbg_abi_version() == _abi.ABI_VERSION == 6
+    assert L.kbg_abi_version() == _abi.ABI_VERSION == 7
     assert L.kbg_device_count() >= 0
 
 
