@@ -799,6 +799,7 @@ struct Session {  // framework/session.go:35-61
   std::vector<std::pair<std::string, std::string>> binds;  // (ns/name, node) in dispatch order
   int64_t predicate_calls = 0;
   int threads = 1;  // > 1: allocate's node loop evaluated in parallel blocks (B-omp CPU baseline only)
+  size_t min_parallel_nodes = 512;  // B-omp: smaller clusters walk the nodes on one thread
   std::vector<TaskInfo*> evaluated;  // every task whose node loop ran, in order
 
   // session_plugins.go:142-156
@@ -1594,7 +1595,9 @@ static void allocate_execute(Session* ssn) {
       ssn->evaluated.push_back(task);
       bool assigned = false;
       if (!job->nodesFitDelta.empty()) job->nodesFitDelta.clear();
-      if (ssn->threads > 1) {  // B-omp: the same loop, predicates evaluated in parallel blocks
+      // B-omp: the same loop, predicates evaluated in parallel blocks; below
+      // min_parallel_nodes a fork/join per task costs more than the whole walk
+      if (ssn->threads > 1 && ssn->nodes.size() >= ssn->min_parallel_nodes) {
         if (threaded_node_loop(ssn, job, task)) { jobs->Push(job); break; }
         continue;
       }
@@ -1907,6 +1910,7 @@ static void reorder(std::vector<T*>& v, const Value* order, std::function<std::s
   v = out;
 }
 
+size_t g_min_parallel_nodes = 512;  // kbref --min-parallel-nodes
 static std::string run_session(const Value& fx, bool faithful, bool no_cache, int threads) {
   World w;
   std::string defaultQueue;
@@ -2014,6 +2018,7 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache, in
   Predicates preds;
   preds.faithful_scan = faithful;
   ssn->threads = std::max(1, threads);
+  ssn->min_parallel_nodes = g_min_parallel_nodes;
   // OnSessionOpen in plugin registration (tier) order; the plugins touch disjoint state.
   std::set<std::string> opened;
   for (auto& tier : ssn->tiers)
@@ -2186,11 +2191,12 @@ int main(int argc, char** argv) {
     if (a == "--faithful") faithful = true;
     else if (a == "--no-cache") no_cache = true;
     else if (a == "--threads" && i + 1 < argc) threads = std::atoi(argv[++i]);
+    else if (a == "--min-parallel-nodes" && i + 1 < argc) ref::g_min_parallel_nodes = std::atol(argv[++i]);
     else if (a == "-o" && i + 1 < argc) out = argv[++i];
     else in = a;
   }
   if (in.empty()) {
-    fprintf(stderr, "usage: kbref [--faithful] [--no-cache] [--threads N] fixture.json [-o out.json]\n");
+    fprintf(stderr, "usage: kbref [--faithful] [--no-cache] [--threads N] [--min-parallel-nodes N] fixture.json [-o out.json]\n");
     return 2;
   }
   std::string result;

@@ -65,7 +65,7 @@ def test_threaded_oracle_matches_single_thread():
     fxs = [synth.random_fixture(s) for s in range(0, 60, 3)] + [synth.affinity_fixture(s) for s in range(0, 30, 3)]
     for fx in fxs:
         outs = []
-        for flags in ([], ["--threads", "4"]):
+        for flags in ([], ["--threads", "4", "--min-parallel-nodes", "0"], ["--threads", "4"]):
             with tempfile.TemporaryDirectory() as d:
                 src, dst = os.path.join(d, "fx.json"), os.path.join(d, "out.json")
                 with open(src, "w") as f:
@@ -75,4 +75,4 @@ def test_threaded_oracle_matches_single_thread():
                     o = json.load(f)
             o.pop("stats", None)
             outs.append(o)
-        assert outs[0] == outs[1], fx["name"]
+        assert outs[0] == outs[1] == outs[2], fx["name"]
