@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KBG_ABI_VERSION 7
+#define KBG_ABI_VERSION 8
 
 typedef enum kbg_status {
   KBG_OK = 0,
@@ -101,6 +101,11 @@ typedef struct kbg_node {
   int32_t task_off, task_len;   /* the session-job tasks in NodeInfo.Tasks, in its (insertion) order:
                                    node_tasks[task_off ..] are indices into tasks. preempt/reclaim
                                    take victims in this order (preempt.go:199-206, reclaim.go:113-126) */
+  int32_t key_off, key_len;     /* the keys of NodeInfo.Tasks (PodKey "<ns>/<name>", api/helpers.go:27-33)
+                                   of EVERY pod on the node, session job or not: node_pod_keys[key_off ..],
+                                   string ids; key_len == num_tasks. A placement whose pod key is already
+                                   there is logged but leaves the node unchanged (AddTask's "already on
+                                   node" error, node_info.go:101-106) */
 } kbg_node;
 
 /* One v1.ContainerPort as HostPortInfo sees it (vendor cache/host_ports.go). */
@@ -138,6 +143,8 @@ typedef struct kbg_task {
   kbg_resource resreq;
   int32_t spec;      /* index into specs (the pod's predicate inputs) */
   int32_t node_name; /* string id of TaskInfo.NodeName */
+  int32_t pod_key;   /* string id of PodKey(task.Pod) = "<namespace>/<name>" (the NodeInfo.Tasks key) */
+  int32_t reserved;
 } kbg_task;
 
 /* Predicate-relevant part of a pod spec (predicates.go:121-201). */
@@ -209,6 +216,7 @@ typedef struct kbg_snapshot {
   const int32_t* node_tasks;       int32_t n_node_tasks;
   const kbg_pod_term* pod_terms;   int32_t n_pod_terms;
   const int32_t* pod_labels;       int32_t n_pod_labels;  /* 2*n_pod_labels ints */
+  const int32_t* node_pod_keys;    int32_t n_node_pod_keys;
 } kbg_snapshot;
 
 typedef struct kbg_options {
@@ -289,6 +297,9 @@ typedef struct kbg_stats {
   double victim_kernel_ms; /* victim-scan kernel time: HIP-event time of every 16th launch x launches / timed */
   int64_t victim_tries;    /* reclaimer / preemptor tasks tried (a scan, or the kept stop maps) */
   int64_t victim_host_evals; /* nodes re-evaluated on the host after a change since the last scan */
+  int64_t task_evaluations;  /* node-loop runs of the reference (allocate.go:105-171: every task popped,
+                                placed or not) in the last kbg_allocate: SURVEY §8(d)'s unit */
+  int64_t reserved_stats[7];
 } kbg_stats;
 
 typedef struct kbg_session kbg_session;
@@ -394,16 +405,19 @@ kbg_status kbg_stats_get(kbg_session* s, kbg_stats* out);
 void kbg_session_close(kbg_session* s);
 
 /* Snapshot wire format: the flat kbg_snapshot as one
- * little-endian byte string — the header "KBGS", format version, ABI
- * version, the 20 counts of kbg_snapshot in declaration order, then every
+ * little-endian byte string — the header "KBGS", format version, layout
+ * word (a hash of every snapshot struct's size: blobs survive ABI bumps that
+ * leave those structs unchanged), the 21 counts of kbg_snapshot in
+ * declaration order, then every
  * string as (uint32 length, bytes) and every array as its raw struct bytes in
  * declaration order. A cache adapter builds it once per scheduling cycle (or a
  * recorder keeps it for replay); decoding rebuilds the arrays in library-owned
  * memory, validates them as kbg_session_open does, and the snapshot it hands
- * back opens sessions unchanged.
+ * back opens sessions unchanged. Counts are checked against the input length
+ * before anything is allocated, so a corrupt blob is KBG_E_INVALID.
  * kbg_snapshot_encode with out == NULL / cap == 0 stores the size in *n_out. */
 typedef struct kbg_snapshot_blob kbg_snapshot_blob;
-#define KBG_SNAPSHOT_FORMAT 1
+#define KBG_SNAPSHOT_FORMAT 2
 kbg_status kbg_snapshot_encode(const kbg_snapshot* snap, uint8_t* out, int64_t cap, int64_t* n_out);
 kbg_status kbg_snapshot_decode(const uint8_t* data, int64_t n, kbg_snapshot_blob** out);
 kbg_status kbg_snapshot_save(const kbg_snapshot* snap, const char* path);

@@ -743,13 +743,28 @@ void add_ports(Session& S, int32_t c, int32_t nd) {
   }
 }
 
-void mirror_add(Session& S, int32_t t, int32_t nd, int32_t kind) {
-  if (!S.nil_node[nd]) {
-    if (kind == KBG_KIND_ALLOCATE) kbg::res_sub(S.idle[nd], S.treq[t]);
-    else kbg::res_sub(S.rel[nd], S.treq[t]);
+// NodeInfo.Tasks already holds the task's PodKey (node_info.go:101-106)
+inline int64_t node_key_of(const Session& S, int32_t t, int32_t nd) {
+  return ((int64_t)nd << 32) | (uint32_t)S.task_key[t];
+}
+bool node_has_key(const Session& S, int32_t t, int32_t nd) {
+  return S.has_dupkeys && S.key_hot[S.task_key[t]] && S.node_keys.count(node_key_of(S, t, nd)) != 0;
+}
+
+// Returns true when the node already held the task's pod key: the decision
+// stands, the node is unchanged (AddTask's error), the pod is not among
+// node.Pods() (ports), but it is an Allocated pod of its job (the podLister).
+bool mirror_add(Session& S, int32_t t, int32_t nd, int32_t kind) {
+  const bool dup = node_has_key(S, t, nd);
+  if (!dup) {
+    if (!S.nil_node[nd]) {
+      if (kind == KBG_KIND_ALLOCATE) kbg::res_sub(S.idle[nd], S.treq[t]);
+      else kbg::res_sub(S.rel[nd], S.treq[t]);
+    }
+    S.ntasks[nd]++;
+    if (S.has_ports) add_ports(S, S.task_class[t], nd);
+    if (S.has_dupkeys && S.key_hot[S.task_key[t]]) S.node_keys.insert(node_key_of(S, t, nd));
   }
-  S.ntasks[nd]++;
-  if (S.has_ports) add_ports(S, S.task_class[t], nd);
   // an Allocated pod joins the podLister (api/helpers.go:63-70); Pipelined does not
   if (S.has_aff && kind == KBG_KIND_ALLOCATE) {
     static const bool prof = getenv("KBG_PROFILE_AFF") != nullptr;
@@ -760,6 +775,42 @@ void mirror_add(Session& S, int32_t t, int32_t nd, int32_t kind) {
       S.affm->prof_calls++;
     }
   }
+  return dup;
+}
+
+// Which pod keys can collide: a candidate task's key that another candidate
+// shares or that some node already holds (a StatefulSet pod recreated while
+// its predecessor is still on a node). Usually none: then nothing is tracked.
+void setup_pod_keys(Session& S, const kbg_snapshot* snap) {
+  S.task_key.resize(S.n_tasks);
+  for (int32_t t = 0; t < S.n_tasks; ++t) S.task_key[t] = S.canon[S.tasks_in[t].pod_key];
+  S.key_hot.assign(S.strs.size(), 0);
+  S.has_dupkeys = false;
+  S.node_keys.clear();
+  std::vector<uint8_t> seen(S.strs.size(), 0);
+  for (int32_t t = 0; t < S.n_tasks; ++t) {
+    if (!S.pending_candidate[t] && !S.be_task[t]) continue;
+    uint8_t& c = seen[S.task_key[t]];
+    if (c) S.key_hot[S.task_key[t]] = 1;
+    c = 1;
+  }
+  for (int32_t n = 0; n < S.n_nodes; ++n) {
+    const kbg_node& nd = S.nodes_in[n];
+    for (int32_t i = 0; i < nd.key_len; ++i) {
+      const int32_t k = S.canon[snap->node_pod_keys[nd.key_off + i]];
+      if (seen[k]) S.key_hot[k] = 1;
+    }
+  }
+  for (int32_t t = 0; t < S.n_tasks && !S.has_dupkeys; ++t) S.has_dupkeys = S.key_hot[S.task_key[t]] != 0;
+  if (S.has_dupkeys)
+    for (int32_t n = 0; n < S.n_nodes; ++n) {
+      const kbg_node& nd = S.nodes_in[n];
+      for (int32_t i = 0; i < nd.key_len; ++i) {
+        const int32_t k = S.canon[snap->node_pod_keys[nd.key_off + i]];
+        if (S.key_hot[k]) S.node_keys.insert(((int64_t)n << 32) | (uint32_t)k);
+      }
+    }
+  S.node_keys0 = S.node_keys;
 }
 
 // Builds the port-atom dictionary (distinct sanitized (ip, protocol, port)
@@ -847,6 +898,18 @@ kbg_status validate(const kbg_snapshot* s) {
   auto in = [](int32_t v, int32_t n) { return v >= 0 && v < n; };
   auto range = [](int32_t off, int32_t len, int32_t n) { return off >= 0 && len >= 0 && (int64_t)off + len <= n; };
   if (s->n_strings < 0 || (s->n_strings > 0 && !s->strings)) return fail(KBG_E_INVALID, "strings");
+  {  // every count non-negative, every non-empty array present (encode must never emit an unreadable blob)
+    const std::pair<const void*, int32_t> arrays[] = {
+        {s->nodes, s->n_nodes},         {s->jobs, s->n_jobs},           {s->queues, s->n_queues},
+        {s->tasks, s->n_tasks},         {s->others, s->n_others},       {s->specs, s->n_specs},
+        {s->terms, s->n_terms},         {s->reqs, s->n_reqs},           {s->values, s->n_values},
+        {s->tolerations, s->n_tolerations}, {s->labels, s->n_labels},   {s->taints, s->n_taints},
+        {s->selectors, s->n_selectors}, {s->plugins, s->n_plugins},     {s->tier_sizes, s->n_tiers},
+        {s->ports, s->n_ports},         {s->node_tasks, s->n_node_tasks}, {s->pod_terms, s->n_pod_terms},
+        {s->pod_labels, s->n_pod_labels}, {s->node_pod_keys, s->n_node_pod_keys}};
+    for (const auto& a : arrays)
+      if (a.second < 0 || (a.second > 0 && !a.first)) return fail(KBG_E_INVALID, "negative count or null array");
+  }
   for (int32_t i = 0; i < s->n_strings; ++i)
     if (!s->strings[i]) return fail(KBG_E_INVALID, "null string " + std::to_string(i));
   const int32_t NS = s->n_strings;
@@ -870,7 +933,8 @@ kbg_status validate(const kbg_snapshot* s) {
     if (!in(s->jobs[i].uid, NS) || !in(s->jobs[i].queue, s->n_queues)) return fail(KBG_E_INVALID, "job " + std::to_string(i));
   for (int32_t i = 0; i < s->n_tasks; ++i) {
     const kbg_task& t = s->tasks[i];
-    if (!in(t.uid, NS) || !in(t.job, s->n_jobs) || !(t.spec == -1 || in(t.spec, s->n_specs)) || !in(t.node_name, NS))
+    if (!in(t.uid, NS) || !in(t.job, s->n_jobs) || !(t.spec == -1 || in(t.spec, s->n_specs)) || !in(t.node_name, NS) ||
+        !in(t.pod_key, NS))
       return fail(KBG_E_INVALID, "task " + std::to_string(i));
     if (t.status <= 0 || t.status > KBG_UNKNOWN || (t.status & (t.status - 1))) return fail(KBG_E_INVALID, "task status");
   }
@@ -910,6 +974,13 @@ kbg_status validate(const kbg_snapshot* s) {
       return fail(KBG_E_INVALID, "node task list " + std::to_string(i));
   for (int32_t i = 0; i < s->n_node_tasks; ++i)
     if (!in(s->node_tasks[i], s->n_tasks)) return fail(KBG_E_INVALID, "node task index");
+  for (int32_t i = 0; i < s->n_nodes; ++i) {  // NodeInfo.Tasks keys: one per pod on the node
+    const kbg_node& n = s->nodes[i];
+    if (!range(n.key_off, n.key_len, s->n_node_pod_keys) || n.key_len != n.num_tasks)
+      return fail(KBG_E_INVALID, "node pod keys " + std::to_string(i) + " (key_len must equal num_tasks)");
+  }
+  for (int32_t i = 0; i < s->n_node_pod_keys; ++i)
+    if (!in(s->node_pod_keys[i], NS)) return fail(KBG_E_INVALID, "node pod key string");
   for (int32_t i = 0; i < s->n_ports; ++i)
     if (!in(s->ports[i].host_ip, NS) || !in(s->ports[i].protocol, NS)) return fail(KBG_E_INVALID, "port");
   for (int32_t i = 0; i < s->n_tolerations; ++i) {
@@ -1130,6 +1201,8 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
       S.max_candidates = std::max(S.max_candidates, S.nt_off[n + 1] - S.nt_off[n]);
     }
   }
+
+  setup_pod_keys(S, snap);
 
   // ---- engine initial state
   Engine& E = S.init;
@@ -1463,11 +1536,13 @@ void compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, const 
     while (k > le.before) {
       --k;
       const int32_t n = dec[k].node;
-      if (!S.nil_node[n]) (dec[k].kind == KBG_KIND_ALLOCATE ? idle[n] : rel[n]) = dec_old[k];
-      ntasks[n]--;
-      if (S.has_ports)
-        std::copy(dec_oldp.begin() + (size_t)k * PW, dec_oldp.begin() + (size_t)(k + 1) * PW,
-                  ports.begin() + (size_t)n * PW);
+      if (!S.dec_dup[k]) {  // a decision whose pod key the node held left the node unchanged
+        if (!S.nil_node[n]) (dec[k].kind == KBG_KIND_ALLOCATE ? idle[n] : rel[n]) = dec_old[k];
+        ntasks[n]--;
+        if (S.has_ports)
+          std::copy(dec_oldp.begin() + (size_t)k * PW, dec_oldp.begin() + (size_t)(k + 1) * PW,
+                    ports.begin() + (size_t)n * PW);
+      }
       if (S.has_aff && dec[k].kind == KBG_KIND_ALLOCATE) kbg::aff_place(S, dec[k].task, n, -1, aff, false);
     }
     const int32_t t = le.task;
@@ -1531,6 +1606,8 @@ void begin_cycle(Session& S) {
   S.stats.int_scan = prev.int_scan;
   S.stats.open_ms = prev.open_ms;
   S.dec_action.clear();
+  S.dec_dup.clear();
+  S.node_keys = S.node_keys0;
   S.evictions.clear();
   S.tstat.resize(S.n_tasks);
   for (int32_t t = 0; t < S.n_tasks; ++t) S.tstat[t] = S.tasks_in[t].status;
@@ -1571,21 +1648,23 @@ Engine live_engine(Session& S) {
   return E;
 }
 
-// Appends a decision to the cycle's log (no gang bookkeeping).
-void append_log(Session& S, int32_t t, int32_t node, int32_t kind) {
+// Appends a decision to the cycle's log (no gang bookkeeping). `dup`: the
+// node already held the pod key and was left unchanged.
+void append_log(Session& S, int32_t t, int32_t node, int32_t kind, bool dup = false) {
   S.dec.push_back(kbg_decision{t, node, kind, -1});
   S.undisp_next.push_back(-1);
   S.dec_action.push_back(S.action);
+  S.dec_dup.push_back(dup ? 1 : 0);
 }
 
 // Appends one committed decision to the log and runs the gang part of
 // ssn.Allocate (session.go:283-290): every Allocated task of the job is
 // dispatched when this decision makes the job ready. Pipelined tasks count
 // toward readiness (gang.go:44-55) but never dispatch.
-void record_decision(Session& S, int32_t t, int32_t node, int32_t kind) {
+void record_decision(Session& S, int32_t t, int32_t node, int32_t kind, bool dup) {
   const int32_t j = S.task_job[t];
   const int32_t di = (int32_t)S.dec.size();
-  append_log(S, t, node, kind);
+  append_log(S, t, node, kind, dup);
   S.committed_ready[j]++;
   S.tstat[t] = kind == KBG_KIND_ALLOCATE ? KBG_ALLOCATED : KBG_PIPELINED;
   if (kind == KBG_KIND_ALLOCATE) {
@@ -1805,6 +1884,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       }
       const bool ok = node >= 0;
       bactual[i] = ok;
+      S.stats.task_evaluations++;
       const int32_t j = S.task_job[t];
       last[j] = LastEval{t, (int32_t)dec.size(), node, kind};
       if (ok) {
@@ -1812,12 +1892,12 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         if (S.has_ports)
           dec_oldp.insert(dec_oldp.end(), S.node_ports.begin() + (size_t)node * S.PW,
                           S.node_ports.begin() + (size_t)(node + 1) * S.PW);
-        mirror_add(S, t, node, kind);
+        const bool dup = mirror_add(S, t, node, kind);
         if (mark[node] != stamp) {
           mark[node] = stamp;
           touched.push_back(node);
         }
-        record_decision(S, t, node, kind);
+        record_decision(S, t, node, kind, dup);
       } else {
         failed[S.task_shape[t]].store(1, std::memory_order_relaxed);
       }
@@ -1943,12 +2023,13 @@ kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       }
       if (node < 0) continue;  // no node passes the predicates: the task stays Pending
       // ssn.Allocate -> NodeInfo.AddTask -> Idle.Sub panics when even the
-      // tolerance does not cover the request (resource_info.go:100-110)
-      if (!S.nil_node[node] && !kbg::res_le(S.treq[t], S.idle[node])) {
+      // tolerance does not cover the request (resource_info.go:100-110),
+      // unless AddTask already failed on the pod key (node_info.go:101-106)
+      if (!S.nil_node[node] && !node_has_key(S, t, node) && !kbg::res_le(S.treq[t], S.idle[node])) {
         result = fail(KBG_E_REF_PANIC, "backfill: Resource.Sub underflow on the node's Idle (resource_info.go:100-110)");
         break;
       }
-      mirror_add(S, t, node, KBG_KIND_ALLOCATE);
+      const bool dup = mirror_add(S, t, node, KBG_KIND_ALLOCATE);
       if (mark[node] != stamp) {
         mark[node] = stamp;
         touched.push_back(node);
@@ -1966,7 +2047,7 @@ kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         E.qshare[jq] = share_of(E.qalloc[jq], S.q_deserved[jq]);
       }
       E.jready[j]++;
-      record_decision(S, t, node, KBG_KIND_ALLOCATE);
+      record_decision(S, t, node, KBG_KIND_ALLOCATE, dup);
       if (!S.aff_gain_classes.empty() && i + 1 < cnt) {
         // pod affinity gave a class new nodes: rescan the rest of the batch
         for (int32_t c : S.aff_gain_classes) S.aff_gain_flag[c] = 0;
@@ -2239,13 +2320,18 @@ struct Live {
     return plugins(v, false);
   }
   // job Pipelined, NodeInfo.AddTask as Pipelined, AllocateFunc (session.go:205-241, statement.go:110-151)
-  bool pipeline(int32_t t, int32_t n) {
+  // *dup: the node already held the pod key (node_info.go:101-106): unchanged
+  bool pipeline(int32_t t, int32_t n, bool* dup) {
     const int32_t j = S.task_job[t];
     if (!ready_status(S.tstat[t])) ready(j, +1);
     S.tstat[t] = KBG_PIPELINED;
-    if (!S.nil_node[n] && !kbg::res_sub(S.rel[n], S.treq[t])) return false;  // node_info.go:117-118
-    S.ntasks[n]++;
-    touch(n);
+    *dup = node_has_key(S, t, n);
+    if (!*dup) {
+      if (!S.nil_node[n] && !kbg::res_sub(S.rel[n], S.treq[t])) return false;  // node_info.go:117-118
+      S.ntasks[n]++;
+      if (S.has_dupkeys && S.key_hot[S.task_key[t]]) S.node_keys.insert(node_key_of(S, t, n));
+      touch(n);
+    }
     return plugins(t, true);
   }
   // statement.go:81-108: job Running again; node.AddTask fails (the task is
@@ -2263,6 +2349,7 @@ struct Live {
     S.tstat[t] = KBG_PENDING;
     if (!S.nil_node[n]) kbg::res_add(S.rel[n], S.treq[t]);  // node_info.go:145-146
     S.ntasks[n]--;
+    if (S.has_dupkeys && S.key_hot[S.task_key[t]]) S.node_keys.erase(node_key_of(S, t, n));
     touch(n);
     return plugins(t, false);
   }
@@ -2351,6 +2438,7 @@ struct Stmt {
   struct Op {
     bool evict;
     int32_t task, node, by;
+    bool dup;  // a pipeline the node's pod key table refused (the node is unchanged)
   };
   std::vector<Op> ops;
 };
@@ -2463,15 +2551,16 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
     return fail(KBG_E_INVALID, "internal: device and host victim validation disagree");
   Res resreq = req;
   for (int32_t v : victims) {
-    if (stmt) stmt->ops.push_back({true, v, -1, t});
+    if (stmt) stmt->ops.push_back({true, v, -1, t, false});
     else S.evictions.push_back(kbg_eviction{v, t, S.action, 0});
     if (!L.evict(v)) return fail(KBG_E_REF_PANIC, "eviction: Resource.Sub underflow (resource_info.go:100-110)");
     if (kbg::res_le(resreq, S.treq[v])) break;  // preempt.go:221-224
     if (!kbg::res_sub(resreq, S.treq[v])) return fail(KBG_E_REF_PANIC, "preempt: resreq.Sub underflow (preempt.go:225)");
   }
-  if (!L.pipeline(t, n)) return fail(KBG_E_REF_PANIC, "pipeline: Releasing.Sub underflow (node_info.go:117-118)");
-  if (stmt) stmt->ops.push_back({false, t, n, -1});
-  else append_log(S, t, n, KBG_KIND_PIPELINE);
+  bool dup = false;
+  if (!L.pipeline(t, n, &dup)) return fail(KBG_E_REF_PANIC, "pipeline: Releasing.Sub underflow (node_info.go:117-118)");
+  if (stmt) stmt->ops.push_back({false, t, n, -1, dup});
+  else append_log(S, t, n, KBG_KIND_PIPELINE, dup);
   (void)clk::now();
   *outcome = TRY_ASSIGNED;
   return KBG_OK;
@@ -2480,20 +2569,24 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
 void stmt_commit(Session& S, Stmt& stmt) {  // statement.go:207-217
   for (auto& op : stmt.ops) {
     if (op.evict) S.evictions.push_back(kbg_eviction{op.task, op.by, S.action, 0});
-    else append_log(S, op.task, op.node, KBG_KIND_PIPELINE);
+    else append_log(S, op.task, op.node, KBG_KIND_PIPELINE, op.dup);
   }
   stmt.ops.clear();
 }
 
-bool stmt_discard(Session& S, Live& L, Stmt& stmt) {  // statement.go:194-205
+kbg_status stmt_discard(Session& S, Live& L, Stmt& stmt) {  // statement.go:194-205
   bool ok = true;
+  for (const Stmt::Op& op : stmt.ops)
+    if (!op.evict && op.dup)  // unpipeline's RemoveTask would drop the pod that held the key
+      return fail(KBG_E_UNSUPPORTED, "statement discard of a pipeline whose pod key was already on the node "
+                                     "(node_info.go:131-157 removes the other pod): run the reference path");
   for (size_t k = stmt.ops.size(); k-- > 0;) {
     const Stmt::Op& op = stmt.ops[k];
     if (op.evict) L.unevict(op.task);
     else ok = L.unpipeline(op.task, op.node) && ok;
   }
   stmt.ops.clear();
-  return ok;
+  return ok ? KBG_OK : fail(KBG_E_REF_PANIC, "statement discard: DeallocateFunc Sub underflow (resource_info.go:100-110)");
 }
 
 // Per job, its Pending tasks in TaskOrderFn order (a strict order, so the
@@ -2663,8 +2756,7 @@ kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
           }
         }
         if (!job_ready(pj)) {
-          if (!stmt_discard(S, R.L, stmt))
-            return fail(KBG_E_REF_PANIC, "statement discard: DeallocateFunc Sub underflow (resource_info.go:100-110)");
+          if ((s2 = stmt_discard(S, R.L, stmt)) != KBG_OK) return s2;
           if ((s2 = R.sync()) != KBG_OK) return s2;
           continue;
         }
@@ -2849,6 +2941,7 @@ kbg_status kbg_session_reset(kbg_session* s) {
   S.rel = S.rel0;
   S.ntasks = S.ntasks0;
   S.allocated = S.backfilled = S.reclaimed = S.preempted = S.cycle_started = false;
+  S.node_keys = S.node_keys0;
   if (S.has_ports || S.has_aff) {  // the class masks carry the port fit / affinity: back to the snapshot's
     S.node_ports = S.node_ports0;
     S.h_class_mask = S.h_class_mask0;
@@ -3010,7 +3103,23 @@ struct kbg_snapshot_blob {
 namespace {
 
 constexpr char kSnapMagic[4] = {'K', 'B', 'G', 'S'};
-constexpr int kSnapCounts = 20;
+constexpr int kSnapCounts = 21;
+
+// Layout word of the wire format: a hash of the element size of every array
+// (FNV-1a over the sizes). Blobs stay readable across ABI bumps that leave the
+// snapshot structs unchanged; a struct change makes old blobs fail loudly.
+uint32_t snapshot_layout() {
+  const size_t sizes[] = {sizeof(kbg_node), sizeof(kbg_job), sizeof(kbg_queue), sizeof(kbg_task),
+                          sizeof(kbg_resource), sizeof(kbg_spec), sizeof(kbg_term), sizeof(kbg_requirement),
+                          sizeof(kbg_toleration), sizeof(kbg_taint), sizeof(kbg_plugin_option),
+                          sizeof(kbg_host_port), sizeof(kbg_pod_term)};
+  uint32_t h = 2166136261u;
+  for (size_t v : sizes) {
+    h ^= (uint32_t)v;
+    h *= 16777619u;
+  }
+  return h;
+}
 
 // The arrays of a kbg_snapshot in declaration order: (pointer slot, count
 // slot, element size, elements per count).
@@ -3035,6 +3144,7 @@ void for_each_array(kbg_snapshot& s, F f) {
   f((const void**)&s.node_tasks, &s.n_node_tasks, sizeof(int32_t), 1);
   f((const void**)&s.pod_terms, &s.n_pod_terms, sizeof(kbg_pod_term), 1);
   f((const void**)&s.pod_labels, &s.n_pod_labels, sizeof(int32_t), 2);
+  f((const void**)&s.node_pod_keys, &s.n_node_pod_keys, sizeof(int32_t), 1);
 }
 
 struct Writer {
@@ -3053,7 +3163,7 @@ kbg_status encode(const kbg_snapshot* snap, Writer& w) {
   kbg_snapshot s = *snap;
   w.put(kSnapMagic, 4);
   w.u32(KBG_SNAPSHOT_FORMAT);
-  w.u32(KBG_ABI_VERSION);
+  w.u32(snapshot_layout());
   w.u32((uint32_t)s.n_strings);
   for_each_array(s, [&](const void**, int32_t* cnt, size_t, int) { w.u32((uint32_t)*cnt); });
   for (int32_t i = 0; i < s.n_strings; ++i) {
@@ -3080,48 +3190,52 @@ kbg_status kbg_snapshot_encode(const kbg_snapshot* snap, uint8_t* out, int64_t c
   return KBG_OK;
 }
 
-kbg_status kbg_snapshot_decode(const uint8_t* data, int64_t n, kbg_snapshot_blob** out) {
-  if (!data || !out || n < 0) return fail(KBG_E_INVALID, "null argument");
-  *out = nullptr;
+static kbg_status snapshot_decode(const uint8_t* data, int64_t n, kbg_snapshot_blob** out) {
   int64_t pos = 0;
   auto take = [&](void* dst, int64_t len) {
-    if (len < 0 || pos + len > n) return false;
-    std::memcpy(dst, data + pos, (size_t)len);
+    if (len < 0 || len > n - pos) return false;
+    if (len > 0) std::memcpy(dst, data + pos, (size_t)len);
     pos += len;
     return true;
   };
   char magic[4];
-  uint32_t fmt = 0, abi = 0, nstr = 0;
+  uint32_t fmt = 0, layout = 0, nstr = 0;
   if (!take(magic, 4) || std::memcmp(magic, kSnapMagic, 4) != 0) return fail(KBG_E_INVALID, "not a kbg snapshot");
-  if (!take(&fmt, 4) || !take(&abi, 4) || fmt != KBG_SNAPSHOT_FORMAT || abi != KBG_ABI_VERSION)
-    return fail(KBG_E_INVALID, "snapshot format " + std::to_string(fmt) + " / ABI " + std::to_string(abi) +
+  if (!take(&fmt, 4) || !take(&layout, 4) || fmt != KBG_SNAPSHOT_FORMAT || layout != snapshot_layout())
+    return fail(KBG_E_INVALID, "snapshot format " + std::to_string(fmt) + " / layout " + std::to_string(layout) +
                                    " (this library: " + std::to_string(KBG_SNAPSHOT_FORMAT) + " / " +
-                                   std::to_string(KBG_ABI_VERSION) + ")");
+                                   std::to_string(snapshot_layout()) + ")");
   if (!take(&nstr, 4) || nstr > (uint32_t)INT32_MAX) return fail(KBG_E_INVALID, "truncated snapshot header");
   auto blob = std::make_unique<kbg_snapshot_blob>();
   kbg_snapshot& s = blob->snap;
   s.n_strings = (int32_t)nstr;
   bool ok = true;
-  for_each_array(s, [&](const void**, int32_t* cnt, size_t, int) {
+  int64_t array_bytes = 0;  // what the counts promise, checked against the input before any allocation
+  for_each_array(s, [&](const void**, int32_t* cnt, size_t size, int per) {
     uint32_t v = 0;
     ok = ok && take(&v, 4) && v <= (uint32_t)INT32_MAX;
     *cnt = (int32_t)v;
+    array_bytes += (int64_t)v * per * (int64_t)size;
   });
   if (!ok) return fail(KBG_E_INVALID, "truncated snapshot header");
+  // every string takes at least its 4-byte length; every array its raw bytes
+  if ((int64_t)nstr * 4 > n - pos || array_bytes > n - pos - (int64_t)nstr * 4)
+    return fail(KBG_E_INVALID, "snapshot counts exceed the input");
   blob->strs.resize(nstr);
   for (uint32_t i = 0; i < nstr; ++i) {
     uint32_t len = 0;
-    if (!take(&len, 4) || pos + (int64_t)len > n) return fail(KBG_E_INVALID, "truncated snapshot strings");
+    if (!take(&len, 4) || (int64_t)len > n - pos) return fail(KBG_E_INVALID, "truncated snapshot strings");
     blob->strs[i].assign((const char*)data + pos, len);
     pos += len;
   }
   blob->ptrs.resize(nstr);
   for (uint32_t i = 0; i < nstr; ++i) blob->ptrs[i] = blob->strs[i].c_str();
   s.strings = blob->ptrs.data();
+  if (array_bytes != n - pos) return fail(KBG_E_INVALID, "snapshot arrays do not match the input length");
   blob->arrays.reserve(kSnapCounts);
   for_each_array(s, [&](const void** ptr, int32_t* cnt, size_t size, int per) {
     const int64_t len = (int64_t)*cnt * per * (int64_t)size;
-    blob->arrays.emplace_back((size_t)std::max<int64_t>(len, 0));
+    blob->arrays.emplace_back((size_t)len);
     std::vector<uint8_t>& a = blob->arrays.back();
     ok = ok && take(a.data(), len);
     *ptr = *cnt > 0 ? a.data() : nullptr;
@@ -3132,6 +3246,18 @@ kbg_status kbg_snapshot_decode(const uint8_t* data, int64_t n, kbg_snapshot_blob
   if (st != KBG_OK) return st;
   *out = blob.release();
   return KBG_OK;
+}
+
+kbg_status kbg_snapshot_decode(const uint8_t* data, int64_t n, kbg_snapshot_blob** out) {
+  if (!data || !out || n < 0) return fail(KBG_E_INVALID, "null argument");
+  *out = nullptr;
+  try {
+    return snapshot_decode(data, n, out);
+  } catch (const std::bad_alloc&) {
+    return fail(KBG_E_NOMEM, "host allocation failed");
+  } catch (const std::length_error&) {
+    return fail(KBG_E_INVALID, "snapshot counts exceed the input");
+  }
 }
 
 kbg_status kbg_snapshot_save(const kbg_snapshot* snap, const char* path) {

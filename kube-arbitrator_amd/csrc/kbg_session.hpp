@@ -5,6 +5,7 @@
 #include <memory>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/kbgpu.h"
@@ -279,6 +280,16 @@ struct Session {
   int32_t mstamp = 0;                          // the current batch stamp
   std::vector<uint8_t> aff_gain_flag;          // per class: gained nodes since the last cut
   std::vector<int32_t> aff_gain_classes;
+
+  // ---- NodeInfo.Tasks keys (node_info.go:101-106): AddTask of a PodKey the
+  // node already holds returns an error and leaves the node unchanged, while
+  // ssn.Allocate / ssn.Pipeline still log the decision and run the handlers
+  // (session.go:205-293). Only keys that can collide are tracked.
+  std::vector<int32_t> task_key;                      // canonical string id of each task's PodKey
+  bool has_dupkeys = false;                           // some candidate task's key can meet itself on a node
+  std::vector<uint8_t> key_hot;                       // per canonical string id: a colliding key
+  std::unordered_set<int64_t> node_keys, node_keys0;  // (node << 32 | key) of hot keys on nodes (now / at open)
+  std::vector<uint8_t> dec_dup;                       // per decision of the cycle: the node was left unchanged
 
   // ---- device
   int32_t device = 0;

@@ -35,7 +35,7 @@ DISABLE_RECLAIMABLE = 1 << 4
 DISABLE_QUEUE_ORDER = 1 << 5
 DISABLE_PREDICATE = 1 << 6
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 COMM_ID_BYTES = 128
 
 KIND_ALLOCATE = 0
@@ -55,7 +55,8 @@ class kbg_node(ctypes.Structure):
     _fields_ = [("name", i32), ("has_node", i32), ("allocatable", kbg_resource), ("idle", kbg_resource),
                 ("releasing", kbg_resource), ("max_task_num", i32), ("num_tasks", i32), ("unschedulable", i32),
                 ("label_off", i32), ("label_len", i32), ("taint_off", i32), ("taint_len", i32),
-                ("port_off", i32), ("port_len", i32), ("task_off", i32), ("task_len", i32)]
+                ("port_off", i32), ("port_len", i32), ("task_off", i32), ("task_len", i32),
+                ("key_off", i32), ("key_len", i32)]
 
 
 class kbg_host_port(ctypes.Structure):
@@ -76,7 +77,7 @@ class kbg_queue(ctypes.Structure):
 
 class kbg_task(ctypes.Structure):
     _fields_ = [("uid", i32), ("job", i32), ("status", i32), ("priority", i32), ("resreq", kbg_resource),
-                ("spec", i32), ("node_name", i32)]
+                ("spec", i32), ("node_name", i32), ("pod_key", i32), ("reserved", i32)]
 
 
 class kbg_spec(ctypes.Structure):
@@ -130,6 +131,7 @@ class kbg_snapshot(ctypes.Structure):
         ("node_tasks", P(i32)), ("n_node_tasks", i32),
         ("pod_terms", P(kbg_pod_term)), ("n_pod_terms", i32),
         ("pod_labels", P(i32)), ("n_pod_labels", i32),
+        ("node_pod_keys", P(i32)), ("n_node_pod_keys", i32),
     ]
 
 
@@ -164,7 +166,8 @@ class kbg_stats(ctypes.Structure):
                 ("device_ms", f64), ("delta_ms", f64), ("replayed", i64), ("n_classes", i32), ("shards", i32), ("shard_index", i32),
                 ("int_scan", i32), ("exchange_ms", f64), ("backfill_ms", f64),
                 ("reclaim_ms", f64), ("preempt_ms", f64), ("victim_scans", i64), ("victim_kernel_ms", f64),
-                ("victim_tries", i64), ("victim_host_evals", i64)]
+                ("victim_tries", i64), ("victim_host_evals", i64), ("task_evaluations", i64),
+                ("reserved_stats", i64 * 7)]
 
 
 class kbg_eviction(ctypes.Structure):

@@ -10,7 +10,7 @@ import json
 import numpy as np
 
 from . import _abi
-from .api import PENDING
+from .api import PENDING, pod_key
 
 
 class Interner:
@@ -64,7 +64,7 @@ class FlatSnapshot:
             qs[i].weight = q.weight
         # nodes
         nd = np.zeros(len(nodes), dtype=np.dtype(_abi.kbg_node))
-        labels, taints, ports = [], [], []
+        labels, taints, ports, node_keys = [], [], [], []
         for i, n in enumerate(nodes):
             obj = n.node or {}
             r = nd[i]
@@ -94,6 +94,10 @@ class FlatSnapshot:
             for ip, proto, port in used:
                 ports.append((S(ip), S(proto), port))
             r["port_len"] = len(ports) - r["port_off"]
+            # NodeInfo.Tasks keys (PodKey) of every pod on the node, in order
+            r["key_off"] = len(node_keys)
+            node_keys.extend(S(k) for k in n.tasks.keys())
+            r["key_len"] = len(node_keys) - r["key_off"]
         self.node_names = [n.name for n in nodes]
         # jobs + tasks + specs (node task lists are filled once task indices exist)
         jb = np.zeros(len(jobs), dtype=np.dtype(_abi.kbg_job))
@@ -178,7 +182,8 @@ class FlatSnapshot:
             r["priority"] = job.priority
             r["creation_ns"] = job.creation_timestamp
             for t in job.tasks.values():
-                task_rows.append((S(t.uid), j, t.status, t.priority, t.resreq.as_tuple(), spec_of(t.pod), S(t.node_name)))
+                task_rows.append((S(t.uid), j, t.status, t.priority, t.resreq.as_tuple(), spec_of(t.pod), S(t.node_name),
+                                  S(pod_key(t.pod)), 0))
                 self.task_objs.append(t)
         # NodeInfo.Tasks order of the session-job tasks on each node (preempt/reclaim victims)
         task_index = {t.uid: i for i, t in enumerate(self.task_objs)}
@@ -215,7 +220,8 @@ class FlatSnapshot:
             selectors=np.asarray(selectors or [0, 0], dtype=np.int32),
             plugins=arr(_abi.kbg_plugin_option, plugin_rows), tier_sizes=np.asarray(tier_sizes or [0], dtype=np.int32),
             ports=arr(_abi.kbg_host_port, ports), node_tasks=np.asarray(node_tasks or [0], dtype=np.int32),
-            pod_terms=arr(_abi.kbg_pod_term, pterms), pod_labels=np.asarray(plabels or [0, 0], dtype=np.int32))
+            pod_terms=arr(_abi.kbg_pod_term, pterms), pod_labels=np.asarray(plabels or [0, 0], dtype=np.int32),
+            node_pod_keys=np.asarray(node_keys or [0], dtype=np.int32))
         A = self.arrays
 
         def ptr(a, ctype):
@@ -245,6 +251,7 @@ class FlatSnapshot:
         snap.node_tasks, snap.n_node_tasks = ptr(A["node_tasks"], ctypes.c_int32), len(node_tasks)
         snap.pod_terms, snap.n_pod_terms = ptr(A["pod_terms"], _abi.kbg_pod_term), len(pterms)
         snap.pod_labels, snap.n_pod_labels = ptr(A["pod_labels"], ctypes.c_int32), len(plabels) // 2
+        snap.node_pod_keys, snap.n_node_pod_keys = ptr(A["node_pod_keys"], ctypes.c_int32), len(node_keys)
         self.snap = snap
 
 
@@ -266,6 +273,9 @@ class SnapshotBlob:
     def __init__(self, handle):
         self.handle = handle
         self.snap = _abi.lib().kbg_snapshot_blob_get(handle).contents
+        # the view points into library-owned memory that close() frees: keep
+        # the owner reachable from the view (`blob.snap` alone stays valid)
+        self.snap._owner = self
 
     @classmethod
     def decode(cls, data):

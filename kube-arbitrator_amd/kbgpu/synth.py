@@ -107,6 +107,53 @@ def config_fixture(cid):
     return {"name": f"C{cid}", "tiers": c["tiers"], "nodes": nodes, "pods": pods, "podGroups": pgs, "queues": queues}
 
 
+def saturated_config(nodes=5000, jobs=2000, tasks_per_job=50, demand=1.08, seed=7):
+    """C3's cluster (not a BASELINE config: the stress case the verdict asks
+    for) with a request drawn per task instead of per job, and total demand
+    about `demand` x the schedulable CPU, so the cluster fills up during the
+    cycle: many (class, request) shapes fail mid-batch at the default K,
+    which cuts batches and replays the ordering engine, and late tasks walk
+    long infeasible prefixes. 10% of the jobs are GPU jobs (1-2 GPUs, tolerate
+    the dedicated taint), 30% carry a zone / type selector."""
+    rng = random.Random(BASE_SEED + 200 + seed)
+    nds = [_node(i, rng, "hetero") for i in range(nodes)]
+    usable = sum(int(n["allocatable"]["cpu"]) * 1000 for n in nds
+                 if not n.get("unschedulable") and n["labels"]["type"] != "gpu")
+    queues = [{"name": q, "weight": w} for q, w in (("q1", 1), ("q2", 2), ("q3", 3), ("q4", 4))]
+    cpus = (250, 500, 1000, 1500, 2000, 3000, 4000, 6000)
+    mems = (0.5, 1, 2, 3, 4, 6, 8, 12, 16)
+    mean_cpu = sum(cpus) / len(cpus)
+    scale = demand * usable / (0.9 * jobs * tasks_per_job * mean_cpu)  # GPU jobs land on the GPU nodes
+    pods, pgs = [], []
+    for j in range(jobs):
+        ns = f"ns{j % 8}"
+        pg = f"pg-{j:05d}"
+        spec = {}
+        r = rng.random()
+        gpu_job = r < 0.10
+        if gpu_job:
+            spec["tolerations"] = [{"key": "dedicated", "operator": "Equal", "value": "gpu", "effect": "NoSchedule"}]
+        elif r < 0.40:
+            spec["nodeSelector"] = ({"zone": f"z{rng.randrange(4)}"} if rng.random() < 0.5
+                                    else {"type": ("cpu", "mem")[rng.randrange(2)]})
+        pgs.append({"namespace": ns, "name": pg, "minMember": (1, 25, 50)[rng.randrange(3)],
+                    "queue": queues[rng.randrange(4)]["name"],
+                    "creationTimestamp": (1_700_000_000 + j) * 1_000_000_000})
+        for t in range(tasks_per_job):
+            cpu = max(100, int(rng.choice(cpus) * scale) // 50 * 50)
+            req = {"cpu": f"{cpu}m", "memory": f"{int(rng.choice(mems) * 1024)}Mi"}
+            if gpu_job:
+                req["nvidia.com/gpu"] = str(rng.choice((1, 1, 2)))
+            p = {"uid": f"uid-{j:05d}-{t:03d}", "namespace": ns, "name": f"{pg}-{t:03d}", "phase": "Pending",
+                 "annotations": {"scheduling.k8s.io/group-name": pg}, "containers": [{"requests": req}]}
+            if rng.random() < 0.2:
+                p["priority"] = rng.choice((5, 10))
+            p.update(spec)
+            pods.append(p)
+    return {"name": f"saturated-{seed}", "tiers": None, "nodes": nds, "pods": pods, "podGroups": pgs,
+            "queues": queues}
+
+
 # ------------------------------------------------------------------ fuzz
 _OPS = ("In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt")
 
@@ -277,6 +324,32 @@ def random_fixture(seed, max_nodes=24, max_jobs=10, max_tasks=8, be_frac=0.06):
         fx["actions"] = ["preempt"]
     elif r < 0.9:
         fx["actions"] = ["reclaim"]
+    return fx
+
+
+def dupkey_fixture(seed, **kw):
+    """random_fixture with colliding pod keys (PodKey = "<ns>/<name>",
+    api/helpers.go:27-33): some Running / deleting pods take the namespace and
+    name of a Pending pod (a StatefulSet pod recreated while its predecessor
+    is still on a node), and some Pending pods share a name with a Pending
+    pod of another job in their namespace. NodeInfo.AddTask refuses a key the
+    node already holds (node_info.go:101-106): the decision is logged, the
+    node is left unchanged."""
+    fx = random_fixture(seed, **kw)
+    rng = random.Random(seed * 7919 + 1)
+    pods = fx["pods"]
+    pending = [p for p in pods if p["phase"] == "Pending"]
+    placed = [p for p in pods if p["phase"] == "Running"]
+    if pending:
+        for p in placed:
+            if rng.random() < 0.6:
+                q = rng.choice(pending)
+                p["namespace"], p["name"] = q["namespace"], q["name"]
+        for _ in range(max(1, len(pending) // 4)):
+            a, b = rng.choice(pending), rng.choice(pending)
+            if a is not b and a["namespace"] == b["namespace"]:
+                b["name"] = a["name"]
+    fx["name"] = f"dupkey-{seed}"
     return fx
 
 

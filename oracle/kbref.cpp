@@ -1559,6 +1559,18 @@ static bool threaded_node_loop(Session* ssn, JobInfo* job, TaskInfo* task) {
   return false;
 }
 
+// kbref --budget SECONDS: stop the actions after this much wall time (CPU
+// baselines that cannot finish, e.g. B-faithful at C2-C4) and report the
+// placements reached; 0 = no budget
+double g_budget_s = 0;
+std::chrono::steady_clock::time_point g_budget_t0;
+struct BudgetExceeded {};
+inline void budget_check(size_t evaluated) {
+  if (g_budget_s <= 0 || (evaluated & 63) != 0) return;
+  if (std::chrono::duration<double>(std::chrono::steady_clock::now() - g_budget_t0).count() > g_budget_s)
+    throw BudgetExceeded{};
+}
+
 // pkg/scheduler/actions/allocate/allocate.go:41-176
 static void allocate_execute(Session* ssn) {
   PriorityQueue<QueueInfo> queues([ssn](QueueInfo* l, QueueInfo* r) { return ssn->QueueOrderFn(l, r); });
@@ -1593,6 +1605,7 @@ static void allocate_execute(Session* ssn) {
     while (!tasks->Empty()) {
       TaskInfo* task = tasks->Pop();
       ssn->evaluated.push_back(task);
+      budget_check(ssn->evaluated.size());
       bool assigned = false;
       if (!job->nodesFitDelta.empty()) job->nodesFitDelta.clear();
       // B-omp: the same loop, predicates evaluated in parallel blocks; below
@@ -2046,6 +2059,8 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache, in
     for (auto& x : a->arr) actions.push_back(x.s);
   }
   auto t0 = std::chrono::steady_clock::now();
+  g_budget_t0 = t0;
+  try {
   for (auto& a : actions) {
     if (a == "allocate") { ssn->action = ""; allocate_execute(ssn); }
     else if (a == "backfill") { ssn->action = "backfill"; backfill_execute(ssn); }
@@ -2054,6 +2069,13 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache, in
     else if (a == "reclaim") { ssn->action = "reclaim"; reclaim_execute(ssn); }
     else if (a == "preempt") { ssn->action = "preempt"; preempt_execute(ssn); }
     else throw BadInput("unsupported action " + a);
+  }
+  } catch (const BudgetExceeded&) {
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return "{\"status\":\"budget\",\"stats\":{\"seconds\":" + kbjson::num(secs) +
+           ",\"predicate_calls\":" + std::to_string(ssn->predicate_calls) +
+           ",\"decisions\":" + std::to_string(ssn->decisions.size()) +
+           ",\"evaluated\":" + std::to_string(ssn->evaluated.size()) + "}}";
   }
   auto t1 = std::chrono::steady_clock::now();
   double secs = std::chrono::duration<double>(t1 - t0).count();
@@ -2192,11 +2214,12 @@ int main(int argc, char** argv) {
     else if (a == "--no-cache") no_cache = true;
     else if (a == "--threads" && i + 1 < argc) threads = std::atoi(argv[++i]);
     else if (a == "--min-parallel-nodes" && i + 1 < argc) ref::g_min_parallel_nodes = std::atol(argv[++i]);
+    else if (a == "--budget" && i + 1 < argc) ref::g_budget_s = std::atof(argv[++i]);
     else if (a == "-o" && i + 1 < argc) out = argv[++i];
     else in = a;
   }
   if (in.empty()) {
-    fprintf(stderr, "usage: kbref [--faithful] [--no-cache] [--threads N] [--min-parallel-nodes N] fixture.json [-o out.json]\n");
+    fprintf(stderr, "usage: kbref [--faithful] [--no-cache] [--threads N] [--min-parallel-nodes N] [--budget SECONDS] fixture.json [-o out.json]\n");
     return 2;
   }
   std::string result;

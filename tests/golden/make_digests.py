@@ -1,0 +1,57 @@
+"""Generates the digest fixtures of sessions too large to keep whole:
+runs the kbref oracle (test infrastructure, --threads: identical outputs to
+one thread, tests/test_oracle_golden.py) on the seeded generator's session
+and stores helpers.digest_outputs of its output.
+
+    python tests/golden/make_digests.py [name ...]
+
+digest_c4.json        synth.config_fixture(4): BASELINE C4, 20k nodes x 500k tasks
+digest_saturated.json synth.saturated_config(): C3's cluster, per-task requests,
+                      ~108% CPU demand (batch cuts and engine replays at K=8192)
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "kube-arbitrator_amd"))
+sys.path.insert(0, os.path.dirname(HERE))
+
+from helpers import digest_outputs, ensure_oracle  # noqa: E402
+from kbgpu import synth  # noqa: E402
+
+SESSIONS = {
+    "c4": ("synth.config_fixture(4)", lambda: synth.config_fixture(4)),
+    "saturated": ("synth.saturated_config()", lambda: synth.saturated_config()),
+}
+
+
+def make(name):
+    gen, fn = SESSIONS[name]
+    fx = fn()
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "fx.json"), os.path.join(d, "out.json")
+        with open(src, "w") as f:
+            json.dump(fx, f)
+        t = time.time()
+        threads = str(os.cpu_count() or 1)
+        subprocess.run([ensure_oracle(), "--threads", threads, src, "-o", dst], check=True)
+        secs = time.time() - t
+        with open(dst) as f:
+            out = json.load(f)
+    dg = digest_outputs(out)
+    dg["generator"] = gen
+    dg["oracle"] = f"oracle/build/kbref --threads {threads} ({secs:.0f} s here)"
+    dg["evaluated"] = len(out.get("evaluated", []))
+    with open(os.path.join(HERE, f"digest_{name}.json"), "w") as f:
+        json.dump(dg, f, separators=(",", ":"))
+    print(name, dg["status"], dg.get("n_decisions"), f"{secs:.0f}s")
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:] or list(SESSIONS):
+        make(n)

@@ -398,6 +398,23 @@ KATS = {
         "podGroups": [pg("pg0"), pg()], "queues": Q,
         "expected": {"decisions": [], "binds": {}},
     },
+    # NodeInfo.AddTask keys the node's tasks by PodKey "<ns>/<name>"
+    # (node_info.go:101-106, api/helpers.go:27-33): t1 is a new pod named like
+    # the Running r still on n1, so ssn.Allocate logs t1 -> n1 and runs the
+    # handlers but AddTask returns "already on node" and Idle stays 1 CPU
+    # (session.go:243-293); t2 then fits the same CPU. Without the key rule
+    # t2 would find Idle 0 and fit nowhere.
+    "kat_dup_pod_key": {
+        "tiers": [[{"name": "predicates"}]],
+        "nodes": [node("n1", "2")],
+        "pods": [pod("r", "p1", {"cpu": "1"}, group="pg0", phase="Running", node="n1"),
+                 pod("t1", "p1", {"cpu": "1"}),
+                 pod("t2", "p2", {"cpu": "1"})],
+        "podGroups": [pg("pg0"), pg()], "queues": Q,
+        "expected": {"decisions": [["t1", "n1", "allocate"], ["t2", "n1", "allocate"]],
+                     "binds": {"ns/p1": "n1", "ns/p2": "n1"},
+                     "nodes": {"n1": [[0.0, 64.0 * GI, 0.0], [0.0, 0.0, 0.0], 2]}},
+    },
 }
 
 

@@ -363,3 +363,16 @@ def test_affinity_config_scaled_parity(nodes, jobs, tasks):
     got, ssn = run_fixture(fx)
     compare_outputs(run_oracle(fx), got)
     ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(200))
+def test_dupkey_fuzz_parity(seed):
+    """Colliding pod keys (synth.dupkey_fixture): a placement onto a node that
+    already holds the PodKey is logged and dispatched but leaves the node
+    unchanged (node_info.go:101-106, session.go:205-293), across allocate,
+    backfill, reclaim and preempt, batch sizes and both scan modes."""
+    fx = synth.dupkey_fixture(seed)
+    got, ssn = run_fixture(fx, {"batch_tasks": 1 + seed % 9, "candidates": 1 + seed % 5, "full_scan": seed % 2})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()

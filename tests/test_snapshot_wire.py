@@ -42,6 +42,17 @@ def test_round_trip_is_byte_identical(kind, seed):
     blob.close()
 
 
+def test_blob_view_keeps_its_owner_alive():
+    """`SnapshotBlob.decode(...).snap` alone must stay valid: the view holds
+    its blob (the library frees the arrays only when the blob goes away)."""
+    import gc
+    flat = flat_of(synth.config_fixture(1))
+    data = encode(flat.snap)
+    snap = SnapshotBlob.decode(data).snap
+    gc.collect()
+    assert encode(snap) == data
+
+
 def test_save_and_load(tmp_path):
     flat = flat_of(synth.config_fixture(1))
     path = tmp_path / "c1.kbgs"
@@ -57,10 +68,21 @@ def test_corrupt_input_is_rejected():
     for bad in (b"", data[:10], data[:-1], data + b"x", b"XXXX" + data[4:]):
         with pytest.raises(_abi.KbgError):
             SnapshotBlob.decode(bytes(bad))
-    wrong_abi = bytearray(data)
-    wrong_abi[8] ^= 0xFF  # the ABI version word
+    wrong_layout = bytearray(data)
+    wrong_layout[8] ^= 0xFF  # the layout word (struct sizes)
     with pytest.raises(_abi.KbgError):
-        SnapshotBlob.decode(bytes(wrong_abi))
+        SnapshotBlob.decode(bytes(wrong_layout))
+    # inflated counts: rejected before anything is allocated (no bad_alloc, no OOM)
+    for off in range(12, 12 + 4 * 22, 4):  # n_strings, then the 21 array counts
+        big = bytearray(data)
+        big[off:off + 4] = (0x7FFFFFFF).to_bytes(4, "little")
+        with pytest.raises(_abi.KbgError):
+            SnapshotBlob.decode(bytes(big))
+    # a negative count in a snapshot: encode refuses it up front
+    flat = flat_of(synth.random_fixture(7))
+    flat.snap.n_taints = -1
+    with pytest.raises(_abi.KbgError):
+        encode(flat.snap)
     # a task pointing past the job table: decode validates like kbg_session_open
     flat = flat_of(synth.random_fixture(7))
     flat.arrays["tasks"][0]["job"] = 10_000
