@@ -434,11 +434,17 @@ kbg_status copy_soa(Session& S, const kbg::NodeSoA& dst, const kbg::NodeSoA& src
 }
 
 void free_device(Session& S) {
-  if (S.h_up) (void)hipHostFree(S.h_up);
-  if (S.h_down) (void)hipHostFree(S.h_down);
-  S.h_up = nullptr;
-  S.h_down = nullptr;
-  S.h_capoff = nullptr;
+  for (kbg::Stage& g : S.stages) {
+    if (g.inflight) (void)hipEventSynchronize(g.ev[6]);  // nothing may still write the staging
+    if (g.h_up) (void)hipHostFree(g.h_up);
+    if (g.h_down) (void)hipHostFree(g.h_down);
+    for (auto& e : g.ev)
+      if (e) {
+        (void)hipEventDestroy(e);
+        e = nullptr;
+      }
+    g = kbg::Stage{};
+  }
   if (S.h_deltas) (void)hipHostFree(S.h_deltas);
   if (S.h_mdeltas) (void)hipHostFree(S.h_mdeltas);
   S.h_mdeltas = nullptr;
@@ -447,8 +453,6 @@ void free_device(Session& S) {
   S.h_vbits = nullptr;
   S.h_sdeltas = nullptr;
   S.vt_ready = false;
-  S.h_tasks = nullptr;
-  S.h_cand = S.h_count = nullptr;
   S.h_deltas = nullptr;
   for (void* p : S.d_allocs) (void)hipFree(p);
   S.d_allocs.clear();
@@ -504,16 +508,21 @@ kbg_status upload_nodes(Session& S) {
   return copy_soa(S, S.d_nodes, S.d_nodes0);
 }
 
-// One device round trip for a batch: rows[0..G) are the distinct evaluation
-// rows (a task in full-scan mode, a (class, request) shape otherwise), each
-// given cap_off[g+1]-cap_off[g] candidate slots. Fills S.h_cand / S.h_count.
-kbg_status device_launch(Session& S, int32_t G) {
-  const uint32_t total = S.h_capoff[G];
+// One device round trip for a batch: rows[0..G) of stage `sg` are the
+// distinct evaluation rows (a task in full-scan mode, a (class, request) shape
+// otherwise), each given cap_off[g+1]-cap_off[g] candidate slots. Everything
+// is enqueued on the session stream; sg.ev[6] fires when the candidate lists
+// are on the host. The device buffers are reused in stream order (the next
+// upload runs after this batch's select has read them); only the host staging
+// is per stage. `base`: the newest resolution whose node deltas are already
+// enqueued, i.e. what this scan sees.
+kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
+  const uint32_t total = sg.h_capoff[G];
   const int32_t Gp = kbg::kbg_pad_rows(G);  // Grouper::build padded the rows
   const size_t up_bytes = (size_t)Gp * sizeof(kbg::TaskRec) + (size_t)(G + 1) * 4;
   const kbg::TaskRec* d_tasks = (const kbg::TaskRec*)S.d_up;
   const uint32_t* d_capoff = (const uint32_t*)(S.d_up + (size_t)Gp * sizeof(kbg::TaskRec));
-  HIP_TRY(hipMemcpyAsync(S.d_up, S.h_up, up_bytes, hipMemcpyHostToDevice, S.stream));
+  HIP_TRY(hipMemcpyAsync(S.d_up, sg.h_up, up_bytes, hipMemcpyHostToDevice, S.stream));
   // this process scans its shard (or every shard when they are all local)
   kbg::ScanGeom geo{S.n_nodes, S.W, S.Wl, 0, S.R * S.Wl, S.tab_lo};
   const size_t slot_words = (size_t)2 * G * S.Wl;
@@ -524,29 +533,35 @@ kbg_status device_launch(Session& S, int32_t G) {
     out = S.d_bits + (size_t)S.shard * slot_words;
   }
   HIP_TRY(kbg::launch_scan(S.d_nodes, geo, S.d_class_mask, d_tasks, G, S.pred_active ? 1 : 0, S.int_mode ? 1 : 0, out,
-                           S.stream, S.ev[0], S.ev[1]));
+                           S.stream, sg.ev[0], sg.ev[1]));
   if (S.comm) {  // in-place all-gather: every rank receives every shard's slot, in rank (= node) order
-    HIP_TRY(hipEventRecord(S.ev[4], S.stream));
+    HIP_TRY(hipEventRecord(sg.ev[4], S.stream));
     const ncclResult_t nr = ncclAllGather(out, S.d_bits, slot_words, ncclUint64, S.comm->nccl, S.stream);
     if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
-    HIP_TRY(hipEventRecord(S.ev[5], S.stream));
+    HIP_TRY(hipEventRecord(sg.ev[5], S.stream));
   }
-  HIP_TRY(kbg::launch_select(S.d_bits, S.W, S.Wl, G, d_capoff, S.d_down + G, S.d_down, S.stream, S.ev[2], S.ev[3]));
-  HIP_TRY(hipMemcpyAsync(S.h_down, S.d_down, ((size_t)G + total) * 4, hipMemcpyDeviceToHost, S.stream));
+  HIP_TRY(kbg::launch_select(S.d_bits, S.W, S.Wl, G, d_capoff, S.d_down + G, S.d_down, S.stream, sg.ev[2], sg.ev[3]));
+  HIP_TRY(hipMemcpyAsync(sg.h_down, S.d_down, ((size_t)G + total) * 4, hipMemcpyDeviceToHost, S.stream));
+  HIP_TRY(hipEventRecord(sg.ev[6], S.stream));
+  sg.G = G;
+  sg.base = base;
+  sg.inflight = true;
   return KBG_OK;
 }
 
-kbg_status device_wait(Session& S, int32_t G) {
-  HIP_TRY(hipStreamSynchronize(S.stream));
-  S.h_count = S.h_down;
-  S.h_cand = S.h_down + G;
+kbg_status device_wait(Session& S, kbg::Stage& sg) {
+  HIP_TRY(hipEventSynchronize(sg.ev[6]));
+  sg.inflight = false;
+  const int32_t G = sg.G;
+  sg.h_count = sg.h_down;
+  sg.h_cand = sg.h_down + G;
   float ms = 0;
-  HIP_TRY(hipEventElapsedTime(&ms, S.ev[0], S.ev[1]));
+  HIP_TRY(hipEventElapsedTime(&ms, sg.ev[0], sg.ev[1]));
   S.stats.scan_kernel_ms += ms;
-  HIP_TRY(hipEventElapsedTime(&ms, S.ev[2], S.ev[3]));
+  HIP_TRY(hipEventElapsedTime(&ms, sg.ev[2], sg.ev[3]));
   S.stats.select_kernel_ms += ms;
   if (S.comm) {
-    HIP_TRY(hipEventElapsedTime(&ms, S.ev[4], S.ev[5]));
+    HIP_TRY(hipEventElapsedTime(&ms, sg.ev[4], sg.ev[5]));
     S.stats.exchange_ms += ms;
   }
   S.stats.scan_launches++;
@@ -555,10 +570,17 @@ kbg_status device_wait(Session& S, int32_t G) {
   return KBG_OK;
 }
 
-// One synchronous device round trip (kbg_select path).
-kbg_status device_scan(Session& S, int32_t G) {
-  kbg_status st = device_launch(S, G);
-  return st != KBG_OK ? st : device_wait(S, G);
+// Results of a launch that will not be used (its batch was predicted before a
+// cut): wait for it so its staging can be rewritten, keep the kernel times.
+kbg_status device_drop(Session& S, kbg::Stage& sg) {
+  if (!sg.inflight) return KBG_OK;
+  return device_wait(S, sg);
+}
+
+// One synchronous device round trip (backfill, kbg_select).
+kbg_status device_scan(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
+  kbg_status st = device_launch(S, sg, G, base);
+  return st != KBG_OK ? st : device_wait(S, sg);
 }
 
 // Writes the rows of the nodes touched by the last commits back to HBM (only
@@ -601,36 +623,41 @@ kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
 }
 
 // Groups the tasks of a batch into device rows and sizes their candidate
-// lists. Full-scan mode: one row per task with M slots (every evaluation
-// scans the whole table — the SURVEY §8(d) roofline rule). Grouped mode: one
-// row per distinct (class, request) shape with (tasks of the shape + M) slots;
-// tasks of a shape share one first-fit list and a cursor (Resolver).
-constexpr int32_t kGroupSlack = 512;  // extra candidate slots per shape row (grouped mode)
+// lists. Full-scan mode: one row per task (every evaluation scans the whole
+// table — the SURVEY §8(d) roofline rule) with M + r slots, r = the number of
+// earlier rows of the same (class, request) shape in this scan: each earlier
+// commit can exhaust at most one node of the list, so a row rarely runs out
+// before the table does. Grouped mode: one row per distinct shape with (tasks
+// of the shape + slack) slots; tasks of a shape share the row and a cursor.
+constexpr int32_t kGroupSlack = 512;  // extra candidate slots per shape row (grouped) / rank cap (full-scan)
 
 struct Grouper {
   Session& S;
   std::vector<int32_t> shape_row, shape_stamp, count;
-  std::vector<int32_t> row_of;  // per batch entry
   int32_t stamp = 0;
   explicit Grouper(Session& s) : S(s), shape_row(s.n_shapes, -1), shape_stamp(s.n_shapes, -1) {}
-  int32_t build(const int32_t* bt, int32_t n) {
-    S.h_tasks = (kbg::TaskRec*)S.h_up;
+  int32_t build(kbg::Stage& sg, const int32_t* bt, int32_t n) {
+    sg.h_tasks = (kbg::TaskRec*)sg.h_up;
     ++stamp;
-    row_of.resize(n);
+    sg.row_of.resize(n);
+    sg.row_shape.clear();
     count.clear();
     int32_t G = 0;
     for (int32_t i = 0; i < n; ++i) {
       const int32_t t = bt[i];
       int32_t g;
       const int32_t sh = S.task_shape[t];
-      if (!S.opts.full_scan && shape_stamp[sh] == stamp) {
+      const bool seen = shape_stamp[sh] == stamp;
+      if (!S.opts.full_scan && seen) {
         g = shape_row[sh];
       } else {
         g = G++;
-        count.push_back(0);
+        // full-scan: count[g] = earlier rows of this shape in the scan (the list grows with them)
+        count.push_back(S.opts.full_scan && seen ? count[shape_row[sh]] + 1 : 0);
         shape_stamp[sh] = stamp;
         shape_row[sh] = g;
-        kbg::TaskRec& r = S.h_tasks[g];
+        sg.row_shape.push_back(sh);
+        kbg::TaskRec& r = sg.h_tasks[g];
         const Res& q = S.treq[t];
         if (S.be_task[t]) {  // backfill: PredicateFn only — every node fits (a > -inf in both modes)
           r.req[0] = r.req[1] = r.req[2] = -INFINITY;
@@ -646,47 +673,80 @@ struct Grouper {
         r.cls = S.task_class[t];
         r.flags = (S.be_task[t] || kbg::res_le(q, Res{})) ? kbg::kRowRelZeroFits : 0;
       }
-      row_of[i] = g;
-      count[g]++;
+      sg.row_of[i] = g;
+      if (!S.opts.full_scan) count[g]++;
     }
     const int32_t Gp = kbg::kbg_pad_rows(G);
-    for (int32_t g = G; g < Gp; ++g) S.h_tasks[g] = S.h_tasks[0];  // padding rows: scanned, never stored
-    S.h_capoff = (uint32_t*)(S.h_up + (size_t)Gp * sizeof(kbg::TaskRec));
-    S.h_capoff[0] = 0;
+    for (int32_t g = G; g < Gp; ++g) sg.h_tasks[g] = sg.h_tasks[0];  // padding rows: scanned, never stored
+    sg.h_capoff = (uint32_t*)(sg.h_up + (size_t)Gp * sizeof(kbg::TaskRec));
+    sg.h_capoff[0] = 0;
     for (int32_t g = 0; g < G; ++g) {
-      const uint32_t want = S.opts.full_scan ? (uint32_t)S.M : (uint32_t)std::min(count[g] + kGroupSlack, 4096);
-      S.h_capoff[g + 1] = S.h_capoff[g] + want;
+      const uint32_t want = S.opts.full_scan ? (uint32_t)(S.M + std::min(count[g], kGroupSlack))
+                                             : (uint32_t)std::min(count[g] + kGroupSlack, 4096);
+      sg.h_capoff[g + 1] = sg.h_capoff[g] + want;
     }
     return G;
   }
 };
 
-// In-order commit against the batch-start candidate lists. A row's cursor
-// only moves forward: a candidate found infeasible for a (class, request)
-// shape stays infeasible for every later task of that shape (monotonicity).
+// In-order commit against the candidate lists of one scan. A node the list
+// names is taken as it is unless a resolution newer than the scan touched it
+// (mark > base: resources, pod count, or a class-mask bit it lost); those are
+// re-checked on the host mirror. A row's cursor only moves forward: a
+// candidate found infeasible for a (class, request) shape stays infeasible
+// for every later task of that shape (monotonicity). In full-scan mode every
+// task has its own row, and rows of one shape in one scan hold the same list
+// (same inputs, same table): the prefix an earlier row of the shape rejected
+// is skipped instead of re-checked (`shape_skip`).
 enum { RES_OK = 0, RES_TRUNC = 1, RES_PANIC = 2 };
 struct Resolver {
   Session& S;
   std::vector<int32_t>& mark;
-  int32_t stamp;
+  const kbg::Stage* sg = nullptr;
+  int32_t base = 0;
   std::vector<int32_t> cursor;
-  void reset(int32_t G) { cursor.assign(G, 0); }
+  std::vector<int32_t> shape_skip, skip_stamp;
+  int32_t skip_gen = 0;
+  void reset(const kbg::Stage& stage) {
+    sg = &stage;
+    base = stage.base;
+    cursor.assign(stage.G, 0);
+    if (S.opts.full_scan) {
+      if (shape_skip.size() < (size_t)S.n_shapes) {
+        shape_skip.assign(S.n_shapes, 0);
+        skip_stamp.assign(S.n_shapes, -1);
+      }
+      ++skip_gen;
+    }
+  }
+  bool dirty(int32_t t, int32_t nd) const {
+    return mark[nd] > base || (S.has_aff && S.mwmark[(size_t)S.task_class[t] * S.W + (nd >> 6)] > base);
+  }
   int resolve(int32_t g, int32_t t, int32_t* node, int32_t* kind) {
-    const uint32_t cnt = S.h_count[g];
+    const uint32_t cnt = sg->h_count[g];
     const int32_t n = (int32_t)(cnt & kbg::kCountMask);
-    const uint32_t* c = S.h_cand + S.h_capoff[g];
+    const uint32_t* c = sg->h_cand + sg->h_capoff[g];
     const Res& r = S.treq[t];
-    for (int32_t& k = cursor[g]; k < n; ++k) {
+    int32_t sh = -1;
+    if (S.opts.full_scan) {
+      sh = sg->row_shape[g];
+      if (skip_stamp[sh] == skip_gen) cursor[g] = std::max(cursor[g], std::min(shape_skip[sh], n));
+    }
+    int res = -1;
+    int32_t& k = cursor[g];
+    for (; k < n; ++k) {
       const int32_t nd = (int32_t)(c[k] & ~kbg::kCandPipelineBit);
-      if (S.panic_node[nd]) return RES_PANIC;
-      if (mark[nd] != stamp &&
-          (!S.has_aff || S.mwmark[(size_t)S.task_class[t] * S.W + (nd >> 6)] != S.mstamp)) {
+      if (S.panic_node[nd]) {
+        res = RES_PANIC;
+        break;
+      }
+      if (!dirty(t, nd)) {
         *node = nd;
         *kind = (c[k] & kbg::kCandPipelineBit) ? KBG_KIND_PIPELINE : KBG_KIND_ALLOCATE;
-        return RES_OK;
+        res = RES_OK;
+        break;
       }
-      // touched by an earlier commit of this batch (resources, or a class-mask
-      // bit it lost): re-check on the host mirror
+      // touched since the scan: re-check on the host mirror
       if (S.pred_active && S.ntasks[nd] >= S.maxtasks[nd]) continue;
       if ((S.has_ports || S.has_aff) &&
           !((S.h_class_mask[(size_t)S.task_class[t] * S.W + (nd >> 6)] >> (nd & 63)) & 1ull))
@@ -694,19 +754,27 @@ struct Resolver {
       if (S.be_task[t]) {  // backfill: PredicateFn only, always ssn.Allocate
         *node = nd;
         *kind = KBG_KIND_ALLOCATE;
-        return RES_OK;
+        res = RES_OK;
+        break;
       }
       if (kbg::res_le(r, S.idle[nd])) {
         *node = nd;
         *kind = KBG_KIND_ALLOCATE;
-        return RES_OK;
+        res = RES_OK;
+        break;
       }
       if (kbg::res_le(r, S.rel[nd])) {
         *node = nd;
         *kind = KBG_KIND_PIPELINE;
-        return RES_OK;
+        res = RES_OK;
+        break;
       }
     }
+    if (sh >= 0 && res != RES_PANIC) {  // entries before k are infeasible for the shape from now on
+      shape_skip[sh] = k;
+      skip_stamp[sh] = skip_gen;
+    }
+    if (res >= 0) return res;
     if (cnt & kbg::kCountIncompleteBit) return RES_TRUNC;
     *node = -1;
     return RES_OK;
@@ -1035,7 +1103,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.M = S.opts.candidates > 0 ? S.opts.candidates : 32;
   if (S.M > 4096) return fail(KBG_E_INVALID, "candidates > 4096");
   // full-scan: K rows x M slots; grouped: sum over shapes of min(n_s + slack, 4096)
-  S.cand_cap = S.opts.full_scan ? (int64_t)S.K * S.M : (int64_t)S.K * (512 + 1);
+  S.cand_cap = S.opts.full_scan ? (int64_t)S.K * (S.M + kGroupSlack) : (int64_t)S.K * (kGroupSlack + 1);
 
   S.strs.assign(snap->strings, snap->strings + snap->n_strings);
   {
@@ -1410,8 +1478,12 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
       (st = dalloc(S, &S.d_bits, (size_t)S.R * 2 * S.K * S.Wl)) ||
       (st = dalloc(S, &S.d_down, down_cap)) || (st = dalloc(S, &S.d_deltas, S.K)))
     return st;
-  HIP_TRY(hipHostMalloc((void**)&S.h_up, up_cap, hipHostMallocDefault));
-  HIP_TRY(hipHostMalloc((void**)&S.h_down, down_cap * 4, hipHostMallocDefault));
+  for (kbg::Stage& g : S.stages) {
+    HIP_TRY(hipHostMalloc((void**)&g.h_up, up_cap, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&g.h_down, down_cap * 4, hipHostMallocDefault));
+    for (int e = 0; e < 6; ++e) HIP_TRY(hipEventCreate(&g.ev[e]));
+    HIP_TRY(hipEventCreateWithFlags(&g.ev[6], hipEventDisableTiming));
+  }
   HIP_TRY(hipHostMalloc((void**)&S.h_deltas, (size_t)S.K * sizeof(kbg::NodeDelta), hipHostMallocDefault));
   if ((st = upload_nodes(S))) return st;
   phase("device alloc+nodes");
@@ -1712,10 +1784,9 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   for (int32_t i = 0; i < S.n_shapes; ++i) failed[i].store(0, std::memory_order_relaxed);
   std::vector<int32_t> mark(S.n_nodes, -1), touched;
   std::vector<char> bactual;
-  int32_t stamp = 0;
   kbg_status result = KBG_OK;
   Grouper grouper(S);
-  Resolver rs{S, mark, 0, {}};
+  Resolver rs{S, mark};
 
   // ------------------------------------------------------------ predictor
   Pipe P;
@@ -1782,8 +1853,15 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
   });
 
-  auto take = [&]() -> Batch* {
+  // a predicted batch; nullptr when the predictor failed. Non-blocking: also
+  // nullptr (with *none = true) when no batch is ready yet.
+  auto take = [&](bool block, bool* none) -> Batch* {
     std::unique_lock<std::mutex> lk(P.mu);
+    if (!block && P.ready.empty()) {
+      *none = true;
+      return nullptr;
+    }
+    *none = false;
     P.cv.wait(lk, [&] { return !P.ready.empty(); });
     Batch* b = P.ready.front();
     P.ready.pop_front();
@@ -1810,47 +1888,79 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   };
 
   // ------------------------------------------------------------ committer
+  // Two stages in flight: while the host resolves batch b (stage `si`), the
+  // device scans batch b+1 (stage si^1) against the table without b's commits;
+  // b+1's resolve re-checks every node b touched (mark > that scan's base).
   int64_t cur_epoch = 0;
-  for (;;) {
-    Batch* b = take();
-    if (!b) {  // predictor failed
-      finish();
-      return fail(KBG_E_INVALID, pred_error);
+  int32_t pushed = S.res_stamp;  // newest resolution whose node deltas are enqueued
+  bool pred_failed = false;
+  // the next batch of the current epoch (stale ones are recycled); nullptr:
+  // none ready (non-blocking) or the predictor failed (pred_failed)
+  auto next_batch = [&](bool block) -> Batch* {
+    for (;;) {
+      bool none = false;
+      Batch* b = take(block, &none);
+      if (none) return nullptr;
+      if (!b) {
+        pred_failed = true;
+        return nullptr;
+      }
+      if (b->epoch != cur_epoch) {
+        recycle(b);
+        continue;
+      }
+      return b;
     }
-    if (b->epoch != cur_epoch) {  // predicted before the last cut
-      recycle(b);
-      continue;
-    }
-    if (b->bt.empty()) {  // engine exhausted in the current epoch: the cycle is over
-      recycle(b);
-      break;
-    }
-    const std::vector<int32_t>& bt = b->bt;
-    S.stats.batches++;
-    // device: feasibility scan + first-fit candidate lists against the batch-start table
+  };
+  auto launch = [&](kbg::Stage& sg, Batch* b) -> kbg_status {
+    const int32_t G = grouper.build(sg, b->bt.data(), (int32_t)b->bt.size());
+    return device_launch(S, sg, G, pushed);
+  };
+  auto abort = [&](kbg_status st) {
+    for (kbg::Stage& g : S.stages) (void)device_drop(S, g);
+    finish();
+    return st;
+  };
+  int si = 0;
+  Batch* cur = next_batch(true);
+  if (!cur) {
+    finish();
+    return fail(KBG_E_INVALID, pred_error);
+  }
+  if (!cur->bt.empty()) {
     auto tp = clk::now();
-    int32_t G = grouper.build(bt.data(), (int32_t)bt.size());
-    kbg_status st = device_launch(S, G);
-    if (st == KBG_OK) st = device_wait(S, G);
-    if (st != KBG_OK) {
-      finish();
-      return st;
-    }
+    kbg_status st = launch(S.stages[si], cur);
+    S.stats.device_ms += ms_since(tp);
+    if (st != KBG_OK) return abort(st);
+  }
+  while (cur && !cur->bt.empty()) {
+    const std::vector<int32_t>& bt = cur->bt;
+    kbg::Stage* sg = &S.stages[si];
+    kbg::Stage& other = S.stages[si ^ 1];
+    S.stats.batches++;
+    auto tp = clk::now();
+    kbg_status st = device_wait(S, *sg);
+    if (st != KBG_OK) return abort(st);
+    // the next batch's scan overlaps this batch's resolve when it is ready
+    Batch* nxt = next_batch(false);
+    if (pred_failed) return abort(fail(KBG_E_INVALID, pred_error));
+    if (nxt && !nxt->bt.empty() && (st = launch(other, nxt)) != KBG_OK) return abort(st);
     S.stats.device_ms += ms_since(tp);
     // commit in order
     tp = clk::now();
-    rs.stamp = ++stamp;
+    rs.reset(*sg);
+    const int32_t stamp = ++S.res_stamp;  // this resolution's commits
     S.mstamp = stamp;
-    rs.reset(G);
     touched.clear();
     bactual.assign(bt.size(), 0);
     int32_t cut = -1;
-    int32_t seg = 0;  // first batch entry covered by the current device scan
+    int32_t seg = 0;  // first batch entry covered by the current scan of this stage
     bool panic = false;
+    int32_t rstamp = stamp;
     for (int32_t i = 0; i < (int32_t)bt.size(); ++i) {
       const int32_t t = bt[i];
       int32_t node = -1, kind = 0;
-      int r = rs.resolve(grouper.row_of[i - seg], t, &node, &kind);
+      int r = rs.resolve(sg->row_of[i - seg], t, &node, &kind);
       if (r == RES_TRUNC) {
         // A candidate list ran out before the table did. The predictions
         // still hold (no outcome differed), so instead of cutting the batch
@@ -1860,23 +1970,21 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         tp = clk::now();
         S.stats.truncations++;
         st = push_deltas(S, touched);
+        pushed = rstamp;
         if (st == KBG_OK) {
-          G = grouper.build(bt.data() + i, (int32_t)bt.size() - i);
-          st = device_launch(S, G);
+          const int32_t G = grouper.build(*sg, bt.data() + i, (int32_t)bt.size() - i);
+          st = device_launch(S, *sg, G, pushed);
         }
-        if (st == KBG_OK) st = device_wait(S, G);
-        if (st != KBG_OK) {
-          finish();
-          return st;
-        }
+        if (st == KBG_OK) st = device_wait(S, *sg);
+        if (st != KBG_OK) return abort(st);
         S.stats.device_ms += ms_since(tp);
         tp = clk::now();
         seg = i;
-        rs.stamp = ++stamp;  // the device table now holds every commit so far
-        S.mstamp = stamp;
-        rs.reset(G);
+        rs.reset(*sg);
+        rstamp = ++S.res_stamp;  // commits after the rescan
+        S.mstamp = rstamp;
         touched.clear();
-        r = rs.resolve(grouper.row_of[0], t, &node, &kind);  // a fresh list always decides its first task
+        r = rs.resolve(sg->row_of[0], t, &node, &kind);  // a fresh list always decides its first task
       }
       if (r == RES_PANIC) {
         panic = true;
@@ -1893,15 +2001,15 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
           dec_oldp.insert(dec_oldp.end(), S.node_ports.begin() + (size_t)node * S.PW,
                           S.node_ports.begin() + (size_t)(node + 1) * S.PW);
         const bool dup = mirror_add(S, t, node, kind);
-        if (mark[node] != stamp) {
-          mark[node] = stamp;
+        if (mark[node] != rstamp) {
+          mark[node] = rstamp;
           touched.push_back(node);
         }
         record_decision(S, t, node, kind, dup);
       } else {
         failed[S.task_shape[t]].store(1, std::memory_order_relaxed);
       }
-      if (ok != (bool)b->bpred[i]) {
+      if (ok != (bool)cur->bpred[i]) {
         cut = i + 1;
         S.stats.mispredictions++;
         break;
@@ -1923,28 +2031,58 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
     S.stats.resolve_ms += ms_since(tp);
     tp = clk::now();
-    if ((st = push_deltas(S, touched)) != KBG_OK) {
-      finish();
-      return st;
-    }
+    if ((st = push_deltas(S, touched)) != KBG_OK) return abort(st);
+    pushed = rstamp;
     S.stats.delta_ms += ms_since(tp);
     if (panic) {
-      recycle(b);
+      recycle(cur);
+      recycle(nxt);
+      cur = nullptr;
       result = fail(KBG_E_REF_PANIC, "allocate reached a node whose NodeInfo.Node is nil with the predicates plugin on "
                                      "(predicates.go:122-123)");
       break;
     }
     if (cut >= 0) {  // roll the predictor back to this batch's checkpoint + the actual prefix
-      std::lock_guard<std::mutex> lk(P.mu);
-      P.epoch = ++cur_epoch;
-      P.rollback = true;
-      P.rb_ckpt = b->ckpt;
-      P.rb_tasks.assign(bt.begin(), bt.begin() + cut);
-      P.rb_actual.assign(bactual.begin(), bactual.begin() + cut);
-      P.free.push_back(b);
-      P.cv.notify_all();
-    } else {
-      recycle(b);
+      if ((st = device_drop(S, other)) != KBG_OK) return abort(st);  // nxt was predicted before the cut
+      {
+        std::lock_guard<std::mutex> lk(P.mu);
+        P.epoch = ++cur_epoch;
+        P.rollback = true;
+        P.rb_ckpt = cur->ckpt;
+        P.rb_tasks.assign(bt.begin(), bt.begin() + cut);
+        P.rb_actual.assign(bactual.begin(), bactual.begin() + cut);
+        P.free.push_back(cur);
+        if (nxt) P.free.push_back(nxt);
+        P.cv.notify_all();
+      }
+      cur = next_batch(true);
+      if (!cur) return abort(fail(KBG_E_INVALID, pred_error));
+      if (!cur->bt.empty()) {
+        tp = clk::now();
+        if ((st = launch(S.stages[si], cur)) != KBG_OK) return abort(st);
+        S.stats.device_ms += ms_since(tp);
+      }
+      continue;
+    }
+    recycle(cur);
+    if (!nxt) {  // the predictor was behind: take its next batch now and scan it
+      nxt = next_batch(true);
+      if (!nxt) return abort(fail(KBG_E_INVALID, pred_error));
+      if (!nxt->bt.empty()) {
+        tp = clk::now();
+        if ((st = launch(other, nxt)) != KBG_OK) return abort(st);
+        S.stats.device_ms += ms_since(tp);
+      }
+    }
+    cur = nxt;
+    si ^= 1;
+  }
+  if (cur) recycle(cur);  // the epoch's end marker
+  for (kbg::Stage& g : S.stages) {
+    kbg_status st = device_drop(S, g);  // a scan launched before a panic
+    if (st != KBG_OK) {
+      finish();
+      return st;
     }
   }
   finish();
@@ -1985,36 +2123,39 @@ kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     for (int32_t k = S.jt_off[j]; k < S.jt_off[j + 1]; ++k)
       if (S.be_task[S.jt[k]] && S.tstat[S.jt[k]] == KBG_PENDING) be.push_back(S.jt[k]);
   std::vector<int32_t> mark(S.n_nodes, -1), touched;
-  int32_t stamp = 0;
   Grouper grouper(S);
-  Resolver rs{S, mark, 0, {}};
+  Resolver rs{S, mark};
+  kbg::Stage& sg = S.stages[0];
+  int32_t pushed = S.res_stamp, rstamp = 0;
   kbg_status result = KBG_OK, st = KBG_OK;
   Engine& E = S.fin;
+  // one synchronous scan of bt[0..n) against the table with every commit so far
+  auto rescan = [&](const int32_t* b, int32_t n) -> kbg_status {
+    kbg_status s2 = push_deltas(S, touched);
+    if (s2 != KBG_OK) return s2;
+    pushed = rstamp ? rstamp : pushed;
+    touched.clear();
+    const int32_t G = grouper.build(sg, b, n);
+    if ((s2 = device_scan(S, sg, G, pushed)) != KBG_OK) return s2;
+    rs.reset(sg);
+    rstamp = ++S.res_stamp;
+    S.mstamp = rstamp;
+    return KBG_OK;
+  };
   for (size_t done = 0; done < be.size() && result == KBG_OK;) {
     const int32_t cnt = (int32_t)std::min<size_t>(be.size() - done, (size_t)S.K);
     const int32_t* bt = be.data() + done;
-    int32_t G = grouper.build(bt, cnt);
-    if ((st = device_scan(S, G)) != KBG_OK) return st;
-    rs.stamp = ++stamp;
-    S.mstamp = stamp;
-    rs.reset(G);
-    touched.clear();
+    if ((st = rescan(bt, cnt)) != KBG_OK) return st;
     int32_t seg = 0;
     for (int32_t i = 0; i < cnt; ++i) {
       const int32_t t = bt[i];
       int32_t node = -1, kind = 0;
-      int r = rs.resolve(grouper.row_of[i - seg], t, &node, &kind);
+      int r = rs.resolve(sg.row_of[i - seg], t, &node, &kind);
       if (r == RES_TRUNC) {  // list exhausted: write back, rescan the rest of the batch
         S.stats.truncations++;
-        if ((st = push_deltas(S, touched)) != KBG_OK) return st;
-        G = grouper.build(bt + i, cnt - i);
-        if ((st = device_scan(S, G)) != KBG_OK) return st;
+        if ((st = rescan(bt + i, cnt - i)) != KBG_OK) return st;
         seg = i;
-        rs.stamp = ++stamp;
-        S.mstamp = stamp;
-        rs.reset(G);
-        touched.clear();
-        r = rs.resolve(grouper.row_of[0], t, &node, &kind);
+        r = rs.resolve(sg.row_of[0], t, &node, &kind);
       }
       if (r == RES_PANIC) {
         result = fail(KBG_E_REF_PANIC, "backfill reached a node whose NodeInfo.Node is nil with the predicates plugin on "
@@ -2030,8 +2171,8 @@ kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         break;
       }
       const bool dup = mirror_add(S, t, node, KBG_KIND_ALLOCATE);
-      if (mark[node] != stamp) {
-        mark[node] = stamp;
+      if (mark[node] != rstamp) {
+        mark[node] = rstamp;
         touched.push_back(node);
       }
       // drf / proportion AllocateFunc (drf.go:130-139, proportion.go:196-206)
@@ -2052,17 +2193,13 @@ kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         // pod affinity gave a class new nodes: rescan the rest of the batch
         for (int32_t c : S.aff_gain_classes) S.aff_gain_flag[c] = 0;
         S.aff_gain_classes.clear();
-        if ((st = push_deltas(S, touched)) != KBG_OK) return st;
-        G = grouper.build(bt + i + 1, cnt - i - 1);
-        if ((st = device_scan(S, G)) != KBG_OK) return st;
+        if ((st = rescan(bt + i + 1, cnt - i - 1)) != KBG_OK) return st;
         seg = i + 1;
-        rs.stamp = ++stamp;
-        S.mstamp = stamp;
-        rs.reset(G);
-        touched.clear();
       }
     }
     if ((st = push_deltas(S, touched)) != KBG_OK) return st;
+    touched.clear();
+    pushed = rstamp;
     done += cnt;
   }
   HIP_TRY(hipStreamSynchronize(S.stream));
@@ -2967,22 +3104,24 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
   if (S.has_aff) return fail(KBG_E_UNSUPPORTED, "kbg_select with pod (anti)affinity: use kbg_allocate");
   std::vector<int32_t> mark(S.n_nodes, -1), touched, bt;
   Grouper grouper(S);
-  Resolver rs{S, mark, 0, {}};
-  int32_t done = 0, stamp = 0;
+  Resolver rs{S, mark};
+  kbg::Stage& sg = S.stages[0];
+  int32_t done = 0;
   bool stop = false;
   while (done < n && !stop) {
     const int32_t cnt = std::min(n - done, S.K);
     bt.assign(tasks + done, tasks + done + cnt);
-    const int32_t G = grouper.build(bt.data(), cnt);
-    kbg_status st = device_scan(S, G);
+    const int32_t G = grouper.build(sg, bt.data(), cnt);
+    kbg_status st = device_scan(S, sg, G, S.res_stamp);  // every earlier commit is in the table
     if (st != KBG_OK) return st;
     touched.clear();
-    rs.stamp = ++stamp;
-    rs.reset(G);
+    rs.reset(sg);
+    const int32_t rstamp = ++S.res_stamp;
+    S.mstamp = rstamp;
     int32_t i = 0;
     for (; i < cnt; ++i) {
       int32_t node = -1, kind = 0;
-      const int r = rs.resolve(grouper.row_of[i], bt[i], &node, &kind);
+      const int r = rs.resolve(sg.row_of[i], bt[i], &node, &kind);
       if (r == RES_TRUNC) break;  // rescan from this task with the updated table
       if (r == RES_PANIC) {
         if ((st = push_deltas(S, touched)) != KBG_OK) return st;
@@ -2994,8 +3133,8 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
       if (out_kind) out_kind[done + i] = kind;
       if (node >= 0) {
         mirror_add(S, bt[i], node, kind);
-        if (mark[node] != stamp) {
-          mark[node] = stamp;
+        if (mark[node] != rstamp) {
+          mark[node] = rstamp;
           touched.push_back(node);
         }
         if (stop_at_first_success) {

@@ -150,6 +150,26 @@ struct VictimKey {
   }
 };
 
+// One in-flight device round trip of the batch driver: pinned host staging
+// for the evaluation rows going up and the candidate lists coming down, the
+// batch's row map, and the events that time and complete it. Two stages let
+// the scan of the next batch run while the host resolves the current one.
+struct Stage {
+  char* h_up = nullptr;              // pinned: TaskRec[padded G] then capoff[G + 1]
+  uint32_t* h_down = nullptr;        // pinned: count[G] then the candidates
+  TaskRec* h_tasks = nullptr;        // = h_up
+  uint32_t* h_capoff = nullptr;      // per-row candidate slot offsets (inside h_up)
+  uint32_t* h_count = nullptr;       // = h_down
+  uint32_t* h_cand = nullptr;        // = h_down + G
+  std::vector<int32_t> row_of;       // batch entry -> evaluation row
+  std::vector<int32_t> row_shape;    // evaluation row -> (class, request) shape
+  int32_t G = 0;
+  int32_t base = 0;                  // the scan saw every node delta of resolutions with stamp <= base
+  bool inflight = false;             // launched, results not yet collected
+  hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // scan, select,
+                                     // exchange start/stop; [6] = results on the host
+};
+
 struct Session {
   // ---- copied snapshot
   std::vector<std::string> strs;
@@ -276,8 +296,8 @@ struct Session {
   std::shared_ptr<AffinityModel> affm;
   std::vector<kbg_pod_term> pod_terms_in;
   std::vector<int32_t> pod_labels_in;
-  std::vector<int32_t> mwmark;                 // per class-mask word: batch stamp of the last bit it lost
-  int32_t mstamp = 0;                          // the current batch stamp
+  std::vector<int32_t> mwmark;                 // per class-mask word: resolution stamp of the last bit it lost
+  int32_t mstamp = 0;                          // the current resolution stamp
   std::vector<uint8_t> aff_gain_flag;          // per class: gained nodes since the last cut
   std::vector<int32_t> aff_gain_classes;
 
@@ -308,15 +328,11 @@ struct Session {
   NodeSoA d_nodes0{};       // pristine copy for kbg_session_reset
   uint64_t* d_class_mask = nullptr;
   uint64_t* d_bits = nullptr;     // feasibility bitmaps [slot][plane][row][Wl] (ScanGeom)
-  uint32_t* h_capoff = nullptr;   // per-row candidate slot offsets (inside h_up)
-  char* h_up = nullptr;           // pinned upload staging: TaskRec[G] then capoff[G+1]
-  char* d_up = nullptr;
-  uint32_t* h_down = nullptr;     // pinned download staging: count[G] then candidates
-  uint32_t* d_down = nullptr;
+  char* d_up = nullptr;           // rows + capoff of the batch being scanned (stream-ordered reuse)
+  uint32_t* d_down = nullptr;     // counts + candidates of the batch being selected
+  Stage stages[2];                // host staging of two batches in flight
+  int32_t res_stamp = 0;          // resolution stamps: monotone over the session (mark / mwmark compare)
   NodeDelta* d_deltas = nullptr;
-  TaskRec* h_tasks = nullptr;    // = h_up
-  uint32_t* h_cand = nullptr;    // = h_down + G (set per batch)
-  uint32_t* h_count = nullptr;   // = h_down
   NodeDelta* h_deltas = nullptr; // pinned
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   std::vector<void*> d_allocs;

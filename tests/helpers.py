@@ -90,8 +90,11 @@ def digest_outputs(out):
                         for x in out["decisions"]])
     d["binds"] = h(sorted(out["binds"].items()))
     d["evictions"] = h(out.get("evictions", []))
-    d["nodes"] = h([[n["name"], n["idle"], n["releasing"], n["ntasks"]] for n in out["nodes"]])
-    d["jobs"] = h([[j["uid"], j["ready_num"], j["ready"], j["allocated"], None if j["ready"] else j["fit_error"]]
+    def f(v):  # the oracle prints integral doubles without a fraction: hash every resource as a float
+        return [float(x) for x in v]
+
+    d["nodes"] = h([[n["name"], f(n["idle"]), f(n["releasing"]), n["ntasks"]] for n in out["nodes"]])
+    d["jobs"] = h([[j["uid"], j["ready_num"], j["ready"], f(j["allocated"]), None if j["ready"] else j["fit_error"]]
                    for j in out["jobs"]])
     d["drf_shares"] = [j["drf_share"] for j in out["jobs"] if "drf_share" in j]
     d["queues"] = sorted(([q["uid"], q["share"], q["deserved"], q["allocated"], q["request"]] for q in out["queues"]))
