@@ -214,7 +214,7 @@ def main():
         for _ in range(warmup):
             step()
         agg = {"cycle_ms": [], "decisions": 0, "evals": 0, "visits": 0, "scan_ms": 0.0, "sel_ms": 0.0,
-               "launches": 0, "task_evals": 0, "steps": steps}
+               "launches": 0, "task_evals": 0, "steps": steps, "alloc_ms": []}
         if barrier:
             kdist.barrier()
         torch.cuda.synchronize()
@@ -230,6 +230,7 @@ def main():
             agg["sel_ms"] += st.select_kernel_ms
             agg["launches"] += st.scan_launches
             agg["task_evals"] += st.task_evaluations
+            agg["alloc_ms"].append(st.allocate_ms)
         torch.cuda.synchronize()
         agg["elapsed"] = time.perf_counter() - t_start
         if barrier:
@@ -309,7 +310,9 @@ def main():
 
     def breakdown(agg):
         s2 = agg["stats"]
-        return {"scan_ms": s2.scan_kernel_ms, "select_ms": s2.select_kernel_ms, "launches": s2.scan_launches,
+        return {"allocate_ms_p50": statistics.median(agg["alloc_ms"]), "resolve_steps": s2.resolve_steps,
+                "resolve_rechecks": s2.resolve_rechecks, "overlapped_batches": s2.overlapped,
+                "scan_ms": s2.scan_kernel_ms, "select_ms": s2.select_kernel_ms, "launches": s2.scan_launches,
                 "evaluations": s2.evaluations, "batches": s2.batches, "mispredictions": s2.mispredictions,
                 "truncations": s2.truncations, "replayed": s2.replayed, "host_engine_ms": s2.engine_ms,
                 "host_resolve_ms": s2.resolve_ms, "device_roundtrip_ms": s2.device_ms,

@@ -299,7 +299,12 @@ typedef struct kbg_stats {
   int64_t victim_host_evals; /* nodes re-evaluated on the host after a change since the last scan */
   int64_t task_evaluations;  /* node-loop runs of the reference (allocate.go:105-171: every task popped,
                                 placed or not) in the last kbg_allocate: SURVEY §8(d)'s unit */
-  int64_t reserved_stats[7];
+  int64_t resolve_steps;     /* candidate-list entries the in-order commit examined */
+  int64_t resolve_rechecks;  /* of those, nodes touched since their scan and re-checked on the host mirror */
+  int64_t overlapped;        /* batches whose scan ran while the host resolved the previous batch */
+  double update_ms;          /* wall time of the last kbg_session_update */
+  int64_t update_rebuilds;   /* kbg_session_update calls that rebuilt the static masks / device tables */
+  int64_t reserved_stats[2];
 } kbg_stats;
 
 typedef struct kbg_session kbg_session;
@@ -381,6 +386,49 @@ enum { KBG_ACTION_ALLOCATE = 0, KBG_ACTION_BACKFILL = 1, KBG_ACTION_RECLAIM = 2,
 kbg_status kbg_evictions_get(kbg_session* s, kbg_eviction* out, int32_t cap, int32_t* n_out);
 /* The action that produced decision i of the cycle's log (KBG_ACTION_*). */
 kbg_status kbg_decision_actions_get(kbg_session* s, int32_t* out, int32_t cap, int32_t* n_out);
+
+/* Resident sessions: cache events between scheduling cycles
+ * (pkg/scheduler/cache/event_handlers.go) applied to an opened session as
+ * deltas, instead of re-opening it from the next cache.Snapshot()
+ * (cache.go:549-597). The session afterwards is exactly the session
+ * kbg_session_open would build from the snapshot of the updated cache (same
+ * decisions, tested): a pod update is the cache's delete + add (the task moves
+ * to the end of its job's and its node's insertion order), a pod on a node is
+ * NodeInfo.AddTask / RemoveTask by PodKey (node_info.go:101-157, including the
+ * "already on node" and "not found" errors and updateTask's early return on
+ * the latter), a node update is SetNode's new Allocatable (a snapshot clone
+ * recomputes Idle from it). The host mirror, plugin state, pending lists and
+ * the changed node rows in HBM are refreshed; the static predicate and the
+ * device tables are rebuilt only when an event needs a class the session has
+ * not compiled, flips the ghost-pod rule or changes schedulability. */
+enum {
+  KBG_EV_POD_UPDATE = 1, /* cache.UpdatePod: `task` gets `status` and NodeName = node `node` (-1: none) */
+  KBG_EV_POD_DELETE = 2, /* cache.DeletePod: `task` leaves its job and its node */
+  KBG_EV_POD_ADD = 3,    /* cache.AddPod: a new pod of session job `job` (index = the session's task count) */
+  KBG_EV_NODE_UPDATE = 4 /* cache.UpdateNode -> NodeInfo.SetNode: node `node` gets `resource` as Allocatable,
+                            `max_task_num` pods and `unschedulable` */
+};
+typedef struct kbg_event {
+  int32_t kind;
+  int32_t task;          /* POD_UPDATE / POD_DELETE */
+  int32_t status;        /* POD_UPDATE / POD_ADD: TaskStatus (api/helpers.go:35-61) */
+  int32_t node;          /* POD_UPDATE / POD_ADD: node index of NodeName or -1; NODE_UPDATE: the node */
+  int32_t job;           /* POD_ADD */
+  int32_t spec;          /* POD_ADD: index into the session's specs, -1 = none */
+  int32_t priority;      /* POD_ADD: TaskInfo.Priority */
+  int32_t max_task_num;  /* NODE_UPDATE */
+  kbg_resource resource; /* POD_ADD: Resreq; NODE_UPDATE: Allocatable */
+  int32_t unschedulable; /* NODE_UPDATE */
+  int32_t reserved;
+  const char* uid;       /* POD_ADD: pod UID */
+  const char* pod_key;   /* POD_ADD: "<namespace>/<name>" */
+} kbg_event;
+/* Applies events[0..n) in order; the cycle state is reset as by
+ * kbg_session_reset. KBG_E_REF_PANIC: the cache itself would panic (a
+ * Resource.Sub underflow in AddTask / RemoveTask / SetNode); the session must
+ * then be re-opened. KBG_E_UNSUPPORTED (session unchanged): a removed pod whose
+ * key is held by a pod outside the session jobs, or that used host ports. */
+kbg_status kbg_session_update(kbg_session* s, const kbg_event* events, int32_t n);
 
 /* Restores the state captured at kbg_session_open (device-side copy); used to
  * re-run a cycle on the same snapshot without re-uploading it. */

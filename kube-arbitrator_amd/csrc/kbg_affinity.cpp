@@ -465,7 +465,7 @@ void setup_affinity(Session& S) {
   st.cntB.assign(C, {});
   st.cntC.assign(C, {});
   for (int32_t t = 0; t < S.n_tasks; ++t)
-    if (allocated_status(S.tasks_in[t].status)) aff_place(S, t, S.task_node[t], +1, st, false);
+    if (S.task_live[t] && allocated_status(S.tasks_in[t].status)) aff_place(S, t, S.task_node[t], +1, st, false);
   M->st = st;
   // the predictor's failed-shape flags to clear when a class gains nodes
   M->class_shapes.assign(C, {});

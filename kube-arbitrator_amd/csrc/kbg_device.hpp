@@ -61,6 +61,8 @@ struct NodeDelta {
   int32_t ntasks;
   double idle[3];
   double rel[3];
+  int32_t maxtasks;  // Allocatable pods (changes only through a session update)
+  int32_t pad;
 };
 
 // One class-mask word rewritten by the host (host-port conflicts).

@@ -256,6 +256,7 @@ __global__ __launch_bounds__(256) void kbg_apply_kernel(NodeSoA nd, const NodeDe
   nd.rel_mem[node] = d[i].rel[1];
   nd.rel_gpu[node] = d[i].rel[2];
   nd.ntasks[node] = d[i].ntasks;
+  nd.maxtasks[node] = d[i].maxtasks;
 }
 
 hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream) {
@@ -487,6 +488,7 @@ __device__ __forceinline__ void apply_node_delta(const NodeSoA& nd, const NodeDe
   nd.rel_mem[x.node] = x.rel[1];
   nd.rel_gpu[x.node] = x.rel[2];
   nd.ntasks[x.node] = x.ntasks;
+  nd.maxtasks[x.node] = x.maxtasks;
 }
 
 __device__ __forceinline__ void apply_state_delta(const VictimTables& t, const StateDelta& x) {

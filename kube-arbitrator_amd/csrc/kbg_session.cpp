@@ -31,6 +31,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -453,6 +454,7 @@ void free_device(Session& S) {
   S.h_vbits = nullptr;
   S.h_sdeltas = nullptr;
   S.vt_ready = false;
+  S.vt_allocs.clear();
   S.h_deltas = nullptr;
   for (void* p : S.d_allocs) (void)hipFree(p);
   S.d_allocs.clear();
@@ -608,9 +610,8 @@ kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
       const int32_t n = touched[i];
       if (n < S.tab_lo || n >= S.tab_lo + S.tab_n) continue;
       kbg::NodeDelta& d = S.h_deltas[cnt++];
-      int32_t mt;
       d.node = n - S.tab_lo;
-      device_row(S, n, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &mt);
+      device_row(S, n, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &d.maxtasks);
     }
     if (cnt == 0) break;
     HIP_TRY(hipMemcpyAsync(S.d_deltas, S.h_deltas, cnt * sizeof(kbg::NodeDelta), hipMemcpyHostToDevice, S.stream));
@@ -734,6 +735,8 @@ struct Resolver {
     }
     int res = -1;
     int32_t& k = cursor[g];
+    const int32_t k0 = k;
+    int64_t rechecks = 0;
     for (; k < n; ++k) {
       const int32_t nd = (int32_t)(c[k] & ~kbg::kCandPipelineBit);
       if (S.panic_node[nd]) {
@@ -747,6 +750,7 @@ struct Resolver {
         break;
       }
       // touched since the scan: re-check on the host mirror
+      ++rechecks;
       if (S.pred_active && S.ntasks[nd] >= S.maxtasks[nd]) continue;
       if ((S.has_ports || S.has_aff) &&
           !((S.h_class_mask[(size_t)S.task_class[t] * S.W + (nd >> 6)] >> (nd & 63)) & 1ull))
@@ -770,6 +774,8 @@ struct Resolver {
         break;
       }
     }
+    S.stats.resolve_steps += k - k0 + (k < n ? 1 : 0);
+    S.stats.resolve_rechecks += rechecks;
     if (sh >= 0 && res != RES_PANIC) {  // entries before k are infeasible for the shape from now on
       shape_skip[sh] = k;
       skip_stamp[sh] = skip_gen;
@@ -849,7 +855,7 @@ bool mirror_add(Session& S, int32_t t, int32_t nd, int32_t kind) {
 // Which pod keys can collide: a candidate task's key that another candidate
 // shares or that some node already holds (a StatefulSet pod recreated while
 // its predecessor is still on a node). Usually none: then nothing is tracked.
-void setup_pod_keys(Session& S, const kbg_snapshot* snap) {
+void setup_pod_keys(Session& S) {
   S.task_key.resize(S.n_tasks);
   for (int32_t t = 0; t < S.n_tasks; ++t) S.task_key[t] = S.canon[S.tasks_in[t].pod_key];
   S.key_hot.assign(S.strs.size(), 0);
@@ -857,27 +863,19 @@ void setup_pod_keys(Session& S, const kbg_snapshot* snap) {
   S.node_keys.clear();
   std::vector<uint8_t> seen(S.strs.size(), 0);
   for (int32_t t = 0; t < S.n_tasks; ++t) {
-    if (!S.pending_candidate[t] && !S.be_task[t]) continue;
+    if (!S.pending_candidate[t] && !S.be_task[t]) continue;  // (false for removed tasks)
     uint8_t& c = seen[S.task_key[t]];
     if (c) S.key_hot[S.task_key[t]] = 1;
     c = 1;
   }
-  for (int32_t n = 0; n < S.n_nodes; ++n) {
-    const kbg_node& nd = S.nodes_in[n];
-    for (int32_t i = 0; i < nd.key_len; ++i) {
-      const int32_t k = S.canon[snap->node_pod_keys[nd.key_off + i]];
+  for (int32_t n = 0; n < S.n_nodes; ++n)
+    for (int32_t k : S.node_key_order[n])
       if (seen[k]) S.key_hot[k] = 1;
-    }
-  }
   for (int32_t t = 0; t < S.n_tasks && !S.has_dupkeys; ++t) S.has_dupkeys = S.key_hot[S.task_key[t]] != 0;
   if (S.has_dupkeys)
-    for (int32_t n = 0; n < S.n_nodes; ++n) {
-      const kbg_node& nd = S.nodes_in[n];
-      for (int32_t i = 0; i < nd.key_len; ++i) {
-        const int32_t k = S.canon[snap->node_pod_keys[nd.key_off + i]];
+    for (int32_t n = 0; n < S.n_nodes; ++n)
+      for (int32_t k : S.node_key_order[n])
         if (S.key_hot[k]) S.node_keys.insert(((int64_t)n << 32) | (uint32_t)k);
-      }
-    }
   S.node_keys0 = S.node_keys;
 }
 
@@ -1084,17 +1082,21 @@ std::vector<int32_t> ranks_of(const Session& S, const std::vector<int32_t>& ids)
   return rank;
 }
 
-kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options* o, kbg_comm* comm) {
-  const auto t_open = std::chrono::steady_clock::now();
-  // opt-in phase timing of the session open (KBG_PROFILE_OPEN=1)
-  const bool prof = getenv("KBG_PROFILE_OPEN") != nullptr;
-  auto t_last = t_open;
-  auto phase = [&](const char* name) {
-    if (!prof) return;
-    const auto now = std::chrono::steady_clock::now();
-    fprintf(stderr, "[kbg open] %-24s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(now - t_last).count());
-    t_last = now;
-  };
+// ---------------------------------------------------------------- open
+// A session is built in two steps: ingest() copies the snapshot into the
+// session's own mutable inputs (the resident snapshot that kbg_session_update
+// edits), build() derives every host structure and the device tables from
+// those inputs. derive_host() is the host part of build() that an update
+// re-runs without recompiling the static predicate or reallocating HBM.
+
+int32_t intern(Session& S, const char* v) {
+  const int32_t id = (int32_t)S.strs.size();
+  S.strs.emplace_back(v ? v : "");
+  S.canon.push_back(S.canon_of.emplace(S.strs.back(), id).first->second);
+  return id;
+}
+
+kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   kbg_status st = validate(snap);
   if (st != KBG_OK) return st;
   if (o) S.opts = *o;
@@ -1102,15 +1104,14 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.K = S.opts.batch_tasks > 0 ? S.opts.batch_tasks : 8192;
   S.M = S.opts.candidates > 0 ? S.opts.candidates : 32;
   if (S.M > 4096) return fail(KBG_E_INVALID, "candidates > 4096");
-  // full-scan: K rows x M slots; grouped: sum over shapes of min(n_s + slack, 4096)
+  // full-scan: K rows x (M + rank) slots; grouped: sum over shapes of min(n_s + slack, 4096)
   S.cand_cap = S.opts.full_scan ? (int64_t)S.K * (S.M + kGroupSlack) : (int64_t)S.K * (kGroupSlack + 1);
 
   S.strs.assign(snap->strings, snap->strings + snap->n_strings);
-  {
-    std::unordered_map<std::string, int32_t> first;
-    S.canon.resize(S.strs.size());
-    for (size_t i = 0; i < S.strs.size(); ++i) S.canon[i] = first.emplace(S.strs[i], (int32_t)i).first->second;
-  }
+  S.canon_of.clear();
+  S.canon_of.reserve(S.strs.size());
+  S.canon.resize(S.strs.size());
+  for (size_t i = 0; i < S.strs.size(); ++i) S.canon[i] = S.canon_of.emplace(S.strs[i], (int32_t)i).first->second;
   S.n_nodes = snap->n_nodes;
   S.n_jobs = snap->n_jobs;
   S.n_queues = snap->n_queues;
@@ -1130,7 +1131,21 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.ports_in = copy_arr(snap->ports, snap->n_ports);
   S.pod_terms_in = copy_arr(snap->pod_terms, snap->n_pod_terms);
   S.pod_labels_in = copy_arr(snap->pod_labels, 2 * snap->n_pod_labels);
-  phase("validate+copy+strings");
+  S.others_in = copy_arr(snap->others, snap->n_others);
+  S.task_live.assign(S.n_tasks, 1);
+  // JobInfo.Tasks / NodeInfo.Tasks insertion orders, kept as lists
+  // an update reorders the way the cache's delete + add does
+  S.job_task_order.assign(S.n_jobs, {});
+  for (int32_t t = 0; t < S.n_tasks; ++t) S.job_task_order[S.tasks_in[t].job].push_back(t);
+  S.node_task_order.assign(S.n_nodes, {});
+  S.node_key_order.assign(S.n_nodes, {});
+  for (int32_t n = 0; n < S.n_nodes; ++n) {
+    const kbg_node& nd = S.nodes_in[n];
+    S.node_task_order[n].assign(snap->node_tasks + nd.task_off, snap->node_tasks + nd.task_off + nd.task_len);
+    for (int32_t i = 0; i < nd.key_len; ++i) S.node_key_order[n].push_back(S.canon[snap->node_pod_keys[nd.key_off + i]]);
+  }
+  S.node_of.clear();
+  for (int32_t n = 0; n < S.n_nodes; ++n) S.node_of[S.canon[S.nodes_in[n].name]] = n;
 
   // ---- plugins (framework.go:26-46; unknown names ignored)
   {
@@ -1181,7 +1196,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     }
   }
 
-  // ---- ranks, tasks
+  // ---- job / queue ranks (jobs and queues do not change over a resident session)
   {
     std::vector<int32_t> ids(S.n_jobs);
     for (int32_t j = 0; j < S.n_jobs; ++j) ids[j] = S.jobs_in[j].uid;
@@ -1189,9 +1204,6 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     ids.resize(S.n_queues);
     for (int32_t q = 0; q < S.n_queues; ++q) ids[q] = S.queues_in[q].uid;
     S.queue_rank = ranks_of(S, ids);
-    ids.resize(S.n_tasks);
-    for (int32_t t = 0; t < S.n_tasks; ++t) ids[t] = S.tasks_in[t].uid;
-    S.task_rank = ranks_of(S, ids);
   }
   {
     std::vector<int32_t> order(S.n_jobs);
@@ -1211,23 +1223,42 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     for (int32_t j = 0; j < S.n_jobs; ++j)
       S.job_prank[j] = (uint32_t)(std::lower_bound(prios.begin(), prios.end(), S.jobs_in[j].priority,
                                                    std::greater<int32_t>()) - prios.begin());
+    S.job_queue.resize(S.n_jobs);
+    for (int32_t j = 0; j < S.n_jobs; ++j) S.job_queue[j] = S.jobs_in[j].queue;
   }
-  S.treq.resize(S.n_tasks);
-  S.pending_candidate.assign(S.n_tasks, 0);
-  S.be_task.assign(S.n_tasks, 0);
-  for (int32_t t = 0; t < S.n_tasks; ++t) {
+  S.task_ranks_stale = true;
+  return KBG_OK;
+}
+
+enum { DERIVE_OK = 0, DERIVE_REBUILD = 1 };  // REBUILD: the static classes / masks must be recompiled
+
+// Every host structure that follows from the inputs. `sh` non-null: compile
+// the static predicate classes (build); null: keep the session's classes and
+// map each candidate task to its spec's class (update), or ask for a rebuild
+// when a candidate needs a class the session does not have.
+kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
+  *outcome = DERIVE_OK;
+  const int32_t N = S.n_nodes, T = S.n_tasks;
+  if (S.task_ranks_stale) {  // bytewise UID order (TaskOrderFn fallback); only when tasks were added
+    std::vector<int32_t> ids(T);
+    for (int32_t t = 0; t < T; ++t) ids[t] = S.tasks_in[t].uid;
+    S.task_rank = ranks_of(S, ids);
+    S.task_ranks_stale = false;
+  }
+  S.treq.resize(T);
+  S.pending_candidate.assign(T, 0);
+  S.be_task.assign(T, 0);
+  S.task_job.resize(T);
+  for (int32_t t = 0; t < T; ++t) {
     S.treq[t] = to_res(S.tasks_in[t].resreq);
+    S.task_job[t] = S.tasks_in[t].job;
+    if (!S.task_live[t]) continue;
     // allocate.go:88-96: only Pending, non-BestEffort tasks enter the node loop
     S.pending_candidate[t] = S.tasks_in[t].status == KBG_PENDING && !kbg::res_empty(S.treq[t]);
     S.be_task[t] = S.tasks_in[t].status == KBG_PENDING && kbg::res_empty(S.treq[t]);
   }
-  S.task_job.resize(S.n_tasks);
-  for (int32_t t = 0; t < S.n_tasks; ++t) S.task_job[t] = S.tasks_in[t].job;
-  S.job_queue.resize(S.n_jobs);
-  for (int32_t j = 0; j < S.n_jobs; ++j) S.job_queue[j] = S.jobs_in[j].queue;
 
   // ---- nodes
-  const int32_t N = S.n_nodes;
   S.idle.resize(N);
   S.rel.resize(N);
   S.ntasks.resize(N);
@@ -1248,32 +1279,25 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.ntasks0 = S.ntasks;
   // victim candidates (preempt/reclaim): session tasks Running on each node,
   // in NodeInfo.Tasks order; a task's node by NodeName (ssn.NodeIndex)
-  {
-    std::unordered_map<int32_t, int32_t> node_of;
-    for (int32_t n = 0; n < N; ++n) node_of[S.canon[S.nodes_in[n].name]] = n;
-    S.task_node.assign(S.n_tasks, -1);
-    for (int32_t t = 0; t < S.n_tasks; ++t) {
-      auto it = node_of.find(S.canon[S.tasks_in[t].node_name]);
-      if (it != node_of.end()) S.task_node[t] = it->second;
-    }
-    S.nt_off.assign(N + 1, 0);
-    S.nt_task.clear();
-    S.max_candidates = 0;
-    for (int32_t n = 0; n < N; ++n) {
-      const kbg_node& nd = S.nodes_in[n];
-      for (int32_t i = 0; i < nd.task_len; ++i) {
-        const int32_t t = snap->node_tasks[nd.task_off + i];
-        if (S.tasks_in[t].status == KBG_RUNNING) S.nt_task.push_back(t);
-      }
-      S.nt_off[n + 1] = (int32_t)S.nt_task.size();
-      S.max_candidates = std::max(S.max_candidates, S.nt_off[n + 1] - S.nt_off[n]);
-    }
+  S.task_node.assign(T, -1);
+  for (int32_t t = 0; t < T; ++t) {
+    auto it = S.node_of.find(S.canon[S.tasks_in[t].node_name]);
+    if (it != S.node_of.end()) S.task_node[t] = it->second;
   }
-
-  setup_pod_keys(S, snap);
+  S.nt_off.assign(N + 1, 0);
+  S.nt_task.clear();
+  S.max_candidates = 0;
+  for (int32_t n = 0; n < N; ++n) {
+    for (int32_t t : S.node_task_order[n])
+      if (S.tasks_in[t].status == KBG_RUNNING) S.nt_task.push_back(t);
+    S.nt_off[n + 1] = (int32_t)S.nt_task.size();
+    S.max_candidates = std::max(S.max_candidates, S.nt_off[n + 1] - S.nt_off[n]);
+  }
+  setup_pod_keys(S);
 
   // ---- engine initial state
   Engine& E = S.init;
+  E = Engine{};
   E.jalloc.assign(S.n_jobs, Res{});
   E.jshare.assign(S.n_jobs, 0.0);
   E.jready.assign(S.n_jobs, 0);
@@ -1283,34 +1307,34 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.q_has_attr.assign(S.n_queues, 0);
   S.q_deserved.assign(S.n_queues, Res{});
   S.q_request.assign(S.n_queues, Res{});
-
-  std::vector<std::vector<int32_t>> job_tasks(S.n_jobs);
-  for (int32_t t = 0; t < S.n_tasks; ++t) job_tasks[S.tasks_in[t].job].push_back(t);
   S.jt_off.assign(S.n_jobs + 1, 0);
   S.jt.clear();
   for (int32_t j = 0; j < S.n_jobs; ++j) {
-    S.jt.insert(S.jt.end(), job_tasks[j].begin(), job_tasks[j].end());
+    S.jt.insert(S.jt.end(), S.job_task_order[j].begin(), S.job_task_order[j].end());
     S.jt_off[j + 1] = (int32_t)S.jt.size();
   }
+  auto job_tasks = [&](int32_t j) { return std::make_pair(S.jt.begin() + S.jt_off[j], S.jt.begin() + S.jt_off[j + 1]); };
   for (int32_t j = 0; j < S.n_jobs; ++j)
-    for (int32_t t : job_tasks[j])
-      if (ready_status(S.tasks_in[t].status)) E.jready[j]++;
+    for (auto [b, e] = job_tasks(j); b != e; ++b)
+      if (ready_status(S.tasks_in[*b].status)) E.jready[j]++;
   S.job_ready0 = E.jready;
 
   // drf.go:55-78
+  S.drf_total = Res{};
+  S.prop_total = Res{};
   if (S.has_drf) {
     for (int32_t n = 0; n < N; ++n) kbg::res_add(S.drf_total, to_res(S.nodes_in[n].allocatable));
     for (int32_t j = 0; j < S.n_jobs; ++j) {
-      for (int32_t t : job_tasks[j])
-        if (allocated_status(S.tasks_in[t].status)) kbg::res_add(E.jalloc[j], S.treq[t]);
+      for (auto [b, e] = job_tasks(j); b != e; ++b)
+        if (allocated_status(S.tasks_in[*b].status)) kbg::res_add(E.jalloc[j], S.treq[*b]);
       E.jshare[j] = share_of(E.jalloc[j], S.drf_total);
     }
   }
   // proportion.go:54-144 (queue attrs in order of first job)
   if (S.has_prop) {
     for (int32_t n = 0; n < N; ++n) kbg::res_add(S.prop_total, to_res(S.nodes_in[n].allocatable));
-    for (int32_t i = 0; i < snap->n_others; ++i)
-      if (!kbg::res_sub(S.prop_total, to_res(snap->others[i])))
+    for (const kbg_resource& o : S.others_in)
+      if (!kbg::res_sub(S.prop_total, to_res(o)))
         return fail(KBG_E_REF_PANIC, "proportion: Others exceed the cluster total (proportion.go:61-63)");
     std::vector<int32_t> qorder;
     for (int32_t j = 0; j < S.n_jobs; ++j) {
@@ -1319,13 +1343,13 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
         S.q_has_attr[q] = 1;
         qorder.push_back(q);
       }
-      for (int32_t t : job_tasks[j]) {
-        const int32_t s = S.tasks_in[t].status;
+      for (auto [b, e] = job_tasks(j); b != e; ++b) {
+        const int32_t s = S.tasks_in[*b].status;
         if (allocated_status(s)) {
-          kbg::res_add(E.qalloc[q], S.treq[t]);
-          kbg::res_add(S.q_request[q], S.treq[t]);
+          kbg::res_add(E.qalloc[q], S.treq[*b]);
+          kbg::res_add(S.q_request[q], S.treq[*b]);
         } else if (s == KBG_PENDING) {
-          kbg::res_add(S.q_request[q], S.treq[t]);
+          kbg::res_add(S.q_request[q], S.treq[*b]);
         }
       }
     }
@@ -1357,14 +1381,16 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   }
 
   // ---- predicates preconditions
+  const bool had_ghost = S.ghost;
+  S.has_aff = false;
+  S.ghost = false;
   if (S.pred_active) {
-    std::unordered_set<int32_t> names;
-    for (int32_t n = 0; n < N; ++n) names.insert(S.canon[S.nodes_in[n].name]);
-    for (int32_t t = 0; t < S.n_tasks; ++t) {
+    for (int32_t t = 0; t < T; ++t) {
+      if (!S.task_live[t]) continue;
       const kbg_task& tk = S.tasks_in[t];
       const kbg_spec* sp = tk.spec >= 0 ? &S.specs_in[tk.spec] : nullptr;
       if (sp && (sp->aff_len > 0 || sp->anti_len > 0)) S.has_aff = true;  // kbg_affinity.cpp
-      if (allocated_status(tk.status) && !names.count(S.canon[tk.node_name])) S.ghost = true;
+      if (allocated_status(tk.status) && S.task_node[t] < 0) S.ghost = true;
     }
   }
 
@@ -1374,8 +1400,8 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.pend.clear();
   for (int32_t j = 0; j < S.n_jobs; ++j) {
     S.pend_off[j] = (int32_t)S.pend.size();
-    for (int32_t t : job_tasks[j])
-      if (S.pending_candidate[t]) S.pend.push_back(t);
+    for (auto [b, e] = job_tasks(j); b != e; ++b)
+      if (S.pending_candidate[*b]) S.pend.push_back(*b);
     auto b = S.pend.begin() + S.pend_off[j];
     std::sort(b, S.pend.end(), [&](int32_t a, int32_t c) {
       if (S.task_order_prio && S.tasks_in[a].priority != S.tasks_in[c].priority)
@@ -1395,12 +1421,28 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.pend_len_all = S.pend_len;
   build_heaps(S, E);
 
-  // ---- static predicates
-  phase("plugins+ranks+engine");
-  kbg::StaticHost sh;
-  compile_static_predicates(S, &sh);
-  phase("static predicates");
-  S.n_classes = sh.n_classes;
+  // ---- static predicate classes
+  if (sh) {
+    compile_static_predicates(S, sh);
+    S.n_classes = sh->n_classes;
+  } else {
+    if (S.ghost != had_ghost) {  // the ghost rule fails every node (NF_DEAD): the masks change
+      *outcome = DERIVE_REBUILD;
+      return KBG_OK;
+    }
+    S.task_class.assign(T, 0);
+    if (S.pred_active)
+      for (int32_t t = 0; t < T; ++t) {
+        if (!S.pending_candidate[t] && !S.be_task[t]) continue;
+        const int32_t sp = S.tasks_in[t].spec;
+        const int32_t c = sp >= 0 ? S.spec_class[sp] : S.nospec_class;
+        if (c < 0) {  // a pod spec no candidate had at open: compile its class
+          *outcome = DERIVE_REBUILD;
+          return KBG_OK;
+        }
+        S.task_class[t] = c;
+      }
+  }
   S.W = (N + 63) / 64;
   // ---- integer scan mode (kbg_device.hpp TaskRec): every value the scan
   // compares is an exact integer and stays one through the cycle
@@ -1412,7 +1454,7 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
       ok = exact(S.idle[n].c) && exact(S.idle[n].m) && exact(S.idle[n].g) && exact(S.rel[n].c) &&
            exact(S.rel[n].m) && exact(S.rel[n].g);
     double sum_c = 0, sum_m = 0, sum_g = 0;
-    for (int32_t t = 0; t < S.n_tasks && ok; ++t) {
+    for (int32_t t = 0; t < T && ok; ++t) {
       if (!S.pending_candidate[t]) continue;
       const Res& q = S.treq[t];
       ok = exact(q.c) && exact(q.m) && exact(q.g) && q.c >= 0 && q.m >= 0 && q.g >= 0;
@@ -1423,6 +1465,36 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     S.int_mode = ok && sum_c <= kLim && sum_m <= kLim && sum_g <= kLim &&
                  getenv("KBG_FORCE_GENERAL_SCAN") == nullptr;
   }
+  // ---- (class, request) shapes of the candidates
+  {
+    std::unordered_map<ShapeKey, int32_t, ShapeHash> ids;
+    S.task_shape.assign(T, -1);
+    for (int32_t t = 0; t < T; ++t) {
+      if (!S.pending_candidate[t]) continue;
+      auto it = ids.emplace(ShapeKey{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g}, (int32_t)ids.size());
+      S.task_shape[t] = it.first->second;
+    }
+    S.n_shapes = (int32_t)ids.size();
+    // backfill rows: one grouping id per class (the request does not matter)
+    S.be_shape.assign(std::max(1, S.n_classes), -1);
+    for (int32_t t = 0; t < T; ++t) {
+      if (!S.be_task[t]) continue;
+      int32_t& b = S.be_shape[S.task_class[t]];
+      if (b < 0) b = S.n_shapes++;
+      S.task_shape[t] = b;
+    }
+  }
+  return KBG_OK;
+}
+
+// Derived state, device tables and static masks from the session's inputs.
+kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char*)>& phase) {
+  kbg_status st;
+  kbg::StaticHost sh;
+  int outcome;
+  if ((st = derive_host(S, &sh, &outcome)) != KBG_OK) return st;
+  phase("plugins+ranks+engine+static");
+  const int32_t N = S.n_nodes;
   // ---- node-axis shards: contiguous 64-node word ranges, so
   // rank order is node order and first-fit survives the split
   S.comm = comm;
@@ -1442,27 +1514,8 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     S.tab_lo = 0;
     S.tab_n = N;
   }
-  {
-    std::unordered_map<ShapeKey, int32_t, ShapeHash> ids;
-    S.task_shape.assign(S.n_tasks, -1);
-    for (int32_t t = 0; t < S.n_tasks; ++t) {
-      if (!S.pending_candidate[t]) continue;
-      auto it = ids.emplace(ShapeKey{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g}, (int32_t)ids.size());
-      S.task_shape[t] = it.first->second;
-    }
-    S.n_shapes = (int32_t)ids.size();
-    // backfill rows: one grouping id per class (the request does not matter)
-    S.be_shape.assign(std::max(1, S.n_classes), -1);
-    for (int32_t t = 0; t < S.n_tasks; ++t) {
-      if (!S.be_task[t]) continue;
-      int32_t& b = S.be_shape[S.task_class[t]];
-      if (b < 0) b = S.n_shapes++;
-      S.task_shape[t] = b;
-    }
-  }
 
   // ---- device
-  phase("int mode+shapes");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(KBG_E_HIP, "no HIP device visible");
   S.device = S.opts.device >= 0 ? S.opts.device : 0;
@@ -1489,7 +1542,8 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   phase("device alloc+nodes");
 
   {
-    kbg::StaticTables t{};
+    kbg::StaticTables& t = S.static_tab;
+    t = kbg::StaticTables{};
     uint64_t *lb, *tb, *mp, *tp;
     int64_t* nv;
     uint8_t *nok, *nf;
@@ -1517,6 +1571,8 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
     t.reqs = rq;
     t.terms = tm;
     t.classes = cl;
+    S.d_node_flags = nf;
+    S.node_flags = sh.node_flags;
     HIP_TRY(kbg::launch_build_class_mask(t, S.n_classes, S.W, S.d_class_mask, S.stream));
     S.h_class_mask.resize((size_t)S.n_classes * S.W);
     HIP_TRY(hipMemcpyAsync(S.h_class_mask.data(), S.d_class_mask, S.h_class_mask.size() * 8, hipMemcpyDeviceToHost,
@@ -1528,17 +1584,34 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
   S.h_class_mask_static = S.h_class_mask;
   setup_host_ports(S);
   setup_affinity(S);  // inter-pod (anti)affinity: folded in the same way (kbg_affinity.cpp)
-  if (S.has_ports || S.has_aff) {
+  HIP_TRY(hipHostMalloc((void**)&S.h_mdeltas, (size_t)kbg::kMaskDeltaCap * sizeof(kbg::MaskDelta), hipHostMallocDefault));
+  if ((st = dalloc(S, &S.d_mdeltas, kbg::kMaskDeltaCap))) return st;
+  if (S.has_ports || S.has_aff)
     HIP_TRY(hipMemcpy(S.d_class_mask, S.h_class_mask.data(), S.h_class_mask.size() * 8, hipMemcpyHostToDevice));
-    HIP_TRY(hipHostMalloc((void**)&S.h_mdeltas, (size_t)kbg::kMaskDeltaCap * sizeof(kbg::MaskDelta), hipHostMallocDefault));
-    if ((st = dalloc(S, &S.d_mdeltas, kbg::kMaskDeltaCap))) return st;
-  }
   S.h_class_mask0 = S.h_class_mask;
   phase("ports+affinity");
   S.stats.n_classes = S.n_classes;
   S.stats.shards = S.R;
   S.stats.shard_index = S.comm ? S.shard : -1;
   S.stats.int_scan = S.int_mode ? 1 : 0;
+  return KBG_OK;
+}
+
+kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options* o, kbg_comm* comm) {
+  const auto t_open = std::chrono::steady_clock::now();
+  // opt-in phase timing of the session open (KBG_PROFILE_OPEN=1)
+  const bool prof = getenv("KBG_PROFILE_OPEN") != nullptr;
+  auto t_last = t_open;
+  auto phase = [&](const char* name) {
+    if (!prof) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[kbg open] %-24s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(now - t_last).count());
+    t_last = now;
+  };
+  kbg_status st = ingest(S, snap, o);
+  if (st != KBG_OK) return st;
+  phase("validate+copy+strings");
+  if ((st = build(S, comm, phase)) != KBG_OK) return st;
   S.stats.open_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_open).count();
   return KBG_OK;
 }
@@ -1944,7 +2017,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     // the next batch's scan overlaps this batch's resolve when it is ready
     Batch* nxt = next_batch(false);
     if (pred_failed) return abort(fail(KBG_E_INVALID, pred_error));
-    if (nxt && !nxt->bt.empty() && (st = launch(other, nxt)) != KBG_OK) return abort(st);
+    if (nxt && !nxt->bt.empty()) {
+      if ((st = launch(other, nxt)) != KBG_OK) return abort(st);
+      S.stats.overlapped++;
+    }
     S.stats.device_ms += ms_since(tp);
     // commit in order
     tp = clk::now();
@@ -2242,9 +2318,8 @@ kbg_status victim_push(Session& S, const std::vector<int32_t>& touched) {
       for (int32_t n : touched) {
         if (n < S.tab_lo || n >= S.tab_lo + S.tab_n) continue;
         kbg::NodeDelta& d = a.nd[a.nn++];
-        int32_t mt;
         d.node = n - S.tab_lo;
-        device_row(S, n, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &mt);
+        device_row(S, n, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &d.maxtasks);
       }
       a.ns = (int32_t)S.sdeltas.size();
       if (a.ns) std::memcpy(a.sd, S.sdeltas.data(), (size_t)a.ns * sizeof(kbg::StateDelta));
@@ -2261,9 +2336,8 @@ kbg_status victim_push(Session& S, const std::vector<int32_t>& touched) {
       const int32_t n = touched[ti];
       if (n < S.tab_lo || n >= S.tab_lo + S.tab_n) continue;  // another rank's row
       kbg::NodeDelta& d = S.h_deltas[nn++];
-      int32_t mt;
       d.node = n - S.tab_lo;
-      device_row(S, n, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &mt);
+      device_row(S, n, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &d.maxtasks);
     }
     const int32_t ns = (int32_t)std::min<size_t>(S.sdeltas.size() - si, (size_t)kbg::kMaskDeltaCap);
     if (ns > 0) std::memcpy(S.h_sdeltas, S.sdeltas.data() + si, (size_t)ns * sizeof(kbg::StateDelta));
@@ -2282,7 +2356,17 @@ kbg_status vt_setup(Session& S) {
   const size_t T = (size_t)std::max(1, S.n_tasks), J = (size_t)std::max(1, S.n_jobs),
                Q = (size_t)std::max(1, S.n_queues);
   kbg_status st;
+  if (S.vt_ready && S.vt_stale) {  // a session update changed the tasks behind them
+    for (void* p : S.vt_allocs) {
+      (void)hipFree(p);
+      S.d_allocs.erase(std::find(S.d_allocs.begin(), S.d_allocs.end(), p));
+    }
+    S.vt_allocs.clear();
+    S.vt_ready = false;
+  }
+  S.vt_stale = false;
   if (!S.vt_ready) {
+    const size_t a0 = S.d_allocs.size();
     S.W32 = kbg::kbg_victim_words(S.n_nodes);
     kbg::VictimTables& v = S.vt;
     v.ntasks = S.d_nodes.ntasks;
@@ -2312,10 +2396,13 @@ kbg_status vt_setup(Session& S) {
         (st = dalloc(S, &dja, 3 * J)) || (st = dalloc(S, &dqa, 3 * Q)) || (st = hupload(S, &dqd, qd)) ||
         (st = dalloc(S, &S.d_vbits, 2 * (size_t)S.W32)) || (st = dalloc(S, &S.d_vbits_red, 2 * (size_t)S.W32)))
       return st;
+    S.vt_allocs.assign(S.d_allocs.begin() + a0, S.d_allocs.end());
     HIP_TRY(hipMemset(S.d_vbits, 0, 2 * (size_t)S.W32 * sizeof(uint32_t)));  // other ranks' words stay 0
-    HIP_TRY(hipHostMalloc((void**)&S.h_vbits, 2 * (size_t)S.W32 * sizeof(uint32_t),
-                          hipHostMallocCoherent | hipHostMallocMapped));
-    HIP_TRY(hipHostGetDevicePointer((void**)&S.h_vbits_dev, S.h_vbits, 0));
+    if (!S.h_vbits) {
+      HIP_TRY(hipHostMalloc((void**)&S.h_vbits, 2 * (size_t)S.W32 * sizeof(uint32_t),
+                            hipHostMallocCoherent | hipHostMallocMapped));
+      HIP_TRY(hipHostGetDevicePointer((void**)&S.h_vbits_dev, S.h_vbits, 0));
+    }
     // per job, the nodes holding its tasks Running at open (the only tasks a
     // victim fn can see; their job's readiness / allocation feed the fns)
     std::vector<std::vector<int32_t>> jn(S.n_jobs);
@@ -2334,9 +2421,11 @@ kbg_status vt_setup(Session& S) {
     S.vc.panic.assign(S.W32, 0u);
     S.vc.unk.assign(S.W32, 0u);
     HIP_TRY(hipHostGetDevicePointer((void**)&S.h_deltas_dev, S.h_deltas, 0));
-    HIP_TRY(hipHostMalloc((void**)&S.h_sdeltas, (size_t)kbg::kMaskDeltaCap * sizeof(kbg::StateDelta),
-                          hipHostMallocMapped));
-    HIP_TRY(hipHostGetDevicePointer((void**)&S.h_sdeltas_dev, S.h_sdeltas, 0));
+    if (!S.h_sdeltas) {
+      HIP_TRY(hipHostMalloc((void**)&S.h_sdeltas, (size_t)kbg::kMaskDeltaCap * sizeof(kbg::StateDelta),
+                            hipHostMallocMapped));
+      HIP_TRY(hipHostGetDevicePointer((void**)&S.h_sdeltas_dev, S.h_sdeltas, 0));
+    }
     v.panic_node = dpn;
     v.nt_off = doff;
     v.nt_task = dtask;
@@ -2924,6 +3013,265 @@ kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
   return copy_log(S, out, cap, n_out, result);
 }
 
+
+// ================================================== resident session updates
+// kbgpu.h kbg_session_update. The events edit the session's inputs the way the
+// cache edits its objects (event_handlers.go:40-188, node_info.go:84-157);
+// Snapshot's clones (cache.go:549-597) then equal those inputs: a clone
+// re-adds a node's tasks to NewNodeInfo, and since Idle only decreases along
+// AddTask (Releasing pods add to Releasing, no cache pod is Pipelined) the
+// clone panics iff the final Idle drops below the tolerance, which is checked
+// on the node rows an event touches.
+
+bool terminated(int32_t status) { return status == KBG_SUCCEEDED || status == KBG_FAILED; }
+
+struct UpdateCtx {
+  std::vector<int32_t> nodes;  // node rows to rewrite in HBM
+  std::vector<uint8_t> seen;
+  bool rebuild = false;        // the static masks must be recompiled
+  void touch(int32_t n) {
+    if (!seen[n]) {
+      seen[n] = 1;
+      nodes.push_back(n);
+    }
+  }
+};
+
+// Sub with the reference's panic condition (resource_info.go:100-110)
+bool kres_sub(kbg_resource& a, const Res& r) {
+  Res x = to_res(a);
+  if (!kbg::res_sub(x, r)) return false;
+  a = to_kres(x);
+  return true;
+}
+void kres_add(kbg_resource& a, const Res& r) {
+  Res x = to_res(a);
+  kbg::res_add(x, r);
+  a = to_kres(x);
+}
+
+// NodeInfo.AddTask of session task t (node_info.go:101-129) on the inputs.
+// false: the cache would panic.
+bool in_node_add(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
+  kbg_node& nd = S.nodes_in[n];
+  const int32_t key = S.canon[S.tasks_in[t].pod_key];
+  std::vector<int32_t>& keys = S.node_key_order[n];
+  if (std::find(keys.begin(), keys.end(), key) != keys.end()) return true;  // "already on node": unchanged
+  const Res r = S.treq[t];
+  if (nd.has_node) {
+    switch (S.tasks_in[t].status) {
+      case KBG_RELEASING:
+        kres_add(nd.releasing, r);
+        if (!kres_sub(nd.idle, r)) return false;
+        break;
+      case KBG_PIPELINED:
+        if (!kres_sub(nd.releasing, r)) return false;
+        break;
+      default:
+        if (!kres_sub(nd.idle, r)) return false;
+    }
+  }
+  nd.num_tasks++;
+  keys.push_back(key);
+  S.node_task_order[n].push_back(t);
+  // the pod's host ports join the node's (a set: duplicates are harmless to setup_host_ports)
+  const int32_t sp = S.tasks_in[t].spec;
+  if (sp >= 0 && S.specs_in[sp].port_len > 0) {
+    const kbg_spec& spec = S.specs_in[sp];
+    std::vector<kbg_host_port> mine(S.ports_in.begin() + nd.port_off, S.ports_in.begin() + nd.port_off + nd.port_len);
+    for (int32_t i = 0; i < spec.port_len; ++i)
+      if (S.ports_in[spec.port_off + i].host_port > 0) mine.push_back(S.ports_in[spec.port_off + i]);
+    nd.port_off = (int32_t)S.ports_in.size();
+    nd.port_len = (int32_t)mine.size();
+    S.ports_in.insert(S.ports_in.end(), mine.begin(), mine.end());
+  }
+  U.touch(n);
+  return true;
+}
+
+// NodeInfo.RemoveTask(t) (node_info.go:131-157): the pod holding t's key
+// leaves the node. 0 removed, 1 not found (an error), else a kbg_status.
+int in_node_remove(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
+  kbg_node& nd = S.nodes_in[n];
+  const int32_t key = S.canon[S.tasks_in[t].pod_key];
+  std::vector<int32_t>& keys = S.node_key_order[n];
+  auto kit = std::find(keys.begin(), keys.end(), key);
+  if (kit == keys.end()) return 1;
+  std::vector<int32_t>& tl = S.node_task_order[n];
+  auto hit = std::find_if(tl.begin(), tl.end(), [&](int32_t u) { return S.canon[S.tasks_in[u].pod_key] == key; });
+  if (hit == tl.end())
+    return fail(KBG_E_UNSUPPORTED, "the pod key is held on the node by a pod outside the session jobs "
+                                   "(its resources are unknown): re-open the session");
+  const int32_t u = *hit;
+  const int32_t sp = S.tasks_in[u].spec;
+  if (sp >= 0 && S.specs_in[sp].has_host_ports)
+    return fail(KBG_E_UNSUPPORTED, "a pod with host ports leaves a node (its used ports are a set over "
+                                   "every pod): re-open the session");
+  const Res r = S.treq[u];
+  if (nd.has_node) {
+    switch (S.tasks_in[u].status) {
+      case KBG_RELEASING:
+        if (!kres_sub(nd.releasing, r)) return fail(KBG_E_REF_PANIC, "RemoveTask: Releasing.Sub underflow");
+        kres_add(nd.idle, r);
+        break;
+      case KBG_PIPELINED:
+        kres_add(nd.releasing, r);
+        break;
+      default:
+        kres_add(nd.idle, r);
+    }
+  }
+  nd.num_tasks--;
+  keys.erase(kit);
+  tl.erase(hit);
+  U.touch(n);
+  return 0;
+}
+
+// event_handlers.go deleteTask: the job side always, then the node side.
+// Returns 0, 1 (the node side failed: updateTask stops there) or a status.
+int in_delete_task(Session& S, UpdateCtx& U, int32_t t) {
+  std::vector<int32_t>& jl = S.job_task_order[S.tasks_in[t].job];
+  jl.erase(std::find(jl.begin(), jl.end(), t));  // JobInfo.DeleteTaskInfo
+  const std::string& nn = S.strs[S.tasks_in[t].node_name];
+  if (nn.empty()) return 0;
+  auto it = S.node_of.find(S.canon[S.tasks_in[t].node_name]);
+  if (it == S.node_of.end()) return 0;  // sc.Nodes[...] == nil
+  return in_node_remove(S, U, it->second, t);
+}
+
+kbg_status in_add_task(Session& S, UpdateCtx& U, int32_t t) {  // event_handlers.go addTask
+  S.job_task_order[S.tasks_in[t].job].push_back(t);            // JobInfo.AddTaskInfo
+  const int32_t n = S.task_node[t];
+  if (n >= 0 && !terminated(S.tasks_in[t].status) && !in_node_add(S, U, n, t))
+    return fail(KBG_E_REF_PANIC, "NodeInfo.AddTask: Resource.Sub underflow (node_info.go:117-123)");
+  return KBG_OK;
+}
+
+kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
+  auto status_ok = [](int32_t st) { return st > 0 && st <= KBG_UNKNOWN && !(st & (st - 1)); };
+  switch (e.kind) {
+    case KBG_EV_POD_UPDATE:
+    case KBG_EV_POD_DELETE: {
+      const int32_t t = e.task;
+      if (t < 0 || t >= S.n_tasks || !S.task_live[t]) return fail(KBG_E_INVALID, "event task index");
+      if (e.kind == KBG_EV_POD_UPDATE && (!status_ok(e.status) || e.node < -1 || e.node >= S.n_nodes))
+        return fail(KBG_E_INVALID, "event status / node");
+      const int r = in_delete_task(S, U, t);
+      if (r > 1) return (kbg_status)r;
+      if (e.kind == KBG_EV_POD_DELETE || r == 1) {  // deleted, or updateTask returned deleteTask's error
+        S.task_live[t] = 0;
+        return KBG_OK;
+      }
+      S.tasks_in[t].status = e.status;
+      S.tasks_in[t].node_name = e.node >= 0 ? S.nodes_in[e.node].name : intern(S, "");
+      S.task_node[t] = e.node;
+      return in_add_task(S, U, t);
+    }
+    case KBG_EV_POD_ADD: {
+      if (e.job < 0 || e.job >= S.n_jobs || e.spec < -1 || e.spec >= (int32_t)S.specs_in.size() ||
+          !status_ok(e.status) || e.node < -1 || e.node >= S.n_nodes || !e.uid || !e.pod_key)
+        return fail(KBG_E_INVALID, "POD_ADD event");
+      kbg_task k{};
+      k.uid = intern(S, e.uid);
+      k.job = e.job;
+      k.status = e.status;
+      k.priority = e.priority;
+      k.resreq = e.resource;
+      k.spec = e.spec;
+      k.node_name = e.node >= 0 ? S.nodes_in[e.node].name : intern(S, "");
+      k.pod_key = intern(S, e.pod_key);
+      const int32_t t = S.n_tasks++;
+      S.tasks_in.push_back(k);
+      S.task_live.push_back(1);
+      S.treq.push_back(to_res(k.resreq));
+      S.task_node.push_back(e.node);
+      S.task_ranks_stale = true;
+      return in_add_task(S, U, t);
+    }
+    case KBG_EV_NODE_UPDATE: {
+      if (e.node < 0 || e.node >= S.n_nodes) return fail(KBG_E_INVALID, "event node index");
+      kbg_node& nd = S.nodes_in[e.node];
+      if (!nd.has_node) return fail(KBG_E_UNSUPPORTED, "update of a node the cache only knows from a pod: re-open");
+      // SetNode (node_info.go:84-99) + the snapshot clone: Idle = Allocatable - every task
+      Res idle = to_res(nd.idle);
+      const Res a0 = to_res(nd.allocatable), a1 = to_res(e.resource);
+      idle = Res{idle.c + (a1.c - a0.c), idle.m + (a1.m - a0.m), idle.g + (a1.g - a0.g)};
+      if (nd.num_tasks > 0 && !kbg::res_le(Res{}, idle))
+        return fail(KBG_E_REF_PANIC, "NodeInfo.SetNode: Idle.Sub underflow (node_info.go:84-99)");
+      nd.idle = to_kres(idle);
+      nd.allocatable = e.resource;
+      nd.max_task_num = e.max_task_num;
+      if ((nd.unschedulable != 0) != (e.unschedulable != 0)) U.rebuild = true;  // the static masks change
+      nd.unschedulable = e.unschedulable;
+      U.touch(e.node);
+      return KBG_OK;
+    }
+  }
+  return fail(KBG_E_INVALID, "event kind");
+}
+
+kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
+  const auto t0 = std::chrono::steady_clock::now();
+  if (n < 0 || (n > 0 && !ev)) return fail(KBG_E_INVALID, "events");
+  // the cycle state goes back to "just opened"
+  S.allocated = S.backfilled = S.reclaimed = S.preempted = S.cycle_started = false;
+  UpdateCtx U;
+  U.seen.assign(S.n_nodes, 0);
+  for (int32_t i = 0; i < n; ++i) {
+    kbg_status st = apply_event(S, U, ev[i]);
+    if (st != KBG_OK) return st;
+  }
+  S.vt_stale = true;
+  S.vc.valid = false;
+  const bool had_masks = S.has_ports || S.has_aff;
+  kbg_status st = KBG_OK;
+  int outcome = DERIVE_OK;
+  if (!U.rebuild) st = derive_host(S, nullptr, &outcome);
+  if (st != KBG_OK) return st;
+  if (U.rebuild || outcome == DERIVE_REBUILD) {
+    // new static classes or node flags: recompile and rebuild the device tables
+    free_device(S);
+    const int64_t rebuilds = S.rebuilds + 1;
+    S.stats = kbg_stats{};
+    if ((st = build(S, S.comm, [](const char*) {})) != KBG_OK) return st;
+    S.rebuilds = rebuilds;
+  } else {
+    HIP_TRY(hipSetDevice(S.device));
+    // the changed node rows, into the live table and the reset copy
+    for (size_t i = 0; i < U.nodes.size();) {
+      int32_t cnt = 0;
+      for (; i < U.nodes.size() && cnt < S.K; ++i) {
+        const int32_t nd = U.nodes[i];
+        if (nd < S.tab_lo || nd >= S.tab_lo + S.tab_n) continue;
+        kbg::NodeDelta& d = S.h_deltas[cnt++];
+        d.node = nd - S.tab_lo;
+        device_row(S, nd, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &d.maxtasks);
+      }
+      if (cnt == 0) break;
+      HIP_TRY(hipMemcpyAsync(S.d_deltas, S.h_deltas, cnt * sizeof(kbg::NodeDelta), hipMemcpyHostToDevice, S.stream));
+      HIP_TRY(kbg::launch_apply(S.d_nodes0, S.d_deltas, cnt, S.stream));
+      HIP_TRY(kbg::launch_apply(S.d_nodes, S.d_deltas, cnt, S.stream));
+      HIP_TRY(hipStreamSynchronize(S.stream));  // staging reuse
+    }
+    // host ports / pod affinity live in the class masks: refold them
+    if (had_masks || S.has_ports || S.has_aff) {
+      S.h_class_mask = S.h_class_mask_static;
+      setup_host_ports(S);
+      setup_affinity(S);
+      S.mask_dirty.clear();
+      HIP_TRY(hipMemcpy(S.d_class_mask, S.h_class_mask.data(), S.h_class_mask.size() * 8, hipMemcpyHostToDevice));
+    }
+    S.h_class_mask0 = S.h_class_mask;
+    S.stats.int_scan = S.int_mode ? 1 : 0;
+  }
+  S.updates++;
+  S.update_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  S.stats.update_ms = S.update_ms;
+  S.stats.update_rebuilds = S.rebuilds;
+  return KBG_OK;
+}
+
 }  // namespace
 
 // ================================================================== C ABI
@@ -3091,6 +3439,16 @@ kbg_status kbg_session_reset(kbg_session* s) {
   if (st != KBG_OK) return st;
   HIP_TRY(hipStreamSynchronize(S.stream));
   return KBG_OK;
+}
+
+kbg_status kbg_session_update(kbg_session* s, const kbg_event* events, int32_t n) {
+  if (!s) return fail(KBG_E_INVALID, "null session");
+  HIP_TRY(hipSetDevice(s->s.device));
+  try {
+    return session_update(s->s, events, n);
+  } catch (const std::bad_alloc&) {
+    return fail(KBG_E_NOMEM, "host allocation failed");
+  }
 }
 
 kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t stop_at_first_success, int32_t* out_node,

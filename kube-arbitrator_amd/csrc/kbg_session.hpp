@@ -301,6 +301,25 @@ struct Session {
   std::vector<uint8_t> aff_gain_flag;          // per class: gained nodes since the last cut
   std::vector<int32_t> aff_gain_classes;
 
+  // ---- resident session (kbg_session_update edits the inputs above)
+  std::unordered_map<std::string, int32_t> canon_of;  // string content -> canonical id
+  std::unordered_map<int32_t, int32_t> node_of;       // canonical node name -> node index
+  std::vector<uint8_t> task_live;                     // 0: the pod was deleted (event_handlers.go deletePod)
+  std::vector<std::vector<int32_t>> job_task_order;   // per job: its tasks in JobInfo.Tasks insertion order
+  std::vector<std::vector<int32_t>> node_task_order;  // per node: the session tasks in NodeInfo.Tasks order
+  std::vector<std::vector<int32_t>> node_key_order;   // per node: PodKey (canonical id) of every pod on it
+  std::vector<kbg_resource> others_in;                // Session.Others resreq
+  bool task_ranks_stale = true;                       // tasks were added: recompute the UID ranks
+  std::vector<int32_t> spec_class;                    // per spec: its static class (-1: none compiled)
+  int32_t nospec_class = -1;                          // class of a task without a spec
+  StaticTables static_tab{};                          // device static predicate inputs (mask rebuilds)
+  uint8_t* d_node_flags = nullptr;
+  std::vector<uint8_t> node_flags;                    // host copy of the device node flags
+  double update_ms = 0;
+  int64_t updates = 0, rebuilds = 0;
+  bool vt_stale = false;                              // the victim tables follow older inputs
+  std::vector<void*> vt_allocs;                       // their HBM (freed when they are rebuilt)
+
   // ---- NodeInfo.Tasks keys (node_info.go:101-106): AddTask of a PodKey the
   // node already holds returns an error and leaves the node unchanged, while
   // ssn.Allocate / ssn.Pipeline still log the decision and run the handlers

@@ -334,6 +334,8 @@ void compile_static_predicates(Session& S, StaticHost* out) {
     c.sel_req = -1;
     c.always = 1;
     C.classes.push_back(c);
+    S.spec_class.assign(S.specs_in.size(), 0);
+    S.nospec_class = 0;
   } else {
     std::unordered_map<std::string, int32_t> class_of_key;
     std::vector<int32_t> class_spec;
@@ -354,6 +356,15 @@ void compile_static_predicates(Session& S, StaticHost* out) {
     }
     if (class_spec.empty()) class_spec.push_back(-1);
     S.class_spec = class_spec;
+    // the class of every spec (for tasks that become candidates in a session
+    // update): a spec whose key no candidate had at compile time has none
+    S.spec_class.assign(S.specs_in.size(), -1);
+    for (size_t sp = 0; sp < S.specs_in.size(); ++sp) {
+      auto it = class_of_key.find(spec_key(S, &S.specs_in[sp]));
+      if (it != class_of_key.end()) S.spec_class[sp] = it->second;
+    }
+    auto it0 = class_of_key.find(spec_key(S, nullptr));
+    S.nospec_class = it0 != class_of_key.end() ? it0->second : -1;
     for (int32_t sp : class_spec) C.classes.push_back(C.compile_spec(sp >= 0 ? &S.specs_in[sp] : nullptr));
 
     // taint dictionary over NoSchedule/NoExecute taints of the session nodes

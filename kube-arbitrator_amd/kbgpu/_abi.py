@@ -167,7 +167,20 @@ class kbg_stats(ctypes.Structure):
                 ("int_scan", i32), ("exchange_ms", f64), ("backfill_ms", f64),
                 ("reclaim_ms", f64), ("preempt_ms", f64), ("victim_scans", i64), ("victim_kernel_ms", f64),
                 ("victim_tries", i64), ("victim_host_evals", i64), ("task_evaluations", i64),
-                ("reserved_stats", i64 * 7)]
+                ("resolve_steps", i64), ("resolve_rechecks", i64), ("overlapped", i64),
+                ("update_ms", f64), ("update_rebuilds", i64), ("reserved_stats", i64 * 2)]
+
+
+EV_POD_UPDATE = 1
+EV_POD_DELETE = 2
+EV_POD_ADD = 3
+EV_NODE_UPDATE = 4
+
+
+class kbg_event(ctypes.Structure):
+    _fields_ = [("kind", i32), ("task", i32), ("status", i32), ("node", i32), ("job", i32), ("spec", i32),
+                ("priority", i32), ("max_task_num", i32), ("resource", kbg_resource), ("unschedulable", i32),
+                ("reserved", i32), ("uid", ctypes.c_char_p), ("pod_key", ctypes.c_char_p)]
 
 
 class kbg_eviction(ctypes.Structure):
@@ -194,6 +207,7 @@ SIGNATURES = {
     "kbg_evictions_get": (i32, [ctypes.c_void_p, P(kbg_eviction), i32, P(i32)]),
     "kbg_decision_actions_get": (i32, [ctypes.c_void_p, P(i32), i32, P(i32)]),
     "kbg_session_reset": (i32, [ctypes.c_void_p]),
+    "kbg_session_update": (i32, [ctypes.c_void_p, P(kbg_event), i32]),
     "kbg_select": (i32, [ctypes.c_void_p, P(i32), i32, i32, P(i32), P(i32), P(i32)]),
     "kbg_apply": (i32, [ctypes.c_void_p, i32, P(kbg_resource), i32]),
     "kbg_job_state_get": (i32, [ctypes.c_void_p, i32, P(kbg_job_state)]),

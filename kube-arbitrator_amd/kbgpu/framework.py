@@ -142,6 +142,57 @@ class Session:
             for mine, dev in ((node.idle, st.idle), (node.releasing, st.releasing)):
                 mine.milli_cpu, mine.memory, mine.milli_gpu = dev.milli_cpu, dev.memory, dev.milli_gpu
 
+    def update(self, changes):
+        """kbg_session_update: cache events since the session's snapshot,
+        applied to the resident session (include/kbgpu.h). `changes` is a list
+        of ("pod_update", pod) | ("pod_delete", pod) | ("pod_add", pod) |
+        ("node_update", node) in event order, pods and nodes as the informer
+        delivers them. New pods must use a pod spec the session already has.
+        The host-side objects (jobs / nodes of this wrapper) are not replayed:
+        read results through the C ABI (decisions, job / queue / node state)."""
+        from .api import NodeInfo, TaskInfo, pod_key
+        tidx = {t.uid: i for i, t in enumerate(self.flat.task_objs)}
+        nidx = {n: i for i, n in enumerate(self.flat.node_names)}
+        evs = (_abi.kbg_event * max(1, len(changes)))()
+        keep = []
+        for k, (kind, obj) in enumerate(changes):
+            e = evs[k]
+            if kind == "node_update":
+                ni = NodeInfo(obj)
+                e.kind = _abi.EV_NODE_UPDATE
+                e.node = nidx[obj["name"]]
+                e.resource = _abi.kbg_resource(*ni.allocatable.as_tuple())
+                e.max_task_num = ni.allocatable.max_task_num
+                e.unschedulable = 1 if obj.get("unschedulable") else 0
+                continue
+            ti = TaskInfo(obj)
+            if kind in ("pod_update", "pod_delete"):
+                e.kind = _abi.EV_POD_UPDATE if kind == "pod_update" else _abi.EV_POD_DELETE
+                e.task = tidx[obj["uid"]]
+                e.status = ti.status
+                e.node = nidx.get(ti.node_name, -1) if ti.node_name else -1
+                self.flat.task_objs[e.task] = ti
+            elif kind == "pod_add":
+                e.kind = _abi.EV_POD_ADD
+                e.job = self.flat.job_index[ti.job]
+                e.spec = self.flat.spec_index(obj)
+                e.status = ti.status
+                e.priority = ti.priority
+                e.node = nidx.get(ti.node_name, -1) if ti.node_name else -1
+                e.resource = _abi.kbg_resource(*ti.resreq.as_tuple())
+                keep += [ti.uid.encode(), pod_key(obj).encode()]
+                e.uid, e.pod_key = keep[-2], keep[-1]
+                tidx[ti.uid] = len(self.flat.task_objs)
+                self.flat.task_objs.append(ti)
+            else:
+                raise ValueError(f"unknown change {kind}")
+        _abi.check(_abi.lib().kbg_session_update(self.handle, evs, len(changes)))
+        from .api import PENDING
+        live = set(tidx)  # (deleted pods keep their index; counts only size output buffers)
+        self.flat.pending_all = max(self.flat.pending_all, sum(1 for t in self.flat.task_objs
+                                                               if t.uid in live and t.status == PENDING))
+        self.flat.pending_count = max(self.flat.pending_count, self.flat.pending_all)
+
     def job_state(self, j):
         st = _abi.kbg_job_state()
         _abi.check(_abi.lib().kbg_job_state_get(self.handle, j, ctypes.byref(st)))

@@ -174,6 +174,7 @@ class FlatSnapshot:
             spec_ids[key] = sid
             return sid
 
+        self._spec_ids, self._any_terms = spec_ids, any_terms
         for j, job in enumerate(jobs):
             r = jb[j]
             r["uid"] = S(job.uid)
@@ -195,6 +196,7 @@ class FlatSnapshot:
         tk = np.zeros(len(task_rows), dtype=np.dtype(_abi.kbg_task))
         for i, row in enumerate(task_rows):
             tk[i] = row
+        self.job_index = {job.uid: j for j, job in enumerate(jobs)}
         self.pending_count = sum(1 for t in self.task_objs if t.status == PENDING and not t.resreq.is_empty())
         self.pending_all = sum(1 for t in self.task_objs if t.status == PENDING)
 
@@ -253,6 +255,12 @@ class FlatSnapshot:
         snap.pod_labels, snap.n_pod_labels = ptr(A["pod_labels"], ctypes.c_int32), len(plabels) // 2
         snap.node_pod_keys, snap.n_node_pod_keys = ptr(A["node_pod_keys"], ctypes.c_int32), len(node_keys)
         self.snap = snap
+
+
+    def spec_index(self, pod):
+        """Index of the session spec a new pod of the same predicate inputs
+        would use (kbg_session_update POD_ADD); KeyError when it has none."""
+        return self._spec_ids[_spec_key(pod, self._any_terms)]
 
 
 # ---- wire format (include/kbgpu.h "Snapshot wire format")

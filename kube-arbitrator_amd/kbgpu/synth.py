@@ -154,6 +154,63 @@ def saturated_config(nodes=5000, jobs=2000, tasks_per_job=50, demand=1.08, seed=
             "queues": queues}
 
 
+def churn(fx, seed, session_uids, decided=(), bind=0.6, done=0.08, delete=0.03, add=0.02, node_frac=0.02):
+    """Cache events between two scheduling cycles of session `fx`
+    (kbg_session_update, event_handlers.go): binds of the last cycle's
+    Allocate decisions confirmed (the pod Running on its node), completions
+    (Running -> Succeeded: the pod leaves its node, stays in its job),
+    deletions, new pods of existing jobs (a copy of a job's pod under a new
+    UID and name) and node allocatable growth. Returns (changes, fx1): the
+    event list in order, and the fixture of the cache after them — updated pods
+    move to the end of the pod order (the cache's delete + add), and
+    `sessionOrder.jobs` keeps the job order (jobs persist in the cache)."""
+    rng = random.Random(seed)
+    pods = {p["uid"]: dict(p) for p in fx["pods"]}  # insertion order = cache order
+    changes = []
+
+    def update(p):
+        pods.pop(p["uid"], None)
+        pods[p["uid"]] = p
+        changes.append(("pod_update", p))
+
+    for d in decided:  # cache.Bind confirmed: the pod runs where the last cycle put it
+        if d["kind"] == "allocate" and rng.random() < bind:
+            p = dict(pods[d["task"]], phase="Running", nodeName=d["node"])
+            update(p)
+    for uid in list(pods):
+        p = pods[uid]
+        if uid not in session_uids or p.get("phase") != "Running":
+            continue
+        if rng.random() < done:
+            update(dict(p, phase="Succeeded"))
+    for uid in list(pods):
+        if uid in session_uids and rng.random() < delete:
+            changes.append(("pod_delete", pods.pop(uid)))
+    groups = {}
+    for p in pods.values():
+        g = (p.get("annotations") or {}).get("scheduling.k8s.io/group-name")
+        if g and p["uid"] in session_uids:
+            groups.setdefault((p.get("namespace", ""), g), p)
+    keys = sorted(groups)
+    for i in range(int(add * len(pods)) + 1):
+        if not keys:
+            break
+        base = groups[keys[rng.randrange(len(keys))]]
+        p = dict(base, uid=f"new-{seed}-{i:05d}", name=f"{base['name']}-n{i}", phase="Pending", nodeName="")
+        p.pop("deletionTimestamp", None)
+        pods[p["uid"]] = p
+        changes.append(("pod_add", p))
+    nodes = [dict(n) for n in fx["nodes"]]
+    for n in nodes:
+        if rng.random() < node_frac and "cpu" in n["allocatable"]:
+            cpu = n["allocatable"]["cpu"]
+            cores = int(cpu[:-1]) // 1000 if cpu.endswith("m") else int(float(cpu))
+            n["allocatable"] = dict(n["allocatable"], cpu=str(cores + rng.choice((1, 2, 8))))
+            changes.append(("node_update", n))
+    fx1 = dict(fx, pods=list(pods.values()), nodes=nodes)
+    return changes, fx1
+
+
 # ------------------------------------------------------------------ fuzz
 _OPS = ("In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt")
 

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 
 STRUCTS = ["kbg_resource", "kbg_node", "kbg_host_port", "kbg_taint", "kbg_job", "kbg_queue", "kbg_task", "kbg_spec", "kbg_pod_term", "kbg_term",
            "kbg_requirement", "kbg_toleration", "kbg_plugin_option", "kbg_snapshot", "kbg_options", "kbg_decision",
-           "kbg_job_state", "kbg_queue_state", "kbg_node_state", "kbg_stats", "kbg_eviction"]
+           "kbg_job_state", "kbg_queue_state", "kbg_node_state", "kbg_stats", "kbg_eviction", "kbg_event"]
 
 
 def test_struct_layouts_match_c(tmp_path):

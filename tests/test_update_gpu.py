@@ -1,0 +1,135 @@
+"""Resident sessions (kbg_session_update, include/kbgpu.h): open(S0) +
+update(events) + the cycle's actions must equal open(S1) + the same actions,
+where S1 is the snapshot of the cache after the same events
+(event_handlers.go:40-188: a pod update is delete + add, node-side AddTask /
+RemoveTask by PodKey, SetNode on a node update). The fresh-open side is also
+checked against the kbref oracle on S1."""
+import ctypes
+
+import pytest
+
+from helpers import compare_outputs, run_oracle
+
+pytestmark = pytest.mark.gpu
+
+kbgpu = pytest.importorskip("kbgpu")
+from kbgpu import _abi, synth  # noqa: E402
+from kbgpu.cache import FakeBinder, cache_from_fixture  # noqa: E402
+from kbgpu.fixture import _OrderedCache, fixture_tiers, run_fixture  # noqa: E402
+from kbgpu.framework import open_session  # noqa: E402
+from kbgpu.api import pod_key  # noqa: E402
+
+ENTRY = {"allocate": "kbg_allocate", "backfill": "kbg_backfill", "reclaim": "kbg_reclaim", "preempt": "kbg_preempt"}
+
+
+def _open(fx, opts=None):
+    return open_session(_OrderedCache(cache_from_fixture(fx, FakeBinder()), fx), fixture_tiers(fx), opts or {})
+
+
+def abi_cycle(ssn, actions):
+    """The cycle's actions through the C ABI; results in run_fixture's schema
+    (decisions, binds, job / queue / node state), without the host replay."""
+    L = _abi.lib()
+    cap = max(1, len(ssn.flat.task_objs))
+    buf = (_abi.kbg_decision * cap)()
+    n = ctypes.c_int32(0)
+    status = "ok"
+    for a in actions:
+        code = getattr(L, ENTRY[a])(ssn.handle, buf, cap, ctypes.byref(n))
+        if code == _abi.KBG_E_REF_PANIC:
+            return {"status": "ref_panic"}
+        _abi.check(code)
+    acts = (ctypes.c_int32 * cap)()
+    m = ctypes.c_int32(0)
+    _abi.check(L.kbg_decision_actions_get(ssn.handle, acts, cap, ctypes.byref(m)))
+    tasks, names = ssn.flat.task_objs, ssn.flat.node_names
+    out = {"status": status, "decisions": [], "binds": {}, "jobs": [], "queues": [], "nodes": []}
+    for i in range(n.value):
+        d = buf[i]
+        row = {"task": tasks[d.task].uid, "job": tasks[d.task].job, "node": names[d.node],
+               "kind": "allocate" if d.kind == _abi.KIND_ALLOCATE else "pipeline", "dispatched_at": d.dispatched_at}
+        if acts[i] != 0:
+            row["action"] = _abi.ACTION_NAMES[acts[i]]
+        out["decisions"].append(row)
+        if d.dispatched_at >= 0:
+            out["binds"][pod_key(tasks[d.task].pod)] = names[d.node]
+    for j, job in enumerate(ssn.jobs):
+        st = ssn.job_state(j)
+        row = {"uid": job.uid, "ready_num": st.ready_num, "ready": bool(st.ready), "drf_share": st.drf_share}
+        if st.fit_valid:
+            from kbgpu.fixture import fit_error
+            row["fit_error"] = fit_error(st.fit_nodes, st.fit_cpu, st.fit_memory, st.fit_gpu)
+        out["jobs"].append(row)
+    for q, queue in enumerate(ssn.queues):
+        st = ssn.queue_state(q)
+        if st.has_attr:
+            out["queues"].append({"uid": queue.uid, "share": st.share,
+                                  "deserved": [st.deserved.milli_cpu, st.deserved.memory, st.deserved.milli_gpu]})
+    for i, nd in enumerate(ssn.nodes):
+        st = ssn.node_state(i)
+        out["nodes"].append({"name": nd.name, "idle": [st.idle.milli_cpu, st.idle.memory, st.idle.milli_gpu],
+                             "releasing": [st.releasing.milli_cpu, st.releasing.memory, st.releasing.milli_gpu],
+                             "ntasks": st.num_tasks})
+    return out
+
+
+def check_update(fx0, seed, opts=None, rounds=1):
+    actions = fx0.get("actions") or ["allocate"]
+    ssn = _open(fx0, opts)
+    try:
+        fx = dict(fx0, sessionOrder={"jobs": [j.uid for j in ssn.jobs], "nodes": list(ssn.flat.node_names)})
+        ref0 = run_oracle(fx)
+        for r in range(rounds):
+            uids = {t.uid for t in ssn.flat.task_objs}
+            decided = ref0.get("decisions", []) if ref0["status"] == "ok" else []
+            changes, fx1 = synth.churn(fx, seed * 31 + r, uids, decided)
+            try:
+                ssn.update(changes)
+            except _abi.KbgError as e:
+                if e.status == "unsupported":
+                    pytest.skip(str(e))
+                raise
+            got = abi_cycle(ssn, actions)
+            fresh, fssn = run_fixture(fx1, opts)
+            ref1 = run_oracle(fx1)
+            compare_outputs(ref1, fresh)  # the fresh open of S1 agrees with the oracle
+            assert got["status"] == fresh["status"], (got, fresh.get("error"))
+            if fresh["status"] == "ok":
+                assert got["decisions"] == fresh["decisions"]
+                assert got["binds"] == fresh["binds"]
+                assert got["nodes"] == fresh["nodes"]
+                for a, b in zip(got["jobs"], fresh["jobs"]):
+                    assert (a["uid"], a["ready_num"], a["ready"], a.get("fit_error")) == \
+                           (b["uid"], b["ready_num"], b["ready"], b.get("fit_error")), (a, b)
+                    if "drf_share" in b:
+                        assert a["drf_share"] == b["drf_share"]
+                for a, b in zip(got["queues"], fresh["queues"]):
+                    assert a["uid"] == b["uid"] and a["share"] == b["share"] and a["deserved"] == b["deserved"]
+            if fssn:
+                fssn.close()
+            _abi.check(_abi.lib().kbg_session_reset(ssn.handle))
+            fx, ref0 = fx1, ref1
+    finally:
+        ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(120))
+def test_update_fuzz(seed):
+    fx = synth.random_fixture(7000 + seed)
+    check_update(fx, seed, {"batch_tasks": 1 + seed % 9, "candidates": 1 + seed % 5, "full_scan": seed % 2},
+                 rounds=2)
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_update_contended(seed):
+    check_update(synth.contended_fixture(8000 + seed, nodes=20, jobs=16, tasks=8), seed, rounds=2)
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_update_affinity(seed):
+    check_update(synth.affinity_fixture(9000 + seed), seed, rounds=2)
+
+
+@pytest.mark.parametrize("cid", [1, 2])
+def test_update_configs(cid):
+    check_update(synth.config_fixture(cid), cid, rounds=3)
