@@ -904,9 +904,14 @@ void setup_host_ports(Session& S) {
   };
   std::vector<std::vector<int32_t>> want(C);
   bool any = false;
+  // only classes some candidate task uses (a resident session keeps classes
+  // whose tasks have left; they must not switch the port machinery on)
+  std::vector<uint8_t> in_use(C, 0);
+  for (int32_t t = 0; t < S.n_tasks; ++t)
+    if (S.pending_candidate[t] || S.be_task[t]) in_use[S.task_class[t]] = 1;
   for (int32_t c = 0; c < C; ++c) {
     const int32_t sp = S.class_spec[c];
-    if (sp < 0) continue;
+    if (sp < 0 || !in_use[c]) continue;
     const kbg_spec& spec = S.specs_in[sp];
     for (int32_t i = 0; i < spec.port_len; ++i) {
       const kbg_host_port& hp = S.ports_in[spec.port_off + i];

@@ -196,7 +196,7 @@ def churn(fx, seed, session_uids, decided=(), bind=0.6, done=0.08, delete=0.03, 
         if not keys:
             break
         base = groups[keys[rng.randrange(len(keys))]]
-        p = dict(base, uid=f"new-{seed}-{i:05d}", name=f"{base['name']}-n{i}", phase="Pending", nodeName="")
+        p = dict(base, uid=f"new-{seed}-{i:05d}", name=f"{base['name']}-n{seed}-{i}", phase="Pending", nodeName="")
         p.pop("deletionTimestamp", None)
         pods[p["uid"]] = p
         changes.append(("pod_add", p))

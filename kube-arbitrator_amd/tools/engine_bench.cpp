@@ -38,3 +38,35 @@ extern "C" double kbg_tool_engine_ns_per_step(const kbg_snapshot* snap, const kb
             (double)prof.apply / prof.steps, (double)prof.jtop / prof.steps, (double)prof.qpush / prof.steps);
   return best;
 }
+
+// Host side of kbg_session_update without a device: opens the snapshot's host
+// state, applies the events to the inputs and re-derives; returns the node
+// rows (Idle, Releasing, task count) and the pending candidates in job order,
+// for comparison with a fresh snapshot of the updated cache (CPU test).
+extern "C" int32_t kbg_tool_update_nodes(const kbg_snapshot* snap, const kbg_options* o, const kbg_event* ev,
+                                         int32_t n, double* idle, double* rel, int32_t* ntasks, int32_t* pend,
+                                         int32_t* n_pend) {
+  kbg::Session S;
+  if (ingest(S, snap, o) != KBG_OK) return -1;
+  kbg::StaticHost sh;
+  int outcome;
+  if (derive_host(S, &sh, &outcome) != KBG_OK) return -2;
+  S.n_classes = sh.n_classes;
+  UpdateCtx U;
+  U.seen.assign(S.n_nodes, 0);
+  for (int32_t i = 0; i < n; ++i)
+    if (apply_event(S, U, ev[i]) != KBG_OK) return -3;
+  if (derive_host(S, nullptr, &outcome) != KBG_OK) return -4;
+  for (int32_t k = 0; k < S.n_nodes; ++k) {
+    idle[3 * k] = S.idle[k].c;
+    idle[3 * k + 1] = S.idle[k].m;
+    idle[3 * k + 2] = S.idle[k].g;
+    rel[3 * k] = S.rel[k].c;
+    rel[3 * k + 1] = S.rel[k].m;
+    rel[3 * k + 2] = S.rel[k].g;
+    ntasks[k] = S.ntasks[k];
+  }
+  *n_pend = (int32_t)S.pend_all.size();
+  std::copy(S.pend_all.begin(), S.pend_all.end(), pend);
+  return outcome;
+}

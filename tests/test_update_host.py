@@ -1,0 +1,130 @@
+"""Host side of kbg_session_update on the CPU (no device): the session's
+inputs after a sequence of cache events must equal a fresh snapshot of the
+cache after them — node Idle / Releasing / task count, and the pending lists
+in TaskOrderFn order (event_handlers.go:40-188, node_info.go:84-157). Runs
+through the developer tool library (kube-arbitrator_amd/tools/engine_bench.cpp),
+which drives the same ingest / apply_event / derive_host code as the library."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+from helpers import ROOT, run_oracle
+
+PKG = os.path.join(ROOT, "kube-arbitrator_amd")
+TOOLS = os.path.join(PKG, "tools", "libkbg_tools.so")
+
+
+@pytest.fixture(scope="module")
+def tools():
+    subprocess.run(["make", "-s", "-C", PKG, "tools"], check=True)
+    L = ctypes.CDLL(TOOLS)
+    L.kbg_tool_update_nodes.restype = ctypes.c_int32
+    return L
+
+
+def flat(fx):
+    from kbgpu.cache import FakeBinder, cache_from_fixture
+    from kbgpu.fixture import _OrderedCache, fixture_tiers
+    from kbgpu.snapshot import FlatSnapshot
+    s = _OrderedCache(cache_from_fixture(fx, FakeBinder()), fx).snapshot()
+    return FlatSnapshot(s.nodes, s.jobs, s.queues, s.others, fixture_tiers(fx)), s
+
+
+def events(f0, changes):
+    """framework.Session.update's event marshaling, against flat snapshot f0."""
+    from kbgpu import _abi
+    from kbgpu.api import NodeInfo, TaskInfo, pod_key
+    tidx = {t.uid: i for i, t in enumerate(f0.task_objs)}
+    nidx = {n: i for i, n in enumerate(f0.node_names)}
+    evs = (_abi.kbg_event * max(1, len(changes)))()
+    keep = []
+    for k, (kind, obj) in enumerate(changes):
+        e = evs[k]
+        if kind == "node_update":
+            ni = NodeInfo(obj)
+            e.kind, e.node = _abi.EV_NODE_UPDATE, nidx[obj["name"]]
+            e.resource = _abi.kbg_resource(*ni.allocatable.as_tuple())
+            e.max_task_num = ni.allocatable.max_task_num
+            e.unschedulable = 1 if obj.get("unschedulable") else 0
+            continue
+        ti = TaskInfo(obj)
+        e.status = ti.status
+        e.node = nidx.get(ti.node_name, -1) if ti.node_name else -1
+        if kind == "pod_add":
+            e.kind, e.job, e.spec, e.priority = _abi.EV_POD_ADD, f0.job_index[ti.job], f0.spec_index(obj), ti.priority
+            e.resource = _abi.kbg_resource(*ti.resreq.as_tuple())
+            keep += [ti.uid.encode(), pod_key(obj).encode()]
+            e.uid, e.pod_key = keep[-2], keep[-1]
+            tidx[ti.uid] = len(tidx)
+        else:
+            e.kind = _abi.EV_POD_UPDATE if kind == "pod_update" else _abi.EV_POD_DELETE
+            e.task = tidx[obj["uid"]]
+    return evs, keep, tidx
+
+
+def check(tools, fx0, seed, rounds):
+    from kbgpu import _abi, synth
+    from kbgpu.api import PENDING, RefPanic
+    try:
+        f0, s0 = flat(fx0)
+    except RefPanic:
+        pytest.skip("S0 panics in the cache")
+    fx = dict(fx0, sessionOrder={"jobs": [j.uid for j in s0.jobs], "nodes": list(f0.node_names)})
+    uids = {t.uid for t in f0.task_objs}
+    changes, cur = [], fx
+    ref = run_oracle(cur)
+    for r in range(rounds):
+        ch, nxt = synth.churn(cur, seed * 31 + r, uids, ref["decisions"] if ref["status"] == "ok" else [])
+        changes += ch
+        uids |= {p["uid"] for kind, p in ch if kind == "pod_add"}
+        cur = nxt
+        if r + 1 < rounds:
+            ref = run_oracle(cur)
+    try:
+        f1, s1 = flat(cur)
+    except RefPanic:
+        pytest.skip("S1 panics in the cache")
+    evs, keep, tidx = events(f0, changes)
+    N = len(f0.node_names)
+    idle, rel = (ctypes.c_double * (3 * N))(), (ctypes.c_double * (3 * N))()
+    nt = (ctypes.c_int32 * max(1, N))()
+    pend = (ctypes.c_int32 * max(1, len(tidx)))()
+    npend = ctypes.c_int32()
+    rc = tools.kbg_tool_update_nodes(ctypes.byref(f0.snap), ctypes.byref(_abi.kbg_options()), evs, len(changes),
+                                     idle, rel, nt, pend, ctypes.byref(npend))
+    tools.kbg_last_error.restype = ctypes.c_char_p
+    err = tools.kbg_last_error().decode() if rc < 0 else ""
+    if rc == -2:
+        pytest.skip("S0 open panics")
+    if rc == -3 and ("unsupported" in err or "host ports" in err or "outside the session" in err):
+        pytest.skip(err)
+    assert rc in (0, 1), (rc, err)  # 1: a rebuild was needed (new class / ghost rule)
+    A = f1.arrays["nodes"]
+    for i in range(N):
+        assert list(A[i]["idle"]) == list(idle[3 * i:3 * i + 3]), i
+        assert list(A[i]["releasing"]) == list(rel[3 * i:3 * i + 3]), i
+        assert A[i]["num_tasks"] == nt[i], i
+    if rc == 0:
+        inv = {i: u for u, i in tidx.items()}
+        fresh_pend = set(t.uid for job in s1.jobs for t in job.tasks.values()
+                         if t.status == PENDING and not t.resreq.is_empty())
+        assert {inv[pend[i]] for i in range(npend.value)} == fresh_pend
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_update_host_fuzz(tools, seed):
+    from kbgpu import synth
+    check(tools, synth.random_fixture(7000 + seed), seed, 2)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_update_host_contended(tools, seed):
+    from kbgpu import synth
+    check(tools, synth.contended_fixture(8000 + seed, nodes=20, jobs=16, tasks=8), seed, 3)
+
+
+def test_update_host_c1(tools):
+    from kbgpu import synth
+    check(tools, synth.config_fixture(1), 1, 3)
