@@ -24,7 +24,9 @@
 // mirror. An unpredicted outcome or an exhausted candidate list cuts the
 // batch; the engine is restored from a checkpoint and replayed to the cut.
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 #include <rccl/rccl.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -630,7 +632,9 @@ kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
 // commit can exhaust at most one node of the list, so a row rarely runs out
 // before the table does. Grouped mode: one row per distinct shape with (tasks
 // of the shape + slack) slots; tasks of a shape share the row and a cursor.
-constexpr int32_t kGroupSlack = 512;  // extra candidate slots per shape row (grouped) / rank cap (full-scan)
+constexpr int32_t kGroupSlack = 512;     // extra candidate slots per shape row (grouped mode)
+constexpr int32_t kFullScanGrow = 1024;  // cap on a full-scan row's extra slots
+constexpr int32_t kFullScanK = 8192;     // default batch of the full-scan mode
 
 struct Grouper {
   Session& S;
@@ -681,9 +685,27 @@ struct Grouper {
     for (int32_t g = G; g < Gp; ++g) sg.h_tasks[g] = sg.h_tasks[0];  // padding rows: scanned, never stored
     sg.h_capoff = (uint32_t*)(sg.h_up + (size_t)Gp * sizeof(kbg::TaskRec));
     sg.h_capoff[0] = 0;
+    // full-scan: rows of one shape in one scan evaluate identical inputs
+    // against the same table, so their lists are one sequence cut at
+    // different lengths. Every row keeps M slots; the shape's last row keeps
+    // a long list (every commit before it can exhaust one node), and a row
+    // whose own M run out continues in it (Resolver) instead of a rescan.
+    if (S.opts.full_scan) {
+      sg.row_ext.resize(G);
+      for (int32_t g = 0; g < G; ++g) sg.row_ext[g] = shape_row[sg.row_shape[g]];
+    }
+    int32_t grow_cap = kFullScanGrow;
+    if (S.opts.full_scan) {  // more shapes than the buffers were sized for: shorter long lists
+      int64_t longs = 0;
+      for (int32_t g = 0; g < G; ++g) longs += sg.row_ext[g] == g;
+      const int64_t spare = S.cand_cap - (int64_t)G * S.M;
+      if (longs * kFullScanGrow > spare) grow_cap = (int32_t)std::max<int64_t>(0, spare / std::max<int64_t>(1, longs));
+    }
     for (int32_t g = 0; g < G; ++g) {
-      const uint32_t want = S.opts.full_scan ? (uint32_t)(S.M + std::min(count[g], kGroupSlack))
-                                             : (uint32_t)std::min(count[g] + kGroupSlack, 4096);
+      uint32_t want;
+      if (!S.opts.full_scan) want = (uint32_t)std::min(count[g] + kGroupSlack, 4096);
+      else if (sg.row_ext[g] != g) want = (uint32_t)S.M;
+      else want = (uint32_t)(S.M + std::min(2 * count[g] + (g >> 3) + 64, grow_cap));
       sg.h_capoff[g + 1] = sg.h_capoff[g] + want;
     }
     return G;
@@ -731,13 +753,26 @@ struct Resolver {
     int32_t sh = -1;
     if (S.opts.full_scan) {
       sh = sg->row_shape[g];
-      if (skip_stamp[sh] == skip_gen) cursor[g] = std::max(cursor[g], std::min(shape_skip[sh], n));
+      // the skip may pass this row's own M entries: the loop moves to the long list
+      if (skip_stamp[sh] == skip_gen) cursor[g] = std::max(cursor[g], shape_skip[sh]);
     }
     int res = -1;
     int32_t& k = cursor[g];
     const int32_t k0 = k;
     int64_t rechecks = 0;
-    for (; k < n; ++k) {
+    int32_t n_end = n;
+    uint32_t cnt_end = cnt;
+    for (;; ++k) {
+      if (k >= n_end) {  // full-scan: continue in the shape's longest list of this scan
+        if (sh < 0 || !(cnt_end & kbg::kCountIncompleteBit)) break;
+        const int32_t g2 = sg->row_ext[g];
+        const uint32_t cnt2 = sg->h_count[g2];
+        if (g2 == g || (int32_t)(cnt2 & kbg::kCountMask) <= n_end) break;
+        c = sg->h_cand + sg->h_capoff[g2];
+        n_end = (int32_t)(cnt2 & kbg::kCountMask);
+        cnt_end = cnt2;
+        if (k >= n_end) break;
+      }
       const int32_t nd = (int32_t)(c[k] & ~kbg::kCandPipelineBit);
       if (S.panic_node[nd]) {
         res = RES_PANIC;
@@ -774,14 +809,14 @@ struct Resolver {
         break;
       }
     }
-    S.stats.resolve_steps += k - k0 + (k < n ? 1 : 0);
+    S.stats.resolve_steps += k - k0 + (k < n_end ? 1 : 0);
     S.stats.resolve_rechecks += rechecks;
     if (sh >= 0 && res != RES_PANIC) {  // entries before k are infeasible for the shape from now on
       shape_skip[sh] = k;
       skip_stamp[sh] = skip_gen;
     }
     if (res >= 0) return res;
-    if (cnt & kbg::kCountIncompleteBit) return RES_TRUNC;
+    if (cnt_end & kbg::kCountIncompleteBit) return RES_TRUNC;
     *node = -1;
     return RES_OK;
   }
@@ -1106,11 +1141,11 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   if (st != KBG_OK) return st;
   if (o) S.opts = *o;
   S.heap_go111 = S.opts.heap_rule == 0;
-  S.K = S.opts.batch_tasks > 0 ? S.opts.batch_tasks : 8192;
+  S.K = S.opts.batch_tasks > 0 ? S.opts.batch_tasks : (S.opts.full_scan ? kFullScanK : 8192);
   S.M = S.opts.candidates > 0 ? S.opts.candidates : 32;
   if (S.M > 4096) return fail(KBG_E_INVALID, "candidates > 4096");
   // full-scan: K rows x (M + rank) slots; grouped: sum over shapes of min(n_s + slack, 4096)
-  S.cand_cap = S.opts.full_scan ? (int64_t)S.K * (S.M + kGroupSlack) : (int64_t)S.K * (kGroupSlack + 1);
+
 
   S.strs.assign(snap->strings, snap->strings + snap->n_strings);
   S.canon_of.clear();
@@ -1520,6 +1555,13 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
     S.tab_n = N;
   }
 
+  // candidate slots: grouped, sum over shapes of min(n_s + slack, 4096) <= K (slack + 1);
+  // full-scan, K rows x M plus the long list of each shape's last row (sessions
+  // that gain shapes in an update share what is left: Grouper::build)
+  S.n_shapes_cap = std::max(S.n_shapes, 64);
+  S.cand_cap = S.opts.full_scan
+                   ? (int64_t)S.K * S.M + (int64_t)std::min(S.K, S.n_shapes_cap) * (kFullScanGrow + S.M)
+                   : (int64_t)S.K * (kGroupSlack + 1);
   // ---- device
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(KBG_E_HIP, "no HIP device visible");
@@ -1651,6 +1693,50 @@ struct Pipe {
   bool stop = false;
   static constexpr size_t kDepth = 3;
 };
+
+// The predictor and the committer exchange batches, the failed-shape flags
+// and the engine checkpoints: keep the predictor on another physical core of
+// the committer's last-level cache (sysfs topology), never on its SMT
+// sibling. KBG_NO_PIN=1 leaves placement to the OS.
+void pin_near(int cpu) {
+  static const bool off = getenv("KBG_NO_PIN") != nullptr;
+  if (off || cpu < 0) return;
+  auto read_list = [](const std::string& path) {
+    std::vector<int> out;
+    FILE* f = std::fopen(path.c_str(), "r");
+    if (!f) return out;
+    char buf[4096];
+    const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+    std::fclose(f);
+    buf[n] = 0;
+    for (char* p = buf; *p;) {  // "0-7,128-135"
+      char* e;
+      const long a = std::strtol(p, &e, 10);
+      if (e == p) break;
+      long b = a;
+      if (*e == '-') b = std::strtol(e + 1, &e, 10);
+      for (long c = a; c <= b; ++c) out.push_back((int)c);
+      p = (*e == ',') ? e + 1 : e;
+      if (*p == '\n') break;
+    }
+    return out;
+  };
+  const std::string base = "/sys/devices/system/cpu/cpu" + std::to_string(cpu);
+  const std::vector<int> llc = read_list(base + "/cache/index3/shared_cpu_list");
+  const std::vector<int> smt = read_list(base + "/topology/thread_siblings_list");
+  cpu_set_t allowed;
+  if (llc.empty() || sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
+  const size_t at = std::find(llc.begin(), llc.end(), cpu) - llc.begin();
+  for (size_t k = 1; k <= llc.size(); ++k) {  // the next core after the committer's
+    const int c = llc[(at + k) % llc.size()];
+    if (std::find(smt.begin(), smt.end(), c) != smt.end() || !CPU_ISSET(c, &allowed)) continue;
+    cpu_set_t one;
+    CPU_ZERO(&one);
+    CPU_SET(c, &one);
+    (void)pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+    return;
+  }
+}
 
 // Last node-loop run of a job: the task, how many decisions preceded it and
 // where it ended (node -1 = fitted nowhere).
@@ -1874,7 +1960,9 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   std::string pred_error;
   EngineProfile eprof;
   eprof.on = getenv("KBG_PROFILE_ENGINE") != nullptr;
+  const int committer_cpu = sched_getcpu();
   std::thread predictor([&]() {
+    pin_near(committer_cpu);
     Ops ops{S, E, eprof.on ? &eprof : nullptr};
     bool exhausted = false;
     for (;;) {
@@ -1999,6 +2087,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     finish();
     return st;
   };
+  // opt-in cycle counters of the in-order commit (KBG_PROFILE_RESOLVE=1):
+  // candidate walk, host mirror, decision log, whole loop
+  const bool rprof = getenv("KBG_PROFILE_RESOLVE") != nullptr;
+  uint64_t rcyc[4] = {0, 0, 0, 0};
   int si = 0;
   Batch* cur = next_batch(true);
   if (!cur) {
@@ -2038,10 +2130,20 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     int32_t seg = 0;  // first batch entry covered by the current scan of this stage
     bool panic = false;
     int32_t rstamp = stamp;
-    for (int32_t i = 0; i < (int32_t)bt.size(); ++i) {
+    const uint64_t cl0 = rprof ? cycles() : 0;
+    const int32_t nb = (int32_t)bt.size();
+    for (int32_t i = 0; i < nb; ++i) {
       const int32_t t = bt[i];
+      if (i + 8 < nb) {  // task-indexed rows of the tasks ahead (batch order is not index order)
+        const int32_t t8 = bt[i + 8];
+        __builtin_prefetch(&S.treq[t8]);
+        __builtin_prefetch(&S.task_job[t8]);
+        __builtin_prefetch(&last[S.task_job[bt[i + 4]]]);
+      }
       int32_t node = -1, kind = 0;
+      const uint64_t c0 = rprof ? cycles() : 0;
       int r = rs.resolve(sg->row_of[i - seg], t, &node, &kind);
+      if (rprof) rcyc[0] += cycles() - c0;
       if (r == RES_TRUNC) {
         // A candidate list ran out before the table did. The predictions
         // still hold (no outcome differed), so instead of cutting the batch
@@ -2081,12 +2183,18 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         if (S.has_ports)
           dec_oldp.insert(dec_oldp.end(), S.node_ports.begin() + (size_t)node * S.PW,
                           S.node_ports.begin() + (size_t)(node + 1) * S.PW);
+        const uint64_t c1 = rprof ? cycles() : 0;
         const bool dup = mirror_add(S, t, node, kind);
         if (mark[node] != rstamp) {
           mark[node] = rstamp;
           touched.push_back(node);
         }
+        const uint64_t c2 = rprof ? cycles() : 0;
         record_decision(S, t, node, kind, dup);
+        if (rprof) {
+          rcyc[1] += c2 - c1;
+          rcyc[2] += cycles() - c2;
+        }
       } else {
         failed[S.task_shape[t]].store(1, std::memory_order_relaxed);
       }
@@ -2110,6 +2218,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         break;
       }
     }
+    if (rprof) rcyc[3] += cycles() - cl0;
     S.stats.resolve_ms += ms_since(tp);
     tp = clk::now();
     if ((st = push_deltas(S, touched)) != KBG_OK) return abort(st);
@@ -2177,6 +2286,12 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   S.fin = E;
   S.stats.engine_ms = engine_ms;
   S.stats.replayed = replayed;
+  if (rprof)
+    fprintf(stderr, "[kbg resolve] %lld tasks, cycles/task: walk %.1f mirror %.1f log %.1f loop %.1f (incl. rescans)\n",
+            (long long)S.stats.task_evaluations, (double)rcyc[0] / std::max<int64_t>(1, S.stats.task_evaluations),
+            (double)rcyc[1] / std::max<int64_t>(1, S.stats.task_evaluations),
+            (double)rcyc[2] / std::max<int64_t>(1, S.stats.task_evaluations),
+            (double)rcyc[3] / std::max<int64_t>(1, S.stats.task_evaluations));
   if (eprof.on && eprof.steps)
     fprintf(stderr, "[kbg engine] steps %llu cycles/step: qpop %.1f apply %.1f jfix %.1f qpush %.1f (engine %.3f ms)\n",
             (unsigned long long)eprof.steps, (double)eprof.qpop / eprof.steps, (double)eprof.apply / eprof.steps,

@@ -163,6 +163,7 @@ struct Stage {
   uint32_t* h_cand = nullptr;        // = h_down + G
   std::vector<int32_t> row_of;       // batch entry -> evaluation row
   std::vector<int32_t> row_shape;    // evaluation row -> (class, request) shape
+  std::vector<int32_t> row_ext;      // full-scan: the last (longest-list) row of the row's shape in this scan
   int32_t G = 0;
   int32_t base = 0;                  // the scan saw every node delta of resolutions with stamp <= base
   bool inflight = false;             // launched, results not yet collected
@@ -343,6 +344,7 @@ struct Session {
   int32_t n_classes = 0;
   int32_t K = 0, M = 0;     // batch tasks, candidates per row (full-scan) / slack (grouped)
   int64_t cand_cap = 0;     // candidate slots allocated
+  int32_t n_shapes_cap = 0; // upper bound on the shapes of one scan (cand_cap sizing)
   NodeSoA d_nodes{};
   NodeSoA d_nodes0{};       // pristine copy for kbg_session_reset
   uint64_t* d_class_mask = nullptr;
