@@ -167,6 +167,7 @@ def main():
     ap.add_argument("--candidates", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-faithful", action="store_true", help="skip the 60 s B-faithful CPU baseline")
+    ap.add_argument("--no-resident", action="store_true", help="skip the resident-session (kbg_session_update) lines")
     ap.add_argument("--comm", action="store_true",
                     help="open the session through the RCCL sharded entry point even at N=1 (rehearsal)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on MI355X; gloo to rehearse on one GPU")
@@ -354,6 +355,8 @@ def main():
         "open_ms": st.open_ms,
         "open_ms_first_in_process": open_ms_first,
     }
+    if world == 1 and not args.no_resident:
+        line["resident_session"] = resident_bench(cache, fx, base_opts)
     if rank == 0 and not args.no_cpu_baseline:
         # C4 cannot finish on one thread within minutes: bounded samples there
         budget = 60.0 if cid >= 4 else 0.0
@@ -366,6 +369,90 @@ def main():
     if comm is not None:
         comm.close()
     kdist.shutdown()
+
+
+def resident_bench(cache, fx, base_opts, steps=5, churn=0.01, seed=5):
+    """Resident session (kbg_session_update, include/kbgpu.h) on the same
+    cluster: open once, run a cycle, confirm every Allocate decision's bind
+    as a cache event (the pod Running on its node), then `steps` cycles of
+    churn — `churn` x pods complete (Running -> Succeeded, they leave their
+    nodes) and as many new pods arrive for random jobs (copies of a job's pod
+    spec and request) — each an update plus an allocate cycle. Times are the
+    library's own (kbg_stats.update_ms / allocate_ms); the events are built
+    in numpy, outside the timed calls."""
+    import random
+    from kbgpu import _abi
+    from kbgpu.fixture import fixture_tiers
+    from kbgpu.framework import open_session
+    L = _abi.lib()
+    ssn = open_session(cache, fixture_tiers(fx), dict(base_opts))
+    rng = random.Random(seed)
+    tasks = ssn.flat.arrays["tasks"]
+    T = len(ssn.flat.task_objs)
+    cap = T + int(T * churn * (steps + 1)) + 16
+    buf = (_abi.kbg_decision * cap)()
+    n = ctypes.c_int32(0)
+    _abi.check(L.kbg_allocate(ssn.handle, buf, cap, ctypes.byref(n)))
+    first_ms = ssn.stats().allocate_ms
+    running = {}  # task -> node
+    evs = (_abi.kbg_event * max(1, n.value))()
+    k = 0
+    for i in range(n.value):
+        d = buf[i]
+        if d.kind == _abi.KIND_ALLOCATE:
+            e = evs[k]
+            e.kind, e.task, e.status, e.node = _abi.EV_POD_UPDATE, d.task, 1 << 5, d.node  # Running
+            running[d.task] = d.node
+            k += 1
+    _abi.check(L.kbg_session_update(ssn.handle, evs, k))
+    bind_ms = ssn.stats().update_ms
+    out = {"open_ms": ssn.stats().open_ms, "first_cycle_allocate_ms": first_ms, "bind_events": k,
+           "bind_update_ms": bind_ms, "churn_events_per_step": 0, "churn_update_ms": [], "churn_allocate_ms": [],
+           "churn_placements": []}
+    keep = []
+    jobs_of = {}
+    for t in range(T):
+        jobs_of.setdefault(int(tasks[t]["job"]), t)
+    job_ids = sorted(jobs_of)
+    binds = []  # (task, node) of the last cycle's Allocate decisions, confirmed in the next update
+    for step in range(steps):
+        m = int(len(running) * churn)
+        done = rng.sample(sorted(running), m)
+        evs = (_abi.kbg_event * (len(binds) + 2 * m))()
+        i = 0
+        for t, nd in binds:
+            evs[i].kind, evs[i].task, evs[i].status, evs[i].node = _abi.EV_POD_UPDATE, t, 1 << 5, nd  # Running
+            running[t] = nd
+            i += 1
+        for t in done:
+            if t not in running:
+                continue
+            evs[i].kind, evs[i].task, evs[i].status, evs[i].node = _abi.EV_POD_UPDATE, t, 1 << 7, running.pop(t)
+            i += 1
+        for a in range(m):
+            base = jobs_of[job_ids[rng.randrange(len(job_ids))]]
+            src = tasks[base]
+            e = evs[i]
+            e.kind, e.job, e.spec, e.status, e.node = _abi.EV_POD_ADD, int(src["job"]), int(src["spec"]), 1, -1
+            e.priority = int(src["priority"])
+            e.resource = _abi.kbg_resource(*[float(x) for x in src["resreq"]])
+            keep += [f"churn-{step}-{a}".encode(), f"churn/{step}-{a}".encode()]
+            e.uid, e.pod_key = keep[-2], keep[-1]
+            i += 1
+        _abi.check(L.kbg_session_update(ssn.handle, evs, i))
+        out["churn_update_ms"].append(ssn.stats().update_ms)
+        out["churn_events_per_step"] = i
+        _abi.check(L.kbg_allocate(ssn.handle, buf, cap, ctypes.byref(n)))
+        out["churn_allocate_ms"].append(ssn.stats().allocate_ms)
+        out["churn_placements"].append(n.value)
+        binds = [(buf[j].task, buf[j].node) for j in range(n.value) if buf[j].kind == _abi.KIND_ALLOCATE]
+    ssn.close()
+    out["churn_update_ms_p50"] = statistics.median(out["churn_update_ms"])
+    out["churn_allocate_ms_p50"] = statistics.median(out["churn_allocate_ms"])
+    out["note"] = ("kbg_session_update replaces a session open per cycle (open_ms): binds of the first cycle, then "
+                   f"{churn:.0%} completions + {churn:.0%} new pods + the last cycle's binds per update, each "
+                   "followed by an allocate cycle")
+    return out
 
 
 def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid, open_ms_first):

@@ -1129,10 +1129,15 @@ std::vector<int32_t> ranks_of(const Session& S, const std::vector<int32_t>& ids)
 // those inputs. derive_host() is the host part of build() that an update
 // re-runs without recompiling the static predicate or reallocating HBM.
 
+// String id of `v` for an event: an existing content's canonical id, or a new entry.
 int32_t intern(Session& S, const char* v) {
+  const std::string key(v ? v : "");
+  auto it = S.canon_of.find(key);
+  if (it != S.canon_of.end()) return it->second;  // a canonical id is its own canonical id
   const int32_t id = (int32_t)S.strs.size();
-  S.strs.emplace_back(v ? v : "");
-  S.canon.push_back(S.canon_of.emplace(S.strs.back(), id).first->second);
+  S.strs.push_back(key);
+  S.canon.push_back(id);
+  S.canon_of.emplace(key, id);
   return id;
 }
 
@@ -1173,6 +1178,13 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   S.pod_labels_in = copy_arr(snap->pod_labels, 2 * snap->n_pod_labels);
   S.others_in = copy_arr(snap->others, snap->n_others);
   S.task_live.assign(S.n_tasks, 1);
+  {  // headroom for pods added by session updates (no reallocation per event batch)
+    const size_t more = (size_t)S.n_tasks / 4 + 1024;
+    S.tasks_in.reserve(S.n_tasks + more);
+    S.task_live.reserve(S.n_tasks + more);
+    S.strs.reserve(S.strs.size() + 2 * more);
+    S.canon.reserve(S.strs.size() + 2 * more);
+  }
   // JobInfo.Tasks / NodeInfo.Tasks insertion orders, kept as lists
   // an update reorders the way the cache's delete + add does
   S.job_task_order.assign(S.n_jobs, {});
@@ -1266,7 +1278,7 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
     S.job_queue.resize(S.n_jobs);
     for (int32_t j = 0; j < S.n_jobs; ++j) S.job_queue[j] = S.jobs_in[j].queue;
   }
-  S.task_ranks_stale = true;
+  S.task_rank.clear();  // computed by derive_host
   return KBG_OK;
 }
 
@@ -1279,12 +1291,33 @@ enum { DERIVE_OK = 0, DERIVE_REBUILD = 1 };  // REBUILD: the static classes / ma
 kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   *outcome = DERIVE_OK;
   const int32_t N = S.n_nodes, T = S.n_tasks;
-  if (S.task_ranks_stale) {  // bytewise UID order (TaskOrderFn fallback); only when tasks were added
+  static const bool prof = getenv("KBG_PROFILE_OPEN") != nullptr;
+  auto tl = std::chrono::steady_clock::now();
+  auto phase = [&](const char* name) {
+    if (!prof) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[kbg derive] %-20s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(now - tl).count());
+    tl = now;
+  };
+  // bytewise UID order: TaskOrderFn's fallback compares tasks of one job only
+  // (session_plugins.go:266-276), so a job that gained tasks is re-ranked alone
+  if (S.task_rank.empty() && T > 0) {
     std::vector<int32_t> ids(T);
     for (int32_t t = 0; t < T; ++t) ids[t] = S.tasks_in[t].uid;
     S.task_rank = ranks_of(S, ids);
-    S.task_ranks_stale = false;
+  } else if (S.task_ranks_stale) {
+    S.task_rank.resize(T, 0);
+    for (int32_t j : S.rank_dirty_jobs) {
+      std::vector<int32_t> ids;
+      for (int32_t t : S.job_task_order[j]) ids.push_back(S.tasks_in[t].uid);
+      const std::vector<int32_t> r = ranks_of(S, ids);
+      for (size_t i = 0; i < r.size(); ++i) S.task_rank[S.job_task_order[j][i]] = r[i];
+    }
   }
+  S.task_ranks_stale = false;
+  S.rank_dirty_jobs.clear();
+  if (S.treq.capacity() < (size_t)T) S.treq.reserve((size_t)T + T / 4 + 1024);
+  S.task_node.reserve(S.treq.capacity());
   S.treq.resize(T);
   S.pending_candidate.assign(T, 0);
   S.be_task.assign(T, 0);
@@ -1298,6 +1331,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     S.be_task[t] = S.tasks_in[t].status == KBG_PENDING && kbg::res_empty(S.treq[t]);
   }
 
+  phase("ranks+tasks");
   // ---- nodes
   S.idle.resize(N);
   S.rel.resize(N);
@@ -1333,8 +1367,10 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     S.nt_off[n + 1] = (int32_t)S.nt_task.size();
     S.max_candidates = std::max(S.max_candidates, S.nt_off[n + 1] - S.nt_off[n]);
   }
+  phase("nodes+victims");
   setup_pod_keys(S);
 
+  phase("pod keys");
   // ---- engine initial state
   Engine& E = S.init;
   E = Engine{};
@@ -1420,6 +1456,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     }
   }
 
+  phase("engine+drf+prop");
   // ---- predicates preconditions
   const bool had_ghost = S.ghost;
   S.has_aff = false;
@@ -1434,6 +1471,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     }
   }
 
+  phase("preconditions");
   // ---- pending task lists in TaskOrderFn order (session_plugins.go:266-276)
   S.pend_off.assign(S.n_jobs, 0);
   S.pend_len.assign(S.n_jobs, 0);
@@ -1451,6 +1489,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     S.pend_len[j] = (int32_t)S.pend.size() - S.pend_off[j];
   }
 
+  phase("pend lists");
   // ---- per-queue job heaps (allocate.go:45-59)
   S.joff.assign(S.n_queues, 0);
   S.jcap.assign(S.n_queues, 0);
@@ -1461,6 +1500,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   S.pend_len_all = S.pend_len;
   build_heaps(S, E);
 
+  phase("heaps");
   // ---- static predicate classes
   if (sh) {
     compile_static_predicates(S, sh);
@@ -1483,6 +1523,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
         S.task_class[t] = c;
       }
   }
+  phase("classes");
   S.W = (N + 63) / 64;
   // ---- integer scan mode (kbg_device.hpp TaskRec): every value the scan
   // compares is an exact integer and stays one through the cycle
@@ -1505,6 +1546,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     S.int_mode = ok && sum_c <= kLim && sum_m <= kLim && sum_g <= kLim &&
                  getenv("KBG_FORCE_GENERAL_SCAN") == nullptr;
   }
+  phase("int mode");
   // ---- (class, request) shapes of the candidates
   {
     std::unordered_map<ShapeKey, int32_t, ShapeHash> ids;
@@ -1524,6 +1566,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
       S.task_shape[t] = b;
     }
   }
+  phase("shapes");
   return KBG_OK;
 }
 
@@ -3307,6 +3350,7 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
       S.treq.push_back(to_res(k.resreq));
       S.task_node.push_back(e.node);
       S.task_ranks_stale = true;
+      S.rank_dirty_jobs.push_back(e.job);
       return in_add_task(S, U, t);
     }
     case KBG_EV_NODE_UPDATE: {

@@ -310,7 +310,8 @@ struct Session {
   std::vector<std::vector<int32_t>> node_task_order;  // per node: the session tasks in NodeInfo.Tasks order
   std::vector<std::vector<int32_t>> node_key_order;   // per node: PodKey (canonical id) of every pod on it
   std::vector<kbg_resource> others_in;                // Session.Others resreq
-  bool task_ranks_stale = true;                       // tasks were added: recompute the UID ranks
+  bool task_ranks_stale = false;                      // tasks were added: re-rank their jobs' UIDs
+  std::vector<int32_t> rank_dirty_jobs;
   std::vector<int32_t> spec_class;                    // per spec: its static class (-1: none compiled)
   int32_t nospec_class = -1;                          // class of a task without a spec
   StaticTables static_tab{};                          // device static predicate inputs (mask rebuilds)

@@ -54,9 +54,15 @@ extern "C" int32_t kbg_tool_update_nodes(const kbg_snapshot* snap, const kbg_opt
   S.n_classes = sh.n_classes;
   UpdateCtx U;
   U.seen.assign(S.n_nodes, 0);
+  const auto t0 = std::chrono::steady_clock::now();
   for (int32_t i = 0; i < n; ++i)
     if (apply_event(S, U, ev[i]) != KBG_OK) return -3;
+  const auto t1 = std::chrono::steady_clock::now();
   if (derive_host(S, nullptr, &outcome) != KBG_OK) return -4;
+  if (getenv("KBG_TOOL_TIME"))
+    fprintf(stderr, "[tool] %d events: apply %.3f ms, derive %.3f ms\n", n,
+            std::chrono::duration<double, std::milli>(t1 - t0).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
   for (int32_t k = 0; k < S.n_nodes; ++k) {
     idle[3 * k] = S.idle[k].c;
     idle[3 * k + 1] = S.idle[k].m;
