@@ -165,6 +165,7 @@ void recompute_bit(Session& S, int32_t c, int32_t n) {
   if (v && !S.panic_node[n]) v = ports_ok(S, c, n) && aff_ok(S, S.affm->st, c, n);
   const bool old = (S.h_class_mask[idx] & bit) != 0;
   if (v == old) return;
+  vc_mask_changed(S, c, n);
   if (v) {
     S.h_class_mask[idx] |= bit;
     if (!S.aff_gain_flag[c]) {
@@ -284,6 +285,7 @@ void aff_place(Session& S, int32_t t, int32_t n, int32_t sign, AffState& st, boo
           const size_t idx = (size_t)c * S.W + w;
           const uint64_t old = S.h_class_mask[idx], nw = old & keep[w];
           if (nw == old) continue;
+          for (uint64_t d = old & ~nw; d; d &= d - 1) vc_mask_changed(S, c, w * 64 + __builtin_ctzll(d));
           S.h_class_mask[idx] = nw;
           S.mwmark[idx] = S.mstamp;
           if (!S.mask_dirty_flag[idx]) {

@@ -77,7 +77,8 @@ constexpr int32_t kMaskDeltaCap = 8192;
 enum VictimPlugin : int32_t { VP_GANG = 1, VP_DRF = 2, VP_PROP = 4 };
 enum VictimMode : int32_t { VM_PREEMPT_JOBS = 0, VM_PREEMPT_TASKS = 1, VM_RECLAIM = 2 };
 constexpr int kMaxVictimTiers = 8;
-constexpr int kMaxNodeCandidates = 128;  // victim candidates per node (two 64-bit masks)
+constexpr int kVictimChunks = 16;                      // 64-candidate chunks per node in one victim scan
+constexpr int kMaxNodeCandidates = 64 * kVictimChunks;  // victim candidates per node
 
 // One reclaimer / preemptor against every node.
 struct VictimScan {
@@ -220,6 +221,10 @@ constexpr int kVictimBlockWaves = 16;
 inline int32_t kbg_victim_words(int32_t n_nodes) { return (n_nodes + 31) / 32; }
 hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* stop_bits, uint32_t* panic_bits,
                               hipStream_t stream, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+// Nodes of the scanned range with more than 128 candidates (`rows`, table
+// rows), evaluated after launch_victim_scan and ORed into its device words.
+hipError_t launch_victim_big(const VictimScan& p, const VictimTables& t, const int32_t* rows, int32_t n_rows,
+                             uint32_t* stop_bits, uint32_t* panic_bits, hipStream_t stream);
 // Host-side changes before a scan, read in place from host-mapped memory:
 // node rows (NodeInfo.Tasks count / Idle / Releasing) and victim-table
 // entries, in one launch.

@@ -299,13 +299,14 @@ __device__ __forceinline__ double share3(const double* a, const double* tot) {
 // One wave per node, in ssn.Nodes order; the lowest node where the reference
 // stops (validated victims, or a panic inside PredicateFn or a victim fn)
 // wins. The node's candidates — the session tasks Running on it at open, in
-// NodeInfo.Tasks order, at most kMaxNodeCandidates (the host checks) — sit
-// one per lane (k = h * 64 + lane, h = 0, 1). The victim fns that accumulate
-// per job (drf.go:87-100) or per queue (proportion.go:166-183) walk the
-// preemptees in order as a wave-uniform loop: candidate k2's job, queue and
-// request come to every lane through v_readlane, and lane k applies it while
-// k2 <= k, so each lane sees exactly the subtractions the reference has made
-// when it reaches its candidate.
+// NodeInfo.Tasks order — are taken in chunks of 64, one per lane
+// (k = h * 64 + lane, h < kVictimChunks; the host checks the bound). The
+// victim fns that accumulate per job (drf.go:87-100) or per queue
+// (proportion.go:166-183) walk the preemptees in order as a wave-uniform
+// loop: lane k applies preemptee k2 while k2 <= k, so each lane sees exactly
+// the subtractions the reference has made when it reaches its candidate.
+// Preemptees of the lane's own chunk come through v_readlane, those of
+// earlier chunks through wave-uniform (scalar) loads.
 
 __device__ __forceinline__ int32_t rl_i(int32_t v, int32_t l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ double rl_d(double v, int32_t l) {
@@ -315,132 +316,157 @@ __device__ __forceinline__ double rl_d(double v, int32_t l) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-// The stop key of one node (wave-uniform), UINT32_MAX when the reference
-// moves on to the next node.
-__device__ uint32_t victim_node(const VictimScan& p, const VictimTables& t, int row, int lane) {
-  constexpr uint32_t kNone = 0xffffffffu;
-  const int n = p.node_lo + row;
-  if (!((t.class_mask[(size_t)p.cls * p.W + (n >> 6)] >> (n & 63)) & 1ull)) return kNone;  // static predicate
-  if (t.panic_node[n]) return ((uint32_t)n << 1) | 1u;  // SetNode(nil) inside PredicateFn (predicates.go:122-123)
-  if (p.cap_check && t.ntasks[row] >= t.maxtasks[row]) return kNone;  // predicates.go:125-127
-  const int off = t.nt_off[n];
-  const int L = t.nt_off[n + 1] - off;
-  // this lane's two candidates: job, queue, request, preemptee filter
-  int32_t jv[2], qv[2];
-  double rq[2][3];
-  uint64_t pm[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int k = h * 64 + lane;
-    bool f = false;
-    jv[h] = -1;
-    qv[h] = -1;
-    rq[h][0] = rq[h][1] = rq[h][2] = 0.0;
-    if (k < L) {
-      const int task = t.nt_task[off + k];
-      jv[h] = t.t_job[task];
-      qv[h] = t.j_queue[jv[h]];
-      rq[h][0] = t.t_req[3 * (size_t)task];
-      rq[h][1] = t.t_req[3 * (size_t)task + 1];
-      rq[h][2] = t.t_req[3 * (size_t)task + 2];
-      if (t.t_run[task]) {
-        if (p.mode == VM_PREEMPT_JOBS) f = qv[h] == p.queue && jv[h] != p.job;  // preempt.go:100-112
-        else if (p.mode == VM_PREEMPT_TASKS) f = jv[h] == p.job;              // :146-154
-        else f = qv[h] != p.queue;                                              // reclaim.go:113-126
-      }
+// Candidate k of a node: its job, queue, request and preemptee filter.
+struct VCand {
+  int32_t job, queue;
+  double r[3];
+  bool f;
+};
+__device__ __forceinline__ VCand load_cand(const VictimScan& p, const VictimTables& t, int off, int L, int k) {
+  VCand c{-1, -1, {0.0, 0.0, 0.0}, false};
+  if (k < L) {
+    const int task = t.nt_task[off + k];
+    c.job = t.t_job[task];
+    c.queue = t.j_queue[c.job];
+    c.r[0] = t.t_req[3 * (size_t)task];
+    c.r[1] = t.t_req[3 * (size_t)task + 1];
+    c.r[2] = t.t_req[3 * (size_t)task + 2];
+    if (t.t_run[task]) {
+      if (p.mode == VM_PREEMPT_JOBS) c.f = c.queue == p.queue && c.job != p.job;  // preempt.go:100-112
+      else if (p.mode == VM_PREEMPT_TASKS) c.f = c.job == p.job;                // :146-154
+      else c.f = c.queue != p.queue;                                            // reclaim.go:113-126
     }
-    pm[h] = __ballot(f);
   }
-  if (!(pm[0] | pm[1])) return kNone;  // no preemptee: every fn returns nil
-  const int nh = L > 64 ? 2 : 1;
+  return c;
+}
+
+// One preemptee k2 applied to this lane's running allocations (drf per job,
+// proportion per queue) when k2 <= k; sets *panic on a Sub underflow, *vp at
+// k2 == k (proportion's verdict is taken right after its own subtraction).
+__device__ __forceinline__ void apply_preemptee(const VictimTables& t, int fns, int32_t j2, int32_t q2,
+                                                const double (&r2)[3], bool self, int32_t jv, int32_t qv, double (&xd)[3],
+                                                double (&xp)[3], bool& panic, bool& vp) {
+  if ((fns & VP_DRF) && j2 == jv) {
+    if (!res_le3(r2, xd)) panic = true;  // Resource.Sub (resource_info.go:100-110)
+    xd[0] -= r2[0];
+    xd[1] -= r2[1];
+    xd[2] -= r2[2];
+  }
+  if ((fns & VP_PROP) && q2 == qv) {
+    if (!res_less3(xp, r2)) {  // Less: skipped, allocation untouched
+      if (!res_le3(r2, xp)) panic = true;
+      xp[0] -= r2[0];
+      xp[1] -= r2[1];
+      xp[2] -= r2[2];
+      if (self) vp = res_le3(t.q_deserved + 3 * (size_t)qv, xp);
+    }
+  }
+}
+
+// The stop key of node n with its candidates in at most NCH chunks
+// (wave-uniform), UINT32_MAX when the reference moves on to the next node.
+// NCH is a compile-time bound so the per-chunk masks stay in registers.
+template <int NCH>
+__device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t, int n, int off, int L, int lane) {
+  constexpr uint32_t kNone = 0xffffffffu;
+  const int nch = (L + 63) >> 6;  // <= NCH
+  uint64_t pm[NCH];
+  uint64_t any_pm = 0ull;
+#pragma unroll
+  for (int h = 0; h < NCH; ++h) {
+    pm[h] = h < nch ? __ballot(load_cand(p, t, off, L, h * 64 + lane).f) : 0ull;
+    any_pm |= pm[h];
+  }
+  if (!any_pm) return kNone;  // no preemptee: every fn returns nil
   bool panic = false;
-  uint64_t vm[2] = {0ull, 0ull};
-  for (int ti = 0; ti < p.n_tiers; ++ti) {
+  uint64_t vm[NCH];
+  bool victims = false;
+  for (int ti = 0; ti < p.n_tiers && !victims && !panic; ++ti) {
     const int fns = p.tier_fns[ti];
-    uint64_t tm[2] = {pm[0], pm[1]};
-    if (fns & VP_GANG) {  // gang.go:104-124
+    uint64_t tm[NCH];
+    bool any = false;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const bool c = jv[h] >= 0 && t.j_min[jv[h]] <= t.j_ready[jv[h]] - 1;
-        tm[h] &= __ballot(c);
-      }
-    }
-    if (fns & (VP_DRF | VP_PROP)) {
-      // running per-lane allocation: drf per job, proportion per queue
-      double xd[2][3], xp[2][3];
-      bool vd[2] = {false, false}, vp[2] = {false, false};
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NCH; ++h) {
+      tm[h] = 0ull;
+      if (h >= nch) continue;
+      const VCand c = load_cand(p, t, off, L, h * 64 + lane);
+      uint64_t m = pm[h];
+      if (fns & VP_GANG)  // gang.go:104-124
+        m &= __ballot(c.job >= 0 && t.j_min[c.job] <= t.j_ready[c.job] - 1);
+      if (fns & (VP_DRF | VP_PROP)) {
         const bool on = (pm[h] >> lane) & 1ull;
+        double xd[3], xp[3];
         for (int d = 0; d < 3; ++d) {
-          xd[h][d] = on && (fns & VP_DRF) ? t.j_alloc[3 * (size_t)jv[h] + d] : 0.0;
-          xp[h][d] = on && (fns & VP_PROP) ? t.q_alloc[3 * (size_t)qv[h] + d] : 0.0;
+          xd[d] = on && (fns & VP_DRF) ? t.j_alloc[3 * (size_t)c.job + d] : 0.0;
+          xp[d] = on && (fns & VP_PROP) ? t.q_alloc[3 * (size_t)c.queue + d] : 0.0;
         }
-      }
-      bool lpanic = false;
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        if (h2 >= nh) break;
-        const uint64_t bits = pm[h2];
-        for (uint64_t b = bits; b; b &= b - 1) {  // preemptees k2 in order (wave-uniform)
-          const int l2 = __builtin_ctzll(b);
-          const int k2 = h2 * 64 + l2;
-          const int32_t j2 = rl_i(jv[h2], l2);
-          const int32_t q2 = rl_i(qv[h2], l2);
-          const double r2[3] = {rl_d(rq[h2][0], l2), rl_d(rq[h2][1], l2), rl_d(rq[h2][2], l2)};
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int k = h * 64 + lane;
-            if (!((pm[h] >> lane) & 1ull) || k2 > k) continue;
-            if ((fns & VP_DRF) && j2 == jv[h]) {
-              if (!res_le3(r2, xd[h])) lpanic = true;  // Resource.Sub (resource_info.go:100-110)
-              xd[h][0] -= r2[0];
-              xd[h][1] -= r2[1];
-              xd[h][2] -= r2[2];
-            }
-            if ((fns & VP_PROP) && q2 == qv[h]) {
-              if (!res_less3(xp[h], r2)) {  // Less: skipped, allocation untouched
-                if (!res_le3(r2, xp[h])) lpanic = true;
-                xp[h][0] -= r2[0];
-                xp[h][1] -= r2[1];
-                xp[h][2] -= r2[2];
-                if (k2 == k) vp[h] = res_le3(t.q_deserved + 3 * (size_t)qv[h], xp[h]);
-              }
-            }
+        bool lpanic = false, vp = false;
+        for (int h2 = 0; h2 < h; ++h2)  // preemptees of earlier chunks (all before this lane's k)
+          for (uint64_t b = pm[h2]; b; b &= b - 1) {
+            const int task2 = t.nt_task[off + h2 * 64 + __builtin_ctzll(b)];  // wave-uniform
+            const int32_t j2 = t.t_job[task2];
+            const int32_t q2 = t.j_queue[j2];
+            const double r2[3] = {t.t_req[3 * (size_t)task2], t.t_req[3 * (size_t)task2 + 1],
+                                  t.t_req[3 * (size_t)task2 + 2]};
+            if (on) apply_preemptee(t, fns, j2, q2, r2, false, c.job, c.queue, xd, xp, lpanic, vp);
           }
+        for (uint64_t b = pm[h]; b; b &= b - 1) {  // this chunk, in order, while k2 <= k
+          const int l2 = __builtin_ctzll(b);
+          const int32_t j2 = rl_i(c.job, l2);
+          const int32_t q2 = rl_i(c.queue, l2);
+          const double r2[3] = {rl_d(c.r[0], l2), rl_d(c.r[1], l2), rl_d(c.r[2], l2)};
+          if (on && l2 <= lane) apply_preemptee(t, fns, j2, q2, r2, l2 == lane, c.job, c.queue, xd, xp, lpanic, vp);
         }
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if ((fns & VP_DRF) && ((pm[h] >> lane) & 1ull)) {
-          const double rs = share3(xd[h], t.drf_total);
-          vd[h] = p.ls < rs || fabs(p.ls - rs) <= 0.000001;
+        bool vd = false;
+        if ((fns & VP_DRF) && on) {
+          const double rs = share3(xd, t.drf_total);
+          vd = p.ls < rs || fabs(p.ls - rs) <= 0.000001;
         }
-        if (fns & VP_DRF) tm[h] &= __ballot(vd[h]);
-        if (fns & VP_PROP) tm[h] &= __ballot(vp[h]);
+        if (fns & VP_DRF) m &= __ballot(vd);
+        if (fns & VP_PROP) m &= __ballot(vp);
+        if (__ballot(lpanic) != 0ull) panic = true;
       }
-      panic = __ballot(lpanic) != 0ull;
-      if (panic) break;
+      tm[h] = m;
+      any = any || m != 0ull;
     }
-    if (tm[0] | tm[1]) {  // the host passes only the deciding tier (session_plugins.go:59-98)
-      vm[0] = tm[0];
-      vm[1] = tm[1];
-      break;
+    if (!panic && any) {  // the host passes only the deciding tier (session_plugins.go:59-98)
+#pragma unroll
+      for (int h = 0; h < NCH; ++h) vm[h] = tm[h];
+      victims = true;
     }
   }
   if (panic) return ((uint32_t)n << 1) | 1u;
-  if (!(vm[0] | vm[1])) return kNone;
+  if (!victims) return kNone;
   double all[3] = {0.0, 0.0, 0.0};  // validateVictims (preempt.go:242-253), in victims order
 #pragma unroll
-  for (int h2 = 0; h2 < 2; ++h2)
-    for (uint64_t b = vm[h2]; b; b &= b - 1) {
-      const int l2 = __builtin_ctzll(b);
-      all[0] += rl_d(rq[h2][0], l2);
-      all[1] += rl_d(rq[h2][1], l2);
-      all[2] += rl_d(rq[h2][2], l2);
+  for (int h = 0; h < NCH; ++h)
+    for (uint64_t b = vm[h]; b; b &= b - 1) {
+      const int task2 = t.nt_task[off + h * 64 + __builtin_ctzll(b)];
+      all[0] += t.t_req[3 * (size_t)task2];
+      all[1] += t.t_req[3 * (size_t)task2 + 1];
+      all[2] += t.t_req[3 * (size_t)task2 + 2];
     }
   if (res_less3(all, p.req)) return kNone;
   return (uint32_t)n << 1;
+}
+
+// NCH_MAX: the chunk bound of this kernel. The main scan takes nodes of up
+// to 128 candidates; nodes holding more (rare: pod caps are ~110) are left to
+// kbg_victim_big_kernel, whose larger per-chunk state would otherwise raise
+// the register budget of every wave.
+template <int NCH_MAX>
+__device__ uint32_t victim_node(const VictimScan& p, const VictimTables& t, int row, int lane) {
+  constexpr uint32_t kNone = 0xffffffffu;
+  const int n = p.node_lo + row;
+  const int off = t.nt_off[n];
+  const int L = t.nt_off[n + 1] - off;
+  if (NCH_MAX <= 2 && L > 128) return kNone;  // evaluated by the big-node kernel
+  if (!((t.class_mask[(size_t)p.cls * p.W + (n >> 6)] >> (n & 63)) & 1ull)) return kNone;  // static predicate
+  if (t.panic_node[n]) return ((uint32_t)n << 1) | 1u;  // SetNode(nil) inside PredicateFn (predicates.go:122-123)
+  if (p.cap_check && t.ntasks[row] >= t.maxtasks[row]) return kNone;  // predicates.go:125-127
+  if (NCH_MAX > 2) return victim_candidates<NCH_MAX>(p, t, n, off, L, lane);
+  if (L <= 64) return victim_candidates<1>(p, t, n, off, L, lane);
+  return victim_candidates<2>(p, t, n, off, L, lane);
 }
 
 __global__ __launch_bounds__(64 * kVictimBlockWaves) void kbg_victim_kernel(VictimScan p, VictimTables t,
@@ -457,7 +483,7 @@ __global__ __launch_bounds__(64 * kVictimBlockWaves) void kbg_victim_kernel(Vict
     const int off = w + k * kVictimBlockWaves;
     const int row = base + off;
     if (row < p.node_n) {
-      const uint32_t key = victim_node(p, t, row, lane);  // wave-uniform
+      const uint32_t key = victim_node<2>(p, t, row, lane);  // wave-uniform
       if (key != 0xffffffffu && lane == 0) {
         atomicOr(&s_stop, 1u << off);
         if (key & 1u) atomicOr(&s_panic, 1u << off);
@@ -467,9 +493,35 @@ __global__ __launch_bounds__(64 * kVictimBlockWaves) void kbg_victim_kernel(Vict
   __syncthreads();
   if (threadIdx.x == 0) {
     const int word = (p.node_lo >> 5) + blockIdx.x;  // node_lo is 64-node aligned
-    *(volatile uint32_t*)(stop_bits + word) = s_stop;
-    *(volatile uint32_t*)(panic_bits + word) = s_panic;
+    stop_bits[word] = s_stop;
+    panic_bits[word] = s_panic;
   }
+}
+
+// The nodes of the range holding more than 128 candidates, one wave each,
+// after the main scan on the same stream: their bits are ORed into the words
+// it wrote (several big nodes may share a word).
+__global__ __launch_bounds__(256) void kbg_victim_big_kernel(VictimScan p, VictimTables t,
+                                                             const int32_t* __restrict__ rows, int32_t n_rows,
+                                                             uint32_t* __restrict__ stop_bits,
+                                                             uint32_t* __restrict__ panic_bits) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n_rows) return;
+  const int row = rows[i];
+  const uint32_t key = victim_node<kVictimChunks>(p, t, row, lane);
+  if (key == 0xffffffffu || lane != 0) return;
+  const int n = p.node_lo + row;
+  atomicOr(stop_bits + (n >> 5), 1u << (n & 31));
+  if (key & 1u) atomicOr(panic_bits + (n >> 5), 1u << (n & 31));
+}
+
+hipError_t launch_victim_big(const VictimScan& p, const VictimTables& t, const int32_t* rows, int32_t n_rows,
+                             uint32_t* stop_bits, uint32_t* panic_bits, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kbg_victim_big_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, stream, p, t, rows, n_rows, stop_bits,
+                     panic_bits);
+  return hipGetLastError();
 }
 
 hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* stop_bits, uint32_t* panic_bits,

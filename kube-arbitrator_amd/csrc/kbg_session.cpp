@@ -589,8 +589,9 @@ kbg_status device_scan(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
 
 // Writes the rows of the nodes touched by the last commits back to HBM (only
 // the rows this process holds; every shard's host mirror saw every commit).
-kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
-  // class-mask words cleared by host-port conflicts (every shard holds the whole mask)
+// Class-mask words changed on the host (host ports, pod affinity) into HBM;
+// every shard holds the whole mask.
+kbg_status push_mask_deltas(Session& S) {
   for (size_t m = 0; m < S.mask_dirty.size();) {
     const int32_t cnt = (int32_t)std::min<size_t>(S.mask_dirty.size() - m, (size_t)kbg::kMaskDeltaCap);
     for (int32_t k = 0; k < cnt; ++k) {
@@ -605,6 +606,12 @@ kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
   }
   // (the last chunk's copy is retired by the next device round trip's synchronize)
   S.mask_dirty.clear();
+  return KBG_OK;
+}
+
+kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
+  kbg_status st = push_mask_deltas(S);
+  if (st != KBG_OK) return st;
   size_t i = 0;
   while (i < touched.size()) {
     int32_t cnt = 0;
@@ -829,6 +836,27 @@ void clear_mask_bit(Session& S, int32_t c, int32_t nd) {
   const uint64_t bit = 1ull << (nd & 63);
   if (!(S.h_class_mask[idx] & bit)) return;
   S.h_class_mask[idx] &= ~bit;
+  vc_mask_changed(S, c, nd);
+  if (!S.mask_dirty_flag[idx]) {
+    S.mask_dirty_flag[idx] = 1;
+    S.mask_dirty.push_back(idx);
+  }
+}
+
+// The bit of (c, n) from the static predicate, the port fit and the pod
+// affinity counts (a nil-Node node stays reachable: SetNode panics first).
+void refresh_mask_bit(Session& S, int32_t c, int32_t n) {
+  const uint32_t idx = (uint32_t)((size_t)c * S.W + (n >> 6));
+  const uint64_t bit = 1ull << (n & 63);
+  bool v = (S.h_class_mask_static[idx] & bit) != 0;
+  if (v && !S.panic_node[n]) {
+    for (int32_t w = 0; w < S.PW && v; ++w)
+      v = (S.node_ports[(size_t)n * S.PW + w] & S.cls_conf[(size_t)c * S.PW + w]) == 0;
+    if (v && S.has_aff) v = kbg::aff_ok(S, S.affm->st, c, n);
+  }
+  if (v == ((S.h_class_mask[idx] & bit) != 0)) return;
+  S.h_class_mask[idx] ^= bit;
+  vc_mask_changed(S, c, n);
   if (!S.mask_dirty_flag[idx]) {
     S.mask_dirty_flag[idx] = 1;
     S.mask_dirty.push_back(idx);
@@ -842,6 +870,8 @@ void add_ports(Session& S, int32_t c, int32_t nd) {
   uint64_t* np = &S.node_ports[(size_t)nd * S.PW];
   const uint64_t* add = &S.cls_add[(size_t)c * S.PW];
   for (int32_t w = 0; w < S.PW; ++w) {
+    for (uint64_t b = add[w]; b; b &= b - 1)  // holders, for a statement discard (remove_ports)
+      S.port_hold[((int64_t)nd << 32) | (uint32_t)(w * 64 + __builtin_ctzll(b))]++;
     uint64_t nb = add[w] & ~np[w];
     np[w] |= nb;
     while (nb) {
@@ -850,6 +880,27 @@ void add_ports(Session& S, int32_t c, int32_t nd) {
       for (int32_t c2 : S.atom_cls[a]) clear_mask_bit(S, c2, nd);
     }
   }
+}
+
+// The pod leaves node.Pods() (statement.go:156-192 unpipeline ->
+// NodeInfo.RemoveTask): an atom no other pod holds — and that no pod held at
+// open — is free again, and the classes it blocked get the node back where
+// nothing else forbids it.
+void remove_ports(Session& S, int32_t c, int32_t nd) {
+  uint64_t* np = &S.node_ports[(size_t)nd * S.PW];
+  const uint64_t* np0 = &S.node_ports0[(size_t)nd * S.PW];
+  const uint64_t* add = &S.cls_add[(size_t)c * S.PW];
+  for (int32_t w = 0; w < S.PW; ++w)
+    for (uint64_t b = add[w]; b; b &= b - 1) {
+      const int32_t a = w * 64 + __builtin_ctzll(b);
+      auto it = S.port_hold.find(((int64_t)nd << 32) | (uint32_t)a);
+      if (it == S.port_hold.end() || --it->second > 0) continue;
+      S.port_hold.erase(it);
+      const uint64_t bit = 1ull << (a & 63);
+      if (np0[w] & bit) continue;  // a pod on the node at open holds it
+      np[w] &= ~bit;
+      for (int32_t c2 : S.atom_cls[a]) refresh_mask_bit(S, c2, nd);
+    }
 }
 
 // NodeInfo.Tasks already holds the task's PodKey (node_info.go:101-106)
@@ -1887,6 +1938,7 @@ void begin_cycle(Session& S) {
   S.dec_action.clear();
   S.dec_dup.clear();
   S.node_keys = S.node_keys0;
+  S.port_hold.clear();
   S.evictions.clear();
   S.tstat.resize(S.n_tasks);
   for (int32_t t = 0; t < S.n_tasks; ++t) S.tstat[t] = S.tasks_in[t].status;
@@ -2464,6 +2516,11 @@ void vt_delta(Session& S, int32_t kind, int32_t index, double a, double b, doubl
 // staging buffers are rewritten only once the previous launch has retired
 // (the victim scan's synchronize, or an explicit one here).
 kbg_status victim_push(Session& S, const std::vector<int32_t>& touched) {
+  if (!S.mask_dirty.empty()) {  // class-mask words (ports / affinity) changed since the last scan
+    if (S.vstage_busy) HIP_TRY(hipStreamSynchronize(S.stream));
+    kbg_status st = push_mask_deltas(S);
+    if (st != KBG_OK) return st;
+  }
   if (!S.sdeltas.empty()) {  // last write of each entry wins
     std::unordered_set<int64_t> seen;
     std::vector<kbg::StateDelta> uniq;
@@ -2559,6 +2616,11 @@ kbg_status vt_setup(Session& S) {
         (st = dalloc(S, &dja, 3 * J)) || (st = dalloc(S, &dqa, 3 * Q)) || (st = hupload(S, &dqd, qd)) ||
         (st = dalloc(S, &S.d_vbits, 2 * (size_t)S.W32)) || (st = dalloc(S, &S.d_vbits_red, 2 * (size_t)S.W32)))
       return st;
+    // nodes of this process's range holding more than 128 candidates (kbg_victim_big_kernel)
+    S.big_rows.clear();
+    for (int32_t n = S.tab_lo; n < S.tab_lo + S.tab_n; ++n)
+      if (S.nt_off[n + 1] - S.nt_off[n] > 128) S.big_rows.push_back(n - S.tab_lo);
+    if ((st = hupload(S, &S.d_big_rows, S.big_rows))) return st;
     S.vt_allocs.assign(S.d_allocs.begin() + a0, S.d_allocs.end());
     HIP_TRY(hipMemset(S.d_vbits, 0, 2 * (size_t)S.W32 * sizeof(uint32_t)));  // other ranks' words stay 0
     if (!S.h_vbits) {
@@ -2688,11 +2750,22 @@ struct Live {
     }
     return true;
   }
+  // An AllocatedStatus pod enters (+1) or leaves (-1) the predicates'
+  // podLister (api/helpers.go:63-70): the pod affinity counts and the class
+  // masks follow (kbg_affinity.cpp); allocate's batch-cut bookkeeping is not
+  // used by the victim actions.
+  void lister(int32_t v, int32_t sign) {
+    if (!S.has_aff) return;
+    kbg::aff_place(S, v, S.task_node[v], sign, S.affm->st, true);
+    for (int32_t c : S.aff_gain_classes) S.aff_gain_flag[c] = 0;
+    S.aff_gain_classes.clear();
+  }
   // job Releasing, NodeInfo.UpdateTask (Running copy out, Releasing copy
   // in), DeallocateFunc (session.go:323-349, statement.go:36-59)
   bool evict(int32_t v) {
     const int32_t j = S.task_job[v];
     if (ready_status(S.tstat[v])) ready(j, -1);
+    if (allocated_status(S.tstat[v])) lister(v, -1);
     S.tstat[v] = KBG_RELEASING;
     const int32_t n = S.task_node[v];
     if (n >= 0) {
@@ -2719,6 +2792,7 @@ struct Live {
       if (!S.nil_node[n] && !kbg::res_sub(S.rel[n], S.treq[t])) return false;  // node_info.go:117-118
       S.ntasks[n]++;
       if (S.has_dupkeys && S.key_hot[S.task_key[t]]) S.node_keys.insert(node_key_of(S, t, n));
+      if (S.has_ports) add_ports(S, S.task_class[t], n);  // the pod joins node.Pods()
       touch(n);
     }
     return plugins(t, true);
@@ -2728,6 +2802,7 @@ struct Live {
   void unevict(int32_t v) {
     const int32_t j = S.task_job[v];
     S.tstat[v] = KBG_RUNNING;
+    lister(v, +1);
     ready(j, +1);
     plugins(v, true);
   }
@@ -2739,6 +2814,7 @@ struct Live {
     if (!S.nil_node[n]) kbg::res_add(S.rel[n], S.treq[t]);  // node_info.go:145-146
     S.ntasks[n]--;
     if (S.has_dupkeys && S.key_hot[S.task_key[t]]) S.node_keys.erase(node_key_of(S, t, n));
+    if (S.has_ports) remove_ports(S, S.task_class[t], n);  // the pod leaves node.Pods()
     touch(n);
     return plugins(t, false);
   }
@@ -2873,17 +2949,22 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
     if (st != KBG_OK) return st;
     L.touched.clear();
     ++L.stamp;
-    uint32_t* bits = S.comm ? S.d_vbits : S.h_vbits_dev;
+    uint32_t* bits = S.d_vbits;
     const bool timed = (S.stats.victim_scans & 15) == 0 && p.node_n > 0;  // HIP-event time of every 16th launch
     HIP_TRY(kbg::launch_victim_scan(p, S.vt, bits, bits + S.W32, S.stream, timed ? S.ev[0] : nullptr,
                                     timed ? S.ev[1] : nullptr));
+    if (!S.big_rows.empty())  // nodes with more than 128 candidates: ORed into the same words
+      HIP_TRY(kbg::launch_victim_big(p, S.vt, S.d_big_rows, (int32_t)S.big_rows.size(), bits, bits + S.W32,
+                                     S.stream));
+    const uint32_t* done_bits = S.d_vbits;
     if (S.comm) {  // disjoint words of the ranks: element-wise max is their OR
       const ncclResult_t nr =
           ncclAllReduce(S.d_vbits, S.d_vbits_red, 2 * (size_t)S.W32, ncclUint32, ncclMax, S.comm->nccl, S.stream);
       if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
-      HIP_TRY(hipMemcpyAsync(S.h_vbits, S.d_vbits_red, 2 * (size_t)S.W32 * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                             S.stream));
+      done_bits = S.d_vbits_red;
     }
+    HIP_TRY(hipMemcpyAsync(S.h_vbits, done_bits, 2 * (size_t)S.W32 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           S.stream));
     HIP_TRY(hipStreamSynchronize(S.stream));
     S.vstage_busy = false;
     if (timed) {
@@ -2995,10 +3076,9 @@ std::vector<std::vector<int32_t>> pending_by_job(const Session& S) {
 }
 
 kbg_status victim_action_check(Session& S) {
-  if (S.has_ports) return fail(KBG_E_UNSUPPORTED, "preempt/reclaim with host ports: run the reference path");
-  if (S.has_aff) return fail(KBG_E_UNSUPPORTED, "preempt/reclaim with pod (anti)affinity: run the reference path");
   if (S.max_candidates > kbg::kMaxNodeCandidates)
-    return fail(KBG_E_UNSUPPORTED, "a node holds more than 128 running session tasks");
+    return fail(KBG_E_UNSUPPORTED, "a node holds more than " + std::to_string(kbg::kMaxNodeCandidates) +
+                                       " running session tasks: run the reference path");
   return KBG_OK;
 }
 
@@ -3591,6 +3671,7 @@ kbg_status kbg_session_reset(kbg_session* s) {
   S.ntasks = S.ntasks0;
   S.allocated = S.backfilled = S.reclaimed = S.preempted = S.cycle_started = false;
   S.node_keys = S.node_keys0;
+  S.port_hold.clear();
   if (S.has_ports || S.has_aff) {  // the class masks carry the port fit / affinity: back to the snapshot's
     S.node_ports = S.node_ports0;
     S.h_class_mask = S.h_class_mask0;
@@ -3623,7 +3704,6 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
   for (int32_t i = 0; i < n; ++i)
     if (tasks[i] < 0 || tasks[i] >= S.n_tasks || !S.pending_candidate[tasks[i]])
       return fail(KBG_E_INVALID, "task index (must be a Pending, non-BestEffort session task)");
-  if (S.has_aff) return fail(KBG_E_UNSUPPORTED, "kbg_select with pod (anti)affinity: use kbg_allocate");
   std::vector<int32_t> mark(S.n_nodes, -1), touched, bt;
   Grouper grouper(S);
   Resolver rs{S, mark};
@@ -3662,6 +3742,12 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
         if (stop_at_first_success) {
           ++i;
           stop = true;
+          break;
+        }
+        if (!S.aff_gain_classes.empty()) {  // pod affinity gave a class nodes: rescan the rest
+          for (int32_t c : S.aff_gain_classes) S.aff_gain_flag[c] = 0;
+          S.aff_gain_classes.clear();
+          ++i;
           break;
         }
       }

@@ -285,6 +285,7 @@ struct Session {
   bool has_ports = false;
   int32_t PW = 0;                              // u64 words per port-atom set
   std::vector<uint64_t> node_ports, node_ports0;  // [N][PW] used (ip, protocol, port) atoms
+  std::unordered_map<int64_t, int32_t> port_hold; // (node << 32 | atom) -> pods placed this cycle holding it
   std::vector<uint64_t> cls_conf, cls_add;     // [class][PW] atoms a class conflicts with / records
   std::vector<std::vector<int32_t>> atom_cls;  // classes that conflict with each atom
   std::vector<uint64_t> h_class_mask0, h_class_mask_static;  // at open (ports applied) / static predicate only
@@ -321,6 +322,8 @@ struct Session {
   int64_t updates = 0, rebuilds = 0;
   bool vt_stale = false;                              // the victim tables follow older inputs
   std::vector<void*> vt_allocs;                       // their HBM (freed when they are rebuilt)
+  std::vector<int32_t> big_rows;                      // table rows of nodes with > 128 victim candidates
+  int32_t* d_big_rows = nullptr;
 
   // ---- NodeInfo.Tasks keys (node_info.go:101-106): AddTask of a PodKey the
   // node already holds returns an error and leaves the node unchanged, while
@@ -361,6 +364,12 @@ struct Session {
 
   kbg_stats stats{};
 };
+
+// A class-mask bit of (c, n) changed: the host-kept victim stop maps of that
+// class no longer know node n (Session::VictimCache).
+inline void vc_mask_changed(Session& S, int32_t c, int32_t n) {
+  if (S.vc.valid && S.vc.key.cls == c) S.vc.unk[n >> 5] |= 1u << (n & 31);
+}
 
 bool parse_go_int64(const std::string& s, int64_t* out);
 bool label_key_valid(const std::string& k);    // IsQualifiedName (validation.go:42-70)

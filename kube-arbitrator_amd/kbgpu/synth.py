@@ -410,7 +410,7 @@ def dupkey_fixture(seed, **kw):
     return fx
 
 
-def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3):
+def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3, aff=0.0, ports=0.0, big=False):
     """A cluster already full of Running gang jobs in several queues, with
     Pending jobs of every queue: the regime of reclaim and preempt
     (BASELINE config 5 in miniature). Tasks of a job share one request so the
@@ -422,12 +422,19 @@ def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3):
     for i in range(nodes):
         alloc = {"cpu": str(rng.choice([4, 8])), "memory": f"{rng.choice([8, 16])}Gi",
                  "pods": str(rng.choice([4, 8, 110]))}
-        nds.append({"name": f"n{i:02d}", "allocatable": alloc, "labels": {"zone": rng.choice(["a", "b"])}})
+        if big:  # nodes that hold hundreds of small pods (victim scans in several 64-candidate chunks)
+            alloc = {"cpu": "64", "memory": "256Gi", "pods": str(rng.choice([300, 600, 1100]))}
+        nds.append({"name": f"n{i:02d}", "allocatable": alloc,
+                    "labels": {"zone": rng.choice(["a", "b"]), "host": f"n{i:02d}"}})
     free = {n["name"]: [int(n["allocatable"]["cpu"]) * 1000, int(n["allocatable"]["pods"])] for n in nds}
+    used_ports = {}
     pods, pgs = [], []
     uid = 0
     uniform = rng.random() < 0.7  # one request size for every job: evictions free exactly what a pipeline needs
     base = (rng.choice([500, 1000, 2000]), rng.choice(["0", "512Mi", "1Gi"]))
+    if big:
+        base = (rng.choice([50, 100, 200]), "0")
+        uniform = True
     for j in range(jobs):
         ns = rng.choice(["c1", "c2"])
         pg = f"pg{j}"
@@ -438,16 +445,30 @@ def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3):
         cpu, mem = base if uniform else (rng.choice([500, 1000, 2000]), rng.choice(["0", "512Mi", "1Gi"]))
         req = {"cpu": f"{cpu}m", "memory": mem}
         running = rng.random() < 0.6
+        app = f"app{rng.randrange(3)}"
+        job_aff = None
+        if rng.random() < aff:  # required pod (anti)affinity on the zone or the host
+            term = {"labelSelector": {"matchLabels": {"app": rng.choice([app, f"app{rng.randrange(3)}"])}},
+                    "topologyKey": rng.choice(["zone", "host"])}
+            job_aff = {rng.choice(["podAffinity", "podAntiAffinity", "podAntiAffinity"]):
+                       {"requiredDuringSchedulingIgnoredDuringExecution": [term]}}
+        job_ports = None
+        if rng.random() < ports:
+            job_ports = [{"hostPort": rng.choice([80, 443]), "protocol": rng.choice(["", "UDP"]),
+                          "hostIP": rng.choice(["", "10.0.0.1"])}]
         for t in range(n_t):
             uid += 1
             phase, node = "Pending", ""
             if running:
-                cands = [n["name"] for n in nds if free[n["name"]][0] >= cpu and free[n["name"]][1] > 0]
+                cands = [n["name"] for n in nds if free[n["name"]][0] >= cpu and free[n["name"]][1] > 0
+                         and not (job_ports and used_ports.get(n["name"]))]
                 if cands:
                     node = rng.choice(cands)
                     free[node][0] -= cpu
                     free[node][1] -= 1
                     phase = "Running"
+                    if job_ports:
+                        used_ports[node] = True
             p = {"uid": f"u{uid:04d}", "namespace": ns, "name": f"{pg}-t{t}", "phase": phase, "nodeName": node,
                  "annotations": {"scheduling.k8s.io/group-name": pg},
                  "containers": [{"requests": dict(req) if rng.random() < 0.95 or not uniform else {"cpu": "5m"}}]}
@@ -455,6 +476,12 @@ def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3):
                 p["priority"] = rng.choice([1, 5, 10])
             if rng.random() < 0.15:
                 p["nodeSelector"] = {"zone": rng.choice(["a", "b"])}
+            if aff:
+                p["labels"] = {"app": app}
+                if job_aff:
+                    p["affinity"] = job_aff
+            if job_ports:
+                p["containers"][0]["ports"] = job_ports
             pods.append(p)
     plugins = ["priority", "gang", "drf", "predicates", "proportion"]
     rng.shuffle(plugins)

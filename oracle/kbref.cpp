@@ -15,6 +15,7 @@
 //   pkg/scheduler/plugins/{drf,proportion,gang,priority,predicates}
 //   pkg/scheduler/actions/allocate/allocate.go:41-176
 //   pkg/scheduler/actions/backfill/backfill.go:40-71 (fixture "actions": [..., "backfill"])
+//   pkg/scheduler/actions/{reclaim/reclaim.go:41-188, preempt/preempt.go:43-253}, framework/statement.go
 //   vendor/k8s.io/kubernetes/pkg/scheduler/algorithm/predicates/predicates.go:797-862,1031-1051,1489-1517
 //   vendor/k8s.io/kubernetes/pkg/scheduler/cache/host_ports.go:29-135, node_info.go:593-605 (host ports)
 //   vendor/k8s.io/kubernetes/pkg/apis/core/v1/helper/helpers.go:222-331,412-441
@@ -33,9 +34,11 @@
 // Go map iteration order (random in the reference) is replaced by insertion
 // order everywhere; SURVEY F4 makes that order an input of both sides.
 //
-// Not supported (the session is rejected with status "unsupported", the same
-// boundary the device path draws): any pod with PodAffinity/PodAntiAffinity
-// while the predicates plugin is enabled.
+// Inter-pod (anti)affinity (vendor predicates.go:1155-1466, the meta == nil
+// slow path) and host ports run in every action, with the podLister and
+// node.Pods() read live. Nothing is rejected as "unsupported" by the oracle;
+// the device path refuses only nodes with more than 1024 Running candidates
+// in a victim scan.
 
 #include <algorithm>
 #include <atomic>
@@ -2064,8 +2067,6 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache, in
   for (auto& a : actions) {
     if (a == "allocate") { ssn->action = ""; allocate_execute(ssn); }
     else if (a == "backfill") { ssn->action = "backfill"; backfill_execute(ssn); }
-    else if ((a == "reclaim" || a == "preempt") && (ssn->pending_host_ports || ssn->pod_affinity_terms))
-      throw Unsupported("reclaim/preempt with pending host ports: not on the device path");
     else if (a == "reclaim") { ssn->action = "reclaim"; reclaim_execute(ssn); }
     else if (a == "preempt") { ssn->action = "preempt"; preempt_execute(ssn); }
     else throw BadInput("unsupported action " + a);

@@ -376,3 +376,69 @@ def test_dupkey_fuzz_parity(seed):
     compare_outputs(run_oracle(fx), got)
     if ssn:
         ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(120))
+def test_victim_affinity_parity(seed):
+    """reclaim/preempt (reclaim.go, preempt.go) on contended clusters whose
+    jobs carry required pod (anti)affinity on the zone or the host: the
+    victim scan's class masks follow evictions, pipelines and discarded
+    statements through kbg_affinity.cpp's counts."""
+    fx = synth.contended_fixture(7000 + seed, nodes=12, jobs=14, tasks=8, aff=0.5)
+    got, ssn = run_fixture(fx)
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(100))
+def test_victim_host_ports_parity(seed):
+    """reclaim/preempt with host ports: an eviction frees the victim's port
+    atoms, a pipelined preemptor takes them (predicates.go host-port check)."""
+    fx = synth.contended_fixture(8000 + seed, nodes=12, jobs=14, tasks=8, ports=0.4)
+    got, ssn = run_fixture(fx)
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_victim_big_node_parity(seed):
+    """Nodes with 130-250 Running pods: the victim scan walks the candidates in
+    several 64-wide chunks (kbg_victim_big_kernel), evictions exact."""
+    fx = synth.contended_fixture(9000 + seed, big=True, nodes=2, jobs=50, tasks=24)
+    running = {}
+    for p in fx["pods"]:
+        if p["phase"] == "Running":
+            running[p["nodeName"]] = running.get(p["nodeName"], 0) + 1
+    assert max(running.values()) > 128
+    got, ssn = run_fixture(fx)
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
+@pytest.mark.parametrize("seed", list(range(0, 60, 4)))
+def test_select_replays_with_affinity(seed):
+    """kbg_select on affinity fixtures: a placement that creates an affinity
+    gain for later tasks is seen by the next call (the gain rescan)."""
+    import ctypes
+    from kbgpu import _abi
+    fx = synth.affinity_fixture(seed)
+    fx["actions"] = ["allocate"]
+    ref = run_oracle(fx)
+    if ref["status"] != "ok":
+        pytest.skip(ref["status"])
+    ssn = _open(fx)
+    idx = {t.uid: i for i, t in enumerate(ssn.flat.task_objs)}
+    decided = {d["task"]: (d["node"], d["kind"]) for d in ref["decisions"]}
+    L = _abi.lib()
+    node, kind, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    for uid in ref["evaluated"]:
+        arr = (ctypes.c_int32 * 1)(idx[uid])
+        _abi.check(L.kbg_select(ssn.handle, arr, 1, 1, ctypes.byref(node), ctypes.byref(kind), ctypes.byref(n)))
+        if uid in decided:
+            assert ssn.flat.node_names[node.value] == decided[uid][0], uid
+        else:
+            assert node.value == -1, uid
+    ssn.close()
