@@ -141,19 +141,30 @@ def cpu_baseline(fx, label, threads=1, faithful=False, budget=0.0):
 
 
 def load_pmc(n_nodes, mode):
-    """The scan kernel's per-launch PMC figures in `mode` ("full_scan" /
-    "grouped") from the committed rocprofv3 summary of this same bench
-    command (profiles/pmc_scan.json), if it matches the workload."""
+    """A kernel's per-launch PMC figures from the committed rocprofv3 summary
+    of this same bench command (profiles/pmc_scan.json), if it matches the
+    workload: the scan kernel in `mode` "full_scan" / "grouped", or the
+    victim kernel ("victim", C5)."""
     p = os.path.join(ROOT, "profiles", "pmc_scan.json")
     if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
-        if d.get("n_nodes") == n_nodes and d.get(mode):
-            return dict(d[mode], source=d.get("source"))
+        sec = d.get(mode)
+        if sec and sec.get("n_nodes", d.get("n_nodes")) == n_nodes:
+            return dict(sec, source=d.get("source"))
     except (OSError, ValueError):
         pass
     return None
+
+
+def valu_ceiling(pmc, avg_us):
+    """The VALU-issue ceiling of a kernel: its PMC wave instructions at 4
+    cycles each spread over every SIMD of the chip at the peak clock."""
+    floor_us = pmc["valu_insts_per_launch"] * VALU_CYC / (SIMDS * CLOCK_GHZ * 1e3)
+    return {"wave_insts_per_launch": pmc["valu_insts_per_launch"], "issue_floor_us": floor_us,
+            "frac": floor_us / avg_us if avg_us > 0 else None,
+            "model": f"{VALU_CYC} cycles per wave64 VALU instruction per SIMD, {SIMDS} SIMDs at {CLOCK_GHZ} GHz"}
 
 
 def main():
@@ -286,10 +297,7 @@ def main():
                 out["hbm"] = {"bytes_per_launch": b, "achieved_gbs": b / (avg_us * 1e-6) / 1e9,
                               "peak_gbs": HBM_PEAK_GBS, "frac": b / (avg_us * 1e-6) / 1e9 / HBM_PEAK_GBS}
             if pmc.get("valu_insts_per_launch") is not None:
-                floor_us = pmc["valu_insts_per_launch"] * VALU_CYC / (SIMDS * CLOCK_GHZ * 1e3)
-                out["valu"] = {"wave_insts_per_launch": pmc["valu_insts_per_launch"], "issue_floor_us": floor_us,
-                               "frac": floor_us / avg_us, "model": f"{VALU_CYC} cycles per wave64 VALU instruction "
-                               f"per SIMD, {SIMDS} SIMDs at {CLOCK_GHZ} GHz"}
+                out["valu"] = valu_ceiling(pmc, avg_us)
             out["pmc_source"] = pmc.get("source")
         return out
 
@@ -520,6 +528,13 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid, open_ms_
     algo = nodes_per_rank * NODE_RECORD_B + running / max(1, world) * TASK_RECORD_B
     launch_us = vms * 1e3 / max(1, vscans)
     ach = algo / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
+    pmc = load_pmc(n_nodes, "victim") if comm is None else None
+    roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": pmc["hbm_bytes_per_launch"] if pmc else None, "kernel": "kbg_victim_kernel",
+            "avg_launch_us": launch_us, "algo_bytes_per_launch": algo}
+    if pmc:
+        roof["valu"] = valu_ceiling(pmc, launch_us)
+        roof["pmc_source"] = pmc.get("source")
     line = {
         "metric": "task placements/sec + p50 scheduling-cycle latency, contended cluster (reclaim/preempt)",
         "value": total / elapsed,
@@ -538,9 +553,7 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid, open_ms_
                                f"(~95% CPU), actions {', '.join(fx['actions'])}, default tiers",
                    "parallelism": f"node-axis shards x{world} (RCCL min-reduce of the victim-scan stop node)"
                                   if world > 1 else "single-gpu"},
-        "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": "kbg_victim_kernel",
-                     "avg_launch_us": launch_us, "algo_bytes_per_launch": algo},
+        "roofline": roof,
         "decisions_per_cycle": dec // max(1, args.steps),
         "evictions_per_cycle": ev // max(1, args.steps),
         "victim_scans_per_cycle": vscans // max(1, args.steps),

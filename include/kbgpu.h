@@ -35,9 +35,13 @@ extern "C" {
 typedef enum kbg_status {
   KBG_OK = 0,
   KBG_E_INVALID = 1,     /* malformed snapshot / arguments */
-  KBG_E_UNSUPPORTED = 2, /* session uses a predicate the device path does not run
-                            (pod (anti)affinity): run the reference path
-                            instead. Never a silent fallback. */
+  KBG_E_UNSUPPORTED = 2, /* a case the device path declines, named in
+                            kbg_last_error: reclaim / preempt with more than
+                            1024 Running session tasks on one node, a
+                            statement discard of a pipeline onto a node that
+                            already held its pod key, and the session-update
+                            cases listed at kbg_session_update. The caller
+                            runs the reference path. Never a silent fallback. */
   KBG_E_REF_PANIC = 3,   /* the reference would panic here (Resource.Sub underflow
                             resource_info.go:100-110, proportion water-fill F9
                             proportion.go:119-140, nil-Node predicate
@@ -369,8 +373,10 @@ kbg_status kbg_backfill(kbg_session* s, kbg_decision* out, int32_t cap, int32_t*
  * reference does and pipelines the task. Statements (preempt) commit or
  * discard as statement.go does, including the node-side quirk of unevict.
  * Both write the cycle's decision log (pipelines carry the action); the
- * evictions are read with kbg_evictions_get. Sessions with host ports or
- * node-axis shards are refused (KBG_E_UNSUPPORTED). */
+ * evictions are read with kbg_evictions_get. Pod (anti)affinity and host
+ * ports are re-derived per eviction / pipeline (kbg_affinity.cpp, the port
+ * atoms); nodes with up to 1024 Running session tasks are scanned in 64-wide
+ * candidate chunks; more than that is refused (KBG_E_UNSUPPORTED). */
 kbg_status kbg_reclaim(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out);
 kbg_status kbg_preempt(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out);
 

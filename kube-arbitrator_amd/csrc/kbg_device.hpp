@@ -98,11 +98,11 @@ struct VictimTables {
   const int32_t* maxtasks;
   const uint8_t* panic_node;    // nil Node under an active predicates plugin
   const uint64_t* class_mask;
-  const int32_t* nt_off;        // [N+1] candidate lists: session tasks Running on the node at open
-  const int32_t* nt_task;       //       in NodeInfo.Tasks order
-  const int32_t* t_job;         // per task
-  const double* t_req;          // [T][3]
-  uint8_t* t_run;               // node-side status still Running
+  const int32_t* nt_off;        // [N+1] candidate lists: session tasks Running on the node at open,
+                                //       in NodeInfo.Tasks order; position p = nt_off[n] + k
+  const int2* c_jq;             // [P] {job, queue} of the candidate at position p (coalesced per lane)
+  const double* c_req;          // [P][3] its Resreq
+  uint8_t* c_run;               // [P] node-side status still Running
   const int32_t* j_queue;       // per job
   const int32_t* j_min;
   int32_t* j_ready;             // gang readyTaskNum
@@ -114,7 +114,7 @@ struct VictimTables {
 
 // A host-side change to the victim tables.
 struct StateDelta {
-  int32_t kind;   // 0 task running flag, 1 job ready, 2 job drf alloc, 3 queue alloc
+  int32_t kind;   // 0 candidate running flag (index = candidate position), 1 job ready, 2 job drf alloc, 3 queue alloc
   int32_t index;
   double v[3];
 };
@@ -176,12 +176,20 @@ enum NodeFlag : uint8_t { NF_UNSCHED = 1, NF_NIL = 2, NF_DEAD = 4 };
 hipError_t launch_build_class_mask(const StaticTables& t, int32_t n_classes, int32_t W, uint64_t* class_mask,
                                    hipStream_t stream);
 
+// Words a row takes in one shard slot of the feasibility bitmaps: Wl rounded
+// up to whole quads (a quad = the 4 words one scan workgroup produces).
+__host__ __device__ inline int32_t kbg_slot_words(int32_t Wl) { return (Wl + 3) & ~3; }
+
 // Feasibility bitmaps of a batch of G evaluation rows live in one buffer laid
-// out [slot][plane][row][Wl] (u64 words; plane 0 = Idle-or-Releasing fit,
-// plane 1 = Idle fit; slot = node-axis shard, Wl = 64-node words per shard).
-// Unsharded, slot count 1 and Wl = W. Sharded, the per-shard slots are exactly
-// an all-gather's receive layout, so the select kernel reads the same buffer
-// whether the slots were written locally or gathered over RCCL.
+// out [slot][plane][quad][row][4] (u64 words; plane 0 = Idle-or-Releasing
+// fit, plane 1 = Idle fit; slot = node-axis shard of Wl 64-node words, quad
+// = 4 consecutive words of it, kbg_slot_words(Wl) / 4 quads per row). A scan
+// workgroup writes its rows' quad as one contiguous run, so no cache line is
+// shared between workgroups (or XCDs). Unsharded, slot count 1 and Wl = W.
+// Sharded, the per-shard slots are exactly an all-gather's receive layout, so
+// the select kernel reads the same buffer whether the slots were written
+// locally or gathered over RCCL.
+
 struct ScanGeom {
   int32_t n_nodes;   // global node count N
   int32_t W;         // global 64-node words, ceil(N/64)

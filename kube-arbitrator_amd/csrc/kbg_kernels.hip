@@ -45,29 +45,27 @@ __device__ __forceinline__ uint64_t fit_mask(double a0, double a1, double a2, do
 }
 
 // One row J of the workgroup's 64: its request (q, read from LDS as a
-// same-address broadcast by the caller), its class-mask word for this wave's
-// 64 nodes from lane J (v_readlane); lane J keeps the row's two masks
-// (v_writelane_b32 with an inline-constant lane select: one scalar operand
-// per VALU op on gfx9).
+// same-address broadcast by the caller) against this wave's 64 nodes. The raw
+// fit ballots go to lane J (v_writelane_b32 with an inline-constant lane
+// select: one scalar operand per VALU op on gfx9); the class mask, the pod
+// cap and the Releasing-zero shortcut are applied by lane J itself once all
+// rows are done, so a row costs its compares plus two lane moves (four when
+// the wave holds Releasing resources).
 template <bool INT_MODE, bool REL_ZERO, int J>
-__device__ __forceinline__ void scan_row(double q0, double q1, double q2, uint64_t lane_mw, uint64_t rzm,
-                                         uint64_t okm, double ic, double im, double ig, double rc, double rm,
-                                         double rg, uint32_t (&keep)[4]) {
-  // (the builtin returns int: go through uint32_t so the low word is not sign-extended)
-  const uint32_t mw_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lane_mw, J);
-  const uint32_t mw_hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lane_mw >> 32), J);
-  const uint64_t mw = (((uint64_t)mw_hi << 32) | (uint64_t)mw_lo) & okm;
-  const uint64_t mi = fit_mask<INT_MODE>(ic, im, ig, q0, q1, q2) & mw;
-  uint64_t mr;
-  if (REL_ZERO) mr = ((rzm >> J) & 1ull) ? mw : 0ull;  // LessEqual(req, 0) on every lane
-  else mr = fit_mask<INT_MODE>(rc, rm, rg, q0, q1, q2) & mw;
-  const uint64_t mf = mi | mr;
-  asm("v_writelane_b32 %0, %4, %8\n\t"
-      "v_writelane_b32 %1, %5, %8\n\t"
-      "v_writelane_b32 %2, %6, %8\n\t"
-      "v_writelane_b32 %3, %7, %8"
-      : "+v"(keep[0]), "+v"(keep[1]), "+v"(keep[2]), "+v"(keep[3])
-      : "s"((uint32_t)mf), "s"((uint32_t)(mf >> 32)), "s"((uint32_t)mi), "s"((uint32_t)(mi >> 32)), "i"(J));
+__device__ __forceinline__ void scan_row(double q0, double q1, double q2, double ic, double im, double ig, double rc,
+                                         double rm, double rg, uint32_t (&keep)[4]) {
+  const uint64_t mi = fit_mask<INT_MODE>(ic, im, ig, q0, q1, q2);
+  asm("v_writelane_b32 %0, %2, %4\n\t"
+      "v_writelane_b32 %1, %3, %4"
+      : "+v"(keep[0]), "+v"(keep[1])
+      : "s"((uint32_t)mi), "s"((uint32_t)(mi >> 32)), "i"(J));
+  if constexpr (!REL_ZERO) {
+    const uint64_t mr = fit_mask<INT_MODE>(rc, rm, rg, q0, q1, q2);
+    asm("v_writelane_b32 %0, %2, %4\n\t"
+        "v_writelane_b32 %1, %3, %4"
+        : "+v"(keep[2]), "+v"(keep[3])
+        : "s"((uint32_t)mr), "s"((uint32_t)(mr >> 32)), "i"(J));
+  }
 }
 
 // All ROWS rows of the workgroup, unrolled at compile time in groups of
@@ -81,9 +79,8 @@ constexpr int kRowGroup = 8;
 #endif
 constexpr int kSmallBatchRows = KBG_SMALL_BATCH_ROWS;  // launch_scan: batches up to this many rows use 16-row workgroups
 template <bool INT_MODE, bool REL_ZERO, int ROWS, int J = 0>
-__device__ __forceinline__ void scan_rows(const double (*s_req)[3], uint64_t lane_mw, uint64_t rzm, uint64_t okm,
-                                          double ic, double im, double ig, double rc, double rm, double rg,
-                                          uint32_t (&keep)[4]) {
+__device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, double im, double ig, double rc,
+                                          double rm, double rg, uint32_t (&keep)[4]) {
   double q[kRowGroup][3];
 #pragma unroll
   for (int u = 0; u < kRowGroup; ++u) {
@@ -92,11 +89,10 @@ __device__ __forceinline__ void scan_rows(const double (*s_req)[3], uint64_t lan
     q[u][2] = s_req[J + u][2];
   }
   [&]<int... U>(std::integer_sequence<int, U...>) {
-    (scan_row<INT_MODE, REL_ZERO, J + U>(q[U][0], q[U][1], q[U][2], lane_mw, rzm, okm, ic, im, ig, rc, rm, rg, keep),
-     ...);
+    (scan_row<INT_MODE, REL_ZERO, J + U>(q[U][0], q[U][1], q[U][2], ic, im, ig, rc, rm, rg, keep), ...);
   }(std::make_integer_sequence<int, kRowGroup>{});
   if constexpr (J + kRowGroup < ROWS)
-    scan_rows<INT_MODE, REL_ZERO, ROWS, J + kRowGroup>(s_req, lane_mw, rzm, okm, ic, im, ig, rc, rm, rg, keep);
+    scan_rows<INT_MODE, REL_ZERO, ROWS, J + kRowGroup>(s_req, ic, im, ig, rc, rm, rg, keep);
 }
 
 template <bool INT_MODE, int ROWS>
@@ -121,7 +117,6 @@ __global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, ScanGeom geo,
     s_req[lane][2] = tr.req[2];
   }
   const uint64_t lane_mw = live ? class_mask[(size_t)tr.cls * geo.W + chunk] : 0ull;  // row `lane`, this chunk
-  const uint64_t rzm = __ballot((tr.flags & kRowRelZeroFits) != 0);  // bits >= ROWS are never read
   __syncthreads();
   if (!live) return;  // wave-uniform, after the barrier
   const int node = chunk * 64 + lane;
@@ -141,20 +136,27 @@ __global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, ScanGeom geo,
   }
   const uint64_t okm = __ballot(valid && (!cap_check || nt < mt));  // predicates.go:125-127 pod cap
   // Releasing is usually zero on every node of the wave; then a row's
-  // Releasing fit is LessEqual(req, 0) on every lane, precomputed per row.
+  // Releasing fit is LessEqual(req, 0) on every lane (kRowRelZeroFits).
   const bool rel_zero_wave = __ballot(!(rc == 0.0 && rm == 0.0 && rg == 0.0)) == 0ull;
-  uint32_t keep[4] = {0u, 0u, 0u, 0u};  // lane j: (feasible, idle-fit) masks of row t0+j
-  if (rel_zero_wave)
-    scan_rows<INT_MODE, true, ROWS>(s_req, lane_mw, rzm, okm, ic, im, ig, rc, rm, rg, keep);
-  else
-    scan_rows<INT_MODE, false, ROWS>(s_req, lane_mw, rzm, okm, ic, im, ig, rc, rm, rg, keep);
+  uint32_t keep[4] = {0u, 0u, 0u, 0u};  // lane j: raw (idle-fit, releasing-fit) masks of row t0+j
+  uint64_t mr;
+  if (rel_zero_wave) {
+    scan_rows<INT_MODE, true, ROWS>(s_req, ic, im, ig, rc, rm, rg, keep);
+    mr = (tr.flags & kRowRelZeroFits) ? ~0ull : 0ull;
+  } else {
+    scan_rows<INT_MODE, false, ROWS>(s_req, ic, im, ig, rc, rm, rg, keep);
+    mr = (uint64_t)keep[2] | ((uint64_t)keep[3] << 32);
+  }
   if (lane < nt_blk) {
-    // [slot][plane][row][Wl] (kbg_device.hpp ScanGeom)
+    const uint64_t mw = lane_mw & okm;  // static predicate and pod cap of row t0+lane on this wave's nodes
+    const uint64_t mi = ((uint64_t)keep[0] | ((uint64_t)keep[1] << 32)) & mw;
+    // [slot][plane][quad][row][4] (kbg_device.hpp ScanGeom): the workgroup's
+    // four waves fill 32 contiguous bytes per row, its rows one 2-KB run
     const int slot = rel / geo.Wl, w = rel - slot * geo.Wl;
-    const size_t plane = (size_t)n_tasks * geo.Wl;
-    uint64_t* o = out + (size_t)slot * 2 * plane + (size_t)(t0 + lane) * geo.Wl + w;
-    o[0] = (uint64_t)keep[0] | ((uint64_t)keep[1] << 32);
-    o[plane] = (uint64_t)keep[2] | ((uint64_t)keep[3] << 32);
+    const size_t plane = (size_t)n_tasks * kbg_slot_words(geo.Wl);
+    uint64_t* o = out + (size_t)slot * 2 * plane + ((size_t)(w >> 2) * n_tasks + t0 + lane) * 4 + (w & 3);
+    o[0] = mi | (mr & mw);
+    o[plane] = mi;
   }
 }
 
@@ -195,8 +197,7 @@ __global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restr
   const int lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= n_rows) return;
-  const size_t plane = (size_t)n_rows * Wl;
-  const uint64_t* row = bits + (size_t)t * Wl;
+  const size_t plane = (size_t)n_rows * kbg_slot_words(Wl);
   const int M = (int)(cap_off[t + 1] - cap_off[t]);
   uint32_t* cand = out_cand + cap_off[t];
   int found = 0;
@@ -205,8 +206,8 @@ __global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restr
     const int c = base + lane;
     uint64_t f = 0ull, iw = 0ull;
     if (c < W) {
-      const int slot = c / Wl;
-      const uint64_t* p = row + (size_t)slot * 2 * plane + (c - slot * Wl);
+      const int slot = c / Wl, w = c - slot * Wl;
+      const uint64_t* p = bits + (size_t)slot * 2 * plane + ((size_t)(w >> 2) * n_rows + t) * 4 + (w & 3);
       f = p[0];
       iw = p[plane];
     }
@@ -325,13 +326,14 @@ struct VCand {
 __device__ __forceinline__ VCand load_cand(const VictimScan& p, const VictimTables& t, int off, int L, int k) {
   VCand c{-1, -1, {0.0, 0.0, 0.0}, false};
   if (k < L) {
-    const int task = t.nt_task[off + k];
-    c.job = t.t_job[task];
-    c.queue = t.j_queue[c.job];
-    c.r[0] = t.t_req[3 * (size_t)task];
-    c.r[1] = t.t_req[3 * (size_t)task + 1];
-    c.r[2] = t.t_req[3 * (size_t)task + 2];
-    if (t.t_run[task]) {
+    const size_t pos = (size_t)off + k;  // candidate records in node order: a chunk is one contiguous read
+    const int2 jq = t.c_jq[pos];
+    c.job = jq.x;
+    c.queue = jq.y;
+    c.r[0] = t.c_req[3 * pos];
+    c.r[1] = t.c_req[3 * pos + 1];
+    c.r[2] = t.c_req[3 * pos + 2];
+    if (t.c_run[pos]) {
       if (p.mode == VM_PREEMPT_JOBS) c.f = c.queue == p.queue && c.job != p.job;  // preempt.go:100-112
       else if (p.mode == VM_PREEMPT_TASKS) c.f = c.job == p.job;                // :146-154
       else c.f = c.queue != p.queue;                                            // reclaim.go:113-126
@@ -403,11 +405,11 @@ __device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t
         bool lpanic = false, vp = false;
         for (int h2 = 0; h2 < h; ++h2)  // preemptees of earlier chunks (all before this lane's k)
           for (uint64_t b = pm[h2]; b; b &= b - 1) {
-            const int task2 = t.nt_task[off + h2 * 64 + __builtin_ctzll(b)];  // wave-uniform
-            const int32_t j2 = t.t_job[task2];
-            const int32_t q2 = t.j_queue[j2];
-            const double r2[3] = {t.t_req[3 * (size_t)task2], t.t_req[3 * (size_t)task2 + 1],
-                                  t.t_req[3 * (size_t)task2 + 2]};
+            const size_t p2 = (size_t)off + h2 * 64 + __builtin_ctzll(b);  // wave-uniform
+            const int2 jq2 = t.c_jq[p2];
+            const int32_t j2 = jq2.x;
+            const int32_t q2 = jq2.y;
+            const double r2[3] = {t.c_req[3 * p2], t.c_req[3 * p2 + 1], t.c_req[3 * p2 + 2]};
             if (on) apply_preemptee(t, fns, j2, q2, r2, false, c.job, c.queue, xd, xp, lpanic, vp);
           }
         for (uint64_t b = pm[h]; b; b &= b - 1) {  // this chunk, in order, while k2 <= k
@@ -439,13 +441,18 @@ __device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t
   if (!victims) return kNone;
   double all[3] = {0.0, 0.0, 0.0};  // validateVictims (preempt.go:242-253), in victims order
 #pragma unroll
-  for (int h = 0; h < NCH; ++h)
+  for (int h = 0; h < NCH; ++h) {
+    if (!vm[h]) continue;
+    // each lane reads its own candidate's request (one coalesced load), the
+    // wave-uniform sum takes them lane by lane in order
+    const VCand c = load_cand(p, t, off, L, h * 64 + lane);
     for (uint64_t b = vm[h]; b; b &= b - 1) {
-      const int task2 = t.nt_task[off + h * 64 + __builtin_ctzll(b)];
-      all[0] += t.t_req[3 * (size_t)task2];
-      all[1] += t.t_req[3 * (size_t)task2 + 1];
-      all[2] += t.t_req[3 * (size_t)task2 + 2];
+      const int l2 = __builtin_ctzll(b);
+      all[0] += rl_d(c.r[0], l2);
+      all[1] += rl_d(c.r[1], l2);
+      all[2] += rl_d(c.r[2], l2);
     }
+  }
   if (res_less3(all, p.req)) return kNone;
   return (uint32_t)n << 1;
 }
@@ -545,7 +552,7 @@ __device__ __forceinline__ void apply_node_delta(const NodeSoA& nd, const NodeDe
 
 __device__ __forceinline__ void apply_state_delta(const VictimTables& t, const StateDelta& x) {
   switch (x.kind) {
-    case 0: t.t_run[x.index] = (uint8_t)(x.v[0] != 0.0); break;
+    case 0: t.c_run[x.index] = (uint8_t)(x.v[0] != 0.0); break;
     case 1: t.j_ready[x.index] = (int32_t)x.v[0]; break;
     case 2:
       for (int k = 0; k < 3; ++k) t.j_alloc[3 * (size_t)x.index + k] = x.v[k];

@@ -529,7 +529,7 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   HIP_TRY(hipMemcpyAsync(S.d_up, sg.h_up, up_bytes, hipMemcpyHostToDevice, S.stream));
   // this process scans its shard (or every shard when they are all local)
   kbg::ScanGeom geo{S.n_nodes, S.W, S.Wl, 0, S.R * S.Wl, S.tab_lo};
-  const size_t slot_words = (size_t)2 * G * S.Wl;
+  const size_t slot_words = (size_t)2 * G * kbg::kbg_slot_words(S.Wl);
   uint64_t* out = S.d_bits;
   if (S.comm) {
     geo.chunk_lo = S.shard * S.Wl;
@@ -1669,7 +1669,7 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   const size_t up_cap = (size_t)kbg::kbg_pad_rows(S.K) * sizeof(kbg::TaskRec) + ((size_t)S.K + 1) * 4;
   const size_t down_cap = (size_t)S.K + (size_t)S.cand_cap;
   if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) || (st = dalloc(S, &S.d_up, up_cap)) ||
-      (st = dalloc(S, &S.d_bits, (size_t)S.R * 2 * S.K * S.Wl)) ||
+      (st = dalloc(S, &S.d_bits, (size_t)S.R * 2 * S.K * kbg::kbg_slot_words(S.Wl))) ||
       (st = dalloc(S, &S.d_down, down_cap)) || (st = dalloc(S, &S.d_deltas, S.K)))
     return st;
   for (kbg::Stage& g : S.stages) {
@@ -2573,7 +2573,7 @@ kbg_status victim_push(Session& S, const std::vector<int32_t>& touched) {
 // Device copies of the victim tables; the live parts (running flags, gang
 // readiness, drf / proportion allocations) are re-uploaded at every action.
 kbg_status vt_setup(Session& S) {
-  const size_t T = (size_t)std::max(1, S.n_tasks), J = (size_t)std::max(1, S.n_jobs),
+  const size_t J = (size_t)std::max(1, S.n_jobs),
                Q = (size_t)std::max(1, S.n_queues);
   kbg_status st;
   if (S.vt_ready && S.vt_stale) {  // a session update changed the tasks behind them
@@ -2595,11 +2595,19 @@ kbg_status vt_setup(Session& S) {
     std::vector<uint8_t> pn(S.panic_node.begin(), S.panic_node.end());
     std::vector<int32_t> jq(S.job_queue), jm(S.n_jobs);
     for (int32_t j = 0; j < S.n_jobs; ++j) jm[j] = S.jobs_in[j].min_available;
-    std::vector<double> tr(3 * T, 0.0), qd(3 * Q, 0.0);
-    for (int32_t t = 0; t < S.n_tasks; ++t) {
-      tr[3 * t] = S.treq[t].c;
-      tr[3 * t + 1] = S.treq[t].m;
-      tr[3 * t + 2] = S.treq[t].g;
+    // candidate records in node-list order (position p = nt_off[n] + k)
+    const size_t P = std::max<size_t>(1, S.nt_task.size());
+    std::vector<double> cr(3 * P, 0.0), qd(3 * Q, 0.0);
+    std::vector<int32_t> cjq(2 * P, 0);
+    S.t_pos.assign(S.n_tasks, -1);
+    for (size_t k = 0; k < S.nt_task.size(); ++k) {
+      const int32_t t = S.nt_task[k];
+      S.t_pos[t] = (int32_t)k;
+      cjq[2 * k] = S.task_job[t];
+      cjq[2 * k + 1] = S.job_queue[S.task_job[t]];
+      cr[3 * k] = S.treq[t].c;
+      cr[3 * k + 1] = S.treq[t].m;
+      cr[3 * k + 2] = S.treq[t].g;
     }
     for (int32_t q = 0; q < S.n_queues; ++q) {
       qd[3 * q] = S.q_deserved[q].c;
@@ -2607,11 +2615,10 @@ kbg_status vt_setup(Session& S) {
       qd[3 * q + 2] = S.q_deserved[q].g;
     }
     uint8_t *dpn, *drun;
-    int32_t *doff, *dtask, *djob, *djq, *djm, *djr;
-    double *dtr, *dja, *dqa, *dqd;
-    std::vector<int32_t> tj(S.task_job);
-    if ((st = hupload(S, &dpn, pn)) || (st = hupload(S, &doff, S.nt_off)) || (st = hupload(S, &dtask, S.nt_task)) ||
-        (st = hupload(S, &djob, tj)) || (st = hupload(S, &dtr, tr)) || (st = dalloc(S, &drun, T)) ||
+    int32_t *doff, *dcjq, *djq, *djm, *djr;
+    double *dcr, *dja, *dqa, *dqd;
+    if ((st = hupload(S, &dpn, pn)) || (st = hupload(S, &doff, S.nt_off)) || (st = hupload(S, &dcjq, cjq)) ||
+        (st = hupload(S, &dcr, cr)) || (st = dalloc(S, &drun, P)) ||
         (st = hupload(S, &djq, jq)) || (st = hupload(S, &djm, jm)) || (st = dalloc(S, &djr, J)) ||
         (st = dalloc(S, &dja, 3 * J)) || (st = dalloc(S, &dqa, 3 * Q)) || (st = hupload(S, &dqd, qd)) ||
         (st = dalloc(S, &S.d_vbits, 2 * (size_t)S.W32)) || (st = dalloc(S, &S.d_vbits_red, 2 * (size_t)S.W32)))
@@ -2653,10 +2660,9 @@ kbg_status vt_setup(Session& S) {
     }
     v.panic_node = dpn;
     v.nt_off = doff;
-    v.nt_task = dtask;
-    v.t_job = djob;
-    v.t_req = dtr;
-    v.t_run = drun;
+    v.c_jq = reinterpret_cast<const int2*>(dcjq);
+    v.c_req = dcr;
+    v.c_run = drun;
     v.j_queue = djq;
     v.j_min = djm;
     v.j_ready = djr;
@@ -2681,7 +2687,9 @@ kbg_status vt_setup(Session& S) {
     qa[3 * q + 1] = S.fin.qalloc[q].m;
     qa[3 * q + 2] = S.fin.qalloc[q].g;
   }
-  HIP_TRY(hipMemcpyAsync(S.vt.t_run, S.trun.data(), S.trun.size(), hipMemcpyHostToDevice, S.stream));
+  S.c_run_host.resize(std::max<size_t>(1, S.nt_task.size()));
+  for (size_t k = 0; k < S.nt_task.size(); ++k) S.c_run_host[k] = S.trun[S.nt_task[k]];
+  HIP_TRY(hipMemcpyAsync(S.vt.c_run, S.c_run_host.data(), S.nt_task.size(), hipMemcpyHostToDevice, S.stream));
   HIP_TRY(hipMemcpyAsync(S.vt.j_ready, S.committed_ready.data(), (size_t)S.n_jobs * 4, hipMemcpyHostToDevice,
                          S.stream));
   HIP_TRY(hipMemcpyAsync(S.vt.j_alloc, ja.data(), ja.size() * 8, hipMemcpyHostToDevice, S.stream));
@@ -2722,7 +2730,11 @@ struct Live {
     }
   }
   void ready(int32_t j, int32_t d) {
-    vc_dirty_job(S, j);
+    // the victim scan reads a job's readiness only through the gang fn's
+    // `MinAvailable <= ready - 1` (gang.go:104-124): its nodes change only
+    // when that test flips
+    const int32_t ma = S.jobs_in[j].min_available, r0 = S.committed_ready[j];
+    if ((S.vc.fns & kbg::VP_GANG) && ((ma <= r0 - 1) != (ma <= r0 + d - 1))) vc_dirty_job(S, j);
     S.committed_ready[j] += d;
     S.fin.jready[j] = S.committed_ready[j];
     vt_delta(S, 1, j, (double)S.committed_ready[j], 0, 0);
@@ -2778,7 +2790,7 @@ struct Live {
       touch(n);
     }
     S.trun[v] = 0;
-    vt_delta(S, 0, v, 0, 0, 0);
+    if (S.t_pos[v] >= 0) vt_delta(S, 0, S.t_pos[v], 0, 0, 0);
     return plugins(v, false);
   }
   // job Pipelined, NodeInfo.AddTask as Pipelined, AllocateFunc (session.go:205-241, statement.go:110-151)

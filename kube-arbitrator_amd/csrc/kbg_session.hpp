@@ -245,6 +245,8 @@ struct Session {
                                               // for good: unevict's AddTask fails, node_info.go:101-106)
   std::vector<int32_t> task_node;             // node index of a task's NodeName (-1: not a session node)
   std::vector<kbg_eviction> evictions;        // committed cache.Evict calls
+  std::vector<int32_t> t_pos;                 // a task's position in the candidate lists (-1: none)
+  std::vector<uint8_t> c_run_host;            // running flags in candidate order (upload staging)
   std::vector<int32_t> tier_preempt, tier_reclaim;  // VictimPlugin bits per tier holding an enabled victim fn
   int32_t max_candidates = 0;
   kbg::VictimTables vt{};                     // device copies (allocated at the first victim action)
@@ -352,7 +354,7 @@ struct Session {
   NodeSoA d_nodes{};
   NodeSoA d_nodes0{};       // pristine copy for kbg_session_reset
   uint64_t* d_class_mask = nullptr;
-  uint64_t* d_bits = nullptr;     // feasibility bitmaps [slot][plane][row][Wl] (ScanGeom)
+  uint64_t* d_bits = nullptr;     // feasibility bitmaps [slot][plane][quad][row][4] (ScanGeom)
   char* d_up = nullptr;           // rows + capoff of the batch being scanned (stream-ordered reuse)
   uint32_t* d_down = nullptr;     // counts + candidates of the batch being selected
   Stage stages[2];                // host staging of two batches in flight

@@ -1,0 +1,99 @@
+"""Summarise a gpurun_pmc.sh session (rocprofv3 kernel trace + separate PMC
+passes of one bench command) per kernel.
+
+Usage: python profiles/summarize_pmc.py <session dir> <config> > summary.json
+  <session dir>/c<config>_kt/kt_kernel_trace.csv        kernel durations
+  <session dir>/c<config>_pmc<i>/pmc<i>_counter_collection.csv  counters
+
+Kernels are keyed by their name up to the argument list, template arguments
+kept: kbg_scan_kernel<true, 64> runs the full-scan mode's batches (> 1024
+rows), kbg_scan_kernel<true, 16> the production mode's grouped batches.
+Derived figures (MI355X_MICROARCH.md):
+  hbm_read_bytes  = 2 x FETCH_SIZE KiB x 1024 (gfx950 tallies 128-B requests
+                    at 64 B; Infinity-Cache hits are counted too)
+  hbm_write_bytes = WRITE_SIZE KiB x 1024
+  valu_issue_floor_us = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x 2.4 GHz):
+                    the time the kernel's wave64 VALU instructions need at
+                    full issue on every SIMD of the chip
+  eff_clock_ghz   = GRBM_GUI_ACTIVE / 8 XCDs / profiled duration (reads high
+                    below ~0.3 ms dispatches)
+"""
+import csv
+import glob
+import json
+import os
+import re
+import statistics
+import sys
+
+SIMDS = 1024
+CLOCK_GHZ = 2.4
+VALU_CYC = 4
+WANT = ("kbg_scan_kernel", "kbg_select_kernel", "kbg_victim_kernel", "kbg_victim_big_kernel",
+        "kbg_victim_prep_kernel", "kbg_apply_kernel")
+
+
+def key(name):
+    base = name.split("(")[0]
+    base = re.sub(r"^void ", "", base)
+    return base.replace("kbg::", "")
+
+
+def rows(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def main():
+    d, cfg = sys.argv[1], sys.argv[2]
+    out = {"source": f"gpurun_pmc.sh: rocprofv3 --kernel-trace --stats, then one --pmc pass per counter group, of "
+                     f"`python3 bench.py --config {cfg} --steps 3 --warmup 1 --no-cpu-baseline --no-resident`",
+           "config": int(cfg), "kernels": {}}
+    ks = out["kernels"]
+    for r in rows(os.path.join(d, f"c{cfg}_kt", "kt_kernel_trace.csv")):
+        k = key(r["Kernel_Name"])
+        if not any(w in k for w in WANT):
+            continue
+        ks.setdefault(k, {"durations_ns": []})["durations_ns"].append(
+            int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    counters = {}
+    for p in sorted(glob.glob(os.path.join(d, f"c{cfg}_pmc*", "*_counter_collection.csv"))):
+        for r in rows(p):
+            k = key(r["Kernel_Name"])
+            if k not in ks:
+                continue
+            c = counters.setdefault(k, {}).setdefault(r["Counter_Name"], {})
+            c[int(r["Dispatch_Id"])] = c.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
+            dur = counters[k].setdefault("_dur", {}).setdefault(r["Counter_Name"], {})
+            dur[int(r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    for k, v in ks.items():
+        ds = v.pop("durations_ns")
+        v.update(launches=len(ds), avg_ns=statistics.mean(ds), median_ns=statistics.median(ds), min_ns=min(ds),
+                 max_ns=max(ds))
+        c = counters.get(k, {})
+        avg = {n: statistics.mean(x.values()) for n, x in c.items() if n != "_dur" and x}
+        v["counters_per_launch"] = avg
+        if "FETCH_SIZE" in avg:
+            v["hbm_read_bytes_per_launch"] = 2 * avg["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in avg:
+            v["hbm_write_bytes_per_launch"] = avg["WRITE_SIZE"] * 1024
+        if "hbm_read_bytes_per_launch" in v and "hbm_write_bytes_per_launch" in v:
+            v["hbm_bytes_per_launch"] = v["hbm_read_bytes_per_launch"] + v["hbm_write_bytes_per_launch"]
+        if avg.get("TCC_HIT_sum", 0) + avg.get("TCC_MISS_sum", 0) > 0:
+            v["l2_hit_rate"] = avg["TCC_HIT_sum"] / (avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
+        if "SQ_INSTS_VALU" in avg:
+            v["valu_insts_per_launch"] = avg["SQ_INSTS_VALU"]
+            v["valu_issue_floor_us"] = avg["SQ_INSTS_VALU"] * VALU_CYC / (SIMDS * CLOCK_GHZ * 1e3)
+            v["valu_issue_frac"] = v["valu_issue_floor_us"] * 1e3 / v["avg_ns"]
+            if avg.get("SQ_WAVES"):
+                v["valu_insts_per_wave"] = avg["SQ_INSTS_VALU"] / avg["SQ_WAVES"]
+        if "GRBM_GUI_ACTIVE" in avg:
+            pd = statistics.mean(c["_dur"]["GRBM_GUI_ACTIVE"].values())
+            v["profiled_avg_ns"] = pd
+            v["eff_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / pd
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main()
