@@ -293,7 +293,8 @@ typedef struct kbg_stats {
   int32_t shard_index;     /* the shard this process holds; -1 = every shard is local */
   int32_t int_scan;        /* 1 = the scan compares exact-integer thresholds (every value an
                               integer <= 2^51); 0 = the reference's LessEqual expression */
-  double exchange_ms;      /* summed HIP-event time of the per-batch RCCL all-gather */
+  double exchange_ms;      /* sharded sessions: time in the per-batch RCCL collectives (the bitmap
+                              all-gather, or the owner-resolve broadcast / min-reduces) */
   double backfill_ms;      /* wall time of the last kbg_backfill */
   double reclaim_ms;       /* wall time of the last kbg_reclaim */
   double preempt_ms;       /* wall time of the last kbg_preempt */
@@ -308,7 +309,8 @@ typedef struct kbg_stats {
   int64_t overlapped;        /* batches whose scan ran while the host resolved the previous batch */
   double update_ms;          /* wall time of the last kbg_session_update */
   int64_t update_rebuilds;   /* kbg_session_update calls that rebuilt the static masks / device tables */
-  int64_t reserved_stats[2];
+  int64_t owner_rounds;      /* owner-resolve (sharded allocate): exchange rounds over all batches */
+  int64_t reserved_stats[1];
 } kbg_stats;
 
 typedef struct kbg_session kbg_session;

@@ -206,10 +206,11 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
                        int32_t n_tasks, int32_t cap_check, int32_t int_mode, uint64_t* out, hipStream_t stream,
                        hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
-// Row g gets cap_off[g+1]-cap_off[g] candidate slots at out_cand[cap_off[g]].
-hipError_t launch_select(const uint64_t* bits, int32_t W, int32_t Wl, int32_t n_rows, const uint32_t* cap_off,
-                         uint32_t* out_cand, uint32_t* out_count, hipStream_t stream, hipEvent_t start = nullptr,
-                         hipEvent_t stop = nullptr);
+// Row g gets cap_off[g+1]-cap_off[g] candidate slots at out_cand[cap_off[g]],
+// taken from the global words [w_lo, w_hi) in node order.
+hipError_t launch_select(const uint64_t* bits, int32_t w_lo, int32_t w_hi, int32_t Wl, int32_t n_rows,
+                         const uint32_t* cap_off, uint32_t* out_cand, uint32_t* out_count, hipStream_t stream,
+                         hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
 hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream);
 hipError_t launch_mask_apply(uint64_t* class_mask, const MaskDelta* deltas, int32_t n_deltas, hipStream_t stream);

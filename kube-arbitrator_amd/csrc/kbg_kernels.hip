@@ -188,10 +188,12 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
 }
 
 // ---------------------------------------------------------------- select
-// One wave per row walks the row's words in global node order (shard slots in
-// rank order = ascending node index), so the candidates come out first-fit.
-__global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restrict__ bits, int32_t W, int32_t Wl,
-                                                         int32_t n_rows, const uint32_t* __restrict__ cap_off,
+// One wave per row walks the row's words [w_lo, w_hi) in global node order
+// (shard slots in rank order = ascending node index), so the candidates come
+// out first-fit. An owner-resolve shard selects over its own words only.
+__global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restrict__ bits, int32_t w_lo, int32_t w_hi,
+                                                         int32_t Wl, int32_t n_rows,
+                                                         const uint32_t* __restrict__ cap_off,
                                                          uint32_t* __restrict__ out_cand,
                                                          uint32_t* __restrict__ out_count) {
   const int lane = threadIdx.x & 63;
@@ -201,11 +203,11 @@ __global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restr
   const int M = (int)(cap_off[t + 1] - cap_off[t]);
   uint32_t* cand = out_cand + cap_off[t];
   int found = 0;
-  int base = 0;
-  for (; base < W && found < M; base += 64) {
+  int base = w_lo;
+  for (; base < w_hi && found < M; base += 64) {
     const int c = base + lane;
     uint64_t f = 0ull, iw = 0ull;
-    if (c < W) {
+    if (c < w_hi) {
       const int slot = c / Wl, w = c - slot * Wl;
       const uint64_t* p = bits + (size_t)slot * 2 * plane + ((size_t)(w >> 2) * n_rows + t) * 4 + (w & 3);
       f = p[0];
@@ -230,18 +232,18 @@ __global__ __launch_bounds__(256) void kbg_select_kernel(const uint64_t* __restr
     found += total;
   }
   if (lane == 0) {
-    const bool complete = base >= W && found <= M;
+    const bool complete = base >= w_hi && found <= M;
     const uint32_t cnt = (uint32_t)(found < M ? found : M);
     out_count[t] = cnt | (complete ? 0u : kCountIncompleteBit);
   }
 }
 
-hipError_t launch_select(const uint64_t* bits, int32_t W, int32_t Wl, int32_t n_rows, const uint32_t* cap_off,
-                         uint32_t* out_cand, uint32_t* out_count, hipStream_t stream, hipEvent_t start,
-                         hipEvent_t stop) {
+hipError_t launch_select(const uint64_t* bits, int32_t w_lo, int32_t w_hi, int32_t Wl, int32_t n_rows,
+                         const uint32_t* cap_off, uint32_t* out_cand, uint32_t* out_count, hipStream_t stream,
+                         hipEvent_t start, hipEvent_t stop) {
   if (n_rows <= 0) return hipSuccess;
-  hipExtLaunchKernelGGL(kbg_select_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, stream, start, stop, 0, bits, W, Wl,
-                        n_rows, cap_off, out_cand, out_count);
+  hipExtLaunchKernelGGL(kbg_select_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, stream, start, stop, 0, bits, w_lo,
+                        w_hi, Wl, n_rows, cap_off, out_cand, out_count);
   return hipGetLastError();
 }
 

@@ -538,13 +538,17 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   }
   HIP_TRY(kbg::launch_scan(S.d_nodes, geo, S.d_class_mask, d_tasks, G, S.pred_active ? 1 : 0, S.int_mode ? 1 : 0, out,
                            S.stream, sg.ev[0], sg.ev[1]));
-  if (S.comm) {  // in-place all-gather: every rank receives every shard's slot, in rank (= node) order
+  if (S.comm && !S.owner) {  // in-place all-gather: every rank receives every shard's slot, in rank (= node) order
     HIP_TRY(hipEventRecord(sg.ev[4], S.stream));
     const ncclResult_t nr = ncclAllGather(out, S.d_bits, slot_words, ncclUint64, S.comm->nccl, S.stream);
     if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
     HIP_TRY(hipEventRecord(sg.ev[5], S.stream));
   }
-  HIP_TRY(kbg::launch_select(S.d_bits, S.W, S.Wl, G, d_capoff, S.d_down + G, S.d_down, S.stream, sg.ev[2], sg.ev[3]));
+  // an owner-resolve shard (S.owner) selects its own words; otherwise every word
+  const int32_t w_lo = S.owner ? S.shard * S.Wl : 0;
+  const int32_t w_hi = S.owner ? std::min(S.W, (S.shard + 1) * S.Wl) : S.W;
+  HIP_TRY(kbg::launch_select(S.d_bits, w_lo, w_hi, S.Wl, G, d_capoff, S.d_down + G, S.d_down, S.stream, sg.ev[2],
+                             sg.ev[3]));
   HIP_TRY(hipMemcpyAsync(sg.h_down, S.d_down, ((size_t)G + total) * 4, hipMemcpyDeviceToHost, S.stream));
   HIP_TRY(hipEventRecord(sg.ev[6], S.stream));
   sg.G = G;
@@ -564,7 +568,7 @@ kbg_status device_wait(Session& S, kbg::Stage& sg) {
   S.stats.scan_kernel_ms += ms;
   HIP_TRY(hipEventElapsedTime(&ms, sg.ev[2], sg.ev[3]));
   S.stats.select_kernel_ms += ms;
-  if (S.comm) {
+  if (S.comm && !S.owner) {
     HIP_TRY(hipEventElapsedTime(&ms, sg.ev[4], sg.ev[5]));
     S.stats.exchange_ms += ms;
   }
@@ -2021,44 +2025,29 @@ kbg_status copy_log(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out, 
   return result;
 }
 
-kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
-  if (S.allocated || S.backfilled || S.preempted)
-    return fail(KBG_E_INVALID, "allocate runs once per cycle, before backfill and preempt; call kbg_session_reset");
-  const bool first = !S.cycle_started;  // else reclaim ran first: start from the live state
-  if (first) begin_cycle(S);
-  S.action = KBG_ACTION_ALLOCATE;
+// The predictor thread of an allocate cycle (the ordering engine) and its
+// hand-off with the committer: predicted batches, recycled buffers, rollbacks.
+struct Predictor {
   using clk = std::chrono::steady_clock;
-  auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
-  const auto t0 = clk::now();
-
-  std::vector<kbg_decision>& dec = S.dec;
-  // the Idle (Allocate) or Releasing (Pipeline) row before each decision
-  // (indexed by decision; earlier actions' decisions are never undone)
-  std::vector<Res> dec_old(dec.size());
-  dec_old.reserve(dec.size() + S.pend.size());
-  std::vector<uint64_t> dec_oldp(dec.size() * (size_t)S.PW);  // host ports: used-port atoms before each decision
-  std::vector<LastEval> last(S.n_jobs);
-  // shapes known to fit nowhere (monotone): written by the committer, read by the predictor
-  std::unique_ptr<std::atomic<uint8_t>[]> failed(new std::atomic<uint8_t>[std::max(1, S.n_shapes)]);
-  for (int32_t i = 0; i < S.n_shapes; ++i) failed[i].store(0, std::memory_order_relaxed);
-  std::vector<int32_t> mark(S.n_nodes, -1), touched;
-  std::vector<char> bactual;
-  kbg_status result = KBG_OK;
-  Grouper grouper(S);
-  Resolver rs{S, mark};
-
-  // ------------------------------------------------------------ predictor
+  Session& S;
+  Engine& E;                      // the engine state the predictor advances
+  std::atomic<uint8_t>* failed;   // shapes known to fit nowhere (monotone), set by the committer
   Pipe P;
-  Engine E = first ? S.init : live_engine(S);
   double engine_ms = 0;
   int64_t replayed = 0;
-  std::string pred_error;
-  EngineProfile eprof;
-  eprof.on = getenv("KBG_PROFILE_ENGINE") != nullptr;
-  const int committer_cpu = sched_getcpu();
-  std::thread predictor([&]() {
+  std::string error;
+  EngineProfile prof;
+  std::thread th;
+  Predictor(Session& s, Engine& e, std::atomic<uint8_t>* f) : S(s), E(e), failed(f) {
+    prof.on = getenv("KBG_PROFILE_ENGINE") != nullptr;
+  }
+  void start(int committer_cpu) {
+    th = std::thread([this, committer_cpu]() { run(committer_cpu); });
+  }
+  void run(int committer_cpu) {
+    auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     pin_near(committer_cpu);
-    Ops ops{S, E, eprof.on ? &eprof : nullptr};
+    Ops ops{S, E, prof.on ? &prof : nullptr};
     bool exhausted = false;
     for (;;) {
       Batch* b = nullptr;
@@ -2073,7 +2062,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
           for (size_t k = 0; k < P.rb_tasks.size(); ++k) {
             const int32_t t = ops.next_task();
             if (t != P.rb_tasks[k]) {
-              pred_error = "internal: replay diverged";
+              error = "internal: replay diverged";
               P.stop = true;
               P.ready.push_back(nullptr);
               P.cv.notify_all();
@@ -2112,11 +2101,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       P.ready.push_back(b);
       P.cv.notify_all();
     }
-  });
-
+  }
   // a predicted batch; nullptr when the predictor failed. Non-blocking: also
   // nullptr (with *none = true) when no batch is ready yet.
-  auto take = [&](bool block, bool* none) -> Batch* {
+  Batch* take(bool block, bool* none) {
     std::unique_lock<std::mutex> lk(P.mu);
     if (!block && P.ready.empty()) {
       *none = true;
@@ -2128,25 +2116,75 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     P.ready.pop_front();
     P.cv.notify_all();
     return b;
-  };
-  auto recycle = [&](Batch* b) {
+  }
+  void recycle(Batch* b) {
     if (!b) return;
     std::lock_guard<std::mutex> lk(P.mu);
     P.free.push_back(b);
-  };
-  auto finish = [&]() {
+  }
+  // a new epoch: the predictor restores `cur`'s checkpoint and replays the
+  // actual outcomes of its first `cut` tasks; `cur` and `nxt` are recycled
+  void rollback(int64_t epoch, Batch* cur, int32_t cut, const std::vector<char>& actual, Batch* nxt) {
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.epoch = epoch;
+    P.rollback = true;
+    P.rb_ckpt = cur->ckpt;
+    P.rb_tasks.assign(cur->bt.begin(), cur->bt.begin() + cut);
+    P.rb_actual.assign(actual.begin(), actual.begin() + cut);
+    P.free.push_back(cur);
+    if (nxt) P.free.push_back(nxt);
+    P.cv.notify_all();
+  }
+  ~Predictor() { finish(); }
+  void finish() {
     {
       std::lock_guard<std::mutex> lk(P.mu);
       P.stop = true;
       P.cv.notify_all();
     }
-    predictor.join();
+    if (th.joinable()) th.join();
     std::lock_guard<std::mutex> lk(P.mu);
     for (Batch* b : P.ready) delete b;
     for (Batch* b : P.free) delete b;
     P.ready.clear();
     P.free.clear();
-  };
+  }
+};
+
+kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
+  if (S.allocated || S.backfilled || S.preempted)
+    return fail(KBG_E_INVALID, "allocate runs once per cycle, before backfill and preempt; call kbg_session_reset");
+  const bool first = !S.cycle_started;  // else reclaim ran first: start from the live state
+  if (first) begin_cycle(S);
+  S.action = KBG_ACTION_ALLOCATE;
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+  const auto t0 = clk::now();
+
+  std::vector<kbg_decision>& dec = S.dec;
+  // the Idle (Allocate) or Releasing (Pipeline) row before each decision
+  // (indexed by decision; earlier actions' decisions are never undone)
+  std::vector<Res> dec_old(dec.size());
+  dec_old.reserve(dec.size() + S.pend.size());
+  std::vector<uint64_t> dec_oldp(dec.size() * (size_t)S.PW);  // host ports: used-port atoms before each decision
+  std::vector<LastEval> last(S.n_jobs);
+  // shapes known to fit nowhere (monotone): written by the committer, read by the predictor
+  std::unique_ptr<std::atomic<uint8_t>[]> failed(new std::atomic<uint8_t>[std::max(1, S.n_shapes)]);
+  for (int32_t i = 0; i < S.n_shapes; ++i) failed[i].store(0, std::memory_order_relaxed);
+  std::vector<int32_t> mark(S.n_nodes, -1), touched;
+  std::vector<char> bactual;
+  kbg_status result = KBG_OK;
+  Grouper grouper(S);
+  Resolver rs{S, mark};
+
+  // ------------------------------------------------------------ predictor
+  Engine E = first ? S.init : live_engine(S);
+  Predictor pr(S, E, failed.get());
+  EngineProfile& eprof = pr.prof;
+  pr.start(sched_getcpu());
+  auto take = [&](bool block, bool* none) { return pr.take(block, none); };
+  auto recycle = [&](Batch* b) { pr.recycle(b); };
+  auto finish = [&]() { pr.finish(); };
 
   // ------------------------------------------------------------ committer
   // Two stages in flight: while the host resolves batch b (stage `si`), the
@@ -2190,7 +2228,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   Batch* cur = next_batch(true);
   if (!cur) {
     finish();
-    return fail(KBG_E_INVALID, pred_error);
+    return fail(KBG_E_INVALID, pr.error);
   }
   if (!cur->bt.empty()) {
     auto tp = clk::now();
@@ -2208,7 +2246,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     if (st != KBG_OK) return abort(st);
     // the next batch's scan overlaps this batch's resolve when it is ready
     Batch* nxt = next_batch(false);
-    if (pred_failed) return abort(fail(KBG_E_INVALID, pred_error));
+    if (pred_failed) return abort(fail(KBG_E_INVALID, pr.error));
     if (nxt && !nxt->bt.empty()) {
       if ((st = launch(other, nxt)) != KBG_OK) return abort(st);
       S.stats.overlapped++;
@@ -2329,19 +2367,9 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
     if (cut >= 0) {  // roll the predictor back to this batch's checkpoint + the actual prefix
       if ((st = device_drop(S, other)) != KBG_OK) return abort(st);  // nxt was predicted before the cut
-      {
-        std::lock_guard<std::mutex> lk(P.mu);
-        P.epoch = ++cur_epoch;
-        P.rollback = true;
-        P.rb_ckpt = cur->ckpt;
-        P.rb_tasks.assign(bt.begin(), bt.begin() + cut);
-        P.rb_actual.assign(bactual.begin(), bactual.begin() + cut);
-        P.free.push_back(cur);
-        if (nxt) P.free.push_back(nxt);
-        P.cv.notify_all();
-      }
+      pr.rollback(++cur_epoch, cur, cut, bactual, nxt);
       cur = next_batch(true);
-      if (!cur) return abort(fail(KBG_E_INVALID, pred_error));
+      if (!cur) return abort(fail(KBG_E_INVALID, pr.error));
       if (!cur->bt.empty()) {
         tp = clk::now();
         if ((st = launch(S.stages[si], cur)) != KBG_OK) return abort(st);
@@ -2352,7 +2380,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     recycle(cur);
     if (!nxt) {  // the predictor was behind: take its next batch now and scan it
       nxt = next_batch(true);
-      if (!nxt) return abort(fail(KBG_E_INVALID, pred_error));
+      if (!nxt) return abort(fail(KBG_E_INVALID, pr.error));
       if (!nxt->bt.empty()) {
         tp = clk::now();
         if ((st = launch(other, nxt)) != KBG_OK) return abort(st);
@@ -2379,8 +2407,8 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
             S.affm->prof_calls ? (double)S.affm->prof_cycles / S.affm->prof_calls : 0.0,
             (unsigned long long)S.affm->prof_recomputes, S.mask_dirty.size());
   S.fin = E;
-  S.stats.engine_ms = engine_ms;
-  S.stats.replayed = replayed;
+  S.stats.engine_ms = pr.engine_ms;
+  S.stats.replayed = pr.replayed;
   if (rprof)
     fprintf(stderr, "[kbg resolve] %lld tasks, cycles/task: walk %.1f mirror %.1f log %.1f loop %.1f (incl. rescans)\n",
             (long long)S.stats.task_evaluations, (double)rcyc[0] / std::max<int64_t>(1, S.stats.task_evaluations),
@@ -2390,7 +2418,486 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   if (eprof.on && eprof.steps)
     fprintf(stderr, "[kbg engine] steps %llu cycles/step: qpop %.1f apply %.1f jfix %.1f qpush %.1f (engine %.3f ms)\n",
             (unsigned long long)eprof.steps, (double)eprof.qpop / eprof.steps, (double)eprof.apply / eprof.steps,
-            (double)eprof.jtop / eprof.steps, (double)eprof.qpush / eprof.steps, engine_ms);
+            (double)eprof.jtop / eprof.steps, (double)eprof.qpush / eprof.steps, pr.engine_ms);
+  S.allocated = true;
+  S.stats.allocate_ms = ms_since(t0);
+  return copy_log(S, out, cap, n_out, result);
+}
+
+// ============================================== sharded allocate: owner-resolve
+// SURVEY §8(e). Rank r holds the node rows [tab_lo, tab_lo + tab_n); first-fit
+// over the whole cluster is the lowest rank that has a fitting node, then that
+// rank's first fitting node. Per batch:
+//   1. rank 0 runs the ordering engine (Predictor) and broadcasts the batch's
+//      task list with the predicted outcomes;
+//   2. every rank scans its own rows on its device and selects its own
+//      candidates (kbg_select_kernel over its words);
+//   3. a sum-reduce of one bit per rank and row says which ranks have any
+//      fitting node for each row (`avail`);
+//   4. rounds: each rank resolves, in batch order, exactly the tasks it owns —
+//      the lowest rank in `avail` that has not failed the row at or before the
+//      task — against its host mirror of its own rows; one min-reduce per round
+//      publishes the packed winners (node << 1 | kind) and each rank's first
+//      failure per row. A failure hands the row's later tasks to the next rank
+//      (a rank never fits a row again once it failed it: Idle, Releasing and
+//      the pod cap only shrink during allocate), which rolls its own commits
+//      back to the first task it gained and resolves again. No new failure:
+//      every owned task has its node;
+//   5. every rank walks the outcomes in order exactly as the single-rank
+//      committer does (decision log, gang dispatch, mirror of the other ranks'
+//      rows, cut at the first misprediction), rolls its own commits past the
+//      cut back and writes its touched rows to HBM.
+// The collectives go through ShardIO: RCCL over xGMI in the library, a host
+// transport in the CPU tests (tools/engine_bench.cpp).
+struct ShardIO {
+  virtual ~ShardIO() = default;
+  virtual kbg_status bcast(uint32_t* buf, size_t n) = 0;                   // rank 0's words to every rank
+  virtual kbg_status scan(Session& S, kbg::Stage& sg, int32_t G, int32_t base) = 0;  // this rank's candidates
+  virtual kbg_status allreduce(uint32_t* buf, size_t n, bool sum) = 0;      // element-wise min (sum), in place
+  // this rank's committed rows (and class-mask words) to the table its scans read
+  virtual kbg_status push(Session& S, const std::vector<int32_t>& touched) { return push_deltas(S, touched); }
+  virtual kbg_status sync(Session& S) {
+    HIP_TRY(hipStreamSynchronize(S.stream));
+    return KBG_OK;
+  }
+  double ms = 0;                                                            // time in collectives
+};
+
+// The library's transport: the session's stream, a device exchange buffer
+// and the communicator.
+struct RcclIO final : ShardIO {
+  Session& S;
+  uint32_t* d = nullptr;  // device exchange buffer
+  uint32_t* h = nullptr;  // pinned staging
+  size_t cap = 0;
+  explicit RcclIO(Session& s) : S(s) {}
+  ~RcclIO() override {
+    if (d) (void)hipFree(d);
+    if (h) (void)hipHostFree(h);
+  }
+  kbg_status reserve(size_t n) {
+    if (n <= cap) return KBG_OK;
+    if (d) (void)hipFree(d);
+    if (h) (void)hipHostFree(h);
+    d = nullptr;
+    h = nullptr;
+    cap = 0;
+    HIP_TRY(hipMalloc((void**)&d, n * 4));
+    HIP_TRY(hipHostMalloc((void**)&h, n * 4, hipHostMallocDefault));
+    cap = n;
+    return KBG_OK;
+  }
+  kbg_status bcast(uint32_t* buf, size_t n) override {
+    const auto t0 = std::chrono::steady_clock::now();
+    kbg_status st = reserve(n);
+    if (st != KBG_OK) return st;
+    if (S.shard == 0) {
+      std::memcpy(h, buf, n * 4);
+      HIP_TRY(hipMemcpyAsync(d, h, n * 4, hipMemcpyHostToDevice, S.stream));
+    }
+    const ncclResult_t nr = ncclBroadcast(d, d, n, ncclUint32, 0, S.comm->nccl, S.stream);
+    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclBroadcast: ") + ncclGetErrorString(nr));
+    HIP_TRY(hipMemcpyAsync(h, d, n * 4, hipMemcpyDeviceToHost, S.stream));
+    HIP_TRY(hipStreamSynchronize(S.stream));
+    std::memcpy(buf, h, n * 4);
+    ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return KBG_OK;
+  }
+  kbg_status scan(Session& S2, kbg::Stage& sg, int32_t G, int32_t base) override {
+    return device_scan(S2, sg, G, base);
+  }
+  kbg_status allreduce(uint32_t* buf, size_t n, bool sum) override {
+    const auto t0 = std::chrono::steady_clock::now();
+    kbg_status st = reserve(n);
+    if (st != KBG_OK) return st;
+    std::memcpy(h, buf, n * 4);
+    HIP_TRY(hipMemcpyAsync(d, h, n * 4, hipMemcpyHostToDevice, S.stream));
+    const ncclResult_t nr = ncclAllReduce(d, d, n, ncclUint32, sum ? ncclSum : ncclMin, S.comm->nccl, S.stream);
+    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+    HIP_TRY(hipMemcpyAsync(h, d, n * 4, hipMemcpyDeviceToHost, S.stream));
+    HIP_TRY(hipStreamSynchronize(S.stream));
+    std::memcpy(buf, h, n * 4);
+    ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return KBG_OK;
+  }
+};
+
+// Sessions whose allocate runs the owner-resolve protocol: sharded over a
+// communicator of at most 32 ranks (one availability bit each), without pod
+// affinity (its counts couple nodes of different ranks through a topology
+// domain; those sessions all-gather the bitmaps and resolve on every rank).
+// KBG_OWNER_RESOLVE=1 also runs it on a one-rank communicator (the RCCL
+// transport and the own-word select on a one-GPU box).
+bool owner_resolve_ok(const Session& S) {
+  static const bool off = getenv("KBG_REPLICATED_RESOLVE") != nullptr;
+  const char* force = getenv("KBG_OWNER_RESOLVE");
+  const bool ranks = S.R > 1 || (force && force[0] == '1');
+  return S.comm && ranks && S.shard >= 0 && S.R <= 32 && !S.has_aff && !off;
+}
+
+// Ranks other than 0 do not predict: they replay the committed outcomes into
+// their own copy of the engine (the plugin state later actions and the state
+// queries read) on a thread of their own, as rank 0's predictor does.
+struct Replayer {
+  Session& S;
+  Engine& E;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::vector<std::pair<int32_t, char>>> q;
+  bool done = false;
+  std::string error;
+  Replayer(Session& s, Engine& e) : S(s), E(e) {
+    th = std::thread([this]() { run(); });
+  }
+  ~Replayer() { join(); }
+  void push(std::vector<std::pair<int32_t, char>>&& v) {
+    std::lock_guard<std::mutex> lk(mu);
+    q.push_back(std::move(v));
+    cv.notify_all();
+  }
+  void join() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      done = true;
+      cv.notify_all();
+    }
+    if (th.joinable()) th.join();
+  }
+  void run() {
+    Ops ops{S, E, nullptr};
+    for (;;) {
+      std::vector<std::pair<int32_t, char>> v;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return done || !q.empty(); });
+        if (q.empty()) return;
+        v = std::move(q.front());
+        q.pop_front();
+      }
+      for (const auto& [t, ok] : v) {
+        if (!error.empty()) break;
+        if (ops.next_task() != t) {
+          error = "internal: engine replay diverged from rank 0";
+          break;
+        }
+        ops.apply(t, ok);
+      }
+    }
+  }
+};
+
+kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t cap, int32_t* n_out) {
+  if (S.allocated || S.backfilled || S.preempted)
+    return fail(KBG_E_INVALID, "allocate runs once per cycle, before backfill and preempt; call kbg_session_reset");
+  const bool first = !S.cycle_started;
+  if (first) begin_cycle(S);
+  S.action = KBG_ACTION_ALLOCATE;
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+  const auto t0 = clk::now();
+  const int32_t R = S.R, me = S.shard;
+  constexpr uint32_t kNone = 0xffffffffu;
+  std::vector<kbg_decision>& dec = S.dec;
+  std::vector<Res> dec_old(dec.size());
+  std::vector<uint64_t> dec_oldp(dec.size() * (size_t)S.PW);
+  std::vector<LastEval> last(S.n_jobs);
+  std::unique_ptr<std::atomic<uint8_t>[]> failed(new std::atomic<uint8_t>[std::max(1, S.n_shapes)]);
+  for (int32_t i = 0; i < S.n_shapes; ++i) failed[i].store(0, std::memory_order_relaxed);
+  std::vector<int32_t> mark(S.n_nodes, -1), touched;
+  Grouper grouper(S);
+  Resolver rs{S, mark};
+  kbg::Stage& sg = S.stages[0];
+  kbg_status result = KBG_OK;
+
+  // rank 0: the ordering engine; the others replay its committed outcomes
+  Engine E = first ? S.init : live_engine(S);
+  std::unique_ptr<Predictor> pr;
+  std::unique_ptr<Replayer> rp;
+  if (me == 0) {
+    pr.reset(new Predictor(S, E, failed.get()));
+    pr->start(sched_getcpu());
+  } else {
+    rp.reset(new Replayer(S, E));
+  }
+  int64_t cur_epoch = 0;
+  auto next_batch = [&]() -> Batch* {  // rank 0: the next batch of the current epoch (nullptr: predictor failed)
+    for (;;) {
+      bool none = false;
+      Batch* b = pr->take(true, &none);
+      if (!b) return nullptr;
+      if (b->epoch != cur_epoch) {
+        pr->recycle(b);
+        continue;
+      }
+      return b;
+    }
+  };
+  // batch message: [kind, n, task ids..., predicted outcomes...]; kind 0 =
+  // batch, 1 = end of the cycle, 2 = the predictor failed
+  std::vector<uint32_t> msg(2 + 2 * (size_t)S.K);
+  std::vector<int32_t> bt;
+  std::vector<char> bpred, bactual;
+  // own commits of the current segment, in batch order (rolled back past a cut)
+  struct Undo {
+    int32_t pos, node, kind;
+    bool dup;
+    Res old;
+  };
+  std::vector<Undo> undo;
+  auto rollback_from = [&](int32_t pos) {
+    while (!undo.empty() && undo.back().pos >= pos) {
+      const Undo& u = undo.back();
+      const int32_t t = bt[u.pos];
+      if (!u.dup) {
+        if (!S.nil_node[u.node]) (u.kind == KBG_KIND_ALLOCATE ? S.idle[u.node] : S.rel[u.node]) = u.old;
+        S.ntasks[u.node]--;
+        if (S.has_ports) remove_ports(S, S.task_class[t], u.node);
+        if (S.has_dupkeys && S.key_hot[S.task_key[t]]) S.node_keys.erase(node_key_of(S, t, u.node));
+      }
+      undo.pop_back();
+    }
+  };
+  std::vector<uint64_t> pos_oldp;  // host ports before each own commit (decision log order needs them)
+  Batch* cur = nullptr;
+  int32_t seg = 0;  // rank 0: first entry of `cur` in the current segment
+  int32_t stamp = S.res_stamp;
+  auto finish = [&]() {
+    if (pr) {
+      if (cur) pr->recycle(cur);
+      cur = nullptr;
+      pr->finish();
+    }
+    if (rp) rp->join();
+  };
+  auto abort = [&](kbg_status st) {
+    finish();
+    S.owner = false;
+    return st;
+  };
+  S.owner = true;  // device_launch: own words, no all-gather
+  for (;;) {
+    // ---- 1. the segment's tasks from rank 0
+    auto tp = clk::now();
+    if (me == 0) {
+      if (!cur) {
+        cur = next_batch();
+        seg = 0;
+      }
+      if (!cur) {
+        msg[0] = 2;
+        msg[1] = 0;
+      } else {
+        const int32_t n = (int32_t)cur->bt.size() - seg;
+        msg[0] = n > 0 ? 0 : 1;
+        msg[1] = (uint32_t)n;
+        for (int32_t i = 0; i < n; ++i) {
+          msg[2 + i] = (uint32_t)cur->bt[seg + i];
+          msg[2 + S.K + i] = (uint32_t)cur->bpred[seg + i];
+        }
+      }
+    }
+    kbg_status st = io.bcast(msg.data(), msg.size());
+    if (st != KBG_OK) return abort(st);
+    if (msg[0] == 2) return abort(fail(KBG_E_INVALID, pr ? pr->error : std::string("the ordering engine failed on rank 0")));
+    if (msg[0] == 1) break;
+    const int32_t n = (int32_t)msg[1];
+    if (n <= 0 || n > S.K) return abort(fail(KBG_E_INVALID, "internal: bad batch message"));
+    bt.assign(n, 0);
+    bpred.assign(n, 0);
+    for (int32_t i = 0; i < n; ++i) {
+      bt[i] = (int32_t)msg[2 + i];
+      bpred[i] = (char)msg[2 + S.K + i];
+      if (bt[i] < 0 || bt[i] >= S.n_tasks) return abort(fail(KBG_E_INVALID, "internal: bad task in batch message"));
+    }
+    S.stats.batches++;
+    // ---- 2. own candidates against the table with every earlier commit
+    const int32_t G = grouper.build(sg, bt.data(), n);
+    if ((st = io.scan(S, sg, G, stamp)) != KBG_OK) return abort(st);
+    // ---- 3. which ranks fit each row at all
+    std::vector<uint32_t> avail(G);
+    for (int32_t g = 0; g < G; ++g) avail[g] = (sg.h_count[g] & kbg::kCountMask) ? (1u << me) : 0u;
+    if ((st = io.allreduce(avail.data(), G, true)) != KBG_OK) return abort(st);
+    S.stats.device_ms += ms_since(tp);
+    // ---- 4. owner rounds
+    tp = clk::now();
+    std::vector<uint32_t> fail_at((size_t)G * R, kNone);  // first failing task of (row, rank), global
+    auto owner_of = [&](int32_t g, int32_t i) -> int32_t {
+      for (uint32_t m = avail[g]; m; m &= m - 1) {
+        const int32_t r = __builtin_ctz(m);
+        if (fail_at[(size_t)g * R + r] > (uint32_t)i) return r;
+      }
+      return -1;
+    };
+    std::vector<uint32_t> xbuf((size_t)n + (size_t)G * R + 2);
+    std::vector<uint32_t> win(n, kNone);
+    std::vector<uint32_t> my_fail(G, kNone);
+    std::vector<Res> pos_old(n);
+    std::vector<char> pos_dup(n, 0);
+    pos_oldp.assign((size_t)n * S.PW, 0);
+    undo.clear();
+    const int32_t stamp0 = ++S.res_stamp;  // commits of this segment
+    S.mstamp = stamp0;
+    touched.clear();
+    int32_t from = 0, end = n;
+    uint32_t my_trunc = kNone, my_panic = kNone;
+    for (;;) {
+      S.stats.owner_rounds++;
+      // resolve the own tasks from `from` on (earlier ones keep their commits)
+      rollback_from(from);
+      for (int32_t i = from; i < n; ++i) win[i] = kNone;
+      for (int32_t g = 0; g < G; ++g)
+        if (my_fail[g] != kNone && my_fail[g] >= (uint32_t)from) my_fail[g] = kNone;
+      if (my_trunc >= (uint32_t)from) my_trunc = kNone;
+      if (my_panic >= (uint32_t)from) my_panic = kNone;
+      rs.reset(sg);  // rolled-back commits may make skipped candidates fit again
+      for (int32_t i = from; i < n; ++i) {
+        const int32_t g = sg.row_of[i];
+        if (my_fail[g] != kNone || owner_of(g, i) != me) continue;
+        const int32_t t = bt[i];
+        int32_t node = -1, kind = 0;
+        const int r = rs.resolve(g, t, &node, &kind);
+        if (r == RES_TRUNC) {  // the list ran out before the rows did: rescan from here
+          my_trunc = (uint32_t)i;
+          break;
+        }
+        if (r == RES_PANIC) {
+          my_panic = (uint32_t)i;
+          break;
+        }
+        if (node < 0) {
+          my_fail[g] = (uint32_t)i;  // the row's later tasks go to the next rank
+          continue;
+        }
+        pos_old[i] = kind == KBG_KIND_ALLOCATE ? S.idle[node] : S.rel[node];
+        if (S.has_ports)
+          std::copy(S.node_ports.begin() + (size_t)node * S.PW, S.node_ports.begin() + (size_t)(node + 1) * S.PW,
+                    pos_oldp.begin() + (size_t)i * S.PW);
+        const bool dup = mirror_add(S, t, node, kind);
+        pos_dup[i] = dup;
+        undo.push_back(Undo{i, node, kind, dup, pos_old[i]});
+        if (mark[node] != stamp0) {
+          mark[node] = stamp0;
+          touched.push_back(node);
+        }
+        win[i] = ((uint32_t)node << 1) | (kind == KBG_KIND_PIPELINE ? 1u : 0u);
+      }
+      // publish: winners, this rank's first failure per row, truncation and panic points
+      std::copy(win.begin(), win.end(), xbuf.begin());
+      std::fill(xbuf.begin() + n, xbuf.end(), kNone);
+      for (int32_t g = 0; g < G; ++g) xbuf[(size_t)n + (size_t)g * R + me] = my_fail[g];
+      xbuf[(size_t)n + (size_t)G * R] = my_trunc;
+      xbuf[(size_t)n + (size_t)G * R + 1] = my_panic;
+      if ((st = io.allreduce(xbuf.data(), xbuf.size(), false)) != KBG_OK) return abort(st);
+      end = (int32_t)std::min<uint32_t>((uint32_t)n, std::min(xbuf[(size_t)n + (size_t)G * R], xbuf[(size_t)n + (size_t)G * R + 1]));
+      // new failures before `end` move ownership; the first task a rank gains is where it resolves again
+      int32_t my_from = n;
+      bool changed = false;
+      for (int32_t g = 0; g < G; ++g)
+        for (int32_t r = 0; r < R; ++r) {
+          const uint32_t f = xbuf[(size_t)n + (size_t)g * R + r];
+          uint32_t& cur_f = fail_at[(size_t)g * R + r];
+          if (f == cur_f || f >= (uint32_t)end) continue;
+          cur_f = std::min(cur_f, f);
+          changed = true;
+        }
+      if (!changed) {
+        for (int32_t i = 0; i < end; ++i) win[i] = xbuf[i];
+        break;
+      }
+      // the earliest task whose owner is now this rank but was not a task it resolved
+      for (int32_t i = 0; i < end && my_from == n; ++i) {
+        const int32_t g = sg.row_of[i];
+        if (owner_of(g, i) == me && xbuf[i] == kNone) my_from = i;
+      }
+      from = my_from;
+    }
+    S.stats.resolve_ms += ms_since(tp);
+    // ---- 5. outcomes in order (every rank), cut at the first misprediction
+    int32_t cut = end;  // entries [0, cut) are final
+    bool mispred = false;
+    bactual.assign(n, 0);
+    for (int32_t i = 0; i < end; ++i) {
+      const int32_t t = bt[i];
+      const int32_t g = sg.row_of[i];
+      const int32_t own = owner_of(g, i);
+      const bool ok = own >= 0;
+      if (ok && win[i] == kNone) return abort(fail(KBG_E_INVALID, "internal: owner-resolve left a task without a node"));
+      const int32_t node = ok ? (int32_t)(win[i] >> 1) : -1;
+      const int32_t kind = ok && (win[i] & 1u) ? KBG_KIND_PIPELINE : KBG_KIND_ALLOCATE;
+      bactual[i] = ok;
+      S.stats.task_evaluations++;
+      last[S.task_job[t]] = LastEval{t, (int32_t)dec.size(), node, kind};
+      if (ok) {
+        bool dup;
+        if (own == me) {  // committed during the resolve
+          dec_old.push_back(pos_old[i]);
+          if (S.has_ports) dec_oldp.insert(dec_oldp.end(), pos_oldp.begin() + (size_t)i * S.PW,
+                                           pos_oldp.begin() + (size_t)(i + 1) * S.PW);
+          dup = pos_dup[i];
+        } else {  // another rank's row: this rank's mirror follows
+          dec_old.push_back(kind == KBG_KIND_ALLOCATE ? S.idle[node] : S.rel[node]);
+          if (S.has_ports)
+            dec_oldp.insert(dec_oldp.end(), S.node_ports.begin() + (size_t)node * S.PW,
+                            S.node_ports.begin() + (size_t)(node + 1) * S.PW);
+          dup = mirror_add(S, t, node, kind);
+        }
+        record_decision(S, t, node, kind, dup);
+      } else {
+        failed[S.task_shape[t]].store(1, std::memory_order_relaxed);
+      }
+      if (ok != (bool)bpred[i]) {
+        cut = i + 1;
+        mispred = true;
+        S.stats.mispredictions++;
+        break;
+      }
+    }
+    rollback_from(cut);
+    if (rp) {
+      std::vector<std::pair<int32_t, char>> v(cut);
+      for (int32_t i = 0; i < cut; ++i) v[i] = {bt[i], bactual[i]};
+      rp->push(std::move(v));
+    }
+    tp = clk::now();
+    if ((st = io.push(S, touched)) != KBG_OK) return abort(st);
+    stamp = S.res_stamp;
+    S.stats.delta_ms += ms_since(tp);
+    const uint32_t panic_at = xbuf[(size_t)n + (size_t)G * R + 1];
+    if (!mispred && panic_at != kNone && (int32_t)panic_at == end) {
+      result = fail(KBG_E_REF_PANIC, "allocate reached a node whose NodeInfo.Node is nil with the predicates plugin on "
+                                     "(predicates.go:122-123)");
+      break;
+    }
+    const bool trunc = !mispred && end < n;
+    if (trunc) S.stats.truncations++;
+    if (me == 0) {
+      if (mispred) {
+        pr->rollback(++cur_epoch, cur, seg + cut, [&] {
+          std::vector<char> a(cur->bpred.begin(), cur->bpred.begin() + seg);  // earlier segments: as predicted
+          a.insert(a.end(), bactual.begin(), bactual.begin() + cut);
+          return a;
+        }(), nullptr);
+        cur = nullptr;
+      } else if (trunc) {
+        seg += end;  // the rest of the batch, rescanned against the commits so far
+      } else {
+        pr->recycle(cur);
+        cur = nullptr;
+      }
+    }
+  }
+  finish();
+  S.owner = false;
+  if (kbg_status st = io.sync(S); st != KBG_OK) return st;
+  compute_fit_deltas(S, dec, dec_old, dec_oldp, last);
+  if (rp && !rp->error.empty()) return fail(KBG_E_INVALID, rp->error);
+  S.fin = E;
+  if (pr) {
+    S.stats.engine_ms = pr->engine_ms;
+    S.stats.replayed = pr->replayed;
+  }
+  S.stats.exchange_ms = io.ms;
   S.allocated = true;
   S.stats.allocate_ms = ms_since(t0);
   return copy_log(S, out, cap, n_out, result);
@@ -3616,6 +4123,10 @@ kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t*
   if (!s) return fail(KBG_E_INVALID, "null session");
   HIP_TRY(hipSetDevice(s->s.device));
   try {
+    if (owner_resolve_ok(s->s)) {
+      RcclIO io(s->s);
+      return allocate_sharded(s->s, io, out, cap, n_out);
+    }
     return allocate_cycle(s->s, out, cap, n_out);
   } catch (const std::bad_alloc&) {
     return fail(KBG_E_NOMEM, "host allocation failed");

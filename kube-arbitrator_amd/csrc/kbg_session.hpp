@@ -345,6 +345,7 @@ struct Session {
   // node-axis sharding: R shards of Wl words; this process holds
   // shard `shard` (comm != null) or every shard (shard = -1)
   int32_t R = 1, Wl = 0, shard = -1;
+  bool owner = false;  // owner-resolve protocol (allocate_sharded): each rank resolves the rows it owns
   int32_t tab_lo = 0, tab_n = 0;  // global node range of the device node table
   kbg_comm* comm = nullptr;
   int32_t n_classes = 0;

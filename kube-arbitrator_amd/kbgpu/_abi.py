@@ -168,7 +168,8 @@ class kbg_stats(ctypes.Structure):
                 ("reclaim_ms", f64), ("preempt_ms", f64), ("victim_scans", i64), ("victim_kernel_ms", f64),
                 ("victim_tries", i64), ("victim_host_evals", i64), ("task_evaluations", i64),
                 ("resolve_steps", i64), ("resolve_rechecks", i64), ("overlapped", i64),
-                ("update_ms", f64), ("update_rebuilds", i64), ("reserved_stats", i64 * 2)]
+                ("update_ms", f64), ("update_rebuilds", i64), ("owner_rounds", i64),
+                ("reserved_stats", i64 * 1)]
 
 
 EV_POD_UPDATE = 1

@@ -3,6 +3,8 @@
 // source to reach the engine, runs open_session (which builds all host state
 // and then stops at the missing device) and drives the predictor with every
 // outcome = placed, i.e. the engine work of a cycle where everything fits.
+#include <barrier>
+
 #include "../csrc/kbg_session.cpp"
 
 extern "C" double kbg_tool_engine_ns_per_step(const kbg_snapshot* snap, const kbg_options* o, int32_t reps,
@@ -75,4 +77,253 @@ extern "C" int32_t kbg_tool_update_nodes(const kbg_snapshot* snap, const kbg_opt
   *n_pend = (int32_t)S.pend_all.size();
   std::copy(S.pend_all.begin(), S.pend_all.end(), pend);
   return outcome;
+}
+
+// ---------------------------------------------------------------------------
+// The owner-resolve protocol of a sharded allocate (allocate_sharded) without a
+// device: each rank's host state is opened from the snapshot, the class masks
+// come from a host evaluation of the static predicate programs (the same
+// programs kbg_mask_kernel runs), the scan of the rank's own rows is a host
+// walk of its mirror, and the collectives are either an in-process transport
+// (R threads, kbg_tool_sharded_allocate_local) or a caller's callback
+// (kbg_tool_sharded_allocate_rank: one rank per process, e.g. torch.distributed
+// gloo in tests/test_shard_protocol.py). Test infrastructure only.
+namespace {
+
+bool host_req(const kbg::StaticHost& sh, const kbg::ReqProg& r, int32_t N, int32_t node) {
+  switch (r.kind) {
+    case kbg::REQ_FALSE: return false;
+    case kbg::REQ_TRUE: return true;
+    case kbg::REQ_ALL:
+    case kbg::REQ_ANY:
+    case kbg::REQ_NONE: {
+      bool any = false, all = true;
+      for (int32_t w = 0; w < sh.label_words; ++w) {
+        const uint64_t m = sh.mask_pool[r.mask_off + w];
+        const uint64_t b = sh.label_bits[(size_t)w * N + node] & m;
+        any |= b != 0;
+        all &= b == m;
+      }
+      return r.kind == kbg::REQ_ALL ? all : (r.kind == kbg::REQ_ANY ? any : !any);
+    }
+    case kbg::REQ_GT:
+    case kbg::REQ_LT: {
+      const size_t k = (size_t)r.col * N + node;
+      if (!sh.num_ok[k]) return false;
+      return r.kind == kbg::REQ_GT ? sh.num_vals[k] > r.value : sh.num_vals[k] < r.value;
+    }
+    case kbg::REQ_NAME_EQ: return (int64_t)sh.name_id[node] == r.value;
+    case kbg::REQ_NAME_NE: return (int64_t)sh.name_id[node] != r.value;
+  }
+  return false;
+}
+
+void host_class_mask(Session& S, const kbg::StaticHost& sh) {
+  const int32_t N = S.n_nodes;
+  S.h_class_mask.assign((size_t)S.n_classes * S.W, 0);
+  for (int32_t c = 0; c < S.n_classes; ++c) {
+    const kbg::ClassProg& cp = sh.classes[c];
+    for (int32_t n = 0; n < N; ++n) {
+      const uint8_t fl = sh.node_flags[n];
+      bool ok;
+      if (cp.always || (fl & kbg::NF_NIL)) ok = true;
+      else if (fl & (kbg::NF_UNSCHED | kbg::NF_DEAD)) ok = false;
+      else {
+        ok = cp.sel_req < 0 || host_req(sh, sh.reqs[cp.sel_req], N, n);
+        if (ok && cp.has_affinity) {
+          bool any_term = false;
+          for (int32_t i = 0; i < cp.term_len && !any_term; ++i) {
+            const kbg::TermProg& tp = sh.terms[cp.term_off + i];
+            bool all = true;
+            for (int32_t j = 0; j < tp.req_len && all; ++j) all = host_req(sh, sh.reqs[tp.req_off + j], N, n);
+            any_term = all;
+          }
+          ok = any_term;
+        }
+        for (int32_t w = 0; ok && w < sh.taint_words; ++w)
+          if (sh.taint_bits[(size_t)w * N + n] & ~sh.tol_pool[cp.tol_off + w]) ok = false;
+      }
+      if (ok) S.h_class_mask[(size_t)c * S.W + (n >> 6)] |= 1ull << (n & 63);
+    }
+  }
+}
+
+// Host state of rank `rank` of R (R = 1: the whole table), as build() leaves it
+// minus the device.
+kbg_status host_open(Session& S, const kbg_snapshot* snap, const kbg_options* o, int32_t R, int32_t rank) {
+  kbg_status st = ingest(S, snap, o);
+  if (st != KBG_OK) return st;
+  kbg::StaticHost sh;
+  int outcome;
+  if ((st = derive_host(S, &sh, &outcome)) != KBG_OK) return st;
+  const int32_t N = S.n_nodes;
+  S.R = R;
+  S.shard = rank;
+  S.Wl = std::max(1, (S.W + R - 1) / R);
+  S.tab_lo = std::min(N, rank * S.Wl * 64);
+  S.tab_n = std::min(N, (rank + 1) * S.Wl * 64) - S.tab_lo;
+  S.n_shapes_cap = std::max(S.n_shapes, 64);
+  S.cand_cap = S.opts.full_scan ? (int64_t)S.K * S.M + (int64_t)std::min(S.K, S.n_shapes_cap) * (kFullScanGrow + S.M)
+                                : (int64_t)S.K * (kGroupSlack + 1);
+  const size_t up_cap = (size_t)kbg::kbg_pad_rows(S.K) * sizeof(kbg::TaskRec) + ((size_t)S.K + 1) * 4;
+  const size_t down_cap = (size_t)S.K + (size_t)S.cand_cap;
+  for (kbg::Stage& g : S.stages) {
+    g.h_up = (char*)std::malloc(up_cap);
+    g.h_down = (uint32_t*)std::malloc(down_cap * 4);
+  }
+  host_class_mask(S, sh);
+  S.h_class_mask_static = S.h_class_mask;
+  setup_host_ports(S);
+  setup_affinity(S);
+  S.h_class_mask0 = S.h_class_mask;
+  return KBG_OK;
+}
+
+void host_close(Session& S) {
+  for (kbg::Stage& g : S.stages) {
+    std::free(g.h_up);
+    std::free(g.h_down);
+    g.h_up = nullptr;
+    g.h_down = nullptr;
+  }
+}
+
+// first-fit candidates of each row over this rank's rows, from the mirror:
+// what kbg_scan_kernel + kbg_select_kernel produce on the device
+struct HostIO : ShardIO {
+  kbg_status scan(Session& S, kbg::Stage& sg, int32_t G, int32_t base) override {
+    sg.G = G;
+    sg.base = base;
+    sg.h_count = sg.h_down;
+    sg.h_cand = sg.h_down + G;
+    for (int32_t g = 0; g < G; ++g) {
+      const kbg::TaskRec& r = sg.h_tasks[g];
+      const uint32_t capn = sg.h_capoff[g + 1] - sg.h_capoff[g];
+      uint32_t* c = sg.h_cand + sg.h_capoff[g];
+      uint32_t found = 0;
+      auto fits = [&](const Res& a) {
+        if (S.int_mode) return a.c > r.req[0] && a.m > r.req[1] && a.g > r.req[2];
+        return (r.req[0] < a.c || std::fabs(a.c - r.req[0]) < kbg::kMinMilliCPU) &&
+               (r.req[1] < a.m || std::fabs(a.m - r.req[1]) < kbg::kMinMemory) &&
+               (r.req[2] < a.g || std::fabs(a.g - r.req[2]) < kbg::kMinMilliGPU);
+      };
+      for (int32_t n = S.tab_lo; n < S.tab_lo + S.tab_n; ++n) {
+        if (!((S.h_class_mask[(size_t)r.cls * S.W + (n >> 6)] >> (n & 63)) & 1ull)) continue;
+        if (S.pred_active && S.ntasks[n] >= S.maxtasks[n]) continue;
+        const bool mi = fits(S.idle[n]);
+        if (!mi && !fits(S.rel[n])) continue;
+        if (found < capn) c[found] = (uint32_t)n | (mi ? 0u : kbg::kCandPipelineBit);
+        ++found;
+      }
+      sg.h_count[g] = std::min(found, capn) | (found > capn ? kbg::kCountIncompleteBit : 0u);
+    }
+    S.stats.scan_launches++;
+    S.stats.evaluations += G;
+    return KBG_OK;
+  }
+  kbg_status push(Session& S, const std::vector<int32_t>&) override {
+    S.mask_dirty.clear();  // the host scan reads the mirror itself
+    return KBG_OK;
+  }
+  kbg_status sync(Session&) override { return KBG_OK; }
+};
+
+// R ranks in one process: a barrier and one slot per rank
+struct LocalHub {
+  int32_t R;
+  std::barrier<> bar;
+  std::vector<std::vector<uint32_t>> slot;
+  explicit LocalHub(int32_t r) : R(r), bar(r), slot(r) {}
+};
+struct LocalIO final : HostIO {
+  LocalHub& hub;
+  int32_t me;
+  LocalIO(LocalHub& h, int32_t r) : hub(h), me(r) {}
+  kbg_status bcast(uint32_t* buf, size_t n) override {
+    if (me == 0) hub.slot[0].assign(buf, buf + n);
+    hub.bar.arrive_and_wait();
+    if (me != 0) std::copy(hub.slot[0].begin(), hub.slot[0].begin() + n, buf);
+    hub.bar.arrive_and_wait();
+    return KBG_OK;
+  }
+  kbg_status allreduce(uint32_t* buf, size_t n, bool sum) override {
+    hub.slot[me].assign(buf, buf + n);
+    hub.bar.arrive_and_wait();
+    for (size_t i = 0; i < n; ++i) {
+      uint32_t v = sum ? 0u : 0xffffffffu;
+      for (int32_t r = 0; r < hub.R; ++r) v = sum ? v + hub.slot[r][i] : std::min(v, hub.slot[r][i]);
+      buf[i] = v;
+    }
+    hub.bar.arrive_and_wait();
+    return KBG_OK;
+  }
+};
+
+typedef int32_t (*kbg_tool_coll)(void* user, int32_t op, uint32_t* buf, int64_t n);  // op 0 bcast, 1 min, 2 sum
+struct CallbackIO final : HostIO {
+  kbg_tool_coll fn;
+  void* user;
+  CallbackIO(kbg_tool_coll f, void* u) : fn(f), user(u) {}
+  kbg_status bcast(uint32_t* buf, size_t n) override {
+    return fn(user, 0, buf, (int64_t)n) == 0 ? KBG_OK : fail(KBG_E_RCCL, "bcast callback failed");
+  }
+  kbg_status allreduce(uint32_t* buf, size_t n, bool sum) override {
+    return fn(user, sum ? 2 : 1, buf, (int64_t)n) == 0 ? KBG_OK : fail(KBG_E_RCCL, "allreduce callback failed");
+  }
+};
+
+// stats of one rank's cycle for the caller: rounds, batches, mispredictions, truncations
+void tool_stats(const Session& S, int64_t* st) {
+  if (!st) return;
+  st[0] = S.stats.owner_rounds;
+  st[1] = S.stats.batches;
+  st[2] = S.stats.mispredictions;
+  st[3] = S.stats.truncations;
+  st[4] = S.stats.task_evaluations;
+}
+
+}  // namespace
+
+// R ranks as threads; rank r's decision log at out + r * cap. Returns 0, or
+// the first failing rank's status (negated) with its message in kbg_last_error.
+extern "C" int32_t kbg_tool_sharded_allocate_local(const kbg_snapshot* snap, const kbg_options* o, int32_t R,
+                                                   kbg_decision* out, int32_t cap, int32_t* n_out, int64_t* stats) {
+  LocalHub hub(R);
+  std::vector<kbg_status> res(R, KBG_OK);
+  std::vector<std::string> err(R);
+  std::vector<std::thread> th;
+  for (int32_t r = 0; r < R; ++r)
+    th.emplace_back([&, r]() {
+      Session S;
+      kbg_status st = host_open(S, snap, o, R, r);
+      if (st == KBG_OK) {  // (an open failure is the same on every rank: no collective is left waiting)
+        LocalIO io(hub, r);
+        st = allocate_sharded(S, io, out + (size_t)r * cap, cap, n_out + r);
+      }
+      tool_stats(S, stats ? stats + 5 * r : nullptr);
+      res[r] = st;
+      err[r] = g_err;
+      host_close(S);
+    });
+  for (auto& t : th) t.join();
+  for (int32_t r = 0; r < R; ++r)
+    if (res[r] != KBG_OK) {
+      g_err = err[r];
+      return -(int32_t)res[r];
+    }
+  return 0;
+}
+
+extern "C" int32_t kbg_tool_sharded_allocate_rank(const kbg_snapshot* snap, const kbg_options* o, int32_t R,
+                                                  int32_t rank, kbg_tool_coll fn, void* user, kbg_decision* out,
+                                                  int32_t cap, int32_t* n_out, int64_t* stats) {
+  Session S;
+  kbg_status st = host_open(S, snap, o, R, rank);
+  if (st == KBG_OK) {
+    CallbackIO io(fn, user);
+    st = allocate_sharded(S, io, out, cap, n_out);
+  }
+  tool_stats(S, stats);
+  host_close(S);
+  return -(int32_t)st;
 }

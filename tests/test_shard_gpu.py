@@ -130,3 +130,42 @@ def test_rccl_one_rank_affinity(seed, comm1):
     compare_outputs(run_oracle(fx), got)
     if ssn:
         ssn.close()
+
+
+@pytest.fixture
+def owner_resolve(monkeypatch):
+    """Allocate through the owner-resolve protocol (allocate_sharded) on the
+    one-rank communicator: ncclBroadcast of the batch, the own-word select,
+    the availability sum-reduce and the winner min-reduce rounds over RCCL."""
+    monkeypatch.setenv("KBG_OWNER_RESOLVE", "1")
+
+
+@pytest.mark.parametrize("cid", [1, 2])
+def test_rccl_owner_resolve_parity(cid, comm1, owner_resolve):
+    fx = synth.config_fixture(cid)
+    got, ssn = run_fixture(fx, {"comm": comm1})
+    st = ssn.stats()
+    assert st.owner_rounds >= st.batches > 0 and st.exchange_ms > 0.0
+    compare_outputs(run_oracle(fx), got)
+    ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 60, 3))
+def test_rccl_owner_resolve_fuzz(seed, comm1, owner_resolve):
+    fx = synth.random_fixture(seed)
+    opts = {"comm": comm1, "batch_tasks": 1 + seed % 9, "candidates": 1 + seed % 5, "full_scan": seed % 2}
+    got, ssn = run_fixture(fx, opts)
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 40, 4))
+def test_rccl_owner_resolve_contended(seed, comm1, owner_resolve):
+    """Allocate by owner-resolve inside a reclaim, allocate, backfill, preempt
+    cycle (the victim actions keep the all-reduced stop maps)."""
+    fx = synth.contended_fixture(seed)
+    got, ssn = run_fixture(fx, {"comm": comm1})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
