@@ -373,26 +373,7 @@ void build_heaps(const Session& S, Engine& E) {
     std::sort(E.jheap.begin() + S.joff[q], E.jheap.begin() + S.joff[q] + E.jlen[q]);
 }
 
-struct ShapeKey {
-  int32_t cls;
-  double c, m, g;
-  bool operator==(const ShapeKey& o) const {
-    return cls == o.cls && std::memcmp(&c, &o.c, 8) == 0 && std::memcmp(&m, &o.m, 8) == 0 && std::memcmp(&g, &o.g, 8) == 0;
-  }
-};
-struct ShapeHash {
-  size_t operator()(const ShapeKey& k) const {
-    uint64_t h = (uint64_t)k.cls * 0x9E3779B97F4A7C15ull;
-    uint64_t v;
-    std::memcpy(&v, &k.c, 8);
-    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
-    std::memcpy(&v, &k.m, 8);
-    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
-    std::memcpy(&v, &k.g, 8);
-    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
-    return (size_t)h;
-  }
-};
+
 
 // ---------------------------------------------------------------- device
 template <class T>
@@ -1356,21 +1337,50 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   };
   // bytewise UID order: TaskOrderFn's fallback compares tasks of one job only
   // (session_plugins.go:266-276), so a job that gained tasks is re-ranked alone
+  // a full derive (open, or a rebuild after an update) recomputes everything;
+  // an update's derive keeps what its events cannot have changed
+  const bool full = sh != nullptr;
   if (S.task_rank.empty() && T > 0) {
     std::vector<int32_t> ids(T);
     for (int32_t t = 0; t < T; ++t) ids[t] = S.tasks_in[t].uid;
     S.task_rank = ranks_of(S, ids);
   } else if (S.task_ranks_stale) {
+    // a job that gained tasks: its ranked tasks keep their order, the new ones
+    // are merged in by UID (dense ranks, equal UIDs share one)
+    const int32_t T_old = (int32_t)S.task_rank.size();
     S.task_rank.resize(T, 0);
+    std::sort(S.rank_dirty_jobs.begin(), S.rank_dirty_jobs.end());
+    S.rank_dirty_jobs.erase(std::unique(S.rank_dirty_jobs.begin(), S.rank_dirty_jobs.end()), S.rank_dirty_jobs.end());
+    std::vector<int32_t> olds, news, merged, rank;
     for (int32_t j : S.rank_dirty_jobs) {
-      std::vector<int32_t> ids;
-      for (int32_t t : S.job_task_order[j]) ids.push_back(S.tasks_in[t].uid);
-      const std::vector<int32_t> r = ranks_of(S, ids);
-      for (size_t i = 0; i < r.size(); ++i) S.task_rank[S.job_task_order[j][i]] = r[i];
+      olds.clear();
+      news.clear();
+      for (int32_t t : S.job_task_order[j]) (t < T_old ? olds : news).push_back(t);
+      const auto uid = [&](int32_t t) -> const std::string& { return S.strs[S.tasks_in[t].uid]; };
+      std::sort(olds.begin(), olds.end(), [&](int32_t a, int32_t b) { return S.task_rank[a] < S.task_rank[b]; });
+      std::stable_sort(news.begin(), news.end(), [&](int32_t a, int32_t b) { return uid(a) < uid(b); });
+      merged.clear();
+      size_t a = 0;
+      for (int32_t nt : news) {  // each new UID goes after the ranked tasks that do not sort above it
+        const size_t at = std::upper_bound(olds.begin() + a, olds.end(), nt,
+                                           [&](int32_t x, int32_t y) { return uid(x) < uid(y); }) - olds.begin();
+        merged.insert(merged.end(), olds.begin() + a, olds.begin() + at);
+        merged.push_back(nt);
+        a = at;
+      }
+      merged.insert(merged.end(), olds.begin() + a, olds.end());
+      rank.assign(merged.size(), 0);
+      for (size_t k = 1; k < merged.size(); ++k) {
+        const int32_t p = merged[k - 1], q = merged[k];
+        const bool same = (p < T_old && q < T_old) ? S.task_rank[p] == S.task_rank[q] : uid(p) == uid(q);
+        rank[k] = rank[k - 1] + (same ? 0 : 1);
+      }
+      for (size_t k = 0; k < merged.size(); ++k) S.task_rank[merged[k]] = rank[k];
     }
   }
   S.task_ranks_stale = false;
   S.rank_dirty_jobs.clear();
+  phase("ranks");
   if (S.treq.capacity() < (size_t)T) S.treq.reserve((size_t)T + T / 4 + 1024);
   S.task_node.reserve(S.treq.capacity());
   S.treq.resize(T);
@@ -1386,7 +1396,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     S.be_task[t] = S.tasks_in[t].status == KBG_PENDING && kbg::res_empty(S.treq[t]);
   }
 
-  phase("ranks+tasks");
+  phase("tasks");
   // ---- nodes
   S.idle.resize(N);
   S.rel.resize(N);
@@ -1408,10 +1418,12 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   S.ntasks0 = S.ntasks;
   // victim candidates (preempt/reclaim): session tasks Running on each node,
   // in NodeInfo.Tasks order; a task's node by NodeName (ssn.NodeIndex)
-  S.task_node.assign(T, -1);
-  for (int32_t t = 0; t < T; ++t) {
-    auto it = S.node_of.find(S.canon[S.tasks_in[t].node_name]);
-    if (it != S.node_of.end()) S.task_node[t] = it->second;
+  if (full || (int32_t)S.task_node.size() != T) {  // an update's events keep task_node current (apply_event)
+    S.task_node.assign(T, -1);
+    for (int32_t t = 0; t < T; ++t) {
+      auto it = S.node_of.find(S.canon[S.tasks_in[t].node_name]);
+      if (it != S.node_of.end()) S.task_node[t] = it->second;
+    }
   }
   S.nt_off.assign(N + 1, 0);
   S.nt_task.clear();
@@ -1528,19 +1540,67 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
 
   phase("preconditions");
   // ---- pending task lists in TaskOrderFn order (session_plugins.go:266-276)
+  // an update's derive copies the lists of the jobs no event touched
+  const bool keep_lists = !full && (int32_t)S.pend_off_all.size() == S.n_jobs;
+  std::vector<char> jdirty, listed;
+  std::vector<int32_t> fresh_off, fresh;  // per dirty job: its tasks that entered Pending through an event
+  auto task_before = [&](int32_t a, int32_t c) {
+    if (S.task_order_prio && S.tasks_in[a].priority != S.tasks_in[c].priority)
+      return S.tasks_in[a].priority > S.tasks_in[c].priority;
+    return S.task_rank[a] < S.task_rank[c];
+  };
+  if (keep_lists) {
+    listed.assign(T, 0);
+    jdirty.assign(S.n_jobs, 0);
+    for (int32_t j : S.pend_dirty_jobs) jdirty[j] = 1;
+    std::sort(S.pend_new.begin(), S.pend_new.end());
+    S.pend_new.erase(std::unique(S.pend_new.begin(), S.pend_new.end()), S.pend_new.end());
+    fresh_off.assign(S.n_jobs + 1, 0);
+    for (int32_t t : S.pend_new)
+      if (t < T && S.pending_candidate[t]) fresh_off[S.task_job[t] + 1]++;
+    for (int32_t j = 0; j < S.n_jobs; ++j) fresh_off[j + 1] += fresh_off[j];
+    fresh.assign(fresh_off[S.n_jobs], 0);
+    std::vector<int32_t> at(fresh_off.begin(), fresh_off.end() - 1);
+    for (int32_t t : S.pend_new)
+      if (t < T && S.pending_candidate[t]) fresh[at[S.task_job[t]]++] = t;
+  }
+  S.pend_dirty_jobs.clear();
+  S.pend_new.clear();
   S.pend_off.assign(S.n_jobs, 0);
   S.pend_len.assign(S.n_jobs, 0);
   S.pend.clear();
+  S.pend.reserve(keep_lists ? S.pend_all.size() + 1024 : 0);
   for (int32_t j = 0; j < S.n_jobs; ++j) {
     S.pend_off[j] = (int32_t)S.pend.size();
+    if (keep_lists) {
+      const auto b0 = S.pend_all.begin() + S.pend_off_all[j];
+      if (!jdirty[j]) {
+        S.pend.insert(S.pend.end(), b0, b0 + S.pend_len_all[j]);
+        S.pend_len[j] = S.pend_len_all[j];
+        continue;
+      }
+      // the old list minus the tasks that left Pending (order kept), merged
+      // with the tasks that entered it
+      for (auto b = b0; b != b0 + S.pend_len_all[j]; ++b)
+        if (*b < T && S.pending_candidate[*b]) {
+          S.pend.push_back(*b);
+          listed[*b] = 1;
+        }
+      auto f0 = fresh.begin() + fresh_off[j], f1 = fresh.begin() + fresh_off[j + 1];
+      f1 = std::remove_if(f0, f1, [&](int32_t t) { return listed[t] != 0; });  // already Pending before the event
+      for (auto b = S.pend.begin() + S.pend_off[j]; b != S.pend.end(); ++b) listed[*b] = 0;
+      if (f0 != f1) {
+        std::sort(f0, f1, task_before);
+        const size_t mid = S.pend.size();
+        S.pend.insert(S.pend.end(), f0, f1);
+        std::inplace_merge(S.pend.begin() + S.pend_off[j], S.pend.begin() + mid, S.pend.end(), task_before);
+      }
+      S.pend_len[j] = (int32_t)S.pend.size() - S.pend_off[j];
+      continue;
+    }
     for (auto [b, e] = job_tasks(j); b != e; ++b)
       if (S.pending_candidate[*b]) S.pend.push_back(*b);
-    auto b = S.pend.begin() + S.pend_off[j];
-    std::sort(b, S.pend.end(), [&](int32_t a, int32_t c) {
-      if (S.task_order_prio && S.tasks_in[a].priority != S.tasks_in[c].priority)
-        return S.tasks_in[a].priority > S.tasks_in[c].priority;
-      return S.task_rank[a] < S.task_rank[c];
-    });
+    std::sort(S.pend.begin() + S.pend_off[j], S.pend.end(), task_before);
     S.pend_len[j] = (int32_t)S.pend.size() - S.pend_off[j];
   }
 
@@ -1584,7 +1644,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   // compares is an exact integer and stays one through the cycle
   {
     constexpr double kLim = 2251799813685248.0;  // 2^51
-    auto exact = [&](double v) { return std::isfinite(v) && std::fabs(v) <= kLim && v == std::floor(v); };
+    auto exact = [&](double v) { return std::fabs(v) <= kLim && v == (double)(int64_t)v; };  // (NaN fails the bound)
     bool ok = true;
     for (int32_t n = 0; n < N && ok; ++n)
       ok = exact(S.idle[n].c) && exact(S.idle[n].m) && exact(S.idle[n].g) && exact(S.rel[n].c) &&
@@ -1603,17 +1663,30 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   }
   phase("int mode");
   // ---- (class, request) shapes of the candidates
+  // Shape ids persist across updates (a task's class and request never
+  // change): an update looks up only the tasks that are new candidates.
   {
-    std::unordered_map<ShapeKey, int32_t, ShapeHash> ids;
+    if (full) {
+      S.shape_ids.clear();
+      S.shape_of_task.assign(T, -1);
+      S.be_shape.assign(std::max(1, S.n_classes), -1);
+      S.n_shapes = 0;
+    } else {
+      S.shape_of_task.resize(T, -1);
+      if ((int32_t)S.be_shape.size() < std::max(1, S.n_classes)) S.be_shape.resize(std::max(1, S.n_classes), -1);
+    }
     S.task_shape.assign(T, -1);
     for (int32_t t = 0; t < T; ++t) {
       if (!S.pending_candidate[t]) continue;
-      auto it = ids.emplace(ShapeKey{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g}, (int32_t)ids.size());
-      S.task_shape[t] = it.first->second;
+      int32_t& sh_t = S.shape_of_task[t];
+      if (sh_t < 0) {
+        auto it = S.shape_ids.emplace(kbg::ShapeKey{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g}, S.n_shapes);
+        if (it.second) S.n_shapes++;
+        sh_t = it.first->second;
+      }
+      S.task_shape[t] = sh_t;
     }
-    S.n_shapes = (int32_t)ids.size();
     // backfill rows: one grouping id per class (the request does not matter)
-    S.be_shape.assign(std::max(1, S.n_classes), -1);
     for (int32_t t = 0; t < T; ++t) {
       if (!S.be_task[t]) continue;
       int32_t& b = S.be_shape[S.task_class[t]];
@@ -3919,6 +3992,7 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
       if (t < 0 || t >= S.n_tasks || !S.task_live[t]) return fail(KBG_E_INVALID, "event task index");
       if (e.kind == KBG_EV_POD_UPDATE && (!status_ok(e.status) || e.node < -1 || e.node >= S.n_nodes))
         return fail(KBG_E_INVALID, "event status / node");
+      S.pend_dirty_jobs.push_back(S.tasks_in[t].job);
       const int r = in_delete_task(S, U, t);
       if (r > 1) return (kbg_status)r;
       if (e.kind == KBG_EV_POD_DELETE || r == 1) {  // deleted, or updateTask returned deleteTask's error
@@ -3928,6 +4002,7 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
       S.tasks_in[t].status = e.status;
       S.tasks_in[t].node_name = e.node >= 0 ? S.nodes_in[e.node].name : intern(S, "");
       S.task_node[t] = e.node;
+      if (e.status == KBG_PENDING) S.pend_new.push_back(t);
       return in_add_task(S, U, t);
     }
     case KBG_EV_POD_ADD: {
@@ -3950,6 +4025,8 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
       S.task_node.push_back(e.node);
       S.task_ranks_stale = true;
       S.rank_dirty_jobs.push_back(e.job);
+      S.pend_dirty_jobs.push_back(e.job);
+      S.pend_new.push_back(t);
       return in_add_task(S, U, t);
     }
     case KBG_EV_NODE_UPDATE: {

@@ -2,6 +2,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <cstring>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -38,6 +39,28 @@ inline bool res_sub(Res& r, const Res& b) {
 }
 // resource_info.go:75-77
 inline bool res_empty(const Res& r) { return r.c < kMinMilliCPU && r.m < kMinMemory && r.g < kMinMilliGPU; }
+
+// (class, request) shape of a pending task: identical rows of a scan
+struct ShapeKey {
+  int32_t cls;
+  double c, m, g;
+  bool operator==(const ShapeKey& o) const {
+    return cls == o.cls && std::memcmp(&c, &o.c, 8) == 0 && std::memcmp(&m, &o.m, 8) == 0 && std::memcmp(&g, &o.g, 8) == 0;
+  }
+};
+struct ShapeHash {
+  size_t operator()(const ShapeKey& k) const {
+    uint64_t h = (uint64_t)k.cls * 0x9E3779B97F4A7C15ull;
+    uint64_t v;
+    std::memcpy(&v, &k.c, 8);
+    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    std::memcpy(&v, &k.m, 8);
+    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    std::memcpy(&v, &k.g, 8);
+    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    return (size_t)h;
+  }
+};
 
 struct StaticHost {
   int32_t n_classes = 0;
@@ -213,6 +236,10 @@ struct Session {
   std::vector<int32_t> task_class;
   std::vector<int32_t> class_spec;                       // spec of each static class (-1: none)
   std::vector<int32_t> task_shape;                       // (class, request) shape id of a pending task
+  std::unordered_map<ShapeKey, int32_t, ShapeHash> shape_ids;  // shape ids, kept across updates
+  std::vector<int32_t> shape_of_task;                    // a task's shape once it was a candidate (-1: not yet)
+  std::vector<int32_t> pend_dirty_jobs;                  // jobs an update's events touched (their pending lists)
+  std::vector<int32_t> pend_new;                         // tasks an update's events made (or re-made) Pending
   int32_t n_shapes = 0;
   std::vector<Res> treq;
   Res drf_total, prop_total;

@@ -111,6 +111,16 @@ def check(tools, fx0, seed, rounds):
         fresh_pend = set(t.uid for job in s1.jobs for t in job.tasks.values()
                          if t.status == PENDING and not t.resreq.is_empty())
         assert {inv[pend[i]] for i in range(npend.value)} == fresh_pend
+        # the order too (jobs in session order, each job's tasks in TaskOrderFn
+        # order): a fresh open of S1 derives the same sequence
+        T1 = len(f1.task_objs)
+        idle1, rel1 = (ctypes.c_double * (3 * N))(), (ctypes.c_double * (3 * N))()
+        nt1, pend1, npend1 = (ctypes.c_int32 * max(1, N))(), (ctypes.c_int32 * max(1, T1))(), ctypes.c_int32()
+        rc1 = tools.kbg_tool_update_nodes(ctypes.byref(f1.snap), ctypes.byref(_abi.kbg_options()), None, 0,
+                                          idle1, rel1, nt1, pend1, ctypes.byref(npend1))
+        assert rc1 == 0
+        assert [inv[pend[i]] for i in range(npend.value)] == \
+            [f1.task_objs[pend1[i]].uid for i in range(npend1.value)]
 
 
 @pytest.mark.parametrize("seed", range(40))
