@@ -98,6 +98,21 @@ def omp_threads():
     return max(1, min(16, len(job_cpus())))
 
 
+_FX_FILES = {}
+
+
+def fixture_file(fx):
+    """The fixture as JSON on disk, written once per process for every baseline run."""
+    key = id(fx)
+    if key not in _FX_FILES:
+        d = tempfile.mkdtemp(prefix="kbg_bench_")
+        path = os.path.join(d, "fx.json")
+        with open(path, "w") as f:
+            json.dump(fx, f)
+        _FX_FILES[key] = path
+    return _FX_FILES[key]
+
+
 def cpu_baseline(fx, label, threads=1, faithful=False, budget=0.0):
     """kbref oracle on the same workload (kind "port"), SURVEY §8(d):
     B-ref     1 thread (the Go allocate loop is single-goroutine), podLister
@@ -110,13 +125,14 @@ def cpu_baseline(fx, label, threads=1, faithful=False, budget=0.0):
     the rate is over the placements reached within it. None on failure (the
     bench line is never lost to a baseline)."""
     ref = os.path.join(ROOT, "oracle", "build", "kbref")
+    log(f"cpu baseline {label}: {threads} thread(s){', faithful' if faithful else ''}"
+        f"{f', {budget:.0f} s budget' if budget else ''}")
     try:
         if not os.path.exists(ref):
             subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+        src = fixture_file(fx)
         with tempfile.TemporaryDirectory() as d:
-            src, dst = os.path.join(d, "fx.json"), os.path.join(d, "out.json")
-            with open(src, "w") as f:
-                json.dump(fx, f)
+            dst = os.path.join(d, "out.json")
             cpus = ",".join(str(c) for c in job_cpus()[:threads])
             cmd = ["taskset", "-c", cpus, ref, "--threads", str(threads)]
             if faithful:
