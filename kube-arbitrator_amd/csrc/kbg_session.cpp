@@ -3288,7 +3288,7 @@ kbg_status vt_setup(Session& S) {
 // affect unknown; a queue allocation change under a proportion fn affects
 // every node and drops the maps.
 void vc_dirty_node(Session& S, int32_t n) {
-  if (S.vc.valid && n >= 0) S.vc.unk[n >> 5] |= 1u << (n & 31);
+  if (S.vc.valid && n >= 0) S.vc.dirty(n);
 }
 void vc_dirty_job(Session& S, int32_t j) {
   if (!S.vc.valid) return;
@@ -3417,7 +3417,9 @@ struct Live {
 // deciding tier (session_plugins.go:59-140). false = a fn would panic.
 bool host_victims(Session& S, int32_t mode, int32_t t, int32_t n, std::vector<int32_t>* victims) {
   const int32_t pj = S.task_job[t], pq = S.job_queue[pj];
-  std::vector<int32_t> pre;
+  thread_local std::vector<int32_t> pre;
+  thread_local std::vector<char> keep;
+  pre.clear();
   for (int32_t k = S.nt_off[n]; k < S.nt_off[n + 1]; ++k) {
     const int32_t v = S.nt_task[k];
     if (!S.trun[v]) continue;
@@ -3432,7 +3434,7 @@ bool host_victims(Session& S, int32_t mode, int32_t t, int32_t n, std::vector<in
   if (pre.empty()) return true;
   const std::vector<int32_t>& tiers = mode == kbg::VM_RECLAIM ? S.tier_reclaim : S.tier_preempt;
   for (int32_t fns : tiers) {
-    std::vector<char> keep(pre.size(), 1);
+    keep.assign(pre.size(), 1);
     if (fns & kbg::VP_GANG)  // gang.go:104-124
       for (size_t i = 0; i < pre.size(); ++i) {
         const int32_t jv = S.task_job[pre[i]];
@@ -3573,6 +3575,7 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
       vc.panic[w] = hb[S.W32 + w];
     }
     std::fill(vc.unk.begin(), vc.unk.end(), 0u);
+    vc.lb = 0;
     vc.key = key;
     vc.fns = dfns;
     vc.valid = true;
@@ -3581,7 +3584,11 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
   // re-evaluated on the host (host_stop) when the search reaches it
   int32_t n = -1;
   bool pan = false;
-  for (int32_t w = 0; w < S.W32 && n < 0; ++w) {
+  for (int32_t w = vc.lb; w < S.W32 && n < 0; ++w) {
+    if (w == vc.lb && !(vc.stop[w] | vc.unk[w])) {  // nothing left below the next word
+      vc.lb = w + 1;
+      continue;
+    }
     for (uint32_t cand = vc.stop[w] | vc.unk[w]; cand; cand &= cand - 1) {
       const int b = __builtin_ctz(cand);
       const uint32_t bit = 1u << b;

@@ -292,6 +292,11 @@ struct Session {
     VictimKey key;                            // the preemptor shape the maps are for
     int32_t fns = 0;                          // victim fns of the deciding tier
     std::vector<uint32_t> stop, panic, unk;   // [W32]
+    int32_t lb = 0;                           // every word below lb has no stop and no unknown bit
+    void dirty(int32_t n) {
+      unk[n >> 5] |= 1u << (n & 31);
+      if ((n >> 5) < lb) lb = n >> 5;
+    }
   } vc;
   std::vector<int32_t> jn_off, jn_node;       // per job: the nodes holding its tasks Running at open
   kbg::StateDelta* h_sdeltas = nullptr;       // pinned, device-mapped (the prep kernel reads it in place)
@@ -398,7 +403,7 @@ struct Session {
 // A class-mask bit of (c, n) changed: the host-kept victim stop maps of that
 // class no longer know node n (Session::VictimCache).
 inline void vc_mask_changed(Session& S, int32_t c, int32_t n) {
-  if (S.vc.valid && S.vc.key.cls == c) S.vc.unk[n >> 5] |= 1u << (n & 31);
+  if (S.vc.valid && S.vc.key.cls == c) S.vc.dirty(n);
 }
 
 bool parse_go_int64(const std::string& s, int64_t* out);
