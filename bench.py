@@ -169,6 +169,9 @@ def load_pmc(n_nodes, mode):
         sec = d.get(mode)
         if sec and sec.get("n_nodes", d.get("n_nodes")) == n_nodes:
             return dict(sec, source=d.get("source"))
+        other = d.get("by_nodes", {}).get(str(n_nodes), {})  # other workloads' profiles (C4)
+        if other.get(mode):
+            return dict(other[mode], source=other.get("source"))
     except (OSError, ValueError):
         pass
     return None
@@ -286,11 +289,25 @@ def main():
         traffic = None
         if pmc and pmc.get("hbm_bytes_per_launch") is not None:  # measured HBM bytes of the scan launches of a cycle
             traffic = pmc["hbm_bytes_per_launch"] * agg["launches"] / max(1, agg["steps"])
-        return {"bound": "hbm", "achieved": ach, "peak": peak, "unit": "GB/s", "frac": ach / peak,
-                "traffic": traffic, "scope": "allocate cycle",
-                "definition": "SURVEY 8(d): task evaluations x (N x 64 B + 32 B) per allocate cycle / p50 wall time "
-                              "of kbg_allocate (allocate Execute); traffic = PMC HBM bytes of the cycle's scan launches",
-                "task_evaluations_per_cycle": units, "algo_bytes_per_cycle": per_cycle, "p50_cycle_ms": t * 1e3}
+        out = {"bound": "hbm", "achieved": ach, "peak": peak, "unit": "GB/s", "frac": ach / peak,
+               "traffic": traffic, "scope": "allocate cycle",
+               "definition": "SURVEY 8(d): task evaluations x (N x 64 B + 32 B) per allocate cycle / p50 wall time "
+                             "of kbg_allocate (allocate Execute); traffic = PMC HBM bytes of the cycle's scan launches",
+               "task_evaluations_per_cycle": units, "algo_bytes_per_cycle": per_cycle, "p50_cycle_ms": t * 1e3}
+        if ach <= peak:
+            return out
+        # The 8(d) byte count exceeds what HBM could deliver in the cycle (C4:
+        # each wave keeps its 64 node rows in registers across the workgroup's
+        # rows, so a node record is not re-read per evaluation): the roofline
+        # is then the physical one, the measured HBM bytes of the cycle's scan
+        # launches over the cycle, and the 8(d) figure is kept beside it.
+        eq = {k: out[k] for k in ("achieved", "frac", "task_evaluations_per_cycle", "algo_bytes_per_cycle")}
+        eq["note"] = "SURVEY 8(d) byte count / cycle: above the HBM peak, not a fraction of anything physical"
+        phys = traffic / t / 1e9 if traffic is not None else None
+        out.update({"achieved": phys, "frac": phys / peak if phys is not None else None,
+                    "definition": "PMC HBM bytes (2 x FETCH_SIZE + WRITE_SIZE) of the cycle's scan launches / p50 "
+                                  "wall time of kbg_allocate", "equivalent_8d": eq})
+        return out
 
     def scan_kernel(agg, mode):
         """The dominant device kernel against its physical ceilings: HBM
