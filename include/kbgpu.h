@@ -319,11 +319,18 @@ typedef struct kbg_session kbg_session;
  * clique, one rank per GPU, created collectively from one unique id that the
  * caller distributes (rank 0 calls kbg_comm_unique_id; any side channel
  * carries the bytes). Shard r holds the node-table rows of 64-node words
- * [r*Wl, (r+1)*Wl), Wl = ceil(ceil(N/64)/R); per batch every rank scans its
- * rows and an RCCL all-gather over xGMI publishes the feasibility bitmaps, so
- * every rank resolves the identical decision sequence; each rank writes back
- * only the node rows it owns. All ranks must call kbg_session_open_sharded
- * and kbg_allocate with the same snapshot and options, in lockstep. */
+ * [r*Wl, (r+1)*Wl), Wl = ceil(ceil(N/64)/R), so rank order is node order and
+ * first-fit is the lowest rank with a fitting node. kbg_allocate (owner-
+ * resolve, up to 32 ranks, sessions without pod affinity): rank 0 runs the
+ * ordering engine and broadcasts each batch; every rank scans and selects its
+ * own rows; a sum-reduce says which ranks fit each row; min-reduce rounds of
+ * packed winners (node << 1 | kind) decide each task on the lowest rank that
+ * still fits its row (a rank that fails a row hands the row's later tasks to
+ * the next). The other actions (and pod-affinity sessions) all-gather the
+ * per-rank bitmaps / all-reduce the victim-scan words and resolve on every
+ * rank. Every rank returns the identical decision log and writes back only the
+ * node rows it owns. All ranks must call kbg_session_open_sharded and the
+ * actions with the same snapshot and options, in lockstep. */
 #define KBG_COMM_ID_BYTES 128
 typedef struct kbg_comm kbg_comm;
 kbg_status kbg_comm_unique_id(uint8_t out[KBG_COMM_ID_BYTES]);
