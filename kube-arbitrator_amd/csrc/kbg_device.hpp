@@ -225,8 +225,8 @@ hipError_t launch_mask_apply(uint64_t* class_mask, const MaskDelta* deltas, int3
 // consecutive nodes, two per wave, and writes its two words; sharded, each
 // rank writes the words of its node range (64-node aligned) into zeroed
 // arrays and an element-wise ncclAllReduce(max) of disjoint words is their OR.
-constexpr int kVictimNodesPerBlock = 32;
-constexpr int kVictimBlockWaves = 16;
+constexpr int kVictimNodesPerBlock = 8;  // one node per wave; a workgroup writes one byte of stop bits
+constexpr int kVictimBlockWaves = 8;
 inline int32_t kbg_victim_words(int32_t n_nodes) { return (n_nodes + 31) / 32; }
 hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* stop_bits, uint32_t* panic_bits,
                               hipStream_t stream, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);

@@ -371,14 +371,15 @@ __device__ __forceinline__ void apply_preemptee(const VictimTables& t, int fns, 
 // (wave-uniform), UINT32_MAX when the reference moves on to the next node.
 // NCH is a compile-time bound so the per-chunk masks stay in registers.
 template <int NCH>
-__device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t, int n, int off, int L, int lane) {
+__device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t, int n, int off, int L, int lane,
+                                      const VCand& c0) {
   constexpr uint32_t kNone = 0xffffffffu;
   const int nch = (L + 63) >> 6;  // <= NCH
   uint64_t pm[NCH];
   uint64_t any_pm = 0ull;
 #pragma unroll
   for (int h = 0; h < NCH; ++h) {
-    pm[h] = h < nch ? __ballot(load_cand(p, t, off, L, h * 64 + lane).f) : 0ull;
+    pm[h] = h < nch ? __ballot((h == 0 ? c0 : load_cand(p, t, off, L, h * 64 + lane)).f) : 0ull;
     any_pm |= pm[h];
   }
   if (!any_pm) return kNone;  // no preemptee: every fn returns nil
@@ -470,14 +471,22 @@ __device__ uint32_t victim_node(const VictimScan& p, const VictimTables& t, int 
   const int off = t.nt_off[n];
   const int L = t.nt_off[n + 1] - off;
   if (NCH_MAX <= 2 && L > 128) return kNone;  // evaluated by the big-node kernel
+  // the first chunk's records are requested before the node's own tests
+  // resolve, so the two loads overlap
+  const VCand c0 = load_cand(p, t, off, L, lane);
   if (!((t.class_mask[(size_t)p.cls * p.W + (n >> 6)] >> (n & 63)) & 1ull)) return kNone;  // static predicate
   if (t.panic_node[n]) return ((uint32_t)n << 1) | 1u;  // SetNode(nil) inside PredicateFn (predicates.go:122-123)
   if (p.cap_check && t.ntasks[row] >= t.maxtasks[row]) return kNone;  // predicates.go:125-127
-  if (NCH_MAX > 2) return victim_candidates<NCH_MAX>(p, t, n, off, L, lane);
-  if (L <= 64) return victim_candidates<1>(p, t, n, off, L, lane);
-  return victim_candidates<2>(p, t, n, off, L, lane);
+  if (NCH_MAX > 2) return victim_candidates<NCH_MAX>(p, t, n, off, L, lane, c0);
+  if (L <= 64) return victim_candidates<1>(p, t, n, off, L, lane, c0);
+  return victim_candidates<2>(p, t, n, off, L, lane, c0);
 }
 
+// One node per wave, kVictimNodesPerBlock waves per workgroup: every node's
+// dependent loads (header -> candidate records -> job tables) are in flight
+// at once instead of two nodes back to back per wave. The workgroup writes
+// its byte of stop bits and of panic bits (node_lo is 64-node aligned, so a
+// shard starts on a byte).
 __global__ __launch_bounds__(64 * kVictimBlockWaves) void kbg_victim_kernel(VictimScan p, VictimTables t,
                                                                            uint32_t* __restrict__ stop_bits,
                                                                            uint32_t* __restrict__ panic_bits) {
@@ -486,24 +495,19 @@ __global__ __launch_bounds__(64 * kVictimBlockWaves) void kbg_victim_kernel(Vict
   const int w = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_stop = s_panic = 0u;
   __syncthreads();
-  const int base = blockIdx.x * kVictimNodesPerBlock;  // rows of this workgroup
-#pragma unroll
-  for (int k = 0; k < kVictimNodesPerBlock / kVictimBlockWaves; ++k) {
-    const int off = w + k * kVictimBlockWaves;
-    const int row = base + off;
-    if (row < p.node_n) {
-      const uint32_t key = victim_node<2>(p, t, row, lane);  // wave-uniform
-      if (key != 0xffffffffu && lane == 0) {
-        atomicOr(&s_stop, 1u << off);
-        if (key & 1u) atomicOr(&s_panic, 1u << off);
-      }
+  const int row = blockIdx.x * kVictimNodesPerBlock + w;
+  if (row < p.node_n) {
+    const uint32_t key = victim_node<2>(p, t, row, lane);  // wave-uniform
+    if (key != 0xffffffffu && lane == 0) {
+      atomicOr(&s_stop, 1u << w);
+      if (key & 1u) atomicOr(&s_panic, 1u << w);
     }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int word = (p.node_lo >> 5) + blockIdx.x;  // node_lo is 64-node aligned
-    stop_bits[word] = s_stop;
-    panic_bits[word] = s_panic;
+    const int byte = (p.node_lo >> 3) + blockIdx.x;
+    reinterpret_cast<uint8_t*>(stop_bits)[byte] = (uint8_t)s_stop;
+    reinterpret_cast<uint8_t*>(panic_bits)[byte] = (uint8_t)s_panic;
   }
 }
 
