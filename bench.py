@@ -20,10 +20,11 @@ scan_kernel = the dominant kernel against its physical ceilings: PMC HBM bytes
 cpu_baseline= the kbref oracle on this host, CPU model stated: B-ref (1 thread),
               B-omp (every core of the job's share, <= 16), B-faithful (the
               per-call podLister walk, 60 s budget); C4 runs 60 s samples
-N > 1       = ONE cluster with its node axis sharded over the N GPUs:
-              each rank scans its node rows, an RCCL all-gather over xGMI
-              publishes the per-shard feasibility bitmaps every batch, every
-              rank resolves the identical decision sequence (strong scaling;
+N > 1       = ONE cluster with its node axis sharded over the N GPUs (SURVEY §8e,
+              DESIGN.md §7): rank 0 runs the ordering engine and broadcasts each
+              batch, each rank scans its node rows and resolves the tasks its
+              rows win, RCCL min-reduces over xGMI publish the packed winners;
+              every rank returns the identical decision log (strong scaling;
               the whole job places decisions_per_cycle per step)
 """
 import argparse
@@ -359,6 +360,7 @@ def main():
                 "truncations": s2.truncations, "replayed": s2.replayed, "host_engine_ms": s2.engine_ms,
                 "host_resolve_ms": s2.resolve_ms, "device_roundtrip_ms": s2.device_ms,
                 "delta_writeback_ms": s2.delta_ms, "exchange_ms": s2.exchange_ms, "shards": s2.shards,
+                "owner_rounds": s2.owner_rounds,
                 "cycle_ms": s2.allocate_ms}
 
     line = {
@@ -377,7 +379,8 @@ def main():
         "data": "synthetic (seeded BASELINE config generator, kbgpu/synth.py)",
         "config": {"workload": f"C{cid}: {n_nodes} nodes x {prod['pending']} pending tasks, "
                                f"{prod['jobs']} gang PodGroups, {prod['queues']} proportion queues, default tiers",
-                   "parallelism": f"node-axis shards x{world} (RCCL all-gather)" if world > 1 else "single-gpu",
+                   "parallelism": (f"node-axis shards x{world} (owner-resolve: batch broadcast, RCCL sum/min-reduce "
+                                   f"of availability and packed winners)") if world > 1 else "single-gpu",
                    "batch_tasks": base_opts.get("batch_tasks", 8192),
                    "candidates": base_opts.get("candidates", 32)},
         "roofline": cycle_roofline(full, "full_scan"),
@@ -398,7 +401,7 @@ def main():
     }
     if world == 1 and not args.no_resident:
         line["resident_session"] = resident_bench(cache, fx, base_opts)
-    if rank == 0 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline:  # the CPU baseline is an N=1 figure
         # C4 cannot finish on one thread within minutes: bounded samples there
         budget = 60.0 if cid >= 4 else 0.0
         line["cpu_baseline"] = cpu_baseline(fx, f"C{cid}", 1, budget=budget)
@@ -596,7 +599,7 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid, open_ms_
         "open_ms": st.open_ms,
         "open_ms_first_in_process": open_ms_first,
     }
-    if rank == 0 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(fx, f"C{cid} ({', '.join(fx['actions'])})")
     if rank == 0:
         emit(line)
