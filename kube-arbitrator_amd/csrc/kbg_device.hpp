@@ -206,6 +206,9 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
                        int32_t n_tasks, int32_t cap_check, int32_t int_mode, uint64_t* out, hipStream_t stream,
                        hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
+// avail[g] = bit when row g has any candidate (count[g] != 0), else 0.
+hipError_t launch_avail(const uint32_t* count, int32_t n_rows, uint32_t bit, uint32_t* avail, hipStream_t stream);
+
 // Row g gets cap_off[g+1]-cap_off[g] candidate slots at out_cand[cap_off[g]],
 // taken from the global words [w_lo, w_hi) in node order.
 hipError_t launch_select(const uint64_t* bits, int32_t w_lo, int32_t w_hi, int32_t Wl, int32_t n_rows,

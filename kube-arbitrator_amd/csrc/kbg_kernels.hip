@@ -247,6 +247,20 @@ hipError_t launch_select(const uint64_t* bits, int32_t w_lo, int32_t w_hi, int32
   return hipGetLastError();
 }
 
+// Owner-resolve: this rank's availability bit of each row (any candidate in
+// its own words), summed over the ranks by the all-reduce that follows.
+__global__ __launch_bounds__(256) void kbg_avail_kernel(const uint32_t* __restrict__ count, int32_t n_rows,
+                                                        uint32_t bit, uint32_t* __restrict__ avail) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n_rows) avail[g] = (count[g] & kCountMask) ? bit : 0u;
+}
+
+hipError_t launch_avail(const uint32_t* count, int32_t n_rows, uint32_t bit, uint32_t* avail, hipStream_t stream) {
+  if (n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kbg_avail_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, stream, count, n_rows, bit, avail);
+  return hipGetLastError();
+}
+
 // ----------------------------------------------------------------- apply
 __global__ __launch_bounds__(256) void kbg_apply_kernel(NodeSoA nd, const NodeDelta* __restrict__ d, int32_t n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;

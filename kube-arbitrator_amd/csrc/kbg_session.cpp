@@ -530,7 +530,15 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   const int32_t w_hi = S.owner ? std::min(S.W, (S.shard + 1) * S.Wl) : S.W;
   HIP_TRY(kbg::launch_select(S.d_bits, w_lo, w_hi, S.Wl, G, d_capoff, S.d_down + G, S.d_down, S.stream, sg.ev[2],
                              sg.ev[3]));
-  HIP_TRY(hipMemcpyAsync(sg.h_down, S.d_down, ((size_t)G + total) * 4, hipMemcpyDeviceToHost, S.stream));
+  size_t down = (size_t)G + total;
+  if (S.owner && S.comm) {  // owner-resolve: the rows' availability over the ranks, in the same round trip
+    uint32_t* d_avail = S.d_down + down;
+    HIP_TRY(kbg::launch_avail(S.d_down, G, 1u << S.shard, d_avail, S.stream));
+    const ncclResult_t nr = ncclAllReduce(d_avail, d_avail, (size_t)G, ncclUint32, ncclSum, S.comm->nccl, S.stream);
+    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+    down += (size_t)G;
+  }
+  HIP_TRY(hipMemcpyAsync(sg.h_down, S.d_down, down * 4, hipMemcpyDeviceToHost, S.stream));
   HIP_TRY(hipEventRecord(sg.ev[6], S.stream));
   sg.G = G;
   sg.base = base;
@@ -1744,7 +1752,7 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   for (auto& e : S.ev) HIP_TRY(hipEventCreate(&e));
   if ((st = alloc_soa(S, &S.d_nodes)) || (st = alloc_soa(S, &S.d_nodes0))) return st;
   const size_t up_cap = (size_t)kbg::kbg_pad_rows(S.K) * sizeof(kbg::TaskRec) + ((size_t)S.K + 1) * 4;
-  const size_t down_cap = (size_t)S.K + (size_t)S.cand_cap;
+  const size_t down_cap = 2 * (size_t)S.K + (size_t)S.cand_cap;  // counts, candidates, owner-resolve availability
   if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) || (st = dalloc(S, &S.d_up, up_cap)) ||
       (st = dalloc(S, &S.d_bits, (size_t)S.R * 2 * S.K * kbg::kbg_slot_words(S.Wl))) ||
       (st = dalloc(S, &S.d_down, down_cap)) || (st = dalloc(S, &S.d_deltas, S.K)))
@@ -2527,6 +2535,13 @@ struct ShardIO {
   virtual kbg_status bcast(uint32_t* buf, size_t n) = 0;                   // rank 0's words to every rank
   virtual kbg_status scan(Session& S, kbg::Stage& sg, int32_t G, int32_t base) = 0;  // this rank's candidates
   virtual kbg_status allreduce(uint32_t* buf, size_t n, bool sum) = 0;      // element-wise min (sum), in place
+  // the scan plus the rows' availability over the ranks (bit r: rank r has a candidate)
+  virtual kbg_status scan_avail(Session& S, kbg::Stage& sg, int32_t G, int32_t base, uint32_t* avail) {
+    kbg_status st = scan(S, sg, G, base);
+    if (st != KBG_OK) return st;
+    for (int32_t g = 0; g < G; ++g) avail[g] = (sg.h_count[g] & kbg::kCountMask) ? (1u << S.shard) : 0u;
+    return allreduce(avail, G, true);
+  }
   // this rank's committed rows (and class-mask words) to the table its scans read
   virtual kbg_status push(Session& S, const std::vector<int32_t>& touched) { return push_deltas(S, touched); }
   virtual kbg_status sync(Session& S) {
@@ -2578,6 +2593,14 @@ struct RcclIO final : ShardIO {
   }
   kbg_status scan(Session& S2, kbg::Stage& sg, int32_t G, int32_t base) override {
     return device_scan(S2, sg, G, base);
+  }
+  // one round trip: scan, select, availability bits and their sum-reduce
+  kbg_status scan_avail(Session& S2, kbg::Stage& sg, int32_t G, int32_t base, uint32_t* avail) override {
+    kbg_status st = device_scan(S2, sg, G, base);
+    if (st != KBG_OK) return st;
+    const uint32_t* h_avail = sg.h_down + G + sg.h_capoff[G];
+    std::copy(h_avail, h_avail + G, avail);
+    return KBG_OK;
   }
   kbg_status allreduce(uint32_t* buf, size_t n, bool sum) override {
     const auto t0 = std::chrono::steady_clock::now();
@@ -2786,11 +2809,9 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
     S.stats.batches++;
     // ---- 2. own candidates against the table with every earlier commit
     const int32_t G = grouper.build(sg, bt.data(), n);
-    if ((st = io.scan(S, sg, G, stamp)) != KBG_OK) return abort(st);
     // ---- 3. which ranks fit each row at all
     std::vector<uint32_t> avail(G);
-    for (int32_t g = 0; g < G; ++g) avail[g] = (sg.h_count[g] & kbg::kCountMask) ? (1u << me) : 0u;
-    if ((st = io.allreduce(avail.data(), G, true)) != KBG_OK) return abort(st);
+    if ((st = io.scan_avail(S, sg, G, stamp, avail.data())) != KBG_OK) return abort(st);
     S.stats.device_ms += ms_since(tp);
     // ---- 4. owner rounds
     tp = clk::now();
