@@ -418,6 +418,7 @@ kbg_status copy_soa(Session& S, const kbg::NodeSoA& dst, const kbg::NodeSoA& src
 }
 
 void free_device(Session& S) {
+  if (S.stream) (void)hipStreamSynchronize(S.stream);  // every enqueued reader of the staging has run
   for (kbg::Stage& g : S.stages) {
     if (g.inflight) (void)hipEventSynchronize(g.ev[6]);  // nothing may still write the staging
     if (g.h_up) (void)hipHostFree(g.h_up);
@@ -446,6 +447,9 @@ void free_device(Session& S) {
       (void)hipEventDestroy(e);
       e = nullptr;
     }
+  if (S.stage_ev) (void)hipEventDestroy(S.stage_ev);
+  S.stage_ev = nullptr;
+  S.stage_pending = false;
   if (S.stream) (void)hipStreamDestroy(S.stream);
   S.stream = nullptr;
 }
@@ -582,10 +586,30 @@ kbg_status device_scan(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
 
 // Writes the rows of the nodes touched by the last commits back to HBM (only
 // the rows this process holds; every shard's host mirror saw every commit).
+// The pinned staging buffers (h_deltas, h_mdeltas, h_sdeltas) are read by
+// the stream when a copy or kernel executes, not when it is enqueued, and the
+// stream may still be behind (a scan enqueued earlier runs first): a writer
+// waits for the last reader (stage_acquire) and every enqueued reader marks
+// the stream (stage_release).
+kbg_status stage_acquire(Session& S) {
+  if (S.stage_pending) {
+    HIP_TRY(hipEventSynchronize(S.stage_ev));
+    S.stage_pending = false;
+  }
+  return KBG_OK;
+}
+kbg_status stage_release(Session& S) {
+  HIP_TRY(hipEventRecord(S.stage_ev, S.stream));
+  S.stage_pending = true;
+  return KBG_OK;
+}
+
 // Class-mask words changed on the host (host ports, pod affinity) into HBM;
 // every shard holds the whole mask.
 kbg_status push_mask_deltas(Session& S) {
   for (size_t m = 0; m < S.mask_dirty.size();) {
+    kbg_status st = stage_acquire(S);
+    if (st != KBG_OK) return st;
     const int32_t cnt = (int32_t)std::min<size_t>(S.mask_dirty.size() - m, (size_t)kbg::kMaskDeltaCap);
     for (int32_t k = 0; k < cnt; ++k) {
       const uint32_t idx = S.mask_dirty[m + k];
@@ -594,10 +618,9 @@ kbg_status push_mask_deltas(Session& S) {
     }
     HIP_TRY(hipMemcpyAsync(S.d_mdeltas, S.h_mdeltas, cnt * sizeof(kbg::MaskDelta), hipMemcpyHostToDevice, S.stream));
     HIP_TRY(kbg::launch_mask_apply(S.d_class_mask, S.d_mdeltas, cnt, S.stream));
+    if ((st = stage_release(S)) != KBG_OK) return st;
     m += cnt;
-    if (m < S.mask_dirty.size()) HIP_TRY(hipStreamSynchronize(S.stream));  // staging reuse
   }
-  // (the last chunk's copy is retired by the next device round trip's synchronize)
   S.mask_dirty.clear();
   return KBG_OK;
 }
@@ -607,6 +630,7 @@ kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
   if (st != KBG_OK) return st;
   size_t i = 0;
   while (i < touched.size()) {
+    if ((st = stage_acquire(S)) != KBG_OK) return st;
     int32_t cnt = 0;
     for (; i < touched.size() && cnt < S.K; ++i) {
       const int32_t n = touched[i];
@@ -618,9 +642,7 @@ kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
     if (cnt == 0) break;
     HIP_TRY(hipMemcpyAsync(S.d_deltas, S.h_deltas, cnt * sizeof(kbg::NodeDelta), hipMemcpyHostToDevice, S.stream));
     HIP_TRY(kbg::launch_apply(S.d_nodes, S.d_deltas, cnt, S.stream));
-    // The staging buffer is reused by the next chunk or the next batch; the
-    // next device_scan's synchronize (same stream) retires this copy first.
-    if (i < touched.size()) HIP_TRY(hipStreamSynchronize(S.stream));
+    if ((st = stage_release(S)) != KBG_OK) return st;
   }
   return KBG_OK;
 }
@@ -1750,6 +1772,8 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   HIP_TRY(hipSetDevice(S.device));
   HIP_TRY(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   for (auto& e : S.ev) HIP_TRY(hipEventCreate(&e));
+  HIP_TRY(hipEventCreateWithFlags(&S.stage_ev, hipEventDisableTiming));
+  S.stage_pending = false;
   if ((st = alloc_soa(S, &S.d_nodes)) || (st = alloc_soa(S, &S.d_nodes0))) return st;
   const size_t up_cap = (size_t)kbg::kbg_pad_rows(S.K) * sizeof(kbg::TaskRec) + ((size_t)S.K + 1) * 4;
   const size_t down_cap = 2 * (size_t)S.K + (size_t)S.cand_cap;  // counts, candidates, owner-resolve availability
@@ -3152,6 +3176,8 @@ kbg_status victim_push(Session& S, const std::vector<int32_t>& touched) {
   size_t ti = 0, si = 0;
   while (ti < touched.size() || si < S.sdeltas.size()) {
     if (S.vstage_busy) HIP_TRY(hipStreamSynchronize(S.stream));
+    S.vstage_busy = false;
+    if (kbg_status st = stage_acquire(S); st != KBG_OK) return st;
     int32_t nn = 0;
     for (; ti < touched.size() && nn < S.K; ++ti) {
       const int32_t n = touched[ti];
@@ -3166,6 +3192,7 @@ kbg_status victim_push(Session& S, const std::vector<int32_t>& touched) {
     if (nn + ns == 0) break;
     HIP_TRY(kbg::launch_victim_prep(S.d_nodes, S.vt, S.h_deltas_dev, nn, S.h_sdeltas_dev, ns, S.stream));
     S.vstage_busy = true;
+    if (kbg_status st = stage_release(S); st != KBG_OK) return st;
   }
   S.sdeltas.clear();
   return KBG_OK;
@@ -4108,6 +4135,7 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
     HIP_TRY(hipSetDevice(S.device));
     // the changed node rows, into the live table and the reset copy
     for (size_t i = 0; i < U.nodes.size();) {
+      if ((st = stage_acquire(S)) != KBG_OK) return st;
       int32_t cnt = 0;
       for (; i < U.nodes.size() && cnt < S.K; ++i) {
         const int32_t nd = U.nodes[i];

@@ -394,6 +394,8 @@ struct Session {
   int32_t res_stamp = 0;          // resolution stamps: monotone over the session (mark / mwmark compare)
   NodeDelta* d_deltas = nullptr;
   NodeDelta* h_deltas = nullptr; // pinned
+  hipEvent_t stage_ev = nullptr; // after the last enqueued reader of the pinned staging (stage_acquire)
+  bool stage_pending = false;
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   std::vector<void*> d_allocs;
 

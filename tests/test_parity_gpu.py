@@ -442,3 +442,22 @@ def test_select_replays_with_affinity(seed):
         else:
             assert node.value == -1, uid
     ssn.close()
+
+
+def test_staging_reuse_under_overlap():
+    """A resident-session churn fixture (update fuzz seed 83, round 2) whose
+    allocate runs 3-task batches with the next scan in flight: the pinned
+    delta staging must not be rewritten before the stream has copied it
+    (stage_acquire / stage_release), or a lost node delta shows up as a
+    backfill onto a full node. Repeated in one process, where the stream runs
+    behind the host."""
+    fx = load_golden("fx_staging_race.json")
+    ref = run_oracle(fx)
+    for it in range(120):
+        opts = {"batch_tasks": 3, "candidates": 4, "full_scan": 1} if it % 2 else \
+               {"batch_tasks": 1 + it % 9, "candidates": 1 + it % 5, "full_scan": it % 4 == 0}
+        opts["full_scan"] = int(opts["full_scan"])
+        got, ssn = run_fixture(fx, opts)
+        compare_outputs(ref, got)
+        if ssn:
+            ssn.close()
