@@ -206,6 +206,18 @@ class NodeInfo:
             res.add_task(t)
         return res
 
+    def set_node(self, node):  # node_info.go:84-99 (Releasing and Used are not reset: the reference's own quirk)
+        self.name = node["name"]
+        self.node = node
+        self.allocatable = Resource.from_list(node.get("allocatable"))
+        self.capability = Resource.from_list(node.get("capacity", node.get("allocatable")))
+        self.idle = Resource.from_list(node.get("allocatable"))
+        for t in self.tasks.values():
+            if t.status == RELEASING:
+                self.releasing.add(t.resreq)
+            self.idle.sub(t.resreq)
+            self.used.add(t.resreq)
+
     def add_task(self, task):  # node_info.go:101-129
         key = pod_key(task.pod)
         if key in self.tasks:

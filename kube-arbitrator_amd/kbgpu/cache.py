@@ -59,9 +59,10 @@ class SchedulerCache:
         self._add_task(TaskInfo(pod))
 
     def add_node(self, node):  # :232-240
-        if node["name"] in self.nodes:
-            raise ValueError("add_node after a pod referenced it (NodeInfo.SetNode path) is not modelled")
-        self.nodes[node["name"]] = NodeInfo(node)
+        if node["name"] in self.nodes:  # a pod named the node first: NodeInfo(nil) gets its Node (SetNode)
+            self.nodes[node["name"]].set_node(node)
+        else:
+            self.nodes[node["name"]] = NodeInfo(node)
 
     def add_pod_group(self, pg):  # :344-358
         jid = f"{pg.get('namespace', '')}/{pg['name']}"

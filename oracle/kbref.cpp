@@ -491,6 +491,18 @@ struct NodeInfo {  // api/node_info.go:26-42
     }
     return ni;
   }
+  void SetNode(const Node* n) {  // :84-99 (Releasing and Used are not reset, as in the reference)
+    name = n->name;
+    node = n;
+    allocatable = n->allocatable;
+    capability = n->capacity;
+    idle = n->allocatable;
+    for (auto& kv : tasks.items) {
+      if (kv.second->status == Releasing) releasing.Add(kv.second->resreq);
+      idle.Sub(kv.second->resreq);
+      used.Add(kv.second->resreq);
+    }
+  }
   bool AddTask(const TaskInfo* task) {  // :101-129
     std::string key = pod_key(task->pod);
     if (tasks.find(key)) return false;  // "already on node" error
@@ -667,9 +679,9 @@ struct SchedulerCache {
     ti->spec_class = spec_class;
     addTask(ti);
   }
-  void addNode(const Node* n) {  // :232-240 (SetNode path unused: nodes precede pods in fixtures)
-    if (nodes.find(n->name)) throw BadInput("duplicate node " + n->name);
-    nodes.set(n->name, NodeInfo::make(n));
+  void addNode(const Node* n) {  // :232-240
+    if (NodeInfo** ni = nodes.find(n->name)) (*ni)->SetNode(n);  // a pod named it first: NodeInfo(nil)
+    else nodes.set(n->name, NodeInfo::make(n));
   }
   void setPodGroup(const PodGroup* pg) {  // :344-358
     std::string id = pg->ns + "/" + pg->name;
@@ -2186,6 +2198,59 @@ static std::string run_ops(const Value& fx) {
       std::sort(ids.begin(), ids.end());
       for (size_t i = 0; i < ids.size(); i++) o += (i ? "," : "") + kbjson::quote(ids[i]);
       o += "]";
+    }
+    o += "}}";
+  } else if (kind == "cache_ops") {  // cache_test.go: AddNode / AddPod in the listed order
+    std::vector<Node*> nodes;
+    if (const Value* ns = fx.get("nodes"))
+      for (auto& nv : ns->arr) {
+        Node* node = new Node();
+        node->name = nv.str("name");
+        node->allocatable = new_resource(nv.get("allocatable"));
+        node->capacity = nv.get("capacity") ? new_resource(nv.get("capacity")) : node->allocatable;
+        nodes.push_back(node);
+      }
+    SchedulerCache c;
+    for (auto& op : fx.get("ops")->arr) {
+      if (op.str("op") == "add_node") {
+        const Node* n = nullptr;
+        for (const Node* x : nodes)
+          if (x->name == op.str("node")) n = x;
+        if (!n) throw BadInput("unknown node " + op.str("node"));
+        c.addNode(n);
+      } else {
+        c.addPod(find_pod(op.str("pod")), 0);
+      }
+    }
+    o += "\"nodes\":{";
+    bool f = true;
+    for (auto& kv : c.nodes.items) {
+      const NodeInfo* ni = kv.second;
+      o += std::string(f ? "" : ",") + kbjson::quote(kv.first) + ":{\"idle\":" + res_json(ni->idle) +
+           ",\"used\":" + res_json(ni->used) + ",\"releasing\":" + res_json(ni->releasing) +
+           ",\"allocatable\":" + res_json(ni->allocatable) + ",\"tasks\":[";
+      f = false;
+      bool g = true;
+      for (auto& t : ni->tasks.items) { o += (g ? "" : ",") + kbjson::quote(t.first); g = false; }
+      o += "]}";
+    }
+    o += "},\"jobs\":{";
+    f = true;
+    for (auto& kv : c.jobs.items) {
+      const JobInfo* ji = kv.second;
+      o += std::string(f ? "" : ",") + kbjson::quote(kv.first) + ":{\"status_index\":{";
+      f = false;
+      bool g = true;
+      for (auto& si : ji->statusIndex) {
+        o += (g ? "" : ",") + std::string("\"") + std::to_string(si.first) + "\":[";
+        g = false;
+        std::vector<std::string> ids;
+        for (auto& t : si.second.items) ids.push_back(t.first);
+        std::sort(ids.begin(), ids.end());
+        for (size_t i = 0; i < ids.size(); i++) o += (i ? "," : "") + kbjson::quote(ids[i]);
+        o += "]";
+      }
+      o += "},\"allocated\":" + res_json(ji->allocated) + ",\"total_request\":" + res_json(ji->totalRequest) + "}";
     }
     o += "}}";
   } else if (kind == "quantity") {

@@ -133,6 +133,32 @@ FIXTURES = {
         "expected": {"allocated": [3000, 3e9, 0], "total_request": [4000, 4e9, 0],
                      "status_index": {"1": ["c1-p1"], "32": ["c1-p3"]}},
     },
+    # pkg/scheduler/cache/cache_test.go:128-186 TestAddPod (nodes, then pods; job from the controller owner)
+    "ref_cache_addpod": {
+        "source": "pkg/scheduler/cache/cache_test.go:128-186",
+        "kind": "cache_ops",
+        "nodes": [{"name": "n1", "allocatable": {"cpu": "2000m", "memory": "10G"}}],
+        "pods": [api_pod("c1", "p1", "", "Pending", ("1000m", "1G"), "j1"),
+                 api_pod("c1", "p2", "n1", "Running", ("1000m", "1G"), "j1")],
+        "ops": [{"op": "add_node", "node": "n1"}, {"op": "add_pod", "pod": "c1/p1"}, {"op": "add_pod", "pod": "c1/p2"}],
+        "expected": {"nodes": {"n1": {"idle": [1000, 9e9, 0], "used": [1000, 1e9, 0], "releasing": [0, 0, 0],
+                                      "allocatable": [2000, 10e9, 0], "tasks": ["c1/p2"]}},
+                     "jobs": {"j1": {"status_index": {"1": ["c1-p1"], "32": ["c1-p2"]},
+                                     "allocated": [1000, 1e9, 0], "total_request": [2000, 2e9, 0]}}},
+    },
+    # pkg/scheduler/cache/cache_test.go:188-236 TestAddNode (pods first: the node is a NodeInfo(nil)
+    # until AddNode's SetNode; pods without a controller join no job)
+    "ref_cache_addnode": {
+        "source": "pkg/scheduler/cache/cache_test.go:188-236",
+        "kind": "cache_ops",
+        "nodes": [{"name": "n1", "allocatable": {"cpu": "2000m", "memory": "10G"}}],
+        "pods": [api_pod("c1", "p1", "", "Pending", ("1000m", "1G")),
+                 api_pod("c1", "p2", "n1", "Running", ("1000m", "1G"))],
+        "ops": [{"op": "add_pod", "pod": "c1/p1"}, {"op": "add_pod", "pod": "c1/p2"}, {"op": "add_node", "node": "n1"}],
+        "expected": {"nodes": {"n1": {"idle": [1000, 9e9, 0], "used": [1000, 1e9, 0], "releasing": [0, 0, 0],
+                                      "allocatable": [2000, 10e9, 0], "tasks": ["c1/p2"]}},
+                     "jobs": {}},
+    },
 }
 
 
