@@ -2707,6 +2707,54 @@ struct Replayer {
   }
 };
 
+// One committed outcome of the owner-resolve walk, for the log side.
+struct LogItem {
+  int32_t t, node, kind;
+  bool ok, own, dup;
+  Res old;  // own commit: the Idle / Releasing row before it
+};
+
+// The log side of the owner-resolve walk on a thread of its own: batches of
+// committed outcomes in commit order.
+struct Logger {
+  std::function<void(const LogItem&)> fn;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::vector<LogItem>> q;
+  bool done = false;
+  explicit Logger(std::function<void(const LogItem&)> f) : fn(std::move(f)) {
+    th = std::thread([this]() { run(); });
+  }
+  ~Logger() { join(); }
+  void push(std::vector<LogItem>&& v) {
+    std::lock_guard<std::mutex> lk(mu);
+    q.push_back(std::move(v));
+    cv.notify_all();
+  }
+  void join() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      done = true;
+      cv.notify_all();
+    }
+    if (th.joinable()) th.join();
+  }
+  void run() {
+    for (;;) {
+      std::vector<LogItem> v;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return done || !q.empty(); });
+        if (q.empty()) return;
+        v = std::move(q.front());
+        q.pop_front();
+      }
+      for (const LogItem& it : v) fn(it);
+    }
+  }
+};
+
 kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t cap, int32_t* n_out) {
   if (S.allocated || S.backfilled || S.preempted)
     return fail(KBG_E_INVALID, "allocate runs once per cycle, before backfill and preempt; call kbg_session_reset");
@@ -2782,6 +2830,7 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
   Batch* cur = nullptr;
   int32_t seg = 0;  // rank 0: first entry of `cur` in the current segment
   int32_t stamp = S.res_stamp;
+  std::unique_ptr<Logger>* lg_ref = nullptr;  // set once the logger exists (below)
   auto finish = [&]() {
     if (pr) {
       if (cur) pr->recycle(cur);
@@ -2789,12 +2838,38 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
       pr->finish();
     }
     if (rp) rp->join();
+    if (lg_ref && *lg_ref) (*lg_ref)->join();
   };
   auto abort = [&](kbg_status st) {
     finish();
     S.owner = false;
     return st;
   };
+  // The log side of a committed outcome: decision log and gang dispatch
+  // (record_decision), FitError bookkeeping, and — for another rank's row —
+  // this rank's mirror of it. `oldp`: host ports before an own commit.
+  auto log_one = [&](const LogItem& it, const uint64_t* oldp) {
+    S.stats.task_evaluations++;
+    last[S.task_job[it.t]] = LastEval{it.t, (int32_t)dec.size(), it.node, it.kind};
+    if (!it.ok) return;
+    bool dup = it.dup;
+    if (it.own) {  // committed during the resolve
+      dec_old.push_back(it.old);
+      if (S.has_ports) dec_oldp.insert(dec_oldp.end(), oldp, oldp + S.PW);
+    } else {  // another rank's row: this rank's mirror follows
+      dec_old.push_back(it.kind == KBG_KIND_ALLOCATE ? S.idle[it.node] : S.rel[it.node]);
+      if (S.has_ports)
+        dec_oldp.insert(dec_oldp.end(), S.node_ports.begin() + (size_t)it.node * S.PW,
+                        S.node_ports.begin() + (size_t)(it.node + 1) * S.PW);
+      dup = mirror_add(S, it.t, it.node, it.kind);
+    }
+    record_decision(S, it.t, it.node, it.kind, dup);
+  };
+  // On a thread of its own unless host ports or colliding pod keys make the
+  // mirror share state across nodes (used-port holders, the pod-key set).
+  std::unique_ptr<Logger> lg;
+  if (!S.has_ports && !S.has_dupkeys) lg.reset(new Logger([&](const LogItem& it) { log_one(it, nullptr); }));
+  lg_ref = &lg;
   S.owner = true;  // device_launch: own words, no all-gather
   for (;;) {
     // ---- 1. the segment's tasks from rank 0
@@ -2931,39 +3006,27 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
       from = my_from;
     }
     S.stats.resolve_ms += ms_since(tp);
-    // ---- 5. outcomes in order (every rank), cut at the first misprediction
+    // ---- 5. outcomes in order (every rank), cut at the first misprediction;
+    // the log side (decision log, gang dispatch, the other ranks' rows in
+    // this rank's mirror) goes to the logger thread when it can run beside
+    // the next batch's resolve
     int32_t cut = end;  // entries [0, cut) are final
     bool mispred = false;
     bactual.assign(n, 0);
+    std::vector<LogItem> items;
+    if (lg) items.reserve(end);
     for (int32_t i = 0; i < end; ++i) {
       const int32_t t = bt[i];
       const int32_t g = sg.row_of[i];
       const int32_t own = owner_of(g, i);
       const bool ok = own >= 0;
       if (ok && win[i] == kNone) return abort(fail(KBG_E_INVALID, "internal: owner-resolve left a task without a node"));
-      const int32_t node = ok ? (int32_t)(win[i] >> 1) : -1;
-      const int32_t kind = ok && (win[i] & 1u) ? KBG_KIND_PIPELINE : KBG_KIND_ALLOCATE;
+      LogItem it{t, ok ? (int32_t)(win[i] >> 1) : -1, ok && (win[i] & 1u) ? KBG_KIND_PIPELINE : KBG_KIND_ALLOCATE,
+                 ok, own == me, own == me && pos_dup[i], own == me ? pos_old[i] : Res{}};
       bactual[i] = ok;
-      S.stats.task_evaluations++;
-      last[S.task_job[t]] = LastEval{t, (int32_t)dec.size(), node, kind};
-      if (ok) {
-        bool dup;
-        if (own == me) {  // committed during the resolve
-          dec_old.push_back(pos_old[i]);
-          if (S.has_ports) dec_oldp.insert(dec_oldp.end(), pos_oldp.begin() + (size_t)i * S.PW,
-                                           pos_oldp.begin() + (size_t)(i + 1) * S.PW);
-          dup = pos_dup[i];
-        } else {  // another rank's row: this rank's mirror follows
-          dec_old.push_back(kind == KBG_KIND_ALLOCATE ? S.idle[node] : S.rel[node]);
-          if (S.has_ports)
-            dec_oldp.insert(dec_oldp.end(), S.node_ports.begin() + (size_t)node * S.PW,
-                            S.node_ports.begin() + (size_t)(node + 1) * S.PW);
-          dup = mirror_add(S, t, node, kind);
-        }
-        record_decision(S, t, node, kind, dup);
-      } else {
-        failed[S.task_shape[t]].store(1, std::memory_order_relaxed);
-      }
+      if (!ok) failed[S.task_shape[t]].store(1, std::memory_order_relaxed);
+      if (lg) items.push_back(it);
+      else log_one(it, pos_oldp.data() + (size_t)i * S.PW);
       if (ok != (bool)bpred[i]) {
         cut = i + 1;
         mispred = true;
@@ -2971,6 +3034,7 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
         break;
       }
     }
+    if (lg) lg->push(std::move(items));
     rollback_from(cut);
     if (rp) {
       std::vector<std::pair<int32_t, char>> v(cut);
