@@ -1901,7 +1901,7 @@ struct Pipe {
 // and the engine checkpoints: keep the predictor on another physical core of
 // the committer's last-level cache (sysfs topology), never on its SMT
 // sibling. KBG_NO_PIN=1 leaves placement to the OS.
-void pin_near(int cpu) {
+void pin_near(int cpu, int nth = 1) {
   static const bool off = getenv("KBG_NO_PIN") != nullptr;
   if (off || cpu < 0) return;
   auto read_list = [](const std::string& path) {
@@ -1930,9 +1930,11 @@ void pin_near(int cpu) {
   cpu_set_t allowed;
   if (llc.empty() || sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
   const size_t at = std::find(llc.begin(), llc.end(), cpu) - llc.begin();
-  for (size_t k = 1; k <= llc.size(); ++k) {  // the next core after the committer's
+  int seen = 0;
+  for (size_t k = 1; k <= llc.size(); ++k) {  // the nth usable core after the committer's
     const int c = llc[(at + k) % llc.size()];
     if (std::find(smt.begin(), smt.end(), c) != smt.end() || !CPU_ISSET(c, &allowed)) continue;
+    if (++seen < nth) continue;
     cpu_set_t one;
     CPU_ZERO(&one);
     CPU_SET(c, &one);
@@ -2723,8 +2725,11 @@ struct Logger {
   std::condition_variable cv;
   std::deque<std::vector<LogItem>> q;
   bool done = false;
-  explicit Logger(std::function<void(const LogItem&)> f) : fn(std::move(f)) {
-    th = std::thread([this]() { run(); });
+  explicit Logger(std::function<void(const LogItem&)> f, int committer_cpu) : fn(std::move(f)) {
+    th = std::thread([this, committer_cpu]() {
+      pin_near(committer_cpu, 2);  // not the predictor's core
+      run();
+    });
   }
   ~Logger() { join(); }
   void push(std::vector<LogItem>&& v) {
@@ -2848,8 +2853,9 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
   // The log side of a committed outcome: decision log and gang dispatch
   // (record_decision), FitError bookkeeping, and — for another rank's row —
   // this rank's mirror of it. `oldp`: host ports before an own commit.
+  int64_t logged = 0;  // task evaluations: counted apart from S.stats (the committer updates that line)
   auto log_one = [&](const LogItem& it, const uint64_t* oldp) {
-    S.stats.task_evaluations++;
+    ++logged;
     last[S.task_job[it.t]] = LastEval{it.t, (int32_t)dec.size(), it.node, it.kind};
     if (!it.ok) return;
     bool dup = it.dup;
@@ -2868,7 +2874,8 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
   // On a thread of its own unless host ports or colliding pod keys make the
   // mirror share state across nodes (used-port holders, the pod-key set).
   std::unique_ptr<Logger> lg;
-  if (!S.has_ports && !S.has_dupkeys) lg.reset(new Logger([&](const LogItem& it) { log_one(it, nullptr); }));
+  if (!S.has_ports && !S.has_dupkeys)
+    lg.reset(new Logger([&](const LogItem& it) { log_one(it, nullptr); }, sched_getcpu()));
   lg_ref = &lg;
   S.owner = true;  // device_launch: own words, no all-gather
   for (;;) {
@@ -3073,6 +3080,7 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
   S.owner = false;
   if (kbg_status st = io.sync(S); st != KBG_OK) return st;
   compute_fit_deltas(S, dec, dec_old, dec_oldp, last);
+  S.stats.task_evaluations += logged;
   if (rp && !rp->error.empty()) return fail(KBG_E_INVALID, rp->error);
   S.fin = E;
   if (pr) {
