@@ -137,6 +137,15 @@ inline void go_down(int32_t* h, int i0, int n, L less, bool go111) {
 }
 
 kbg::JobKey make_job_key(const Session& S, const Engine& E, int32_t j) {
+  if (S.job_chain_pgd) {  // the default tiers' chain (priority, gang, drf), without the loop
+    const bool ready = E.jready[j] >= S.jobs_in[j].min_available;
+    uint64_t u;
+    __builtin_memcpy(&u, &E.jshare[j], 8);
+    const uint64_t lo = ready ? (u & ~(1ull << 63)) : 0;  // fields after a non-ready gang are zero
+    kbg::JobKey k = ((kbg::JobKey)S.job_prank[j] << 1) | (ready ? 1u : 0u);
+    k = (k << 63) | lo;
+    return (k << 32) | (uint32_t)S.job_frank[j];
+  }
   kbg::JobKey k = 0;
   bool zero = false;
   for (int32_t p : S.job_chain) {
@@ -1356,6 +1365,7 @@ enum { DERIVE_OK = 0, DERIVE_REBUILD = 1 };  // REBUILD: the static classes / ma
 // when a candidate needs a class the session does not have.
 kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   *outcome = DERIVE_OK;
+  S.job_chain_pgd = S.job_chain == std::vector<int32_t>{kbg::JO_PRIORITY, kbg::JO_GANG, kbg::JO_DRF};
   const int32_t N = S.n_nodes, T = S.n_tasks;
   static const bool prof = getenv("KBG_PROFILE_OPEN") != nullptr;
   auto tl = std::chrono::steady_clock::now();

@@ -216,6 +216,7 @@ struct Session {
   bool has_drf = false, has_prop = false, has_gang = false, has_prio = false;
   bool pred_active = false;         // some tier entry "predicates" without disablePredicate
   std::vector<int32_t> job_chain;   // JobOrderPlugin in tier order (disabled entries removed)
+  bool job_chain_pgd = false;       // job_chain is exactly (priority, gang, drf): make_job_key's fast path
   bool queue_order_prop = false;
   bool task_order_prio = false;
   bool ready_gang = false;
