@@ -1,0 +1,240 @@
+"""The reference's e2e specs (test/e2e/{job,predicates,queue}.go) restated as
+multi-cycle runs on a fake cluster (tests/e2e_sim.py), each asserting what the
+spec asserts. CPU: every cycle runs on the kbref oracle, so the oracle is
+pinned to the reference's own behavioural expectations. GPU: every cycle runs
+on the MI355X path (reclaim, allocate, backfill, preempt through the C ABI)
+and is compared bit for bit with the oracle on the same snapshot."""
+import pytest
+
+from e2e_sim import CPU, Cluster, WaitTimeout
+from helpers import compare_outputs, run_oracle
+
+ONE, HALF, TWO = CPU["one"], CPU["half"], CPU["two"]
+
+
+def job(req, mn, rep, **kw):
+    return dict(req=req, min=mn, rep=rep, **kw)
+
+
+# ---------------------------------------------------------------- job.go
+# Each step below is the spec's own: create objects, then the wait helper it
+# calls (`w`: poll between cycles until the condition holds).
+def schedule_job(c, w):  # job.go:27-44
+    rep = c.size(ONE)
+    c.create_job("qj-1", [job(ONE, 2, rep)])
+    w(lambda: c.running("qj-1") >= c.min_member("qj-1"))  # waitPodGroupReady
+
+
+def schedule_multiple_jobs(c, w):  # job.go:46-78
+    rep = c.size(ONE)
+    for n in ("mqj-1", "mqj-2", "mqj-3"):
+        c.create_job(n, [job(ONE, 2, rep)])
+    for n in ("mqj-1", "mqj-2", "mqj-3"):
+        w(lambda: c.running(n) >= c.min_member(n))
+
+
+def gang_scheduling(c, w):  # job.go:80-113
+    rep = c.size(ONE) // 2 + 1
+    c.create_replicaset("rs-1", rep, ONE)  # waitReplicaSetReady: placed and Running at once here
+    c.create_job("gang-qj", [job(ONE, rep, rep)])
+    w(lambda: c.pending("gang-qj") >= c.min_member("gang-qj"))  # waitPodGroupPending
+    c.cycle_once()
+    w(lambda: c.unschedulable("gang-qj"))                         # waitPodGroupUnschedulable
+    c.delete_replicaset("rs-1")
+    w(lambda: c.running("gang-qj") >= c.min_member("gang-qj"))
+
+
+def gang_full_occupied(c, w):  # job.go:115-143
+    rep = c.size(ONE)
+    c.create_job("gang-fq-qj1", [job(ONE, rep, rep)])
+    w(lambda: c.running("gang-fq-qj1") >= rep)
+    c.create_job("gang-fq-qj2", [job(ONE, rep, rep)])
+    c.cycle_once()
+    w(lambda: c.pending("gang-fq-qj2") >= rep)
+    w(lambda: c.running("gang-fq-qj1") >= rep)
+    c.settle()  # and it stays so: the full job is never preempted (gang: ready - 1 < MinAvailable)
+    assert c.running("gang-fq-qj1") >= rep and c.running("gang-fq-qj2") == 0
+
+
+def preemption(c, w):  # job.go:145-174
+    rep = c.size(ONE)
+    c.create_job("preemptee-qj", [job(ONE, 1, rep)])
+    w(lambda: c.running("preemptee-qj") >= rep)
+    c.create_job("preemptor-qj", [job(ONE, 1, rep)])
+    w(lambda: c.running("preemptee-qj") >= rep // 2)
+    w(lambda: c.running("preemptor-qj") >= rep // 2)
+
+
+def multiple_preemption(c, w):  # job.go:176-213
+    rep = c.size(ONE)
+    c.create_job("preemptee-qj", [job(ONE, 1, rep)])
+    w(lambda: c.running("preemptee-qj") >= rep)
+    c.create_job("preemptor-qj1", [job(ONE, 1, rep)])
+    c.create_job("preemptor-qj2", [job(ONE, 1, rep)])
+    for n in ("preemptee-qj", "preemptor-qj1", "preemptor-qj2"):
+        w(lambda: c.running(n) >= rep // 3)
+
+
+def best_effort(c, w):  # job.go:215-242
+    rep = c.size(ONE)
+    c.create_job("test", [job(ONE, 2, rep), job(None, 2, rep // 2)])
+    w(lambda: c.running("test") >= c.min_member("test"))
+
+
+def statement(c, w):  # job.go:244-278
+    rep = c.size(ONE)
+    c.create_job("st-qj-1", [job(ONE, rep, rep)])
+    w(lambda: c.running("st-qj-1") >= rep)
+    since = c.cycles
+    c.create_job("st-qj-2", [job(ONE, rep, rep)])
+    c.cycle_once()
+    w(lambda: c.unschedulable("st-qj-2"))
+    assert not c.evicted("st-qj-1", since)  # "No preemption event"
+    c.settle()  # preempt pipelines st-qj-2 onto st-qj-1's nodes, the job never gets ready: discarded
+    assert not c.evicted("st-qj-1", since)
+
+
+def task_priority(c, w):  # job.go:280-318
+    rep = c.size(ONE)
+    c.create_replicaset("rs-1", rep // 2, ONE)
+    c.create_job("multi-pod-job", [job(ONE, rep // 2 - 1, rep, pri="worker-pri"),
+                                   job(ONE, 1, 1, pri="master-pri")])
+    w(lambda: c.running("multi-pod-job", "master-pri") >= 1 and
+      c.running("multi-pod-job", "worker-pri") >= rep // 2 - 1)  # waitTasksReadyEx
+
+
+def fit_unassigned(c, w):  # job.go:320-367
+    rep = c.size(ONE)
+    c.create_replicaset("rs-1", rep - 1, ONE)
+    c.create_job("multi-task-diff-resource-job", [job(TWO, 1, 1, pri="master-pri"),
+                                                  job(HALF, 1, 1, pri="worker-pri")], min_member=1)
+    w(lambda: c.pending("multi-task-diff-resource-job") >= 1)
+    w(lambda: c.running("multi-task-diff-resource-job") >= 1)  # "task_1 has been scheduled"
+    c.settle()  # the half-CPU worker runs, the two-CPU master fits nowhere
+    assert c.running("multi-task-diff-resource-job", "worker-pri") == 1
+    assert c.running("multi-task-diff-resource-job", "master-pri") == 0
+
+
+# ---------------------------------------------------------------- predicates.go
+def node_affinity(c, w):  # predicates.go:29-76
+    name, rep = c.compute_node(ONE)
+    assert rep != 0
+    aff = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
+        {"matchFields": [{"key": "metadata.name", "operator": "In", "values": [name]}]}]}}}
+    c.create_job("na-job", [job(ONE, 1, 1, affinity=aff)])
+    w(lambda: c.running("na-job") >= 1)
+    assert c.nodes_of("na-job") == [name]
+
+
+def hostport(c, w):  # predicates.go:78-104
+    nn = c.node_number()
+    c.create_job("hp-job", [job(ONE, nn, nn * 2, hostport=28080)])
+    w(lambda: c.running("hp-job") >= nn)
+    w(lambda: c.pending("hp-job") >= nn)
+    c.settle()
+    assert c.running("hp-job") == nn and len(set(c.nodes_of("hp-job"))) == nn  # one per node
+
+
+def pod_affinity(c, w):  # predicates.go:106-153
+    _, rep = c.compute_node(ONE)
+    assert rep != 0
+    labels = {"foo": "bar"}
+    aff = {"podAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"labelSelector": {"matchLabels": labels}, "topologyKey": "kubernetes.io/hostname"}]}}
+    c.create_job("pa-job", [job(ONE, rep, rep, affinity=aff, labels=labels)])
+    w(lambda: c.running("pa-job") >= rep)
+    assert len(set(c.nodes_of("pa-job"))) == 1  # all pods on the same node
+
+
+def taints(c, w):  # predicates.go:155-191
+    t = [{"key": "test-taint-key", "value": "test-taint-val", "effect": "NoSchedule"}]
+    c.taint_all(t)
+    c.create_job("tt-job", [job(ONE, 1, 1)])
+    w(lambda: c.pending("tt-job") >= 1)
+    c.settle()
+    assert c.running("tt-job") == 0
+    c.untaint_all()
+    w(lambda: c.running("tt-job") >= 1)
+
+
+# ---------------------------------------------------------------- queue.go
+def reclaim(c, w):  # queue.go:27-70
+    rep = c.size(ONE)
+    c.create_job("q1-qj-1", [job(ONE, 1, rep)], queue="q1")
+    w(lambda: c.running("q1-qj-1") >= 1)
+    expected = rep // 2
+    assert expected > 1, "expected replica is too small"
+    expected -= 1  # "Reduce one pod to tolerate decimal fraction."
+    c.create_job("q2-qj-2", [job(ONE, 1, rep)], queue="q2")
+    w(lambda: c.running("q2-qj-2") >= expected)
+    w(lambda: c.running("q1-qj-1") >= expected)
+
+
+SCENARIOS = {f.__name__: f for f in (schedule_job, schedule_multiple_jobs, gang_scheduling, gang_full_occupied,
+                                     preemption, multiple_preemption, best_effort, statement, task_priority,
+                                     fit_unassigned, node_affinity, hostport, pod_affinity, taints, reclaim)}
+# cluster shapes: the dind workers' CPU (the host's), a kube-system pod on the first
+SHAPES = {"3x4cpu": dict(worker_cpu=(4000, 4000, 4000), system_cpu=(250, 0, 0)),
+          "3x8cpu": dict(worker_cpu=(8000, 8000, 8000), system_cpu=(100, 100, 100))}
+
+
+def oracle_runner(fx):
+    return run_oracle(fx)
+
+
+def device_runner(fx):
+    from kbgpu.fixture import run_fixture
+    ref = run_oracle(fx)
+    got, ssn = run_fixture(fx, {"device": 0})
+    if ssn is not None:
+        ssn.close()
+    compare_outputs(ref, got)
+    return got
+
+
+# Spec conditions this fake cluster does not reach within the e2e's minute of
+# polling (60 one-second cycles), and why. Under the conf's tiers gang's tier
+# alone answers Preemptable / Reclaimable (session_plugins.go:100-140,
+# gang.go:104-127: any victim whose job keeps ready - 1 >= MinAvailable), and
+# preempt's second phase lets a job's Pending replacement pods evict their own
+# Running siblings (preempt.go:116-140, `preemptor.Job == task.Job`); together
+# they make the cluster churn in a fixed cycle (evict all but MinAvailable,
+# pipeline, bind, evict again) instead of settling at the fair split. The
+# oracle and the device still agree bit for bit on every cycle of the churn.
+KNOWN_MISSES = {
+    ("reclaim", "3x4cpu"): "q1 and q2 reclaim from each other and self-preempt; never both >= rep/2 - 1",
+    ("reclaim", "3x8cpu"): "q1 and q2 reclaim from each other and self-preempt; never both >= rep/2 - 1",
+    ("multiple_preemption", "3x8cpu"): "period-3 churn peaks at 7/7/6 of 21 slots (spec: >= 7 each)",
+}
+
+
+def run_scenario(name, shape, runner):
+    """Runs the spec; a miss listed in KNOWN_MISSES returns its reason (and a
+    listed miss that starts passing fails, so the list stays exact)."""
+    c = Cluster(**SHAPES[shape], runner=runner)
+    try:
+        SCENARIOS[name](c, c.wait)
+    except WaitTimeout:
+        if (name, shape) in KNOWN_MISSES:
+            return KNOWN_MISSES[(name, shape)]
+        raise
+    assert (name, shape) not in KNOWN_MISSES, "a known miss now passes: update KNOWN_MISSES"
+    return None
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_e2e_spec_oracle(name, shape):
+    miss = run_scenario(name, shape, oracle_runner)
+    if miss:
+        pytest.xfail(miss)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_e2e_spec_device(name, shape):
+    # every cycle is compared with the oracle inside device_runner
+    miss = run_scenario(name, shape, device_runner)
+    if miss:
+        pytest.xfail(miss)
