@@ -439,6 +439,8 @@ void free_device(Session& S) {
       }
     g = kbg::Stage{};
   }
+  for (char* b : S.up_pool) (void)hipHostFree(b);
+  S.up_pool.clear();
   if (S.h_deltas) (void)hipHostFree(S.h_deltas);
   if (S.h_mdeltas) (void)hipHostFree(S.h_mdeltas);
   S.h_mdeltas = nullptr;
@@ -514,13 +516,19 @@ kbg_status upload_nodes(Session& S) {
 // upload runs after this batch's select has read them); only the host staging
 // is per stage. `base`: the newest resolution whose node deltas are already
 // enqueued, i.e. what this scan sees.
+struct Trace;
+thread_local Trace* t_trace = nullptr;  // the committer's KBG_TRACE timeline, if on
+void trace_add(const char* what, int64_t v = 0);
+
 kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
+  trace_add("l.begin", G);
   const uint32_t total = sg.h_capoff[G];
   const int32_t Gp = kbg::kbg_pad_rows(G);  // Grouper::build padded the rows
   const size_t up_bytes = (size_t)Gp * sizeof(kbg::TaskRec) + (size_t)(G + 1) * 4;
   const kbg::TaskRec* d_tasks = (const kbg::TaskRec*)S.d_up;
   const uint32_t* d_capoff = (const uint32_t*)(S.d_up + (size_t)Gp * sizeof(kbg::TaskRec));
   HIP_TRY(hipMemcpyAsync(S.d_up, sg.h_up, up_bytes, hipMemcpyHostToDevice, S.stream));
+  trace_add("l.h2d", (int64_t)up_bytes);
   // this process scans its shard (or every shard when they are all local)
   kbg::ScanGeom geo{S.n_nodes, S.W, S.Wl, 0, S.R * S.Wl, S.tab_lo};
   const size_t slot_words = (size_t)2 * G * kbg::kbg_slot_words(S.Wl);
@@ -532,6 +540,7 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   }
   HIP_TRY(kbg::launch_scan(S.d_nodes, geo, S.d_class_mask, d_tasks, G, S.pred_active ? 1 : 0, S.int_mode ? 1 : 0, out,
                            S.stream, sg.ev[0], sg.ev[1]));
+  trace_add("l.scan");
   if (S.comm && !S.owner) {  // in-place all-gather: every rank receives every shard's slot, in rank (= node) order
     HIP_TRY(hipEventRecord(sg.ev[4], S.stream));
     const ncclResult_t nr = ncclAllGather(out, S.d_bits, slot_words, ncclUint64, S.comm->nccl, S.stream);
@@ -543,6 +552,7 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   const int32_t w_hi = S.owner ? std::min(S.W, (S.shard + 1) * S.Wl) : S.W;
   HIP_TRY(kbg::launch_select(S.d_bits, w_lo, w_hi, S.Wl, G, d_capoff, S.d_down + G, S.d_down, S.stream, sg.ev[2],
                              sg.ev[3]));
+  trace_add("l.select");
   size_t down = (size_t)G + total;
   if (S.owner && S.comm) {  // owner-resolve: the rows' availability over the ranks, in the same round trip
     uint32_t* d_avail = S.d_down + down;
@@ -552,7 +562,9 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
     down += (size_t)G;
   }
   HIP_TRY(hipMemcpyAsync(sg.h_down, S.d_down, down * 4, hipMemcpyDeviceToHost, S.stream));
+  trace_add("l.d2h", (int64_t)down * 4);
   HIP_TRY(hipEventRecord(sg.ev[6], S.stream));
+  trace_add("l.event");
   sg.G = G;
   sg.base = base;
   sg.inflight = true;
@@ -1786,6 +1798,7 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   S.stage_pending = false;
   if ((st = alloc_soa(S, &S.d_nodes)) || (st = alloc_soa(S, &S.d_nodes0))) return st;
   const size_t up_cap = (size_t)kbg::kbg_pad_rows(S.K) * sizeof(kbg::TaskRec) + ((size_t)S.K + 1) * 4;
+  S.up_cap = up_cap;
   const size_t down_cap = 2 * (size_t)S.K + (size_t)S.cand_cap;  // counts, candidates, owner-resolve availability
   if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) || (st = dalloc(S, &S.d_up, up_cap)) ||
       (st = dalloc(S, &S.d_bits, (size_t)S.R * 2 * S.K * kbg::kbg_slot_words(S.Wl))) ||
@@ -1886,11 +1899,44 @@ kbg_status open_session(Session& S, const kbg_snapshot* snap, const kbg_options*
 // the committer bumps the epoch and hands the predictor the batch's
 // checkpoint plus the actual outcomes up to the cut; the predictor restores,
 // replays them and continues; batches of an older epoch are dropped.
+// Opt-in timeline of an allocate cycle (KBG_TRACE=1): per thread, (µs since
+// the cycle start, event, value), printed to stderr when the cycle ends.
+struct Trace {
+  using clk = std::chrono::steady_clock;
+  bool on = false;
+  clk::time_point t0;
+  std::vector<std::tuple<double, const char*, int64_t>> ev;
+  void start(clk::time_point t) {
+    on = getenv("KBG_TRACE") != nullptr;
+    t0 = t;
+    if (on) ev.reserve(4096);
+  }
+  void add(const char* what, int64_t v = 0) {
+    if (on) ev.emplace_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count(), what, v);
+  }
+};
+void trace_add(const char* what, int64_t v) {
+  if (t_trace) t_trace->add(what, v);
+}
+void print_traces(const Trace& a, const Trace& b) {
+  if (!a.on) return;
+  std::vector<std::tuple<double, const char*, int64_t, char>> all;
+  for (auto& [t, w, v] : a.ev) all.emplace_back(t, w, v, 'C');
+  for (auto& [t, w, v] : b.ev) all.emplace_back(t, w, v, 'P');
+  std::sort(all.begin(), all.end(), [](const auto& x, const auto& y) { return std::get<0>(x) < std::get<0>(y); });
+  for (auto& [t, w, v, who] : all) fprintf(stderr, "[kbg trace] %9.1f %c %-10s %lld\n", t, who, w, (long long)v);
+}
+
 struct Batch {
   std::vector<int32_t> bt;
   std::vector<char> bpred;
   Engine ckpt;
   int64_t epoch = 0;
+  // rows built ahead by the builder thread (G >= 0) into a pinned buffer
+  // (st.h_up) that launch swaps with the stage's: no copy, and the buffer the
+  // stage gives back has been read by its last upload (the stage was waited)
+  kbg::Stage st;
+  int32_t G = -1;
 };
 
 struct Pipe {
@@ -1904,8 +1950,20 @@ struct Pipe {
   std::vector<int32_t> rb_tasks;
   std::vector<char> rb_actual;
   bool stop = false;
+  std::atomic<bool> hungry{false};  // the committer is blocked on an empty queue: emit what is predicted
+  std::deque<Batch*> raw;      // predicted, waiting for the builder (allocate_cycle)
+  bool building = false;       // the builder holds a batch
   static constexpr size_t kDepth = 3;
 };
+// Smallest batch the predictor hands over early to a waiting committer (the
+// first batch of an epoch, and near the end of the cycle); KBG_MIN_EMIT overrides.
+int32_t min_emit() {
+  static const int32_t v = [] {
+    const char* e = getenv("KBG_MIN_EMIT");
+    return e ? std::max(1, atoi(e)) : 512;
+  }();
+  return v;
+}
 
 // The predictor and the committer exchange batches, the failed-shape flags
 // and the engine checkpoints: keep the predictor on another physical core of
@@ -2154,12 +2212,57 @@ struct Predictor {
   int64_t replayed = 0;
   std::string error;
   EngineProfile prof;
-  std::thread th;
+  Trace tr;
+  std::thread th, bth;
+  bool builder = false;       // a builder thread turns predicted batches into device rows (allocate_cycle)
+  std::vector<Batch*> all;    // every batch of this predictor (freed by finish)
   Predictor(Session& s, Engine& e, std::atomic<uint8_t>* f) : S(s), E(e), failed(f) {
     prof.on = getenv("KBG_PROFILE_ENGINE") != nullptr;
   }
-  void start(int committer_cpu) {
+  void start(int committer_cpu, bool with_builder = false) {
+    builder = with_builder;
     th = std::thread([this, committer_cpu]() { run(committer_cpu); });
+    if (builder) bth = std::thread([this, committer_cpu]() { build_run(committer_cpu); });
+  }
+  // Builder: Grouper::build of each predicted batch into the batch's own
+  // pinned row buffer, so the committer only swaps buffers at launch.
+  void build_run(int committer_cpu) {
+    pin_near(committer_cpu, 3);
+    Grouper g(S);
+    for (;;) {
+      Batch* b;
+      {
+        std::unique_lock<std::mutex> lk(P.mu);
+        P.cv.wait(lk, [&] { return P.stop || !P.raw.empty(); });
+        if (P.stop) return;
+        b = P.raw.front();
+        P.raw.pop_front();
+        P.building = true;
+      }
+      b->G = 0;
+      if (!b->bt.empty()) {
+        if (!b->st.h_up) {
+          if (!S.up_pool.empty()) {  // only this thread takes from the pool during a cycle
+            b->st.h_up = S.up_pool.back();
+            S.up_pool.pop_back();
+          } else if (hipHostMalloc((void**)&b->st.h_up, S.up_cap, hipHostMallocDefault) != hipSuccess) {
+            b->st.h_up = nullptr;
+            std::lock_guard<std::mutex> lk(P.mu);
+            error = "hipHostMalloc of a batch row buffer failed";
+            P.stop = true;
+            P.building = false;
+            P.ready.push_back(nullptr);
+            P.cv.notify_all();
+            return;
+          }
+        }
+        b->G = g.build(b->st, b->bt.data(), (int32_t)b->bt.size());
+      }
+      std::lock_guard<std::mutex> lk(P.mu);
+      P.building = false;
+      P.ready.push_back(b);
+      P.cv.notify_all();
+    }
   }
   void run(int committer_cpu) {
     auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
@@ -2171,7 +2274,9 @@ struct Predictor {
       int64_t my_epoch;
       {
         std::unique_lock<std::mutex> lk(P.mu);
-        P.cv.wait(lk, [&] { return P.stop || P.rollback || (!exhausted && P.ready.size() < Pipe::kDepth); });
+        P.cv.wait(lk, [&] {
+          return P.stop || P.rollback || (!exhausted && P.ready.size() + P.raw.size() < Pipe::kDepth);
+        });
         if (P.stop) return;
         if (P.rollback) {
           const auto tp = clk::now();
@@ -2198,12 +2303,17 @@ struct Predictor {
           P.free.pop_back();
         }
       }
-      if (!b) b = new Batch();
+      if (!b) {
+        b = new Batch();
+        std::lock_guard<std::mutex> lk(P.mu);
+        all.push_back(b);
+      }
       const auto tp = clk::now();
       b->ckpt = E;
       b->epoch = my_epoch;
       b->bt.clear();
       b->bpred.clear();
+      const size_t emit_at = (size_t)min_emit();
       while ((int32_t)b->bt.size() < S.K) {
         const int32_t t = ops.next_task();
         if (t < 0) break;
@@ -2211,11 +2321,17 @@ struct Predictor {
         b->bt.push_back(t);
         b->bpred.push_back(p);
         ops.apply(t, p);
+        // a committer with nothing to do takes a short batch now
+        if ((b->bt.size() & 63) == 0 && b->bt.size() >= emit_at && P.hungry.load(std::memory_order_relaxed)) {
+          P.hungry.store(false, std::memory_order_relaxed);  // one early batch per wait
+          break;
+        }
       }
       engine_ms += ms_since(tp);
+      tr.add("emit", (int64_t)b->bt.size());
       if (b->bt.empty()) exhausted = true;  // the empty batch marks the end of this epoch
       std::lock_guard<std::mutex> lk(P.mu);
-      P.ready.push_back(b);
+      (builder ? P.raw : P.ready).push_back(b);
       P.cv.notify_all();
     }
   }
@@ -2228,7 +2344,12 @@ struct Predictor {
       return nullptr;
     }
     *none = false;
-    P.cv.wait(lk, [&] { return !P.ready.empty(); });
+    if (P.ready.empty()) {
+      // nothing predicted on its way: the predictor hands over what it has
+      if (P.raw.empty() && !P.building) P.hungry.store(true, std::memory_order_relaxed);
+      P.cv.wait(lk, [&] { return !P.ready.empty(); });
+      P.hungry.store(false, std::memory_order_relaxed);
+    }
     Batch* b = P.ready.front();
     P.ready.pop_front();
     P.cv.notify_all();
@@ -2260,11 +2381,67 @@ struct Predictor {
       P.cv.notify_all();
     }
     if (th.joinable()) th.join();
+    if (bth.joinable()) bth.join();
     std::lock_guard<std::mutex> lk(P.mu);
-    for (Batch* b : P.ready) delete b;
-    for (Batch* b : P.free) delete b;
+    for (Batch* b : all) {  // row buffers go back to the session's pool
+      if (b->st.h_up) S.up_pool.push_back(b->st.h_up);
+      delete b;
+    }
+    all.clear();
     P.ready.clear();
+    P.raw.clear();
     P.free.clear();
+  }
+};
+
+// One committed outcome of a resolve walk (single-rank or owner-resolve), for the log side.
+struct LogItem {
+  int32_t t, node, kind;
+  bool ok, own, dup;
+  Res old;  // own commit: the Idle / Releasing row before it
+};
+
+// The log side of a resolve walk on a thread of its own: batches of committed
+// outcomes in commit order.
+struct Logger {
+  std::function<void(const LogItem&)> fn;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::vector<LogItem>> q;
+  bool done = false;
+  explicit Logger(std::function<void(const LogItem&)> f, int committer_cpu) : fn(std::move(f)) {
+    th = std::thread([this, committer_cpu]() {
+      pin_near(committer_cpu, 2);  // not the predictor's core (the builder takes the third)
+      run();
+    });
+  }
+  ~Logger() { join(); }
+  void push(std::vector<LogItem>&& v) {
+    std::lock_guard<std::mutex> lk(mu);
+    q.push_back(std::move(v));
+    cv.notify_all();
+  }
+  void join() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      done = true;
+      cv.notify_all();
+    }
+    if (th.joinable()) th.join();
+  }
+  void run() {
+    for (;;) {
+      std::vector<LogItem> v;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return done || !q.empty(); });
+        if (q.empty()) return;
+        v = std::move(q.front());
+        q.pop_front();
+      }
+      for (const LogItem& it : v) fn(it);
+    }
   }
 };
 
@@ -2293,12 +2470,33 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   kbg_status result = KBG_OK;
   Grouper grouper(S);
   Resolver rs{S, mark};
+  // The log side of the walk (decision log, gang dispatch, FitError
+  // bookkeeping) on a thread of its own, unless host ports or colliding pod
+  // keys need the pre-commit port rows (then inline, below).
+  auto log_one = [&](const LogItem& it) {
+    last[S.task_job[it.t]] = LastEval{it.t, (int32_t)dec.size(), it.node, it.kind};
+    if (!it.ok) return;
+    dec_old.push_back(it.old);
+    record_decision(S, it.t, it.node, it.kind, it.dup);
+  };
+  static const bool no_logger = getenv("KBG_NO_LOGGER") != nullptr;
+  std::unique_ptr<Logger> lg;
+  if (!S.has_ports && !S.has_dupkeys && !no_logger) lg.reset(new Logger(log_one, sched_getcpu()));
+  std::vector<LogItem> items;
 
   // ------------------------------------------------------------ predictor
   Engine E = first ? S.init : live_engine(S);
   Predictor pr(S, E, failed.get());
   EngineProfile& eprof = pr.prof;
-  pr.start(sched_getcpu());
+  Trace ctr;
+  ctr.start(t0);
+  pr.tr.start(t0);
+  struct TraceHook {  // cleared on every return path
+    explicit TraceHook(Trace* t) { t_trace = t; }
+    ~TraceHook() { t_trace = nullptr; }
+  } trace_hook(ctr.on ? &ctr : nullptr);
+  static const bool no_builder = getenv("KBG_NO_BUILDER") != nullptr;
+  pr.start(sched_getcpu(), !no_builder);
   auto take = [&](bool block, bool* none) { return pr.take(block, none); };
   auto recycle = [&](Batch* b) { pr.recycle(b); };
   auto finish = [&]() { pr.finish(); };
@@ -2329,8 +2527,22 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
   };
   auto launch = [&](kbg::Stage& sg, Batch* b) -> kbg_status {
-    const int32_t G = grouper.build(sg, b->bt.data(), (int32_t)b->bt.size());
-    return device_launch(S, sg, G, pushed);
+    int32_t G;
+    if (b->G >= 0) {  // built by the builder thread: take its row buffer and row maps
+      std::swap(sg.h_up, b->st.h_up);
+      sg.h_tasks = (kbg::TaskRec*)sg.h_up;
+      sg.h_capoff = b->st.h_capoff;  // inside the buffer sg now holds
+      sg.row_of.swap(b->st.row_of);
+      sg.row_shape.swap(b->st.row_shape);
+      sg.row_ext.swap(b->st.row_ext);
+      G = b->G;
+      b->G = -1;
+    } else {
+      G = grouper.build(sg, b->bt.data(), (int32_t)b->bt.size());
+    }
+    const kbg_status st = device_launch(S, sg, G, pushed);
+    ctr.add("launch", G);
+    return st;
   };
   auto abort = [&](kbg_status st) {
     for (kbg::Stage& g : S.stages) (void)device_drop(S, g);
@@ -2342,7 +2554,9 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   const bool rprof = getenv("KBG_PROFILE_RESOLVE") != nullptr;
   uint64_t rcyc[4] = {0, 0, 0, 0};
   int si = 0;
+  ctr.add("take");
   Batch* cur = next_batch(true);
+  ctr.add("took");
   if (!cur) {
     finish();
     return fail(KBG_E_INVALID, pr.error);
@@ -2359,7 +2573,9 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     kbg::Stage& other = S.stages[si ^ 1];
     S.stats.batches++;
     auto tp = clk::now();
+    ctr.add("wait");
     kbg_status st = device_wait(S, *sg);
+    ctr.add("waited");
     if (st != KBG_OK) return abort(st);
     // the next batch's scan overlaps this batch's resolve when it is ready
     Batch* nxt = next_batch(false);
@@ -2382,8 +2598,17 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     int32_t rstamp = stamp;
     const uint64_t cl0 = rprof ? cycles() : 0;
     const int32_t nb = (int32_t)bt.size();
+    ctr.add("resolve", nb);
     for (int32_t i = 0; i < nb; ++i) {
       const int32_t t = bt[i];
+      if ((i & 1023) == 1023 && !nxt && !pred_failed) {
+        // the predictor's next batch, if it is ready now, scans while this one resolves
+        nxt = next_batch(false);
+        if (nxt && !nxt->bt.empty()) {
+          if ((st = launch(other, nxt)) != KBG_OK) return abort(st);
+          S.stats.overlapped++;
+        }
+      }
       if (i + 8 < nb) {  // task-indexed rows of the tasks ahead (batch order is not index order)
         const int32_t t8 = bt[i + 8];
         __builtin_prefetch(&S.treq[t8]);
@@ -2426,10 +2651,8 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       const bool ok = node >= 0;
       bactual[i] = ok;
       S.stats.task_evaluations++;
-      const int32_t j = S.task_job[t];
-      last[j] = LastEval{t, (int32_t)dec.size(), node, kind};
       if (ok) {
-        dec_old.push_back(kind == KBG_KIND_ALLOCATE ? S.idle[node] : S.rel[node]);
+        const Res old = kind == KBG_KIND_ALLOCATE ? S.idle[node] : S.rel[node];
         if (S.has_ports)
           dec_oldp.insert(dec_oldp.end(), S.node_ports.begin() + (size_t)node * S.PW,
                           S.node_ports.begin() + (size_t)(node + 1) * S.PW);
@@ -2440,13 +2663,18 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
           touched.push_back(node);
         }
         const uint64_t c2 = rprof ? cycles() : 0;
-        record_decision(S, t, node, kind, dup);
+        const LogItem it{t, node, kind, true, true, dup, old};
+        if (lg) items.push_back(it);
+        else log_one(it);
         if (rprof) {
           rcyc[1] += c2 - c1;
           rcyc[2] += cycles() - c2;
         }
       } else {
         failed[S.task_shape[t]].store(1, std::memory_order_relaxed);
+        const LogItem it{t, -1, 0, false, true, false, Res{}};
+        if (lg) items.push_back(it);
+        else log_one(it);
       }
       if (ok != (bool)cur->bpred[i]) {
         cut = i + 1;
@@ -2469,6 +2697,13 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       }
     }
     if (rprof) rcyc[3] += cycles() - cl0;
+    if (lg && !items.empty()) {
+      lg->push(std::move(items));
+      items = std::vector<LogItem>();
+      items.reserve(bt.size());
+    }
+    ctr.add("resolved");
+    if (pred_failed) return abort(fail(KBG_E_INVALID, pr.error));  // seen by the look-ahead above
     S.stats.resolve_ms += ms_since(tp);
     tp = clk::now();
     if ((st = push_deltas(S, touched)) != KBG_OK) return abort(st);
@@ -2496,7 +2731,9 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
     recycle(cur);
     if (!nxt) {  // the predictor was behind: take its next batch now and scan it
+      ctr.add("take");
       nxt = next_batch(true);
+      ctr.add("took");
       if (!nxt) return abort(fail(KBG_E_INVALID, pr.error));
       if (!nxt->bt.empty()) {
         tp = clk::now();
@@ -2516,6 +2753,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
   }
   finish();
+  if (lg) lg->join();  // the decision log and FitError records are complete
   HIP_TRY(hipStreamSynchronize(S.stream));  // last delta write-back
   compute_fit_deltas(S, dec, dec_old, dec_oldp, last);
   if (S.has_aff && getenv("KBG_PROFILE_AFF"))
@@ -2538,6 +2776,8 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
             (double)eprof.jtop / eprof.steps, (double)eprof.qpush / eprof.steps, pr.engine_ms);
   S.allocated = true;
   S.stats.allocate_ms = ms_since(t0);
+  ctr.add("end");
+  print_traces(ctr, pr.tr);
   return copy_log(S, out, cap, n_out, result);
 }
 
@@ -2715,57 +2955,6 @@ struct Replayer {
         }
         ops.apply(t, ok);
       }
-    }
-  }
-};
-
-// One committed outcome of the owner-resolve walk, for the log side.
-struct LogItem {
-  int32_t t, node, kind;
-  bool ok, own, dup;
-  Res old;  // own commit: the Idle / Releasing row before it
-};
-
-// The log side of the owner-resolve walk on a thread of its own: batches of
-// committed outcomes in commit order.
-struct Logger {
-  std::function<void(const LogItem&)> fn;
-  std::thread th;
-  std::mutex mu;
-  std::condition_variable cv;
-  std::deque<std::vector<LogItem>> q;
-  bool done = false;
-  explicit Logger(std::function<void(const LogItem&)> f, int committer_cpu) : fn(std::move(f)) {
-    th = std::thread([this, committer_cpu]() {
-      pin_near(committer_cpu, 2);  // not the predictor's core
-      run();
-    });
-  }
-  ~Logger() { join(); }
-  void push(std::vector<LogItem>&& v) {
-    std::lock_guard<std::mutex> lk(mu);
-    q.push_back(std::move(v));
-    cv.notify_all();
-  }
-  void join() {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      done = true;
-      cv.notify_all();
-    }
-    if (th.joinable()) th.join();
-  }
-  void run() {
-    for (;;) {
-      std::vector<LogItem> v;
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return done || !q.empty(); });
-        if (q.empty()) return;
-        v = std::move(q.front());
-        q.pop_front();
-      }
-      for (const LogItem& it : v) fn(it);
     }
   }
 };

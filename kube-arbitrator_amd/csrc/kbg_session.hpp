@@ -392,6 +392,8 @@ struct Session {
   char* d_up = nullptr;           // rows + capoff of the batch being scanned (stream-ordered reuse)
   uint32_t* d_down = nullptr;     // counts + candidates of the batch being selected
   Stage stages[2];                // host staging of two batches in flight
+  size_t up_cap = 0;              // bytes of one pinned row buffer (Stage::h_up)
+  std::vector<char*> up_pool;     // spare pinned row buffers: the allocate builder's batches borrow them
   int32_t res_stamp = 0;          // resolution stamps: monotone over the session (mark / mwmark compare)
   NodeDelta* d_deltas = nullptr;
   NodeDelta* h_deltas = nullptr; // pinned
