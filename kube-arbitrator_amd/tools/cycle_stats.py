@@ -18,6 +18,8 @@ def main():
         torch.cuda.set_device(0)
         torch.cuda.synchronize()
     from kbgpu import _abi, synth
+    if os.environ.get("KBG_LIB"):  # A/B of library builds
+        _abi.LIB_PATH = os.path.abspath(os.environ["KBG_LIB"])
     from kbgpu.cache import cache_from_fixture
     from kbgpu.fixture import fixture_tiers
     from kbgpu.framework import open_session
