@@ -26,10 +26,13 @@
 //
 // Parity pinning: the reference's own tests are restated as fixtures under
 // tests/golden/ref_* (allocate_test.go:140-300 cases 1-2, node_info_test.go,
-// job_info_test.go). Those pin the data model and the drf/proportion/queue
-// path. The predicate truth tables, gang and priority paths are pinned only
-// by hand-derived KATs (tests/golden/kat_*): for them parity is
-// "restated, not executed" because no Go toolchain exists here.
+// job_info_test.go, cache_test.go). Those pin the data model and the
+// drf/proportion/queue path. The predicate truth tables, gang and priority
+// paths are pinned by hand-derived KATs (tests/golden/kat_*) and by the
+// reference's e2e specs (test/e2e/{job,predicates,queue}.go) restated as
+// multi-cycle fake-cluster runs whose conditions the oracle must reach
+// (tests/e2e_sim.py, tests/test_e2e_scenarios.py): "restated, not executed",
+// because no Go toolchain exists here.
 //
 // Go map iteration order (random in the reference) is replaced by insertion
 // order everywhere; SURVEY F4 makes that order an input of both sides.
