@@ -1,0 +1,53 @@
+"""Builds profiles/pmc_scan.json (what bench.py reads for its PMC-based
+figures) from the per-config summaries of profiles/summarize_pmc.py:
+
+  python profiles/make_pmc_scan.py profiles/r02   # reads pmc_c3.json, pmc_c4.json, pmc_c5.json
+
+C3 (5k nodes) gives the scan kernel in full-scan mode (kbg_scan_kernel<.., 64>,
+batches > 1024 rows) and grouped mode (<.., 16>); C5 the victim kernel; other
+node counts (C4) go under by_nodes."""
+import json
+import os
+import sys
+
+FIELDS = ("avg_ns", "launches", "hbm_bytes_per_launch", "hbm_write_bytes_per_launch", "l2_hit_rate",
+          "valu_insts_per_launch")
+
+
+def section(k):
+    out = {f: k.get(f) for f in FIELDS}
+    out["hbm_read_bytes_per_launch_corrected"] = k.get("hbm_read_bytes_per_launch")
+    out["waves_per_launch"] = k.get("counters_per_launch", {}).get("SQ_WAVES")
+    return out
+
+
+def scan_modes(s):
+    ks = s["kernels"]
+    return {"full_scan": section(ks["kbg_scan_kernel<true, 64>"]) if "kbg_scan_kernel<true, 64>" in ks else None,
+            "grouped": section(ks["kbg_scan_kernel<true, 16>"]) if "kbg_scan_kernel<true, 16>" in ks else None}
+
+
+def main():
+    d = sys.argv[1]
+    rel = os.path.relpath(d, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    load = lambda c: json.load(open(os.path.join(d, f"pmc_c{c}.json"))) if os.path.exists(
+        os.path.join(d, f"pmc_c{c}.json")) else None
+    c3, c4, c5 = load(3), load(4), load(5)
+    out = {"kernel": "kbg_scan_kernel", "n_nodes": 5000}
+    out.update(scan_modes(c3))
+    if c5 and "kbg_victim_kernel" in c5["kernels"]:
+        out["victim"] = dict(section(c5["kernels"]["kbg_victim_kernel"]), kernel="kbg_victim_kernel", n_nodes=10000)
+    out["source"] = (f"{rel}/pmc_c3.json, pmc_c5.json (profiles/summarize_pmc.py over gpurun_pmc.sh): rocprofv3 "
+                     "--kernel-trace --stats, then separate --pmc passes (FETCH_SIZE / WRITE_SIZE / "
+                     "TCC_HIT_sum+TCC_MISS_sum / SQ_INSTS_VALU,SQ_WAVES,... + GRBM_GUI_ACTIVE) of `python3 bench.py "
+                     "--config {3,5} --steps 3 --warmup 1 --no-cpu-baseline --no-resident`; read = 2 x FETCH_SIZE "
+                     "(gfx950 correction, MI355X_MICROARCH.md HBM section); FETCH/WRITE count Infinity-Cache hits too")
+    if c4:
+        out["by_nodes"] = {"20000": dict(scan_modes(c4), source=f"{rel}/pmc_c4.json (gpurun_pmc.sh CFGS=4, same "
+                                                                "passes as C3)")}
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main()
