@@ -191,8 +191,8 @@ def main():
     _capture_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--candidates", type=int, default=0)
@@ -345,7 +345,7 @@ def main():
         contended_bench(args, fx, cache, base_opts, comm, rank, world, cid, open_ms_first)
         return
     prod = run_mode(0, args.steps, args.warmup, True)      # production: grouped shapes
-    full = run_mode(1, max(1, min(3, args.steps)), 1, False)  # SURVEY roofline rule: every task scans all N
+    full = run_mode(1, max(1, min(10, args.steps)), 2, False)  # SURVEY roofline rule: every task scans all N
     decisions = prod["decisions"]
     elapsed, total_decisions = kdist.aggregate(prod["elapsed"], decisions, sharded=world > 1)
     st = prod["stats"]
