@@ -1435,17 +1435,39 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   phase("ranks");
   if (S.treq.capacity() < (size_t)T) S.treq.reserve((size_t)T + T / 4 + 1024);
   S.task_node.reserve(S.treq.capacity());
-  S.treq.resize(T);
-  S.pending_candidate.assign(T, 0);
-  S.be_task.assign(T, 0);
-  S.task_job.resize(T);
-  for (int32_t t = 0; t < T; ++t) {
+  // An update recomputes the tasks its events touched; their old candidate
+  // state is kept aside for the counts below (`was`: bit 0 candidate, 1 BE).
+  const bool incr = !full && (int32_t)S.pending_candidate.size() <= T && !S.t_aff.empty();
+  std::sort(S.upd_tasks.begin(), S.upd_tasks.end());
+  S.upd_tasks.erase(std::unique(S.upd_tasks.begin(), S.upd_tasks.end()), S.upd_tasks.end());
+  std::vector<uint8_t> was;
+  auto task_row = [&](int32_t t) {
     S.treq[t] = to_res(S.tasks_in[t].resreq);
     S.task_job[t] = S.tasks_in[t].job;
-    if (!S.task_live[t]) continue;
+    S.tstat_in[t] = (uint16_t)S.tasks_in[t].status;
+    S.pending_candidate[t] = 0;
+    S.be_task[t] = 0;
+    if (!S.task_live[t]) return;
     // allocate.go:88-96: only Pending, non-BestEffort tasks enter the node loop
     S.pending_candidate[t] = S.tasks_in[t].status == KBG_PENDING && !kbg::res_empty(S.treq[t]);
     S.be_task[t] = S.tasks_in[t].status == KBG_PENDING && kbg::res_empty(S.treq[t]);
+  };
+  S.treq.resize(T);
+  S.task_job.resize(T);
+  S.tstat_in.resize(T);
+  if (incr) {
+    S.pending_candidate.resize(T, 0);
+    S.be_task.resize(T, 0);
+    was.resize(S.upd_tasks.size());
+    for (size_t i = 0; i < S.upd_tasks.size(); ++i) {
+      const int32_t t = S.upd_tasks[i];
+      was[i] = (S.pending_candidate[t] ? 1 : 0) | (S.be_task[t] ? 2 : 0);
+      task_row(t);
+    }
+  } else {
+    S.pending_candidate.assign(T, 0);
+    S.be_task.assign(T, 0);
+    for (int32_t t = 0; t < T; ++t) task_row(t);
   }
 
   phase("tasks");
@@ -1482,7 +1504,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   S.max_candidates = 0;
   for (int32_t n = 0; n < N; ++n) {
     for (int32_t t : S.node_task_order[n])
-      if (S.tasks_in[t].status == KBG_RUNNING) S.nt_task.push_back(t);
+      if (S.tstat_in[t] == KBG_RUNNING) S.nt_task.push_back(t);
     S.nt_off[n + 1] = (int32_t)S.nt_task.size();
     S.max_candidates = std::max(S.max_candidates, S.nt_off[n + 1] - S.nt_off[n]);
   }
@@ -1492,6 +1514,18 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   phase("pod keys");
   // ---- engine initial state
   Engine& E = S.init;
+  // an update recomputes the ready counts and drf allocations of the jobs its
+  // events touched (each from its own tasks, in order: the same sums)
+  const bool jincr = incr && (int32_t)E.jalloc.size() == S.n_jobs && (int32_t)S.job_ready0.size() == S.n_jobs;
+  std::vector<Res> prev_jalloc;
+  std::vector<int32_t> prev_jready;
+  std::vector<char> jtouch;
+  if (jincr) {
+    prev_jalloc = std::move(E.jalloc);
+    prev_jready = std::move(S.job_ready0);
+    jtouch.assign(S.n_jobs, 0);
+    for (int32_t j : S.pend_dirty_jobs) jtouch[j] = 1;
+  }
   E = Engine{};
   E.jalloc.assign(S.n_jobs, Res{});
   E.jshare.assign(S.n_jobs, 0.0);
@@ -1509,9 +1543,14 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     S.jt_off[j + 1] = (int32_t)S.jt.size();
   }
   auto job_tasks = [&](int32_t j) { return std::make_pair(S.jt.begin() + S.jt_off[j], S.jt.begin() + S.jt_off[j + 1]); };
-  for (int32_t j = 0; j < S.n_jobs; ++j)
+  for (int32_t j = 0; j < S.n_jobs; ++j) {
+    if (jincr && !jtouch[j]) {
+      E.jready[j] = prev_jready[j];
+      continue;
+    }
     for (auto [b, e] = job_tasks(j); b != e; ++b)
-      if (ready_status(S.tasks_in[*b].status)) E.jready[j]++;
+      if (ready_status(S.tstat_in[*b])) E.jready[j]++;
+  }
   S.job_ready0 = E.jready;
 
   // drf.go:55-78
@@ -1520,9 +1559,13 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   if (S.has_drf) {
     for (int32_t n = 0; n < N; ++n) kbg::res_add(S.drf_total, to_res(S.nodes_in[n].allocatable));
     for (int32_t j = 0; j < S.n_jobs; ++j) {
-      for (auto [b, e] = job_tasks(j); b != e; ++b)
-        if (allocated_status(S.tasks_in[*b].status)) kbg::res_add(E.jalloc[j], S.treq[*b]);
-      E.jshare[j] = share_of(E.jalloc[j], S.drf_total);
+      if (jincr && !jtouch[j]) {
+        E.jalloc[j] = prev_jalloc[j];
+      } else {
+        for (auto [b, e] = job_tasks(j); b != e; ++b)
+          if (allocated_status(S.tstat_in[*b])) kbg::res_add(E.jalloc[j], S.treq[*b]);
+      }
+      E.jshare[j] = share_of(E.jalloc[j], S.drf_total);  // the total may have changed (SetNode)
     }
   }
   // proportion.go:54-144 (queue attrs in order of first job)
@@ -1539,7 +1582,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
         qorder.push_back(q);
       }
       for (auto [b, e] = job_tasks(j); b != e; ++b) {
-        const int32_t s = S.tasks_in[*b].status;
+        const int32_t s = S.tstat_in[*b];
         if (allocated_status(s)) {
           kbg::res_add(E.qalloc[q], S.treq[*b]);
           kbg::res_add(S.q_request[q], S.treq[*b]);
@@ -1578,16 +1621,33 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   phase("engine+drf+prop");
   // ---- predicates preconditions
   const bool had_ghost = S.ghost;
-  S.has_aff = false;
-  S.ghost = false;
-  if (S.pred_active) {
-    for (int32_t t = 0; t < T; ++t) {
-      if (!S.task_live[t]) continue;
+  {
+    // per task: a pod (anti)affinity spec (kbg_affinity.cpp) and the ghost
+    // rule (an allocated task whose node is outside the session), counted
+    auto flags = [&](int32_t t) {
+      S.n_aff -= S.t_aff[t];
+      S.n_ghost -= S.t_ghost[t];
+      S.t_aff[t] = S.t_ghost[t] = 0;
+      if (!S.task_live[t]) return;
       const kbg_task& tk = S.tasks_in[t];
       const kbg_spec* sp = tk.spec >= 0 ? &S.specs_in[tk.spec] : nullptr;
-      if (sp && (sp->aff_len > 0 || sp->anti_len > 0)) S.has_aff = true;  // kbg_affinity.cpp
-      if (allocated_status(tk.status) && S.task_node[t] < 0) S.ghost = true;
+      S.t_aff[t] = sp && (sp->aff_len > 0 || sp->anti_len > 0);
+      S.t_ghost[t] = allocated_status(tk.status) && S.task_node[t] < 0;
+      S.n_aff += S.t_aff[t];
+      S.n_ghost += S.t_ghost[t];
+    };
+    if (incr) {
+      S.t_aff.resize(T, 0);
+      S.t_ghost.resize(T, 0);
+      for (int32_t t : S.upd_tasks) flags(t);
+    } else {
+      S.t_aff.assign(T, 0);
+      S.t_ghost.assign(T, 0);
+      S.n_aff = S.n_ghost = 0;
+      for (int32_t t = 0; t < T; ++t) flags(t);
     }
+    S.has_aff = S.pred_active && S.n_aff > 0;
+    S.ghost = S.pred_active && S.n_ghost > 0;
   }
 
   phase("preconditions");
@@ -1677,18 +1737,27 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
       *outcome = DERIVE_REBUILD;
       return KBG_OK;
     }
-    S.task_class.assign(T, 0);
-    if (S.pred_active)
-      for (int32_t t = 0; t < T; ++t) {
-        if (!S.pending_candidate[t] && !S.be_task[t]) continue;
-        const int32_t sp = S.tasks_in[t].spec;
-        const int32_t c = sp >= 0 ? S.spec_class[sp] : S.nospec_class;
-        if (c < 0) {  // a pod spec no candidate had at open: compile its class
-          *outcome = DERIVE_REBUILD;
-          return KBG_OK;
-        }
-        S.task_class[t] = c;
-      }
+    auto cls = [&](int32_t t) {  // false: a pod spec no candidate had at open (compile its class)
+      S.task_class[t] = 0;
+      if (!S.pred_active || (!S.pending_candidate[t] && !S.be_task[t])) return true;
+      const int32_t sp = S.tasks_in[t].spec;
+      const int32_t c = sp >= 0 ? S.spec_class[sp] : S.nospec_class;
+      if (c < 0) return false;
+      S.task_class[t] = c;
+      return true;
+    };
+    bool ok = true;
+    if (incr) {
+      S.task_class.resize(T, 0);
+      for (int32_t t : S.upd_tasks) ok = ok && cls(t);
+    } else {
+      S.task_class.assign(T, 0);
+      for (int32_t t = 0; t < T && ok; ++t) ok = cls(t);
+    }
+    if (!ok) {
+      *outcome = DERIVE_REBUILD;
+      return KBG_OK;
+    }
   }
   phase("classes");
   S.W = (N + 63) / 64;
@@ -1701,17 +1770,41 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     for (int32_t n = 0; n < N && ok; ++n)
       ok = exact(S.idle[n].c) && exact(S.idle[n].m) && exact(S.idle[n].g) && exact(S.rel[n].c) &&
            exact(S.rel[n].m) && exact(S.rel[n].g);
-    double sum_c = 0, sum_m = 0, sum_g = 0;
-    for (int32_t t = 0; t < T && ok; ++t) {
-      if (!S.pending_candidate[t]) continue;
+    // every candidate's request an exact non-negative integer, and their sum
+    // (exact as an integer; the doubles summed in any order agree on the bound)
+    // within 2^51: counts of the candidates, kept per task across updates
+    auto contrib = [&](int32_t t, int sign) {
+      if (S.t_inexact[t]) {
+        S.n_inexact += sign;
+        return;
+      }
       const Res& q = S.treq[t];
-      ok = exact(q.c) && exact(q.m) && exact(q.g) && q.c >= 0 && q.m >= 0 && q.g >= 0;
-      sum_c += q.c;
-      sum_m += q.m;
-      sum_g += q.g;
+      S.isum_c += sign * (__int128)(int64_t)q.c;
+      S.isum_m += sign * (__int128)(int64_t)q.m;
+      S.isum_g += sign * (__int128)(int64_t)q.g;
+    };
+    auto enter = [&](int32_t t) {  // t is a candidate now
+      const Res& q = S.treq[t];
+      S.t_inexact[t] = !(exact(q.c) && exact(q.m) && exact(q.g) && q.c >= 0 && q.m >= 0 && q.g >= 0);
+      contrib(t, +1);
+    };
+    if (incr) {
+      S.t_inexact.resize(T, 0);
+      for (size_t i = 0; i < S.upd_tasks.size(); ++i) {
+        const int32_t t = S.upd_tasks[i];
+        if (was[i] & 1) contrib(t, -1);  // the old candidate leaves (its request never changes)
+        if (S.pending_candidate[t]) enter(t);
+      }
+    } else {
+      S.t_inexact.assign(T, 0);
+      S.n_inexact = 0;
+      S.isum_c = S.isum_m = S.isum_g = 0;
+      for (int32_t t = 0; t < T; ++t)
+        if (S.pending_candidate[t]) enter(t);
     }
-    S.int_mode = ok && sum_c <= kLim && sum_m <= kLim && sum_g <= kLim &&
-                 getenv("KBG_FORCE_GENERAL_SCAN") == nullptr;
+    const __int128 lim = (__int128)kLim;
+    ok = ok && S.n_inexact == 0 && S.isum_c <= lim && S.isum_m <= lim && S.isum_g <= lim;
+    S.int_mode = ok && getenv("KBG_FORCE_GENERAL_SCAN") == nullptr;
   }
   phase("int mode");
   // ---- (class, request) shapes of the candidates
@@ -1727,9 +1820,8 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
       S.shape_of_task.resize(T, -1);
       if ((int32_t)S.be_shape.size() < std::max(1, S.n_classes)) S.be_shape.resize(std::max(1, S.n_classes), -1);
     }
-    S.task_shape.assign(T, -1);
-    for (int32_t t = 0; t < T; ++t) {
-      if (!S.pending_candidate[t]) continue;
+    auto cand_shape = [&](int32_t t) {
+      if (!S.pending_candidate[t]) return;
       int32_t& sh_t = S.shape_of_task[t];
       if (sh_t < 0) {
         auto it = S.shape_ids.emplace(kbg::ShapeKey{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g}, S.n_shapes);
@@ -1737,15 +1829,28 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
         sh_t = it.first->second;
       }
       S.task_shape[t] = sh_t;
-    }
+    };
     // backfill rows: one grouping id per class (the request does not matter)
-    for (int32_t t = 0; t < T; ++t) {
-      if (!S.be_task[t]) continue;
+    auto be_shape = [&](int32_t t) {
+      if (!S.be_task[t]) return;
       int32_t& b = S.be_shape[S.task_class[t]];
       if (b < 0) b = S.n_shapes++;
       S.task_shape[t] = b;
+    };
+    if (incr) {
+      S.task_shape.resize(T, -1);
+      for (int32_t t : S.upd_tasks) {
+        S.task_shape[t] = -1;
+        cand_shape(t);
+      }
+      for (int32_t t : S.upd_tasks) be_shape(t);
+    } else {
+      S.task_shape.assign(T, -1);
+      for (int32_t t = 0; t < T; ++t) cand_shape(t);
+      for (int32_t t = 0; t < T; ++t) be_shape(t);
     }
   }
+  S.upd_tasks.clear();
   phase("shapes");
   return KBG_OK;
 }
@@ -2119,8 +2224,12 @@ void begin_cycle(Session& S) {
   S.node_keys = S.node_keys0;
   S.port_hold.clear();
   S.evictions.clear();
-  S.tstat.resize(S.n_tasks);
-  for (int32_t t = 0; t < S.n_tasks; ++t) S.tstat[t] = S.tasks_in[t].status;
+  if ((int32_t)S.tstat_in.size() == S.n_tasks) {
+    S.tstat.assign(S.tstat_in.begin(), S.tstat_in.end());  // tasks_in[t].status, packed by derive_host
+  } else {  // an update that failed part-way
+    S.tstat.resize(S.n_tasks);
+    for (int32_t t = 0; t < S.n_tasks; ++t) S.tstat[t] = S.tasks_in[t].status;
+  }
   S.trun.assign(S.n_tasks, 0);
   for (int32_t t : S.nt_task) S.trun[t] = 1;
   S.pend = S.pend_all;
@@ -4319,6 +4428,7 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
       if (e.kind == KBG_EV_POD_UPDATE && (!status_ok(e.status) || e.node < -1 || e.node >= S.n_nodes))
         return fail(KBG_E_INVALID, "event status / node");
       S.pend_dirty_jobs.push_back(S.tasks_in[t].job);
+      S.upd_tasks.push_back(t);
       const int r = in_delete_task(S, U, t);
       if (r > 1) return (kbg_status)r;
       if (e.kind == KBG_EV_POD_DELETE || r == 1) {  // deleted, or updateTask returned deleteTask's error
@@ -4353,6 +4463,7 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
       S.rank_dirty_jobs.push_back(e.job);
       S.pend_dirty_jobs.push_back(e.job);
       S.pend_new.push_back(t);
+      S.upd_tasks.push_back(t);
       return in_add_task(S, U, t);
     }
     case KBG_EV_NODE_UPDATE: {
@@ -4382,12 +4493,21 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
   if (n < 0 || (n > 0 && !ev)) return fail(KBG_E_INVALID, "events");
   // the cycle state goes back to "just opened"
   S.allocated = S.backfilled = S.reclaimed = S.preempted = S.cycle_started = false;
+  static const bool prof = getenv("KBG_PROFILE_OPEN") != nullptr;
+  auto tl = t0;
+  auto phase = [&](const char* name) {
+    if (!prof) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[kbg update] %-20s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(now - tl).count());
+    tl = now;
+  };
   UpdateCtx U;
   U.seen.assign(S.n_nodes, 0);
   for (int32_t i = 0; i < n; ++i) {
     kbg_status st = apply_event(S, U, ev[i]);
     if (st != KBG_OK) return st;
   }
+  phase("events");
   S.vt_stale = true;
   S.vc.valid = false;
   const bool had_masks = S.has_ports || S.has_aff;
@@ -4395,6 +4515,7 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
   int outcome = DERIVE_OK;
   if (!U.rebuild) st = derive_host(S, nullptr, &outcome);
   if (st != KBG_OK) return st;
+  phase("derive");
   if (U.rebuild || outcome == DERIVE_REBUILD) {
     // new static classes or node flags: recompile and rebuild the device tables
     free_device(S);
@@ -4432,6 +4553,7 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
     S.h_class_mask0 = S.h_class_mask;
     S.stats.int_scan = S.int_mode ? 1 : 0;
   }
+  phase("device rows");
   S.updates++;
   S.update_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   S.stats.update_ms = S.update_ms;

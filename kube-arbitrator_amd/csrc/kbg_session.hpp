@@ -241,6 +241,15 @@ struct Session {
   std::vector<int32_t> shape_of_task;                    // a task's shape once it was a candidate (-1: not yet)
   std::vector<int32_t> pend_dirty_jobs;                  // jobs an update's events touched (their pending lists)
   std::vector<int32_t> pend_new;                         // tasks an update's events made (or re-made) Pending
+  // An update's derive recomputes the per-task state of the tasks its events
+  // touched only; the aggregates over tasks below are kept as counts.
+  std::vector<int32_t> upd_tasks;                        // tasks an update's events touched (added, updated, deleted)
+  std::vector<uint16_t> tstat_in;                        // tasks_in[t].status, packed for the per-job sums
+  std::vector<uint8_t> t_aff, t_ghost;                   // per task: its contribution to has_aff / ghost
+  int64_t n_aff = 0, n_ghost = 0;
+  std::vector<uint8_t> t_inexact;                        // per candidate: a request the integer scan cannot take
+  int64_t n_inexact = 0;
+  __int128 isum_c = 0, isum_m = 0, isum_g = 0;           // candidates' requests, exact when n_inexact == 0
   int32_t n_shapes = 0;
   std::vector<Res> treq;
   Res drf_total, prop_total;
