@@ -4503,10 +4503,21 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
   };
   UpdateCtx U;
   U.seen.assign(S.n_nodes, 0);
+  uint64_t kc[5] = {0, 0, 0, 0, 0}, kn[5] = {0, 0, 0, 0, 0};
   for (int32_t i = 0; i < n; ++i) {
+    const uint64_t c0 = prof ? __builtin_readcyclecounter() : 0;
     kbg_status st = apply_event(S, U, ev[i]);
     if (st != KBG_OK) return st;
+    if (prof) {
+      const int k = std::min(4, std::max(0, (int)ev[i].kind));
+      kc[k] += __builtin_readcyclecounter() - c0;
+      kn[k]++;
+    }
   }
+  if (prof)
+    for (int k = 0; k < 5; ++k)
+      if (kn[k]) fprintf(stderr, "[kbg update] event kind %d: %llu, %.0f cycles each\n", k, (unsigned long long)kn[k],
+                         (double)kc[k] / kn[k]);
   phase("events");
   S.vt_stale = true;
   S.vc.valid = false;
