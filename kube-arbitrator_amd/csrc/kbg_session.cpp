@@ -1196,6 +1196,8 @@ std::vector<T> copy_arr(const T* p, int32_t n) {
   return (p && n > 0) ? std::vector<T>(p, p + n) : std::vector<T>();
 }
 
+constexpr int64_t kRankGap = int64_t(1) << 20;  // task_rank spacing at open (kbg_session.hpp)
+
 std::vector<int32_t> ranks_of(const Session& S, const std::vector<int32_t>& ids) {
   std::vector<int32_t> idx(ids.size());
   std::iota(idx.begin(), idx.end(), 0);
@@ -1395,39 +1397,57 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   if (S.task_rank.empty() && T > 0) {
     std::vector<int32_t> ids(T);
     for (int32_t t = 0; t < T; ++t) ids[t] = S.tasks_in[t].uid;
-    S.task_rank = ranks_of(S, ids);
+    const std::vector<int32_t> dense = ranks_of(S, ids);
+    S.task_rank.resize(T);
+    for (int32_t t = 0; t < T; ++t) S.task_rank[t] = (int64_t)dense[t] * kRankGap;
+    S.job_rank_order.assign(S.n_jobs, {});
+    for (int32_t j = 0; j < S.n_jobs; ++j) {
+      std::vector<int32_t>& ro = S.job_rank_order[j];
+      ro = S.job_task_order[j];
+      std::stable_sort(ro.begin(), ro.end(), [&](int32_t a, int32_t b) { return S.task_rank[a] < S.task_rank[b]; });
+    }
   } else if (S.task_ranks_stale) {
-    // a job that gained tasks: its ranked tasks keep their order, the new ones
-    // are merged in by UID (dense ranks, equal UIDs share one)
+    // a job that gained tasks: each new UID takes a rank between the ranked
+    // tasks around it (the same rank as an equal UID); a job whose gap ran out
+    // is renumbered first
     const int32_t T_old = (int32_t)S.task_rank.size();
     S.task_rank.resize(T, 0);
     std::sort(S.rank_dirty_jobs.begin(), S.rank_dirty_jobs.end());
     S.rank_dirty_jobs.erase(std::unique(S.rank_dirty_jobs.begin(), S.rank_dirty_jobs.end()), S.rank_dirty_jobs.end());
-    std::vector<int32_t> olds, news, merged, rank;
+    const auto uid = [&](int32_t t) -> const std::string& { return S.strs[S.tasks_in[t].uid]; };
+    std::vector<int32_t> news;
     for (int32_t j : S.rank_dirty_jobs) {
-      olds.clear();
       news.clear();
-      for (int32_t t : S.job_task_order[j]) (t < T_old ? olds : news).push_back(t);
-      const auto uid = [&](int32_t t) -> const std::string& { return S.strs[S.tasks_in[t].uid]; };
-      std::sort(olds.begin(), olds.end(), [&](int32_t a, int32_t b) { return S.task_rank[a] < S.task_rank[b]; });
+      for (int32_t t : S.job_task_order[j])
+        if (t >= T_old) news.push_back(t);
       std::stable_sort(news.begin(), news.end(), [&](int32_t a, int32_t b) { return uid(a) < uid(b); });
-      merged.clear();
-      size_t a = 0;
-      for (int32_t nt : news) {  // each new UID goes after the ranked tasks that do not sort above it
-        const size_t at = std::upper_bound(olds.begin() + a, olds.end(), nt,
-                                           [&](int32_t x, int32_t y) { return uid(x) < uid(y); }) - olds.begin();
-        merged.insert(merged.end(), olds.begin() + a, olds.begin() + at);
-        merged.push_back(nt);
-        a = at;
+      std::vector<int32_t>& ro = S.job_rank_order[j];
+      for (int32_t nt : news) {
+        const auto it = std::upper_bound(ro.begin(), ro.end(), nt, [&](int32_t x, int32_t y) { return uid(x) < uid(y); });
+        size_t pos = it - ro.begin();
+        if (pos > 0 && uid(ro[pos - 1]) == uid(nt)) {
+          S.task_rank[nt] = S.task_rank[ro[pos - 1]];
+        } else {
+          auto bounds = [&](int64_t* lo, int64_t* hi) {
+            *lo = pos > 0 ? S.task_rank[ro[pos - 1]] : (ro.empty() ? 0 : S.task_rank[ro[0]] - 2 * kRankGap);
+            *hi = pos < ro.size() ? S.task_rank[ro[pos]] : (ro.empty() ? 2 * kRankGap : S.task_rank[ro.back()] + 2 * kRankGap);
+          };
+          int64_t lo, hi;
+          bounds(&lo, &hi);
+          if (hi - lo < 2) {  // no rank left between the neighbours: renumber the job (equal ranks stay equal)
+            int64_t r = 0, prev = 0;
+            for (size_t k = 0; k < ro.size(); ++k) {
+              const int64_t old = S.task_rank[ro[k]];
+              if (k > 0 && old != prev) ++r;
+              prev = old;
+              S.task_rank[ro[k]] = r * kRankGap;
+            }
+            bounds(&lo, &hi);
+          }
+          S.task_rank[nt] = lo + (hi - lo) / 2;
+        }
+        ro.insert(ro.begin() + pos, nt);
       }
-      merged.insert(merged.end(), olds.begin() + a, olds.end());
-      rank.assign(merged.size(), 0);
-      for (size_t k = 1; k < merged.size(); ++k) {
-        const int32_t p = merged[k - 1], q = merged[k];
-        const bool same = (p < T_old && q < T_old) ? S.task_rank[p] == S.task_rank[q] : uid(p) == uid(q);
-        rank[k] = rank[k - 1] + (same ? 0 : 1);
-      }
-      for (size_t k = 0; k < merged.size(); ++k) S.task_rank[merged[k]] = rank[k];
     }
   }
   S.task_ranks_stale = false;
@@ -4433,6 +4453,14 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
       if (r > 1) return (kbg_status)r;
       if (e.kind == KBG_EV_POD_DELETE || r == 1) {  // deleted, or updateTask returned deleteTask's error
         S.task_live[t] = 0;
+        // it leaves its job's rank order (an updated task keeps its place there:
+        // same task, same UID; a task added by this update is not in it yet)
+        const int32_t j = S.tasks_in[t].job;
+        if ((size_t)j < S.job_rank_order.size()) {
+          std::vector<int32_t>& ro = S.job_rank_order[j];
+          auto it = std::find(ro.begin(), ro.end(), t);
+          if (it != ro.end()) ro.erase(it);
+        }
         return KBG_OK;
       }
       S.tasks_in[t].status = e.status;

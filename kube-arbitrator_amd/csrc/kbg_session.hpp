@@ -223,7 +223,11 @@ struct Session {
   bool heap_go111 = true;
 
   // ---- derived, immutable after open
-  std::vector<int32_t> job_rank, queue_rank, task_rank;  // bytewise UID order
+  std::vector<int32_t> job_rank, queue_rank;             // bytewise UID order
+  // Tasks: bytewise UID order as gapped ranks (multiples of kRankGap at open),
+  // so a task added by an update takes a rank between its neighbours' without
+  // re-ranking its job; equal UIDs share a rank. Only compared within a job.
+  std::vector<int64_t> task_rank;
   std::vector<int32_t> job_frank;                        // (CreationTimestamp, UID) order
   std::vector<int32_t> job_by_frank;                     // inverse of job_frank
   std::vector<uint32_t> job_prank;                       // dense rank of -Priority
@@ -352,6 +356,7 @@ struct Session {
   std::unordered_map<int32_t, int32_t> node_of;       // canonical node name -> node index
   std::vector<uint8_t> task_live;                     // 0: the pod was deleted (event_handlers.go deletePod)
   std::vector<std::vector<int32_t>> job_task_order;   // per job: its tasks in JobInfo.Tasks insertion order
+  std::vector<std::vector<int32_t>> job_rank_order;   // per job: its ranked tasks in task_rank order
   std::vector<std::vector<int32_t>> node_task_order;  // per node: the session tasks in NodeInfo.Tasks order
   std::vector<std::vector<int32_t>> node_key_order;   // per node: PodKey (canonical id) of every pod on it
   std::vector<kbg_resource> others_in;                // Session.Others resreq
