@@ -1230,6 +1230,16 @@ int32_t intern(Session& S, const char* v) {
   return id;
 }
 
+// A string only ever read as text (a task UID: TaskOrderFn's fallback compares
+// UIDs as strings, nothing looks it up by content): appended without the
+// content map, as its own canonical id.
+int32_t append_str(Session& S, const char* v) {
+  const int32_t id = (int32_t)S.strs.size();
+  S.strs.emplace_back(v ? v : "");
+  S.canon.push_back(id);
+  return id;
+}
+
 kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   kbg_status st = validate(snap);
   if (st != KBG_OK) return st;
@@ -4474,7 +4484,7 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
           !status_ok(e.status) || e.node < -1 || e.node >= S.n_nodes || !e.uid || !e.pod_key)
         return fail(KBG_E_INVALID, "POD_ADD event");
       kbg_task k{};
-      k.uid = intern(S, e.uid);
+      k.uid = append_str(S, e.uid);
       k.job = e.job;
       k.status = e.status;
       k.priority = e.priority;
