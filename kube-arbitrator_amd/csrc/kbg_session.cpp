@@ -1471,6 +1471,8 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   std::sort(S.upd_tasks.begin(), S.upd_tasks.end());
   S.upd_tasks.erase(std::unique(S.upd_tasks.begin(), S.upd_tasks.end()), S.upd_tasks.end());
   std::vector<uint8_t> was;
+  std::vector<uint16_t> was_stat;  // the touched tasks' statuses at the last derive
+  const int32_t T_prev = (int32_t)S.tstat_in.size();
   auto task_row = [&](int32_t t) {
     S.treq[t] = to_res(S.tasks_in[t].resreq);
     S.task_job[t] = S.tasks_in[t].job;
@@ -1489,9 +1491,11 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     S.pending_candidate.resize(T, 0);
     S.be_task.resize(T, 0);
     was.resize(S.upd_tasks.size());
+    was_stat.resize(S.upd_tasks.size());
     for (size_t i = 0; i < S.upd_tasks.size(); ++i) {
       const int32_t t = S.upd_tasks[i];
       was[i] = (S.pending_candidate[t] ? 1 : 0) | (S.be_task[t] ? 2 : 0);
+      was_stat[i] = t < T_prev ? S.tstat_in[t] : 0;
       task_row(t);
     }
   } else {
@@ -1611,13 +1615,72 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
         S.q_has_attr[q] = 1;
         qorder.push_back(q);
       }
-      for (auto [b, e] = job_tasks(j); b != e; ++b) {
-        const int32_t s = S.tstat_in[*b];
-        if (allocated_status(s)) {
-          kbg::res_add(E.qalloc[q], S.treq[*b]);
-          kbg::res_add(S.q_request[q], S.treq[*b]);
-        } else if (s == KBG_PENDING) {
-          kbg::res_add(S.q_request[q], S.treq[*b]);
+    }
+    // a task's part of its queue's sums: allocated -> both, Pending -> request
+    constexpr double kExact = 9007199254740992.0;  // 2^53
+    auto pexact = [&](const Res& r) {
+      auto ok = [&](double v) { return v >= 0 && v <= kExact && v == (double)(int64_t)v; };
+      return ok(r.c) && ok(r.m) && ok(r.g);
+    };
+    auto psum = [&](int32_t t, int32_t st, int sign) {
+      if (S.t_pinexact[t]) {
+        S.n_pinexact += sign;
+        return;
+      }
+      const bool a = allocated_status(st);
+      if (!a && st != KBG_PENDING) return;
+      const int32_t q = S.job_queue[S.task_job[t]];
+      const Res& r = S.treq[t];
+      const __int128 v[3] = {(__int128)(int64_t)r.c, (__int128)(int64_t)r.m, (__int128)(int64_t)r.g};
+      for (int d = 0; d < 3; ++d) {
+        if (a) S.qa_sum[3 * (size_t)q + d] += sign * v[d];
+        S.qr_sum[3 * (size_t)q + d] += sign * v[d];
+      }
+    };
+    bool exact_sums = false;
+    if (incr && S.prop_sums_ok && (int32_t)S.qa_sum.size() == 3 * S.n_queues) {
+      S.t_pinexact.resize(T, 0);
+      for (size_t i = 0; i < S.upd_tasks.size(); ++i) {
+        const int32_t t = S.upd_tasks[i];
+        if (t < T_prev) psum(t, was_stat[i], -1);  // live at the last derive (events only touch live tasks)
+        if (t >= T_prev) S.t_pinexact[t] = !pexact(S.treq[t]);
+        if (S.task_live[t]) psum(t, S.tstat_in[t], +1);
+      }
+      exact_sums = S.n_pinexact == 0;
+    } else {  // (re)build the sums from every live task
+      S.t_pinexact.assign(T, 0);
+      S.n_pinexact = 0;
+      S.qa_sum.assign(3 * (size_t)S.n_queues, 0);
+      S.qr_sum.assign(3 * (size_t)S.n_queues, 0);
+      for (int32_t j = 0; j < S.n_jobs; ++j)
+        for (auto [b, e] = job_tasks(j); b != e; ++b) {
+          S.t_pinexact[*b] = !pexact(S.treq[*b]);
+          psum(*b, S.tstat_in[*b], +1);
+        }
+      S.prop_sums_ok = true;
+      exact_sums = S.n_pinexact == 0;
+    }
+    for (int32_t q = 0; q < S.n_queues && exact_sums; ++q)
+      for (int d = 0; d < 3; ++d)
+        if (S.qr_sum[3 * (size_t)q + d] > (__int128)kExact) exact_sums = false;
+    if (exact_sums) {
+      for (int32_t q = 0; q < S.n_queues; ++q) {
+        E.qalloc[q] = Res{(double)(int64_t)S.qa_sum[3 * (size_t)q], (double)(int64_t)S.qa_sum[3 * (size_t)q + 1],
+                          (double)(int64_t)S.qa_sum[3 * (size_t)q + 2]};
+        S.q_request[q] = Res{(double)(int64_t)S.qr_sum[3 * (size_t)q], (double)(int64_t)S.qr_sum[3 * (size_t)q + 1],
+                             (double)(int64_t)S.qr_sum[3 * (size_t)q + 2]};
+      }
+    } else {  // the reference's sequential fp64 sums, job by job, task by task
+      for (int32_t j = 0; j < S.n_jobs; ++j) {
+        const int32_t q = S.job_queue[j];
+        for (auto [b, e] = job_tasks(j); b != e; ++b) {
+          const int32_t s = S.tstat_in[*b];
+          if (allocated_status(s)) {
+            kbg::res_add(E.qalloc[q], S.treq[*b]);
+            kbg::res_add(S.q_request[q], S.treq[*b]);
+          } else if (s == KBG_PENDING) {
+            kbg::res_add(S.q_request[q], S.treq[*b]);
+          }
         }
       }
     }

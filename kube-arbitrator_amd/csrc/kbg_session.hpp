@@ -254,6 +254,13 @@ struct Session {
   std::vector<uint8_t> t_inexact;                        // per candidate: a request the integer scan cannot take
   int64_t n_inexact = 0;
   __int128 isum_c = 0, isum_m = 0, isum_g = 0;           // candidates' requests, exact when n_inexact == 0
+  // proportion's per-queue sums (allocated; allocated + pending) as exact
+  // integers: while every live task's request is a non-negative integer and
+  // the sums stay within 2^53, the sequential fp64 sums equal them
+  std::vector<uint8_t> t_pinexact;
+  int64_t n_pinexact = 0;
+  std::vector<__int128> qa_sum, qr_sum;                  // [queue * 3 + dim]
+  bool prop_sums_ok = false;                             // the sums above are current
   int32_t n_shapes = 0;
   std::vector<Res> treq;
   Res drf_total, prop_total;
