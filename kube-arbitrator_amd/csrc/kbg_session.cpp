@@ -4461,7 +4461,11 @@ int in_node_remove(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
   auto kit = std::find(keys.begin(), keys.end(), key);
   if (kit == keys.end()) return 1;
   std::vector<int32_t>& tl = S.node_task_order[n];
-  auto hit = std::find_if(tl.begin(), tl.end(), [&](int32_t u) { return S.canon[S.tasks_in[u].pod_key] == key; });
+  // a node's session tasks hold distinct keys (AddTask refuses a key already
+  // there), so the task holding t's key is t itself whenever t is on the node
+  auto hit = std::find(tl.begin(), tl.end(), t);
+  if (hit == tl.end())
+    hit = std::find_if(tl.begin(), tl.end(), [&](int32_t u) { return S.canon[S.tasks_in[u].pod_key] == key; });
   if (hit == tl.end())
     return fail(KBG_E_UNSUPPORTED, "the pod key is held on the node by a pod outside the session jobs "
                                    "(its resources are unknown): re-open the session");
