@@ -51,7 +51,7 @@ def milli_cpu(req):
 
 
 class Cluster:
-    def __init__(self, worker_cpu=(4000, 4000, 4000), system_cpu=(250, 0, 0), runner=None, grace=1):
+    def __init__(self, worker_cpu=(4000, 4000, 4000), system_cpu=(250, 0, 0), runner=None, grace=1, ns_queues=False):
         self.grace = grace  # cycles a terminating pod stays Releasing
         self.runner = runner  # fixture -> output in the oracle's schema (one Scheduler.runOnce)
         self.nodes = [{"name": "master", "allocatable": {"cpu": "4", "memory": "16Gi", "pods": "110"},
@@ -60,7 +60,13 @@ class Cluster:
             self.nodes.append({"name": f"node-{i + 1}", "allocatable": {"cpu": f"{c}m", "memory": "16Gi",
                                                                          "pods": "110"},
                                "labels": {"kubernetes.io/hostname": f"node-{i + 1}"}})
-        self.queues = [{"name": "q1", "weight": 1}, {"name": "q2", "weight": 1}, {"name": "test", "weight": 1}]
+        # queue CRDs q1, q2 and the context namespace's (util.go:180-216), or —
+        # ENABLE_NAMESPACES_AS_QUEUE, which hack/run-e2e.sh:11-15 toggles at
+        # random — every namespace a queue of weight 1 (event_handlers.go:726-736)
+        self.ns_queues = ns_queues
+        self.queues = [] if ns_queues else [{"name": "q1", "weight": 1}, {"name": "q2", "weight": 1},
+                                            {"name": "test", "weight": 1}]
+        self.namespaces = ["kube-system", "test", "q1", "q2"] if ns_queues else []
         self.pods, self.pgs = [], []
         self.templates = {}  # pod uid -> template the Job controller recreates it from
         self.terminating = {}  # uid -> scheduling cycles left before the pod is gone
@@ -88,9 +94,13 @@ class Cluster:
         self.pods.append(p)
         return p
 
-    def create_job(self, name, tasks, ns="test", queue="", min_member=None):
+    def create_job(self, name, tasks, ns=None, queue="", min_member=None):
         """createJobEx (util.go:279-340): one batch Job per task spec, one
-        PodGroup with MinMember = sum of the tasks' min (or the override)."""
+        PodGroup with MinMember = sum of the tasks' min (or the override), in
+        getNS's namespace (util.go:262-277: the job's queue when namespaces
+        are queues, else the context's)."""
+        if ns is None:
+            ns = queue if (self.ns_queues and queue) else "test"
         self.clock += 1
         mn = 0
         for i, t in enumerate(tasks):
@@ -151,9 +161,12 @@ class Cluster:
 
     # ------------------------------------------------------------ cycles
     def fixture(self):
-        return {"actions": list(CONF_ACTIONS), "tiers": copy.deepcopy(CONF_TIERS), "nodes": copy.deepcopy(self.nodes),
-                "pods": copy.deepcopy(self.pods), "podGroups": copy.deepcopy(self.pgs),
-                "queues": copy.deepcopy(self.queues)}
+        fx = {"actions": list(CONF_ACTIONS), "tiers": copy.deepcopy(CONF_TIERS), "nodes": copy.deepcopy(self.nodes),
+              "pods": copy.deepcopy(self.pods), "podGroups": copy.deepcopy(self.pgs),
+              "queues": copy.deepcopy(self.queues)}
+        if self.namespaces:
+            fx["namespaces"] = list(self.namespaces)
+        return fx
 
     def cycle_once(self):
         self.cycle(self.runner)

@@ -208,33 +208,40 @@ KNOWN_MISSES = {
 }
 
 
-def run_scenario(name, shape, runner):
+def run_scenario(name, shape, mode, runner):
     """Runs the spec; a miss listed in KNOWN_MISSES returns its reason (and a
     listed miss that starts passing fails, so the list stays exact)."""
-    c = Cluster(**SHAPES[shape], runner=runner)
+    c = Cluster(**SHAPES[shape], runner=runner, ns_queues=mode == "ns-queues")
+    key = (name, shape) if (name, shape, mode) not in KNOWN_MISSES else (name, shape, mode)
     try:
         SCENARIOS[name](c, c.wait)
     except WaitTimeout:
-        if (name, shape) in KNOWN_MISSES:
-            return KNOWN_MISSES[(name, shape)]
+        if key in KNOWN_MISSES:
+            return KNOWN_MISSES[key]
         raise
-    assert (name, shape) not in KNOWN_MISSES, "a known miss now passes: update KNOWN_MISSES"
+    assert key not in KNOWN_MISSES, "a known miss now passes: update KNOWN_MISSES"
     return None
 
 
+# queue CRDs, or namespaces as queues (hack/run-e2e.sh:11-15 picks one at random)
+MODES = ("crd-queues", "ns-queues")
+
+
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("shape", sorted(SHAPES))
 @pytest.mark.parametrize("name", sorted(SCENARIOS))
-def test_e2e_spec_oracle(name, shape):
-    miss = run_scenario(name, shape, oracle_runner)
+def test_e2e_spec_oracle(name, shape, mode):
+    miss = run_scenario(name, shape, mode, oracle_runner)
     if miss:
         pytest.xfail(miss)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("shape", sorted(SHAPES))
 @pytest.mark.parametrize("name", sorted(SCENARIOS))
-def test_e2e_spec_device(name, shape):
+def test_e2e_spec_device(name, shape, mode):
     # every cycle is compared with the oracle inside device_runner
-    miss = run_scenario(name, shape, device_runner)
+    miss = run_scenario(name, shape, mode, device_runner)
     if miss:
         pytest.xfail(miss)
