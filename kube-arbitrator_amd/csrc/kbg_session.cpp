@@ -977,23 +977,48 @@ bool mirror_add(Session& S, int32_t t, int32_t nd, int32_t kind) {
 // Which pod keys can collide: a candidate task's key that another candidate
 // shares or that some node already holds (a StatefulSet pod recreated while
 // its predecessor is still on a node). Usually none: then nothing is tracked.
-void setup_pod_keys(Session& S) {
-  S.task_key.resize(S.n_tasks);
-  for (int32_t t = 0; t < S.n_tasks; ++t) S.task_key[t] = S.canon[S.tasks_in[t].pod_key];
-  S.key_hot.assign(S.strs.size(), 0);
-  S.has_dupkeys = false;
-  S.node_keys.clear();
-  std::vector<uint8_t> seen(S.strs.size(), 0);
-  for (int32_t t = 0; t < S.n_tasks; ++t) {
-    if (!S.pending_candidate[t] && !S.be_task[t]) continue;  // (false for removed tasks)
-    uint8_t& c = seen[S.task_key[t]];
-    if (c) S.key_hot[S.task_key[t]] = 1;
-    c = 1;
+// Kept as counts per canonical key — candidate (Pending) tasks holding it,
+// node entries holding it — so an update adjusts the keys its events and
+// touched tasks changed instead of rescanning every task and node.
+void pod_key_refresh(Session& S, int32_t k) {
+  const bool hot = S.kc_cand[k] >= 2 || (S.kc_cand[k] >= 1 && S.kc_node[k] >= 1);
+  if (hot != (S.key_hot[k] != 0)) {
+    S.n_hot += hot ? 1 : -1;
+    S.key_hot[k] = hot ? 1 : 0;
   }
-  for (int32_t n = 0; n < S.n_nodes; ++n)
-    for (int32_t k : S.node_key_order[n])
-      if (seen[k]) S.key_hot[k] = 1;
-  for (int32_t t = 0; t < S.n_tasks && !S.has_dupkeys; ++t) S.has_dupkeys = S.key_hot[S.task_key[t]] != 0;
+}
+void setup_pod_keys(Session& S, bool incr = false, const std::vector<int32_t>* touched = nullptr,
+                    const std::vector<uint8_t>* was = nullptr) {
+  const size_t NS = S.strs.size();
+  S.task_key.resize(S.n_tasks);
+  if (!incr || S.kc_cand.empty()) {
+    for (int32_t t = 0; t < S.n_tasks; ++t) S.task_key[t] = S.canon[S.tasks_in[t].pod_key];
+    S.kc_cand.assign(NS, 0);
+    S.kc_node.assign(NS, 0);
+    S.key_hot.assign(NS, 0);
+    S.n_hot = 0;
+    for (int32_t t = 0; t < S.n_tasks; ++t)
+      if (S.pending_candidate[t] || S.be_task[t]) S.kc_cand[S.task_key[t]]++;  // (false for removed tasks)
+    for (int32_t n = 0; n < S.n_nodes; ++n)
+      for (int32_t k : S.node_key_order[n]) S.kc_node[k]++;
+    for (size_t k = 0; k < NS; ++k) pod_key_refresh(S, (int32_t)k);
+  } else {
+    S.kc_cand.resize(NS, 0);
+    if (S.kc_node.size() < NS) S.kc_node.resize(NS, 0);
+    S.key_hot.resize(NS, 0);
+    for (size_t i = 0; i < touched->size(); ++i) {
+      const int32_t t = (*touched)[i];
+      const int32_t k = S.task_key[t] = S.canon[S.tasks_in[t].pod_key];
+      const bool was_c = ((*was)[i] & 3) != 0, now_c = S.pending_candidate[t] || S.be_task[t];
+      if (was_c == now_c) continue;
+      S.kc_cand[k] += now_c ? 1 : -1;
+      pod_key_refresh(S, k);
+    }
+    for (int32_t k : S.upd_keys) pod_key_refresh(S, k);  // node entries added / removed by the events
+  }
+  S.upd_keys.clear();
+  S.has_dupkeys = S.n_hot > 0;
+  S.node_keys.clear();
   if (S.has_dupkeys)
     for (int32_t n = 0; n < S.n_nodes; ++n)
       for (int32_t k : S.node_key_order[n])
@@ -1421,6 +1446,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     // tasks around it (the same rank as an equal UID); a job whose gap ran out
     // is renumbered first
     const int32_t T_old = (int32_t)S.task_rank.size();
+    if (S.task_rank.capacity() < (size_t)T) S.task_rank.reserve((size_t)T + T / 4 + 1024);
     S.task_rank.resize(T, 0);
     std::sort(S.rank_dirty_jobs.begin(), S.rank_dirty_jobs.end());
     S.rank_dirty_jobs.erase(std::unique(S.rank_dirty_jobs.begin(), S.rank_dirty_jobs.end()), S.rank_dirty_jobs.end());
@@ -1463,8 +1489,28 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   S.task_ranks_stale = false;
   S.rank_dirty_jobs.clear();
   phase("ranks");
-  if (S.treq.capacity() < (size_t)T) S.treq.reserve((size_t)T + T / 4 + 1024);
-  S.task_node.reserve(S.treq.capacity());
+  // per-task vectors grow with every update's new pods: keep headroom so an
+  // update does not reallocate (and copy) them
+  auto headroom = [](auto& v, size_t n) {
+    if (v.capacity() < n) v.reserve(n + n / 4 + 1024);
+  };
+  headroom(S.treq, T);
+  headroom(S.task_node, T);
+  headroom(S.task_job, T);
+  headroom(S.tstat_in, T);
+  headroom(S.pending_candidate, T);
+  headroom(S.be_task, T);
+  headroom(S.t_aff, T);
+  headroom(S.t_ghost, T);
+  headroom(S.t_inexact, T);
+  headroom(S.t_pinexact, T);
+  headroom(S.task_class, T);
+  headroom(S.task_shape, T);
+  headroom(S.shape_of_task, T);
+  headroom(S.task_key, T);
+  headroom(S.kc_cand, S.strs.size());
+  headroom(S.kc_node, S.strs.size());
+  headroom(S.key_hot, S.strs.size());
   // An update recomputes the tasks its events touched; their old candidate
   // state is kept aside for the counts below (`was`: bit 0 candidate, 1 BE).
   const bool incr = !full && (int32_t)S.pending_candidate.size() <= T && !S.t_aff.empty();
@@ -1543,7 +1589,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     S.max_candidates = std::max(S.max_candidates, S.nt_off[n + 1] - S.nt_off[n]);
   }
   phase("nodes+victims");
-  setup_pod_keys(S);
+  setup_pod_keys(S, incr, &S.upd_tasks, &was);
 
   phase("pod keys");
   // ---- engine initial state
@@ -4436,6 +4482,9 @@ bool in_node_add(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
   }
   nd.num_tasks++;
   keys.push_back(key);
+  if ((size_t)key >= S.kc_node.size()) S.kc_node.resize((size_t)key + 1, 0);
+  S.kc_node[key]++;
+  S.upd_keys.push_back(key);
   S.node_task_order[n].push_back(t);
   // the pod's host ports join the node's (a set: duplicates are harmless to setup_host_ports)
   const int32_t sp = S.tasks_in[t].spec;
@@ -4490,6 +4539,8 @@ int in_node_remove(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
   }
   nd.num_tasks--;
   keys.erase(kit);
+  if ((size_t)key < S.kc_node.size()) S.kc_node[key]--;
+  S.upd_keys.push_back(key);
   tl.erase(hit);
   U.touch(n);
   return 0;

@@ -388,6 +388,9 @@ struct Session {
   std::vector<int32_t> task_key;                      // canonical string id of each task's PodKey
   bool has_dupkeys = false;                           // some candidate task's key can meet itself on a node
   std::vector<uint8_t> key_hot;                       // per canonical string id: a colliding key
+  std::vector<int32_t> kc_cand, kc_node;              // per canonical key: candidate tasks / node entries holding it
+  int64_t n_hot = 0;                                  // keys with key_hot set
+  std::vector<int32_t> upd_keys;                      // keys whose node entries an update's events changed
   std::unordered_set<int64_t> node_keys, node_keys0;  // (node << 32 | key) of hot keys on nodes (now / at open)
   std::vector<uint8_t> dec_dup;                       // per decision of the cycle: the node was left unchanged
 
