@@ -1406,6 +1406,18 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   return KBG_OK;
 }
 
+// S.task_uid_key[from, n_tasks): each UID's first 8 bytes, big-endian and
+// zero-padded, so unequal keys order the UIDs as their bytes do
+void fill_uid_keys(Session& S, int32_t from) {
+  S.task_uid_key.resize(S.n_tasks);
+  for (int32_t t = from; t < S.n_tasks; ++t) {
+    const std::string& u = S.strs[S.tasks_in[t].uid];
+    uint64_t k = 0;
+    for (size_t i = 0; i < 8; ++i) k = k << 8 | (i < u.size() ? (uint8_t)u[i] : 0);
+    S.task_uid_key[t] = k;
+  }
+}
+
 enum { DERIVE_OK = 0, DERIVE_REBUILD = 1 };  // REBUILD: the static classes / masks must be recompiled
 
 // Every host structure that follows from the inputs. `sh` non-null: compile
@@ -1435,6 +1447,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     const std::vector<int32_t> dense = ranks_of(S, ids);
     S.task_rank.resize(T);
     for (int32_t t = 0; t < T; ++t) S.task_rank[t] = (int64_t)dense[t] * kRankGap;
+    fill_uid_keys(S, 0);
     S.job_rank_order.assign(S.n_jobs, {});
     for (int32_t j = 0; j < S.n_jobs; ++j) {
       std::vector<int32_t>& ro = S.job_rank_order[j];
@@ -1448,20 +1461,26 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     const int32_t T_old = (int32_t)S.task_rank.size();
     if (S.task_rank.capacity() < (size_t)T) S.task_rank.reserve((size_t)T + T / 4 + 1024);
     S.task_rank.resize(T, 0);
+    if (S.task_uid_key.size() != (size_t)T_old) fill_uid_keys(S, 0);  // keys follow the ranks
+    if (S.task_uid_key.capacity() < (size_t)T) S.task_uid_key.reserve((size_t)T + T / 4 + 1024);
+    fill_uid_keys(S, T_old);
     std::sort(S.rank_dirty_jobs.begin(), S.rank_dirty_jobs.end());
     S.rank_dirty_jobs.erase(std::unique(S.rank_dirty_jobs.begin(), S.rank_dirty_jobs.end()), S.rank_dirty_jobs.end());
     const auto uid = [&](int32_t t) -> const std::string& { return S.strs[S.tasks_in[t].uid]; };
+    // bytewise UID order: the 8-byte keys decide unless they tie
+    const uint64_t* key = S.task_uid_key.data();
+    const auto uid_less = [&](int32_t a, int32_t b) { return key[a] != key[b] ? key[a] < key[b] : uid(a) < uid(b); };
     std::vector<int32_t> news;
     for (int32_t j : S.rank_dirty_jobs) {
       news.clear();
       for (int32_t t : S.job_task_order[j])
         if (t >= T_old) news.push_back(t);
-      std::stable_sort(news.begin(), news.end(), [&](int32_t a, int32_t b) { return uid(a) < uid(b); });
+      std::stable_sort(news.begin(), news.end(), uid_less);
       std::vector<int32_t>& ro = S.job_rank_order[j];
       for (int32_t nt : news) {
-        const auto it = std::upper_bound(ro.begin(), ro.end(), nt, [&](int32_t x, int32_t y) { return uid(x) < uid(y); });
+        const auto it = std::upper_bound(ro.begin(), ro.end(), nt, uid_less);
         size_t pos = it - ro.begin();
-        if (pos > 0 && uid(ro[pos - 1]) == uid(nt)) {
+        if (pos > 0 && key[ro[pos - 1]] == key[nt] && uid(ro[pos - 1]) == uid(nt)) {
           S.task_rank[nt] = S.task_rank[ro[pos - 1]];
         } else {
           auto bounds = [&](int64_t* lo, int64_t* hi) {
@@ -1795,6 +1814,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   const bool keep_lists = !full && (int32_t)S.pend_off_all.size() == S.n_jobs;
   std::vector<char> jdirty, listed;
   std::vector<int32_t> fresh_off, fresh;  // per dirty job: its tasks that entered Pending through an event
+  std::vector<int32_t> merge_tmp;
   auto task_before = [&](int32_t a, int32_t c) {
     if (S.task_order_prio && S.tasks_in[a].priority != S.tasks_in[c].priority)
       return S.tasks_in[a].priority > S.tasks_in[c].priority;
@@ -1840,11 +1860,12 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
       auto f0 = fresh.begin() + fresh_off[j], f1 = fresh.begin() + fresh_off[j + 1];
       f1 = std::remove_if(f0, f1, [&](int32_t t) { return listed[t] != 0; });  // already Pending before the event
       for (auto b = S.pend.begin() + S.pend_off[j]; b != S.pend.end(); ++b) listed[*b] = 0;
-      if (f0 != f1) {
+      if (f0 != f1) {  // a stable merge (old tasks first among equals) through one reused buffer
         std::sort(f0, f1, task_before);
-        const size_t mid = S.pend.size();
-        S.pend.insert(S.pend.end(), f0, f1);
-        std::inplace_merge(S.pend.begin() + S.pend_off[j], S.pend.begin() + mid, S.pend.end(), task_before);
+        const size_t o = S.pend_off[j], mid = S.pend.size();
+        merge_tmp.assign(S.pend.begin() + o, S.pend.begin() + mid);
+        S.pend.resize(mid + (f1 - f0));
+        std::merge(merge_tmp.begin(), merge_tmp.end(), f0, f1, S.pend.begin() + o, task_before);
       }
       S.pend_len[j] = (int32_t)S.pend.size() - S.pend_off[j];
       continue;

@@ -228,7 +228,8 @@ struct Session {
   // so a task added by an update takes a rank between its neighbours' without
   // re-ranking its job; equal UIDs share a rank. Only compared within a job.
   std::vector<int64_t> task_rank;
-  std::vector<int32_t> job_frank;                        // (CreationTimestamp, UID) order
+  std::vector<uint64_t> task_uid_key;  // first 8 UID bytes, big-endian, zero-padded: a prefix of the byte order
+  std::vector<int32_t> job_frank;                       // (CreationTimestamp, UID) order
   std::vector<int32_t> job_by_frank;                     // inverse of job_frank
   std::vector<uint32_t> job_prank;                       // dense rank of -Priority
   std::vector<int32_t> job_queue;                        // job -> queue index
