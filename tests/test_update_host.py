@@ -64,7 +64,23 @@ def events(f0, changes):
     return evs, keep, tidx
 
 
-def check(tools, fx0, seed, rounds):
+def tricky_uids(cur, ch, r):
+    """New pods renamed after a pod of their own job, so their UIDs tie with it
+    in the first 8 bytes, are a prefix of it, or extend it: the update ranks
+    them by UID (bytewise) between the job's ranked tasks."""
+    group = lambda p: (p.get("namespace", ""), (p.get("annotations") or {}).get("scheduling.k8s.io/group-name"))
+    members = {}
+    for p in cur["pods"]:
+        members.setdefault(group(p), []).append(p["uid"])
+    for i, (kind, p) in enumerate(ch):
+        if kind != "pod_add" or not members.get(group(p)):
+            continue
+        base = sorted(members[group(p)])[i % len(members[group(p)])]
+        tag = f"{r}{i:04d}"
+        p["uid"] = (base[:8] + "~" + tag, base[:8] + tag, base[:3] + tag, base + tag, base[:5] + "!" + tag)[i % 5]
+
+
+def check(tools, fx0, seed, rounds, rename=False):
     from kbgpu import _abi, synth
     from kbgpu.api import PENDING, RefPanic
     try:
@@ -77,6 +93,8 @@ def check(tools, fx0, seed, rounds):
     ref = run_oracle(cur)
     for r in range(rounds):
         ch, nxt = synth.churn(cur, seed * 31 + r, uids, ref["decisions"] if ref["status"] == "ok" else [])
+        if rename:
+            tricky_uids(cur, ch, r)
         changes += ch
         uids |= {p["uid"] for kind, p in ch if kind == "pod_add"}
         cur = nxt
@@ -138,3 +156,12 @@ def test_update_host_contended(tools, seed):
 def test_update_host_c1(tools):
     from kbgpu import synth
     check(tools, synth.config_fixture(1), 1, 3)
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_update_host_uid_order(tools, seed):
+    """New pods whose UIDs share their first 8 bytes with (or are prefixes of)
+    their job's ranked tasks: the update's prefix keys fall back to the full
+    bytewise compare, and the pending order equals a fresh open's."""
+    from kbgpu import synth
+    check(tools, synth.random_fixture(9000 + seed, max_tasks=12), seed, 3, rename=True)
