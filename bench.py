@@ -18,8 +18,11 @@ roofline    = SURVEY §8(d) at the cycle level, in full-scan mode (every task
 scan_kernel = the dominant kernel against its physical ceilings: PMC HBM bytes
               and PMC VALU wave instructions per launch over its HIP-event time
 cpu_baseline= the kbref oracle on this host, CPU model stated: B-ref (1 thread),
-              B-omp (every core of the job's share, <= 16), B-faithful (the
-              per-call podLister walk, 60 s budget); C4 runs 60 s samples
+              B-omp (the best of 16, 64 and every CPU the job may use, the
+              sweep beside it), B-faithful (the per-call podLister walk, 20 s
+              budget); C3 runs 20 s samples, C4 60 s samples
+--gpus N    = N ranks: under torchrun its WORLD_SIZE must be N; without a
+              launcher bench.py starts the N rank processes itself
 N > 1       = ONE cluster with its node axis sharded over the N GPUs (SURVEY §8e,
               DESIGN.md §7): rank 0 runs the ordering engine and broadcasts each
               batch, each rank scans its node rows and resolves the tasks its
@@ -93,10 +96,46 @@ def job_cpus():
     return list(range(os.cpu_count() or 1))
 
 
-def omp_threads():
-    # the box's CPU share for one GPU is 16 cores (gpurun contract): B-omp uses
-    # every core the job may use, at most that share
-    return max(1, min(16, len(job_cpus())))
+def omp_sweep():
+    """B-omp thread counts: 16, 64 and every CPU the job may run on (SURVEY
+    §8(d): the node loop parallelised over all host cores, stated)."""
+    n = len(job_cpus())
+    return sorted({t for t in (16, 64) if t < n} | {n})
+
+
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: N child processes of this script, rank r
+    on GPU r (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment,
+    rendezvous on 127.0.0.1), started before this process touches a GPU; the
+    parent only waits for them (no exec). A rank that fails ends the others,
+    so none is left blocked in a collective. Rank 0 prints the result line on
+    the inherited stdout."""
+    import signal
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    log(f"bench: started {n} ranks (pids {', '.join(str(p.pid) for p in procs)})")
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                log(f"bench: rank pid {p.pid} exited with {c}; stopping the other ranks")
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
 
 
 _FX_FILES = {}
@@ -191,7 +230,6 @@ def valu_ceiling(pmc, avg_us):
 
 
 def main():
-    _capture_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
@@ -205,11 +243,30 @@ def main():
     ap.add_argument("--comm", action="store_true",
                     help="open the session through the RCCL sharded entry point even at N=1 (rehearsal)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on MI355X; gloo to rehearse on one GPU")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch, rendezvous and report without touching a GPU (CPU test of --gpus)")
     args = ap.parse_args()
+    # --gpus N is authoritative: without a launcher start N ranks, under one
+    # its world size must agree
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        log(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={os.environ['WORLD_SIZE']} ranks")
+        sys.exit(2)
+    _capture_stdout()
 
     import torch
     from kbgpu import dist as kdist
     rank, world, local_rank = kdist.env_rank()
+    if args.dry_run:
+        kdist.init("gloo")
+        log(f"bench: rank {rank} of {world} (local rank {local_rank}) up, dry run")
+        kdist.barrier()
+        _, ranks = kdist.aggregate(0.0, 1, sharded=False)
+        if rank == 0:
+            emit({"metric": "dry run", "value": None, "n_gpus": world, "ranks_reporting": ranks, "dry_run": True})
+        kdist.shutdown()
+        return
     # KBG_BENCH_DEVICE pins every rank to one device (rehearsal on a 1-GPU box only)
     device = int(os.environ.get("KBG_BENCH_DEVICE", local_rank))
     torch.cuda.set_device(device)
@@ -405,12 +462,18 @@ def main():
     if world == 1 and not args.no_resident:
         line["resident_session"] = resident_bench(cache, fx, base_opts)
     if world == 1 and not args.no_cpu_baseline:  # the CPU baseline is an N=1 figure
-        # C4 cannot finish on one thread within minutes: bounded samples there
-        budget = 60.0 if cid >= 4 else 0.0
+        # bounded samples where a full cycle takes longer than ~30 s of CPU
+        # (C3's failing tasks walk every node, C4 is 500k tasks)
+        budget = {1: 0.0, 2: 0.0, 3: 20.0}.get(cid, 60.0)
         line["cpu_baseline"] = cpu_baseline(fx, f"C{cid}", 1, budget=budget)
-        line["cpu_baseline_omp"] = cpu_baseline(fx, f"C{cid}", omp_threads(), budget=budget)
+        sweep = [cpu_baseline(fx, f"C{cid}", t, budget=budget) for t in omp_sweep()]
+        sweep = [b for b in sweep if b]
+        if sweep:
+            line["cpu_baseline_omp"] = max(sweep, key=lambda b: b["value"])
+            line["cpu_baseline_omp_sweep"] = [{"cores": b["cores"], "value": b["value"], "sample": b["sample"]}
+                                              for b in sweep]
         if not args.no_faithful:
-            line["cpu_baseline_faithful"] = cpu_baseline(fx, f"C{cid}", 1, faithful=True, budget=60.0)
+            line["cpu_baseline_faithful"] = cpu_baseline(fx, f"C{cid}", 1, faithful=True, budget=20.0)
     if rank == 0:
         emit(line)
     if comm is not None:

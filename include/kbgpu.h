@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KBG_ABI_VERSION 8
+#define KBG_ABI_VERSION 9
 
 typedef enum kbg_status {
   KBG_OK = 0,
@@ -194,9 +194,21 @@ typedef struct kbg_toleration {
 } kbg_toleration;
 
 typedef struct kbg_plugin_option {
-  int32_t name;   /* string id of the plugin name; unknown names are ignored (framework.go:30-35) */
-  uint32_t flags; /* KBG_DISABLE_* */
+  int32_t name;   /* string id of the plugin name (conf.PluginOption.Name) */
+  uint32_t flags; /* KBG_DISABLE_*, and KBG_PLUGIN_REGISTERED (see kbg_options.plugin_registry) */
 } kbg_plugin_option;
+
+/* framework.OpenSession instantiates a tier entry only when the process has a
+ * builder registered under its name (framework.go:30-35, RegisterPluginBuilder
+ * plugins.go:28-33); a name without one is skipped. The caller reports its
+ * registry with this flag on every entry when kbg_options.plugin_registry = 1:
+ * an entry without the flag is skipped (even one of the five names this path
+ * implements); an entry with it whose name is not one of priority, gang, drf,
+ * predicates, proportion is a plugin this path cannot evaluate, and
+ * kbg_session_open returns KBG_E_UNSUPPORTED (the caller runs the reference
+ * path). With plugin_registry = 0 the five names are taken as registered and
+ * every other name as unregistered. */
+#define KBG_PLUGIN_REGISTERED 0x80000000u
 
 typedef struct kbg_snapshot {
   const char* const* strings;
@@ -233,7 +245,8 @@ typedef struct kbg_options {
                            shard lives in this process (same layout and exchange buffer as the
                            multi-GPU path, for single-device parity runs); with one (see
                            kbg_session_open_sharded) it must equal the communicator size. */
-  int32_t reserved[6];
+  int32_t plugin_registry; /* 1 = kbg_plugin_option.flags carry KBG_PLUGIN_REGISTERED (framework.go:30-35) */
+  int32_t reserved[5];
 } kbg_options;
 
 /* One placement decision, in reference order. */
@@ -439,10 +452,16 @@ typedef struct kbg_event {
   const char* pod_key;   /* POD_ADD: "<namespace>/<name>" */
 } kbg_event;
 /* Applies events[0..n) in order; the cycle state is reset as by
- * kbg_session_reset. KBG_E_REF_PANIC: the cache itself would panic (a
- * Resource.Sub underflow in AddTask / RemoveTask / SetNode); the session must
- * then be re-opened. KBG_E_UNSUPPORTED (session unchanged): a removed pod whose
- * key is held by a pod outside the session jobs, or that used host ports. */
+ * kbg_session_reset (node table, class masks, plugin state back to the
+ * updated snapshot, whatever actions ran since the last open / reset / update).
+ * KBG_E_UNSUPPORTED and KBG_E_INVALID found before the first event is applied
+ * leave the session unchanged: an event naming a deleted task or an index out
+ * of range, a removed pod whose key is held on its node by a pod outside the
+ * session jobs, a pod with host ports leaving a node, a node update of a node
+ * the cache only knows from a pod. KBG_E_REF_PANIC (the cache itself would
+ * panic: a Resource.Sub underflow in AddTask / RemoveTask / SetNode) is found
+ * while the events are applied: the session is then unusable and every later
+ * call on it but kbg_session_close returns KBG_E_INVALID (re-open it). */
 kbg_status kbg_session_update(kbg_session* s, const kbg_event* events, int32_t n);
 
 /* Restores the state captured at kbg_session_open (device-side copy); used to

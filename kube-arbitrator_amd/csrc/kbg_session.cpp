@@ -557,8 +557,10 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   if (S.owner && S.comm) {  // owner-resolve: the rows' availability over the ranks, in the same round trip
     uint32_t* d_avail = S.d_down + down;
     HIP_TRY(kbg::launch_avail(S.d_down, G, 1u << S.shard, d_avail, S.stream));
-    const ncclResult_t nr = ncclAllReduce(d_avail, d_avail, (size_t)G, ncclUint32, ncclSum, S.comm->nccl, S.stream);
-    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+    if (S.comm->nccl) {  // (a communicator without RCCL — R sessions of one process, tools — sums on the host)
+      const ncclResult_t nr = ncclAllReduce(d_avail, d_avail, (size_t)G, ncclUint32, ncclSum, S.comm->nccl, S.stream);
+      if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+    }
     down += (size_t)G;
   }
   HIP_TRY(hipMemcpyAsync(sg.h_down, S.d_down, down * 4, hipMemcpyDeviceToHost, S.stream));
@@ -1320,15 +1322,42 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
     S.node_task_order[n].assign(snap->node_tasks + nd.task_off, snap->node_tasks + nd.task_off + nd.task_len);
     for (int32_t i = 0; i < nd.key_len; ++i) S.node_key_order[n].push_back(S.canon[snap->node_pod_keys[nd.key_off + i]]);
   }
+  // keys held on a node by pods outside the session jobs: no event ever
+  // names those pods, so the set holds for the whole resident session
+  S.outsider_keys.clear();
+  for (int32_t n = 0; n < S.n_nodes; ++n) {
+    if (S.node_key_order[n].size() == S.node_task_order[n].size()) continue;  // every entry is a session task's
+    std::unordered_set<int32_t> mine;
+    for (int32_t t : S.node_task_order[n]) mine.insert(S.canon[S.tasks_in[t].pod_key]);
+    for (int32_t k : S.node_key_order[n])
+      if (!mine.count(k)) S.outsider_keys.insert(((int64_t)n << 32) | (uint32_t)k);
+  }
+  S.broken.clear();
   S.node_of.clear();
   for (int32_t n = 0; n < S.n_nodes; ++n) S.node_of[S.canon[S.nodes_in[n].name]] = n;
 
-  // ---- plugins (framework.go:26-46; unknown names ignored)
+  // ---- plugins (framework.go:26-46): a tier entry counts only when the
+  // caller's process has a builder under its name (GetPluginBuilder); one of
+  // its own builders this path cannot evaluate refuses the session
+  std::vector<char> active(snap->n_plugins, 1);
+  {
+    static const char* const kImplemented[] = {"priority", "gang", "drf", "predicates", "proportion"};
+    for (int32_t p = 0; p < snap->n_plugins; ++p) {
+      const std::string& name = S.strs[snap->plugins[p].name];
+      const bool known = std::find(std::begin(kImplemented), std::end(kImplemented), name) != std::end(kImplemented);
+      const bool registered = S.opts.plugin_registry ? (snap->plugins[p].flags & KBG_PLUGIN_REGISTERED) != 0 : known;
+      if (registered && !known)
+        return fail(KBG_E_UNSUPPORTED, "plugin \"" + name + "\" is registered in the caller's process but the device "
+                                       "path does not implement it (framework.go:30-35): run the reference path");
+      active[p] = registered;
+    }
+  }
   {
     int32_t p = 0;
     bool seen_prio = false, seen_gang = false, seen_drf = false;
     for (int32_t ti = 0; ti < snap->n_tiers; ++ti)
       for (int32_t k = 0; k < snap->tier_sizes[ti]; ++k, ++p) {
+        if (!active[p]) continue;
         const kbg_plugin_option& po = snap->plugins[p];
         const std::string& name = S.strs[po.name];
         const uint32_t f = po.flags;
@@ -1357,6 +1386,7 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
     for (int32_t ti = 0; ti < snap->n_tiers; ++ti) {
       int32_t pre = 0, rec = 0;
       for (int32_t k = 0; k < snap->tier_sizes[ti]; ++k, ++p) {
+        if (!active[p]) continue;
         const std::string& name = S.strs[snap->plugins[p].name];
         const uint32_t f = snap->plugins[p].flags;
         if (name == "gang" && !(f & KBG_DISABLE_PREEMPTABLE)) pre |= kbg::VP_GANG;
@@ -4665,6 +4695,115 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
   return fail(KBG_E_INVALID, "event kind");
 }
 
+// The refusals of an event batch (KBG_E_INVALID, KBG_E_UNSUPPORTED), found by
+// walking the events over an overlay of what they change — task liveness,
+// each changed task's node and status, the session task holding a pod key on
+// a node — before the first one is applied, so a refused batch leaves the
+// session unchanged. The walk follows apply_event: deleteTask's node side
+// (in_node_remove) finds the key's holder, addTask's (in_node_add) takes the
+// key when no pod holds it (node_info.go:101-157).
+kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
+  auto status_ok = [](int32_t st) { return st > 0 && st <= KBG_UNKNOWN && !(st & (st - 1)); };
+  bool port_specs = false;
+  for (const kbg_spec& sp : S.specs_in) port_specs |= sp.has_host_ports != 0;
+  const bool holders = port_specs || !S.outsider_keys.empty();  // else no removal can be refused
+  int32_t adds = 0;
+  for (int32_t i = 0; i < n; ++i) adds += ev[i].kind == KBG_EV_POD_ADD;
+  const int32_t T0 = S.n_tasks;
+  std::vector<uint8_t> dead(S.n_tasks + adds, 0);
+  for (int32_t t = 0; t < T0; ++t) dead[t] = !S.task_live[t];
+  struct Now { int32_t node, status, key, spec; };
+  std::unordered_map<int32_t, Now> now;            // tasks an earlier event of the batch changed or added
+  std::unordered_map<int64_t, int32_t> hold;       // (node << 32 | key) -> holding session task, -1 none
+  std::unordered_map<std::string, int32_t> fresh;  // pod keys the session has not interned yet
+  auto task_now = [&](int32_t t) -> Now {
+    auto it = now.find(t);
+    if (it != now.end()) return it->second;
+    const kbg_task& k = S.tasks_in[t];
+    return Now{S.task_node[t], k.status, S.canon[k.pod_key], k.spec};
+  };
+  auto holder = [&](int32_t nd, int32_t key) -> int32_t {  // -2: a pod outside the session jobs
+    const int64_t hk = ((int64_t)nd << 32) | (uint32_t)key;
+    auto it = hold.find(hk);
+    if (it != hold.end()) return it->second;
+    if (S.outsider_keys.count(hk)) return -2;
+    for (int32_t u : S.node_task_order[nd])
+      if (S.canon[S.tasks_in[u].pod_key] == key) return u;
+    return -1;
+  };
+  int32_t T = T0;
+  for (int32_t i = 0; i < n; ++i) {
+    const kbg_event& e = ev[i];
+    switch (e.kind) {
+      case KBG_EV_POD_UPDATE:
+      case KBG_EV_POD_DELETE: {
+        const int32_t t = e.task;
+        if (t < 0 || t >= T || dead[t]) return fail(KBG_E_INVALID, "event task index");
+        if (e.kind == KBG_EV_POD_UPDATE && (!status_ok(e.status) || e.node < -1 || e.node >= S.n_nodes))
+          return fail(KBG_E_INVALID, "event status / node");
+        if (!holders) {
+          if (e.kind == KBG_EV_POD_DELETE) dead[t] = 1;
+          break;
+        }
+        Now c = task_now(t);
+        bool found = false;
+        if (c.node >= 0) {
+          const int32_t h = holder(c.node, c.key);
+          if (h == -2)
+            return fail(KBG_E_UNSUPPORTED, "the pod key is held on the node by a pod outside the session jobs "
+                                           "(its resources are unknown): re-open the session");
+          if (h >= 0) {
+            const int32_t sp = task_now(h).spec;
+            if (sp >= 0 && S.specs_in[sp].has_host_ports)
+              return fail(KBG_E_UNSUPPORTED, "a pod with host ports leaves a node (its used ports are a set over "
+                                             "every pod): re-open the session");
+            hold[((int64_t)c.node << 32) | (uint32_t)c.key] = -1;
+            found = true;
+          }
+        }
+        if (e.kind == KBG_EV_POD_DELETE || (c.node >= 0 && !found)) {  // deleted, or updateTask stopped
+          dead[t] = 1;
+          break;
+        }
+        c.node = e.node;
+        c.status = e.status;
+        now[t] = c;
+        if (c.node >= 0 && !terminated(c.status) && holder(c.node, c.key) == -1)
+          hold[((int64_t)c.node << 32) | (uint32_t)c.key] = t;
+        break;
+      }
+      case KBG_EV_POD_ADD: {
+        if (e.job < 0 || e.job >= S.n_jobs || e.spec < -1 || e.spec >= (int32_t)S.specs_in.size() ||
+            !status_ok(e.status) || e.node < -1 || e.node >= S.n_nodes || !e.uid || !e.pod_key)
+          return fail(KBG_E_INVALID, "POD_ADD event");
+        const int32_t t = T++;
+        if (!holders) break;
+        int32_t key;
+        auto ci = S.canon_of.find(e.pod_key);
+        if (ci != S.canon_of.end()) {
+          key = ci->second;
+        } else {
+          key = (int32_t)S.strs.size() + (int32_t)fresh.size();
+          key = fresh.emplace(e.pod_key, key).first->second;
+        }
+        const Now c{e.node, e.status, key, e.spec};
+        now[t] = c;
+        if (c.node >= 0 && !terminated(c.status) && holder(c.node, c.key) == -1)
+          hold[((int64_t)c.node << 32) | (uint32_t)c.key] = t;
+        break;
+      }
+      case KBG_EV_NODE_UPDATE:
+        if (e.node < 0 || e.node >= S.n_nodes) return fail(KBG_E_INVALID, "event node index");
+        if (!S.nodes_in[e.node].has_node)
+          return fail(KBG_E_UNSUPPORTED, "update of a node the cache only knows from a pod: re-open");
+        break;
+      default:
+        return fail(KBG_E_INVALID, "event kind");
+    }
+  }
+  return KBG_OK;
+}
+
 kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
   const auto t0 = std::chrono::steady_clock::now();
   if (n < 0 || (n > 0 && !ev)) return fail(KBG_E_INVALID, "events");
@@ -4727,15 +4866,23 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
       if (cnt == 0) break;
       HIP_TRY(hipMemcpyAsync(S.d_deltas, S.h_deltas, cnt * sizeof(kbg::NodeDelta), hipMemcpyHostToDevice, S.stream));
       HIP_TRY(kbg::launch_apply(S.d_nodes0, S.d_deltas, cnt, S.stream));
-      HIP_TRY(kbg::launch_apply(S.d_nodes, S.d_deltas, cnt, S.stream));
-      HIP_TRY(hipStreamSynchronize(S.stream));  // staging reuse
+      if ((st = stage_release(S)) != KBG_OK) return st;
     }
+    // the live table restarts from the updated snapshot: the rows an action
+    // committed since the last reset are stale whether or not an event touched them
+    if ((st = copy_soa(S, S.d_nodes, S.d_nodes0)) != KBG_OK) return st;
+    S.idle = S.idle0;
+    S.rel = S.rel0;
+    S.ntasks = S.ntasks0;
+    S.node_keys = S.node_keys0;
+    S.port_hold.clear();
     // host ports / pod affinity live in the class masks: refold them
     if (had_masks || S.has_ports || S.has_aff) {
       S.h_class_mask = S.h_class_mask_static;
       setup_host_ports(S);
       setup_affinity(S);
       S.mask_dirty.clear();
+      std::fill(S.mask_dirty_flag.begin(), S.mask_dirty_flag.end(), 0);
       HIP_TRY(hipMemcpy(S.d_class_mask, S.h_class_mask.data(), S.h_class_mask.size() * 8, hipMemcpyHostToDevice));
     }
     S.h_class_mask0 = S.h_class_mask;
@@ -4752,6 +4899,16 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
 }  // namespace
 
 // ================================================================== C ABI
+namespace {
+// A session whose update failed part-way answers nothing but close.
+kbg_status usable(kbg_session* s) {
+  if (!s) return fail(KBG_E_INVALID, "null session");
+  if (!s->s.broken.empty())
+    return fail(KBG_E_INVALID, "the session is unusable after a failed kbg_session_update (" + s->s.broken + "): re-open it");
+  return KBG_OK;
+}
+}  // namespace
+
 extern "C" {
 
 int32_t kbg_abi_version(void) { return KBG_ABI_VERSION; }
@@ -4834,7 +4991,7 @@ void kbg_comm_destroy(kbg_comm* c) {
 }
 
 kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out) {
-  if (!s) return fail(KBG_E_INVALID, "null session");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
   HIP_TRY(hipSetDevice(s->s.device));
   try {
     if (owner_resolve_ok(s->s)) {
@@ -4848,7 +5005,7 @@ kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t*
 }
 
 kbg_status kbg_backfill(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out) {
-  if (!s) return fail(KBG_E_INVALID, "null session");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
   HIP_TRY(hipSetDevice(s->s.device));
   try {
     return backfill_cycle(s->s, out, cap, n_out);
@@ -4858,7 +5015,7 @@ kbg_status kbg_backfill(kbg_session* s, kbg_decision* out, int32_t cap, int32_t*
 }
 
 kbg_status kbg_reclaim(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out) {
-  if (!s) return fail(KBG_E_INVALID, "null session");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
   HIP_TRY(hipSetDevice(s->s.device));
   try {
     return reclaim_cycle(s->s, out, cap, n_out);
@@ -4868,7 +5025,7 @@ kbg_status kbg_reclaim(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* 
 }
 
 kbg_status kbg_preempt(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out) {
-  if (!s) return fail(KBG_E_INVALID, "null session");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
   HIP_TRY(hipSetDevice(s->s.device));
   try {
     return preempt_cycle(s->s, out, cap, n_out);
@@ -4878,7 +5035,7 @@ kbg_status kbg_preempt(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* 
 }
 
 kbg_status kbg_evictions_get(kbg_session* s, kbg_eviction* out, int32_t cap, int32_t* n_out) {
-  if (!s) return fail(KBG_E_INVALID, "null session");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
   const auto& ev = s->s.evictions;
   if (n_out) *n_out = (int32_t)ev.size();
   if (!out && cap == 0) return KBG_OK;  // size query
@@ -4889,7 +5046,7 @@ kbg_status kbg_evictions_get(kbg_session* s, kbg_eviction* out, int32_t cap, int
 }
 
 kbg_status kbg_decision_actions_get(kbg_session* s, int32_t* out, int32_t cap, int32_t* n_out) {
-  if (!s) return fail(KBG_E_INVALID, "null session");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
   const auto& a = s->s.dec_action;
   if (n_out) *n_out = (int32_t)a.size();
   if (!out && cap == 0) return KBG_OK;  // size query
@@ -4900,7 +5057,7 @@ kbg_status kbg_decision_actions_get(kbg_session* s, int32_t* out, int32_t cap, i
 }
 
 kbg_status kbg_session_reset(kbg_session* s) {
-  if (!s) return fail(KBG_E_INVALID, "null session");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
   Session& S = s->s;
   HIP_TRY(hipSetDevice(S.device));
   S.idle = S.idle0;
@@ -4924,18 +5081,25 @@ kbg_status kbg_session_reset(kbg_session* s) {
 }
 
 kbg_status kbg_session_update(kbg_session* s, const kbg_event* events, int32_t n) {
-  if (!s) return fail(KBG_E_INVALID, "null session");
-  HIP_TRY(hipSetDevice(s->s.device));
+  if (kbg_status st = usable(s); st != KBG_OK) return st;
+  Session& S = s->s;
+  HIP_TRY(hipSetDevice(S.device));
+  if (n < 0 || (n > 0 && !events)) return fail(KBG_E_INVALID, "events");
+  kbg_status st;
   try {
-    return session_update(s->s, events, n);
+    if ((st = update_precheck(S, events, n)) != KBG_OK) return st;  // refused: nothing changed
+    st = session_update(S, events, n);
   } catch (const std::bad_alloc&) {
-    return fail(KBG_E_NOMEM, "host allocation failed");
+    st = fail(KBG_E_NOMEM, "host allocation failed");
   }
+  if (st != KBG_OK) S.broken = g_err;  // events were applied part-way
+  return st;
 }
 
 kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t stop_at_first_success, int32_t* out_node,
                       int32_t* out_kind, int32_t* n_evaluated) {
-  if (!s || (n > 0 && (!tasks || !out_node))) return fail(KBG_E_INVALID, "null argument");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
+  if (n > 0 && (!tasks || !out_node)) return fail(KBG_E_INVALID, "null argument");
   Session& S = s->s;
   HIP_TRY(hipSetDevice(S.device));
   for (int32_t i = 0; i < n; ++i)
@@ -4998,7 +5162,8 @@ kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t s
 }
 
 kbg_status kbg_apply(kbg_session* s, int32_t node, const kbg_resource* req, int32_t kind) {
-  if (!s || !req) return fail(KBG_E_INVALID, "null argument");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
+  if (!req) return fail(KBG_E_INVALID, "null argument");
   Session& S = s->s;
   if (node < 0 || node >= S.n_nodes) return fail(KBG_E_INVALID, "node index");
   HIP_TRY(hipSetDevice(S.device));
@@ -5015,7 +5180,8 @@ kbg_status kbg_apply(kbg_session* s, int32_t node, const kbg_resource* req, int3
 }
 
 kbg_status kbg_job_state_get(kbg_session* s, int32_t job, kbg_job_state* out) {
-  if (!s || !out) return fail(KBG_E_INVALID, "null argument");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
+  if (!out) return fail(KBG_E_INVALID, "null argument");
   Session& S = s->s;
   if (job < 0 || job >= S.n_jobs) return fail(KBG_E_INVALID, "job index");
   const Engine& E = S.cycle_started ? S.fin : S.init;
@@ -5037,7 +5203,8 @@ kbg_status kbg_job_state_get(kbg_session* s, int32_t job, kbg_job_state* out) {
 }
 
 kbg_status kbg_queue_state_get(kbg_session* s, int32_t queue, kbg_queue_state* out) {
-  if (!s || !out) return fail(KBG_E_INVALID, "null argument");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
+  if (!out) return fail(KBG_E_INVALID, "null argument");
   Session& S = s->s;
   if (queue < 0 || queue >= S.n_queues) return fail(KBG_E_INVALID, "queue index");
   const Engine& E = S.cycle_started ? S.fin : S.init;
@@ -5051,7 +5218,8 @@ kbg_status kbg_queue_state_get(kbg_session* s, int32_t queue, kbg_queue_state* o
 }
 
 kbg_status kbg_node_state_get(kbg_session* s, int32_t node, kbg_node_state* out) {
-  if (!s || !out) return fail(KBG_E_INVALID, "null argument");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
+  if (!out) return fail(KBG_E_INVALID, "null argument");
   Session& S = s->s;
   if (node < 0 || node >= S.n_nodes) return fail(KBG_E_INVALID, "node index");
   out->idle = to_kres(S.idle[node]);
@@ -5061,7 +5229,8 @@ kbg_status kbg_node_state_get(kbg_session* s, int32_t node, kbg_node_state* out)
 }
 
 kbg_status kbg_stats_get(kbg_session* s, kbg_stats* out) {
-  if (!s || !out) return fail(KBG_E_INVALID, "null argument");
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
+  if (!out) return fail(KBG_E_INVALID, "null argument");
   *out = s->s.stats;
   return KBG_OK;
 }

@@ -368,6 +368,8 @@ struct Session {
   std::vector<std::vector<int32_t>> node_task_order;  // per node: the session tasks in NodeInfo.Tasks order
   std::vector<std::vector<int32_t>> node_key_order;   // per node: PodKey (canonical id) of every pod on it
   std::vector<kbg_resource> others_in;                // Session.Others resreq
+  std::unordered_set<int64_t> outsider_keys;          // (node << 32 | key) held by pods outside the session jobs
+  std::string broken;                                 // non-empty: an update failed part-way, re-open
   bool task_ranks_stale = false;                      // tasks were added: re-rank their jobs' UIDs
   std::vector<int32_t> rank_dirty_jobs;
   std::vector<int32_t> spec_class;                    // per spec: its static class (-1: none compiled)

@@ -34,8 +34,9 @@ DISABLE_PREEMPTABLE = 1 << 3
 DISABLE_RECLAIMABLE = 1 << 4
 DISABLE_QUEUE_ORDER = 1 << 5
 DISABLE_PREDICATE = 1 << 6
+PLUGIN_REGISTERED = 0x80000000  # kbg_plugin_option.flags, read when kbg_options.plugin_registry = 1
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 COMM_ID_BYTES = 128
 
 KIND_ALLOCATE = 0
@@ -137,7 +138,7 @@ class kbg_snapshot(ctypes.Structure):
 
 class kbg_options(ctypes.Structure):
     _fields_ = [("device", i32), ("heap_rule", i32), ("batch_tasks", i32), ("candidates", i32),
-                ("full_scan", i32), ("shards", i32), ("reserved", i32 * 6)]
+                ("full_scan", i32), ("shards", i32), ("plugin_registry", i32), ("reserved", i32 * 5)]
 
 
 class kbg_decision(ctypes.Structure):

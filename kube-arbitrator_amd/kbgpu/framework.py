@@ -3,9 +3,12 @@
 `open_session` / `close_session` mirror framework.OpenSession / CloseSession
 (framework.go:26-54). The plugins named in the tiers (drf, proportion, gang,
 priority, predicates) run their OnSessionOpen inside the device library
-(kbg_session_open), which also uploads the node table to HBM; plugin names the
-library does not know are ignored, exactly like GetPluginBuilder misses
-(framework.go:30-35). `Session.allocate` / `Session.pipeline` /
+(kbg_session_open), which also uploads the node table to HBM. Every tier
+entry goes to the library with KBG_PLUGIN_REGISTERED set when this process's
+registry has a builder for its name (kbg_options.plugin_registry = 1): names
+without one are skipped, exactly like GetPluginBuilder misses
+(framework.go:30-35), and a registered plugin the library does not implement
+refuses the session (KBG_E_UNSUPPORTED: run the reference path). `Session.allocate` / `Session.pipeline` /
 `Session.dispatch` replay device decisions into the host objects with the
 reference's bookkeeping (session.go:205-316).
 """
@@ -56,10 +59,12 @@ class Session:
         self.others = snap.others
         self.tiers = tiers
         self.plugins = [p.name for t in tiers for p in t.plugins if get_plugin_builder(p.name) is not None]
-        self.flat = FlatSnapshot(self.nodes, self.jobs, self.queues, self.others, self._active_tiers())
+        self.flat = FlatSnapshot(self.nodes, self.jobs, self.queues, self.others, self.tiers,
+                                 registered=lambda name: get_plugin_builder(name) is not None)
         self.handle = ctypes.c_void_p()
         opts = _abi.kbg_options()
         opts.device = -1
+        opts.plugin_registry = 1
         options = dict(options or {})
         comm = options.pop("comm", None)  # dist.ShardComm: node-axis shard of an RCCL clique
         for k, v in options.items():
@@ -74,10 +79,6 @@ class Session:
         self.decisions = []
         self.action_of = []  # action name of each decision of the cycle
         self.evictions = []  # (task, by, action) committed evictions (cache.Evict)
-
-    def _active_tiers(self):
-        from .conf import Tier
-        return [Tier([p for p in t.plugins if get_plugin_builder(p.name) is not None]) for t in self.tiers]
 
     # ---- session.go:205-241
     def pipeline(self, task, hostname):
@@ -155,6 +156,8 @@ class Session:
         nidx = {n: i for i, n in enumerate(self.flat.node_names)}
         evs = (_abi.kbg_event * max(1, len(changes)))()
         keep = []
+        objs = {}  # task index -> its TaskInfo after the events (applied once the library accepts them)
+        n_objs = len(self.flat.task_objs)
         for k, (kind, obj) in enumerate(changes):
             e = evs[k]
             if kind == "node_update":
@@ -171,7 +174,7 @@ class Session:
                 e.task = tidx[obj["uid"]]
                 e.status = ti.status
                 e.node = nidx.get(ti.node_name, -1) if ti.node_name else -1
-                self.flat.task_objs[e.task] = ti
+                objs[e.task] = ti
             elif kind == "pod_add":
                 e.kind = _abi.EV_POD_ADD
                 e.job = self.flat.job_index[ti.job]
@@ -182,11 +185,16 @@ class Session:
                 e.resource = _abi.kbg_resource(*ti.resreq.as_tuple())
                 keep += [ti.uid.encode(), pod_key(obj).encode()]
                 e.uid, e.pod_key = keep[-2], keep[-1]
-                tidx[ti.uid] = len(self.flat.task_objs)
-                self.flat.task_objs.append(ti)
+                tidx[ti.uid] = n_objs
+                objs[n_objs] = ti
+                n_objs += 1
             else:
                 raise ValueError(f"unknown change {kind}")
         _abi.check(_abi.lib().kbg_session_update(self.handle, evs, len(changes)))
+        for i in range(len(self.flat.task_objs), n_objs):
+            self.flat.task_objs.append(None)
+        for i, ti in objs.items():
+            self.flat.task_objs[i] = ti
         from .api import PENDING
         live = set(tidx)  # (deleted pods keep their index; counts only size output buffers)
         self.flat.pending_all = max(self.flat.pending_all, sum(1 for t in self.flat.task_objs

@@ -53,7 +53,7 @@ def _spec_key(pod, with_identity):
 class FlatSnapshot:
     """Owns the arrays behind one kbg_snapshot (keeps them alive for the call)."""
 
-    def __init__(self, nodes, jobs, queues, others, tiers):
+    def __init__(self, nodes, jobs, queues, others, tiers, registered=None):
         S = Interner()
         self.interner = S
         # queues
@@ -211,8 +211,9 @@ class FlatSnapshot:
         plugin_rows, tier_sizes = [], []
         for tier in tiers:
             tier_sizes.append(len(tier.plugins))
-            for p in tier.plugins:
-                plugin_rows.append((S(p.name), p.flags()))
+            for p in tier.plugins:  # KBG_PLUGIN_REGISTERED: this process has a builder for the name
+                reg = _abi.PLUGIN_REGISTERED if registered is not None and registered(p.name) else 0
+                plugin_rows.append((S(p.name), p.flags() | reg))
         self.strings_c = (ctypes.c_char_p * max(1, len(S.strings)))(*[s.encode("utf-8") for s in S.strings])
         self.arrays = dict(
             nodes=nd, jobs=jb, tasks=tk, queues=qs, others=oth,

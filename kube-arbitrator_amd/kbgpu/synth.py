@@ -18,7 +18,7 @@ CONFIGS = {
                    [{"name": "drf"}, {"name": "predicates"}, {"name": "nodeorder"}]]),
     2: dict(nodes=1000, jobs=200, tasks_per_job=50, mix="hetero", queues=[("q1", 1), ("q2", 1)], tiers=None),
     3: dict(nodes=5000, jobs=2000, tasks_per_job=50, mix="hetero", queues=[("q1", 1), ("q2", 2), ("q3", 3), ("q4", 4)],
-            tiers=None),
+            tiers=None, over=1.15),
     4: dict(nodes=20000, jobs=10000, tasks_per_job=50, mix="hetero4", queues=[("q1", 1), ("q2", 2), ("q3", 3), ("q4", 4)],
             tiers=None),
 }
@@ -66,6 +66,8 @@ def config_fixture(cid):
     if cid == 6:  # not a BASELINE config: C3 with inter-pod (anti)affinity (scale check)
         return affinity_config()
     c = CONFIGS[cid]
+    if c.get("over"):
+        return over_requested_config(cid)
     rng = random.Random(BASE_SEED + cid)
     nodes = [_node(i, rng, c["mix"]) for i in range(c["nodes"])]
     queues = [{"name": q, "weight": w} for q, w in c["queues"]]
@@ -105,6 +107,103 @@ def config_fixture(cid):
             p.update(spec)
             pods.append(p)
     return {"name": f"C{cid}", "tiers": c["tiers"], "nodes": nodes, "pods": pods, "podGroups": pgs, "queues": queues}
+
+
+def over_requested_config(cid=3):
+    """BASELINE config 3 as SURVEY §8(d) specifies it: 5k nodes of the C2 mix,
+    2k gang PodGroups x 50 pending tasks, `minAvailable` in {1, 25, 50}, 4
+    proportion queues of weights {1, 2, 3, 4}, ALL over-requested: every
+    queue's request exceeds its deserved share (total x w / 10) in every
+    dimension (cpu, memory, GPU), so the proportion water-fill ends after one
+    round (proportion.go:102-144, no F9 hazard), demand exceeds capacity by
+    the factor `over`, queues become Overused (allocate.go:71-74,
+    proportion.go:188-193) and tasks fail once the cluster fills.
+    Jobs go to the queues in the weighted pattern q1 q2 q2 q3 q3 q3 q4 q4 q4 q4
+    (job j by j % 10), so each queue holds w / 10 of the jobs; one job in ten
+    is a GPU job (2 GPUs per task, tolerates the GPU nodes' taint), one per
+    pattern residue in every block of 100 jobs; 30% of the others carry a
+    zone / type node selector and 5% a required node affinity. A job's tasks
+    share one (cpu, memory) request, drawn per job and scaled so the total
+    requested is `over` x the cluster's allocatable in cpu and memory."""
+    c = CONFIGS[cid]
+    rng = random.Random(BASE_SEED + cid)
+    nodes = [_node(i, rng, c["mix"]) for i in range(c["nodes"])]
+    queues = [{"name": q, "weight": w} for q, w in c["queues"]]
+    pattern = [q for q, w in c["queues"] for _ in range(w)]  # weights in jobs out of every len(pattern)
+    total_cpu = sum(int(n["allocatable"]["cpu"]) * 1000 for n in nodes)        # milli
+    total_mem = sum(int(n["allocatable"]["memory"][:-2]) * 1024 for n in nodes)  # Mi
+    total_gpu = sum(int(n["allocatable"]["nvidia.com/gpu"]) for n in nodes)
+    J, T = c["jobs"], c["tasks_per_job"]
+    base = []
+    for j in range(J):
+        gpu_job = (j // len(pattern)) % len(pattern) == j % len(pattern)
+        base.append((rng.choice((1, 2, 3, 4, 6, 8)), rng.choice((2, 3, 4, 5, 6)), gpu_job, rng.random(), rng.random(),
+                     rng.randrange(4), rng.randrange(2), rng.randrange(3), rng.sample(range(50), 10), rng.random()))
+    cpu_scale = c["over"] * total_cpu / (T * sum(b[0] for b in base))
+    mem_scale = c["over"] * total_mem / (T * sum(b[0] * b[1] for b in base))
+    n_gpu_tasks = T * sum(1 for b in base if b[2])
+    gpus_per_task = max(1, -(-int(c["over"] * total_gpu) // max(1, n_gpu_tasks)))
+    pods, pgs = [], []
+    for j, (units, mem_per, gpu_job, r, r2, zone, typ, aff_kind, racks, mm) in enumerate(base):
+        ns = f"ns{j % 8}"
+        pg = f"pg-{j:05d}"
+        q = pattern[j % len(pattern)]
+        cpu = max(50, int(units * cpu_scale) // 50 * 50)
+        mem = max(64, int(units * mem_per * mem_scale) // 64 * 64)
+        req = {"cpu": f"{cpu}m", "memory": f"{mem}Mi"}
+        spec = {}
+        if gpu_job:
+            req["nvidia.com/gpu"] = str(gpus_per_task)
+            spec["tolerations"] = [{"key": "dedicated", "operator": "Equal", "value": "gpu", "effect": "NoSchedule"}]
+        elif r < 0.30:
+            spec["nodeSelector"] = {"zone": f"z{zone}"} if r2 < 0.5 else {"type": ("cpu", "mem")[typ]}
+        elif r < 0.35:
+            expr = ({"key": "rack", "operator": "In", "values": [f"r{x}" for x in racks]} if aff_kind == 0 else
+                    {"key": "zone", "operator": "NotIn", "values": [f"z{zone}"]} if aff_kind == 1 else
+                    {"key": "cores", "operator": "Gt", "values": ["40"]})
+            spec["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+                "nodeSelectorTerms": [{"matchExpressions": [expr]}]}}}
+        pgs.append({"namespace": ns, "name": pg, "minMember": (1, 25, 50)[int(mm * 3)], "queue": q,
+                    "creationTimestamp": (1_700_000_000 + j) * 1_000_000_000})
+        for t in range(T):
+            p = {"uid": f"uid-{j:05d}-{t:03d}", "namespace": ns, "name": f"{pg}-{t:03d}", "phase": "Pending",
+                 "annotations": {"scheduling.k8s.io/group-name": pg}, "containers": [{"requests": dict(req)}]}
+            p.update(spec)
+            pods.append(p)
+    return {"name": f"C{cid}", "tiers": c["tiers"], "nodes": nodes, "pods": pods, "podGroups": pgs, "queues": queues}
+
+
+def queue_demand(fx):
+    """Per queue: (weight, requested, total x weight / sum of weights) in
+    (milli-cpu, Mi, GPU) — the first water-fill round of proportion.go:102-144
+    (no Others: every pod belongs to a PodGroup)."""
+    def q(v, unit):
+        v = str(v)
+        if v.endswith("m"):
+            return int(v[:-1]) / 1000 * unit
+        if v.endswith("Mi"):
+            return int(v[:-2])
+        if v.endswith("Gi"):
+            return int(v[:-2]) * 1024
+        return float(v) * unit
+    tot = [0.0, 0.0, 0.0]
+    for n in fx["nodes"]:
+        a = n["allocatable"]
+        tot[0] += q(a["cpu"], 1000)
+        tot[1] += q(a["memory"], 1)
+        tot[2] += q(a.get("nvidia.com/gpu", "0"), 1)
+    pgq = {(g["namespace"], g["name"]): g["queue"] for g in fx["podGroups"]}
+    req = {}
+    for p in fx["pods"]:
+        r = p["containers"][0]["requests"]
+        k = pgq[(p["namespace"], p["annotations"]["scheduling.k8s.io/group-name"])]
+        acc = req.setdefault(k, [0.0, 0.0, 0.0])
+        acc[0] += q(r.get("cpu", "0"), 1000)
+        acc[1] += q(r.get("memory", "0"), 1)
+        acc[2] += q(r.get("nvidia.com/gpu", "0"), 1)
+    W = sum(x["weight"] for x in fx["queues"])
+    return {x["name"]: (x["weight"], req.get(x["name"], [0, 0, 0]), [t * x["weight"] / W for t in tot])
+            for x in fx["queues"]}
 
 
 def saturated_config(nodes=5000, jobs=2000, tasks_per_job=50, demand=1.08, seed=7):

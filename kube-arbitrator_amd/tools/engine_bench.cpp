@@ -329,3 +329,92 @@ extern "C" int32_t kbg_tool_sharded_allocate_rank(const kbg_snapshot* snap, cons
   host_close(S);
   return -(int32_t)st;
 }
+
+// ---------------------------------------------------------------------------
+// The owner-resolve protocol with R real device sessions on ONE GPU: rank r is
+// a session opened on `device` holding shard r of R (a communicator without
+// RCCL: the scan, select and availability kernels run on the device over the
+// rank's own words, the collectives are the in-process hub). Every rank but
+// rank 0 has its first 64-node word at w_lo > 0, so this runs exactly the
+// device code of a multi-GPU rank that a one-GPU box cannot host over RCCL
+// (kbg_select_kernel over [w_lo, w_hi), kbg_avail_kernel with bit 1 << r).
+namespace {
+struct DeviceLocalIO final : ShardIO {
+  LocalHub& hub;
+  int32_t me;
+  DeviceLocalIO(LocalHub& h, int32_t r) : hub(h), me(r) {}
+  kbg_status bcast(uint32_t* buf, size_t n) override {
+    if (me == 0) hub.slot[0].assign(buf, buf + n);
+    hub.bar.arrive_and_wait();
+    if (me != 0) std::copy(hub.slot[0].begin(), hub.slot[0].begin() + n, buf);
+    hub.bar.arrive_and_wait();
+    return KBG_OK;
+  }
+  kbg_status allreduce(uint32_t* buf, size_t n, bool sum) override {
+    hub.slot[me].assign(buf, buf + n);
+    hub.bar.arrive_and_wait();
+    for (size_t i = 0; i < n; ++i) {
+      uint32_t v = sum ? 0u : 0xffffffffu;
+      for (int32_t r = 0; r < hub.R; ++r) v = sum ? v + hub.slot[r][i] : std::min(v, hub.slot[r][i]);
+      buf[i] = v;
+    }
+    hub.bar.arrive_and_wait();
+    return KBG_OK;
+  }
+  kbg_status scan(Session& S, kbg::Stage& sg, int32_t G, int32_t base) override { return device_scan(S, sg, G, base); }
+  kbg_status scan_avail(Session& S, kbg::Stage& sg, int32_t G, int32_t base, uint32_t* avail) override {
+    kbg_status st = device_scan(S, sg, G, base);
+    if (st != KBG_OK) return st;
+    const uint32_t* h_avail = sg.h_down + G + sg.h_capoff[G];  // kbg_avail_kernel: this rank's bit per row
+    std::copy(h_avail, h_avail + G, avail);
+    return allreduce(avail, G, true);
+  }
+};
+}  // namespace
+
+extern "C" int32_t kbg_tool_sharded_allocate_device(const kbg_snapshot* snap, const kbg_options* o, int32_t R,
+                                                    int32_t device, kbg_decision* out, int32_t cap, int32_t* n_out,
+                                                    int64_t* stats) {
+  LocalHub hub(R);
+  std::vector<kbg_status> res(R, KBG_OK);
+  std::vector<std::string> err(R);
+  std::vector<kbg_comm> comms(R);
+  // every rank opens before any starts the protocol: an open failure returns
+  // from all of them (no collective is left waiting)
+  std::vector<std::unique_ptr<Session>> sess(R);
+  std::vector<std::thread> th;
+  for (int32_t r = 0; r < R; ++r) {
+    comms[r] = kbg_comm{nullptr, R, r, device};
+    sess[r].reset(new Session());
+  }
+  for (int32_t r = 0; r < R; ++r)
+    th.emplace_back([&, r]() {
+      kbg_status st = open_session(*sess[r], snap, o, &comms[r]);
+      if (st == KBG_OK && sess[r]->has_aff) st = fail(KBG_E_UNSUPPORTED, "pod affinity: the library resolves on every rank");
+      res[r] = st;
+      err[r] = g_err;
+    });
+  for (auto& t : th) t.join();
+  th.clear();
+  bool opened = true;
+  for (int32_t r = 0; r < R; ++r) opened &= res[r] == KBG_OK;
+  if (opened)
+    for (int32_t r = 0; r < R; ++r)
+      th.emplace_back([&, r]() {
+        Session& S = *sess[r];
+        (void)hipSetDevice(S.device);
+        DeviceLocalIO io(hub, r);
+        kbg_status st = allocate_sharded(S, io, out + (size_t)r * cap, cap, n_out + r);
+        tool_stats(S, stats ? stats + 5 * r : nullptr);
+        res[r] = st;
+        err[r] = g_err;
+      });
+  for (auto& t : th) t.join();
+  for (int32_t r = 0; r < R; ++r) free_device(*sess[r]);
+  for (int32_t r = 0; r < R; ++r)
+    if (res[r] != KBG_OK) {
+      g_err = err[r];
+      return -(int32_t)res[r];
+    }
+  return 0;
+}

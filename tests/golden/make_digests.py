@@ -8,6 +8,11 @@ and stores helpers.digest_outputs of its output.
 digest_c4.json        synth.config_fixture(4): BASELINE C4, 20k nodes x 500k tasks
 digest_saturated.json synth.saturated_config(): C3's cluster, per-task requests,
                       ~108% CPU demand (batch cuts and engine replays at K=8192)
+digest_c3.json        synth.config_fixture(3): BASELINE C3 as SURVEY §8(d) has it,
+                      5k nodes x 100k tasks, 4 queues all over-requested
+digest_c3_churn.json  C3 then 3 resident-session churn rounds (helpers.churn_chain):
+                      one digest per snapshot S0 .. S3
+digest_c4_churn.json  the same over C4
 """
 import json
 import os
@@ -27,7 +32,40 @@ from kbgpu import synth  # noqa: E402
 SESSIONS = {
     "c4": ("synth.config_fixture(4)", lambda: synth.config_fixture(4)),
     "saturated": ("synth.saturated_config()", lambda: synth.saturated_config()),
+    "c3": ("synth.config_fixture(3)", lambda: synth.config_fixture(3)),
 }
+CHAINS = {  # name: (generator text, fixture, churn seed, rounds)
+    "c3_churn": ("helpers.churn_chain(synth.config_fixture(3), 3, 3)", lambda: synth.config_fixture(3), 3, 3),
+    "c4_churn": ("helpers.churn_chain(synth.config_fixture(4), 4, 3)", lambda: synth.config_fixture(4), 4, 3),
+}
+
+
+def oracle(fx, _changes=None):
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "fx.json"), os.path.join(d, "out.json")
+        with open(src, "w") as f:
+            json.dump(fx, f)
+        threads = str(os.cpu_count() or 1)
+        subprocess.run([ensure_oracle(), "--threads", threads, src, "-o", dst], check=True)
+        with open(dst) as f:
+            return json.load(f)
+
+
+def make_chain(name):
+    from helpers import churn_chain
+    gen, fn, seed, rounds = CHAINS[name]
+    t = time.time()
+    steps = []
+    for r, changes, fx, out in churn_chain(fn(), seed, rounds, oracle):
+        dg = digest_outputs(out)
+        dg["evaluated"] = len(out.get("evaluated", []))
+        dg["events"] = len(changes)
+        steps.append(dg)
+        print(name, r, dg["status"], dg.get("n_decisions"), len(changes), f"{time.time() - t:.0f}s", flush=True)
+    with open(os.path.join(HERE, f"digest_{name}.json"), "w") as f:
+        json.dump({"generator": gen, "oracle": f"oracle/build/kbref --threads {os.cpu_count()} "
+                                                f"({time.time() - t:.0f} s here)", "steps": steps},
+                  f, separators=(",", ":"))
 
 
 def make(name):
@@ -53,5 +91,5 @@ def make(name):
 
 
 if __name__ == "__main__":
-    for n in sys.argv[1:] or list(SESSIONS):
-        make(n)
+    for n in sys.argv[1:] or list(SESSIONS) + list(CHAINS):
+        (make_chain if n in CHAINS else make)(n)

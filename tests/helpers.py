@@ -112,3 +112,30 @@ def compare_digests(ref, got):
     assert [q[0] for q in got["queues"]] == [q[0] for q in ref["queues"]]
     for a, b in zip(ref["queues"], got["queues"]):
         assert close(a[1], b[1]) and all(close(x, y) for u, v in zip(a[2:], b[2:]) for x, y in zip(u, v)), (a, b)
+
+
+def churn_chain(fx0, seed, rounds, run):
+    """Resident-session churn of a seeded session (synth.churn, the events of
+    tests/test_update_gpu.py): yields (r, changes, fx_r, out_r) for r = 0 ..
+    rounds, where fx_0 is `fx0` in its session order (SURVEY F4), fx_{r+1}
+    the cache after round r's events `changes` — the binds of out_r's
+    Allocate decisions, completions, deletions, new pods, node growth — and
+    out_r = run(fx_r, changes) in the oracle's output schema (the oracle itself in
+    make_digests.py, the device on the GPU box: the same chain whenever the
+    two agree on every decision)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "kube-arbitrator_amd"))
+    from kbgpu import synth
+    from kbgpu.cache import FakeBinder, cache_from_fixture
+    from kbgpu.fixture import _OrderedCache
+    snap = _OrderedCache(cache_from_fixture(fx0, FakeBinder()), fx0).snapshot()
+    fx = dict(fx0, sessionOrder={"jobs": [j.uid for j in snap.jobs], "nodes": [n.name for n in snap.nodes]})
+    uids = {t.uid for j in snap.jobs for t in j.tasks.values()}
+    changes = []
+    for r in range(rounds + 1):
+        out = run(fx, changes)
+        yield r, changes, fx, out
+        if r == rounds or out["status"] != "ok":
+            return
+        changes, fx = synth.churn(fx, seed * 31 + r, uids, out["decisions"])
+        uids |= {p["uid"] for kind, p in changes if kind == "pod_add"}

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for fn in declared_functions():
         assert hasattr(L, fn), fn
     assert set(declared_functions()) == set(_abi.SIGNATURES)
-    assert L.kbg_abi_version() == _abi.ABI_VERSION == 8
+    assert L.kbg_abi_version() == _abi.ABI_VERSION == 9
     assert L.kbg_device_count() >= 0
 
 
@@ -85,3 +85,59 @@ def test_invalid_snapshot_rejected():
     snap.strings = ctypes.cast(strs, ctypes.POINTER(ctypes.c_char_p))
     snap.n_strings = 1
     assert L.kbg_session_open(ctypes.byref(snap), None, ctypes.byref(h)) == _abi.KBG_E_INVALID
+
+
+def _registry_session(extra_plugin, registered, registry=1, drop_flag=()):
+    """C1's session with `extra_plugin` added to the first tier; every entry's
+    KBG_PLUGIN_REGISTERED flag as the caller's registry says."""
+    from kbgpu import _abi, synth
+    from kbgpu.cache import FakeBinder, cache_from_fixture
+    from kbgpu.conf import PluginOption, Tier
+    from kbgpu.fixture import _OrderedCache, fixture_tiers
+    from kbgpu.snapshot import FlatSnapshot
+    fx = synth.config_fixture(1)
+    tiers = fixture_tiers(fx)
+    tiers = [Tier(list(tiers[0].plugins) + [PluginOption(extra_plugin)])] + list(tiers[1:])
+    s = _OrderedCache(cache_from_fixture(fx, FakeBinder()), fx).snapshot()
+    flat = FlatSnapshot(s.nodes, s.jobs, s.queues, s.others, tiers,
+                        registered=lambda n: n in registered and n not in drop_flag)
+    o = _abi.kbg_options()
+    o.device = -1
+    o.plugin_registry = registry
+    return flat, o
+
+
+@pytest.mark.parametrize("registry", [0, 1])
+def test_registered_unknown_plugin_refuses_the_session(registry):
+    """framework.go:30-35: a tier entry with a builder in the caller's process
+    is instantiated. One this path does not implement must not be dropped
+    silently: kbg_session_open refuses (KBG_E_UNSUPPORTED) before any device
+    work; with plugin_registry = 0 the library cannot know, and skips it."""
+    from kbgpu import _abi
+    L = _abi.lib()
+    known = {"priority", "gang", "drf", "predicates", "proportion"}
+    flat, o = _registry_session("binpack", known | {"binpack"}, registry)
+    h = ctypes.c_void_p()
+    code = L.kbg_session_open(ctypes.byref(flat.snap), ctypes.byref(o), ctypes.byref(h))
+    if registry:
+        assert code == _abi.KBG_E_UNSUPPORTED and b"binpack" in L.kbg_last_error()
+    else:
+        assert code in (_abi.KBG_OK, _abi.KBG_E_HIP)  # accepted (no device here: the open then stops at HIP)
+    if h.value:
+        L.kbg_session_close(h)
+
+
+def test_unregistered_plugins_are_skipped():
+    """A name without a builder is skipped like GetPluginBuilder's miss
+    (framework.go:30-35), whether or not this path implements it: the open
+    proceeds to the device."""
+    from kbgpu import _abi
+    L = _abi.lib()
+    known = {"priority", "gang", "drf", "predicates", "proportion"}
+    for extra, drop in (("binpack", ()), ("nodeorder", ("gang",))):
+        flat, o = _registry_session(extra, known, 1, drop_flag=drop)
+        h = ctypes.c_void_p()
+        code = L.kbg_session_open(ctypes.byref(flat.snap), ctypes.byref(o), ctypes.byref(h))
+        assert code in (_abi.KBG_OK, _abi.KBG_E_HIP), L.kbg_last_error()
+        if h.value:
+            L.kbg_session_close(h)

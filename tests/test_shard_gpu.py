@@ -46,17 +46,11 @@ def test_local_shards_fuzz_parity(seed):
 
 
 @pytest.mark.slow
-def test_local_shards_config3(c3_ref):
-    fx, ref = c3_ref
-    got, ssn = run_fixture(fx, {"shards": 8})
-    compare_outputs(ref, got)
+def test_local_shards_config3():
+    from helpers import compare_digests, digest_outputs, load_golden
+    got, ssn = run_fixture(synth.config_fixture(3), {"shards": 8})
     ssn.close()
-
-
-@pytest.fixture(scope="module")
-def c3_ref():
-    fx = synth.config_fixture(3)
-    return fx, run_oracle(fx)
+    compare_digests(load_golden("digest_c3.json"), digest_outputs(got))
 
 
 @pytest.fixture(scope="module")

@@ -8,7 +8,7 @@ import ctypes
 
 import pytest
 
-from helpers import compare_outputs, run_oracle
+from helpers import churn_chain, compare_digests, compare_outputs, digest_outputs, load_golden, run_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -144,3 +144,119 @@ def test_update_affinity(seed):
 @pytest.mark.parametrize("cid", [1, 2])
 def test_update_configs(cid):
     check_update(synth.config_fixture(cid), cid, rounds=3)
+
+
+def _same_cycle(got, fresh):
+    """An updated session's cycle (abi_cycle) against a fresh open's (run_fixture)."""
+    assert got["status"] == fresh["status"], (got, fresh.get("error"))
+    if fresh["status"] != "ok":
+        return
+    assert got["decisions"] == fresh["decisions"]
+    assert got["binds"] == fresh["binds"]
+    assert got["nodes"] == fresh["nodes"]
+    for a, b in zip(got["jobs"], fresh["jobs"]):
+        assert (a["uid"], a["ready_num"], a["ready"], a.get("fit_error")) == \
+               (b["uid"], b["ready_num"], b["ready"], b.get("fit_error")), (a, b)
+        if "drf_share" in b:
+            assert a["drf_share"] == b["drf_share"]
+    for a, b in zip(got["queues"], fresh["queues"]):
+        assert a["uid"] == b["uid"] and a["share"] == b["share"] and a["deserved"] == b["deserved"]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("cid", [3, 4])
+def test_update_chain_at_scale(cid):
+    """BASELINE C3 (5k x 100k, over-requested queues) and C4 (20k x 500k) as
+    resident sessions over 3 churn rounds (helpers.churn_chain: ~20-30k
+    events per round at C3): each snapshot S_r opened fresh must match the
+    oracle's digest of S_r (tests/golden/digest_c{3,4}_churn.json), and the
+    session opened once at S_0 and updated round by round must make the same
+    cycle as the fresh open of S_r."""
+    ref = load_golden(f"digest_c{cid}_churn.json")["steps"]
+    state = {}
+
+    def run(fx, changes):
+        fresh, fssn = run_fixture(fx)
+        if fssn:
+            fssn.close()
+        if not changes:  # S_0: the resident session starts here
+            state["ssn"] = _open(fx)
+            got = abi_cycle(state["ssn"], ["allocate"])
+        else:
+            _abi.check(_abi.lib().kbg_session_reset(state["ssn"].handle))
+            try:
+                state["ssn"].update(changes)
+                got = abi_cycle(state["ssn"], ["allocate"])
+            except _abi.KbgError as e:
+                assert e.status == "ref_panic", e
+                got = {"status": "ref_panic"}
+        _same_cycle(got, fresh)
+        return fresh
+
+    try:
+        for r, changes, fx, out in churn_chain(synth.config_fixture(cid), cid, len(ref) - 1, run):
+            compare_digests(ref[r], digest_outputs(out))
+            assert len(changes) == ref[r]["events"]
+    finally:
+        if "ssn" in state:
+            state["ssn"].close()
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_update_without_reset_restarts_the_table(seed):
+    """An update right after a cycle's actions (no kbg_session_reset): the
+    node rows the actions committed — bound or not, touched by an event or
+    not — go back to the updated snapshot, so the next cycle equals a fresh
+    open's. Events here: none, or completions that miss most decided nodes."""
+    fx0 = synth.random_fixture(17000 + seed) if seed % 2 else synth.config_fixture(2 if seed % 4 == 0 else 1)
+    fx0.pop("actions", None)
+    ssn = _open(fx0)
+    try:
+        fx = dict(fx0, sessionOrder={"jobs": [j.uid for j in ssn.jobs], "nodes": list(ssn.flat.node_names)})
+        first = abi_cycle(ssn, ["allocate"])
+        if first["status"] != "ok":
+            pytest.skip(first["status"])
+        changes = []
+        if seed % 3:
+            running = [p for p in fx["pods"] if p.get("phase") == "Running"]
+            changes = [("pod_update", dict(p, phase="Succeeded")) for p in running[:2]]
+        pods = {p["uid"]: p for p in fx["pods"]}
+        for kind, p in changes:  # the cache's delete + add: an updated pod moves to the end
+            pods.pop(p["uid"])
+            pods[p["uid"]] = p
+        fx1 = dict(fx, pods=list(pods.values()))
+        ssn.update(changes)  # no reset: the cycle's commits are still in the device table
+        got = abi_cycle(ssn, ["allocate"])
+        fresh, fssn = run_fixture(fx1)
+        _same_cycle(got, fresh)
+        assert got["decisions"] == first["decisions"] or changes  # no events: the same cycle again
+        if fssn:
+            fssn.close()
+    finally:
+        ssn.close()
+
+
+def test_refused_update_leaves_the_session_unchanged():
+    """KBG_E_INVALID found before any event applies (a deleted task, an index
+    out of range) leaves the session as it was; the same batch without the
+    bad event then applies."""
+    fx = synth.config_fixture(1)
+    ssn = _open(fx)
+    try:
+        before = abi_cycle(ssn, ["allocate"])
+        pods = [p for p in fx["pods"]][:3]
+        good = [("pod_delete", pods[0]), ("pod_update", dict(pods[1], phase="Succeeded"))]
+        L = _abi.lib()
+        evs = (_abi.kbg_event * 3)()
+        idx = {t.uid: i for i, t in enumerate(ssn.flat.task_objs)}
+        evs[0].kind, evs[0].task = _abi.EV_POD_DELETE, idx[pods[0]["uid"]]
+        evs[1].kind, evs[1].task = _abi.EV_POD_DELETE, idx[pods[0]["uid"]]  # deleted by the event before it
+        evs[2].kind, evs[2].task, evs[2].status, evs[2].node = _abi.EV_POD_UPDATE, idx[pods[1]["uid"]], 1 << 7, -1
+        assert L.kbg_session_update(ssn.handle, evs, 3) == _abi.KBG_E_INVALID
+        _abi.check(L.kbg_session_reset(ssn.handle))
+        assert abi_cycle(ssn, ["allocate"]) == before  # nothing was applied
+        _abi.check(L.kbg_session_reset(ssn.handle))
+        ssn.update(good)
+        assert abi_cycle(ssn, ["allocate"])["status"] == "ok"
+    finally:
+        ssn.close()
