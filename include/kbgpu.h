@@ -300,7 +300,8 @@ typedef struct kbg_stats {
   double resolve_ms;       /* host: in-order commit of the device candidates */
   double device_ms;        /* host wall time spent in scan round trips (H2D, kernels, D2H) */
   double delta_ms;         /* host wall time spent writing touched node rows back to HBM */
-  int64_t replayed;        /* engine steps replayed after a cut */
+  int64_t replayed;        /* engine steps replayed from a batch checkpoint after a cut (sharded rank 0; the
+                              single-rank allocate restarts from the committed outcomes' engine: 0) */
   int32_t n_classes;       /* static predicate classes on the device */
   int32_t shards;          /* node-axis shards of the session (1 = unsharded) */
   int32_t shard_index;     /* the shard this process holds; -1 = every shard is local */

@@ -206,8 +206,29 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
                        int32_t n_tasks, int32_t cap_check, int32_t int_mode, uint64_t* out, hipStream_t stream,
                        hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
-// avail[g] = bit when row g has any candidate (count[g] != 0), else 0.
-hipError_t launch_avail(const uint32_t* count, int32_t n_rows, uint32_t bit, uint32_t* avail, hipStream_t stream);
+// The fused scan + candidate extraction (kbg_firstfit_kernel): for each row g
+// < G the first capoff[g+1]-capoff[g] feasible nodes of the global words
+// [w_lo, w_hi) in node order into cand[capoff[g] ..], count[g] = how many
+// (| kCountIncompleteBit when more exist), avail[g] = avail_bit if any
+// (owner-resolve; null otherwise). rows / capoff / count / cand may be
+// host-mapped (zero-copy).
+struct FirstFitArgs {
+  const double* nodes;          // the node table as one block (NodeSoA of alloc_soa): rows of the nodes
+                                // [tab_lo, tab_lo + tab_n), idle c/m/g, rel c/m/g f64[stride], ntasks,
+                                // maxtasks i32[stride]
+  const uint64_t* class_mask;   // [class][W]
+  const char* up;               // rows TaskRec[G] at 0, capoff u32[G + 1] at up_capoff
+  uint32_t* down;               // count u32[G], then the candidates (cand = down + G)
+  uint32_t* avail;
+  int32_t stride, up_capoff;
+  int32_t G, n_nodes, W, w_lo, w_hi, tab_lo, tab_n;
+  int32_t cap_check;            // the predicates plugin's pod cap is on
+  int32_t early_exit;           // stop once every row's list is full (production mode)
+  uint32_t avail_bit;
+};
+hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t stream, hipEvent_t start = nullptr,
+                           hipEvent_t stop = nullptr);
+
 
 // Row g gets cap_off[g+1]-cap_off[g] candidate slots at out_cand[cap_off[g]],
 // taken from the global words [w_lo, w_hi) in node order.

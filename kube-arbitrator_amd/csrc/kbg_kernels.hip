@@ -78,21 +78,21 @@ constexpr int kRowGroup = 8;
 #define KBG_SMALL_BATCH_ROWS 1024
 #endif
 constexpr int kSmallBatchRows = KBG_SMALL_BATCH_ROWS;  // launch_scan: batches up to this many rows use 16-row workgroups
-template <bool INT_MODE, bool REL_ZERO, int ROWS, int J = 0>
+template <bool INT_MODE, bool REL_ZERO, int ROWS, int J = 0, int GROUP = kRowGroup>
 __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, double im, double ig, double rc,
                                           double rm, double rg, uint32_t (&keep)[4]) {
-  double q[kRowGroup][3];
+  double q[GROUP][3];
 #pragma unroll
-  for (int u = 0; u < kRowGroup; ++u) {
+  for (int u = 0; u < GROUP; ++u) {
     q[u][0] = s_req[J + u][0];
     q[u][1] = s_req[J + u][1];
     q[u][2] = s_req[J + u][2];
   }
   [&]<int... U>(std::integer_sequence<int, U...>) {
     (scan_row<INT_MODE, REL_ZERO, J + U>(q[U][0], q[U][1], q[U][2], ic, im, ig, rc, rm, rg, keep), ...);
-  }(std::make_integer_sequence<int, kRowGroup>{});
-  if constexpr (J + kRowGroup < ROWS)
-    scan_rows<INT_MODE, REL_ZERO, ROWS, J + kRowGroup>(s_req, ic, im, ig, rc, rm, rg, keep);
+  }(std::make_integer_sequence<int, GROUP>{});
+  if constexpr (J + GROUP < ROWS)
+    scan_rows<INT_MODE, REL_ZERO, ROWS, J + GROUP, GROUP>(s_req, ic, im, ig, rc, rm, rg, keep);
 }
 
 template <bool INT_MODE, int ROWS>
@@ -187,6 +187,159 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
   return hipGetLastError();
 }
 
+// ------------------------------------------------------ fused first-fit
+// kbg_firstfit_kernel: the scan and the candidate extraction in one launch,
+// with no feasibility bitmap in between. A workgroup owns kFfRows rows and
+// walks their words [w_lo, w_hi) in node order, kFfWaves words per round:
+// wave w evaluates word (round * kFfWaves + w) for every row exactly as
+// kbg_scan_kernel does (64 nodes in registers, one ballot per dimension, the
+// raw masks moved to lane J with v_writelane_b32, class mask / pod cap /
+// Releasing shortcut applied by lane J), and parks the row masks in LDS; after
+// the round's barrier wave j takes row j's kFfWaves words in node order and
+// appends the set bits to the row's list (lane = node, position = found +
+// mbcnt), at most `want` of them. Rows read their requests and list offsets
+// from host-mapped memory and write counts and candidates straight into it:
+// no copy kernel on either side. `early_exit` (production mode) ends the walk
+// once every row of the workgroup has more nodes than its list holds (the
+// rest of the table cannot change its list); full-scan mode evaluates every
+// node for every row.
+constexpr int kFfRows = 16;
+constexpr int kFfWaves = 16;
+// rows whose requests are read from LDS together: 4 (integer thresholds) / 2
+// (the reference expression) keep the kernel at 8 waves per SIMD, no spills
+template <bool INT_MODE>
+constexpr int kFfGroup = INT_MODE ? 4 : 2;
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <bool INT_MODE>
+__global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArgs a) {
+  __shared__ double s_req[kFfRows][3];
+  __shared__ int32_t s_cls[kFfRows], s_flags[kFfRows];
+  __shared__ uint64_t s_f[2][kFfWaves][kFfRows];  // [round parity][word of the round][row]: fit anywhere
+  __shared__ uint64_t s_i[2][kFfWaves][kFfRows];  //                                       fit in Idle
+  __shared__ uint32_t s_done[2][kFfRows];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g0 = blockIdx.x * kFfRows;
+  if (wave == 0 && lane < kFfRows) {
+    const TaskRec tr = reinterpret_cast<const TaskRec*>(a.up)[min(g0 + lane, a.G - 1)];  // past G: never written
+    s_req[lane][0] = tr.req[0];
+    s_req[lane][1] = tr.req[1];
+    s_req[lane][2] = tr.req[2];
+    s_cls[lane] = tr.cls;
+    s_flags[lane] = tr.flags;
+  }
+  // wave j extracts row g0 + j (kFfWaves == kFfRows)
+  const int g = g0 + wave;
+  const bool has_row = g < a.G;
+  uint32_t base = 0, want = 0;
+  const uint32_t* capoff = reinterpret_cast<const uint32_t*>(a.up + a.up_capoff);
+  if (has_row) {
+    base = capoff[g];
+    want = capoff[g + 1] - base;
+  }
+  uint32_t found = 0;
+  bool done = !has_row;
+  if (lane == 0) s_done[1][wave] = done ? 1u : 0u;  // read by round 0's exit test
+  __syncthreads();
+  const int cls_l = s_cls[lane & (kFfRows - 1)];
+  const int flags_l = s_flags[lane & (kFfRows - 1)];
+  const int rounds = (a.w_hi - a.w_lo + kFfWaves - 1) / kFfWaves;
+  for (int r = 0; r < rounds; ++r) {
+    const int buf = r & 1;
+    const int c = a.w_lo + r * kFfWaves + wave;  // this wave's global 64-node word
+    uint64_t f = 0ull, fi = 0ull;
+    if (c < a.w_hi) {  // wave-uniform
+      const int node = c * 64 + lane;
+      const int row = node - a.tab_lo;
+      const bool valid = node < a.n_nodes && row < a.tab_n;
+      double ic = 0, im = 0, ig = 0, rc = 0, rm = 0, rg = 0;
+      int32_t nt = 0, mt = 0;
+      if (valid) {
+        const double* p = a.nodes + row;
+        ic = p[0];
+        im = p[a.stride];
+        ig = p[2 * a.stride];
+        rc = p[3 * a.stride];
+        rm = p[4 * a.stride];
+        rg = p[5 * a.stride];
+        const int32_t* q = reinterpret_cast<const int32_t*>(a.nodes + 6 * (size_t)a.stride) + row;
+        nt = q[0];
+        mt = q[a.stride];
+      }
+      const uint64_t lane_mw = lane < kFfRows ? a.class_mask[(size_t)cls_l * a.W + c] : 0ull;
+      const uint64_t okm = __ballot(valid && (!a.cap_check || nt < mt));  // predicates.go:125-127 pod cap
+      const bool rel_zero_wave = __ballot(!(rc == 0.0 && rm == 0.0 && rg == 0.0)) == 0ull;
+      uint32_t keep[4] = {0u, 0u, 0u, 0u};
+      uint64_t mr;
+      if (rel_zero_wave) {
+        scan_rows<INT_MODE, true, kFfRows, 0, kFfGroup<INT_MODE>>(s_req, ic, im, ig, rc, rm, rg, keep);
+        mr = (flags_l & kRowRelZeroFits) ? ~0ull : 0ull;
+      } else {
+        scan_rows<INT_MODE, false, kFfRows, 0, kFfGroup<INT_MODE>>(s_req, ic, im, ig, rc, rm, rg, keep);
+        mr = (uint64_t)keep[2] | ((uint64_t)keep[3] << 32);
+      }
+      const uint64_t mw = lane_mw & okm;
+      fi = ((uint64_t)keep[0] | ((uint64_t)keep[1] << 32)) & mw;
+      f = fi | (mr & mw);
+    }
+    if (lane < kFfRows) {
+      s_f[buf][wave][lane] = f;
+      s_i[buf][wave][lane] = fi;
+    }
+    __syncthreads();
+    if (a.early_exit) {  // every row's list is full: the same decision in every wave
+      const uint32_t d = lane < kFfRows ? s_done[buf ^ 1][lane] : 1u;
+      if (__ballot(d == 0u) == 0ull) break;
+    }
+    if (!done) {  // wave-uniform: this wave's row, the round's words in node order
+      uint64_t fk = 0ull, ik = 0ull;
+      if (lane < kFfWaves) {
+        fk = s_f[buf][lane][wave];
+        ik = s_i[buf][lane][wave];
+      }
+      uint64_t nz = __ballot(fk != 0ull);
+      while (nz) {
+        const int k = __builtin_ctzll(nz);
+        nz &= nz - 1ull;
+        const uint64_t m = readlane64(fk, k);
+        const uint64_t mi = readlane64(ik, k);
+        const uint32_t pos =
+            found + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (((m >> lane) & 1ull) && pos < want)
+          a.down[a.G + base + pos] =
+              (uint32_t)((a.w_lo + r * kFfWaves + k) * 64 + lane) | (((mi >> lane) & 1ull) ? 0u : kCandPipelineBit);
+        found += (uint32_t)__popcll(m);
+        if (found > want) {
+          done = true;
+          break;
+        }
+      }
+    }
+    if (lane == 0) s_done[buf][wave] = done ? 1u : 0u;
+  }
+  if (has_row && lane == 0) {
+    a.down[g] = (found < want ? found : want) | (found > want ? kCountIncompleteBit : 0u);
+    if (a.avail) a.avail[g] = found ? a.avail_bit : 0u;
+  }
+}
+
+hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t stream, hipEvent_t start,
+                           hipEvent_t stop) {
+  if (a.G <= 0) return hipSuccess;
+  const dim3 grid((a.G + kFfRows - 1) / kFfRows), block(64 * kFfWaves);
+  if (int_mode)
+    hipExtLaunchKernelGGL(kbg_firstfit_kernel<true>, grid, block, 0, stream, start, stop, 0, a);
+  else
+    hipExtLaunchKernelGGL(kbg_firstfit_kernel<false>, grid, block, 0, stream, start, stop, 0, a);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- select
 // One wave per row walks the row's words [w_lo, w_hi) in global node order
 // (shard slots in rank order = ascending node index), so the candidates come
@@ -244,20 +397,6 @@ hipError_t launch_select(const uint64_t* bits, int32_t w_lo, int32_t w_hi, int32
   if (n_rows <= 0) return hipSuccess;
   hipExtLaunchKernelGGL(kbg_select_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, stream, start, stop, 0, bits, w_lo,
                         w_hi, Wl, n_rows, cap_off, out_cand, out_count);
-  return hipGetLastError();
-}
-
-// Owner-resolve: this rank's availability bit of each row (any candidate in
-// its own words), summed over the ranks by the all-reduce that follows.
-__global__ __launch_bounds__(256) void kbg_avail_kernel(const uint32_t* __restrict__ count, int32_t n_rows,
-                                                        uint32_t bit, uint32_t* __restrict__ avail) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < n_rows) avail[g] = (count[g] & kCountMask) ? bit : 0u;
-}
-
-hipError_t launch_avail(const uint32_t* count, int32_t n_rows, uint32_t bit, uint32_t* avail, hipStream_t stream) {
-  if (n_rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(kbg_avail_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, stream, count, n_rows, bit, avail);
   return hipGetLastError();
 }
 

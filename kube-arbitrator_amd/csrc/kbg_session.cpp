@@ -402,28 +402,44 @@ kbg_status hupload(Session& S, T** p, const std::vector<T>& v) {
   return KBG_OK;
 }
 
+// The node table as ONE block (FirstFitArgs.nodes): idle c/m/g and rel c/m/g
+// f64[stride], then ntasks and maxtasks i32[stride], stride = tab_n rounded
+// up to 64 rows. A reset restores it with one copy.
+int32_t soa_stride(const Session& S) { return std::max(64, (S.tab_n + 63) / 64 * 64); }
+size_t soa_bytes(const Session& S) { return (size_t)soa_stride(S) * (6 * 8 + 2 * 4); }
+
 kbg_status alloc_soa(Session& S, kbg::NodeSoA* soa) {
-  const size_t N = (size_t)S.tab_n;
-  kbg_status st;
-  if ((st = dalloc(S, &soa->idle_cpu, N)) || (st = dalloc(S, &soa->idle_mem, N)) || (st = dalloc(S, &soa->idle_gpu, N)) ||
-      (st = dalloc(S, &soa->rel_cpu, N)) || (st = dalloc(S, &soa->rel_mem, N)) || (st = dalloc(S, &soa->rel_gpu, N)) ||
-      (st = dalloc(S, &soa->ntasks, N)) || (st = dalloc(S, &soa->maxtasks, N)))
-    return st;
+  const size_t L = (size_t)soa_stride(S);
+  double* b = nullptr;
+  kbg_status st = dalloc(S, (char**)&b, soa_bytes(S));
+  if (st != KBG_OK) return st;
+  *soa = kbg::NodeSoA{b, b + L, b + 2 * L, b + 3 * L, b + 4 * L, b + 5 * L, (int32_t*)(b + 6 * L),
+                      (int32_t*)(b + 6 * L) + L};
   return KBG_OK;
 }
 
 kbg_status copy_soa(Session& S, const kbg::NodeSoA& dst, const kbg::NodeSoA& src) {
-  const size_t N = (size_t)S.tab_n;
-  if (N == 0) return KBG_OK;
-  HIP_TRY(hipMemcpyAsync(dst.idle_cpu, src.idle_cpu, N * 8, hipMemcpyDeviceToDevice, S.stream));
-  HIP_TRY(hipMemcpyAsync(dst.idle_mem, src.idle_mem, N * 8, hipMemcpyDeviceToDevice, S.stream));
-  HIP_TRY(hipMemcpyAsync(dst.idle_gpu, src.idle_gpu, N * 8, hipMemcpyDeviceToDevice, S.stream));
-  HIP_TRY(hipMemcpyAsync(dst.rel_cpu, src.rel_cpu, N * 8, hipMemcpyDeviceToDevice, S.stream));
-  HIP_TRY(hipMemcpyAsync(dst.rel_mem, src.rel_mem, N * 8, hipMemcpyDeviceToDevice, S.stream));
-  HIP_TRY(hipMemcpyAsync(dst.rel_gpu, src.rel_gpu, N * 8, hipMemcpyDeviceToDevice, S.stream));
-  HIP_TRY(hipMemcpyAsync(dst.ntasks, src.ntasks, N * 4, hipMemcpyDeviceToDevice, S.stream));
-  HIP_TRY(hipMemcpyAsync(dst.maxtasks, src.maxtasks, N * 4, hipMemcpyDeviceToDevice, S.stream));
+  if (S.tab_n == 0) return KBG_OK;
+  HIP_TRY(hipMemcpyAsync(dst.idle_cpu, src.idle_cpu, soa_bytes(S), hipMemcpyDeviceToDevice, S.stream));
   return KBG_OK;
+}
+
+// Pinned host memory the kernels read and write in place (zero-copy: row
+// uploads, candidate lists, node / mask deltas): mapped and fine-grained
+// (coherent), so a kernel's stores are on the host when its completion event
+// fires and the host's stores are seen by the next launch.
+kbg_status host_alloc(void** p, size_t bytes) {
+  HIP_TRY(hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  return KBG_OK;
+}
+// The device address of such memory (the host address itself under unified
+// addressing, which build() checks once).
+template <class T>
+T* dev_ptr(const Session& S, T* h) {
+  if (S.uva || !h) return h;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, (void*)h, 0) != hipSuccess) return nullptr;
+  return (T*)d;
 }
 
 void free_device(Session& S) {
@@ -524,45 +540,72 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   trace_add("l.begin", G);
   const uint32_t total = sg.h_capoff[G];
   const int32_t Gp = kbg::kbg_pad_rows(G);  // Grouper::build padded the rows
+  if (!S.comm || S.owner) {
+    // one launch: kbg_firstfit_kernel reads the rows from the stage's mapped
+    // buffer and writes counts and candidates straight into the other one;
+    // this process's words only (owner-resolve), or every word
+    kbg::FirstFitArgs a{};
+    a.nodes = S.d_nodes.idle_cpu;
+    a.stride = soa_stride(S);
+    a.class_mask = S.d_class_mask;
+    a.up = dev_ptr(S, sg.h_up);
+    a.up_capoff = (int32_t)((size_t)Gp * sizeof(kbg::TaskRec));
+    a.down = dev_ptr(S, sg.h_down);
+    if (!a.up || !a.down) return fail(KBG_E_HIP, "hipHostGetDevicePointer of a stage buffer failed");
+    a.G = G;
+    a.n_nodes = S.n_nodes;
+    a.W = S.W;
+    a.w_lo = S.owner ? S.shard * S.Wl : 0;
+    a.w_hi = S.owner ? std::min(S.W, (S.shard + 1) * S.Wl) : S.W;
+    a.tab_lo = S.tab_lo;
+    a.tab_n = S.tab_n;
+    a.cap_check = S.pred_active ? 1 : 0;
+    a.early_exit = S.opts.full_scan ? 0 : 1;  // full-scan evaluates every node for every row
+    const bool avail = S.owner && S.comm;
+    if (avail) {  // owner-resolve: the rows' availability over the ranks, summed in the same round trip
+      a.avail = S.d_down;
+      a.avail_bit = 1u << S.shard;
+    }
+    HIP_TRY(kbg::launch_firstfit(a, S.int_mode ? 1 : 0, S.stream, sg.ev[0], sg.ev[1]));
+    trace_add("l.firstfit");
+    if (avail) {
+      if (S.comm->nccl) {  // (a communicator without RCCL — R sessions of one process, tools — sums on the host)
+        const ncclResult_t nr = ncclAllReduce(S.d_down, S.d_down, (size_t)G, ncclUint32, ncclSum, S.comm->nccl, S.stream);
+        if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+      }
+      HIP_TRY(hipMemcpyAsync(sg.h_down + G + total, S.d_down, (size_t)G * 4, hipMemcpyDeviceToHost, S.stream));
+    }
+    HIP_TRY(hipEventRecord(sg.ev[6], S.stream));
+    trace_add("l.event");
+    sg.fused = true;
+    sg.G = G;
+    sg.base = base;
+    sg.inflight = true;
+    return KBG_OK;
+  }
+  sg.fused = false;
+  // replicated sharded sessions (pod affinity, backfill on a communicator):
+  // every rank scans its slot, the slots are all-gathered, every rank selects
   const size_t up_bytes = (size_t)Gp * sizeof(kbg::TaskRec) + (size_t)(G + 1) * 4;
   const kbg::TaskRec* d_tasks = (const kbg::TaskRec*)S.d_up;
   const uint32_t* d_capoff = (const uint32_t*)(S.d_up + (size_t)Gp * sizeof(kbg::TaskRec));
   HIP_TRY(hipMemcpyAsync(S.d_up, sg.h_up, up_bytes, hipMemcpyHostToDevice, S.stream));
   trace_add("l.h2d", (int64_t)up_bytes);
-  // this process scans its shard (or every shard when they are all local)
-  kbg::ScanGeom geo{S.n_nodes, S.W, S.Wl, 0, S.R * S.Wl, S.tab_lo};
+  const kbg::ScanGeom geo{S.n_nodes, S.W, S.Wl, S.shard * S.Wl, S.Wl, S.tab_lo};  // this rank's slot
   const size_t slot_words = (size_t)2 * G * kbg::kbg_slot_words(S.Wl);
-  uint64_t* out = S.d_bits;
-  if (S.comm) {
-    geo.chunk_lo = S.shard * S.Wl;
-    geo.n_chunks = S.Wl;
-    out = S.d_bits + (size_t)S.shard * slot_words;
-  }
+  uint64_t* out = S.d_bits + (size_t)S.shard * slot_words;
   HIP_TRY(kbg::launch_scan(S.d_nodes, geo, S.d_class_mask, d_tasks, G, S.pred_active ? 1 : 0, S.int_mode ? 1 : 0, out,
                            S.stream, sg.ev[0], sg.ev[1]));
   trace_add("l.scan");
-  if (S.comm && !S.owner) {  // in-place all-gather: every rank receives every shard's slot, in rank (= node) order
-    HIP_TRY(hipEventRecord(sg.ev[4], S.stream));
-    const ncclResult_t nr = ncclAllGather(out, S.d_bits, slot_words, ncclUint64, S.comm->nccl, S.stream);
-    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
-    HIP_TRY(hipEventRecord(sg.ev[5], S.stream));
-  }
-  // an owner-resolve shard (S.owner) selects its own words; otherwise every word
-  const int32_t w_lo = S.owner ? S.shard * S.Wl : 0;
-  const int32_t w_hi = S.owner ? std::min(S.W, (S.shard + 1) * S.Wl) : S.W;
-  HIP_TRY(kbg::launch_select(S.d_bits, w_lo, w_hi, S.Wl, G, d_capoff, S.d_down + G, S.d_down, S.stream, sg.ev[2],
+  // in-place all-gather: every rank receives every shard's slot, in rank (= node) order
+  HIP_TRY(hipEventRecord(sg.ev[4], S.stream));
+  const ncclResult_t nr = ncclAllGather(out, S.d_bits, slot_words, ncclUint64, S.comm->nccl, S.stream);
+  if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
+  HIP_TRY(hipEventRecord(sg.ev[5], S.stream));
+  HIP_TRY(kbg::launch_select(S.d_bits, 0, S.W, S.Wl, G, d_capoff, S.d_down + G, S.d_down, S.stream, sg.ev[2],
                              sg.ev[3]));
   trace_add("l.select");
-  size_t down = (size_t)G + total;
-  if (S.owner && S.comm) {  // owner-resolve: the rows' availability over the ranks, in the same round trip
-    uint32_t* d_avail = S.d_down + down;
-    HIP_TRY(kbg::launch_avail(S.d_down, G, 1u << S.shard, d_avail, S.stream));
-    if (S.comm->nccl) {  // (a communicator without RCCL — R sessions of one process, tools — sums on the host)
-      const ncclResult_t nr = ncclAllReduce(d_avail, d_avail, (size_t)G, ncclUint32, ncclSum, S.comm->nccl, S.stream);
-      if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
-    }
-    down += (size_t)G;
-  }
+  const size_t down = (size_t)G + total;
   HIP_TRY(hipMemcpyAsync(sg.h_down, S.d_down, down * 4, hipMemcpyDeviceToHost, S.stream));
   trace_add("l.d2h", (int64_t)down * 4);
   HIP_TRY(hipEventRecord(sg.ev[6], S.stream));
@@ -582,8 +625,10 @@ kbg_status device_wait(Session& S, kbg::Stage& sg) {
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, sg.ev[0], sg.ev[1]));
   S.stats.scan_kernel_ms += ms;
-  HIP_TRY(hipEventElapsedTime(&ms, sg.ev[2], sg.ev[3]));
-  S.stats.select_kernel_ms += ms;
+  if (!sg.fused) {
+    HIP_TRY(hipEventElapsedTime(&ms, sg.ev[2], sg.ev[3]));
+    S.stats.select_kernel_ms += ms;
+  }
   if (S.comm && !S.owner) {
     HIP_TRY(hipEventElapsedTime(&ms, sg.ev[4], sg.ev[5]));
     S.stats.exchange_ms += ms;
@@ -639,8 +684,7 @@ kbg_status push_mask_deltas(Session& S) {
       S.h_mdeltas[k] = kbg::MaskDelta{idx, 0u, S.h_class_mask[idx]};
       S.mask_dirty_flag[idx] = 0;
     }
-    HIP_TRY(hipMemcpyAsync(S.d_mdeltas, S.h_mdeltas, cnt * sizeof(kbg::MaskDelta), hipMemcpyHostToDevice, S.stream));
-    HIP_TRY(kbg::launch_mask_apply(S.d_class_mask, S.d_mdeltas, cnt, S.stream));
+    HIP_TRY(kbg::launch_mask_apply(S.d_class_mask, dev_ptr(S, S.h_mdeltas), cnt, S.stream));  // read in place
     if ((st = stage_release(S)) != KBG_OK) return st;
     m += cnt;
   }
@@ -663,8 +707,7 @@ kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
       device_row(S, n, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &d.maxtasks);
     }
     if (cnt == 0) break;
-    HIP_TRY(hipMemcpyAsync(S.d_deltas, S.h_deltas, cnt * sizeof(kbg::NodeDelta), hipMemcpyHostToDevice, S.stream));
-    HIP_TRY(kbg::launch_apply(S.d_nodes, S.d_deltas, cnt, S.stream));
+    HIP_TRY(kbg::launch_apply(S.d_nodes, S.h_deltas_dev, cnt, S.stream));  // read in place
     if ((st = stage_release(S)) != KBG_OK) return st;
   }
   return KBG_OK;
@@ -2096,16 +2139,21 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   S.up_cap = up_cap;
   const size_t down_cap = 2 * (size_t)S.K + (size_t)S.cand_cap;  // counts, candidates, owner-resolve availability
   if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) || (st = dalloc(S, &S.d_up, up_cap)) ||
-      (st = dalloc(S, &S.d_bits, (size_t)S.R * 2 * S.K * kbg::kbg_slot_words(S.Wl))) ||
-      (st = dalloc(S, &S.d_down, down_cap)) || (st = dalloc(S, &S.d_deltas, S.K)))
+      (st = dalloc(S, &S.d_bits, S.comm ? (size_t)S.R * 2 * S.K * kbg::kbg_slot_words(S.Wl) : 1)) ||
+      (st = dalloc(S, &S.d_down, down_cap)))
     return st;
   for (kbg::Stage& g : S.stages) {
-    HIP_TRY(hipHostMalloc((void**)&g.h_up, up_cap, hipHostMallocDefault));
-    HIP_TRY(hipHostMalloc((void**)&g.h_down, down_cap * 4, hipHostMallocDefault));
+    if ((st = host_alloc((void**)&g.h_up, up_cap)) || (st = host_alloc((void**)&g.h_down, down_cap * 4))) return st;
     for (int e = 0; e < 6; ++e) HIP_TRY(hipEventCreate(&g.ev[e]));
     HIP_TRY(hipEventCreateWithFlags(&g.ev[6], hipEventDisableTiming));
   }
-  HIP_TRY(hipHostMalloc((void**)&S.h_deltas, (size_t)S.K * sizeof(kbg::NodeDelta), hipHostMallocDefault));
+  {  // unified addressing: a mapped host buffer has the same address on the device
+    void* d = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&d, S.stages[0].h_up, 0));
+    S.uva = d == (void*)S.stages[0].h_up;
+  }
+  if ((st = host_alloc((void**)&S.h_deltas, (size_t)S.K * sizeof(kbg::NodeDelta)))) return st;
+  S.h_deltas_dev = dev_ptr(S, S.h_deltas);
   if ((st = upload_nodes(S))) return st;
   phase("device alloc+nodes");
 
@@ -2152,8 +2200,7 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   S.h_class_mask_static = S.h_class_mask;
   setup_host_ports(S);
   setup_affinity(S);  // inter-pod (anti)affinity: folded in the same way (kbg_affinity.cpp)
-  HIP_TRY(hipHostMalloc((void**)&S.h_mdeltas, (size_t)kbg::kMaskDeltaCap * sizeof(kbg::MaskDelta), hipHostMallocDefault));
-  if ((st = dalloc(S, &S.d_mdeltas, kbg::kMaskDeltaCap))) return st;
+  if ((st = host_alloc((void**)&S.h_mdeltas, (size_t)kbg::kMaskDeltaCap * sizeof(kbg::MaskDelta)))) return st;
   if (S.has_ports || S.has_aff)
     HIP_TRY(hipMemcpy(S.d_class_mask, S.h_class_mask.data(), S.h_class_mask.size() * 8, hipMemcpyHostToDevice));
   S.h_class_mask0 = S.h_class_mask;
@@ -2240,12 +2287,14 @@ struct Pipe {
   std::deque<Batch*> ready;    // predicted, waiting for the committer
   std::vector<Batch*> free;    // recycled buffers
   int64_t epoch = 0;           // current epoch (committer-owned, read by predictor under mu)
-  bool rollback = false;       // predictor must restore `rb_ckpt` and replay
+  bool rollback = false;       // predictor must restore `rb_ckpt` and replay (or copy *rb_truth)
   Engine rb_ckpt;
+  const Engine* rb_truth = nullptr;  // the committed outcomes' engine, idle until the next batch
   std::vector<int32_t> rb_tasks;
   std::vector<char> rb_actual;
   bool stop = false;
   std::atomic<bool> hungry{false};  // the committer is blocked on an empty queue: emit what is predicted
+  std::atomic<int64_t> epoch_now{0};  // = epoch, read without the lock: a batch of an older epoch is abandoned
   std::deque<Batch*> raw;      // predicted, waiting for the builder (allocate_cycle)
   bool building = false;       // the builder holds a batch
   static constexpr size_t kDepth = 3;
@@ -2499,6 +2548,75 @@ kbg_status copy_log(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out, 
   return result;
 }
 
+// The committed outcomes replayed into an engine copy on a thread of its own.
+// Ranks other than 0 of a sharded allocate do not predict: this is their
+// engine (the plugin state later actions and the state queries read). In the
+// single-rank allocate it is the engine's "truth" a few tasks behind the
+// committer: at a cut the predictor takes its state instead of restoring a
+// checkpoint and replaying the batch's prefix.
+struct Replayer {
+  Session& S;
+  Engine& E;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::vector<std::pair<int32_t, char>>> q;
+  bool done = false, busy = false;
+  std::string error;
+  // committer_cpu >= 0: on its own core of the committer's last-level cache
+  // (after the predictor, logger and builder), never time-sharing the predictor's
+  Replayer(Session& s, Engine& e, int committer_cpu = -1) : S(s), E(e) {
+    th = std::thread([this, committer_cpu]() {
+      pin_near(committer_cpu, 4);
+      run();
+    });
+  }
+  ~Replayer() { join(); }
+  void push(std::vector<std::pair<int32_t, char>>&& v) {
+    std::lock_guard<std::mutex> lk(mu);
+    q.push_back(std::move(v));
+    cv.notify_all();
+  }
+  void join() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      done = true;
+      cv.notify_all();
+    }
+    if (th.joinable()) th.join();
+  }
+  // blocks until every pushed outcome is applied: E is then the engine state
+  // after the last of them
+  void wait_idle() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return q.empty() && !busy; });
+  }
+  void run() {
+    Ops ops{S, E, nullptr};
+    for (;;) {
+      std::vector<std::pair<int32_t, char>> v;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        busy = false;
+        cv.notify_all();
+        cv.wait(lk, [&] { return done || !q.empty(); });
+        if (q.empty()) return;
+        v = std::move(q.front());
+        q.pop_front();
+        busy = true;
+      }
+      for (const auto& [t, ok] : v) {
+        if (!error.empty()) break;
+        if (ops.next_task() != t) {
+          error = "internal: engine replay diverged from the committed outcomes";
+          break;
+        }
+        ops.apply(t, ok);
+      }
+    }
+  }
+};
+
 // The predictor thread of an allocate cycle (the ordering engine) and its
 // hand-off with the committer: predicted batches, recycled buffers, rollbacks.
 struct Predictor {
@@ -2514,6 +2632,7 @@ struct Predictor {
   Trace tr;
   std::thread th, bth;
   bool builder = false;       // a builder thread turns predicted batches into device rows (allocate_cycle)
+  bool truth_mode = false;    // rollbacks copy a truth engine (rollback_truth): no batch checkpoints
   std::vector<Batch*> all;    // every batch of this predictor (freed by finish)
   Predictor(Session& s, Engine& e, std::atomic<uint8_t>* f) : S(s), E(e), failed(f) {
     prof.on = getenv("KBG_PROFILE_ENGINE") != nullptr;
@@ -2544,7 +2663,7 @@ struct Predictor {
           if (!S.up_pool.empty()) {  // only this thread takes from the pool during a cycle
             b->st.h_up = S.up_pool.back();
             S.up_pool.pop_back();
-          } else if (hipHostMalloc((void**)&b->st.h_up, S.up_cap, hipHostMallocDefault) != hipSuccess) {
+          } else if (host_alloc((void**)&b->st.h_up, S.up_cap) != KBG_OK) {
             b->st.h_up = nullptr;
             std::lock_guard<std::mutex> lk(P.mu);
             error = "hipHostMalloc of a batch row buffer failed";
@@ -2577,7 +2696,14 @@ struct Predictor {
           return P.stop || P.rollback || (!exhausted && P.ready.size() + P.raw.size() < Pipe::kDepth);
         });
         if (P.stop) return;
-        if (P.rollback) {
+        if (P.rollback && P.rb_truth) {  // the engine state at the cut, kept by the truth replayer
+          const auto tp = clk::now();
+          E = *P.rb_truth;
+          P.rb_truth = nullptr;
+          engine_ms += ms_since(tp);
+          P.rollback = false;
+          exhausted = false;
+        } else if (P.rollback) {
           const auto tp = clk::now();
           E = P.rb_ckpt;
           for (size_t k = 0; k < P.rb_tasks.size(); ++k) {
@@ -2608,11 +2734,12 @@ struct Predictor {
         all.push_back(b);
       }
       const auto tp = clk::now();
-      b->ckpt = E;
+      if (!truth_mode) b->ckpt = E;
       b->epoch = my_epoch;
       b->bt.clear();
       b->bpred.clear();
       const size_t emit_at = (size_t)min_emit();
+      bool abandoned = false;
       while ((int32_t)b->bt.size() < S.K) {
         const int32_t t = ops.next_task();
         if (t < 0) break;
@@ -2620,13 +2747,26 @@ struct Predictor {
         b->bt.push_back(t);
         b->bpred.push_back(p);
         ops.apply(t, p);
-        // a committer with nothing to do takes a short batch now
-        if ((b->bt.size() & 63) == 0 && b->bt.size() >= emit_at && P.hungry.load(std::memory_order_relaxed)) {
-          P.hungry.store(false, std::memory_order_relaxed);  // one early batch per wait
-          break;
+        if ((b->bt.size() & 63) == 0) {
+          // the committer cut an earlier batch: this one follows a wrong
+          // prediction, stop here and roll back
+          if (P.epoch_now.load(std::memory_order_relaxed) != my_epoch) {
+            abandoned = true;
+            break;
+          }
+          // a committer with nothing to do takes a short batch now
+          if (b->bt.size() >= emit_at && P.hungry.load(std::memory_order_relaxed)) {
+            P.hungry.store(false, std::memory_order_relaxed);  // one early batch per wait
+            break;
+          }
         }
       }
       engine_ms += ms_since(tp);
+      if (abandoned) {
+        std::lock_guard<std::mutex> lk(P.mu);
+        P.free.push_back(b);
+        continue;
+      }
       tr.add("emit", (int64_t)b->bt.size());
       if (b->bt.empty()) exhausted = true;  // the empty batch marks the end of this epoch
       std::lock_guard<std::mutex> lk(P.mu);
@@ -2662,12 +2802,25 @@ struct Predictor {
   // a new epoch: the predictor restores `cur`'s checkpoint and replays the
   // actual outcomes of its first `cut` tasks; `cur` and `nxt` are recycled
   void rollback(int64_t epoch, Batch* cur, int32_t cut, const std::vector<char>& actual, Batch* nxt) {
+    P.epoch_now.store(epoch, std::memory_order_relaxed);
     std::lock_guard<std::mutex> lk(P.mu);
     P.epoch = epoch;
     P.rollback = true;
     P.rb_ckpt = cur->ckpt;
     P.rb_tasks.assign(cur->bt.begin(), cur->bt.begin() + cut);
     P.rb_actual.assign(actual.begin(), actual.begin() + cut);
+    P.free.push_back(cur);
+    if (nxt) P.free.push_back(nxt);
+    P.cv.notify_all();
+  }
+  // a new epoch from the engine state `truth` holds (the committed outcomes
+  // up to and including the cut, applied); `cur` and `nxt` are recycled
+  void rollback_truth(int64_t epoch, const Engine* truth, Batch* cur, Batch* nxt) {
+    P.epoch_now.store(epoch, std::memory_order_relaxed);
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.epoch = epoch;
+    P.rollback = true;
+    P.rb_truth = truth;
     P.free.push_back(cur);
     if (nxt) P.free.push_back(nxt);
     P.cv.notify_all();
@@ -2785,7 +2938,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
 
   // ------------------------------------------------------------ predictor
   Engine E = first ? S.init : live_engine(S);
+  Engine E_truth = E;  // the committed outcomes only (Replayer), the state a cut restarts from
+  Replayer truth(S, E_truth, sched_getcpu());
   Predictor pr(S, E, failed.get());
+  pr.truth_mode = true;
   EngineProfile& eprof = pr.prof;
   Trace ctr;
   ctr.start(t0);
@@ -2798,7 +2954,19 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   pr.start(sched_getcpu(), !no_builder);
   auto take = [&](bool block, bool* none) { return pr.take(block, none); };
   auto recycle = [&](Batch* b) { pr.recycle(b); };
-  auto finish = [&]() { pr.finish(); };
+  auto finish = [&]() {
+    pr.finish();
+    truth.join();
+  };
+  // committed outcomes of the current batch not yet handed to the truth engine
+  int32_t truth_from = 0;
+  auto to_truth = [&](const std::vector<int32_t>& bt, int32_t end) {
+    if (end <= truth_from) return;
+    std::vector<std::pair<int32_t, char>> v(end - truth_from);
+    for (int32_t k = truth_from; k < end; ++k) v[k - truth_from] = {bt[k], bactual[k]};
+    truth.push(std::move(v));
+    truth_from = end;
+  };
 
   // ------------------------------------------------------------ committer
   // Two stages in flight: while the host resolves batch b (stage `si`), the
@@ -2848,6 +3016,15 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     finish();
     return st;
   };
+  // A row whose scan found no node at all: its (class, request) shape fits
+  // nowhere in that table, so (monotone) nowhere for the rest of the cycle.
+  // The predictor predicts its later tasks as failures from now on instead of
+  // each first failure cutting a batch (predictions only: the committer still
+  // decides every task).
+  auto learn_failed = [&](const kbg::Stage& g) {
+    for (int32_t r = 0; r < g.G; ++r)
+      if (g.h_count[r] == 0) failed[g.row_shape[r]].store(1, std::memory_order_relaxed);
+  };
   // opt-in cycle counters of the in-order commit (KBG_PROFILE_RESOLVE=1):
   // candidate walk, host mirror, decision log, whole loop
   const bool rprof = getenv("KBG_PROFILE_RESOLVE") != nullptr;
@@ -2876,6 +3053,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     kbg_status st = device_wait(S, *sg);
     ctr.add("waited");
     if (st != KBG_OK) return abort(st);
+    learn_failed(*sg);
     // the next batch's scan overlaps this batch's resolve when it is ready
     Batch* nxt = next_batch(false);
     if (pred_failed) return abort(fail(KBG_E_INVALID, pr.error));
@@ -2898,8 +3076,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     const uint64_t cl0 = rprof ? cycles() : 0;
     const int32_t nb = (int32_t)bt.size();
     ctr.add("resolve", nb);
+    truth_from = 0;
     for (int32_t i = 0; i < nb; ++i) {
       const int32_t t = bt[i];
+      if ((i & 511) == 511) to_truth(bt, i);  // keep the truth engine a few hundred tasks behind
       if ((i & 1023) == 1023 && !nxt && !pred_failed) {
         // the predictor's next batch, if it is ready now, scans while this one resolves
         nxt = next_batch(false);
@@ -2934,6 +3114,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         }
         if (st == KBG_OK) st = device_wait(S, *sg);
         if (st != KBG_OK) return abort(st);
+        learn_failed(*sg);
         S.stats.device_ms += ms_since(tp);
         tp = clk::now();
         seg = i;
@@ -3016,10 +3197,16 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
                                      "(predicates.go:122-123)");
       break;
     }
-    if (cut >= 0) {  // roll the predictor back to this batch's checkpoint + the actual prefix
+    if (cut >= 0) {  // restart the predictor from the engine state at the cut
       if ((st = device_drop(S, other)) != KBG_OK) return abort(st);  // nxt was predicted before the cut
-      pr.rollback(++cur_epoch, cur, cut, bactual, nxt);
+      to_truth(bt, cut);
+      ctr.add("cut", cut);
+      truth.wait_idle();
+      ctr.add("truth", cut);
+      if (!truth.error.empty()) return abort(fail(KBG_E_INVALID, truth.error));
+      pr.rollback_truth(++cur_epoch, &E_truth, cur, nxt);
       cur = next_batch(true);
+      ctr.add("took");
       if (!cur) return abort(fail(KBG_E_INVALID, pr.error));
       if (!cur->bt.empty()) {
         tp = clk::now();
@@ -3028,6 +3215,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       }
       continue;
     }
+    to_truth(bt, nb);
     recycle(cur);
     if (!nxt) {  // the predictor was behind: take its next batch now and scan it
       ctr.add("take");
@@ -3052,6 +3240,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
   }
   finish();
+  if (!truth.error.empty()) return fail(KBG_E_INVALID, truth.error);
   if (lg) lg->join();  // the decision log and FitError records are complete
   HIP_TRY(hipStreamSynchronize(S.stream));  // last delta write-back
   compute_fit_deltas(S, dec, dec_old, dec_oldp, last);
@@ -3060,7 +3249,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
             (unsigned long long)S.affm->prof_calls,
             S.affm->prof_calls ? (double)S.affm->prof_cycles / S.affm->prof_calls : 0.0,
             (unsigned long long)S.affm->prof_recomputes, S.mask_dirty.size());
-  S.fin = E;
+  S.fin = E_truth;
   S.stats.engine_ms = pr.engine_ms;
   S.stats.replayed = pr.replayed;
   if (rprof)
@@ -3205,58 +3394,6 @@ bool owner_resolve_ok(const Session& S) {
   const bool ranks = S.R > 1 || (force && force[0] == '1');
   return S.comm && ranks && S.shard >= 0 && S.R <= 32 && !S.has_aff && !off;
 }
-
-// Ranks other than 0 do not predict: they replay the committed outcomes into
-// their own copy of the engine (the plugin state later actions and the state
-// queries read) on a thread of their own, as rank 0's predictor does.
-struct Replayer {
-  Session& S;
-  Engine& E;
-  std::thread th;
-  std::mutex mu;
-  std::condition_variable cv;
-  std::deque<std::vector<std::pair<int32_t, char>>> q;
-  bool done = false;
-  std::string error;
-  Replayer(Session& s, Engine& e) : S(s), E(e) {
-    th = std::thread([this]() { run(); });
-  }
-  ~Replayer() { join(); }
-  void push(std::vector<std::pair<int32_t, char>>&& v) {
-    std::lock_guard<std::mutex> lk(mu);
-    q.push_back(std::move(v));
-    cv.notify_all();
-  }
-  void join() {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      done = true;
-      cv.notify_all();
-    }
-    if (th.joinable()) th.join();
-  }
-  void run() {
-    Ops ops{S, E, nullptr};
-    for (;;) {
-      std::vector<std::pair<int32_t, char>> v;
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return done || !q.empty(); });
-        if (q.empty()) return;
-        v = std::move(q.front());
-        q.pop_front();
-      }
-      for (const auto& [t, ok] : v) {
-        if (!error.empty()) break;
-        if (ops.next_task() != t) {
-          error = "internal: engine replay diverged from rank 0";
-          break;
-        }
-        ops.apply(t, ok);
-      }
-    }
-  }
-};
 
 kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t cap, int32_t* n_out) {
   if (S.allocated || S.backfilled || S.preempted)
@@ -3850,7 +3987,7 @@ kbg_status vt_setup(Session& S) {
     S.vc.stop.assign(S.W32, 0u);
     S.vc.panic.assign(S.W32, 0u);
     S.vc.unk.assign(S.W32, 0u);
-    HIP_TRY(hipHostGetDevicePointer((void**)&S.h_deltas_dev, S.h_deltas, 0));
+
     if (!S.h_sdeltas) {
       HIP_TRY(hipHostMalloc((void**)&S.h_sdeltas, (size_t)kbg::kMaskDeltaCap * sizeof(kbg::StateDelta),
                             hipHostMallocMapped));
@@ -4864,8 +5001,7 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
         device_row(S, nd, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &d.maxtasks);
       }
       if (cnt == 0) break;
-      HIP_TRY(hipMemcpyAsync(S.d_deltas, S.h_deltas, cnt * sizeof(kbg::NodeDelta), hipMemcpyHostToDevice, S.stream));
-      HIP_TRY(kbg::launch_apply(S.d_nodes0, S.d_deltas, cnt, S.stream));
+      HIP_TRY(kbg::launch_apply(S.d_nodes0, S.h_deltas_dev, cnt, S.stream));  // read in place
       if ((st = stage_release(S)) != KBG_OK) return st;
     }
     // the live table restarts from the updated snapshot: the rows an action

@@ -190,6 +190,7 @@ struct Stage {
   int32_t G = 0;
   int32_t base = 0;                  // the scan saw every node delta of resolutions with stamp <= base
   bool inflight = false;             // launched, results not yet collected
+  bool fused = false;                // kbg_firstfit_kernel (no select kernel, no copies)
   hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // scan, select,
                                      // exchange start/stop; [6] = results on the host
 };
@@ -347,8 +348,7 @@ struct Session {
   std::vector<uint64_t> h_class_mask0, h_class_mask_static;  // at open (ports applied) / static predicate only
   std::vector<uint32_t> mask_dirty;            // class-mask words changed since the last write-back
   std::vector<uint8_t> mask_dirty_flag;
-  MaskDelta* h_mdeltas = nullptr;              // pinned staging
-  MaskDelta* d_mdeltas = nullptr;
+  MaskDelta* h_mdeltas = nullptr;              // pinned, mapped staging (read in place)
   // ---- inter-pod (anti)affinity folded into the class masks (kbg_affinity.cpp)
   bool has_aff = false;                        // some task carries a required pod (anti)affinity term
   std::shared_ptr<AffinityModel> affm;
@@ -422,8 +422,8 @@ struct Session {
   size_t up_cap = 0;              // bytes of one pinned row buffer (Stage::h_up)
   std::vector<char*> up_pool;     // spare pinned row buffers: the allocate builder's batches borrow them
   int32_t res_stamp = 0;          // resolution stamps: monotone over the session (mark / mwmark compare)
-  NodeDelta* d_deltas = nullptr;
-  NodeDelta* h_deltas = nullptr; // pinned
+  NodeDelta* h_deltas = nullptr; // pinned, mapped: the apply kernels read it in place
+  bool uva = false;              // mapped host memory has the same address on the device
   hipEvent_t stage_ev = nullptr; // after the last enqueued reader of the pinned staging (stage_acquire)
   bool stage_pending = false;
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};

@@ -34,8 +34,8 @@ def test_saturated_parity(saturated, opts):
     assert st.task_evaluations == ref["evaluated"]
     if not opts:
         # the speculation machinery really ran: unpredicted failures cut
-        # batches and the engine replayed to the cut
-        assert st.mispredictions > 0 and st.replayed > 0, (st.mispredictions, st.replayed)
+        # batches and the predictor restarted from the truth engine at the cut
+        assert st.mispredictions > 0, st.mispredictions
 
 
 @pytest.mark.slow
