@@ -237,6 +237,24 @@ hipError_t launch_select(const uint64_t* bits, int32_t w_lo, int32_t w_hi, int32
                          hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
 hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream);
+
+// FitError counts of not-ready jobs (kbg_fitdelta_kernel).
+struct FitQuery {
+  int32_t cls, end, point, win;  // static class; nodes [0, end); decisions before `point` applied; the winner
+  double req[3];                 // Resreq
+};
+struct FitArgs {
+  const double* nodes;         // the final node table block (FirstFitArgs.nodes)
+  int32_t stride, W;
+  const uint64_t* class_mask;  // static predicate [class][W]
+  const int32_t* hoff;         // [N + 1] each node's decisions
+  const int32_t* hk;           // decision index | 0x80000000 for a Pipeline
+  const double* hold;          // [3] per decision: the Idle (Allocate) / Releasing (Pipeline) before it
+  const FitQuery* q;
+  int32_t nq, cap_check;
+  int32_t* out;                // [nq][4]: entries, negative cpu, memory, GPU deltas
+};
+hipError_t launch_fitdelta(const FitArgs& a, hipStream_t stream);
 hipError_t launch_mask_apply(uint64_t* class_mask, const MaskDelta* deltas, int32_t n_deltas, hipStream_t stream);
 
 // One victim scan evaluates every node of the range for one (preemptor,

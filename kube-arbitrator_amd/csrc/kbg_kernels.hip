@@ -340,6 +340,63 @@ hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t 
   return hipGetLastError();
 }
 
+// ------------------------------------------------------- FitError counts
+// JobInfo.NodesFitDelta of a not-ready job's last evaluated task
+// (allocate.go:116-144), summarised as JobInfo.FitError counts it
+// (job_info.go:329-358), for every such job at once: one workgroup per job,
+// its threads over the nodes before the task's end. A node's state at the
+// task's evaluation point is the final table with the decisions at or after
+// that point undone: the node's decisions in order (hk, hold), the first
+// undone Allocate giving its Idle, the undone count its pod count.
+__global__ __launch_bounds__(256) void kbg_fitdelta_kernel(FitArgs a) {
+  __shared__ int32_t s_cnt[4];
+  const FitQuery fq = a.q[blockIdx.x];
+  if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int32_t* ni = reinterpret_cast<const int32_t*>(a.nodes + 6 * (size_t)a.stride);
+  int32_t c_nodes = 0, c_cpu = 0, c_mem = 0, c_gpu = 0;
+  for (int n = threadIdx.x; n < fq.end; n += blockDim.x) {
+    if (!((a.class_mask[(size_t)fq.cls * a.W + (n >> 6)] >> (n & 63)) & 1ull)) continue;  // static predicate
+    const int e1 = a.hoff[n + 1];
+    int e = a.hoff[n];
+    while (e < e1 && (a.hk[e] & 0x7fffffff) < fq.point) ++e;  // decisions before the evaluation stay applied
+    if (a.cap_check && ni[n] - (e1 - e) >= ni[a.stride + n]) continue;  // pod cap then (predicates.go:125-127)
+    double ic = a.nodes[n], im = a.nodes[a.stride + n], ig = a.nodes[2 * (size_t)a.stride + n];
+    for (int x = e; x < e1; ++x)
+      if (!(a.hk[x] & 0x80000000)) {  // the first undone Allocate: Idle before it
+        ic = a.hold[3 * (size_t)x];
+        im = a.hold[3 * (size_t)x + 1];
+        ig = a.hold[3 * (size_t)x + 2];
+        break;
+      }
+    if (n != fq.win && le(fq.req[0], ic, kMinMilliCPU) && le(fq.req[1], im, kMinMemory) &&
+        le(fq.req[2], ig, kMinMilliGPU))
+      continue;  // would have been chosen
+    // Resource.FitDelta (resource_info.go:116-129)
+    const double dc = fq.req[0] > 0 ? ic - (fq.req[0] + kMinMilliCPU) : ic;
+    const double dm = fq.req[1] > 0 ? im - (fq.req[1] + kMinMemory) : im;
+    const double dg = fq.req[2] > 0 ? ig - (fq.req[2] + kMinMilliGPU) : ig;
+    ++c_nodes;
+    c_cpu += dc < 0;
+    c_mem += dm < 0;
+    c_gpu += dg < 0;
+  }
+  if (c_nodes) {
+    atomicAdd(&s_cnt[0], c_nodes);
+    atomicAdd(&s_cnt[1], c_cpu);
+    atomicAdd(&s_cnt[2], c_mem);
+    atomicAdd(&s_cnt[3], c_gpu);
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) a.out[4 * (size_t)blockIdx.x + threadIdx.x] = s_cnt[threadIdx.x];
+}
+
+hipError_t launch_fitdelta(const FitArgs& a, hipStream_t stream) {
+  if (a.nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kbg_fitdelta_kernel, dim3(a.nq), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- select
 // One wave per row walks the row's words [w_lo, w_hi) in global node order
 // (shard slots in rank order = ascending node index), so the candidates come

@@ -460,6 +460,13 @@ void free_device(Session& S) {
   if (S.h_deltas) (void)hipHostFree(S.h_deltas);
   if (S.h_mdeltas) (void)hipHostFree(S.h_mdeltas);
   S.h_mdeltas = nullptr;
+  if (S.fit_h) (void)hipHostFree(S.fit_h);
+  if (S.fit_out) (void)hipHostFree(S.fit_out);
+  if (S.fit_d) (void)hipFree(S.fit_d);
+  S.fit_h = nullptr;
+  S.fit_out = nullptr;
+  S.fit_d = nullptr;
+  S.fit_cap = S.fit_out_cap = 0;
   if (S.h_vbits) (void)hipHostFree(S.h_vbits);
   if (S.h_sdeltas) (void)hipHostFree(S.h_sdeltas);
   S.h_vbits = nullptr;
@@ -1656,6 +1663,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     S.maxtasks[n] = S.nodes_in[n].max_task_num;
     S.nil_node[n] = S.nodes_in[n].has_node ? 0 : 1;
   }
+  S.any_nil = std::find(S.nil_node.begin(), S.nil_node.end(), 1) != S.nil_node.end();
   S.panic_node.assign(N, 0);
   if (S.pred_active)
     for (int32_t n = 0; n < N; ++n) S.panic_node[n] = S.nil_node[n];
@@ -2366,13 +2374,95 @@ struct LastEval {
 // the counts JobInfo.FitError prints (job_info.go:329-358). The node states
 // at each job's evaluation point are rebuilt by undoing the decision log
 // backwards from the final mirror (exact: the pre-commit values are logged).
-void compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, const std::vector<Res>& dec_old,
-                        const std::vector<uint64_t>& dec_oldp, const std::vector<LastEval>& last) {
+// The same counts on the device (kbg_fitdelta_kernel): one workgroup per job
+// over the final node table with each node's decisions after the job's point
+// undone, for sessions whose predicate at an evaluation point is the static
+// mask plus the pod cap (no host ports, no pod affinity, no nil Node) and
+// whose whole node table is local.
+kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, const std::vector<Res>& dec_old,
+                             const std::vector<LastEval>& last, const std::vector<int32_t>& jobs) {
+  std::vector<int32_t> qj;
+  int32_t kmin = (int32_t)dec.size();
+  for (int32_t j : jobs) {
+    Session::FitCounts& fc = S.fit[j];
+    fc.valid = 1;
+    if (last[j].task < 0) continue;  // never evaluated: empty map, "0 nodes are available"
+    qj.push_back(j);
+    kmin = std::min(kmin, last[j].before);
+  }
+  if (qj.empty()) return KBG_OK;
+  const int32_t N = S.n_nodes, Q = (int32_t)qj.size();
+  std::vector<int32_t> cnt(N + 1, 0);
+  for (int32_t k = kmin; k < (int32_t)dec.size(); ++k)
+    if (!S.dec_dup[k]) cnt[dec[k].node + 1]++;
+  for (int32_t n = 0; n < N; ++n) cnt[n + 1] += cnt[n];
+  const int32_t E = cnt[N];
+  // one block: hoff[N+1] | hk[E] | pad | hold[E][3] | queries[Q]; results [Q][4] mapped
+  const size_t o_hk = (size_t)(N + 1) * 4, o_hold = (o_hk + (size_t)E * 4 + 15) / 16 * 16,
+               o_q = o_hold + (size_t)E * 24, bytes = o_q + (size_t)Q * sizeof(kbg::FitQuery),
+               out_bytes = (size_t)Q * 16;
+  if (bytes > S.fit_cap) {
+    if (S.fit_h) (void)hipHostFree(S.fit_h);
+    if (S.fit_d) (void)hipFree(S.fit_d);
+    S.fit_h = nullptr;
+    S.fit_d = nullptr;
+    S.fit_cap = 0;
+    if (host_alloc((void**)&S.fit_h, bytes) != KBG_OK) return fail(KBG_E_HIP, "FitError staging");
+    HIP_TRY(hipMalloc((void**)&S.fit_d, bytes));
+    S.fit_cap = bytes;
+  }
+  if (out_bytes > S.fit_out_cap) {
+    if (S.fit_out) (void)hipHostFree(S.fit_out);
+    S.fit_out = nullptr;
+    S.fit_out_cap = 0;
+    if (host_alloc((void**)&S.fit_out, out_bytes) != KBG_OK) return fail(KBG_E_HIP, "FitError results");
+    S.fit_out_cap = out_bytes;
+  }
+  int32_t* hoff = (int32_t*)S.fit_h;
+  int32_t* hk = (int32_t*)(S.fit_h + o_hk);
+  double* hold = (double*)(S.fit_h + o_hold);
+  kbg::FitQuery* fq = (kbg::FitQuery*)(S.fit_h + o_q);
+  std::copy(cnt.begin(), cnt.end(), hoff);
+  for (int32_t k = kmin; k < (int32_t)dec.size(); ++k) {
+    if (S.dec_dup[k]) continue;
+    const int32_t e = cnt[dec[k].node]++;
+    hk[e] = k | (dec[k].kind == KBG_KIND_PIPELINE ? (int32_t)0x80000000 : 0);
+    hold[3 * (size_t)e] = dec_old[k].c;
+    hold[3 * (size_t)e + 1] = dec_old[k].m;
+    hold[3 * (size_t)e + 2] = dec_old[k].g;
+  }
+  for (int32_t i = 0; i < Q; ++i) {
+    const LastEval& le = last[qj[i]];
+    const Res& r = S.treq[le.task];
+    fq[i] = kbg::FitQuery{S.task_class[le.task], le.node < 0 ? N : le.node + (le.kind == KBG_KIND_PIPELINE ? 1 : 0),
+                          le.before, le.node, {r.c, r.m, r.g}};
+  }
+  HIP_TRY(hipMemcpyAsync(S.fit_d, S.fit_h, bytes, hipMemcpyHostToDevice, S.stream));
+  kbg::FitArgs a{S.d_nodes.idle_cpu, soa_stride(S), S.W, S.d_class_mask, (const int32_t*)S.fit_d,
+                 (const int32_t*)(S.fit_d + o_hk), (const double*)(S.fit_d + o_hold),
+                 (const kbg::FitQuery*)(S.fit_d + o_q), Q, S.pred_active ? 1 : 0, dev_ptr(S, S.fit_out)};
+  HIP_TRY(kbg::launch_fitdelta(a, S.stream));
+  HIP_TRY(hipStreamSynchronize(S.stream));
+  for (int32_t i = 0; i < Q; ++i) {
+    Session::FitCounts& fc = S.fit[qj[i]];
+    fc.nodes = S.fit_out[4 * i];
+    fc.cpu = S.fit_out[4 * i + 1];
+    fc.mem = S.fit_out[4 * i + 2];
+    fc.gpu = S.fit_out[4 * i + 3];
+  }
+  return KBG_OK;
+}
+
+kbg_status compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, const std::vector<Res>& dec_old,
+                              const std::vector<uint64_t>& dec_oldp, const std::vector<LastEval>& last) {
   S.fit.assign(S.n_jobs, Session::FitCounts{});
   std::vector<int32_t> jobs;
   for (int32_t j = 0; j < S.n_jobs; ++j)
     if (S.committed_ready[j] < S.jobs_in[j].min_available) jobs.push_back(j);
-  if (jobs.empty()) return;
+  if (jobs.empty()) return KBG_OK;
+  static const bool host_only = getenv("KBG_HOST_FITDELTA") != nullptr;
+  if (S.stream && !S.comm && !S.has_ports && !S.has_aff && !S.any_nil && !host_only)
+    return fit_deltas_device(S, dec, dec_old, last, jobs);
   std::sort(jobs.begin(), jobs.end(), [&](int32_t a, int32_t b) { return last[a].before > last[b].before; });
   std::vector<Res> idle = S.idle, rel = S.rel;
   std::vector<int32_t> ntasks = S.ntasks;
@@ -2436,6 +2526,7 @@ void compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, const 
       fc.gpu += nil_delta.g < 0;
     }
   }
+  return KBG_OK;
 }
 
 // State of a cycle's first action: the decision log, gang dispatch lists,
@@ -3240,10 +3331,13 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
   }
   finish();
+  ctr.add("joined");
   if (!truth.error.empty()) return fail(KBG_E_INVALID, truth.error);
   if (lg) lg->join();  // the decision log and FitError records are complete
+  ctr.add("logged");
   HIP_TRY(hipStreamSynchronize(S.stream));  // last delta write-back
-  compute_fit_deltas(S, dec, dec_old, dec_oldp, last);
+  if (kbg_status st = compute_fit_deltas(S, dec, dec_old, dec_oldp, last); st != KBG_OK) return st;
+  ctr.add("fit");
   if (S.has_aff && getenv("KBG_PROFILE_AFF"))
     fprintf(stderr, "[kbg aff] aff_place %llu calls, %.1f cycles/call, %llu bit recomputes, mask words dirty %zu\n",
             (unsigned long long)S.affm->prof_calls,
@@ -3714,7 +3808,7 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
   finish();
   S.owner = false;
   if (kbg_status st = io.sync(S); st != KBG_OK) return st;
-  compute_fit_deltas(S, dec, dec_old, dec_oldp, last);
+  if (kbg_status st = compute_fit_deltas(S, dec, dec_old, dec_oldp, last); st != KBG_OK) return st;
   S.stats.task_evaluations += logged;
   if (rp && !rp->error.empty()) return fail(KBG_E_INVALID, rp->error);
   S.fin = E;

@@ -276,6 +276,7 @@ struct Session {
   std::vector<Res> idle0, rel0, idle, rel;
   std::vector<int32_t> ntasks0, ntasks, maxtasks;
   std::vector<char> nil_node;
+  bool any_nil = false;
   std::vector<char> panic_node;  // nil Node under an active predicates plugin (predicates.go:122-123)
 
   // ---- the cycle's actions (allocate, then backfill) on this snapshot
@@ -333,6 +334,10 @@ struct Session {
   std::vector<int32_t> committed_ready;
   struct FitCounts { int32_t valid = 0, nodes = 0, cpu = 0, mem = 0, gpu = 0; };
   std::vector<FitCounts> fit;               // per job (A17)
+  char* fit_h = nullptr;                    // FitError inputs: pinned staging, device copy, mapped results
+  char* fit_d = nullptr;
+  int32_t* fit_out = nullptr;
+  size_t fit_cap = 0, fit_out_cap = 0;
   std::vector<uint64_t> h_class_mask;       // host copy of the class masks the scan reads (static predicate,
                                             // and with host ports the dynamic port fit)
   // ---- host ports (vendor predicates.go:1031-1051). A node's used ports only
