@@ -190,21 +190,23 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
 // ------------------------------------------------------ fused first-fit
 // kbg_firstfit_kernel: the scan and the candidate extraction in one launch,
 // with no feasibility bitmap in between. A workgroup owns kFfRows rows and
-// walks their words [w_lo, w_hi) in node order, kFfWaves words per round:
-// wave w evaluates word (round * kFfWaves + w) for every row exactly as
-// kbg_scan_kernel does (64 nodes in registers, one ballot per dimension, the
-// raw masks moved to lane J with v_writelane_b32, class mask / pod cap /
-// Releasing shortcut applied by lane J), and parks the row masks in LDS; after
-// the round's barrier wave j takes row j's kFfWaves words in node order and
-// appends the set bits to the row's list (lane = node, position = found +
-// mbcnt), at most `want` of them. Rows read their requests and list offsets
-// from host-mapped memory and write counts and candidates straight into it:
-// no copy kernel on either side. `early_exit` (production mode) ends the walk
-// once every row of the workgroup has more nodes than its list holds (the
-// rest of the table cannot change its list); full-scan mode evaluates every
-// node for every row.
+// walks their words [w_lo, w_hi) in node order, up to kFfMaxRound words per
+// round (C3's 79 in one): wave w evaluates words w, w + kFfWaves, ... of the
+// round for every row exactly as kbg_scan_kernel does (64 nodes in registers,
+// one ballot per dimension, the raw masks moved to lane J with
+// v_writelane_b32, class mask / pod cap / Releasing shortcut applied by lane
+// J) and parks the row masks in LDS; after the round's barrier wave j takes
+// row j's words in node order and appends the set bits to the row's list
+// (lane = node, position = found + mbcnt), at most `want` of them. Rows read
+// their requests and list offsets from host-mapped memory and write counts
+// and candidates straight into it: no copy kernel on either side.
+// `early_exit` (production mode) ends the walk after a round in which every
+// row of the workgroup got more nodes than its list holds (the rest of the
+// table cannot change its list); full-scan mode evaluates every node for
+// every row.
 constexpr int kFfRows = 16;
-constexpr int kFfWaves = 16;
+constexpr int kFfWaves = 16;      // == kFfRows: wave j extracts row j
+constexpr int kFfMaxRound = 128;  // words per round (LDS: 2 x 128 x 16 x 8 B)
 // rows whose requests are read from LDS together: 4 (integer thresholds) / 2
 // (the reference expression) keep the kernel at 8 waves per SIMD, no spills
 template <bool INT_MODE>
@@ -220,9 +222,9 @@ template <bool INT_MODE>
 __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArgs a) {
   __shared__ double s_req[kFfRows][3];
   __shared__ int32_t s_cls[kFfRows], s_flags[kFfRows];
-  __shared__ uint64_t s_f[2][kFfWaves][kFfRows];  // [round parity][word of the round][row]: fit anywhere
-  __shared__ uint64_t s_i[2][kFfWaves][kFfRows];  //                                       fit in Idle
-  __shared__ uint32_t s_done[2][kFfRows];
+  __shared__ uint64_t s_f[kFfMaxRound][kFfRows];  // [word of the round][row]: fits (Idle or Releasing)
+  __shared__ uint64_t s_i[kFfMaxRound][kFfRows];  //                        fits in Idle
+  __shared__ uint32_t s_done[kFfRows];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g0 = blockIdx.x * kFfRows;
@@ -234,7 +236,7 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
     s_cls[lane] = tr.cls;
     s_flags[lane] = tr.flags;
   }
-  // wave j extracts row g0 + j (kFfWaves == kFfRows)
+  // wave j extracts row g0 + j
   const int g = g0 + wave;
   const bool has_row = g < a.G;
   uint32_t base = 0, want = 0;
@@ -245,16 +247,18 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
   }
   uint32_t found = 0;
   bool done = !has_row;
-  if (lane == 0) s_done[1][wave] = done ? 1u : 0u;  // read by round 0's exit test
   __syncthreads();
   const int cls_l = s_cls[lane & (kFfRows - 1)];
   const int flags_l = s_flags[lane & (kFfRows - 1)];
-  const int rounds = (a.w_hi - a.w_lo + kFfWaves - 1) / kFfWaves;
-  for (int r = 0; r < rounds; ++r) {
-    const int buf = r & 1;
-    const int c = a.w_lo + r * kFfWaves + wave;  // this wave's global 64-node word
-    uint64_t f = 0ull, fi = 0ull;
-    if (c < a.w_hi) {  // wave-uniform
+#pragma unroll 1
+  for (int r0 = a.w_lo; r0 < a.w_hi; r0 += kFfMaxRound) {
+    const int nw = min(kFfMaxRound, a.w_hi - r0);  // words of this round
+#pragma unroll 1
+    for (int k = wave; k < nw; k += kFfWaves) {     // this wave's words of the round
+      // the row requests are re-read from LDS per word (kept in registers
+      // across the loop they would take 96 VGPRs)
+      asm volatile("" ::: "memory");
+      const int c = r0 + k;                          // global 64-node word
       const int node = c * 64 + lane;
       const int row = node - a.tab_lo;
       const bool valid = node < a.n_nodes && row < a.tab_n;
@@ -284,44 +288,48 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
         scan_rows<INT_MODE, false, kFfRows, 0, kFfGroup<INT_MODE>>(s_req, ic, im, ig, rc, rm, rg, keep);
         mr = (uint64_t)keep[2] | ((uint64_t)keep[3] << 32);
       }
-      const uint64_t mw = lane_mw & okm;
-      fi = ((uint64_t)keep[0] | ((uint64_t)keep[1] << 32)) & mw;
-      f = fi | (mr & mw);
-    }
-    if (lane < kFfRows) {
-      s_f[buf][wave][lane] = f;
-      s_i[buf][wave][lane] = fi;
+      if (lane < kFfRows) {
+        const uint64_t mw = lane_mw & okm;
+        const uint64_t fi = ((uint64_t)keep[0] | ((uint64_t)keep[1] << 32)) & mw;
+        s_f[k][lane] = fi | (mr & mw);
+        s_i[k][lane] = fi;
+      }
     }
     __syncthreads();
-    if (a.early_exit) {  // every row's list is full: the same decision in every wave
-      const uint32_t d = lane < kFfRows ? s_done[buf ^ 1][lane] : 1u;
-      if (__ballot(d == 0u) == 0ull) break;
-    }
-    if (!done) {  // wave-uniform: this wave's row, the round's words in node order
-      uint64_t fk = 0ull, ik = 0ull;
-      if (lane < kFfWaves) {
-        fk = s_f[buf][lane][wave];
-        ik = s_i[buf][lane][wave];
-      }
-      uint64_t nz = __ballot(fk != 0ull);
-      while (nz) {
-        const int k = __builtin_ctzll(nz);
-        nz &= nz - 1ull;
-        const uint64_t m = readlane64(fk, k);
-        const uint64_t mi = readlane64(ik, k);
-        const uint32_t pos =
-            found + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (((m >> lane) & 1ull) && pos < want)
-          a.down[a.G + base + pos] =
-              (uint32_t)((a.w_lo + r * kFfWaves + k) * 64 + lane) | (((mi >> lane) & 1ull) ? 0u : kCandPipelineBit);
-        found += (uint32_t)__popcll(m);
-        if (found > want) {
-          done = true;
-          break;
+    if (!done) {  // wave-uniform: this wave's row, the round's words in node order, 64 at a time
+#pragma unroll 1
+      for (int k0 = 0; k0 < nw && !done; k0 += 64) {
+        uint64_t fk = 0ull, ik = 0ull;
+        if (k0 + lane < nw) {
+          fk = s_f[k0 + lane][wave];
+          ik = s_i[k0 + lane][wave];
+        }
+        uint64_t nz = __ballot(fk != 0ull);
+        while (nz) {
+          const int k = __builtin_ctzll(nz);
+          nz &= nz - 1ull;
+          const uint64_t m = readlane64(fk, k);
+          const uint64_t mi = readlane64(ik, k);
+          const uint32_t pos =
+              found + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (((m >> lane) & 1ull) && pos < want)
+            a.down[a.G + base + pos] =
+                (uint32_t)((r0 + k0 + k) * 64 + lane) | (((mi >> lane) & 1ull) ? 0u : kCandPipelineBit);
+          found += (uint32_t)__popcll(m);
+          if (found > want) {
+            done = true;
+            break;
+          }
         }
       }
     }
-    if (lane == 0) s_done[buf][wave] = done ? 1u : 0u;
+    if (r0 + kFfMaxRound >= a.w_hi) break;  // the last round: no second barrier
+    if (lane == 0) s_done[wave] = done ? 1u : 0u;
+    __syncthreads();  // the round's masks are read; every row's state is in s_done
+    if (a.early_exit) {  // every row's list is full: the same decision in every wave
+      const uint32_t d = lane < kFfRows ? s_done[lane] : 1u;
+      if (__ballot(d == 0u) == 0ull) break;
+    }
   }
   if (has_row && lane == 0) {
     a.down[g] = (found < want ? found : want) | (found > want ? kCountIncompleteBit : 0u);

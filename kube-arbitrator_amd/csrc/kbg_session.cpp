@@ -2277,6 +2277,35 @@ void print_traces(const Trace& a, const Trace& b) {
   for (auto& [t, w, v, who] : all) fprintf(stderr, "[kbg trace] %9.1f %c %-10s %lld\n", t, who, w, (long long)v);
 }
 
+// A condition variable whose waiters spin briefly before they block: the
+// hand-offs of an allocate cycle (predictor -> committer batches, rollbacks,
+// the truth engine) are tens of microseconds apart, less than a futex wake-up
+// takes to come back. Every state change a waiter can see is followed by
+// notify_all(), which bumps `gen`; a waiter re-checks its predicate under the
+// lock whenever gen moves, for about 50 us, then sleeps on the real
+// condition variable.
+struct SpinCV {
+  std::condition_variable cv;
+  std::atomic<uint64_t> gen{0};
+  void notify_all() {
+    gen.fetch_add(1, std::memory_order_release);
+    cv.notify_all();
+  }
+  template <class Pred>
+  void wait(std::unique_lock<std::mutex>& lk, Pred pred) {
+    if (pred()) return;
+    constexpr int kSpins = 4096;
+    for (int i = 0; i < kSpins;) {
+      const uint64_t g = gen.load(std::memory_order_acquire);
+      lk.unlock();
+      while (gen.load(std::memory_order_acquire) == g && ++i < kSpins) __builtin_ia32_pause();
+      lk.lock();
+      if (pred()) return;
+    }
+    cv.wait(lk, pred);
+  }
+};
+
 struct Batch {
   std::vector<int32_t> bt;
   std::vector<char> bpred;
@@ -2291,7 +2320,7 @@ struct Batch {
 
 struct Pipe {
   std::mutex mu;
-  std::condition_variable cv;
+  SpinCV cv;
   std::deque<Batch*> ready;    // predicted, waiting for the committer
   std::vector<Batch*> free;    // recycled buffers
   int64_t epoch = 0;           // current epoch (committer-owned, read by predictor under mu)
@@ -2650,7 +2679,7 @@ struct Replayer {
   Engine& E;
   std::thread th;
   std::mutex mu;
-  std::condition_variable cv;
+  SpinCV cv;
   std::deque<std::vector<std::pair<int32_t, char>>> q;
   bool done = false, busy = false;
   std::string error;
@@ -2777,7 +2806,7 @@ struct Predictor {
     auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     pin_near(committer_cpu);
     Ops ops{S, E, prof.on ? &prof : nullptr};
-    bool exhausted = false;
+    bool exhausted = false, restarted = false;
     for (;;) {
       Batch* b = nullptr;
       int64_t my_epoch;
@@ -2794,6 +2823,7 @@ struct Predictor {
           engine_ms += ms_since(tp);
           P.rollback = false;
           exhausted = false;
+          restarted = true;
         } else if (P.rollback) {
           const auto tp = clk::now();
           E = P.rb_ckpt;
@@ -2829,7 +2859,10 @@ struct Predictor {
       b->epoch = my_epoch;
       b->bt.clear();
       b->bpred.clear();
-      const size_t emit_at = (size_t)min_emit();
+      // right after a cut the committer waits with nothing to scan: hand it
+      // the first 64 tasks (the next cut is often a few tasks away)
+      const size_t emit_at = restarted ? 64 : (size_t)min_emit();
+      restarted = false;
       bool abandoned = false;
       while ((int32_t)b->bt.size() < S.K) {
         const int32_t t = ops.next_task();
