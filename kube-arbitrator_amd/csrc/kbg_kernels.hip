@@ -195,9 +195,11 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
 // round for every row exactly as kbg_scan_kernel does (64 nodes in registers,
 // one ballot per dimension, the raw masks moved to lane J with
 // v_writelane_b32, class mask / pod cap / Releasing shortcut applied by lane
-// J) and parks the row masks in LDS; after the round's barrier wave j takes
-// row j's words in node order and appends the set bits to the row's list
-// (lane = node, position = found + mbcnt), at most `want` of them. Rows read
+// J) and parks the row masks in LDS; after the round's barrier wave j places
+// row j's words (a prefix sum of their node counts gives each word's first
+// list position) and then all waves append the placed words' nodes to the
+// lists (lane = node, position = word start + mbcnt), at most `want` per row,
+// so a long list is written by 16 waves instead of walked by one. Rows read
 // their requests and list offsets from host-mapped memory and write counts
 // and candidates straight into it: no copy kernel on either side.
 // `early_exit` (production mode) ends the walk after a round in which every
@@ -206,25 +208,20 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
 // every row.
 constexpr int kFfRows = 16;
 constexpr int kFfWaves = 16;      // == kFfRows: wave j extracts row j
-constexpr int kFfMaxRound = 128;  // words per round (LDS: 2 x 128 x 16 x 8 B)
+constexpr int kFfMaxRound = 128;  // words per round (LDS: 2 x 128 x 16 x 8 B); a multiple of kFfWaves
 // rows whose requests are read from LDS together: 4 (integer thresholds) / 2
 // (the reference expression) keep the kernel at 8 waves per SIMD, no spills
 template <bool INT_MODE>
 constexpr int kFfGroup = INT_MODE ? 4 : 2;
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)v, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)(v >> 32), l);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-template <bool INT_MODE>
+template <bool INT_MODE, bool EARLY_EXIT>
 __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArgs a) {
   __shared__ double s_req[kFfRows][3];
   __shared__ int32_t s_cls[kFfRows], s_flags[kFfRows];
   __shared__ uint64_t s_f[kFfMaxRound][kFfRows];  // [word of the round][row]: fits (Idle or Releasing)
   __shared__ uint64_t s_i[kFfMaxRound][kFfRows];  //                        fits in Idle
-  __shared__ uint32_t s_done[kFfRows];
+  __shared__ uint32_t s_pos[kFfMaxRound][kFfRows];  // list position of the word's first node
+  __shared__ uint32_t s_done[kFfRows], s_need[kFfRows], s_want[kFfRows], s_base[kFfRows];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g0 = blockIdx.x * kFfRows;
@@ -245,11 +242,47 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
     base = capoff[g];
     want = capoff[g + 1] - base;
   }
+  if (lane == 0) {
+    s_want[wave] = want;
+    s_base[wave] = base;
+  }
   uint32_t found = 0;
   bool done = !has_row;
+  // A word's node rows (and, once the rows' classes are known, their class
+  // mask words) are loaded one word ahead of its compares: the next word's
+  // loads are in flight while this one is evaluated. The first word's loads
+  // are issued before the rows arrive from host memory.
+  struct Word {
+    double ic = 0, im = 0, ig = 0, rc = 0, rm = 0, rg = 0;
+    int32_t nt = 0, mt = 0;
+    bool valid = false;
+  };
+  auto load_word = [&](int c, Word& w) {
+    const int node = c * 64 + lane;
+    const int row = node - a.tab_lo;
+    w.valid = node < a.n_nodes && row < a.tab_n;
+    if (w.valid) {
+      const double* p = a.nodes + row;
+      w.ic = p[0];
+      w.im = p[a.stride];
+      w.ig = p[2 * a.stride];
+      w.rc = p[3 * a.stride];
+      w.rm = p[4 * a.stride];
+      w.rg = p[5 * a.stride];
+      const int32_t* q = reinterpret_cast<const int32_t*>(a.nodes + 6 * (size_t)a.stride) + row;
+      w.nt = q[0];
+      w.mt = q[a.stride];
+    }
+  };
+  Word cur;
+  if (wave < min(kFfMaxRound, a.w_hi - a.w_lo)) load_word(a.w_lo + wave, cur);
   __syncthreads();
   const int cls_l = s_cls[lane & (kFfRows - 1)];
   const int flags_l = s_flags[lane & (kFfRows - 1)];
+  // rounds are kFfMaxRound (a multiple of kFfWaves) words apart, so a wave's
+  // words are c, c + kFfWaves, ... across rounds too
+  uint64_t lane_mw = (lane < kFfRows && a.w_lo + wave < a.w_hi) ? a.class_mask[(size_t)cls_l * a.W + a.w_lo + wave]
+                                                                   : 0ull;
 #pragma unroll 1
   for (int r0 = a.w_lo; r0 < a.w_hi; r0 += kFfMaxRound) {
     const int nw = min(kFfMaxRound, a.w_hi - r0);  // words of this round
@@ -259,33 +292,24 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
       // across the loop they would take 96 VGPRs)
       asm volatile("" ::: "memory");
       const int c = r0 + k;                          // global 64-node word
-      const int node = c * 64 + lane;
-      const int row = node - a.tab_lo;
-      const bool valid = node < a.n_nodes && row < a.tab_n;
-      double ic = 0, im = 0, ig = 0, rc = 0, rm = 0, rg = 0;
-      int32_t nt = 0, mt = 0;
-      if (valid) {
-        const double* p = a.nodes + row;
-        ic = p[0];
-        im = p[a.stride];
-        ig = p[2 * a.stride];
-        rc = p[3 * a.stride];
-        rm = p[4 * a.stride];
-        rg = p[5 * a.stride];
-        const int32_t* q = reinterpret_cast<const int32_t*>(a.nodes + 6 * (size_t)a.stride) + row;
-        nt = q[0];
-        mt = q[a.stride];
+      const int cn = c + kFfWaves < a.w_hi ? c + kFfWaves : -1;  // this wave's next word
+      Word nxt;
+      uint64_t nxt_mw = 0ull;
+      if (cn >= 0) {
+        load_word(cn, nxt);
+        if (lane < kFfRows) nxt_mw = a.class_mask[(size_t)cls_l * a.W + cn];
       }
-      const uint64_t lane_mw = lane < kFfRows ? a.class_mask[(size_t)cls_l * a.W + c] : 0ull;
-      const uint64_t okm = __ballot(valid && (!a.cap_check || nt < mt));  // predicates.go:125-127 pod cap
-      const bool rel_zero_wave = __ballot(!(rc == 0.0 && rm == 0.0 && rg == 0.0)) == 0ull;
+      const uint64_t okm = __ballot(cur.valid && (!a.cap_check || cur.nt < cur.mt));  // predicates.go:125-127 pod cap
+      const bool rel_zero_wave = __ballot(!(cur.rc == 0.0 && cur.rm == 0.0 && cur.rg == 0.0)) == 0ull;
       uint32_t keep[4] = {0u, 0u, 0u, 0u};
       uint64_t mr;
       if (rel_zero_wave) {
-        scan_rows<INT_MODE, true, kFfRows, 0, kFfGroup<INT_MODE>>(s_req, ic, im, ig, rc, rm, rg, keep);
+        scan_rows<INT_MODE, true, kFfRows, 0, kFfGroup<INT_MODE>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm,
+                                                                  cur.rg, keep);
         mr = (flags_l & kRowRelZeroFits) ? ~0ull : 0ull;
       } else {
-        scan_rows<INT_MODE, false, kFfRows, 0, kFfGroup<INT_MODE>>(s_req, ic, im, ig, rc, rm, rg, keep);
+        scan_rows<INT_MODE, false, kFfRows, 0, kFfGroup<INT_MODE>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm,
+                                                                   cur.rg, keep);
         mr = (uint64_t)keep[2] | ((uint64_t)keep[3] << 32);
       }
       if (lane < kFfRows) {
@@ -294,39 +318,64 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
         s_f[k][lane] = fi | (mr & mw);
         s_i[k][lane] = fi;
       }
+      cur = nxt;
+      lane_mw = nxt_mw;
     }
     __syncthreads();
-    if (!done) {  // wave-uniform: this wave's row, the round's words in node order, 64 at a time
+    // Extraction, phase 1: wave j places row j's words of the round. Lane k
+    // holds word k's node count; the exclusive prefix sum over lanes (one
+    // ballot + mbcnt per bit of the count) is the list position of the
+    // word's first node. Only the words that start below `want` can add a
+    // candidate (positions grow in node order).
+    uint32_t need = 0;
+    if (!done) {
 #pragma unroll 1
-      for (int k0 = 0; k0 < nw && !done; k0 += 64) {
-        uint64_t fk = 0ull, ik = 0ull;
-        if (k0 + lane < nw) {
-          fk = s_f[k0 + lane][wave];
-          ik = s_i[k0 + lane][wave];
+      for (int k0 = 0; k0 < nw; k0 += 64) {
+        const int k = k0 + lane;
+        const uint32_t pc = k < nw ? (uint32_t)__popcll(s_f[k][wave]) : 0u;
+        uint32_t excl = 0, tot = 0;
+#pragma unroll
+        for (int b = 0; b < 7; ++b) {  // pc <= 64
+          const uint64_t bb = __ballot((pc >> b) & 1u);
+          excl += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u)) << b;
+          tot += (uint32_t)__popcll(bb) << b;
         }
-        uint64_t nz = __ballot(fk != 0ull);
-        while (nz) {
-          const int k = __builtin_ctzll(nz);
-          nz &= nz - 1ull;
-          const uint64_t m = readlane64(fk, k);
-          const uint64_t mi = readlane64(ik, k);
-          const uint32_t pos =
-              found + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          if (((m >> lane) & 1ull) && pos < want)
-            a.down[a.G + base + pos] =
-                (uint32_t)((r0 + k0 + k) * 64 + lane) | (((mi >> lane) & 1ull) ? 0u : kCandPipelineBit);
-          found += (uint32_t)__popcll(m);
-          if (found > want) {
-            done = true;
-            break;
-          }
+        const uint32_t pos = found + excl;
+        if (k < nw) s_pos[k][wave] = pos;
+        need = (uint32_t)k0 + (uint32_t)__popcll(__ballot(k < nw && pos < want));
+        found += tot;
+        if (found > want) {
+          done = true;
+          break;
         }
       }
     }
+    if (lane == 0) {
+      s_need[wave] = need;
+      s_done[wave] = done ? 1u : 0u;
+    }
+    __syncthreads();
+    // phase 2: every (row, placed word) pair is one wave-wide append (lane =
+    // node, position = word start + mbcnt), spread over all the waves so a
+    // long list is not walked by one wave alone
+#pragma unroll 1
+    for (int j = 0; j < kFfRows; ++j) {
+      const int nj = (int)s_need[j];
+#pragma unroll 1
+      for (int k = wave; k < nj; k += kFfWaves) {
+        const uint64_t m = s_f[k][j];
+        if (m == 0ull) continue;  // wave-uniform (every lane reads one address)
+        const uint64_t mi = s_i[k][j];
+        const uint32_t pos =
+            s_pos[k][j] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (((m >> lane) & 1ull) && pos < s_want[j])
+          a.down[a.G + s_base[j] + pos] =
+              (uint32_t)((r0 + k) * 64 + lane) | (((mi >> lane) & 1ull) ? 0u : kCandPipelineBit);
+      }
+    }
     if (r0 + kFfMaxRound >= a.w_hi) break;  // the last round: no second barrier
-    if (lane == 0) s_done[wave] = done ? 1u : 0u;
-    __syncthreads();  // the round's masks are read; every row's state is in s_done
-    if (a.early_exit) {  // every row's list is full: the same decision in every wave
+    __syncthreads();  // the round's masks and positions are read
+    if (EARLY_EXIT) {  // every row's list is full: the same decision in every wave
       const uint32_t d = lane < kFfRows ? s_done[lane] : 1u;
       if (__ballot(d == 0u) == 0ull) break;
     }
@@ -341,10 +390,18 @@ hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t 
                            hipEvent_t stop) {
   if (a.G <= 0) return hipSuccess;
   const dim3 grid((a.G + kFfRows - 1) / kFfRows), block(64 * kFfWaves);
-  if (int_mode)
-    hipExtLaunchKernelGGL(kbg_firstfit_kernel<true>, grid, block, 0, stream, start, stop, 0, a);
-  else
-    hipExtLaunchKernelGGL(kbg_firstfit_kernel<false>, grid, block, 0, stream, start, stop, 0, a);
+  // <.., false>: full-scan mode (every node of every row), <.., true>: production
+  if (int_mode) {
+    if (a.early_exit)
+      hipExtLaunchKernelGGL((kbg_firstfit_kernel<true, true>), grid, block, 0, stream, start, stop, 0, a);
+    else
+      hipExtLaunchKernelGGL((kbg_firstfit_kernel<true, false>), grid, block, 0, stream, start, stop, 0, a);
+  } else {
+    if (a.early_exit)
+      hipExtLaunchKernelGGL((kbg_firstfit_kernel<false, true>), grid, block, 0, stream, start, stop, 0, a);
+    else
+      hipExtLaunchKernelGGL((kbg_firstfit_kernel<false, false>), grid, block, 0, stream, start, stop, 0, a);
+  }
   return hipGetLastError();
 }
 

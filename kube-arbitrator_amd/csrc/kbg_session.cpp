@@ -56,6 +56,10 @@
 struct kbg_comm {
   ncclComm_t nccl = nullptr;
   int32_t n_ranks = 1, rank = 0, device = 0;
+  // ncclCommAbort ran (a local failure inside a collective protocol, an
+  // asynchronous RCCL error, or a peer that stopped answering): every later
+  // call on a session of this communicator fails with KBG_E_RCCL
+  std::atomic<bool> aborted{false};
 };
 
 namespace {
@@ -76,6 +80,69 @@ kbg_status fail(kbg_status code, const std::string& msg) {
 using kbg::Engine;
 using kbg::Res;
 using kbg::Session;
+
+// ---------------------------------------------------------- communicator
+// A rank that fails between the collectives of a protocol round (a HIP error,
+// a failed copy) cannot leave its peers blocked in theirs: it aborts the
+// communicator, and a rank waiting on a collective polls RCCL's asynchronous
+// error state and gives up after KBG_COMM_TIMEOUT_MS (default 300 s) without
+// progress, aborting too. Either way the call returns KBG_E_RCCL and the
+// communicator is dead for every session on it (kbgpu.h kbg_comm_init).
+void comm_abort(kbg_comm* c) {
+  if (!c || !c->nccl) return;
+  bool was = false;
+  if (c->aborted.compare_exchange_strong(was, true)) (void)ncclCommAbort(c->nccl);
+}
+
+kbg_status comm_alive(const Session& S) {
+  if (S.comm && S.comm->aborted.load())
+    return fail(KBG_E_RCCL, "the communicator was aborted after a failure on a rank: destroy it and the sessions on it, "
+                            "and re-create them");
+  return KBG_OK;
+}
+
+// Waits for `ev` (recorded after collectives on the session's stream).
+kbg_status comm_wait(Session& S, hipEvent_t ev) {
+  if (!S.comm || !S.comm->nccl) {
+    HIP_TRY(hipEventSynchronize(ev));
+    return KBG_OK;
+  }
+  static const double limit_ms = [] {
+    const char* e = getenv("KBG_COMM_TIMEOUT_MS");
+    return e && atof(e) > 0 ? atof(e) : 300000.0;
+  }();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spin = 0;; ++spin) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return KBG_OK;
+    if (q != hipErrorNotReady) {
+      comm_abort(S.comm);
+      return fail(KBG_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
+    }
+    ncclResult_t ae = ncclSuccess;
+    if ((spin & 63) == 0 && ncclCommGetAsyncError(S.comm->nccl, &ae) == ncclSuccess && ae != ncclSuccess &&
+        ae != ncclInProgress) {
+      comm_abort(S.comm);
+      return fail(KBG_E_RCCL, std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae));
+    }
+    if (S.comm->aborted.load()) return comm_alive(S);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms > limit_ms) {
+      comm_abort(S.comm);
+      return fail(KBG_E_RCCL, "a collective made no progress for KBG_COMM_TIMEOUT_MS: a peer rank failed or stopped");
+    }
+    if (spin > 2000) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+kbg_status comm_sync(Session& S) {
+  if (!S.comm || !S.comm->nccl) {
+    HIP_TRY(hipStreamSynchronize(S.stream));
+    return KBG_OK;
+  }
+  HIP_TRY(hipEventRecord(S.comm_ev, S.stream));
+  return comm_wait(S, S.comm_ev);
+}
 
 inline Res to_res(const kbg_resource& r) { return Res{r.milli_cpu, r.memory, r.milli_gpu}; }
 inline kbg_resource to_kres(const Res& r) { return kbg_resource{r.c, r.m, r.g}; }
@@ -483,6 +550,8 @@ void free_device(Session& S) {
     }
   if (S.stage_ev) (void)hipEventDestroy(S.stage_ev);
   S.stage_ev = nullptr;
+  if (S.comm_ev) (void)hipEventDestroy(S.comm_ev);
+  S.comm_ev = nullptr;
   S.stage_pending = false;
   if (S.stream) (void)hipStreamDestroy(S.stream);
   S.stream = nullptr;
@@ -624,7 +693,7 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
 }
 
 kbg_status device_wait(Session& S, kbg::Stage& sg) {
-  HIP_TRY(hipEventSynchronize(sg.ev[6]));
+  if (kbg_status st = comm_wait(S, sg.ev[6]); st != KBG_OK) return st;
   sg.inflight = false;
   const int32_t G = sg.G;
   sg.h_count = sg.h_down;
@@ -781,10 +850,10 @@ struct Grouper {
     sg.h_capoff = (uint32_t*)(sg.h_up + (size_t)Gp * sizeof(kbg::TaskRec));
     sg.h_capoff[0] = 0;
     // full-scan: rows of one shape in one scan evaluate identical inputs
-    // against the same table, so their lists are one sequence cut at
-    // different lengths. Every row keeps M slots; the shape's last row keeps
-    // a long list (every commit before it can exhaust one node), and a row
-    // whose own M run out continues in it (Resolver) instead of a rescan.
+    // against the same table, so their lists are one sequence. Every row is
+    // evaluated against the whole table on the device; the list is written
+    // once, for the shape's last row (a long list: every commit before it can
+    // exhaust one node), and the shape's other rows read it (Resolver).
     if (S.opts.full_scan) {
       sg.row_ext.resize(G);
       for (int32_t g = 0; g < G; ++g) sg.row_ext[g] = shape_row[sg.row_shape[g]];
@@ -799,7 +868,7 @@ struct Grouper {
     for (int32_t g = 0; g < G; ++g) {
       uint32_t want;
       if (!S.opts.full_scan) want = (uint32_t)std::min(count[g] + kGroupSlack, 4096);
-      else if (sg.row_ext[g] != g) want = (uint32_t)S.M;
+      else if (sg.row_ext[g] != g) want = 0;  // its list is the shape's long one (Resolver: alias rows)
       else want = (uint32_t)(S.M + std::min(2 * count[g] + (g >> 3) + 64, grow_cap));
       sg.h_capoff[g + 1] = sg.h_capoff[g] + want;
     }
@@ -841,6 +910,8 @@ struct Resolver {
     return mark[nd] > base || (S.has_aff && S.mwmark[(size_t)S.task_class[t] * S.W + (nd >> 6)] > base);
   }
   int resolve(int32_t g, int32_t t, int32_t* node, int32_t* kind) {
+    if (S.opts.full_scan && sg->h_capoff[g + 1] == sg->h_capoff[g])
+      g = sg->row_ext[g];  // an alias row: its shape's long list (Grouper::build), this row's cursor
     const uint32_t cnt = sg->h_count[g];
     const int32_t n = (int32_t)(cnt & kbg::kCountMask);
     const uint32_t* c = sg->h_cand + sg->h_capoff[g];
@@ -2141,6 +2212,7 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   HIP_TRY(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   for (auto& e : S.ev) HIP_TRY(hipEventCreate(&e));
   HIP_TRY(hipEventCreateWithFlags(&S.stage_ev, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&S.comm_ev, hipEventDisableTiming));
   S.stage_pending = false;
   if ((st = alloc_soa(S, &S.d_nodes)) || (st = alloc_soa(S, &S.d_nodes0))) return st;
   const size_t up_cap = (size_t)kbg::kbg_pad_rows(S.K) * sizeof(kbg::TaskRec) + ((size_t)S.K + 1) * 4;
@@ -3430,15 +3502,12 @@ struct ShardIO {
   virtual kbg_status scan_avail(Session& S, kbg::Stage& sg, int32_t G, int32_t base, uint32_t* avail) {
     kbg_status st = scan(S, sg, G, base);
     if (st != KBG_OK) return st;
-    for (int32_t g = 0; g < G; ++g) avail[g] = (sg.h_count[g] & kbg::kCountMask) ? (1u << S.shard) : 0u;
+    for (int32_t g = 0; g < G; ++g) avail[g] = sg.h_count[g] != 0 ? (1u << S.shard) : 0u;  // any node (listed or not)
     return allreduce(avail, G, true);
   }
   // this rank's committed rows (and class-mask words) to the table its scans read
   virtual kbg_status push(Session& S, const std::vector<int32_t>& touched) { return push_deltas(S, touched); }
-  virtual kbg_status sync(Session& S) {
-    HIP_TRY(hipStreamSynchronize(S.stream));
-    return KBG_OK;
-  }
+  virtual kbg_status sync(Session& S) { return comm_sync(S); }
   double ms = 0;                                                            // time in collectives
 };
 
@@ -3477,7 +3546,7 @@ struct RcclIO final : ShardIO {
     const ncclResult_t nr = ncclBroadcast(d, d, n, ncclUint32, 0, S.comm->nccl, S.stream);
     if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclBroadcast: ") + ncclGetErrorString(nr));
     HIP_TRY(hipMemcpyAsync(h, d, n * 4, hipMemcpyDeviceToHost, S.stream));
-    HIP_TRY(hipStreamSynchronize(S.stream));
+    if (kbg_status st2 = comm_sync(S); st2 != KBG_OK) return st2;
     std::memcpy(buf, h, n * 4);
     ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return KBG_OK;
@@ -3502,7 +3571,7 @@ struct RcclIO final : ShardIO {
     const ncclResult_t nr = ncclAllReduce(d, d, n, ncclUint32, sum ? ncclSum : ncclMin, S.comm->nccl, S.stream);
     if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
     HIP_TRY(hipMemcpyAsync(h, d, n * 4, hipMemcpyDeviceToHost, S.stream));
-    HIP_TRY(hipStreamSynchronize(S.stream));
+    if (kbg_status st2 = comm_sync(S); st2 != KBG_OK) return st2;
     std::memcpy(buf, h, n * 4);
     ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return KBG_OK;
@@ -3608,6 +3677,10 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
     if (lg_ref && *lg_ref) (*lg_ref)->join();
   };
   auto abort = [&](kbg_status st) {
+    // a failure of this rank alone (the batch messages and the reduced
+    // results are the same on every rank): the peers are, or will be,
+    // blocked in a collective this rank never joins
+    if (st == KBG_E_HIP || st == KBG_E_RCCL || st == KBG_E_NOMEM) comm_abort(S.comm);
     finish();
     S.owner = false;
     return st;
@@ -3811,6 +3884,10 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
       rp->push(std::move(v));
     }
     tp = clk::now();
+    // test hook (tests/test_shard_gpu.py): a failure of this rank alone
+    // between two protocol rounds
+    if (const char* f = getenv("KBG_TEST_FAULT"); f && !strcmp(f, "push"))
+      return abort(fail(KBG_E_HIP, "injected fault before the delta push (KBG_TEST_FAULT=push)"));
     if ((st = io.push(S, touched)) != KBG_OK) return abort(st);
     stamp = S.res_stamp;
     S.stats.delta_ms += ms_since(tp);
@@ -4441,7 +4518,7 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
     }
     HIP_TRY(hipMemcpyAsync(S.h_vbits, done_bits, 2 * (size_t)S.W32 * sizeof(uint32_t), hipMemcpyDeviceToHost,
                            S.stream));
-    HIP_TRY(hipStreamSynchronize(S.stream));
+    if (kbg_status st2 = comm_sync(S); st2 != KBG_OK) return st2;
     S.vstage_busy = false;
     if (timed) {
       float ms = 0;
@@ -5168,7 +5245,7 @@ kbg_status usable(kbg_session* s) {
   if (!s) return fail(KBG_E_INVALID, "null session");
   if (!s->s.broken.empty())
     return fail(KBG_E_INVALID, "the session is unusable after a failed kbg_session_update (" + s->s.broken + "): re-open it");
-  return KBG_OK;
+  return comm_alive(s->s);
 }
 }  // namespace
 
@@ -5211,6 +5288,8 @@ kbg_status kbg_session_open(const kbg_snapshot* snap, const kbg_options* opts, k
 kbg_status kbg_session_open_sharded(const kbg_snapshot* snap, const kbg_options* opts, kbg_comm* comm,
                                     kbg_session** out) {
   if (!comm) return fail(KBG_E_INVALID, "null communicator");
+  if (comm->aborted.load())
+    return fail(KBG_E_RCCL, "the communicator was aborted after a failure on a rank: destroy it and re-create it");
   return session_open(snap, opts, comm, out);
 }
 
@@ -5249,7 +5328,7 @@ kbg_status kbg_comm_init(const uint8_t id[KBG_COMM_ID_BYTES], int32_t n_ranks, i
 void kbg_comm_destroy(kbg_comm* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  if (c->nccl) (void)ncclCommDestroy(c->nccl);
+  if (c->nccl && !c->aborted.load()) (void)ncclCommDestroy(c->nccl);  // (an aborted one is freed)
   delete c;
 }
 

@@ -430,6 +430,7 @@ struct Session {
   NodeDelta* h_deltas = nullptr; // pinned, mapped: the apply kernels read it in place
   bool uva = false;              // mapped host memory has the same address on the device
   hipEvent_t stage_ev = nullptr; // after the last enqueued reader of the pinned staging (stage_acquire)
+  hipEvent_t comm_ev = nullptr;  // comm_sync: the stream's end, polled against RCCL errors and the timeout
   bool stage_pending = false;
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   std::vector<void*> d_allocs;

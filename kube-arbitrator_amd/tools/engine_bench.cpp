@@ -384,7 +384,9 @@ extern "C" int32_t kbg_tool_sharded_allocate_device(const kbg_snapshot* snap, co
   std::vector<std::unique_ptr<Session>> sess(R);
   std::vector<std::thread> th;
   for (int32_t r = 0; r < R; ++r) {
-    comms[r] = kbg_comm{nullptr, R, r, device};
+    comms[r].n_ranks = R;
+    comms[r].rank = r;
+    comms[r].device = device;
     sess[r].reset(new Session());
   }
   for (int32_t r = 0; r < R; ++r)
@@ -417,4 +419,35 @@ extern "C" int32_t kbg_tool_sharded_allocate_device(const kbg_snapshot* snap, co
       return -(int32_t)res[r];
     }
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// The fused first-fit kernel alone on a device session: the first G pending
+// tasks (session order) as one batch of rows (Grouper: full-scan or grouped
+// per the options), launched `reps` times against the session's table;
+// returns the median kernel time (HIP events) in microseconds, or < 0.
+extern "C" double kbg_tool_firstfit_bench(const kbg_snapshot* snap, const kbg_options* o, int32_t G, int32_t reps) {
+  Session S;
+  if (open_session(S, snap, o, nullptr) != KBG_OK) return -1.0;
+  std::vector<int32_t> bt;
+  for (int32_t t : S.pend_all) {
+    if ((int32_t)bt.size() == std::min(G, S.K)) break;
+    bt.push_back(t);
+  }
+  Grouper grouper(S);
+  kbg::Stage& sg = S.stages[0];
+  const int32_t rows = grouper.build(sg, bt.data(), (int32_t)bt.size());
+  std::vector<double> us;
+  for (int32_t r = 0; r < reps; ++r) {
+    if (device_scan(S, sg, rows, S.res_stamp) != KBG_OK) {
+      free_device(S);
+      return -2.0;
+    }
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, sg.ev[0], sg.ev[1]);
+    us.push_back(ms * 1e3);
+  }
+  free_device(S);
+  std::sort(us.begin(), us.end());
+  return us[us.size() / 2];
 }

@@ -3,9 +3,9 @@ figures) from the per-config summaries of profiles/summarize_pmc.py:
 
   python profiles/make_pmc_scan.py profiles/r02   # reads pmc_c3.json, pmc_c4.json, pmc_c5.json
 
-C3 (5k nodes) gives the scan kernel in full-scan mode (kbg_scan_kernel<.., 64>,
-batches > 1024 rows) and grouped mode (<.., 16>); C5 the victim kernel; other
-node counts (C4) go under by_nodes."""
+C3 (5k nodes) gives the fused first-fit kernel in full-scan mode
+(kbg_firstfit_kernel<true, false>) and production mode (<true, true>); C5 the
+victim kernel; other node counts (C4) go under by_nodes."""
 import json
 import os
 import sys
@@ -21,10 +21,13 @@ def section(k):
     return out
 
 
+FULL, PROD = "kbg_firstfit_kernel<true, false>", "kbg_firstfit_kernel<true, true>"
+
+
 def scan_modes(s):
     ks = s["kernels"]
-    return {"full_scan": section(ks["kbg_scan_kernel<true, 64>"]) if "kbg_scan_kernel<true, 64>" in ks else None,
-            "grouped": section(ks["kbg_scan_kernel<true, 16>"]) if "kbg_scan_kernel<true, 16>" in ks else None}
+    return {"full_scan": section(ks[FULL]) if FULL in ks else None,
+            "grouped": section(ks[PROD]) if PROD in ks else None}
 
 
 def main():
@@ -33,7 +36,7 @@ def main():
     load = lambda c: json.load(open(os.path.join(d, f"pmc_c{c}.json"))) if os.path.exists(
         os.path.join(d, f"pmc_c{c}.json")) else None
     c3, c4, c5 = load(3), load(4), load(5)
-    out = {"kernel": "kbg_scan_kernel", "n_nodes": 5000}
+    out = {"kernel": "kbg_firstfit_kernel", "n_nodes": 5000}
     out.update(scan_modes(c3))
     if c5 and "kbg_victim_kernel" in c5["kernels"]:
         out["victim"] = dict(section(c5["kernels"]["kbg_victim_kernel"]), kernel="kbg_victim_kernel", n_nodes=10000)

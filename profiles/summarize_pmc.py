@@ -6,8 +6,9 @@ Usage: python profiles/summarize_pmc.py <session dir> <config> > summary.json
   <session dir>/c<config>_pmc<i>/pmc<i>_counter_collection.csv  counters
 
 Kernels are keyed by their name up to the argument list, template arguments
-kept: kbg_scan_kernel<true, 64> runs the full-scan mode's batches (> 1024
-rows), kbg_scan_kernel<true, 16> the production mode's grouped batches.
+kept: kbg_firstfit_kernel<true, false> runs the full-scan mode's batches
+(every node of every row), kbg_firstfit_kernel<true, true> the production
+mode's grouped batches (a workgroup stops once its rows' lists are full).
 Derived figures (MI355X_MICROARCH.md):
   hbm_read_bytes  = 2 x FETCH_SIZE KiB x 1024 (gfx950 tallies 128-B requests
                     at 64 B; Infinity-Cache hits are counted too)
@@ -29,8 +30,8 @@ import sys
 SIMDS = 1024
 CLOCK_GHZ = 2.4
 VALU_CYC = 4
-WANT = ("kbg_scan_kernel", "kbg_select_kernel", "kbg_victim_kernel", "kbg_victim_big_kernel",
-        "kbg_victim_prep_kernel", "kbg_apply_kernel")
+WANT = ("kbg_firstfit_kernel", "kbg_fitdelta_kernel", "kbg_scan_kernel", "kbg_select_kernel", "kbg_victim_kernel",
+        "kbg_victim_big_kernel", "kbg_victim_prep_kernel", "kbg_apply_kernel", "copyBuffer")
 
 
 def key(name):

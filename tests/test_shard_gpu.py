@@ -163,3 +163,25 @@ def test_rccl_owner_resolve_contended(seed, comm1, owner_resolve):
     compare_outputs(run_oracle(fx), got)
     if ssn:
         ssn.close()
+
+
+def test_rccl_local_failure_aborts_comm(monkeypatch):
+    """A rank failing between two owner-resolve rounds aborts the communicator
+    (its peers would otherwise block in the next collective forever): the
+    failing call reports the local error, every later call on the
+    communicator KBG_E_RCCL, and destroying it still works."""
+    from kbgpu import _abi
+    from kbgpu.dist import ShardComm
+    monkeypatch.setenv("KBG_OWNER_RESOLVE", "1")
+    fx = synth.config_fixture(1)
+    c = ShardComm(device=0, rank=0, world=1)
+    try:
+        monkeypatch.setenv("KBG_TEST_FAULT", "push")
+        with pytest.raises(_abi.KbgError) as e:
+            run_fixture(fx, {"comm": c})
+        assert e.value.status == "hip" and "injected" in str(e.value)
+        monkeypatch.delenv("KBG_TEST_FAULT")
+        got, ssn = run_fixture(fx, {"comm": c})
+        assert got["status"] == "rccl" and ssn is None and "aborted" in got["error"]
+    finally:
+        c.close()
