@@ -14,7 +14,8 @@ parts of Kubernetes the e2e cluster supplies are modelled:
 - the binder / kubelet: a bound pod runs from the next cycle on
   (`cache.Bind`, `cache.go:408-444`); a pipelined task binds nothing;
 - the evictor: an evicted pod terminates (Running with a deletionTimestamp,
-  i.e. Releasing, for one cycle, then gone), and its batch Job creates a
+  i.e. Releasing, for its 3 s grace period = 3 one-second cycles,
+  `cache.go:110-123`, then gone), and its batch Job creates a
   Pending replacement at once (the Job controller does not count terminating
   pods as active);
 - ReplicaSet pods (`util.go:490-535`, default scheduler, no PodGroup) are
@@ -51,8 +52,11 @@ def milli_cpu(req):
 
 
 class Cluster:
-    def __init__(self, worker_cpu=(4000, 4000, 4000), system_cpu=(250, 0, 0), runner=None, grace=1, ns_queues=False):
-        self.grace = grace  # cycles a terminating pod stays Releasing
+    def __init__(self, worker_cpu=(4000, 4000, 4000), system_cpu=(250, 0, 0), runner=None, grace=3, ns_queues=False):
+        # cycles a terminating pod stays Releasing: the evictor deletes with a
+        # 3 s grace period (cache.go:110-123) and a cycle runs every second
+        # (--schedule-period 1s, cmd/kube-batch/app/options/options.go:64)
+        self.grace = grace
         self.runner = runner  # fixture -> output in the oracle's schema (one Scheduler.runOnce)
         self.nodes = [{"name": "master", "allocatable": {"cpu": "4", "memory": "16Gi", "pods": "110"},
                        "labels": {"kubernetes.io/hostname": "master"}, "taints": [dict(MASTER_TAINT)]}]
@@ -235,8 +239,12 @@ class Cluster:
     def group_pods(self, pg):
         return [p for p in self.pods if (p.get("annotations") or {}).get(GROUP) == pg]
 
-    def running(self, pg, pri=None):  # taskPhase / taskPhaseEx with Running|Succeeded (util.go:342-398)
-        return sum(1 for p in self.group_pods(pg) if p["phase"] == "Running" and p["uid"] not in self.terminating
+    def running(self, pg, pri=None):
+        """taskPhase / taskPhaseEx with Running|Succeeded (util.go:342-398,
+        449-457): a count of `pod.Status.Phase` alone, so a pod in its
+        eviction grace period (deletionTimestamp set, containers still up:
+        phase Running) counts, as it does against the live cluster."""
+        return sum(1 for p in self.group_pods(pg) if p["phase"] == "Running"
                    and (pri is None or p.get("priority") == PRIORITY[pri]))
 
     def pending(self, pg):
