@@ -10,11 +10,14 @@ the timed region starts.
 value       = placements/sec (Allocate + Pipeline decisions / wall time), whole job,
               production mode (identical (class, request) shapes share a scan row)
 ms_per_step = mean allocate-cycle wall time; p50_cycle_ms = median
-roofline    = SURVEY §8(d) at the cycle level, in full-scan mode (every task
-              evaluation scans the whole node table on the device): task
-              evaluations x (N x 64 B + 32 B) per cycle / p50 cycle wall time,
-              against 8 TB/s HBM3E; traffic = PMC HBM bytes of the cycle's
-              scan launches (profiles/pmc_scan.json)
+roofline    = the dominant kernel (kbg_firstfit_kernel, full-scan mode: every
+              task evaluation scans the whole node table on the device):
+              SURVEY §8(d) bytes per task evaluation (N x 64 B + 32 B) x rows
+              per launch / average launch time (HIP events on the library's
+              stream), against 8 TB/s HBM3E; traffic = PMC HBM bytes per launch
+              (profiles/pmc_scan.json); binding = its VALU-issue ceiling
+cycle_roofline_8d = BASELINE's north-star form: the same bytes per allocate
+              cycle / p50 cycle wall time
 scan_kernel = the dominant kernel against its physical ceilings: PMC HBM bytes
               and PMC VALU wave instructions per launch over its HIP-event time
 cpu_baseline= the kbref oracle on this host, CPU model stated: B-ref (1 thread),
@@ -220,13 +223,22 @@ def load_pmc(n_nodes, mode):
     return None
 
 
-def valu_ceiling(pmc, avg_us):
+def valu_ceiling(pmc, avg_us, rows=None):
     """The VALU-issue ceiling of a kernel: its PMC wave instructions at 4
-    cycles each spread over every SIMD of the chip at the peak clock."""
-    floor_us = pmc["valu_insts_per_launch"] * VALU_CYC / (SIMDS * CLOCK_GHZ * 1e3)
-    return {"wave_insts_per_launch": pmc["valu_insts_per_launch"], "issue_floor_us": floor_us,
-            "frac": floor_us / avg_us if avg_us > 0 else None,
-            "model": f"{VALU_CYC} cycles per wave64 VALU instruction per SIMD, {SIMDS} SIMDs at {CLOCK_GHZ} GHz"}
+    cycles each spread over every SIMD of the chip at the peak clock. With
+    `rows`, the profiled count is scaled from the profiled command's rows per
+    launch to this run's (the instructions grow with the rows)."""
+    insts = pmc["valu_insts_per_launch"]
+    scaled = bool(rows and pmc.get("rows_per_launch"))
+    if scaled:
+        insts = insts / pmc["rows_per_launch"] * rows
+    floor_us = insts * VALU_CYC / (SIMDS * CLOCK_GHZ * 1e3)
+    out = {"wave_insts_per_launch": insts, "issue_floor_us": floor_us,
+           "frac": floor_us / avg_us if avg_us > 0 else None,
+           "model": f"{VALU_CYC} cycles per wave64 VALU instruction per SIMD, {SIMDS} SIMDs at {CLOCK_GHZ} GHz"}
+    if scaled:
+        out["scaled_from_rows_per_launch"] = pmc["rows_per_launch"]
+    return out
 
 
 def main():
@@ -370,6 +382,38 @@ def main():
                                   "wall time of kbg_allocate", "equivalent_8d": eq})
         return out
 
+    def kernel_roofline(agg, mode):
+        """The contract's roofline of the dominant kernel, kbg_firstfit_kernel
+        in full-scan mode (every row is one task evaluation scanning all N
+        nodes, SURVEY 8(d) cursor rule): achieved = 8(d) bytes per unit (N x
+        64 B + 32 B) x the rows one launch evaluates / the launch's average
+        duration (HIP events around every launch on the library's stream,
+        over the timed steps); traffic = PMC HBM bytes per launch of the same
+        command (profiles/pmc_scan.json). The 8(d) count charges a node
+        record per (row, node) pair; the kernel holds a wave's 64 node records
+        in registers for all the rows of its workgroup, so the count can pass
+        the HBM peak — `binding` is then the ceiling that holds: VALU issue
+        (the kernel's PMC wave instructions at full issue on every SIMD)."""
+        launches = max(1, agg["launches"])
+        rows = agg["evals"] / launches
+        avg_s = agg["scan_ms"] * 1e-3 / launches
+        per_launch = rows * (agg["n_nodes"] * NODE_RECORD_B + TASK_RECORD_B)
+        ach = per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
+        out = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+               "traffic": None, "kernel": "kbg_firstfit_kernel (full-scan mode)", "avg_launch_us": avg_s * 1e6,
+               "rows_per_launch": rows, "algo_bytes_per_launch": per_launch,
+               "definition": "SURVEY 8(d) bytes per task evaluation x rows per launch / average launch time "
+                             "(HIP events on the library stream over the timed steps)"}
+        pmc = load_pmc(agg["n_nodes"], mode) if comm is None else None
+        if pmc:
+            if pmc.get("hbm_bytes_per_launch") is not None:
+                out["traffic"] = pmc["hbm_bytes_per_launch"]
+                out["traffic_frac_of_peak"] = pmc["hbm_bytes_per_launch"] / avg_s / 1e9 / HBM_PEAK_GBS
+            if pmc.get("valu_insts_per_launch") is not None:
+                out["binding"] = dict(valu_ceiling(pmc, avg_s * 1e6, rows), bound="valu issue")
+            out["pmc_source"] = pmc.get("source")
+        return out
+
     def scan_kernel(agg, mode):
         """The dominant device kernel against its physical ceilings: HBM
         (PMC-measured bytes per launch) and VALU issue (PMC-measured wave
@@ -391,7 +435,7 @@ def main():
                 out["hbm"] = {"bytes_per_launch": b, "achieved_gbs": b / (avg_us * 1e-6) / 1e9,
                               "peak_gbs": HBM_PEAK_GBS, "frac": b / (avg_us * 1e-6) / 1e9 / HBM_PEAK_GBS}
             if pmc.get("valu_insts_per_launch") is not None:
-                out["valu"] = valu_ceiling(pmc, avg_us)
+                out["valu"] = valu_ceiling(pmc, avg_us, agg["evals"] / launches)
             out["pmc_source"] = pmc.get("source")
         return out
 
@@ -443,9 +487,10 @@ def main():
                                    f"of availability and packed winners)") if world > 1 else "single-gpu",
                    "batch_tasks": base_opts.get("batch_tasks", 8192),
                    "candidates": base_opts.get("candidates", 32)},
-        "roofline": cycle_roofline(full, "full_scan"),
+        "roofline": kernel_roofline(full, "full_scan"),
         "roofline_note": "full-scan mode (every task evaluation scans all N nodes on the device, SURVEY 8(d) cursor "
                          "rule); `value` is the production mode, which groups identical (class, request) shapes",
+        "cycle_roofline_8d": cycle_roofline(full, "full_scan"),
         "scan_kernel": scan_kernel(full, "full_scan"),
         "full_scan_mode": {"placements_per_s": full["decisions"] / full["elapsed"],
                            "p50_cycle_ms": statistics.median(full["cycle_ms"]), "breakdown": breakdown(full)},

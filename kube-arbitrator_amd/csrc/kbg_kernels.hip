@@ -257,32 +257,37 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
     int32_t nt = 0, mt = 0;
     bool valid = false;
   };
+  // Every load is unconditional, from a clamped (always legal) address, so
+  // the compiler can wait for exactly the current word's loads and leave the
+  // next word's in flight (a load under a branch makes it wait for all of
+  // them, vmcnt(0), and the prefetch would buy nothing). Lanes past the table
+  // read row 0 and are masked out by `valid` (okm).
   auto load_word = [&](int c, Word& w) {
     const int node = c * 64 + lane;
     const int row = node - a.tab_lo;
-    w.valid = node < a.n_nodes && row < a.tab_n;
-    if (w.valid) {
-      const double* p = a.nodes + row;
-      w.ic = p[0];
-      w.im = p[a.stride];
-      w.ig = p[2 * a.stride];
-      w.rc = p[3 * a.stride];
-      w.rm = p[4 * a.stride];
-      w.rg = p[5 * a.stride];
-      const int32_t* q = reinterpret_cast<const int32_t*>(a.nodes + 6 * (size_t)a.stride) + row;
-      w.nt = q[0];
-      w.mt = q[a.stride];
-    }
+    w.valid = node < a.n_nodes && row >= 0 && row < a.tab_n;
+    const int rr = w.valid ? row : 0;
+    const double* p = a.nodes + rr;
+    w.ic = p[0];
+    w.im = p[a.stride];
+    w.ig = p[2 * a.stride];
+    w.rc = p[3 * a.stride];
+    w.rm = p[4 * a.stride];
+    w.rg = p[5 * a.stride];
+    const int32_t* q = reinterpret_cast<const int32_t*>(a.nodes + 6 * (size_t)a.stride) + rr;
+    w.nt = q[0];
+    w.mt = q[a.stride];
   };
+  const int w_last = a.w_hi - 1;
   Word cur;
-  if (wave < min(kFfMaxRound, a.w_hi - a.w_lo)) load_word(a.w_lo + wave, cur);
+  load_word(min(a.w_lo + wave, w_last), cur);
   __syncthreads();
   const int cls_l = s_cls[lane & (kFfRows - 1)];
   const int flags_l = s_flags[lane & (kFfRows - 1)];
   // rounds are kFfMaxRound (a multiple of kFfWaves) words apart, so a wave's
-  // words are c, c + kFfWaves, ... across rounds too
-  uint64_t lane_mw = (lane < kFfRows && a.w_lo + wave < a.w_hi) ? a.class_mask[(size_t)cls_l * a.W + a.w_lo + wave]
-                                                                   : 0ull;
+  // words are c, c + kFfWaves, ... across rounds too; lanes >= kFfRows load a
+  // row's mask word they never use
+  uint64_t lane_mw = a.class_mask[(size_t)cls_l * a.W + min(a.w_lo + wave, w_last)];
 #pragma unroll 1
   for (int r0 = a.w_lo; r0 < a.w_hi; r0 += kFfMaxRound) {
     const int nw = min(kFfMaxRound, a.w_hi - r0);  // words of this round
@@ -291,16 +296,14 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
       // the row requests are re-read from LDS per word (kept in registers
       // across the loop they would take 96 VGPRs)
       asm volatile("" ::: "memory");
-      const int c = r0 + k;                          // global 64-node word
-      const int cn = c + kFfWaves < a.w_hi ? c + kFfWaves : -1;  // this wave's next word
+      const int c = r0 + k;                           // global 64-node word
+      const int cn = min(c + kFfWaves, w_last);       // this wave's next word (the last one again at the end)
       Word nxt;
-      uint64_t nxt_mw = 0ull;
-      if (cn >= 0) {
-        load_word(cn, nxt);
-        if (lane < kFfRows) nxt_mw = a.class_mask[(size_t)cls_l * a.W + cn];
-      }
+      load_word(cn, nxt);
+      const uint64_t nxt_mw = a.class_mask[(size_t)cls_l * a.W + cn];
       const uint64_t okm = __ballot(cur.valid && (!a.cap_check || cur.nt < cur.mt));  // predicates.go:125-127 pod cap
-      const bool rel_zero_wave = __ballot(!(cur.rc == 0.0 && cur.rm == 0.0 && cur.rg == 0.0)) == 0ull;
+      const bool rel_zero_wave =
+          __ballot(cur.valid && !(cur.rc == 0.0 && cur.rm == 0.0 && cur.rg == 0.0)) == 0ull;
       uint32_t keep[4] = {0u, 0u, 0u, 0u};
       uint64_t mr;
       if (rel_zero_wave) {

@@ -17,7 +17,7 @@ def one(cid):
     from kbgpu.cache import FakeBinder, cache_from_fixture
     from kbgpu.fixture import _OrderedCache, fixture_tiers
     from kbgpu.snapshot import FlatSnapshot
-    L = ctypes.CDLL(os.path.join(HERE, "libkbg_tools.so"))
+    L = ctypes.CDLL(os.environ.get("TOOLS_LIB", os.path.join(HERE, "libkbg_tools.so")))
     L.kbg_tool_firstfit_bench.restype = ctypes.c_double
     fx = synth.config_fixture(cid)
     s = _OrderedCache(cache_from_fixture(fx, FakeBinder()), fx).snapshot()

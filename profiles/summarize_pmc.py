@@ -67,6 +67,17 @@ def main():
             c[int(r["Dispatch_Id"])] = c.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
             dur = counters[k].setdefault("_dur", {}).setdefault(r["Counter_Name"], {})
             dur[int(r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    # rows per launch of the profiled bench commands (the PMC figures scale with them)
+    benches = []
+    for p in sorted(glob.glob(os.path.join(d, f"c{cfg}_pmc*_bench.json"))):
+        try:
+            benches.append(json.load(open(p)))
+        except (OSError, ValueError):
+            pass
+    full_rows = [b["scan_kernel"]["rows_per_launch"] for b in benches if "scan_kernel" in b]
+    prod_rows = [b["production_mode"]["scan_kernel"]["rows_per_launch"] for b in benches if "production_mode" in b]
+    out["bench_rows_per_launch"] = {"full_scan": statistics.mean(full_rows) if full_rows else None,
+                                    "grouped": statistics.mean(prod_rows) if prod_rows else None}
     for k, v in ks.items():
         ds = v.pop("durations_ns")
         v.update(launches=len(ds), avg_ns=statistics.mean(ds), median_ns=statistics.median(ds), min_ns=min(ds),
