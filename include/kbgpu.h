@@ -324,7 +324,8 @@ typedef struct kbg_stats {
   double update_ms;          /* wall time of the last kbg_session_update */
   int64_t update_rebuilds;   /* kbg_session_update calls that rebuilt the static masks / device tables */
   int64_t owner_rounds;      /* owner-resolve (sharded allocate): exchange rounds over all batches */
-  int64_t reserved_stats[1];
+  int64_t reused_batches;    /* batches resolved against an earlier scan's candidate lists after a cut
+                                (grouped mode: no device round trip) */
 } kbg_stats;
 
 typedef struct kbg_session kbg_session;

@@ -3225,6 +3225,52 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   // candidate walk, host mirror, decision log, whole loop
   const bool rprof = getenv("KBG_PROFILE_RESOLVE") != nullptr;
   uint64_t rcyc[4] = {0, 0, 0, 0};
+  // Grouped mode, after a cut: the stage's candidate lists still hold for the
+  // committed table (a list is every fitting node in order at scan time, up
+  // to its length; feasibility only shrinks during allocate, and a node
+  // touched since the scan is re-checked on the host mirror), so the
+  // re-predicted tasks resolve against them with no device round trip — by
+  // shape, the same (class, request) row any task of the shape used. A task
+  // whose shape has no row there, or a list that runs out before the table
+  // did, rescans the rest of its batch. Full-scan mode rescans (every task
+  // evaluation scans the table); pod affinity (gains cut) and
+  // sharded sessions too.
+  static const bool no_reuse = getenv("KBG_NO_CUT_REUSE") != nullptr;
+  const bool reuse_ok = !S.opts.full_scan && !S.comm && !S.has_aff && !no_reuse;
+  bool reuse = false;
+  std::vector<int32_t> shape_row_of(reuse_ok ? std::max(1, S.n_shapes) : 0, -1), shapes_set, row_rep;
+  // the stage's row of each shape, and a task of each row (the batch entries
+  // [seg0, ...) of `b` built the stage's rows)
+  auto map_shapes = [&](const kbg::Stage& g, const std::vector<int32_t>& b, int32_t seg0) {
+    for (int32_t sh : shapes_set) shape_row_of[sh] = -1;
+    shapes_set.clear();
+    row_rep.assign(g.G, -1);
+    for (size_t i = seg0; i < b.size(); ++i) {
+      const int32_t r = g.row_of[i - seg0];
+      if (row_rep[r] < 0) row_rep[r] = b[i];
+    }
+    for (int32_t r = 0; r < g.G; ++r) {
+      const int32_t sh = g.row_shape[r];
+      if (shape_row_of[sh] < 0) {
+        shape_row_of[sh] = r;
+        shapes_set.push_back(sh);
+      }
+    }
+  };
+  // A shape whose list holds no fitting node any more (complete, and every
+  // entry from its cursor infeasible on the host mirror) fits nowhere for the
+  // rest of the cycle: the predictor learns it before it predicts again, so
+  // the shape's next task does not cut a batch. The walk only moves cursors
+  // past infeasible entries, as a resolve of a task of the shape would.
+  auto probe_failed = [&](const kbg::Stage& g) {
+    for (int32_t r = 0; r < g.G; ++r) {
+      const int32_t sh = g.row_shape[r];
+      if (row_rep[r] < 0 || failed[sh].load(std::memory_order_relaxed)) continue;
+      int32_t node = -1, kind = 0;
+      if (rs.resolve(r, row_rep[r], &node, &kind) == RES_OK && node < 0)
+        failed[sh].store(1, std::memory_order_relaxed);
+    }
+  };
   int si = 0;
   ctr.add("take");
   Batch* cur = next_batch(true);
@@ -3245,27 +3291,34 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     kbg::Stage& other = S.stages[si ^ 1];
     S.stats.batches++;
     auto tp = clk::now();
-    ctr.add("wait");
-    kbg_status st = device_wait(S, *sg);
-    ctr.add("waited");
-    if (st != KBG_OK) return abort(st);
-    learn_failed(*sg);
-    // the next batch's scan overlaps this batch's resolve when it is ready
-    Batch* nxt = next_batch(false);
-    if (pred_failed) return abort(fail(KBG_E_INVALID, pr.error));
-    if (nxt && !nxt->bt.empty()) {
-      if ((st = launch(other, nxt)) != KBG_OK) return abort(st);
-      S.stats.overlapped++;
+    kbg_status st = KBG_OK;
+    Batch* nxt = nullptr;
+    if (!reuse) {
+      ctr.add("wait");
+      st = device_wait(S, *sg);
+      ctr.add("waited");
+      if (st != KBG_OK) return abort(st);
+      learn_failed(*sg);
+      // the next batch's scan overlaps this batch's resolve when it is ready
+      nxt = next_batch(false);
+      if (pred_failed) return abort(fail(KBG_E_INVALID, pr.error));
+      if (nxt && !nxt->bt.empty()) {
+        if ((st = launch(other, nxt)) != KBG_OK) return abort(st);
+        S.stats.overlapped++;
+      }
+    } else {
+      ctr.add("reuse", (int64_t)bt.size());
     }
     S.stats.device_ms += ms_since(tp);
     // commit in order
     tp = clk::now();
-    rs.reset(*sg);
+    if (!reuse) rs.reset(*sg);  // reuse: the stage's cursors carry on
     const int32_t stamp = ++S.res_stamp;  // this resolution's commits
     S.mstamp = stamp;
     touched.clear();
     bactual.assign(bt.size(), 0);
     int32_t cut = -1;
+    bool aff_cut = false;  // a pod-affinity gain: the lists miss the gained nodes
     int32_t seg = 0;  // first batch entry covered by the current scan of this stage
     bool panic = false;
     int32_t rstamp = stamp;
@@ -3276,7 +3329,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     for (int32_t i = 0; i < nb; ++i) {
       const int32_t t = bt[i];
       if ((i & 511) == 511) to_truth(bt, i);  // keep the truth engine a few hundred tasks behind
-      if ((i & 1023) == 1023 && !nxt && !pred_failed) {
+      if ((i & 1023) == 1023 && !nxt && !pred_failed && !reuse) {
         // the predictor's next batch, if it is ready now, scans while this one resolves
         nxt = next_batch(false);
         if (nxt && !nxt->bt.empty()) {
@@ -3292,9 +3345,17 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       }
       int32_t node = -1, kind = 0;
       const uint64_t c0 = rprof ? cycles() : 0;
-      int r = rs.resolve(sg->row_of[i - seg], t, &node, &kind);
+      int r;
+      if (reuse) {
+        const int32_t row = shape_row_of[S.task_shape[t]];
+        r = row >= 0 ? rs.resolve(row, t, &node, &kind) : RES_TRUNC;  // no row for the shape: rescan
+      } else {
+        r = rs.resolve(sg->row_of[i - seg], t, &node, &kind);
+      }
       if (rprof) rcyc[0] += cycles() - c0;
       if (r == RES_TRUNC) {
+        if (reuse) ctr.add("reuse.rescan", i);
+        reuse = false;  // the rescan's rows, by batch entry
         // A candidate list ran out before the table did. The predictions
         // still hold (no outcome differed), so instead of cutting the batch
         // and replaying the engine, write the commits so far back to HBM and
@@ -3368,6 +3429,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         }
         S.aff_gain_classes.clear();
         cut = i + 1;
+        aff_cut = true;
         S.stats.mispredictions++;
         break;
       }
@@ -3395,6 +3457,14 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
     if (cut >= 0) {  // restart the predictor from the engine state at the cut
       if ((st = device_drop(S, other)) != KBG_OK) return abort(st);  // nxt was predicted before the cut
+      const bool will_reuse = reuse_ok && !aff_cut;
+      if (will_reuse) {  // before the predictor restarts: it reads the failed shapes
+        // a batch that resolved against an earlier batch's stage keeps that
+        // stage's map (its own entries built no rows); otherwise the stage's
+        // rows are this batch's entries from `seg` on
+        if (!reuse) map_shapes(*sg, bt, seg);
+        probe_failed(*sg);
+      }
       to_truth(bt, cut);
       ctr.add("cut", cut);
       truth.wait_idle();
@@ -3404,6 +3474,12 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       cur = next_batch(true);
       ctr.add("took");
       if (!cur) return abort(fail(KBG_E_INVALID, pr.error));
+      if (will_reuse && !cur->bt.empty()) {  // resolve against this stage's lists
+        reuse = true;
+        S.stats.reused_batches++;
+        continue;
+      }
+      reuse = false;
       if (!cur->bt.empty()) {
         tp = clk::now();
         if ((st = launch(S.stages[si], cur)) != KBG_OK) return abort(st);
@@ -3413,6 +3489,15 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
     to_truth(bt, nb);
     recycle(cur);
+    if (reuse) {  // the next batch resolves against the same lists while they last
+      probe_failed(*sg);
+      ctr.add("take");
+      cur = next_batch(true);
+      ctr.add("took");
+      if (!cur) return abort(fail(KBG_E_INVALID, pr.error));
+      if (!cur->bt.empty()) S.stats.reused_batches++;
+      continue;
+    }
     if (!nxt) {  // the predictor was behind: take its next batch now and scan it
       ctr.add("take");
       nxt = next_batch(true);
