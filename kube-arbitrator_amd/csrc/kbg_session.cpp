@@ -628,6 +628,7 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
     a.up_capoff = (int32_t)((size_t)Gp * sizeof(kbg::TaskRec));
     a.down = dev_ptr(S, sg.h_down);
     if (!a.up || !a.down) return fail(KBG_E_HIP, "hipHostGetDevicePointer of a stage buffer failed");
+
     a.G = G;
     a.n_nodes = S.n_nodes;
     a.W = S.W;
@@ -644,6 +645,7 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
     }
     HIP_TRY(kbg::launch_firstfit(a, S.int_mode ? 1 : 0, S.stream, sg.ev[0], sg.ev[1]));
     trace_add("l.firstfit");
+
     if (avail) {
       if (S.comm->nccl) {  // (a communicator without RCCL — R sessions of one process, tools — sums on the host)
         const ncclResult_t nr = ncclAllReduce(S.d_down, S.d_down, (size_t)G, ncclUint32, ncclSum, S.comm->nccl, S.stream);
@@ -797,6 +799,7 @@ kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
 // before the table does. Grouped mode: one row per distinct shape with (tasks
 // of the shape + slack) slots; tasks of a shape share the row and a cursor.
 constexpr int32_t kGroupSlack = 512;     // extra candidate slots per shape row (grouped mode)
+constexpr int32_t kContendedSlack = 4096;  // the same in a rescan of the contended part of a cycle
 constexpr int32_t kFullScanGrow = 1024;  // cap on a full-scan row's extra slots
 constexpr int32_t kFullScanK = 8192;     // default batch of the full-scan mode
 
@@ -805,7 +808,11 @@ struct Grouper {
   std::vector<int32_t> shape_row, shape_stamp, count;
   int32_t stamp = 0;
   explicit Grouper(Session& s) : S(s), shape_row(s.n_shapes, -1), shape_stamp(s.n_shapes, -1) {}
-  int32_t build(kbg::Stage& sg, const int32_t* bt, int32_t n) {
+  // `slack`: grouped mode's extra candidate slots per shape row (the
+  // contended part of a cycle asks for long lists: few nodes still fit a
+  // shape there, and a list that holds all of them needs no rescan to
+  // learn that the shape fits nowhere)
+  int32_t build(kbg::Stage& sg, const int32_t* bt, int32_t n, int32_t slack = kGroupSlack) {
     sg.h_tasks = (kbg::TaskRec*)sg.h_up;
     ++stamp;
     sg.row_of.resize(n);
@@ -865,9 +872,14 @@ struct Grouper {
       const int64_t spare = S.cand_cap - (int64_t)G * S.M;
       if (longs * kFullScanGrow > spare) grow_cap = (int32_t)std::max<int64_t>(0, spare / std::max<int64_t>(1, longs));
     }
+    if (!S.opts.full_scan && slack > kGroupSlack) {  // within the candidate buffer (sized for K x (kGroupSlack + 1))
+      const int64_t room = (S.cand_cap - n) / std::max(1, G);
+      slack = (int32_t)std::max<int64_t>(kGroupSlack, std::min<int64_t>(slack, room));
+    }
+    const int32_t cap_want = std::max(4096, slack);
     for (int32_t g = 0; g < G; ++g) {
       uint32_t want;
-      if (!S.opts.full_scan) want = (uint32_t)std::min(count[g] + kGroupSlack, 4096);
+      if (!S.opts.full_scan) want = (uint32_t)std::min(count[g] + slack, cap_want);
       else if (sg.row_ext[g] != g) want = 0;  // its list is the shape's long one (Resolver: alias rows)
       else want = (uint32_t)(S.M + std::min(2 * count[g] + (g >> 3) + 64, grow_cap));
       sg.h_capoff[g + 1] = sg.h_capoff[g] + want;
@@ -2445,9 +2457,22 @@ void pin_near(int cpu, int nth = 1) {
     }
     return out;
   };
-  const std::string base = "/sys/devices/system/cpu/cpu" + std::to_string(cpu);
-  const std::vector<int> llc = read_list(base + "/cache/index3/shared_cpu_list");
-  const std::vector<int> smt = read_list(base + "/topology/thread_siblings_list");
+  // the topology of a cpu is read from sysfs once per process (every cycle
+  // starts its helper threads here)
+  static std::mutex topo_mu;
+  static std::unordered_map<int, std::pair<std::vector<int>, std::vector<int>>> topo;
+  std::vector<int> llc, smt;
+  {
+    std::lock_guard<std::mutex> lk(topo_mu);
+    auto it = topo.find(cpu);
+    if (it == topo.end()) {
+      const std::string base = "/sys/devices/system/cpu/cpu" + std::to_string(cpu);
+      it = topo.emplace(cpu, std::make_pair(read_list(base + "/cache/index3/shared_cpu_list"),
+                                            read_list(base + "/topology/thread_siblings_list"))).first;
+    }
+    llc = it->second.first;
+    smt = it->second.second;
+  }
   cpu_set_t allowed;
   if (llc.empty() || sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
   const size_t at = std::find(llc.begin(), llc.end(), cpu) - llc.begin();
@@ -2922,8 +2947,13 @@ struct Predictor {
         }
       }
       if (!b) {
-        b = new Batch();
         std::lock_guard<std::mutex> lk(P.mu);
+        if (!S.batch_pool.empty()) {  // an earlier cycle's batch: its vectors keep their capacity
+          b = static_cast<Batch*>(S.batch_pool.back().release());
+          S.batch_pool.pop_back();
+        } else {
+          b = new Batch();
+        }
         all.push_back(b);
       }
       const auto tp = clk::now();
@@ -3031,9 +3061,11 @@ struct Predictor {
     if (th.joinable()) th.join();
     if (bth.joinable()) bth.join();
     std::lock_guard<std::mutex> lk(P.mu);
-    for (Batch* b : all) {  // row buffers go back to the session's pool
+    for (Batch* b : all) {  // row buffers go back to the session's pool, the batch to its batch pool
       if (b->st.h_up) S.up_pool.push_back(b->st.h_up);
-      delete b;
+      b->st.h_up = nullptr;
+      b->G = -1;
+      S.batch_pool.emplace_back(b, [](void* q) { delete static_cast<Batch*>(q); });
     }
     all.clear();
     P.ready.clear();
@@ -3106,7 +3138,8 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   std::vector<kbg_decision>& dec = S.dec;
   // the Idle (Allocate) or Releasing (Pipeline) row before each decision
   // (indexed by decision; earlier actions' decisions are never undone)
-  std::vector<Res> dec_old(dec.size());
+  std::vector<Res>& dec_old = S.dec_old_buf;  // a session buffer: its pages stay mapped across cycles
+  dec_old.assign(dec.size(), Res{});
   dec_old.reserve(dec.size() + S.pend.size());
   std::vector<uint64_t> dec_oldp(dec.size() * (size_t)S.PW);  // host ports: used-port atoms before each decision
   std::vector<LastEval> last(S.n_jobs);
@@ -3147,7 +3180,9 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     ~TraceHook() { t_trace = nullptr; }
   } trace_hook(ctr.on ? &ctr : nullptr);
   static const bool no_builder = getenv("KBG_NO_BUILDER") != nullptr;
+  ctr.add("setup");
   pr.start(sched_getcpu(), !no_builder);
+  ctr.add("started");
   auto take = [&](bool block, bool* none) { return pr.take(block, none); };
   auto recycle = [&](Batch* b) { pr.recycle(b); };
   auto finish = [&]() {
@@ -3238,6 +3273,14 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   static const bool no_reuse = getenv("KBG_NO_CUT_REUSE") != nullptr;
   const bool reuse_ok = !S.opts.full_scan && !S.comm && !S.has_aff && !no_reuse;
   bool reuse = false;
+  // From the first cut on (the contended part of the cycle) every batch
+  // resolves against the latest stage, and a rescan covers the rest of the
+  // batch plus one row for every shape seen this cycle that is not known to
+  // fit nowhere, so a later batch's shapes mostly have rows already.
+  bool contended = false;
+  std::vector<int32_t> shape_rep(reuse_ok ? std::max(1, S.n_shapes) : 0, -1), seen_shapes, scan_list, shape_in;
+  int32_t shape_in_stamp = 0;
+  if (reuse_ok) shape_in.assign(std::max(1, S.n_shapes), 0);
   std::vector<int32_t> shape_row_of(reuse_ok ? std::max(1, S.n_shapes) : 0, -1), shapes_set, row_rep;
   // the stage's row of each shape, and a task of each row (the batch entries
   // [seg0, ...) of `b` built the stage's rows)
@@ -3355,7 +3398,8 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       if (rprof) rcyc[0] += cycles() - c0;
       if (r == RES_TRUNC) {
         if (reuse) ctr.add("reuse.rescan", i);
-        reuse = false;  // the rescan's rows, by batch entry
+        const bool keep_reuse = contended;  // the rescan's rows by shape (else by batch entry)
+        reuse = false;
         // A candidate list ran out before the table did. The predictions
         // still hold (no outcome differed), so instead of cutting the batch
         // and replaying the engine, write the commits so far back to HBM and
@@ -3366,7 +3410,22 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         st = push_deltas(S, touched);
         pushed = rstamp;
         if (st == KBG_OK) {
-          const int32_t G = grouper.build(*sg, bt.data() + i, (int32_t)bt.size() - i);
+          const int32_t* list = bt.data() + i;
+          int32_t len = nb - i;
+          if (keep_reuse) {  // the rest of the batch, then the live shapes it lacks (at most K entries)
+            scan_list.assign(bt.begin() + i, bt.end());
+            ++shape_in_stamp;
+            for (int32_t k = i; k < nb; ++k) shape_in[S.task_shape[bt[k]]] = shape_in_stamp;
+            for (int32_t sh : seen_shapes) {
+              if ((int32_t)scan_list.size() >= S.K) break;
+              if (shape_in[sh] == shape_in_stamp || failed[sh].load(std::memory_order_relaxed)) continue;
+              shape_in[sh] = shape_in_stamp;
+              scan_list.push_back(shape_rep[sh]);
+            }
+            list = scan_list.data();
+            len = (int32_t)scan_list.size();
+          }
+          const int32_t G = grouper.build(*sg, list, len, keep_reuse ? kContendedSlack : kGroupSlack);
           st = device_launch(S, *sg, G, pushed);
         }
         if (st == KBG_OK) st = device_wait(S, *sg);
@@ -3379,6 +3438,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         rstamp = ++S.res_stamp;  // commits after the rescan
         S.mstamp = rstamp;
         touched.clear();
+        if (keep_reuse) {
+          map_shapes(*sg, scan_list, 0);
+          reuse = true;
+        }
         r = rs.resolve(sg->row_of[0], t, &node, &kind);  // a fresh list always decides its first task
       }
       if (r == RES_PANIC) {
@@ -3388,6 +3451,13 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       const bool ok = node >= 0;
       bactual[i] = ok;
       S.stats.task_evaluations++;
+      if (reuse_ok) {
+        const int32_t sh = S.task_shape[t];
+        if (shape_rep[sh] < 0) {
+          shape_rep[sh] = t;
+          seen_shapes.push_back(sh);
+        }
+      }
       if (ok) {
         const Res old = kind == KBG_KIND_ALLOCATE ? S.idle[node] : S.rel[node];
         if (S.has_ports)
@@ -3458,6 +3528,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     if (cut >= 0) {  // restart the predictor from the engine state at the cut
       if ((st = device_drop(S, other)) != KBG_OK) return abort(st);  // nxt was predicted before the cut
       const bool will_reuse = reuse_ok && !aff_cut;
+      contended = will_reuse;
       if (will_reuse) {  // before the predictor restarts: it reads the failed shapes
         // a batch that resolved against an earlier batch's stage keeps that
         // stage's map (its own entries built no rows); otherwise the stage's

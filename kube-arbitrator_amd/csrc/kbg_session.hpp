@@ -426,6 +426,10 @@ struct Session {
   Stage stages[2];                // host staging of two batches in flight
   size_t up_cap = 0;              // bytes of one pinned row buffer (Stage::h_up)
   std::vector<char*> up_pool;     // spare pinned row buffers: the allocate builder's batches borrow them
+  // the allocate predictor's batch objects, kept across cycles (vector
+  // capacities; the type is private to kbg_session.cpp)
+  std::vector<std::unique_ptr<void, void (*)(void*)>> batch_pool;
+  std::vector<Res> dec_old_buf;   // allocate: the Idle / Releasing row before each decision
   int32_t res_stamp = 0;          // resolution stamps: monotone over the session (mark / mwmark compare)
   NodeDelta* h_deltas = nullptr; // pinned, mapped: the apply kernels read it in place
   bool uva = false;              // mapped host memory has the same address on the device
