@@ -205,7 +205,7 @@ inline void go_down(int32_t* h, int i0, int n, L less, bool go111) {
 
 kbg::JobKey make_job_key(const Session& S, const Engine& E, int32_t j) {
   if (S.job_chain_pgd) {  // the default tiers' chain (priority, gang, drf), without the loop
-    const bool ready = E.jready[j] >= S.jobs_in[j].min_available;
+    const bool ready = E.jready[j] >= S.job_min[j];
     uint64_t u;
     __builtin_memcpy(&u, &E.jshare[j], 8);
     const uint64_t lo = ready ? (u & ~(1ull << 63)) : 0;  // fields after a non-ready gang are zero
@@ -219,7 +219,7 @@ kbg::JobKey make_job_key(const Session& S, const Engine& E, int32_t j) {
     if (p == kbg::JO_PRIORITY) {  // priority.go:58-74 (higher first)
       k = (k << 32) | (zero ? 0u : S.job_prank[j]);
     } else if (p == kbg::JO_GANG) {  // gang.go:129-163 (non-ready first)
-      const bool ready = E.jready[j] >= S.jobs_in[j].min_available;
+      const bool ready = E.jready[j] >= S.job_min[j];
       k = (k << 1) | (zero ? 0u : (ready ? 1u : 0u));
       if (!ready) zero = true;
     } else {  // drf.go:109-125 (lower share first)
@@ -295,7 +295,7 @@ struct Ops {
   Engine& E;
   EngineProfile* prof = nullptr;
 
-  bool job_ready(int32_t j) const { return E.jready[j] >= S.jobs_in[j].min_available; }
+  bool job_ready(int32_t j) const { return E.jready[j] >= S.job_min[j]; }
 
   // Session.JobOrderFn (session_plugins.go:196-221) over the configured tiers
   // is the order of kbg_session.hpp JobKey keys, built by make_job_key.
@@ -373,7 +373,10 @@ struct Ops {
     for (;;) {
       if (E.in_job) {
         const int32_t j = E.cur_j;
-        if (E.cursor[j] < S.pend_len[j]) return S.pend[S.pend_off[j] + E.cursor[j]++];
+        if (E.cursor[j] < S.pend_len[j]) {
+          E.cur_pos = S.pend_off[j] + E.cursor[j]++;
+          return S.pend[E.cur_pos];
+        }
         jremove_top(E.cur_q);  // no task of the job fitted: the job is not pushed back
         qpush(E.cur_q);        // allocate.go:173-174
         E.in_job = false;
@@ -397,7 +400,7 @@ struct Ops {
     if (!success) return;
     uint64_t c0 = prof ? cycles() : 0;
     const int32_t j = E.cur_j, q = E.cur_q;
-    const Res& r = S.treq[t];
+    const Res& r = S.pend_req_cur[E.cur_pos];  // == S.treq[t]
     if (S.has_drf) {
       kbg::res_add(E.jalloc[j], r);
       E.jshare[j] = share_of(E.jalloc[j], S.drf_total);
@@ -2049,6 +2052,11 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   S.pend_all = S.pend;
   S.pend_off_all = S.pend_off;
   S.pend_len_all = S.pend_len;
+  S.pend_req_all.resize(S.pend_all.size());
+  for (size_t i = 0; i < S.pend_all.size(); ++i) S.pend_req_all[i] = S.treq[S.pend_all[i]];
+  S.pend_req_cur = S.pend_req_all.data();
+  S.job_min.resize(S.n_jobs);
+  for (int32_t j = 0; j < S.n_jobs; ++j) S.job_min[j] = S.jobs_in[j].min_available;
   build_heaps(S, E);
 
   phase("heaps");
@@ -2691,6 +2699,7 @@ void begin_cycle(Session& S) {
   S.pend = S.pend_all;
   S.pend_off = S.pend_off_all;
   S.pend_len = S.pend_len_all;
+  S.pend_req_cur = S.pend_req_all.data();
   if (S.has_aff) {
     S.affm->st = S.affm->st0;
     std::fill(S.aff_gain_flag.begin(), S.aff_gain_flag.end(), 0);
@@ -2719,6 +2728,9 @@ Engine live_engine(Session& S) {
     }
     S.pend_len[j] = (int32_t)S.pend.size() - S.pend_off[j];
   }
+  S.pend_req.resize(S.pend.size());
+  for (size_t i = 0; i < S.pend.size(); ++i) S.pend_req[i] = S.treq[S.pend[i]];
+  S.pend_req_cur = S.pend_req.data();
   build_heaps(S, E);
   return E;
 }
