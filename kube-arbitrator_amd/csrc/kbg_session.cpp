@@ -4567,26 +4567,36 @@ bool host_victims(Session& S, int32_t mode, int32_t t, int32_t n, std::vector<in
         const int32_t jv = S.task_job[pre[i]];
         if (!(S.jobs_in[jv].min_available <= S.committed_ready[jv] - 1)) keep[i] = 0;
       }
+    // the per-job / per-queue running allocations of the fns' maps
+    // (`allocations`, drf.go:86-100, proportion.go:163-183): a node holds a
+    // few dozen preemptees of a few jobs, so a flat list searched linearly
+    // replaces the hash map (no allocation per call)
+    thread_local std::vector<std::pair<int32_t, Res>> alloc;
+    auto entry = [&](int32_t id, const Res& init) -> Res& {
+      for (auto& e : alloc)
+        if (e.first == id) return e.second;
+      alloc.emplace_back(id, init);
+      return alloc.back().second;
+    };
     if (fns & kbg::VP_DRF) {  // drf.go:80-105
       Res la = S.fin.jalloc[pj];
       kbg::res_add(la, S.treq[t]);
       const double ls = share_of(la, S.drf_total);
-      std::unordered_map<int32_t, Res> alloc;
+      alloc.clear();
       for (size_t i = 0; i < pre.size(); ++i) {
         const int32_t jv = S.task_job[pre[i]];
-        auto it = alloc.emplace(jv, S.fin.jalloc[jv]).first;
-        if (!kbg::res_sub(it->second, S.treq[pre[i]])) return false;
-        const double rs = share_of(it->second, S.drf_total);
+        Res& a = entry(jv, S.fin.jalloc[jv]);
+        if (!kbg::res_sub(a, S.treq[pre[i]])) return false;
+        const double rs = share_of(a, S.drf_total);
         if (!(ls < rs || std::fabs(ls - rs) <= 0.000001)) keep[i] = 0;
       }
     }
     if (fns & kbg::VP_PROP) {  // proportion.go:161-186
-      std::unordered_map<int32_t, Res> alloc;
+      alloc.clear();
       for (size_t i = 0; i < pre.size(); ++i) {
         const int32_t q = S.job_queue[S.task_job[pre[i]]];
-        auto it = alloc.emplace(q, S.fin.qalloc[q]).first;
         const Res& r = S.treq[pre[i]];
-        Res& a = it->second;
+        Res& a = entry(q, S.fin.qalloc[q]);
         if (a.c < r.c && a.m < r.m && a.g < r.g) {  // Resource.Less: skipped
           keep[i] = 0;
           continue;
@@ -4604,12 +4614,12 @@ bool host_victims(Session& S, int32_t mode, int32_t t, int32_t n, std::vector<in
 
 // host_victims plus the rest of the reference's per-node test, for node n
 // against the current host state: 0 the scan moves on, 1 stop, 2 panic.
-int host_stop(Session& S, int32_t mode, int32_t t, int32_t n) {
+// `v` receives the victims (valid when the result is 1).
+int host_stop(Session& S, int32_t mode, int32_t t, int32_t n, std::vector<int32_t>& v) {
   const int32_t cls = S.task_class[t];
   if (!((S.h_class_mask[(size_t)cls * S.W + (n >> 6)] >> (n & 63)) & 1ull)) return 0;  // static predicate
   if (S.panic_node[n]) return 2;                                                      // predicates.go:122-123
   if (S.pred_active && S.ntasks[n] >= S.maxtasks[n]) return 0;                        // :125-127
-  thread_local std::vector<int32_t> v;
   if (!host_victims(S, mode, t, n, &v)) return 2;
   if (v.empty()) return 0;
   Res all{};
@@ -4631,10 +4641,28 @@ struct Stmt {
 
 enum { TRY_NONE = 0, TRY_ASSIGNED = 1 };
 
+// Opt-in cycle counters of the victim actions' host side (KBG_PROFILE_VICTIM=1):
+// device scans, the stop search (with host re-evaluations), victim selection
+// at the chosen node, evictions + pipeline, the action's own loop
+struct VictimProfile {
+  bool on = getenv("KBG_PROFILE_VICTIM") != nullptr;
+  uint64_t scan = 0, walk = 0, select = 0, apply = 0, tries = 0;
+  void print(const char* action, double ms) {
+    if (!on || !tries) return;
+    fprintf(stderr, "[kbg victim] %s %.3f ms, %llu tries, cycles/try: scan %.0f walk %.0f select %.0f apply %.0f\n", action,
+            ms, (unsigned long long)tries, (double)scan / tries, (double)walk / tries, (double)select / tries,
+            (double)apply / tries);
+    scan = walk = select = apply = tries = 0;
+  }
+};
+VictimProfile& vprof() {
+  static VictimProfile p;
+  return p;
+}
+
 // preempt.go:174-240 / reclaim.go:106-176 for one task: the device finds the
 // first node where the reference stops; the host evicts there and pipelines.
 kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, int32_t* outcome) {
-  using clk = std::chrono::steady_clock;
   *outcome = TRY_NONE;
   kbg::VictimScan p{};
   p.n_nodes = S.n_nodes;
@@ -4664,6 +4692,9 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
   const int32_t kjob = mode != kbg::VM_RECLAIM && S.jn_off[pj + 1] > S.jn_off[pj] ? pj : -1;
   const kbg::VictimKey key{mode, kjob, p.cls, p.queue, {p.req[0], p.req[1], p.req[2]}, (dfns & kbg::VP_DRF) ? p.ls : 0.0};
   Session::VictimCache& vc = S.vc;
+  VictimProfile& vp = vprof();
+  uint64_t c0 = vp.on ? cycles() : 0;
+  if (vp.on) vp.tries++;
   if (!(vc.valid && vc.key == key)) {
     // device scan of every node against the current state
     kbg_status st = victim_push(S, L.touched);
@@ -4707,10 +4738,17 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
     vc.fns = dfns;
     vc.valid = true;
   }
+  if (vp.on) {
+    const uint64_t c1 = cycles();
+    vp.scan += c1 - c0;
+    c0 = c1;
+  }
   // the first stop in node order: a node changed since the scan is
   // re-evaluated on the host (host_stop) when the search reaches it
   int32_t n = -1;
   bool pan = false;
+  thread_local std::vector<int32_t> victims;
+  bool have_victims = false;  // the stop node was just re-evaluated: its victims are in `victims`
   for (int32_t w = vc.lb; w < S.W32 && n < 0; ++w) {
     if (w == vc.lb && !(vc.stop[w] | vc.unk[w])) {  // nothing left below the next word
       vc.lb = w + 1;
@@ -4722,29 +4760,39 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
       const int32_t node = w * 32 + b;
       if (vc.unk[w] & bit) {
         vc.unk[w] &= ~bit;
-        const int r = host_stop(S, mode, t, node);
+        const int r = host_stop(S, mode, t, node, victims);
         S.stats.victim_host_evals++;
         vc.stop[w] = r ? (vc.stop[w] | bit) : (vc.stop[w] & ~bit);
         vc.panic[w] = r == 2 ? (vc.panic[w] | bit) : (vc.panic[w] & ~bit);
         if (!r) continue;
+        have_victims = r == 1;
       }
       n = node;
       pan = (vc.panic[w] & bit) != 0;
       break;
     }
   }
+  if (vp.on) {
+    const uint64_t c1 = cycles();
+    vp.walk += c1 - c0;
+    c0 = c1;
+  }
   if (n < 0) return KBG_OK;  // no node: the task stays Pending
   if (pan)
     return fail(KBG_E_REF_PANIC, "victim selection panics on node " + S.strs[S.nodes_in[n].name] +
                                      " (nil Node or Resource.Sub underflow in a victim fn)");
-  std::vector<int32_t> victims;
-  if (!host_victims(S, mode, t, n, &victims) || victims.empty())
+  if (!have_victims && (!host_victims(S, mode, t, n, &victims) || victims.empty()))
     return fail(KBG_E_INVALID, "internal: device and host victim selection disagree");
   Res all{};
   for (int32_t v : victims) kbg::res_add(all, S.treq[v]);
   const Res& req = S.treq[t];
   if (all.c < req.c && all.m < req.m && all.g < req.g)
     return fail(KBG_E_INVALID, "internal: device and host victim validation disagree");
+  if (vp.on) {
+    const uint64_t c1 = cycles();
+    vp.select += c1 - c0;
+    c0 = c1;
+  }
   Res resreq = req;
   for (int32_t v : victims) {
     if (stmt) stmt->ops.push_back({true, v, -1, t, false});
@@ -4757,7 +4805,7 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
   if (!L.pipeline(t, n, &dup)) return fail(KBG_E_REF_PANIC, "pipeline: Releasing.Sub underflow (node_info.go:117-118)");
   if (stmt) stmt->ops.push_back({false, t, n, -1, dup});
   else append_log(S, t, n, KBG_KIND_PIPELINE, dup);
-  (void)clk::now();
+  if (vp.on) vp.apply += cycles() - c0;
   *outcome = TRY_ASSIGNED;
   return KBG_OK;
 }
@@ -4887,6 +4935,7 @@ kbg_status reclaim_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
   HIP_TRY(hipStreamSynchronize(S.stream));
   S.vstage_busy = false;
   S.stats.reclaim_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  vprof().print("reclaim", S.stats.reclaim_ms);
   return copy_log(S, out, cap, n_out, result);
 }
 
@@ -4930,6 +4979,7 @@ kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
     }
   }
   kbg_status result = KBG_OK;
+  Stmt stmt;  // one statement object, emptied by every commit / discard (its ops keep their capacity)
   auto run = [&]() -> kbg_status {
     kbg_status s2;
     int32_t outcome;
@@ -4937,7 +4987,7 @@ kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
       for (;;) {  // preempt.go:81-130: between jobs of the queue
         if (!has_jobs[q] || jheap[q].empty()) break;
         const int32_t pj = pop(jheap[q]);
-        Stmt stmt;
+        stmt.ops.clear();
         bool assigned = false;
         for (;;) {
           if (next[pj] >= pending[pj].size()) break;
@@ -4961,7 +5011,7 @@ kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
         for (;;) {
           if (next[j] >= pending[j].size()) break;
           const int32_t t = pending[j][next[j]++];
-          Stmt stmt;
+          stmt.ops.clear();
           if ((s2 = try_task(S, R.L, kbg::VM_PREEMPT_TASKS, t, &stmt, &outcome)) != KBG_OK) return s2;
           stmt_commit(S, stmt);
           if ((s2 = R.sync()) != KBG_OK) return s2;
@@ -4979,6 +5029,7 @@ kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
   HIP_TRY(hipStreamSynchronize(S.stream));
   S.vstage_busy = false;
   S.stats.preempt_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  vprof().print("preempt", S.stats.preempt_ms);
   return copy_log(S, out, cap, n_out, result);
 }
 
