@@ -539,6 +539,9 @@ void free_device(Session& S) {
   S.fit_cap = S.fit_out_cap = 0;
   if (S.h_vbits) (void)hipHostFree(S.h_vbits);
   if (S.h_sdeltas) (void)hipHostFree(S.h_sdeltas);
+  if (S.c_run_pinned) (void)hipHostFree(S.c_run_pinned);
+  S.c_run_pinned = nullptr;
+  S.c_run_pinned_cap = 0;
   S.h_vbits = nullptr;
   S.h_sdeltas = nullptr;
   S.vt_ready = false;
@@ -4225,12 +4228,24 @@ kbg_status victim_push(Session& S, const std::vector<int32_t>& touched) {
     kbg_status st = push_mask_deltas(S);
     if (st != KBG_OK) return st;
   }
-  if (!S.sdeltas.empty()) {  // last write of each entry wins
-    std::unordered_set<int64_t> seen;
-    std::vector<kbg::StateDelta> uniq;
-    for (size_t i = S.sdeltas.size(); i-- > 0;)
-      if (seen.insert(((int64_t)S.sdeltas[i].kind << 32) | (uint32_t)S.sdeltas[i].index).second)
-        uniq.push_back(S.sdeltas[i]);
+  if (!S.sdeltas.empty()) {  // last write of each entry wins: one stamp per (kind, index), no hashing
+    const size_t sizes[4] = {std::max<size_t>(1, S.nt_task.size()), (size_t)std::max(1, S.n_jobs),
+                             (size_t)std::max(1, S.n_jobs), (size_t)std::max(1, S.n_queues)};
+    for (int k = 0; k < 4; ++k)
+      if (S.sd_seen[k].size() < sizes[k]) S.sd_seen[k].assign(sizes[k], 0);
+    if (++S.sd_gen == 0) {  // wrapped: clear the stamps
+      for (auto& v : S.sd_seen) std::fill(v.begin(), v.end(), 0u);
+      S.sd_gen = 1;
+    }
+    thread_local std::vector<kbg::StateDelta> uniq;
+    uniq.clear();
+    for (size_t i = S.sdeltas.size(); i-- > 0;) {
+      const kbg::StateDelta& d = S.sdeltas[i];
+      uint32_t& seen = S.sd_seen[d.kind][d.index];
+      if (seen == S.sd_gen) continue;
+      seen = S.sd_gen;
+      uniq.push_back(d);
+    }
     S.sdeltas.swap(uniq);
   }
   {  // few changes: in the kernel arguments
@@ -4394,9 +4409,16 @@ kbg_status vt_setup(Session& S) {
     qa[3 * q + 1] = S.fin.qalloc[q].m;
     qa[3 * q + 2] = S.fin.qalloc[q].g;
   }
-  S.c_run_host.resize(std::max<size_t>(1, S.nt_task.size()));
-  for (size_t k = 0; k < S.nt_task.size(); ++k) S.c_run_host[k] = S.trun[S.nt_task[k]];
-  HIP_TRY(hipMemcpyAsync(S.vt.c_run, S.c_run_host.data(), S.nt_task.size(), hipMemcpyHostToDevice, S.stream));
+  const size_t P = std::max<size_t>(1, S.nt_task.size());
+  if (S.c_run_pinned_cap < P) {  // pinned staging: the upload is one DMA, not a pageable copy
+    if (S.c_run_pinned) (void)hipHostFree(S.c_run_pinned);
+    S.c_run_pinned = nullptr;
+    S.c_run_pinned_cap = 0;
+    HIP_TRY(hipHostMalloc((void**)&S.c_run_pinned, P, hipHostMallocDefault));
+    S.c_run_pinned_cap = P;
+  }
+  for (size_t k = 0; k < S.nt_task.size(); ++k) S.c_run_pinned[k] = S.trun[S.nt_task[k]];
+  HIP_TRY(hipMemcpyAsync(S.vt.c_run, S.c_run_pinned, S.nt_task.size(), hipMemcpyHostToDevice, S.stream));
   HIP_TRY(hipMemcpyAsync(S.vt.j_ready, S.committed_ready.data(), (size_t)S.n_jobs * 4, hipMemcpyHostToDevice,
                          S.stream));
   HIP_TRY(hipMemcpyAsync(S.vt.j_alloc, ja.data(), ja.size() * 8, hipMemcpyHostToDevice, S.stream));
@@ -4646,13 +4668,15 @@ enum { TRY_NONE = 0, TRY_ASSIGNED = 1 };
 // at the chosen node, evictions + pipeline, the action's own loop
 struct VictimProfile {
   bool on = getenv("KBG_PROFILE_VICTIM") != nullptr;
-  uint64_t scan = 0, walk = 0, select = 0, apply = 0, tries = 0;
+  uint64_t scan = 0, walk = 0, select = 0, apply = 0, tries = 0, setup = 0, flush = 0;
   void print(const char* action, double ms) {
     if (!on || !tries) return;
-    fprintf(stderr, "[kbg victim] %s %.3f ms, %llu tries, cycles/try: scan %.0f walk %.0f select %.0f apply %.0f\n", action,
-            ms, (unsigned long long)tries, (double)scan / tries, (double)walk / tries, (double)select / tries,
-            (double)apply / tries);
-    scan = walk = select = apply = tries = 0;
+    fprintf(stderr,
+            "[kbg victim] %s %.3f ms, %llu tries, cycles/try: scan %.0f walk %.0f select %.0f apply %.0f; "
+            "setup %.0f kcyc, flush %.0f kcyc\n",
+            action, ms, (unsigned long long)tries, (double)scan / tries, (double)walk / tries, (double)select / tries,
+            (double)apply / tries, setup / 1e3, flush / 1e3);
+    scan = walk = select = apply = tries = setup = flush = 0;
   }
 };
 VictimProfile& vprof() {
@@ -4948,6 +4972,7 @@ kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
   S.preempted = true;
   S.action = KBG_ACTION_PREEMPT;
   S.vc.valid = false;  // other actions changed the session since any earlier scan
+  const uint64_t pc0 = vprof().on ? cycles() : 0;
   if ((st = vt_setup(S)) != KBG_OK) return st;
   VictimRun R(S);
   auto job_less = [&](int32_t a, int32_t b) { return make_job_key(S, S.fin, a) < make_job_key(S, S.fin, b); };
@@ -4978,6 +5003,7 @@ kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
       under.push_back(j);
     }
   }
+  if (vprof().on) vprof().setup += cycles() - pc0;
   kbg_status result = KBG_OK;
   Stmt stmt;  // one statement object, emptied by every commit / discard (its ops keep their capacity)
   auto run = [&]() -> kbg_status {
@@ -5022,10 +5048,12 @@ kbg_status preempt_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_
     return KBG_OK;
   };
   result = run();
+  const uint64_t pc1 = vprof().on ? cycles() : 0;
   if (result == KBG_OK || result == KBG_E_REF_PANIC) {
     kbg_status s2 = R.flush();
     if (s2 != KBG_OK) return s2;
   }
+  if (vprof().on) vprof().flush += cycles() - pc1;
   HIP_TRY(hipStreamSynchronize(S.stream));
   S.vstage_busy = false;
   S.stats.preempt_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -305,7 +305,10 @@ struct Session {
   std::vector<int32_t> task_node;             // node index of a task's NodeName (-1: not a session node)
   std::vector<kbg_eviction> evictions;        // committed cache.Evict calls
   std::vector<int32_t> t_pos;                 // a task's position in the candidate lists (-1: none)
-  std::vector<uint8_t> c_run_host;            // running flags in candidate order (upload staging)
+  uint8_t* c_run_pinned = nullptr;            // running flags in candidate order (pinned upload staging)
+  size_t c_run_pinned_cap = 0;
+  std::vector<uint32_t> sd_seen[4];           // victim_push: last-write dedup stamps per StateDelta kind
+  uint32_t sd_gen = 0;
   std::vector<int32_t> tier_preempt, tier_reclaim;  // VictimPlugin bits per tier holding an enabled victim fn
   int32_t max_candidates = 0;
   kbg::VictimTables vt{};                     // device copies (allocated at the first victim action)
