@@ -373,10 +373,7 @@ struct Ops {
     for (;;) {
       if (E.in_job) {
         const int32_t j = E.cur_j;
-        if (E.cursor[j] < S.pend_len[j]) {
-          E.cur_pos = S.pend_off[j] + E.cursor[j]++;
-          return S.pend[E.cur_pos];
-        }
+        if (E.cursor[j] < S.pend_len[j]) return S.pend[S.pend_off[j] + E.cursor[j]++];
         jremove_top(E.cur_q);  // no task of the job fitted: the job is not pushed back
         qpush(E.cur_q);        // allocate.go:173-174
         E.in_job = false;
@@ -400,7 +397,7 @@ struct Ops {
     if (!success) return;
     uint64_t c0 = prof ? cycles() : 0;
     const int32_t j = E.cur_j, q = E.cur_q;
-    const Res& r = S.pend_req_cur[E.cur_pos];  // == S.treq[t]
+    const Res& r = S.treq[t];
     if (S.has_drf) {
       kbg::res_add(E.jalloc[j], r);
       E.jshare[j] = share_of(E.jalloc[j], S.drf_total);
@@ -2055,9 +2052,6 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   S.pend_all = S.pend;
   S.pend_off_all = S.pend_off;
   S.pend_len_all = S.pend_len;
-  S.pend_req_all.resize(S.pend_all.size());
-  for (size_t i = 0; i < S.pend_all.size(); ++i) S.pend_req_all[i] = S.treq[S.pend_all[i]];
-  S.pend_req_cur = S.pend_req_all.data();
   S.job_min.resize(S.n_jobs);
   for (int32_t j = 0; j < S.n_jobs; ++j) S.job_min[j] = S.jobs_in[j].min_available;
   build_heaps(S, E);
@@ -2702,7 +2696,6 @@ void begin_cycle(Session& S) {
   S.pend = S.pend_all;
   S.pend_off = S.pend_off_all;
   S.pend_len = S.pend_len_all;
-  S.pend_req_cur = S.pend_req_all.data();
   if (S.has_aff) {
     S.affm->st = S.affm->st0;
     std::fill(S.aff_gain_flag.begin(), S.aff_gain_flag.end(), 0);
@@ -2731,9 +2724,6 @@ Engine live_engine(Session& S) {
     }
     S.pend_len[j] = (int32_t)S.pend.size() - S.pend_off[j];
   }
-  S.pend_req.resize(S.pend.size());
-  for (size_t i = 0; i < S.pend.size(); ++i) S.pend_req[i] = S.treq[S.pend[i]];
-  S.pend_req_cur = S.pend_req.data();
   build_heaps(S, E);
   return E;
 }

@@ -98,7 +98,6 @@ struct Engine {
   std::vector<int32_t> jlen;    // live length of each per-queue heap
   std::vector<int32_t> cursor;  // per job: next position in its sorted pending list
   int32_t cur_q = -1, cur_j = -1;
-  int32_t cur_pos = -1;         // pending-list position of the task next_task returned last
   bool in_job = false;
   std::vector<Res> jalloc;      // drf attr.allocated
   std::vector<double> jshare;   // drf attr.share
@@ -239,12 +238,6 @@ struct Session {
   std::vector<int32_t> joff, jcap;                       // per-queue job-heap segment (jcap + 1 slots)
   std::vector<int32_t> pend, pend_off, pend_len;         // per-job pending tasks in TaskOrderFn order (this cycle)
   std::vector<int32_t> pend_all, pend_off_all, pend_len_all;  // the same at open
-  // the request of each pending-list entry, beside it (the ordering engine
-  // reads it with the entry instead of a dependent treq[task] load):
-  // pend_req_all for pend_all, pend_req for a filtered pend (live_engine);
-  // pend_req_cur points at the one that matches pend this cycle
-  std::vector<Res> pend_req_all, pend_req;
-  const Res* pend_req_cur = nullptr;
   std::vector<int32_t> job_min;  // jobs_in[j].min_available, packed for the engine
   std::vector<char> pending_candidate;                   // task is Pending and not BestEffort
   std::vector<char> be_task;                             // task is Pending and BestEffort (backfill.go:48-50)
