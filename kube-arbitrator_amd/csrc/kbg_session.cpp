@@ -3417,10 +3417,18 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         if (st == KBG_OK) {
           const int32_t* list = bt.data() + i;
           int32_t len = nb - i;
-          if (keep_reuse) {  // the rest of the batch, then the live shapes it lacks (at most K entries)
-            scan_list.assign(bt.begin() + i, bt.end());
+          if (keep_reuse) {
+            // one task per shape (rows are looked up by shape from here on):
+            // this task, the other shapes of the rest of the batch, then the
+            // live shapes it lacks (at most K entries)
+            scan_list.clear();
             ++shape_in_stamp;
-            for (int32_t k = i; k < nb; ++k) shape_in[S.task_shape[bt[k]]] = shape_in_stamp;
+            for (int32_t k = i; k < nb && (int32_t)scan_list.size() < S.K; ++k) {
+              const int32_t sh = S.task_shape[bt[k]];
+              if (shape_in[sh] == shape_in_stamp) continue;
+              shape_in[sh] = shape_in_stamp;
+              scan_list.push_back(bt[k]);
+            }
             for (int32_t sh : seen_shapes) {
               if ((int32_t)scan_list.size() >= S.K) break;
               if (shape_in[sh] == shape_in_stamp || failed[sh].load(std::memory_order_relaxed)) continue;

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkbgpu.so")
+# KBG_LIB_PATH: another build of the library (same-box A/B runs of two trees)
+LIB_PATH = os.environ.get("KBG_LIB_PATH") or os.path.join(_HERE, "libkbgpu.so")
 
 # kbg_status
 KBG_OK = 0
