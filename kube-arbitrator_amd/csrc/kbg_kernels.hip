@@ -661,6 +661,9 @@ __device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t
     any_pm |= pm[h];
   }
   if (!any_pm) return kNone;  // no preemptee: every fn returns nil
+  // the first chunk's gang inputs, requested before the tier walk needs them
+  // (one dependent level less on the node's load chain)
+  const bool g0 = c0.job >= 0 && t.j_min[c0.job] <= t.j_ready[c0.job] - 1;
   bool panic = false;
   uint64_t vm[NCH];
   bool victims = false;
@@ -672,10 +675,10 @@ __device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t
     for (int h = 0; h < NCH; ++h) {
       tm[h] = 0ull;
       if (h >= nch) continue;
-      const VCand c = load_cand(p, t, off, L, h * 64 + lane);
+      const VCand c = h == 0 ? c0 : load_cand(p, t, off, L, h * 64 + lane);
       uint64_t m = pm[h];
       if (fns & VP_GANG)  // gang.go:104-124
-        m &= __ballot(c.job >= 0 && t.j_min[c.job] <= t.j_ready[c.job] - 1);
+        m &= __ballot(h == 0 ? g0 : (c.job >= 0 && t.j_min[c.job] <= t.j_ready[c.job] - 1));
       if (fns & (VP_DRF | VP_PROP)) {
         const bool on = (pm[h] >> lane) & 1ull;
         double xd[3], xp[3];
@@ -726,7 +729,7 @@ __device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t
     if (!vm[h]) continue;
     // each lane reads its own candidate's request (one coalesced load), the
     // wave-uniform sum takes them lane by lane in order
-    const VCand c = load_cand(p, t, off, L, h * 64 + lane);
+    const VCand c = h == 0 ? c0 : load_cand(p, t, off, L, h * 64 + lane);
     for (uint64_t b = vm[h]; b; b &= b - 1) {
       const int l2 = __builtin_ctzll(b);
       all[0] += rl_d(c.r[0], l2);
