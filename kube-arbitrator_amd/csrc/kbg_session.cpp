@@ -1765,14 +1765,51 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
       if (it != S.node_of.end()) S.task_node[t] = it->second;
     }
   }
-  S.nt_off.assign(N + 1, 0);
-  S.nt_task.clear();
+  // An update's events change a node's list only through its NodeInfo
+  // (in_node_add / in_node_remove mark the node) and a task's status only by
+  // moving it off and onto its node: the lists of the other nodes are copied
+  // from the last derive, the marked ones (and the updated tasks' nodes) are
+  // rebuilt.
+  const bool vincr = incr && S.upd_nodes_valid && (int32_t)S.nt_off.size() == N + 1;
+  std::vector<int32_t>& off = vincr ? S.nt_off_buf : S.nt_off;
+  std::vector<int32_t>& vt = vincr ? S.nt_task_buf : S.nt_task;
+  std::vector<uint8_t> vdirty;
+  if (vincr) {
+    vdirty.assign(N, 0);
+    for (int32_t n : S.upd_nodes) vdirty[n] = 1;
+    for (int32_t t : S.upd_tasks)
+      if (S.task_node[t] >= 0 && S.task_node[t] < N) vdirty[S.task_node[t]] = 1;
+    vt.reserve(S.nt_task.size() + S.upd_tasks.size());
+  }
+  off.assign(N + 1, 0);
+  vt.clear();
   S.max_candidates = 0;
   for (int32_t n = 0; n < N; ++n) {
-    for (int32_t t : S.node_task_order[n])
-      if (S.tstat_in[t] == KBG_RUNNING) S.nt_task.push_back(t);
-    S.nt_off[n + 1] = (int32_t)S.nt_task.size();
-    S.max_candidates = std::max(S.max_candidates, S.nt_off[n + 1] - S.nt_off[n]);
+    if (vincr && !vdirty[n]) {
+      vt.insert(vt.end(), S.nt_task.begin() + S.nt_off[n], S.nt_task.begin() + S.nt_off[n + 1]);
+    } else {
+      for (int32_t t : S.node_task_order[n])
+        if (S.tstat_in[t] == KBG_RUNNING) vt.push_back(t);
+    }
+    off[n + 1] = (int32_t)vt.size();
+    S.max_candidates = std::max(S.max_candidates, off[n + 1] - off[n]);
+  }
+  if (vincr) {
+    S.nt_off.swap(S.nt_off_buf);
+    S.nt_task.swap(S.nt_task_buf);
+  }
+  S.upd_nodes_valid = false;
+  // KBG_CHECK_DERIVE=1 (tests): an update's incremental results against the
+  // full recomputation, bit for bit
+  const bool check = !full && getenv("KBG_CHECK_DERIVE") != nullptr;
+  if (check) {
+    std::vector<int32_t> o2(N + 1, 0), t2;
+    for (int32_t n = 0; n < N; ++n) {
+      for (int32_t t : S.node_task_order[n])
+        if (S.tstat_in[t] == KBG_RUNNING) t2.push_back(t);
+      o2[n + 1] = (int32_t)t2.size();
+    }
+    if (o2 != S.nt_off || t2 != S.nt_task) return fail(KBG_E_INVALID, "internal: incremental victim lists differ");
   }
   phase("nodes+victims");
   setup_pod_keys(S, incr, &S.upd_tasks, &was);
@@ -1809,31 +1846,62 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     S.jt_off[j + 1] = (int32_t)S.jt.size();
   }
   auto job_tasks = [&](int32_t j) { return std::make_pair(S.jt.begin() + S.jt_off[j], S.jt.begin() + S.jt_off[j + 1]); };
-  for (int32_t j = 0; j < S.n_jobs; ++j) {
-    if (jincr && !jtouch[j]) {
-      E.jready[j] = prev_jready[j];
-      continue;
+  phase("job lists");
+  if (jincr) {
+    // counts: the updated tasks' old statuses out, their new ones in (a task
+    // below T_prev was live, in its job's list, at the last derive)
+    E.jready = std::move(prev_jready);
+    for (size_t i = 0; i < S.upd_tasks.size(); ++i) {
+      const int32_t t = S.upd_tasks[i];
+      const int32_t j = S.task_job[t];
+      if (t < T_prev && ready_status(was_stat[i])) E.jready[j]--;
+      if (S.task_live[t] && ready_status(S.tstat_in[t])) E.jready[j]++;
     }
-    for (auto [b, e] = job_tasks(j); b != e; ++b)
-      if (ready_status(S.tstat_in[*b])) E.jready[j]++;
+  } else {
+    for (int32_t j = 0; j < S.n_jobs; ++j)
+      for (auto [b, e] = job_tasks(j); b != e; ++b)
+        if (ready_status(S.tstat_in[*b])) E.jready[j]++;
   }
   S.job_ready0 = E.jready;
 
-  // drf.go:55-78
+  phase("ready counts");
   S.drf_total = Res{};
   S.prop_total = Res{};
-  if (S.has_drf) {
+  bool prop_exact = false;  // every queue sum below is an exact integer sum (proportion block)
+  // drf.go:55-78, after the proportion sums (they say whether the job sums
+  // are exact): an update's job allocations follow from its tasks' old and
+  // new statuses when every request is an integer and every sum stays below
+  // 2^53 (any summation order then gives the same doubles), else each
+  // touched job is summed again in task order
+  auto drf_block = [&]() {
+    if (!S.has_drf) return;
     for (int32_t n = 0; n < N; ++n) kbg::res_add(S.drf_total, to_res(S.nodes_in[n].allocatable));
+    const bool dexact = jincr && prop_exact && S.jalloc_exact;
+    if (dexact) {
+      E.jalloc = std::move(prev_jalloc);
+      for (size_t i = 0; i < S.upd_tasks.size(); ++i) {  // out first: the partial sums stay below the final
+        const int32_t t = S.upd_tasks[i];
+        if (t < T_prev && allocated_status(was_stat[i])) {
+          Res& a = E.jalloc[S.task_job[t]];
+          const Res& r = S.treq[t];
+          a = Res{a.c - r.c, a.m - r.m, a.g - r.g};
+        }
+      }
+      for (int32_t t : S.upd_tasks)
+        if (S.task_live[t] && allocated_status(S.tstat_in[t])) kbg::res_add(E.jalloc[S.task_job[t]], S.treq[t]);
+    }
     for (int32_t j = 0; j < S.n_jobs; ++j) {
-      if (jincr && !jtouch[j]) {
-        E.jalloc[j] = prev_jalloc[j];
-      } else {
-        for (auto [b, e] = job_tasks(j); b != e; ++b)
-          if (allocated_status(S.tstat_in[*b])) kbg::res_add(E.jalloc[j], S.treq[*b]);
+      if (!dexact) {
+        if (jincr && !jtouch[j]) {
+          E.jalloc[j] = prev_jalloc[j];
+        } else {
+          for (auto [b, e] = job_tasks(j); b != e; ++b)
+            if (allocated_status(S.tstat_in[*b])) kbg::res_add(E.jalloc[j], S.treq[*b]);
+        }
       }
       E.jshare[j] = share_of(E.jalloc[j], S.drf_total);  // the total may have changed (SetNode)
     }
-  }
+  };
   // proportion.go:54-144 (queue attrs in order of first job)
   if (S.has_prop) {
     for (int32_t n = 0; n < N; ++n) kbg::res_add(S.prop_total, to_res(S.nodes_in[n].allocatable));
@@ -1895,6 +1963,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     for (int32_t q = 0; q < S.n_queues && exact_sums; ++q)
       for (int d = 0; d < 3; ++d)
         if (S.qr_sum[3 * (size_t)q + d] > (__int128)kExact) exact_sums = false;
+    prop_exact = exact_sums;
     if (exact_sums) {
       for (int32_t q = 0; q < S.n_queues; ++q) {
         E.qalloc[q] = Res{(double)(int64_t)S.qa_sum[3 * (size_t)q], (double)(int64_t)S.qa_sum[3 * (size_t)q + 1],
@@ -1943,7 +2012,23 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     }
   }
 
-  phase("engine+drf+prop");
+  phase("proportion");
+  drf_block();
+  S.jalloc_exact = prop_exact;
+  if (check) {
+    for (int32_t j = 0; j < S.n_jobs; ++j) {
+      int32_t r = 0;
+      Res a{};
+      for (auto [b, e] = job_tasks(j); b != e; ++b) {
+        if (ready_status(S.tstat_in[*b])) ++r;
+        if (allocated_status(S.tstat_in[*b])) kbg::res_add(a, S.treq[*b]);
+      }
+      if (r != E.jready[j]) return fail(KBG_E_INVALID, "internal: incremental ready count differs");
+      if (S.has_drf && std::memcmp(&a, &E.jalloc[j], sizeof(Res)) != 0)
+        return fail(KBG_E_INVALID, "internal: incremental drf allocation differs");
+    }
+  }
+  phase("drf");
   // ---- predicates preconditions
   const bool had_ghost = S.ghost;
   {
@@ -5406,7 +5491,53 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
   UpdateCtx U;
   U.seen.assign(S.n_nodes, 0);
   uint64_t kc[5] = {0, 0, 0, 0, 0}, kn[5] = {0, 0, 0, 0, 0};
+  // An event touches a handful of rows of task-, node- and job-indexed state
+  // spread over the whole session (cache misses, not work): the rows of the
+  // events ahead are requested before they are applied, in two hops (the
+  // task's row, then what it names). Prefetches only; the order of application
+  // is unchanged.
+  constexpr int32_t kAhead = 16;
+  auto task_of = [&](const kbg_event& e) -> int32_t {
+    const bool pod = e.kind == KBG_EV_POD_UPDATE || e.kind == KBG_EV_POD_DELETE;
+    return pod && e.task >= 0 && e.task < S.n_tasks ? e.task : -1;
+  };
+  auto ahead_far = [&](const kbg_event& e) {
+    if (const int32_t t = task_of(e); t >= 0) {
+      __builtin_prefetch(&S.tasks_in[t]);
+      __builtin_prefetch(&S.task_node[t]);
+      __builtin_prefetch(&S.task_live[t]);
+    } else if (e.kind == KBG_EV_POD_ADD && e.job >= 0 && e.job < S.n_jobs) {
+      __builtin_prefetch(&S.job_task_order[e.job]);
+    }
+    if (e.node >= 0 && e.node < S.n_nodes) {
+      __builtin_prefetch(&S.nodes_in[e.node]);
+      __builtin_prefetch(&S.node_key_order[e.node]);
+      __builtin_prefetch(&S.node_task_order[e.node]);
+    }
+  };
+  auto ahead_near = [&](const kbg_event& e) {
+    if (const int32_t t = task_of(e); t >= 0) {
+      const kbg_task& k = S.tasks_in[t];
+      __builtin_prefetch(&S.job_task_order[k.job]);
+      __builtin_prefetch(&S.canon[k.pod_key]);
+      __builtin_prefetch(&S.strs[k.node_name]);
+      const int32_t on = S.task_node[t];  // the node the task leaves
+      if (on >= 0 && on < S.n_nodes) {
+        __builtin_prefetch(&S.nodes_in[on]);
+        __builtin_prefetch(S.node_key_order[on].data());
+        __builtin_prefetch(S.node_task_order[on].data());
+      }
+    } else if (e.kind == KBG_EV_POD_ADD && e.job >= 0 && e.job < S.n_jobs) {
+      __builtin_prefetch(S.job_task_order[e.job].data() + S.job_task_order[e.job].size());
+    }
+    if (e.node >= 0 && e.node < S.n_nodes) {
+      __builtin_prefetch(S.node_key_order[e.node].data());
+      __builtin_prefetch(S.node_task_order[e.node].data() + S.node_task_order[e.node].size());
+    }
+  };
   for (int32_t i = 0; i < n; ++i) {
+    if (i + kAhead < n) ahead_far(ev[i + kAhead]);
+    if (i + kAhead / 2 < n) ahead_near(ev[i + kAhead / 2]);
     const uint64_t c0 = prof ? __builtin_readcyclecounter() : 0;
     kbg_status st = apply_event(S, U, ev[i]);
     if (st != KBG_OK) return st;
@@ -5426,7 +5557,10 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
   const bool had_masks = S.has_ports || S.has_aff;
   kbg_status st = KBG_OK;
   int outcome = DERIVE_OK;
+  S.upd_nodes = U.nodes;
+  S.upd_nodes_valid = true;
   if (!U.rebuild) st = derive_host(S, nullptr, &outcome);
+  S.upd_nodes_valid = false;
   if (st != KBG_OK) return st;
   phase("derive");
   if (U.rebuild || outcome == DERIVE_REBUILD) {

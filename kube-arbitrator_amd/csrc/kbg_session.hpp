@@ -264,6 +264,7 @@ struct Session {
   int64_t n_pinexact = 0;
   std::vector<__int128> qa_sum, qr_sum;                  // [queue * 3 + dim]
   bool prop_sums_ok = false;                             // the sums above are current
+  bool jalloc_exact = false;  // init.jalloc came from exact integer sums (an update may apply deltas)
   int32_t n_shapes = 0;
   std::vector<Res> treq;
   Res drf_total, prop_total;
@@ -293,6 +294,9 @@ struct Session {
   // ---- preempt / reclaim (preempt.go, reclaim.go, statement.go)
   std::vector<int32_t> nt_off, nt_task;       // victim candidates per node: session tasks Running there at
                                               // open, in NodeInfo.Tasks order
+  std::vector<int32_t> nt_off_buf, nt_task_buf;  // the next derive's copy (an update rebuilds by swap)
+  std::vector<int32_t> upd_nodes;             // nodes an update's events touched (kbg_session_update) ...
+  bool upd_nodes_valid = false;               // ... set for the derive that follows them
   std::vector<uint8_t> trun;                  // node-side copy still Running (an eviction makes it Releasing
                                               // for good: unevict's AddTask fails, node_info.go:101-106)
   std::vector<int32_t> task_node;             // node index of a task's NodeName (-1: not a session node)

@@ -60,6 +60,8 @@ extern "C" int32_t kbg_tool_update_nodes(const kbg_snapshot* snap, const kbg_opt
   for (int32_t i = 0; i < n; ++i)
     if (apply_event(S, U, ev[i]) != KBG_OK) return -3;
   const auto t1 = std::chrono::steady_clock::now();
+  S.upd_nodes = U.nodes;  // as kbg_session_update hands them to the derive
+  S.upd_nodes_valid = true;
   if (derive_host(S, nullptr, &outcome) != KBG_OK) return -4;
   if (getenv("KBG_TOOL_TIME"))
     fprintf(stderr, "[tool] %d events: apply %.3f ms, derive %.3f ms\n", n,

@@ -3,7 +3,9 @@ inputs after a sequence of cache events must equal a fresh snapshot of the
 cache after them — node Idle / Releasing / task count, and the pending lists
 in TaskOrderFn order (event_handlers.go:40-188, node_info.go:84-157). Runs
 through the developer tool library (kube-arbitrator_amd/tools/engine_bench.cpp),
-which drives the same ingest / apply_event / derive_host code as the library."""
+which drives the same ingest / apply_event / derive_host code as the library.
+KBG_CHECK_DERIVE makes each update's derive compare its incremental results
+(victim lists, ready counts, drf allocations) with a full recomputation."""
 import ctypes
 import os
 import subprocess
@@ -11,6 +13,8 @@ import subprocess
 import pytest
 
 from helpers import ROOT, run_oracle
+
+os.environ["KBG_CHECK_DERIVE"] = "1"  # read per derive, by the tool library only in this process
 
 PKG = os.path.join(ROOT, "kube-arbitrator_amd")
 TOOLS = os.path.join(PKG, "tools", "libkbg_tools.so")
