@@ -1637,11 +1637,31 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     const uint64_t* key = S.task_uid_key.data();
     const auto uid_less = [&](int32_t a, int32_t b) { return key[a] != key[b] ? key[a] < key[b] : uid(a) < uid(b); };
     std::vector<int32_t> news;
-    for (int32_t j : S.rank_dirty_jobs) {
+    // the jobs' lists and the first levels of their binary searches are
+    // requested a few jobs ahead (scattered rows: latency, not work)
+    const std::vector<int32_t>& dj = S.rank_dirty_jobs;
+    for (size_t k = 0; k < dj.size(); ++k) {
+      const int32_t j = dj[k];
+      if (k + 4 < dj.size()) {
+        __builtin_prefetch(&S.job_task_order[dj[k + 4]]);
+        __builtin_prefetch(&S.job_rank_order[dj[k + 4]]);
+      }
+      if (k + 2 < dj.size()) {
+        const std::vector<int32_t>& r2 = S.job_rank_order[dj[k + 2]];
+        __builtin_prefetch(S.job_task_order[dj[k + 2]].data());
+        if (!r2.empty()) {
+          const size_t h = r2.size() / 2;
+          __builtin_prefetch(&key[r2[h]]);
+          __builtin_prefetch(&key[r2[h / 2]]);
+          __builtin_prefetch(&key[r2[h + (r2.size() - h) / 2]]);
+        } else {
+          __builtin_prefetch(r2.data());
+        }
+      }
       news.clear();
       for (int32_t t : S.job_task_order[j])
         if (t >= T_old) news.push_back(t);
-      std::stable_sort(news.begin(), news.end(), uid_less);
+      if (news.size() > 1) std::stable_sort(news.begin(), news.end(), uid_less);
       std::vector<int32_t>& ro = S.job_rank_order[j];
       for (int32_t nt : news) {
         const auto it = std::upper_bound(ro.begin(), ro.end(), nt, uid_less);
