@@ -1383,13 +1383,13 @@ std::vector<int32_t> ranks_of(const Session& S, const std::vector<int32_t>& ids)
 
 // String id of `v` for an event: an existing content's canonical id, or a new entry.
 int32_t intern(Session& S, const char* v) {
-  const std::string key(v ? v : "");
+  const std::string_view key(v ? v : "");
   auto it = S.canon_of.find(key);
   if (it != S.canon_of.end()) return it->second;  // a canonical id is its own canonical id
   const int32_t id = (int32_t)S.strs.size();
-  S.strs.push_back(key);
+  S.strs.emplace_back(key);
   S.canon.push_back(id);
-  S.canon_of.emplace(key, id);
+  S.canon_of.emplace(S.strs.back(), id);
   return id;
 }
 

@@ -5,6 +5,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -16,6 +17,12 @@ namespace kbg {
 
 struct Res {
   double c = 0, m = 0, g = 0;
+};
+
+// string-keyed maps looked up by a caller's C string without building a std::string
+struct StrHash {
+  using is_transparent = void;
+  size_t operator()(std::string_view v) const noexcept { return std::hash<std::string_view>{}(v); }
 };
 
 // resource_info.go:142-146
@@ -373,7 +380,7 @@ struct Session {
   std::vector<int32_t> aff_gain_classes;
 
   // ---- resident session (kbg_session_update edits the inputs above)
-  std::unordered_map<std::string, int32_t> canon_of;  // string content -> canonical id
+  std::unordered_map<std::string, int32_t, StrHash, std::equal_to<>> canon_of;  // string content -> canonical id
   std::unordered_map<int32_t, int32_t> node_of;       // canonical node name -> node index
   std::vector<uint8_t> task_live;                     // 0: the pod was deleted (event_handlers.go deletePod)
   std::vector<std::vector<int32_t>> job_task_order;   // per job: its tasks in JobInfo.Tasks insertion order
