@@ -24,6 +24,12 @@ cpu_baseline= the kbref oracle on this host, CPU model stated: B-ref (1 thread),
               B-omp (the best of 16, 64 and every CPU the job may use, the
               sweep beside it), B-faithful (the per-call podLister walk, 20 s
               budget); C3 runs 20 s samples, C4 60 s samples
+parity      = the decision log of the LAST timed cycle of each mode, replayed
+              through the session (actions.replay) and hashed with the node /
+              job / queue states exactly as the parity tests do
+              (kbgpu.digest), against the oracle's digest of the same seeded
+              session committed under tests/golden/digest_c<config>.json (no
+              oracle runs here); a mismatch exits non-zero after the line
 --gpus N    = N ranks: under torchrun its WORLD_SIZE must be N; without a
               launcher bench.py starts the N rank processes itself
 N > 1       = ONE cluster with its node axis sharded over the N GPUs (SURVEY §8e,
@@ -202,6 +208,54 @@ def cpu_baseline(fx, label, threads=1, faithful=False, budget=0.0):
             "sample": f"{label}: {scope}, {secs:.2f} s, {st['predicate_calls']} predicate calls, kbref C++ port, {how}"}
 
 
+def golden_digest(cid):
+    """The oracle's digest of BASELINE config `cid` (tests/golden/make_digests.py), if committed."""
+    p = os.path.join(ROOT, "tests", "golden", f"digest_c{cid}.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)
+
+
+def log_sha(decs, evictions=()):
+    """sha256 of a cycle's raw decision log (task, node, kind, dispatched_at)
+    and evictions (task, by, action) as the library returned them."""
+    import hashlib
+    return hashlib.sha256(json.dumps([[list(d) for d in decs], [list(e) for e in evictions]],
+                                     separators=(",", ":")).encode()).hexdigest()
+
+
+def evictions_list(ssn):
+    """The session's evictions of the cycle as (task, by, action) index triples."""
+    from kbgpu import _abi
+    L = _abi.lib()
+    n = ctypes.c_int32(0)
+    _abi.check(L.kbg_evictions_get(ssn.handle, None, 0, ctypes.byref(n)))
+    buf = (_abi.kbg_eviction * max(1, n.value))()
+    _abi.check(L.kbg_evictions_get(ssn.handle, buf, n.value, ctypes.byref(n)))
+    return [(buf[i].task, buf[i].by, buf[i].action) for i in range(n.value)]
+
+
+def parity_verdict(cid, digests):
+    """{mode: digest} of the timed cycles against the golden digest of the
+    config: every mode must match it."""
+    from kbgpu.digest import digest_mismatches
+    ref = golden_digest(cid)
+    out = {"golden": f"tests/golden/digest_c{cid}.json" if ref else None,
+           "checked": "the last timed cycle of each mode: decision log (task, job, node, kind, dispatched_at), binds, "
+                      "evictions, node and job states bit-exact; drf / proportion shares within 1e-12 relative"}
+    ok = True
+    for mode, dg in digests.items():
+        if ref is None:
+            out[mode] = "no golden digest for this config"
+            continue
+        bad = digest_mismatches(ref, dg)
+        out[mode] = True if not bad else {"mismatch": bad}
+        ok = ok and not bad
+    out["ok"] = ok if ref is not None else None
+    return out
+
+
 def load_pmc(n_nodes, mode):
     """A kernel's per-launch PMC figures from the committed rocprofv3 summary
     of this same bench command (profiles/pmc_scan.json), if it matches the
@@ -285,8 +339,10 @@ def main():
     kdist.init(args.dist_backend)
 
     from kbgpu import _abi, actions, synth  # noqa: F401
-    from kbgpu.cache import cache_from_fixture
-    from kbgpu.fixture import fixture_tiers
+    from kbgpu.actions import decision_list, replay
+    from kbgpu.cache import FakeBinder, cache_from_fixture
+    from kbgpu.digest import digest_outputs
+    from kbgpu.fixture import fixture_tiers, session_output
     from kbgpu.framework import open_session
 
     cid = args.config
@@ -340,6 +396,15 @@ def main():
         if barrier:
             kdist.barrier()
         agg["stats"] = ssn.stats()
+        # parity of the last timed cycle: its log (still in `buf`, the
+        # session not reset since) replayed through the session's host
+        # objects, then digested with the library's node / job / queue states
+        decs = decision_list(buf, nout.value)
+        agg["log_sha256"] = log_sha(decs)
+        binder = FakeBinder()
+        cache.binder = binder
+        replay(ssn, decs, "allocate")
+        agg["digest"] = digest_outputs(session_output(ssn, binder.binds))
         agg["n_nodes"] = len(ssn.nodes)
         agg["pending"] = ssn.flat.pending_count
         agg["jobs"] = len(ssn.jobs)
@@ -503,6 +568,8 @@ def main():
         "decisions_per_cycle": decisions // max(1, args.steps),
         "open_ms": st.open_ms,
         "open_ms_first_in_process": open_ms_first,
+        "parity": dict(parity_verdict(cid, {"production": prod["digest"], "full_scan": full["digest"]}),
+                       log_sha256={"production": prod["log_sha256"], "full_scan": full["log_sha256"]}),
     }
     if world == 1 and not args.no_resident:
         line["resident_session"] = resident_bench(cache, fx, base_opts)
@@ -524,6 +591,9 @@ def main():
     if comm is not None:
         comm.close()
     kdist.shutdown()
+    if line["parity"]["ok"] is False:
+        log(f"bench: PARITY MISMATCH against {line['parity']['golden']}: {line['parity']}")
+        sys.exit(3)
 
 
 def resident_bench(cache, fx, base_opts, steps=5, churn=0.01, seed=5):
@@ -622,8 +692,11 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid, open_ms_
     from kbgpu import _abi
     from kbgpu import dist as kdist
     from kbgpu.api import RUNNING
-    from kbgpu.fixture import fixture_tiers
-    from kbgpu.framework import open_session
+    from kbgpu.actions import decision_list
+    from kbgpu.cache import FakeBinder
+    from kbgpu.digest import digest_outputs
+    from kbgpu.fixture import fixture_tiers, session_output
+    from kbgpu.framework import get_action, open_session
 
     L = _abi.lib()
     ssn = open_session(cache, fixture_tiers(fx), dict(base_opts))
@@ -669,6 +742,18 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid, open_ms_
     n_nodes = len(ssn.nodes)
     running = sum(1 for t in ssn.flat.task_objs if t.status == RUNNING)
     pending = ssn.flat.pending_all
+    # parity: the last timed cycle's raw log, then one more cycle on the reset
+    # session through the framework's actions (the same entry points, each
+    # action's decisions and evictions replayed through the session) whose
+    # log must be the timed one and whose digest must be the oracle's
+    timed_sha = log_sha(decision_list(buf, nout.value), evictions_list(ssn))
+    binder = FakeBinder()
+    cache.binder = binder
+    _abi.check(L.kbg_session_reset(ssn.handle))
+    for name in fx["actions"]:
+        get_action(name).execute(ssn)
+    verify_sha = log_sha(ssn.decisions, evictions_list(ssn))
+    digest = digest_outputs(session_output(ssn, binder.binds))
     ssn.close()
     elapsed, total = kdist.aggregate(elapsed_local, dec, sharded=world > 1)
     nodes_per_rank = n_nodes / max(1, world)
@@ -710,6 +795,15 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid, open_ms_
         "open_ms": st.open_ms,
         "open_ms_first_in_process": open_ms_first,
     }
+    par = parity_verdict(cid, {"cycle": digest})
+    par["timed_cycle_log_sha256"] = timed_sha
+    par["verify_cycle_log_equal"] = verify_sha == timed_sha
+    par["checked"] = ("the last timed cycle's raw log (decisions and evictions) equals that of one more cycle on the "
+                      "reset session through the framework's actions, whose outputs (" + par["checked"] + ") match "
+                      "the golden digest")
+    if not par["verify_cycle_log_equal"]:
+        par["ok"] = False
+    line["parity"] = par
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(fx, f"C{cid} ({', '.join(fx['actions'])})")
     if rank == 0:
@@ -717,6 +811,9 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid, open_ms_
     if comm is not None:
         comm.close()
     kdist.shutdown()
+    if par["ok"] is False:
+        log(f"bench: PARITY MISMATCH: {par}")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

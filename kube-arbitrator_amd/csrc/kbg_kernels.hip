@@ -225,6 +225,13 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g0 = blockIdx.x * kFfRows;
+  if (a.w_hi <= a.w_lo) {  // no words (a session without nodes): empty lists, no table or mask read
+    if (wave == 0 && lane < kFfRows && g0 + lane < a.G) {
+      a.down[g0 + lane] = 0u;
+      if (a.avail) a.avail[g0 + lane] = 0u;
+    }
+    return;
+  }
   if (wave == 0 && lane < kFfRows) {
     const TaskRec tr = reinterpret_cast<const TaskRec*>(a.up)[min(g0 + lane, a.G - 1)];  // past G: never written
     s_req[lane][0] = tr.req[0];

@@ -765,7 +765,9 @@ kbg_status push_mask_deltas(Session& S) {
       S.h_mdeltas[k] = kbg::MaskDelta{idx, 0u, S.h_class_mask[idx]};
       S.mask_dirty_flag[idx] = 0;
     }
-    HIP_TRY(kbg::launch_mask_apply(S.d_class_mask, dev_ptr(S, S.h_mdeltas), cnt, S.stream));  // read in place
+    const kbg::MaskDelta* md = dev_ptr(S, S.h_mdeltas);
+    if (!md) return fail(KBG_E_HIP, "hipHostGetDevicePointer of the mask-delta buffer failed");
+    HIP_TRY(kbg::launch_mask_apply(S.d_class_mask, md, cnt, S.stream));  // read in place
     if ((st = stage_release(S)) != KBG_OK) return st;
     m += cnt;
   }
@@ -2356,6 +2358,7 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   }
   if ((st = host_alloc((void**)&S.h_deltas, (size_t)S.K * sizeof(kbg::NodeDelta)))) return st;
   S.h_deltas_dev = dev_ptr(S, S.h_deltas);
+  if (!S.h_deltas_dev) return fail(KBG_E_HIP, "hipHostGetDevicePointer of the node-delta buffer failed");
   if ((st = upload_nodes(S))) return st;
   phase("device alloc+nodes");
 
@@ -2673,10 +2676,12 @@ kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, c
     fq[i] = kbg::FitQuery{S.task_class[le.task], le.node < 0 ? N : le.node + (le.kind == KBG_KIND_PIPELINE ? 1 : 0),
                           le.before, le.node, {r.c, r.m, r.g}};
   }
+  int32_t* fit_out = dev_ptr(S, S.fit_out);
+  if (!fit_out) return fail(KBG_E_HIP, "hipHostGetDevicePointer of the FitError buffer failed");
   HIP_TRY(hipMemcpyAsync(S.fit_d, S.fit_h, bytes, hipMemcpyHostToDevice, S.stream));
   kbg::FitArgs a{S.d_nodes.idle_cpu, soa_stride(S), S.W, S.d_class_mask, (const int32_t*)S.fit_d,
                  (const int32_t*)(S.fit_d + o_hk), (const double*)(S.fit_d + o_hold),
-                 (const kbg::FitQuery*)(S.fit_d + o_q), Q, S.pred_active ? 1 : 0, dev_ptr(S, S.fit_out)};
+                 (const kbg::FitQuery*)(S.fit_d + o_q), Q, S.pred_active ? 1 : 0, fit_out};
   HIP_TRY(kbg::launch_fitdelta(a, S.stream));
   HIP_TRY(hipStreamSynchronize(S.stream));
   for (int32_t i = 0; i < Q; ++i) {
@@ -2696,7 +2701,7 @@ kbg_status compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, 
   for (int32_t j = 0; j < S.n_jobs; ++j)
     if (S.committed_ready[j] < S.jobs_in[j].min_available) jobs.push_back(j);
   if (jobs.empty()) return KBG_OK;
-  static const bool host_only = getenv("KBG_HOST_FITDELTA") != nullptr;
+  const bool host_only = getenv("KBG_HOST_FITDELTA") != nullptr;  // read per cycle (A/B parity tests)
   if (S.stream && !S.comm && !S.has_ports && !S.has_aff && !S.any_nil && !host_only)
     return fit_deltas_device(S, dec, dec_old, last, jobs);
   std::sort(jobs.begin(), jobs.end(), [&](int32_t a, int32_t b) { return last[a].before > last[b].before; });
@@ -3380,7 +3385,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   // did, rescans the rest of its batch. Full-scan mode rescans (every task
   // evaluation scans the table); pod affinity (gains cut) and
   // sharded sessions too.
-  static const bool no_reuse = getenv("KBG_NO_CUT_REUSE") != nullptr;
+  const bool no_reuse = getenv("KBG_NO_CUT_REUSE") != nullptr;  // read per cycle (A/B parity tests)
   const bool reuse_ok = !S.opts.full_scan && !S.comm && !S.has_aff && !no_reuse;
   bool reuse = false;
   // From the first cut on (the contended part of the cycle) every batch
@@ -5828,7 +5833,12 @@ kbg_status kbg_session_update(kbg_session* s, const kbg_event* events, int32_t n
   if (n < 0 || (n > 0 && !events)) return fail(KBG_E_INVALID, "events");
   kbg_status st;
   try {
-    if ((st = update_precheck(S, events, n)) != KBG_OK) return st;  // refused: nothing changed
+    st = update_precheck(S, events, n);
+  } catch (const std::bad_alloc&) {
+    return fail(KBG_E_NOMEM, "host allocation failed");  // before the first event: the session is unchanged
+  }
+  if (st != KBG_OK) return st;  // refused: nothing changed
+  try {
     st = session_update(S, events, n);
   } catch (const std::bad_alloc&) {
     st = fail(KBG_E_NOMEM, "host allocation failed");

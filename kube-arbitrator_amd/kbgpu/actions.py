@@ -25,6 +25,38 @@ class ActionResult:
 AllocateResult = ActionResult
 
 
+def decision_list(buf, n):
+    """The first n kbg_decision records as (task, node, kind, dispatched_at)."""
+    return [(buf[i].task, buf[i].node, buf[i].kind, buf[i].dispatched_at) for i in range(n)]
+
+
+def replay(ssn, decs, action, evicting=False):
+    """Replays the new part of the cycle's decision log `decs` (the whole log
+    of the cycle so far, as the library returns it) through the session in
+    reference order: ssn.Allocate / ssn.Pipeline per decision, then
+    ssn.dispatch for every task the decision's JobReady check bound
+    (session.go:205-316)."""
+    start = len(ssn.decisions)
+    tasks = ssn.flat.task_objs
+    names = ssn.flat.node_names
+    bound_at = {}
+    for t, _, _, disp in decs:
+        if disp >= start:
+            bound_at.setdefault(disp, []).append(tasks[t])
+    for i in range(start, len(decs)):
+        t, nd, kind, _ = decs[i]
+        if kind == _abi.KIND_ALLOCATE:
+            ssn.allocate(tasks[t], names[nd])
+        elif evicting:
+            ssn.pipeline_replay(tasks[t], names[nd])
+        else:
+            ssn.pipeline(tasks[t], names[nd])
+        for bt in bound_at.pop(i, []):
+            ssn.dispatch(bt)
+    ssn.decisions = decs
+    ssn.action_of.extend([action] * (len(decs) - start))
+
+
 class _DeviceAction:
     _entry = None
     _evicting = False
@@ -44,26 +76,8 @@ class _DeviceAction:
         err = L.kbg_last_error().decode() if code != _abi.KBG_OK else ""
         if code not in (_abi.KBG_OK, _abi.KBG_E_REF_PANIC):
             _abi.check(code)
-        decs = [(buf[i].task, buf[i].node, buf[i].kind, buf[i].dispatched_at) for i in range(n.value)]
-        start = len(ssn.decisions)
-        tasks = ssn.flat.task_objs
-        names = ssn.flat.node_names
-        bound_at = {}
-        for t, _, _, disp in decs:
-            if disp >= start:
-                bound_at.setdefault(disp, []).append(tasks[t])
-        for i in range(start, len(decs)):
-            t, nd, kind, _ = decs[i]
-            if kind == _abi.KIND_ALLOCATE:
-                ssn.allocate(tasks[t], names[nd])
-            elif self._evicting:
-                ssn.pipeline_replay(tasks[t], names[nd])
-            else:
-                ssn.pipeline(tasks[t], names[nd])
-            for bt in bound_at.pop(i, []):
-                ssn.dispatch(bt)
-        ssn.decisions = decs
-        ssn.action_of.extend([self.name()] * (len(decs) - start))
+        decs = decision_list(buf, n.value)
+        replay(ssn, decs, self.name(), self._evicting)
         result = ActionResult(decs, _abi.STATUS_NAMES[code], err)
         if code == _abi.KBG_E_REF_PANIC:
             raise _abi.KbgError(code, err)

@@ -79,8 +79,16 @@ def run_fixture(fx, options=None):
         if e.status != "ref_panic":
             raise
         return {"status": "ref_panic", "error": str(e)}, ssn
+    return session_output(ssn, binder.binds, status), ssn
+
+
+def session_output(ssn, binds, status="ok"):
+    """The session's outputs in the oracle's output schema, after its actions
+    have been replayed through it (actions.replay): the decision log, the
+    binds the fake binder recorded, evictions, job / queue / node states (the
+    latter three read from the library)."""
     tasks, names = ssn.flat.task_objs, ssn.flat.node_names
-    out = {"status": status, "decisions": [], "binds": dict(binder.binds), "jobs": [], "queues": [], "nodes": [],
+    out = {"status": status, "decisions": [], "binds": dict(binds), "jobs": [], "queues": [], "nodes": [],
            "evictions": [{"task": t.uid, "by": by.uid, "action": act} for t, by, act in ssn.evictions]}
     for (t, nd, kind, disp), act in zip(ssn.decisions, ssn.action_of):
         d = {"task": tasks[t].uid, "job": tasks[t].job, "node": names[nd],
@@ -110,4 +118,4 @@ def run_fixture(fx, options=None):
         out["nodes"].append({"name": n.name, "idle": [st.idle.milli_cpu, st.idle.memory, st.idle.milli_gpu],
                              "releasing": [st.releasing.milli_cpu, st.releasing.memory, st.releasing.milli_gpu],
                              "ntasks": st.num_tasks})
-    return out, ssn
+    return out

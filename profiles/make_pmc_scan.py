@@ -56,13 +56,13 @@ def main():
     out.update(scan_modes(c3))
     if c5 and "kbg_victim_kernel" in c5["kernels"]:
         out["victim"] = dict(section(c5["kernels"]["kbg_victim_kernel"]), kernel="kbg_victim_kernel", n_nodes=10000)
-    out["source"] = (f"{', '.join(srcs[c] for c in sorted(srcs))} (profiles/summarize_pmc.py over gpurun_pmc.sh): rocprofv3 "
+    out["source"] = (f"{', '.join(srcs[c] for c in sorted(srcs))} (profiles/summarize_pmc.py over scripts/gpurun/pmc.sh): rocprofv3 "
                      "--kernel-trace --stats, then separate --pmc passes (FETCH_SIZE / WRITE_SIZE / "
                      "TCC_HIT_sum+TCC_MISS_sum / SQ_INSTS_VALU,SQ_WAVES,... + GRBM_GUI_ACTIVE) of `python3 bench.py "
                      "--config {3,5} --steps 3 --warmup 1 --no-cpu-baseline --no-resident`; read = 2 x FETCH_SIZE "
                      "(gfx950 correction, MI355X_MICROARCH.md HBM section); FETCH/WRITE count Infinity-Cache hits too")
     if c4:
-        out["by_nodes"] = {"20000": dict(scan_modes(c4), source=f"{srcs[4]} (gpurun_pmc.sh CFGS=4, same "
+        out["by_nodes"] = {"20000": dict(scan_modes(c4), source=f"{srcs[4]} (scripts/gpurun/pmc.sh CFGS=4, same "
                                                                 "passes as C3)")}
     json.dump(out, sys.stdout, indent=1)
     print()

@@ -1,4 +1,4 @@
-"""Summarise a gpurun_pmc.sh session (rocprofv3 kernel trace + separate PMC
+"""Summarise a scripts/gpurun/pmc.sh session (rocprofv3 kernel trace + separate PMC
 passes of one bench command) per kernel.
 
 Usage: python profiles/summarize_pmc.py <session dir> <config> > summary.json
@@ -47,7 +47,7 @@ def rows(path):
 
 def main():
     d, cfg = sys.argv[1], sys.argv[2]
-    out = {"source": f"gpurun_pmc.sh: rocprofv3 --kernel-trace --stats, then one --pmc pass per counter group, of "
+    out = {"source": f"scripts/gpurun/pmc.sh: rocprofv3 --kernel-trace --stats, then one --pmc pass per counter group, of "
                      f"`python3 bench.py --config {cfg} --steps 3 --warmup 1 --no-cpu-baseline --no-resident`",
            "config": int(cfg), "kernels": {}}
     ks = out["kernels"]

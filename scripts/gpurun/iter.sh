@@ -8,7 +8,7 @@ mkdir -p $O
 cd $R
 timeout -k 10 ${TT:-600} python -u -m pytest ${TESTS:-tests/test_parity_gpu.py tests/test_scale_gpu.py} ${K:+-k "$K"} -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
-if [ -z "$NO_TRACE" ]; then bash gpurun_trace.sh; fi
+if [ -z "$NO_TRACE" ]; then bash $R/scripts/gpurun/trace.sh; fi
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS} > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
 python -c "
 import json; d=json.load(open('$O/bench.json'))

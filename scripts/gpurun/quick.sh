@@ -7,4 +7,4 @@ mkdir -p $O
 cd $R
 timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_parity_gpu.py} -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_quick.log 2>&1 || { tail -40 $O/pytest_quick.log; exit 1; }
 tail -3 $O/pytest_quick.log
-bash gpurun_trace.sh
+bash $R/scripts/gpurun/trace.sh

@@ -18,6 +18,6 @@ if [ -z "$NO_BENCH" ]; then
   cat $O/bench.json
 fi
 if [ -n "$PMC" ]; then
-  CFGS=${CFGS:-3} bash gpurun_pmc.sh
+  CFGS=${CFGS:-3} bash $R/scripts/gpurun/pmc.sh
 fi
 echo R3_DONE

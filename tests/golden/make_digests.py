@@ -13,6 +13,9 @@ digest_c3.json        synth.config_fixture(3): BASELINE C3 as SURVEY §8(d) has 
 digest_c3_churn.json  C3 then 3 resident-session churn rounds (helpers.churn_chain):
                       one digest per snapshot S0 .. S3
 digest_c4_churn.json  the same over C4
+digest_c{1,2,5}.json  BASELINE C1, C2 and C5 (C5: reclaim, allocate, backfill, preempt
+                      on the contended 10k-node cluster); bench.py checks its last
+                      timed cycle against digest_c<config>.json
 """
 import json
 import os
@@ -33,6 +36,9 @@ SESSIONS = {
     "c4": ("synth.config_fixture(4)", lambda: synth.config_fixture(4)),
     "saturated": ("synth.saturated_config()", lambda: synth.saturated_config()),
     "c3": ("synth.config_fixture(3)", lambda: synth.config_fixture(3)),
+    "c1": ("synth.config_fixture(1)", lambda: synth.config_fixture(1)),
+    "c2": ("synth.config_fixture(2)", lambda: synth.config_fixture(2)),
+    "c5": ("synth.config_fixture(5)", lambda: synth.config_fixture(5)),
 }
 CHAINS = {  # name: (generator text, fixture, churn seed, rounds)
     "c3_churn": ("helpers.churn_chain(synth.config_fixture(3), 3, 3)", lambda: synth.config_fixture(3), 3, 3),

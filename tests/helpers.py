@@ -1,13 +1,16 @@
 """Test helpers: run the kbref oracle (the checker) and compare outputs."""
 import json
-import math
 import os
 import subprocess
+import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE = os.path.join(ROOT, "oracle", "build", "kbref")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, os.path.join(ROOT, "kube-arbitrator_amd"))
+
+from kbgpu.digest import close, digest_mismatches, digest_outputs  # noqa: E402,F401
 
 
 def ensure_oracle():
@@ -31,12 +34,6 @@ def run_oracle(fx, *flags):
 def load_golden(name):
     with open(os.path.join(GOLDEN, name)) as f:
         return json.load(f)
-
-
-def close(a, b, rel=1e-12):
-    if a == b:
-        return True
-    return abs(a - b) <= rel * max(abs(a), abs(b))
 
 
 def compare_outputs(ref, got):
@@ -71,47 +68,10 @@ def compare_outputs(ref, got):
         assert a["idle"] == b["idle"] and a["releasing"] == b["releasing"], (a, b)
 
 
-def digest_outputs(out):
-    """Size-independent summary of a run in the oracle's output schema: sha256
-    of the canonical decision log, node states and job states (bit-exact
-    fields), plus the drf / proportion shares themselves (compared within
-    1e-12 relative). Used for sessions too large to keep the oracle's whole
-    output under tests/golden (C4)."""
-    import hashlib
-
-    def h(x):
-        return hashlib.sha256(json.dumps(x, separators=(",", ":")).encode()).hexdigest()
-
-    d = {"status": out["status"]}
-    if out["status"] != "ok":
-        return d
-    d["n_decisions"] = len(out["decisions"])
-    d["decisions"] = h([[x["task"], x["job"], x["node"], x["kind"], x["dispatched_at"], x.get("action", "")]
-                        for x in out["decisions"]])
-    d["binds"] = h(sorted(out["binds"].items()))
-    d["evictions"] = h(out.get("evictions", []))
-    def f(v):  # the oracle prints integral doubles without a fraction: hash every resource as a float
-        return [float(x) for x in v]
-
-    d["nodes"] = h([[n["name"], f(n["idle"]), f(n["releasing"]), n["ntasks"]] for n in out["nodes"]])
-    d["jobs"] = h([[j["uid"], j["ready_num"], j["ready"], f(j["allocated"]), None if j["ready"] else j["fit_error"]]
-                   for j in out["jobs"]])
-    d["drf_shares"] = [j["drf_share"] for j in out["jobs"] if "drf_share" in j]
-    d["queues"] = sorted(([q["uid"], q["share"], q["deserved"], q["allocated"], q["request"]] for q in out["queues"]))
-    return d
-
-
 def compare_digests(ref, got):
-    assert got["status"] == ref["status"]
-    if ref["status"] != "ok":
-        return
-    for k in ("n_decisions", "decisions", "binds", "evictions", "nodes", "jobs"):
-        assert got[k] == ref[k], k
-    assert len(got["drf_shares"]) == len(ref["drf_shares"])
-    assert all(close(a, b) for a, b in zip(ref["drf_shares"], got["drf_shares"]))
-    assert [q[0] for q in got["queues"]] == [q[0] for q in ref["queues"]]
-    for a, b in zip(ref["queues"], got["queues"]):
-        assert close(a[1], b[1]) and all(close(x, y) for u, v in zip(a[2:], b[2:]) for x, y in zip(u, v)), (a, b)
+    """Digests (kbgpu.digest.digest_outputs) of sessions too large to keep the
+    oracle's whole output under tests/golden (C3, C4, C5)."""
+    assert not digest_mismatches(ref, got), digest_mismatches(ref, got)
 
 
 def churn_chain(fx0, seed, rounds, run):

@@ -76,3 +76,21 @@ def test_threaded_oracle_matches_single_thread():
             o.pop("stats", None)
             outs.append(o)
         assert outs[0] == outs[1] == outs[2], fx["name"]
+
+
+@pytest.mark.parametrize("cid", [1, 2])
+def test_golden_digests_reproduce(cid):
+    """The committed digests that bench.py checks its timed cycles against
+    (tests/golden/digest_c<cid>.json) are the oracle's digest of the seeded
+    config, and the comparison bench.py uses accepts them and rejects a
+    perturbed one."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "kube-arbitrator_amd"))
+    from kbgpu import synth
+    from kbgpu.digest import digest_mismatches, digest_outputs
+    with open(os.path.join(GOLDEN, f"digest_c{cid}.json")) as f:
+        ref = json.load(f)
+    got = digest_outputs(run_oracle(synth.config_fixture(cid)))
+    assert digest_mismatches(ref, got) == []
+    bad = dict(got, decisions="0" * 64, drf_shares=[x * (1 + 1e-9) + 1e-300 for x in got["drf_shares"]])
+    assert digest_mismatches(ref, bad) == ["decisions", "drf_shares"]

@@ -97,6 +97,23 @@ def test_config_parity(cid):
     ssn.close()
 
 
+@pytest.mark.parametrize("actions", [None, ["reclaim", "allocate", "backfill", "preempt"]])
+@pytest.mark.parametrize("full_scan", [0, 1])
+def test_zero_nodes(actions, full_scan):
+    """A session without nodes and with pending tasks: every task fails with
+    "0 nodes are available" (job_info.go:329-358). The fused kernel gets no
+    words to walk and must read neither the node table nor the class masks."""
+    fx = synth.config_fixture(1)
+    fx["nodes"] = []
+    if actions:
+        fx["actions"] = actions
+    got, ssn = run_fixture(fx, {"full_scan": full_scan})
+    compare_outputs(run_oracle(fx), got)
+    assert got["decisions"] == []
+    if ssn:
+        ssn.close()
+
+
 @pytest.mark.parametrize("opts", [
     {"batch_tasks": 1, "candidates": 1},
     {"batch_tasks": 7, "candidates": 2},
@@ -149,6 +166,10 @@ def test_config3_full_parity(full_scan):
     ssn.close()
     compare_digests(ref, digest_outputs(got))
     assert st.task_evaluations == ref["evaluated"]
+    if not full_scan:
+        # grouped mode resolved re-predicted tasks against the stage's lists
+        # after cuts (cut-time list reuse) instead of rescanning
+        assert st.reused_batches > 0, st.reused_batches
 
 
 def _open(fx, opts=None):

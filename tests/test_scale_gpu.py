@@ -38,6 +38,22 @@ def test_saturated_parity(saturated, opts):
         assert st.mispredictions > 0, st.mispredictions
 
 
+@pytest.mark.parametrize("env", ["KBG_NO_CUT_REUSE", "KBG_HOST_FITDELTA"])
+def test_saturated_ab_paths(saturated, env, monkeypatch):
+    """The saturated session with the cut-time list reuse turned off (every
+    cut rescans) and with FitError counted on the host instead of by
+    kbg_fitdelta_kernel: the same digest as the default paths, so parity does
+    not hinge on either."""
+    ref = load_golden("digest_saturated.json")
+    monkeypatch.setenv(env, "1")
+    got, ssn = run_fixture(saturated)
+    st = ssn.stats()
+    ssn.close()
+    compare_digests(ref, digest_outputs(got))
+    if env == "KBG_NO_CUT_REUSE":
+        assert st.reused_batches == 0, st.reused_batches
+
+
 @pytest.mark.slow
 def test_config4_parity():
     ref = load_golden("digest_c4.json")
