@@ -496,7 +496,7 @@ kbg_status copy_soa(Session& S, const kbg::NodeSoA& dst, const kbg::NodeSoA& src
 // (coherent), so a kernel's stores are on the host when its completion event
 // fires and the host's stores are seen by the next launch.
 kbg_status host_alloc(void** p, size_t bytes) {
-  HIP_TRY(hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_TRY(hipHostMalloc(p, std::max<size_t>(bytes, 64), hipHostMallocMapped | hipHostMallocCoherent));  // never 0 B
   return KBG_OK;
 }
 // The device address of such memory (the host address itself under unified
@@ -3809,8 +3809,8 @@ struct RcclIO final : ShardIO {
     d = nullptr;
     h = nullptr;
     cap = 0;
-    HIP_TRY(hipMalloc((void**)&d, n * 4));
-    HIP_TRY(hipHostMalloc((void**)&h, n * 4, hipHostMallocDefault));
+    HIP_TRY(hipMalloc((void**)&d, std::max<size_t>((size_t)n * 4, 64)));
+    HIP_TRY(hipHostMalloc((void**)&h, std::max<size_t>((size_t)n * 4, 64), hipHostMallocDefault));
     cap = n;
     return KBG_OK;
   }
@@ -4461,7 +4461,7 @@ kbg_status vt_setup(Session& S) {
     S.vt_allocs.assign(S.d_allocs.begin() + a0, S.d_allocs.end());
     HIP_TRY(hipMemset(S.d_vbits, 0, 2 * (size_t)S.W32 * sizeof(uint32_t)));  // other ranks' words stay 0
     if (!S.h_vbits) {
-      HIP_TRY(hipHostMalloc((void**)&S.h_vbits, 2 * (size_t)S.W32 * sizeof(uint32_t),
+      HIP_TRY(hipHostMalloc((void**)&S.h_vbits, std::max<size_t>(2 * (size_t)S.W32 * sizeof(uint32_t), 64),  // W32 = 0: no nodes
                             hipHostMallocCoherent | hipHostMallocMapped));
       HIP_TRY(hipHostGetDevicePointer((void**)&S.h_vbits_dev, S.h_vbits, 0));
     }
@@ -4522,7 +4522,7 @@ kbg_status vt_setup(Session& S) {
     if (S.c_run_pinned) (void)hipHostFree(S.c_run_pinned);
     S.c_run_pinned = nullptr;
     S.c_run_pinned_cap = 0;
-    HIP_TRY(hipHostMalloc((void**)&S.c_run_pinned, P, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void**)&S.c_run_pinned, std::max<size_t>(P, 64), hipHostMallocDefault));
     S.c_run_pinned_cap = P;
   }
   for (size_t k = 0; k < S.nt_task.size(); ++k) S.c_run_pinned[k] = S.trun[S.nt_task[k]];
