@@ -21,8 +21,9 @@ cycle_roofline_8d = BASELINE's north-star form: the same bytes per allocate
 scan_kernel = the dominant kernel against its physical ceilings: PMC HBM bytes
               and PMC VALU wave instructions per launch over its HIP-event time
 cpu_baseline= the kbref oracle on this host, CPU model stated: B-ref (1 thread),
-              B-omp (the best of 16, 64 and every CPU the job may use, the
-              sweep beside it), B-faithful (the per-call podLister walk, 20 s
+              B-omp (the best of 4 ... 64 threads and every CPU the job can
+              use — affinity mask capped by the cgroup quota — the sweep
+              beside it), B-faithful (the per-call podLister walk, 20 s
               budget); C3 runs 20 s samples, C4 60 s samples
 parity      = the decision log of the LAST timed cycle of each mode, replayed
               through the session (actions.replay) and hashed with the node /
@@ -105,11 +106,40 @@ def job_cpus():
     return list(range(os.cpu_count() or 1))
 
 
-def omp_sweep():
-    """B-omp thread counts: 16, 64 and every CPU the job may run on (SURVEY
-    §8(d): the node loop parallelised over all host cores, stated)."""
+def cpu_quota():
+    """The CPU time the job's cgroup may use, in CPUs (cgroup v2 cpu.max or v1
+    cfs quota / period), None when unlimited. A shared box can show every host
+    CPU in the affinity mask while a quota caps the job far below it: threads
+    past the quota only time-slice."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def usable_cpus():
+    """CPUs the job can run threads on at once: its affinity mask, capped by the cgroup quota."""
     n = len(job_cpus())
-    return sorted({t for t in (16, 64) if t < n} | {n})
+    q = cpu_quota()
+    return max(1, min(n, int(q))) if q else n
+
+
+def omp_sweep():
+    """B-omp thread counts (the node loop parallelised over all
+    host cores, stated): 4, 8, 16, 32, 64 and every CPU the job can use, none
+    above that (past the cgroup quota threads only time-slice)."""
+    n = usable_cpus()
+    return sorted({t for t in (4, 8, 16, 32, 64) if t < n} | {n})
 
 
 def spawn_ranks(n):
@@ -166,8 +196,9 @@ def cpu_baseline(fx, label, threads=1, faithful=False, budget=0.0):
     """kbref oracle on the same workload (kind "port"), SURVEY §8(d):
     B-ref     1 thread (the Go allocate loop is single-goroutine), podLister
               walk elided under the proven-true condition;
-    B-omp     `threads` threads evaluating each task's node loop in parallel
-              blocks (FitDelta map built once per job), the fair multi-core baseline;
+    B-omp     `threads` threads evaluating each task's node loop (a persistent
+              team, 64-node chunks in node order, stopping at the first fit),
+              the fair multi-core baseline;
     B-faithful 1 thread replaying the podLister's per-call O(allocated pods)
               walk of predicates.go:70-89 (F7), under a wall-clock budget.
     All produce the decisions the device path makes (tested). With a budget
@@ -188,10 +219,7 @@ def cpu_baseline(fx, label, threads=1, faithful=False, budget=0.0):
                 cmd.append("--faithful")
             if budget:
                 cmd += ["--budget", str(budget)]
-            # the threads spin between the per-task node loops instead of sleeping
-            # (a sleeping team costs more to wake than a 1k-node loop takes)
-            env = dict(os.environ, OMP_WAIT_POLICY="active") if threads > 1 else None
-            subprocess.run(cmd + [src, "-o", dst], check=True, timeout=max(600, 3 * budget), env=env)
+            subprocess.run(cmd + [src, "-o", dst], check=True, timeout=max(600, 3 * budget))
             with open(dst) as f:
                 out = json.load(f)
     except (subprocess.CalledProcessError, subprocess.TimeoutExpired, OSError, ValueError) as e:
@@ -200,11 +228,14 @@ def cpu_baseline(fx, label, threads=1, faithful=False, budget=0.0):
     st = out["stats"]
     secs, n = st["seconds"], st["decisions"]
     how = ("B-faithful: 1 thread, podLister walk per predicate call" if faithful else
-           "B-ref: 1 thread" if threads == 1 else f"B-omp: {threads} threads (OpenMP node loop, OMP_WAIT_POLICY=active)")
+           "B-ref: 1 thread" if threads == 1 else
+           f"B-omp: {threads} threads (one persistent team for the run; each task's node loop in 64-node chunks "
+           f"handed out in node order, stopping at the first fit)")
     scope = (f"first {n} placements within a {budget:.0f} s budget" if out["status"] == "budget"
              else f"one full cycle ({n} placements)")
     return {"value": n / secs if secs > 0 else 0.0, "unit": "placements/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(), "job_cpus": len(job_cpus()),
+            "cgroup_cpu_quota": cpu_quota(),
             "sample": f"{label}: {scope}, {secs:.2f} s, {st['predicate_calls']} predicate calls, kbref C++ port, {how}"}
 
 

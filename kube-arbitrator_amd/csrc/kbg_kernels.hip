@@ -26,6 +26,30 @@
 
 namespace kbg {
 
+// Diagnostic build only (tools/libkbg_tools_stamps.so, -DKBG_FF_STAMPS): the
+// fused kernel records the global 100 MHz clock at its phase boundaries, per
+// workgroup, into a buffer nothing else reads. The shipped library has no
+// stamps (FF_STAMP expands to nothing).
+#ifdef KBG_FF_STAMPS
+constexpr int kStampWG = 8192, kStampSlots = 8;
+__device__ unsigned long long kbg_ff_stamps[kStampWG][kStampSlots];
+#define FF_STAMP(slot)                                                                   \
+  do {                                                                                   \
+    unsigned long long t_;                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < kStampWG) kbg_ff_stamps[blockIdx.x][slot] = t_; \
+  } while (0)
+hipError_t read_ff_stamps(unsigned long long* out, int n_wg) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(kbg_ff_stamps), (size_t)n_wg * kStampSlots * 8, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define FF_STAMP(slot) \
+  do {                 \
+  } while (0)
+#endif
+
 __device__ __forceinline__ bool le(double r, double a, double mn) {
   // (r < a || |a - r| < min)  — resource_info.go:142-146, one dimension
   return r < a || fabs(a - r) < mn;
@@ -225,6 +249,7 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g0 = blockIdx.x * kFfRows;
+  FF_STAMP(0);
   if (a.w_hi <= a.w_lo) {  // no words (a session without nodes): empty lists, no table or mask read
     if (wave == 0 && lane < kFfRows && g0 + lane < a.G) {
       a.down[g0 + lane] = 0u;
@@ -289,6 +314,7 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
   Word cur;
   load_word(min(a.w_lo + wave, w_last), cur);
   __syncthreads();
+  FF_STAMP(1);
   const int cls_l = s_cls[lane & (kFfRows - 1)];
   const int flags_l = s_flags[lane & (kFfRows - 1)];
   // rounds are kFfMaxRound (a multiple of kFfWaves) words apart, so a wave's
@@ -331,7 +357,9 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
       cur = nxt;
       lane_mw = nxt_mw;
     }
+    if (r0 == a.w_lo) FF_STAMP(2);
     __syncthreads();
+    if (r0 == a.w_lo) FF_STAMP(3);
     // Extraction, phase 1: wave j places row j's words of the round. Lane k
     // holds word k's node count; the exclusive prefix sum over lanes (one
     // ballot + mbcnt per bit of the count) is the list position of the
@@ -365,6 +393,7 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
       s_done[wave] = done ? 1u : 0u;
     }
     __syncthreads();
+    if (r0 == a.w_lo) FF_STAMP(4);
     // phase 2: every (row, placed word) pair is one wave-wide append (lane =
     // node, position = word start + mbcnt), spread over all the waves so a
     // long list is not walked by one wave alone
@@ -383,6 +412,7 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
               (uint32_t)((r0 + k) * 64 + lane) | (((mi >> lane) & 1ull) ? 0u : kCandPipelineBit);
       }
     }
+    if (r0 == a.w_lo) FF_STAMP(5);
     if (r0 + kFfMaxRound >= a.w_hi) break;  // the last round: no second barrier
     __syncthreads();  // the round's masks and positions are read
     if (EARLY_EXIT) {  // every row's list is full: the same decision in every wave
@@ -394,6 +424,7 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
     a.down[g] = (found < want ? found : want) | (found > want ? kCountIncompleteBit : 0u);
     if (a.avail) a.avail[g] = found ? a.avail_bit : 0u;
   }
+  FF_STAMP(6);
 }
 
 hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t stream, hipEvent_t start,

@@ -453,3 +453,35 @@ extern "C" double kbg_tool_firstfit_bench(const kbg_snapshot* snap, const kbg_op
   std::sort(us.begin(), us.end());
   return us[us.size() / 2];
 }
+
+#ifdef KBG_FF_STAMPS
+namespace kbg {
+hipError_t read_ff_stamps(unsigned long long* out, int n_wg);
+}
+// One fused-kernel launch of G rows with phase stamps: out[wg][8] global
+// 100 MHz clock values (slots 0 entry, 1 rows in LDS, 2 wave 0's scan done,
+// 3 round barrier, 4 placement barrier, 5 wave 0's appends done, 6 end).
+// Returns the number of workgroups, < 0 on failure.
+extern "C" int32_t kbg_tool_firstfit_stamps(const kbg_snapshot* snap, const kbg_options* o, int32_t G,
+                                            unsigned long long* out, int32_t max_wg) {
+  Session S;
+  if (open_session(S, snap, o, nullptr) != KBG_OK) return -1;
+  std::vector<int32_t> bt;
+  for (int32_t t : S.pend_all) {
+    if ((int32_t)bt.size() == std::min(G, S.K)) break;
+    bt.push_back(t);
+  }
+  Grouper grouper(S);
+  kbg::Stage& sg = S.stages[0];
+  const int32_t rows = grouper.build(sg, bt.data(), (int32_t)bt.size());
+  for (int r = 0; r < 3; ++r)  // warm, then the stamped launch is the last one
+    if (device_scan(S, sg, rows, S.res_stamp) != KBG_OK) {
+      free_device(S);
+      return -2;
+    }
+  const int32_t n_wg = std::min((rows + 15) / 16, max_wg);
+  const bool ok = kbg::read_ff_stamps(out, n_wg) == hipSuccess;
+  free_device(S);
+  return ok ? n_wg : -3;
+}
+#endif

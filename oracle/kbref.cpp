@@ -54,6 +54,7 @@
 #include <memory>
 #include <set>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -816,7 +817,7 @@ struct Session {  // framework/session.go:35-61
   std::unordered_map<TaskInfo*, int> decisionOf;
   std::vector<std::pair<std::string, std::string>> binds;  // (ns/name, node) in dispatch order
   int64_t predicate_calls = 0;
-  int threads = 1;  // > 1: allocate's node loop evaluated in parallel blocks (B-omp CPU baseline only)
+  int threads = 1;  // > 1: allocate's node loop evaluated by a team of threads (B-omp CPU baseline only)
   size_t min_parallel_nodes = 512;  // B-omp: smaller clusters walk the nodes on one thread
   std::vector<TaskInfo*> evaluated;  // every task whose node loop ran, in order
 
@@ -1527,51 +1528,125 @@ struct Predicates {
 };
 
 // ---------------------------------------------------------------- allocate
-// allocate.go:119-162 for one task with the predicates of a block of nodes
-// evaluated on ssn->threads threads (PredicateFn reads the session only), then
-// the block walked in node order exactly like the sequential loop: the first
-// node whose Idle or Releasing fits wins; NodesFitDelta gets the
-// predicate-passing nodes before it. A panic inside PredicateFn is rethrown
-// when the walk reaches its node. Used for the B-omp CPU baseline only.
-static bool threaded_node_loop(Session* ssn, JobInfo* job, TaskInfo* task) {
-  const size_t N = ssn->nodes.size();
-  const size_t B = (size_t)ssn->threads * 64;
-  // per node of a block: 0 predicates fail, 1 Idle fits, 2 Releasing fits, 3 neither; 4 PredicateFn panics
-  std::vector<int8_t> st(std::min(N, B));
-  std::vector<std::string> panic(st.size());
-  job->fit_log.clear();
-  job->fit_log_pending = true;
-  for (size_t base = 0; base < N; base += B) {
-    const size_t n = std::min(N, base + B) - base;
-#pragma omp parallel for num_threads(ssn->threads) schedule(static)
-    for (size_t i = 0; i < n; ++i) {
-      NodeInfo* node = ssn->nodes[base + i];
-      try {
-        if (!ssn->PredicateFn(task, node, false)) st[i] = 0;
-        else if (task->resreq.LessEqual(node->idle)) st[i] = 1;
-        else if (task->resreq.LessEqual(node->releasing)) st[i] = 2;
-        else st[i] = 3;
-      } catch (const RefPanic& e) {
-        st[i] = 4;
-        panic[i] = e.what();
+// B-omp (the multi-core CPU baseline only): allocate.go:119-162 for one task
+// with PredicateFn and the two fits evaluated on a persistent team of
+// ssn->threads threads (PredicateFn reads the session only). The node axis is
+// cut into chunks of kChunk nodes handed out in node order from one counter;
+// a thread stops taking chunks once a chunk at or below the one it would take
+// holds a stop (Idle or Releasing fit, or a PredicateFn panic), so an early
+// first fit costs one round of chunks and a task that fits nowhere is spread
+// over every thread. The calling thread then walks the evaluated prefix in
+// node order exactly like the sequential loop: the first node whose Idle or
+// Releasing fits wins; NodesFitDelta gets the predicate-passing nodes before
+// it; a panic is rethrown when the walk reaches its node. One parallel region
+// for the whole run (the team spins between tasks): no fork/join per task.
+struct NodeTeam {
+  static constexpr size_t kChunk = 64;
+  Session* ssn = nullptr;
+  TaskInfo* task = nullptr;
+  size_t N = 0, n_chunks = 0;
+  std::vector<int8_t> st;  // per node: 0 predicates fail, 1 Idle fits, 2 Releasing fits, 3 neither, 4 panic, -1 not evaluated
+  std::vector<std::string> panic;
+  std::atomic<uint64_t> gen{0};
+  std::atomic<size_t> next{0};
+  std::atomic<size_t> best{SIZE_MAX};  // lowest chunk holding a stop
+  std::atomic<int> done{0};
+  std::atomic<bool> quit{false};
+  std::vector<std::thread> team;
+
+  explicit NodeTeam(int workers) {
+    for (int w = 0; w < workers; ++w) team.emplace_back([this] { loop(); });
+  }
+  ~NodeTeam() {
+    quit.store(true, std::memory_order_release);
+    gen.fetch_add(1, std::memory_order_release);
+    for (auto& t : team) t.join();
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      uint64_t g;
+      while ((g = gen.load(std::memory_order_acquire)) == seen) __builtin_ia32_pause();
+      seen = g;
+      if (quit.load(std::memory_order_acquire)) return;
+      work();
+      done.fetch_add(1, std::memory_order_release);
+    }
+  }
+  void work() {
+    for (;;) {
+      const size_t c = next.fetch_add(1, std::memory_order_relaxed);
+      if (c >= n_chunks || c > best.load(std::memory_order_relaxed)) return;
+      const size_t lo = c * kChunk, hi = std::min(N, lo + kChunk);
+      for (size_t i = lo; i < hi; ++i) {
+        NodeInfo* node = ssn->nodes[i];
+        int8_t v;
+        try {
+          if (!ssn->PredicateFn(task, node, false)) v = 0;
+          else if (task->resreq.LessEqual(node->idle)) v = 1;
+          else if (task->resreq.LessEqual(node->releasing)) v = 2;
+          else v = 3;
+        } catch (const RefPanic& e) {
+          v = 4;
+          panic[i] = e.what();
+        }
+        st[i] = v;
+        if (v == 1 || v == 2 || v == 4) {  // the walk stops here: the rest of the chunk is not needed
+          size_t b = best.load(std::memory_order_relaxed);
+          while (c < b && !best.compare_exchange_weak(b, c, std::memory_order_relaxed)) {
+          }
+          break;
+        }
       }
     }
-    for (size_t i = 0; i < n; ++i) {
-      ssn->predicate_calls++;
-      if (st[i] == 4) throw RefPanic(panic[i]);
-      if (st[i] == 0) continue;
-      NodeInfo* node = ssn->nodes[base + i];
-      if (st[i] == 1) {
-        ssn->Allocate(task, node);
-        return true;
-      }
-      Resource fd = node->idle;
-      fd.FitDelta(task->resreq);
-      job->fit_log.emplace_back(node, fd);
-      if (st[i] == 2) {
-        ssn->Pipeline(task, node);
-        return true;
-      }
+  }
+  // Evaluates the task's node loop; returns the index one past the last node
+  // the sequential walk needs (every node below it evaluated).
+  size_t run(Session* s, TaskInfo* t) {
+    ssn = s;
+    task = t;
+    N = s->nodes.size();
+    n_chunks = (N + kChunk - 1) / kChunk;
+    if (st.size() < N) {
+      st.resize(N);
+      panic.resize(N);
+    }
+    next.store(0, std::memory_order_relaxed);
+    best.store(SIZE_MAX, std::memory_order_relaxed);
+    done.store(0, std::memory_order_relaxed);
+    gen.fetch_add(1, std::memory_order_release);  // publishes the task and the reset counters
+    work();
+    while (done.load(std::memory_order_acquire) != (int)team.size()) __builtin_ia32_pause();
+    const size_t b = best.load(std::memory_order_relaxed);
+    return b == SIZE_MAX ? N : std::min(N, (b + 1) * kChunk);
+  }
+};
+
+static bool threaded_node_loop(Session* ssn, JobInfo* job, TaskInfo* task) {
+  static std::unique_ptr<NodeTeam> team;
+  if (!team || (int)team->team.size() != ssn->threads - 1) {
+    team.reset();
+    team.reset(new NodeTeam(ssn->threads - 1));
+  }
+  const size_t end = team->run(ssn, task);
+  job->fit_log.clear();
+  job->fit_log_pending = true;
+  for (size_t i = 0; i < end; ++i) {
+    ssn->predicate_calls++;
+    const int8_t v = team->st[i];
+    if (v == 4) throw RefPanic(team->panic[i]);
+    if (v == 0) continue;
+    NodeInfo* node = ssn->nodes[i];
+    if (v == 1) {
+      ssn->Allocate(task, node);
+      return true;
+    }
+    Resource fd = node->idle;
+    fd.FitDelta(task->resreq);
+    job->fit_log.emplace_back(node, fd);
+    if (v == 2) {
+      ssn->Pipeline(task, node);
+      return true;
     }
   }
   return false;
@@ -1626,8 +1701,8 @@ static void allocate_execute(Session* ssn) {
       budget_check(ssn->evaluated.size());
       bool assigned = false;
       if (!job->nodesFitDelta.empty()) job->nodesFitDelta.clear();
-      // B-omp: the same loop, predicates evaluated in parallel blocks; below
-      // min_parallel_nodes a fork/join per task costs more than the whole walk
+      // B-omp: the same loop, predicates evaluated by the node team; below
+      // min_parallel_nodes the hand-off per task costs more than the whole walk
       if (ssn->threads > 1 && ssn->nodes.size() >= ssn->min_parallel_nodes) {
         if (threaded_node_loop(ssn, job, task)) { jobs->Push(job); break; }
         continue;
