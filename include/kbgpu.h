@@ -99,9 +99,11 @@ typedef struct kbg_node {
   int32_t unschedulable;   /* Node.Spec.Unschedulable */
   int32_t label_off, label_len; /* Node.Labels: pairs (key,value) at labels[2*i] */
   int32_t taint_off, taint_len; /* Node.Spec.Taints: taints[taint_off ..] */
-  int32_t port_off, port_len;   /* NodeInfo.UsedPorts(): every container port of the pods on the
-                                   node (node.Pods(), node_info.go:181-187 -> vendor
-                                   cache/node_info.go:593-605), ports[port_off ..] */
+  int32_t port_off, port_len;   /* NodeInfo.UsedPorts(): the container ports (hostPort > 0) of the
+                                   pods on the node (node.Pods(), node_info.go:181-187 -> vendor
+                                   cache/node_info.go:593-605), one entry per pod and port, so a
+                                   port stays used while any pod on the node lists it (duplicates
+                                   are one used port to the predicate), ports[port_off ..] */
   int32_t task_off, task_len;   /* the session-job tasks in NodeInfo.Tasks, in its (insertion) order:
                                    node_tasks[task_off ..] are indices into tasks. preempt/reclaim
                                    take victims in this order (preempt.go:199-206, reclaim.go:113-126) */
@@ -459,8 +461,7 @@ typedef struct kbg_event {
  * KBG_E_UNSUPPORTED and KBG_E_INVALID found before the first event is applied
  * leave the session unchanged: an event naming a deleted task or an index out
  * of range, a removed pod whose key is held on its node by a pod outside the
- * session jobs, a pod with host ports leaving a node, a node update of a node
- * the cache only knows from a pod. KBG_E_REF_PANIC (the cache itself would
+ * session jobs, a node update of a node the cache only knows from a pod. KBG_E_REF_PANIC (the cache itself would
  * panic: a Resource.Sub underflow in AddTask / RemoveTask / SetNode) is found
  * while the events are applied: the session is then unusable and every later
  * call on it but kbg_session_close returns KBG_E_INVALID (re-open it). */

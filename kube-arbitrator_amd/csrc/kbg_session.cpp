@@ -4453,10 +4453,17 @@ kbg_status vt_setup(Session& S) {
         (st = dalloc(S, &dja, 3 * J)) || (st = dalloc(S, &dqa, 3 * Q)) || (st = hupload(S, &dqd, qd)) ||
         (st = dalloc(S, &S.d_vbits, 2 * (size_t)S.W32)) || (st = dalloc(S, &S.d_vbits_red, 2 * (size_t)S.W32)))
       return st;
-    // nodes of this process's range holding more than 128 candidates (kbg_victim_big_kernel)
+    // nodes of this process's range holding more than 128 candidates
+    // (kbg_victim_big_kernel, up to kMaxNodeCandidates); every node holding
+    // more is left out of the device scans and re-evaluated on the host when
+    // a stop search reaches it (try_task marks it unknown after each scan)
     S.big_rows.clear();
-    for (int32_t n = S.tab_lo; n < S.tab_lo + S.tab_n; ++n)
-      if (S.nt_off[n + 1] - S.nt_off[n] > 128) S.big_rows.push_back(n - S.tab_lo);
+    S.huge_nodes.clear();
+    for (int32_t n = 0; n < S.n_nodes; ++n) {
+      const int32_t L = S.nt_off[n + 1] - S.nt_off[n];
+      if (L > kbg::kMaxNodeCandidates) S.huge_nodes.push_back(n);
+      else if (L > 128 && n >= S.tab_lo && n < S.tab_lo + S.tab_n) S.big_rows.push_back(n - S.tab_lo);
+    }
     if ((st = hupload(S, &S.d_big_rows, S.big_rows))) return st;
     S.vt_allocs.assign(S.d_allocs.begin() + a0, S.d_allocs.end());
     HIP_TRY(hipMemset(S.d_vbits, 0, 2 * (size_t)S.W32 * sizeof(uint32_t)));  // other ranks' words stay 0
@@ -4866,6 +4873,7 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
     }
     std::fill(vc.unk.begin(), vc.unk.end(), 0u);
     vc.lb = 0;
+    for (int32_t hn : S.huge_nodes) vc.unk[hn >> 5] |= 1u << (hn & 31);  // not scanned on the device
     vc.key = key;
     vc.fns = dfns;
     vc.valid = true;
@@ -4981,12 +4989,7 @@ std::vector<std::vector<int32_t>> pending_by_job(const Session& S) {
   return out;
 }
 
-kbg_status victim_action_check(Session& S) {
-  if (S.max_candidates > kbg::kMaxNodeCandidates)
-    return fail(KBG_E_UNSUPPORTED, "a node holds more than " + std::to_string(kbg::kMaxNodeCandidates) +
-                                       " running session tasks: run the reference path");
-  return KBG_OK;
-}
+kbg_status victim_action_check(Session&) { return KBG_OK; }  // nodes past kMaxNodeCandidates: host_stop
 
 struct VictimRun {
   Session& S;
@@ -5233,7 +5236,7 @@ bool in_node_add(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
   S.kc_node[key]++;
   S.upd_keys.push_back(key);
   S.node_task_order[n].push_back(t);
-  // the pod's host ports join the node's (a set: duplicates are harmless to setup_host_ports)
+  // the pod's host ports join the node's (one entry per pod and port: a port stays used while any pod lists it)
   const int32_t sp = S.tasks_in[t].spec;
   if (sp >= 0 && S.specs_in[sp].port_len > 0) {
     const kbg_spec& spec = S.specs_in[sp];
@@ -5267,9 +5270,27 @@ int in_node_remove(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
                                    "(its resources are unknown): re-open the session");
   const int32_t u = *hit;
   const int32_t sp = S.tasks_in[u].spec;
-  if (sp >= 0 && S.specs_in[sp].has_host_ports)
-    return fail(KBG_E_UNSUPPORTED, "a pod with host ports leaves a node (its used ports are a set over "
-                                   "every pod): re-open the session");
+  if (sp >= 0 && S.specs_in[sp].port_len > 0) {
+    // the pod's host ports leave the node's: node.Pods() no longer lists it,
+    // so a port stays used exactly while another pod's entry remains (the
+    // node's list holds one entry per pod and port, kbgpu.h kbg_node)
+    auto canon_ip = [&](int32_t id) { return S.strs[id].empty() ? std::string("0.0.0.0") : S.strs[id]; };
+    auto canon_proto = [&](int32_t id) { return S.strs[id].empty() ? std::string("TCP") : S.strs[id]; };
+    std::vector<kbg_host_port> mine(S.ports_in.begin() + nd.port_off, S.ports_in.begin() + nd.port_off + nd.port_len);
+    const kbg_spec& spec = S.specs_in[sp];
+    for (int32_t i = 0; i < spec.port_len; ++i) {
+      const kbg_host_port& hp = S.ports_in[spec.port_off + i];
+      if (hp.host_port <= 0) continue;
+      const std::string ip = canon_ip(hp.host_ip), pr = canon_proto(hp.protocol);
+      auto it = std::find_if(mine.begin(), mine.end(), [&](const kbg_host_port& x) {
+        return x.host_port == hp.host_port && canon_ip(x.host_ip) == ip && canon_proto(x.protocol) == pr;
+      });
+      if (it != mine.end()) mine.erase(it);
+    }
+    nd.port_off = (int32_t)S.ports_in.size();
+    nd.port_len = (int32_t)mine.size();
+    S.ports_in.insert(S.ports_in.end(), mine.begin(), mine.end());
+  }
   const Res r = S.treq[u];
   if (nd.has_node) {
     switch (S.tasks_in[u].status) {
@@ -5449,10 +5470,6 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
             return fail(KBG_E_UNSUPPORTED, "the pod key is held on the node by a pod outside the session jobs "
                                            "(its resources are unknown): re-open the session");
           if (h >= 0) {
-            const int32_t sp = task_now(h).spec;
-            if (sp >= 0 && S.specs_in[sp].has_host_ports)
-              return fail(KBG_E_UNSUPPORTED, "a pod with host ports leaves a node (its used ports are a set over "
-                                             "every pod): re-open the session");
             hold[((int64_t)c.node << 32) | (uint32_t)c.key] = -1;
             found = true;
           }

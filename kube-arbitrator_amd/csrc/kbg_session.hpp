@@ -401,7 +401,8 @@ struct Session {
   int64_t updates = 0, rebuilds = 0;
   bool vt_stale = false;                              // the victim tables follow older inputs
   std::vector<void*> vt_allocs;                       // their HBM (freed when they are rebuilt)
-  std::vector<int32_t> big_rows;                      // table rows of nodes with > 128 victim candidates
+  std::vector<int32_t> big_rows;                      // table rows of nodes with 129 .. kMaxNodeCandidates victim candidates
+  std::vector<int32_t> huge_nodes;                    // nodes (global) with more: evaluated on the host (host_stop)
   int32_t* d_big_rows = nullptr;
 
   // ---- NodeInfo.Tasks keys (node_info.go:101-106): AddTask of a PodKey the

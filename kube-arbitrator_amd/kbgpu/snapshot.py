@@ -84,15 +84,14 @@ class FlatSnapshot:
             for t in obj.get("taints") or []:
                 taints.append((S(t.get("key")), S(t.get("value")), S(t.get("effect"))))
             r["taint_len"] = len(taints) - r["taint_off"]
-            # NodeInfo.UsedPorts over node.Pods(): a set, only hostPort > 0 is recorded (host_ports.go Add)
+            # NodeInfo.UsedPorts over node.Pods(): only hostPort > 0 is recorded
+            # (host_ports.go Add); one entry per pod and port, so a pod that
+            # leaves the node (kbg_session_update) takes exactly its own entries
             r["port_off"] = len(ports)
-            used = {}
             for t in n.tasks.values():
                 for ip, proto, port in container_ports(t.pod):
                     if port > 0:
-                        used.setdefault((ip or "0.0.0.0", proto or "TCP", port), None)
-            for ip, proto, port in used:
-                ports.append((S(ip), S(proto), port))
+                        ports.append((S(ip or "0.0.0.0"), S(proto or "TCP"), port))
             r["port_len"] = len(ports) - r["port_off"]
             # NodeInfo.Tasks keys (PodKey) of every pod on the node, in order
             r["key_off"] = len(node_keys)

@@ -509,7 +509,7 @@ def dupkey_fixture(seed, **kw):
     return fx
 
 
-def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3, aff=0.0, ports=0.0, big=False):
+def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3, aff=0.0, ports=0.0, big=False, huge=False):
     """A cluster already full of Running gang jobs in several queues, with
     Pending jobs of every queue: the regime of reclaim and preempt
     (BASELINE config 5 in miniature). Tasks of a job share one request so the
@@ -523,6 +523,8 @@ def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3, aff=0.0, ports=0
                  "pods": str(rng.choice([4, 8, 110]))}
         if big:  # nodes that hold hundreds of small pods (victim scans in several 64-candidate chunks)
             alloc = {"cpu": "64", "memory": "256Gi", "pods": str(rng.choice([300, 600, 1100]))}
+        if huge:  # more Running pods than one device victim scan takes (kbg_device.hpp kMaxNodeCandidates)
+            alloc = {"cpu": "256", "memory": "1Ti", "pods": "3000"}
         nds.append({"name": f"n{i:02d}", "allocatable": alloc,
                     "labels": {"zone": rng.choice(["a", "b"]), "host": f"n{i:02d}"}})
     free = {n["name"]: [int(n["allocatable"]["cpu"]) * 1000, int(n["allocatable"]["pods"])] for n in nds}
@@ -531,7 +533,7 @@ def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3, aff=0.0, ports=0
     uid = 0
     uniform = rng.random() < 0.7  # one request size for every job: evictions free exactly what a pipeline needs
     base = (rng.choice([500, 1000, 2000]), rng.choice(["0", "512Mi", "1Gi"]))
-    if big:
+    if big or huge:
         base = (rng.choice([50, 100, 200]), "0")
         uniform = True
     for j in range(jobs):

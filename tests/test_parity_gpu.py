@@ -439,6 +439,24 @@ def test_victim_big_node_parity(seed):
         ssn.close()
 
 
+@pytest.mark.parametrize("seed", range(10))
+def test_victim_huge_node_parity(seed):
+    """Nodes with more than kMaxNodeCandidates (1024) Running pods, which the
+    reference walks like any other (preempt.go:169-236): left out of the
+    device victim scans and evaluated on the host when a stop search reaches
+    them (host_stop), evictions exact. No KBG_E_UNSUPPORTED."""
+    fx = synth.contended_fixture(9500 + seed, big=True, huge=True, nodes=2, jobs=240, tasks=30)
+    running = {}
+    for p in fx["pods"]:
+        if p["phase"] == "Running":
+            running[p["nodeName"]] = running.get(p["nodeName"], 0) + 1
+    assert max(running.values()) > 1024
+    got, ssn = run_fixture(fx)
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
 @pytest.mark.parametrize("seed", list(range(0, 60, 4)))
 def test_select_replays_with_affinity(seed):
     """kbg_select on affinity fixtures: a placement that creates an affinity
