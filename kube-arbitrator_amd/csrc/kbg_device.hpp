@@ -206,26 +206,49 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
                        int32_t n_tasks, int32_t cap_check, int32_t int_mode, uint64_t* out, hipStream_t stream,
                        hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
-// The fused scan + candidate extraction (kbg_firstfit_kernel): for each row g
-// < G the first capoff[g+1]-capoff[g] feasible nodes of the global words
-// [w_lo, w_hi) in node order into cand[capoff[g] ..], count[g] = how many
-// (| kCountIncompleteBit when more exist), avail[g] = avail_bit if any
-// (owner-resolve; null otherwise). rows / capoff / count / cand may be
-// host-mapped (zero-copy).
+// The fused scan + first-fit extraction (kbg_firstfit_kernel). Rows map to
+// shapes: row g evaluates shape s = row_shape[g] & ~kRowWriter (grouped mode:
+// row_shape null, s = g, every row a writer). A shape is a TaskRec whose
+// flags carry kRowRelZeroFits and, from bit kRowWantShift, `want`: how many
+// fits its list must hold before the walk may stop (EARLY_EXIT) and the
+// output may end. The writer row of shape s writes, for the words [w_lo,
+// w_lo + covered) in node order, the pair of 64-node masks {fits Idle or
+// Releasing, fits Idle} (static predicate, pod cap and LessEqual applied)
+// into masks[s * mw + (w - w_lo)], and info[s] = covered | kInfoAnyBit (some
+// node of the walked words fits) | kCountIncompleteBit (covered < w_hi -
+// w_lo: the list is cut after the word holding its want-th fit). Every fit of
+// a covered word is in the masks, so the host reads the first-fit candidates
+// in node order by scanning bits. The shape table is in the kernel arguments
+// (n_shapes <= kInlineShapes: no PCIe read at launch) or host-mapped;
+// row_shape, info, masks, avail may be host-mapped (zero-copy).
+constexpr int kInlineShapes = 96;
+constexpr uint32_t kRowWriter = 0x80000000u;
+constexpr int kRowWantShift = 1;
+constexpr uint32_t kInfoAnyBit = 0x20000000u;
+constexpr uint32_t kInfoWordsMask = 0x00ffffffu;
+struct alignas(16) MaskPair {
+  uint64_t f;  // fits Idle or Releasing
+  uint64_t i;  // fits Idle
+};
 struct FirstFitArgs {
   const double* nodes;          // the node table as one block (NodeSoA of alloc_soa): rows of the nodes
                                 // [tab_lo, tab_lo + tab_n), idle c/m/g, rel c/m/g f64[stride], ntasks,
                                 // maxtasks i32[stride]
   const uint64_t* class_mask;   // [class][W]
-  const char* up;               // rows TaskRec[G] at 0, capoff u32[G + 1] at up_capoff
-  uint32_t* down;               // count u32[G], then the candidates (cand = down + G)
-  uint32_t* avail;
-  int32_t stride, up_capoff;
-  int32_t G, n_nodes, W, w_lo, w_hi, tab_lo, tab_n;
+  const TaskRec* shapes;        // host-mapped shape table, or null: inl[]
+  const uint32_t* row_shape;    // [G] shape | kRowWriter, or null: row g is shape g and writes it
+  uint32_t* info;               // [n_shapes]
+  MaskPair* masks;              // [n_shapes][mw]
+  uint32_t* avail;              // owner-resolve: [n_shapes] avail_bit when any node fits, else 0
+  uint32_t avail_bit;
+  int32_t stride, G, n_shapes, mw;
+  int32_t n_nodes, W, w_lo, w_hi, tab_lo, tab_n;
   int32_t cap_check;            // the predicates plugin's pod cap is on
   int32_t early_exit;           // stop once every row's list is full (production mode)
-  uint32_t avail_bit;
+  TaskRec inl[kInlineShapes];
 };
+// Rows per workgroup of a launch of G rows (16, 24 or 32).
+int firstfit_rows(int32_t G);
 hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t stream, hipEvent_t start = nullptr,
                            hipEvent_t stop = nullptr);
 

@@ -212,78 +212,76 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
 }
 
 // ------------------------------------------------------ fused first-fit
-// kbg_firstfit_kernel: the scan and the candidate extraction in one launch,
-// with no feasibility bitmap in between. A workgroup owns kFfRows rows and
-// walks their words [w_lo, w_hi) in node order, up to kFfMaxRound words per
-// round (C3's 79 in one): wave w evaluates words w, w + kFfWaves, ... of the
-// round for every row exactly as kbg_scan_kernel does (64 nodes in registers,
-// one ballot per dimension, the raw masks moved to lane J with
-// v_writelane_b32, class mask / pod cap / Releasing shortcut applied by lane
-// J) and parks the row masks in LDS; after the round's barrier wave j places
-// row j's words (a prefix sum of their node counts gives each word's first
-// list position) and then all waves append the placed words' nodes to the
-// lists (lane = node, position = word start + mbcnt), at most `want` per row,
-// so a long list is written by 16 waves instead of walked by one. Rows read
-// their requests and list offsets from host-mapped memory and write counts
-// and candidates straight into it: no copy kernel on either side.
-// `early_exit` (production mode) ends the walk after a round in which every
-// row of the workgroup got more nodes than its list holds (the rest of the
-// table cannot change its list); full-scan mode evaluates every node for
-// every row.
-constexpr int kFfRows = 16;
-constexpr int kFfWaves = 16;      // == kFfRows: wave j extracts row j
-constexpr int kFfMaxRound = 128;  // words per round (LDS: 2 x 128 x 16 x 8 B); a multiple of kFfWaves
-// rows whose requests are read from LDS together: 4 (integer thresholds) / 2
-// (the reference expression) keep the kernel at 8 waves per SIMD, no spills
+// kbg_firstfit_kernel: the scan and the first-fit extraction in one launch.
+// A workgroup of 16 waves owns ROWS rows (16, 24 or 32: the host picks the
+// smallest that puts every row block on a CU at once, so no launch runs a
+// second round of workgroups) and walks their words [w_lo, w_hi) in node
+// order, up to kFfMaxRound words per round (C3's 79 in one): wave w evaluates
+// words w, w + 16, ... of the round for every row (64 nodes in registers, the
+// next word's loads in flight during the current one; rows read from LDS as
+// same-address broadcasts; one v_cmp_f64 ballot per dimension ANDed on the
+// scalar unit, the raw ballot moved to lane J with v_writelane_b32; class
+// mask, pod cap and Releasing shortcut applied by lane J) and parks the masks
+// in LDS. After the round's barrier the wave owning row j (rows w and w + 16)
+// takes the row's words 64 at a time: a ballot prefix sum of their fit counts
+// gives each word's first list position, and every word starting below the
+// row's `want` is written to the output as its two masks (one 16-B store per
+// word, 1 KB per wave instruction): no per-candidate writes, no second pass.
+// Shapes come from the kernel arguments (no PCIe read at launch) or from
+// host-mapped memory. `EARLY_EXIT` (production mode) ends the walk after a
+// round in which every row's list is full (the rest of the table cannot
+// change it); full-scan mode evaluates every node for every row (SURVEY
+// §8(d)).
+constexpr int kFfWaves = 16;
+constexpr int kFfMaxRound = 128;  // words per round (LDS: 2 x 128 x ROWS x 8 B); a multiple of kFfWaves
+// rows whose requests are read from LDS together
 template <bool INT_MODE>
 constexpr int kFfGroup = INT_MODE ? 4 : 2;
+// (32-row workgroups: 2 rows per group keep the longer unrolled row walk within
+// the register budget)
+template <bool INT_MODE, int ROWS>
+constexpr int kFfGroupR = ROWS > 24 ? 2 : kFfGroup<INT_MODE>;
 
-template <bool INT_MODE, bool EARLY_EXIT>
+template <bool INT_MODE, bool EARLY_EXIT, int ROWS>
 __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArgs a) {
-  __shared__ double s_req[kFfRows][3];
-  __shared__ int32_t s_cls[kFfRows], s_flags[kFfRows];
-  __shared__ uint64_t s_f[kFfMaxRound][kFfRows];  // [word of the round][row]: fits (Idle or Releasing)
-  __shared__ uint64_t s_i[kFfMaxRound][kFfRows];  //                        fits in Idle
-  __shared__ uint32_t s_pos[kFfMaxRound][kFfRows];  // list position of the word's first node
-  __shared__ uint32_t s_done[kFfRows], s_need[kFfRows], s_want[kFfRows], s_base[kFfRows];
+  static_assert(ROWS % 8 == 0 && ROWS <= 2 * kFfWaves, "rows per workgroup");
+  constexpr int RPW = (ROWS + kFfWaves - 1) / kFfWaves;  // rows a wave extracts (1 or 2)
+  __shared__ double s_req[ROWS][3];
+  __shared__ int32_t s_cls[ROWS];
+  __shared__ uint32_t s_flags[ROWS], s_map[ROWS];  // shape flags (want << 1 | rel-zero fit); shape | writer
+  __shared__ uint64_t s_f[kFfMaxRound][ROWS];      // [word of the round][row]: fits (Idle or Releasing)
+  __shared__ uint64_t s_i[kFfMaxRound][ROWS];      //                        fits in Idle
+  __shared__ uint32_t s_done[ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g0 = blockIdx.x * kFfRows;
+  const int g0 = blockIdx.x * ROWS;
   FF_STAMP(0);
-  if (a.w_hi <= a.w_lo) {  // no words (a session without nodes): empty lists, no table or mask read
-    if (wave == 0 && lane < kFfRows && g0 + lane < a.G) {
-      a.down[g0 + lane] = 0u;
-      if (a.avail) a.avail[g0 + lane] = 0u;
-    }
-    return;
-  }
-  if (wave == 0 && lane < kFfRows) {
-    const TaskRec tr = reinterpret_cast<const TaskRec*>(a.up)[min(g0 + lane, a.G - 1)];  // past G: never written
+  if (wave == 0 && lane < ROWS) {
+    const int g = min(g0 + lane, a.G - 1);  // rows past G evaluate a copy of the last row, write nothing
+    const uint32_t m = a.row_shape ? a.row_shape[g] : ((uint32_t)g | kRowWriter);
+    const uint32_t sh = m & ~kRowWriter;
+    const TaskRec tr = a.shapes ? a.shapes[sh] : a.inl[sh];
     s_req[lane][0] = tr.req[0];
     s_req[lane][1] = tr.req[1];
     s_req[lane][2] = tr.req[2];
     s_cls[lane] = tr.cls;
-    s_flags[lane] = tr.flags;
+    s_flags[lane] = (uint32_t)tr.flags;
+    s_map[lane] = g0 + lane < a.G ? m : (m & ~kRowWriter);
   }
-  // wave j extracts row g0 + j
-  const int g = g0 + wave;
-  const bool has_row = g < a.G;
-  uint32_t base = 0, want = 0;
-  const uint32_t* capoff = reinterpret_cast<const uint32_t*>(a.up + a.up_capoff);
-  if (has_row) {
-    base = capoff[g];
-    want = capoff[g + 1] - base;
+  const int32_t tw = a.w_hi - a.w_lo;  // words this launch covers
+  if (tw <= 0) {  // no words (a session without nodes): empty complete lists, no table or mask read
+    __syncthreads();
+    if (wave == 0 && lane < ROWS && (s_map[lane] & kRowWriter)) {
+      const uint32_t sh = s_map[lane] & ~kRowWriter;
+      a.info[sh] = 0u;
+      if (a.avail) a.avail[sh] = 0u;
+    }
+    return;
   }
-  if (lane == 0) {
-    s_want[wave] = want;
-    s_base[wave] = base;
-  }
-  uint32_t found = 0;
-  bool done = !has_row;
   // A word's node rows (and, once the rows' classes are known, their class
   // mask words) are loaded one word ahead of its compares: the next word's
   // loads are in flight while this one is evaluated. The first word's loads
-  // are issued before the rows arrive from host memory.
+  // are issued before the rows arrive.
   struct Word {
     double ic = 0, im = 0, ig = 0, rc = 0, rm = 0, rg = 0;
     int32_t nt = 0, mt = 0;
@@ -315,10 +313,23 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
   load_word(min(a.w_lo + wave, w_last), cur);
   __syncthreads();
   FF_STAMP(1);
-  const int cls_l = s_cls[lane & (kFfRows - 1)];
-  const int flags_l = s_flags[lane & (kFfRows - 1)];
+  // the extraction state of the rows this wave owns (rows wave, wave + 16)
+  uint32_t found[RPW], want[RPW], covered[RPW];
+  bool done[RPW], writer[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int j = wave + i * kFfWaves;
+    found[i] = 0u;
+    covered[i] = 0u;
+    writer[i] = j < ROWS && (s_map[j] & kRowWriter);
+    want[i] = j < ROWS ? (s_flags[j] >> kRowWantShift) : 0u;
+    done[i] = !writer[i];
+  }
+  const int lrow = lane < ROWS ? lane : 0;
+  const int cls_l = s_cls[lrow];
+  const uint32_t flags_l = s_flags[lrow];
   // rounds are kFfMaxRound (a multiple of kFfWaves) words apart, so a wave's
-  // words are c, c + kFfWaves, ... across rounds too; lanes >= kFfRows load a
+  // words are c, c + kFfWaves, ... across rounds too; lanes >= ROWS load a
   // row's mask word they never use
   uint64_t lane_mw = a.class_mask[(size_t)cls_l * a.W + min(a.w_lo + wave, w_last)];
 #pragma unroll 1
@@ -327,7 +338,7 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
 #pragma unroll 1
     for (int k = wave; k < nw; k += kFfWaves) {     // this wave's words of the round
       // the row requests are re-read from LDS per word (kept in registers
-      // across the loop they would take 96 VGPRs)
+      // across the loop they would take 6 VGPRs per row)
       asm volatile("" ::: "memory");
       const int c = r0 + k;                           // global 64-node word
       const int cn = min(c + kFfWaves, w_last);       // this wave's next word (the last one again at the end)
@@ -340,15 +351,15 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
       uint32_t keep[4] = {0u, 0u, 0u, 0u};
       uint64_t mr;
       if (rel_zero_wave) {
-        scan_rows<INT_MODE, true, kFfRows, 0, kFfGroup<INT_MODE>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm,
-                                                                  cur.rg, keep);
+        scan_rows<INT_MODE, true, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm, cur.rg,
+                                                               keep);
         mr = (flags_l & kRowRelZeroFits) ? ~0ull : 0ull;
       } else {
-        scan_rows<INT_MODE, false, kFfRows, 0, kFfGroup<INT_MODE>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm,
-                                                                   cur.rg, keep);
+        scan_rows<INT_MODE, false, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm,
+                                                                cur.rg, keep);
         mr = (uint64_t)keep[2] | ((uint64_t)keep[3] << 32);
       }
-      if (lane < kFfRows) {
+      if (lane < ROWS) {
         const uint64_t mw = lane_mw & okm;
         const uint64_t fi = ((uint64_t)keep[0] | ((uint64_t)keep[1] << 32)) & mw;
         s_f[k][lane] = fi | (mr & mw);
@@ -360,17 +371,23 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
     if (r0 == a.w_lo) FF_STAMP(2);
     __syncthreads();
     if (r0 == a.w_lo) FF_STAMP(3);
-    // Extraction, phase 1: wave j places row j's words of the round. Lane k
-    // holds word k's node count; the exclusive prefix sum over lanes (one
-    // ballot + mbcnt per bit of the count) is the list position of the
-    // word's first node. Only the words that start below `want` can add a
-    // candidate (positions grow in node order).
-    uint32_t need = 0;
-    if (!done) {
+    if (r0 == a.w_lo) FF_STAMP(4);
+    // Extraction: the owner wave of row j takes its words 64 at a time. Lane
+    // k holds word k's fit count; the exclusive prefix sum over lanes (one
+    // ballot + mbcnt per bit of the count) is the list position of the word's
+    // first node. A word starting below `want` goes out whole (its masks);
+    // positions grow in node order, so the first word starting at or past
+    // `want` ends the list.
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int j = wave + i * kFfWaves;
+      if (j >= ROWS || done[i]) continue;  // wave-uniform
+      MaskPair* out = a.masks + (size_t)(s_map[j] & ~kRowWriter) * a.mw + (r0 - a.w_lo);
 #pragma unroll 1
       for (int k0 = 0; k0 < nw; k0 += 64) {
         const int k = k0 + lane;
-        const uint32_t pc = k < nw ? (uint32_t)__popcll(s_f[k][wave]) : 0u;
+        const uint64_t f = k < nw ? s_f[k][j] : 0ull;
+        const uint32_t pc = (uint32_t)__popcll(f);
         uint32_t excl = 0, tot = 0;
 #pragma unroll
         for (int b = 0; b < 7; ++b) {  // pc <= 64
@@ -378,72 +395,76 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
           excl += __builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u)) << b;
           tot += (uint32_t)__popcll(bb) << b;
         }
-        const uint32_t pos = found + excl;
-        if (k < nw) s_pos[k][wave] = pos;
-        need = (uint32_t)k0 + (uint32_t)__popcll(__ballot(k < nw && pos < want));
-        found += tot;
-        if (found > want) {
-          done = true;
+        const bool put = k < nw && found[i] + excl < want[i];
+        if (put) out[k] = MaskPair{f, s_i[k][j]};
+        const uint32_t nput = (uint32_t)__popcll(__ballot(put));
+        found[i] += tot;
+        covered[i] = (uint32_t)(r0 - a.w_lo + k0) + nput;
+        if (found[i] >= want[i]) {  // every later word starts at or past want
+          done[i] = true;
           break;
         }
       }
     }
-    if (lane == 0) {
-      s_need[wave] = need;
-      s_done[wave] = done ? 1u : 0u;
-    }
-    __syncthreads();
-    if (r0 == a.w_lo) FF_STAMP(4);
-    // phase 2: every (row, placed word) pair is one wave-wide append (lane =
-    // node, position = word start + mbcnt), spread over all the waves so a
-    // long list is not walked by one wave alone
-#pragma unroll 1
-    for (int j = 0; j < kFfRows; ++j) {
-      const int nj = (int)s_need[j];
-#pragma unroll 1
-      for (int k = wave; k < nj; k += kFfWaves) {
-        const uint64_t m = s_f[k][j];
-        if (m == 0ull) continue;  // wave-uniform (every lane reads one address)
-        const uint64_t mi = s_i[k][j];
-        const uint32_t pos =
-            s_pos[k][j] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (((m >> lane) & 1ull) && pos < s_want[j])
-          a.down[a.G + s_base[j] + pos] =
-              (uint32_t)((r0 + k) * 64 + lane) | (((mi >> lane) & 1ull) ? 0u : kCandPipelineBit);
-      }
-    }
     if (r0 == a.w_lo) FF_STAMP(5);
     if (r0 + kFfMaxRound >= a.w_hi) break;  // the last round: no second barrier
-    __syncthreads();  // the round's masks and positions are read
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int j = wave + i * kFfWaves;
+      if (j < ROWS && lane == 0) s_done[j] = done[i] ? 1u : 0u;
+    }
+    __syncthreads();  // the round's masks are read, the done flags written
     if (EARLY_EXIT) {  // every row's list is full: the same decision in every wave
-      const uint32_t d = lane < kFfRows ? s_done[lane] : 1u;
+      const uint32_t d = lane < ROWS ? s_done[lane] : 1u;
       if (__ballot(d == 0u) == 0ull) break;
     }
   }
-  if (has_row && lane == 0) {
-    a.down[g] = (found < want ? found : want) | (found > want ? kCountIncompleteBit : 0u);
-    if (a.avail) a.avail[g] = found ? a.avail_bit : 0u;
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int j = wave + i * kFfWaves;
+    if (!writer[i] || lane != 0) continue;
+    const uint32_t sh = s_map[j] & ~kRowWriter;
+    // covered: the words written; a row whose walk ended with its list not
+    // full covered every word of the walk (EARLY_EXIT: the rounds walked)
+    a.info[sh] = covered[i] | (covered[i] < (uint32_t)tw ? kCountIncompleteBit : 0u) | (found[i] ? kInfoAnyBit : 0u);
+    if (a.avail) a.avail[sh] = found[i] ? a.avail_bit : 0u;
   }
   FF_STAMP(6);
+}
+
+template <bool INT_MODE, bool EARLY_EXIT>
+hipError_t launch_firstfit_rows(const FirstFitArgs& a, int rows, hipStream_t stream, hipEvent_t start,
+                                hipEvent_t stop) {
+  const dim3 grid((a.G + rows - 1) / rows), block(64 * kFfWaves);
+  if (rows == 16)
+    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 16>), grid, block, 0, stream, start, stop, 0, a);
+  else if (rows == 24)
+    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 24>), grid, block, 0, stream, start, stop, 0, a);
+  else
+    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 32>), grid, block, 0, stream, start, stop, 0, a);
+  return hipGetLastError();
+}
+
+// Rows per workgroup: one workgroup per CU at a time (16 waves), so a launch
+// of more than 256 workgroups runs a second, mostly idle round; 24 or 32 rows
+// per workgroup keep batches of up to 8192 rows in one.
+int firstfit_rows(int32_t G) {
+  constexpr int kCUs = 256;
+  if (G <= 16 * kCUs) return 16;
+  if (G <= 24 * kCUs) return 24;
+  return 32;
 }
 
 hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t stream, hipEvent_t start,
                            hipEvent_t stop) {
   if (a.G <= 0) return hipSuccess;
-  const dim3 grid((a.G + kFfRows - 1) / kFfRows), block(64 * kFfWaves);
+  const int rows = firstfit_rows(a.G);
   // <.., false>: full-scan mode (every node of every row), <.., true>: production
-  if (int_mode) {
-    if (a.early_exit)
-      hipExtLaunchKernelGGL((kbg_firstfit_kernel<true, true>), grid, block, 0, stream, start, stop, 0, a);
-    else
-      hipExtLaunchKernelGGL((kbg_firstfit_kernel<true, false>), grid, block, 0, stream, start, stop, 0, a);
-  } else {
-    if (a.early_exit)
-      hipExtLaunchKernelGGL((kbg_firstfit_kernel<false, true>), grid, block, 0, stream, start, stop, 0, a);
-    else
-      hipExtLaunchKernelGGL((kbg_firstfit_kernel<false, false>), grid, block, 0, stream, start, stop, 0, a);
-  }
-  return hipGetLastError();
+  if (int_mode)
+    return a.early_exit ? launch_firstfit_rows<true, true>(a, rows, stream, start, stop)
+                        : launch_firstfit_rows<true, false>(a, rows, stream, start, stop);
+  return a.early_exit ? launch_firstfit_rows<false, true>(a, rows, stream, start, stop)
+                      : launch_firstfit_rows<false, false>(a, rows, stream, start, stop);
 }
 
 // ------------------------------------------------------- FitError counts

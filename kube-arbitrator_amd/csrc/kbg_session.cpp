@@ -473,6 +473,15 @@ kbg_status hupload(Session& S, T** p, const std::vector<T>& v) {
 // f64[stride], then ntasks and maxtasks i32[stride], stride = tab_n rounded
 // up to 64 rows. A reset restores it with one copy.
 int32_t soa_stride(const Session& S) { return std::max(64, (S.tab_n + 63) / 64 * 64); }
+
+// Fused-path results in a stage's down buffer (u32 units): per slot the info
+// word, then (16-B aligned) per slot `mw` word-mask pairs, then per slot the
+// owner-resolve availability. mw = the words one launch covers (this rank's
+// words when the session is sharded).
+int32_t fused_mask_words(const Session& S) { return std::max(1, S.comm ? S.Wl : S.W); }
+inline size_t fused_mask_off(int32_t K) { return ((size_t)K + 3) & ~(size_t)3; }
+inline size_t fused_avail_off(int32_t K, int32_t mw) { return fused_mask_off(K) + (size_t)K * mw * 4; }
+inline size_t fused_down_words(int32_t K, int32_t mw) { return fused_avail_off(K, mw) + (size_t)K; }
 size_t soa_bytes(const Session& S) { return (size_t)soa_stride(S) * (6 * 8 + 2 * 4); }
 
 kbg_status alloc_soa(Session& S, kbg::NodeSoA* soa) {
@@ -617,32 +626,40 @@ void trace_add(const char* what, int64_t v = 0);
 
 kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   trace_add("l.begin", G);
-  const uint32_t total = sg.h_capoff[G];
   const int32_t Gp = kbg::kbg_pad_rows(G);  // Grouper::build padded the rows
   if (!S.comm || S.owner) {
-    // one launch: kbg_firstfit_kernel reads the rows from the stage's mapped
-    // buffer and writes counts and candidates straight into the other one;
-    // this process's words only (owner-resolve), or every word
-    kbg::FirstFitArgs a{};
+    // one launch: kbg_firstfit_kernel takes the shapes from its arguments
+    // (or the stage's mapped buffer) and writes each shape's info word and
+    // word masks straight into the other one; this process's words only
+    // (owner-resolve), or every word
+    thread_local kbg::FirstFitArgs a;  // (3 KB: the inline shape table)
+    a = kbg::FirstFitArgs{};
     a.nodes = S.d_nodes.idle_cpu;
     a.stride = soa_stride(S);
     a.class_mask = S.d_class_mask;
-    a.up = dev_ptr(S, sg.h_up);
-    a.up_capoff = (int32_t)((size_t)Gp * sizeof(kbg::TaskRec));
-    a.down = dev_ptr(S, sg.h_down);
-    if (!a.up || !a.down) return fail(KBG_E_HIP, "hipHostGetDevicePointer of a stage buffer failed");
-
     a.G = G;
+    a.n_shapes = sg.n_slots;
     a.n_nodes = S.n_nodes;
     a.W = S.W;
     a.w_lo = S.owner ? S.shard * S.Wl : 0;
     a.w_hi = S.owner ? std::min(S.W, (S.shard + 1) * S.Wl) : S.W;
+    a.mw = fused_mask_words(S);
     a.tab_lo = S.tab_lo;
     a.tab_n = S.tab_n;
     a.cap_check = S.pred_active ? 1 : 0;
     a.early_exit = S.opts.full_scan ? 0 : 1;  // full-scan evaluates every node for every row
+    if (sg.n_slots <= kbg::kInlineShapes) {
+      std::copy(sg.h_shapes, sg.h_shapes + sg.n_slots, a.inl);
+    } else if (!(a.shapes = dev_ptr(S, sg.h_shapes))) {
+      return fail(KBG_E_HIP, "hipHostGetDevicePointer of a stage buffer failed");
+    }
+    if (sg.h_rowshape && !(a.row_shape = dev_ptr(S, sg.h_rowshape)))
+      return fail(KBG_E_HIP, "hipHostGetDevicePointer of a stage buffer failed");
+    a.info = dev_ptr(S, sg.h_down);
+    a.masks = reinterpret_cast<kbg::MaskPair*>(dev_ptr(S, sg.h_down + fused_mask_off(S.K)));
+    if (!a.info || !a.masks) return fail(KBG_E_HIP, "hipHostGetDevicePointer of a stage buffer failed");
     const bool avail = S.owner && S.comm;
-    if (avail) {  // owner-resolve: the rows' availability over the ranks, summed in the same round trip
+    if (avail) {  // owner-resolve: the shapes' availability over the ranks, summed in the same round trip
       a.avail = S.d_down;
       a.avail_bit = 1u << S.shard;
     }
@@ -650,11 +667,13 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
     trace_add("l.firstfit");
 
     if (avail) {
+      const int32_t ns = sg.n_slots;
       if (S.comm->nccl) {  // (a communicator without RCCL — R sessions of one process, tools — sums on the host)
-        const ncclResult_t nr = ncclAllReduce(S.d_down, S.d_down, (size_t)G, ncclUint32, ncclSum, S.comm->nccl, S.stream);
+        const ncclResult_t nr = ncclAllReduce(S.d_down, S.d_down, (size_t)ns, ncclUint32, ncclSum, S.comm->nccl, S.stream);
         if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
       }
-      HIP_TRY(hipMemcpyAsync(sg.h_down + G + total, S.d_down, (size_t)G * 4, hipMemcpyDeviceToHost, S.stream));
+      HIP_TRY(hipMemcpyAsync(sg.h_down + fused_avail_off(S.K, a.mw), S.d_down, (size_t)ns * 4, hipMemcpyDeviceToHost,
+                             S.stream));
     }
     HIP_TRY(hipEventRecord(sg.ev[6], S.stream));
     trace_add("l.event");
@@ -667,6 +686,7 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   sg.fused = false;
   // replicated sharded sessions (pod affinity, backfill on a communicator):
   // every rank scans its slot, the slots are all-gathered, every rank selects
+  const uint32_t total = sg.h_capoff[G];
   const size_t up_bytes = (size_t)Gp * sizeof(kbg::TaskRec) + (size_t)(G + 1) * 4;
   const kbg::TaskRec* d_tasks = (const kbg::TaskRec*)S.d_up;
   const uint32_t* d_capoff = (const uint32_t*)(S.d_up + (size_t)Gp * sizeof(kbg::TaskRec));
@@ -701,8 +721,16 @@ kbg_status device_wait(Session& S, kbg::Stage& sg) {
   if (kbg_status st = comm_wait(S, sg.ev[6]); st != KBG_OK) return st;
   sg.inflight = false;
   const int32_t G = sg.G;
-  sg.h_count = sg.h_down;
-  sg.h_cand = sg.h_down + G;
+  if (sg.fused) {
+    sg.h_info = sg.h_down;
+    sg.h_mask = reinterpret_cast<kbg::MaskPair*>(sg.h_down + fused_mask_off(S.K));
+    sg.mw = fused_mask_words(S);
+    sg.w_lo = S.owner ? S.shard * S.Wl : 0;
+    sg.h_avail = sg.h_down + fused_avail_off(S.K, sg.mw);
+  } else {
+    sg.h_count = sg.h_down;
+    sg.h_cand = sg.h_down + G;
+  }
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, sg.ev[0], sg.ev[1]));
   S.stats.scan_kernel_ms += ms;
@@ -808,9 +836,28 @@ constexpr int32_t kContendedSlack = 4096;  // the same in a rescan of the conten
 constexpr int32_t kFullScanGrow = 1024;  // cap on a full-scan row's extra slots
 constexpr int32_t kFullScanK = 8192;     // default batch of the full-scan mode
 
+// Bytes of one stage's row buffer for batches of K tasks: the rows
+// (TaskRec, padded) and their candidate offsets, then (fused full-scan path)
+// each row's shape slot and the shape table.
+inline size_t up_bytes_for(int32_t K) {
+  const size_t rows = (size_t)kbg::kbg_pad_rows(K) * sizeof(kbg::TaskRec) + ((size_t)K + 1) * 4;
+  return ((rows + 15) & ~(size_t)15) + (((size_t)K * 4 + 15) & ~(size_t)15) + (size_t)K * sizeof(kbg::TaskRec);
+}
+
+// A row whose scan found no fitting node in a complete walk of the table.
+inline bool row_fits_nowhere(const kbg::Stage& g, int32_t r) {
+  if (g.fused) return (g.h_info[g.row_slot[r]] & (kbg::kInfoAnyBit | kbg::kCountIncompleteBit)) == 0;
+  return g.h_count[r] == 0;
+}
+// A row with some fitting node in the words its scan covered (listed or not).
+inline bool row_fits_somewhere(const kbg::Stage& g, int32_t r) {
+  if (g.fused) return (g.h_info[g.row_slot[r]] & kbg::kInfoAnyBit) != 0;
+  return g.h_count[r] != 0;
+}
+
 struct Grouper {
   Session& S;
-  std::vector<int32_t> shape_row, shape_stamp, count;
+  std::vector<int32_t> shape_row, shape_stamp, count, ext_slot;
   int32_t stamp = 0;
   explicit Grouper(Session& s) : S(s), shape_row(s.n_shapes, -1), shape_stamp(s.n_shapes, -1) {}
   // `slack`: grouped mode's extra candidate slots per shape row (the
@@ -888,6 +935,35 @@ struct Grouper {
       else if (sg.row_ext[g] != g) want = 0;  // its list is the shape's long one (Resolver: alias rows)
       else want = (uint32_t)(S.M + std::min(2 * count[g] + (g >> 3) + 64, grow_cap));
       sg.h_capoff[g + 1] = sg.h_capoff[g] + want;
+      // the fused kernel reads the row's want from its flags (kbg_device.hpp FirstFitArgs)
+      sg.h_tasks[g].flags = (sg.h_tasks[g].flags & kbg::kRowRelZeroFits) | (int32_t)(want << kbg::kRowWantShift);
+    }
+    // Fused path: grouped rows are their own shapes; full-scan rows name the
+    // slot of their shape (the shape's last row, which writes the list; the
+    // shape table holds that row's record, so no launch reads all G records)
+    sg.row_slot.resize(G);
+    if (S.opts.full_scan) {
+      const size_t rows_b = ((size_t)Gp * sizeof(kbg::TaskRec) + ((size_t)G + 1) * 4 + 15) & ~(size_t)15;
+      sg.h_rowshape = (uint32_t*)(sg.h_up + rows_b);
+      sg.h_shapes = (kbg::TaskRec*)(sg.h_up + rows_b + (((size_t)G * 4 + 15) & ~(size_t)15));
+      ext_slot.resize(G);
+      int32_t ns = 0;
+      for (int32_t g = 0; g < G; ++g)
+        if (sg.row_ext[g] == g) {
+          ext_slot[g] = ns;
+          sg.h_shapes[ns++] = sg.h_tasks[g];
+        }
+      for (int32_t g = 0; g < G; ++g) {
+        const int32_t sl = ext_slot[sg.row_ext[g]];
+        sg.row_slot[g] = sl;
+        sg.h_rowshape[g] = (uint32_t)sl | (sg.row_ext[g] == g ? kbg::kRowWriter : 0u);
+      }
+      sg.n_slots = ns;
+    } else {
+      for (int32_t g = 0; g < G; ++g) sg.row_slot[g] = g;
+      sg.h_rowshape = nullptr;
+      sg.h_shapes = sg.h_tasks;
+      sg.n_slots = G;
     }
     return G;
   }
@@ -926,7 +1002,79 @@ struct Resolver {
   bool dirty(int32_t t, int32_t nd) const {
     return mark[nd] > base || (S.has_aff && S.mwmark[(size_t)S.task_class[t] * S.W + (nd >> 6)] > base);
   }
+  // the host mirror's verdict on node nd for task t, for a candidate touched
+  // since the scan: 1 Allocate, 2 Pipeline, 0 it no longer fits
+  int recheck(int32_t t, int32_t nd, const Res& r) const {
+    if (S.pred_active && S.ntasks[nd] >= S.maxtasks[nd]) return 0;
+    if ((S.has_ports || S.has_aff) &&
+        !((S.h_class_mask[(size_t)S.task_class[t] * S.W + (nd >> 6)] >> (nd & 63)) & 1ull))
+      return 0;
+    if (S.be_task[t]) return 1;  // backfill: PredicateFn only, always ssn.Allocate
+    if (kbg::res_le(r, S.idle[nd])) return 1;
+    if (kbg::res_le(r, S.rel[nd])) return 2;
+    return 0;
+  }
+  // Fused stages: the row's shape list as word masks (kbg_device.hpp
+  // FirstFitArgs); the cursor is the next node to look at, in node order.
+  int resolve_mask(int32_t g, int32_t t, int32_t* node, int32_t* kind) {
+    const int32_t sl = sg->row_slot[g];
+    const uint32_t info = sg->h_info[sl];
+    const int32_t wl = sg->w_lo;
+    const kbg::MaskPair* m = sg->h_mask + (size_t)sl * sg->mw - wl;  // indexed by global word
+    const int32_t end = (wl + (int32_t)(info & kbg::kInfoWordsMask)) * 64;
+    const Res& r = S.treq[t];
+    int32_t sh = -1;
+    int32_t& k = cursor[g];
+    if (k < wl * 64) k = wl * 64;
+    if (S.opts.full_scan) {
+      sh = sg->row_shape[g];
+      if (skip_stamp[sh] == skip_gen) k = std::max(k, shape_skip[sh]);  // what earlier rows of the shape rejected
+    }
+    int res = -1;
+    int64_t steps = 0, rechecks = 0;
+    while (k < end) {
+      const int32_t w = k >> 6;
+      const uint64_t f = m[w].f & (~0ull << (k & 63));
+      if (!f) {
+        k = (w + 1) << 6;
+        continue;
+      }
+      const int32_t nd = (w << 6) | __builtin_ctzll(f);
+      k = nd;
+      ++steps;
+      if (S.panic_node[nd]) {
+        res = RES_PANIC;
+        break;
+      }
+      if (!dirty(t, nd)) {
+        *node = nd;
+        *kind = ((m[w].i >> (nd & 63)) & 1ull) ? KBG_KIND_ALLOCATE : KBG_KIND_PIPELINE;
+        res = RES_OK;
+        break;
+      }
+      ++rechecks;  // touched since the scan: re-check on the host mirror
+      const int v = recheck(t, nd, r);
+      if (v) {
+        *node = nd;
+        *kind = v == 1 ? KBG_KIND_ALLOCATE : KBG_KIND_PIPELINE;
+        res = RES_OK;
+        break;
+      }
+      ++k;
+    }
+    S.stats.resolve_steps += steps;
+    S.stats.resolve_rechecks += rechecks;
+    if (sh >= 0 && res != RES_PANIC) {  // nodes before k are infeasible for the shape from now on
+      shape_skip[sh] = k;
+      skip_stamp[sh] = skip_gen;
+    }
+    if (res >= 0) return res;
+    if (info & kbg::kCountIncompleteBit) return RES_TRUNC;
+    *node = -1;
+    return RES_OK;
+  }
   int resolve(int32_t g, int32_t t, int32_t* node, int32_t* kind) {
+    if (sg->fused) return resolve_mask(g, t, node, kind);
     if (S.opts.full_scan && sg->h_capoff[g + 1] == sg->h_capoff[g])
       g = sg->row_ext[g];  // an alias row: its shape's long list (Grouper::build), this row's cursor
     const uint32_t cnt = sg->h_count[g];
@@ -2339,9 +2487,12 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   HIP_TRY(hipEventCreateWithFlags(&S.comm_ev, hipEventDisableTiming));
   S.stage_pending = false;
   if ((st = alloc_soa(S, &S.d_nodes)) || (st = alloc_soa(S, &S.d_nodes0))) return st;
-  const size_t up_cap = (size_t)kbg::kbg_pad_rows(S.K) * sizeof(kbg::TaskRec) + ((size_t)S.K + 1) * 4;
+  const size_t up_cap = up_bytes_for(S.K);
   S.up_cap = up_cap;
-  const size_t down_cap = 2 * (size_t)S.K + (size_t)S.cand_cap;  // counts, candidates, owner-resolve availability
+  // counts, candidates and owner-resolve availability (replicated path), or
+  // per-slot info, the slots' word masks and availability (fused path); u32 units
+  const size_t down_cap =
+      std::max(2 * (size_t)S.K + (size_t)S.cand_cap, fused_down_words(S.K, fused_mask_words(S)));
   if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) || (st = dalloc(S, &S.d_up, up_cap)) ||
       (st = dalloc(S, &S.d_bits, S.comm ? (size_t)S.R * 2 * S.K * kbg::kbg_slot_words(S.Wl) : 1)) ||
       (st = dalloc(S, &S.d_down, down_cap)))
@@ -3345,9 +3496,13 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       std::swap(sg.h_up, b->st.h_up);
       sg.h_tasks = (kbg::TaskRec*)sg.h_up;
       sg.h_capoff = b->st.h_capoff;  // inside the buffer sg now holds
+      sg.h_rowshape = b->st.h_rowshape;
+      sg.h_shapes = b->st.h_shapes;
+      sg.n_slots = b->st.n_slots;
       sg.row_of.swap(b->st.row_of);
       sg.row_shape.swap(b->st.row_shape);
       sg.row_ext.swap(b->st.row_ext);
+      sg.row_slot.swap(b->st.row_slot);
       G = b->G;
       b->G = -1;
     } else {
@@ -3369,7 +3524,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   // decides every task).
   auto learn_failed = [&](const kbg::Stage& g) {
     for (int32_t r = 0; r < g.G; ++r)
-      if (g.h_count[r] == 0) failed[g.row_shape[r]].store(1, std::memory_order_relaxed);
+      if (row_fits_nowhere(g, r)) failed[g.row_shape[r]].store(1, std::memory_order_relaxed);
   };
   // opt-in cycle counters of the in-order commit (KBG_PROFILE_RESOLVE=1):
   // candidate walk, host mirror, decision log, whole loop
@@ -3781,7 +3936,7 @@ struct ShardIO {
   virtual kbg_status scan_avail(Session& S, kbg::Stage& sg, int32_t G, int32_t base, uint32_t* avail) {
     kbg_status st = scan(S, sg, G, base);
     if (st != KBG_OK) return st;
-    for (int32_t g = 0; g < G; ++g) avail[g] = sg.h_count[g] != 0 ? (1u << S.shard) : 0u;  // any node (listed or not)
+    for (int32_t g = 0; g < G; ++g) avail[g] = row_fits_somewhere(sg, g) ? (1u << S.shard) : 0u;  // any node (listed or not)
     return allreduce(avail, G, true);
   }
   // this rank's committed rows (and class-mask words) to the table its scans read
@@ -3837,8 +3992,7 @@ struct RcclIO final : ShardIO {
   kbg_status scan_avail(Session& S2, kbg::Stage& sg, int32_t G, int32_t base, uint32_t* avail) override {
     kbg_status st = device_scan(S2, sg, G, base);
     if (st != KBG_OK) return st;
-    const uint32_t* h_avail = sg.h_down + G + sg.h_capoff[G];
-    std::copy(h_avail, h_avail + G, avail);
+    for (int32_t g = 0; g < G; ++g) avail[g] = sg.h_avail[sg.row_slot[g]];  // summed per shape slot
     return KBG_OK;
   }
   kbg_status allreduce(uint32_t* buf, size_t n, bool sum) override {

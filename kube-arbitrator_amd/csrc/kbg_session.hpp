@@ -194,6 +194,16 @@ struct Stage {
   std::vector<int32_t> row_of;       // batch entry -> evaluation row
   std::vector<int32_t> row_shape;    // evaluation row -> (class, request) shape
   std::vector<int32_t> row_ext;      // full-scan: the last (longest-list) row of the row's shape in this scan
+  // fused path (kbg_firstfit_kernel): rows map to shapes (grouped: row g is
+  // shape g); each shape's list comes back as the masks of the words it covers
+  int32_t n_slots = 0;               // shapes of the launch
+  std::vector<int32_t> row_slot;     // row -> its shape's slot
+  uint32_t* h_rowshape = nullptr;    // full-scan: row -> slot | kRowWriter (inside h_up)
+  TaskRec* h_shapes = nullptr;       // full-scan: the shape table (inside h_up; grouped: h_tasks)
+  uint32_t* h_info = nullptr;        // per slot: words covered | kInfoAnyBit | kCountIncompleteBit
+  MaskPair* h_mask = nullptr;        // per slot: mw word masks from word w_lo
+  uint32_t* h_avail = nullptr;       // owner-resolve: per slot, the ranks with a fitting node (summed)
+  int32_t mw = 0, w_lo = 0;
   int32_t G = 0;
   int32_t base = 0;                  // the scan saw every node delta of resolutions with stamp <= base
   bool inflight = false;             // launched, results not yet collected

@@ -167,8 +167,8 @@ kbg_status host_open(Session& S, const kbg_snapshot* snap, const kbg_options* o,
   S.n_shapes_cap = std::max(S.n_shapes, 64);
   S.cand_cap = S.opts.full_scan ? (int64_t)S.K * S.M + (int64_t)std::min(S.K, S.n_shapes_cap) * (kFullScanGrow + S.M)
                                 : (int64_t)S.K * (kGroupSlack + 1);
-  const size_t up_cap = (size_t)kbg::kbg_pad_rows(S.K) * sizeof(kbg::TaskRec) + ((size_t)S.K + 1) * 4;
-  const size_t down_cap = (size_t)S.K + (size_t)S.cand_cap;
+  const size_t up_cap = up_bytes_for(S.K);
+  const size_t down_cap = (size_t)S.K + (size_t)S.cand_cap;  // the host scan's count + candidate lists
   for (kbg::Stage& g : S.stages) {
     g.h_up = (char*)std::malloc(up_cap);
     g.h_down = (uint32_t*)std::malloc(down_cap * 4);
@@ -196,6 +196,7 @@ struct HostIO : ShardIO {
   kbg_status scan(Session& S, kbg::Stage& sg, int32_t G, int32_t base) override {
     sg.G = G;
     sg.base = base;
+    sg.fused = false;  // candidate lists, as kbg_scan_kernel + kbg_select_kernel produce them
     sg.h_count = sg.h_down;
     sg.h_cand = sg.h_down + G;
     for (int32_t g = 0; g < G; ++g) {
@@ -367,8 +368,7 @@ struct DeviceLocalIO final : ShardIO {
   kbg_status scan_avail(Session& S, kbg::Stage& sg, int32_t G, int32_t base, uint32_t* avail) override {
     kbg_status st = device_scan(S, sg, G, base);
     if (st != KBG_OK) return st;
-    const uint32_t* h_avail = sg.h_down + G + sg.h_capoff[G];  // kbg_avail_kernel: this rank's bit per row
-    std::copy(h_avail, h_avail + G, avail);
+    for (int32_t g = 0; g < G; ++g) avail[g] = sg.h_avail[sg.row_slot[g]];  // this rank's bit per shape slot
     return allreduce(avail, G, true);
   }
 };
@@ -479,7 +479,8 @@ extern "C" int32_t kbg_tool_firstfit_stamps(const kbg_snapshot* snap, const kbg_
       free_device(S);
       return -2;
     }
-  const int32_t n_wg = std::min((rows + 15) / 16, max_wg);
+  const int32_t per = kbg::firstfit_rows(rows);
+  const int32_t n_wg = std::min((rows + per - 1) / per, max_wg);
   const bool ok = kbg::read_ff_stamps(out, n_wg) == hipSuccess;
   free_device(S);
   return ok ? n_wg : -3;
