@@ -296,9 +296,10 @@ inline int32_t kbg_victim_words(int32_t n_nodes) { return (n_nodes + 31) / 32; }
 hipError_t launch_victim_scan(const VictimScan& p, const VictimTables& t, uint32_t* stop_bits, uint32_t* panic_bits,
                               hipStream_t stream, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 // Nodes of the scanned range with more than 128 candidates (`rows`, table
-// rows), evaluated after launch_victim_scan and ORed into its device words.
+// rows), evaluated after launch_victim_scan: ORed into its device words, or
+// (row_out non-null) one byte per row, bit 0 stop and bit 1 panic.
 hipError_t launch_victim_big(const VictimScan& p, const VictimTables& t, const int32_t* rows, int32_t n_rows,
-                             uint32_t* stop_bits, uint32_t* panic_bits, hipStream_t stream);
+                             uint32_t* stop_bits, uint32_t* panic_bits, uint8_t* row_out, hipStream_t stream);
 // Host-side changes before a scan, read in place from host-mapped memory:
 // node rows (NodeInfo.Tasks count / Idle / Releasing) and victim-table
 // entries, in one launch.

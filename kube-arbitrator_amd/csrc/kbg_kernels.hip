@@ -857,12 +857,17 @@ __global__ __launch_bounds__(64 * kVictimBlockWaves) void kbg_victim_kernel(Vict
 __global__ __launch_bounds__(256) void kbg_victim_big_kernel(VictimScan p, VictimTables t,
                                                              const int32_t* __restrict__ rows, int32_t n_rows,
                                                              uint32_t* __restrict__ stop_bits,
-                                                             uint32_t* __restrict__ panic_bits) {
+                                                             uint32_t* __restrict__ panic_bits,
+                                                             uint8_t* __restrict__ row_out) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n_rows) return;
   const int row = rows[i];
   const uint32_t key = victim_node<kVictimChunks>(p, t, row, lane);
+  if (row_out) {  // one byte per big node (host-mapped; the host ORs them into its maps): bit 0 stop, bit 1 panic
+    if (lane == 0) row_out[i] = key == 0xffffffffu ? 0u : (uint8_t)(1u | ((key & 1u) << 1));
+    return;
+  }
   if (key == 0xffffffffu || lane != 0) return;
   const int n = p.node_lo + row;
   atomicOr(stop_bits + (n >> 5), 1u << (n & 31));
@@ -870,10 +875,10 @@ __global__ __launch_bounds__(256) void kbg_victim_big_kernel(VictimScan p, Victi
 }
 
 hipError_t launch_victim_big(const VictimScan& p, const VictimTables& t, const int32_t* rows, int32_t n_rows,
-                             uint32_t* stop_bits, uint32_t* panic_bits, hipStream_t stream) {
+                             uint32_t* stop_bits, uint32_t* panic_bits, uint8_t* row_out, hipStream_t stream) {
   if (n_rows <= 0) return hipSuccess;
   hipLaunchKernelGGL(kbg_victim_big_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, stream, p, t, rows, n_rows, stop_bits,
-                     panic_bits);
+                     panic_bits, row_out);
   return hipGetLastError();
 }
 

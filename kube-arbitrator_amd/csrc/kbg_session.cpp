@@ -544,6 +544,10 @@ void free_device(Session& S) {
   S.fit_d = nullptr;
   S.fit_cap = S.fit_out_cap = 0;
   if (S.h_vbits) (void)hipHostFree(S.h_vbits);
+  if (S.h_vbig) (void)hipHostFree(S.h_vbig);
+  S.h_vbig = nullptr;
+  S.h_vbig_dev = nullptr;
+  S.h_vbig_cap = 0;
   if (S.h_sdeltas) (void)hipHostFree(S.h_sdeltas);
   if (S.c_run_pinned) (void)hipHostFree(S.c_run_pinned);
   S.c_run_pinned = nullptr;
@@ -551,6 +555,7 @@ void free_device(Session& S) {
   S.h_vbits = nullptr;
   S.h_sdeltas = nullptr;
   S.vt_ready = false;
+  S.vt_sh_valid = false;
   S.vt_allocs.clear();
   S.h_deltas = nullptr;
   for (void* p : S.d_allocs) (void)hipFree(p);
@@ -4476,6 +4481,19 @@ kbg_status backfill_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
 
 void vt_delta(Session& S, int32_t kind, int32_t index, double a, double b, double c) {
   S.sdeltas.push_back(kbg::StateDelta{kind, index, {a, b, c}});
+  if (!S.vt_sh_valid) return;
+  switch (kind) {  // the device holds it from the next push on
+    case 0: S.vt_sh_run[index] = a != 0.0; break;
+    case 1: S.vt_sh_ready[index] = (int32_t)a; break;
+    case 2:
+    case 3: {
+      double* v = (kind == 2 ? S.vt_sh_jalloc : S.vt_sh_qalloc).data() + 3 * (size_t)index;
+      v[0] = a;
+      v[1] = b;
+      v[2] = c;
+      break;
+    }
+  }
 }
 
 // Applies the queued state changes. Each carries the entry's new value, so
@@ -4555,7 +4573,7 @@ kbg_status victim_push(Session& S, const std::vector<int32_t>& touched) {
 }
 
 // Device copies of the victim tables; the live parts (running flags, gang
-// readiness, drf / proportion allocations) are re-uploaded at every action.
+// readiness, drf / proportion allocations) follow the host at every action.
 kbg_status vt_setup(Session& S) {
   const size_t J = (size_t)std::max(1, S.n_jobs),
                Q = (size_t)std::max(1, S.n_queues);
@@ -4571,6 +4589,7 @@ kbg_status vt_setup(Session& S) {
   S.vt_stale = false;
   if (!S.vt_ready) {
     const size_t a0 = S.d_allocs.size();
+    S.vt_sh_valid = false;  // new device tables: the live state goes up whole
     S.W32 = kbg::kbg_victim_words(S.n_nodes);
     kbg::VictimTables& v = S.vt;
     v.ntasks = S.d_nodes.ntasks;
@@ -4622,9 +4641,17 @@ kbg_status vt_setup(Session& S) {
     S.vt_allocs.assign(S.d_allocs.begin() + a0, S.d_allocs.end());
     HIP_TRY(hipMemset(S.d_vbits, 0, 2 * (size_t)S.W32 * sizeof(uint32_t)));  // other ranks' words stay 0
     if (!S.h_vbits) {
-      HIP_TRY(hipHostMalloc((void**)&S.h_vbits, std::max<size_t>(2 * (size_t)S.W32 * sizeof(uint32_t), 64),  // W32 = 0: no nodes
-                            hipHostMallocCoherent | hipHostMallocMapped));
+      const size_t vb = std::max<size_t>(2 * (size_t)S.W32 * sizeof(uint32_t), 64);  // W32 = 0: no nodes
+      HIP_TRY(hipHostMalloc((void**)&S.h_vbits, vb, hipHostMallocCoherent | hipHostMallocMapped));
       HIP_TRY(hipHostGetDevicePointer((void**)&S.h_vbits_dev, S.h_vbits, 0));
+      std::memset(S.h_vbits, 0, vb);  // the scan writes the bytes of its node blocks; the rest stays 0
+    }
+    if (S.h_vbig_cap < std::max<size_t>(1, S.big_rows.size())) {
+      if (S.h_vbig) (void)hipHostFree(S.h_vbig);
+      S.h_vbig = nullptr;
+      S.h_vbig_cap = std::max<size_t>(64, S.big_rows.size());
+      HIP_TRY(hipHostMalloc((void**)&S.h_vbig, S.h_vbig_cap, hipHostMallocCoherent | hipHostMallocMapped));
+      HIP_TRY(hipHostGetDevicePointer((void**)&S.h_vbig_dev, S.h_vbig, 0));
     }
     // per job, the nodes holding its tasks Running at open (the only tasks a
     // victim fn can see; their job's readiness / allocation feed the fns)
@@ -4666,34 +4693,45 @@ kbg_status vt_setup(Session& S) {
     S.vt_ready = true;
     HIP_TRY(hipStreamSynchronize(S.stream));  // host vectors end here
   }
-  // live state
-  std::vector<double> ja(3 * J, 0.0), qa(3 * Q, 0.0);
-  for (int32_t j = 0; j < S.n_jobs; ++j) {
-    ja[3 * j] = S.fin.jalloc[j].c;
-    ja[3 * j + 1] = S.fin.jalloc[j].m;
-    ja[3 * j + 2] = S.fin.jalloc[j].g;
+  // live state: the first setup of the tables uploads it whole; later ones
+  // queue the entries that differ from what the device holds (vt_sh_*), which
+  // the first scan's prep launch applies (no copy, no synchronize here)
+  const size_t P = S.nt_task.size();
+  auto same3 = [](const double* a, const Res& r) {
+    return std::memcmp(a, &r.c, 8) == 0 && std::memcmp(a + 1, &r.m, 8) == 0 && std::memcmp(a + 2, &r.g, 8) == 0;
+  };
+  if (!S.vt_sh_valid || S.vt_sh_run.size() != P || S.vt_sh_ready.size() != (size_t)S.n_jobs ||
+      S.vt_sh_qalloc.size() != 3 * (size_t)S.n_queues) {
+    S.vt_sh_valid = true;
+    S.vt_sh_run.resize(P);
+    S.vt_sh_ready = S.committed_ready;
+    S.vt_sh_jalloc.assign(3 * J, 0.0);
+    S.vt_sh_qalloc.assign(3 * Q, 0.0);
+    for (size_t k = 0; k < P; ++k) S.vt_sh_run[k] = S.trun[S.nt_task[k]];
+    for (int32_t j = 0; j < S.n_jobs; ++j) std::memcpy(&S.vt_sh_jalloc[3 * (size_t)j], &S.fin.jalloc[j].c, 24);
+    for (int32_t q = 0; q < S.n_queues; ++q) std::memcpy(&S.vt_sh_qalloc[3 * (size_t)q], &S.fin.qalloc[q].c, 24);
+    HIP_TRY(hipMemcpyAsync(S.vt.c_run, S.vt_sh_run.data(), std::max<size_t>(1, P), hipMemcpyHostToDevice, S.stream));
+    HIP_TRY(hipMemcpyAsync(S.vt.j_ready, S.vt_sh_ready.data(), (size_t)S.n_jobs * 4, hipMemcpyHostToDevice,
+                           S.stream));
+    HIP_TRY(hipMemcpyAsync(S.vt.j_alloc, S.vt_sh_jalloc.data(), S.vt_sh_jalloc.size() * 8, hipMemcpyHostToDevice,
+                           S.stream));
+    HIP_TRY(hipMemcpyAsync(S.vt.q_alloc, S.vt_sh_qalloc.data(), S.vt_sh_qalloc.size() * 8, hipMemcpyHostToDevice,
+                           S.stream));
+    HIP_TRY(hipStreamSynchronize(S.stream));
+    S.sdeltas.clear();
+  } else {
+    for (size_t k = 0; k < P; ++k)
+      if (S.vt_sh_run[k] != S.trun[S.nt_task[k]]) vt_delta(S, 0, (int32_t)k, S.trun[S.nt_task[k]] ? 1.0 : 0.0, 0, 0);
+    for (int32_t j = 0; j < S.n_jobs; ++j) {
+      if (S.vt_sh_ready[j] != S.committed_ready[j]) vt_delta(S, 1, j, (double)S.committed_ready[j], 0, 0);
+      const Res& a = S.fin.jalloc[j];
+      if (!same3(&S.vt_sh_jalloc[3 * (size_t)j], a)) vt_delta(S, 2, j, a.c, a.m, a.g);
+    }
+    for (int32_t q = 0; q < S.n_queues; ++q) {
+      const Res& a = S.fin.qalloc[q];
+      if (!same3(&S.vt_sh_qalloc[3 * (size_t)q], a)) vt_delta(S, 3, q, a.c, a.m, a.g);
+    }
   }
-  for (int32_t q = 0; q < S.n_queues; ++q) {
-    qa[3 * q] = S.fin.qalloc[q].c;
-    qa[3 * q + 1] = S.fin.qalloc[q].m;
-    qa[3 * q + 2] = S.fin.qalloc[q].g;
-  }
-  const size_t P = std::max<size_t>(1, S.nt_task.size());
-  if (S.c_run_pinned_cap < P) {  // pinned staging: the upload is one DMA, not a pageable copy
-    if (S.c_run_pinned) (void)hipHostFree(S.c_run_pinned);
-    S.c_run_pinned = nullptr;
-    S.c_run_pinned_cap = 0;
-    HIP_TRY(hipHostMalloc((void**)&S.c_run_pinned, std::max<size_t>(P, 64), hipHostMallocDefault));
-    S.c_run_pinned_cap = P;
-  }
-  for (size_t k = 0; k < S.nt_task.size(); ++k) S.c_run_pinned[k] = S.trun[S.nt_task[k]];
-  HIP_TRY(hipMemcpyAsync(S.vt.c_run, S.c_run_pinned, S.nt_task.size(), hipMemcpyHostToDevice, S.stream));
-  HIP_TRY(hipMemcpyAsync(S.vt.j_ready, S.committed_ready.data(), (size_t)S.n_jobs * 4, hipMemcpyHostToDevice,
-                         S.stream));
-  HIP_TRY(hipMemcpyAsync(S.vt.j_alloc, ja.data(), ja.size() * 8, hipMemcpyHostToDevice, S.stream));
-  HIP_TRY(hipMemcpyAsync(S.vt.q_alloc, qa.data(), qa.size() * 8, hipMemcpyHostToDevice, S.stream));
-  HIP_TRY(hipStreamSynchronize(S.stream));
-  S.sdeltas.clear();
   S.fin.jready = S.committed_ready;  // the job order keys read the live readiness
   return KBG_OK;
 }
@@ -4994,22 +5032,24 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
     if (st != KBG_OK) return st;
     L.touched.clear();
     ++L.stamp;
-    uint32_t* bits = S.d_vbits;
+    // one process: the scan writes its stop bytes straight into the mapped
+    // host words and the big-node kernel one byte per big node (no copy);
+    // sharded: device words, OR-reduced over the ranks, then copied
+    const bool mapped = !S.comm;
+    uint32_t* bits = mapped ? S.h_vbits_dev : S.d_vbits;
     const bool timed = (S.stats.victim_scans & 15) == 0 && p.node_n > 0;  // HIP-event time of every 16th launch
     HIP_TRY(kbg::launch_victim_scan(p, S.vt, bits, bits + S.W32, S.stream, timed ? S.ev[0] : nullptr,
                                     timed ? S.ev[1] : nullptr));
-    if (!S.big_rows.empty())  // nodes with more than 128 candidates: ORed into the same words
+    if (!S.big_rows.empty())  // nodes with more than 128 candidates
       HIP_TRY(kbg::launch_victim_big(p, S.vt, S.d_big_rows, (int32_t)S.big_rows.size(), bits, bits + S.W32,
-                                     S.stream));
-    const uint32_t* done_bits = S.d_vbits;
-    if (S.comm) {  // disjoint words of the ranks: element-wise max is their OR
+                                     mapped ? S.h_vbig_dev : nullptr, S.stream));
+    if (!mapped) {  // disjoint words of the ranks: element-wise max is their OR
       const ncclResult_t nr =
           ncclAllReduce(S.d_vbits, S.d_vbits_red, 2 * (size_t)S.W32, ncclUint32, ncclMax, S.comm->nccl, S.stream);
       if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
-      done_bits = S.d_vbits_red;
+      HIP_TRY(hipMemcpyAsync(S.h_vbits, S.d_vbits_red, 2 * (size_t)S.W32 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                             S.stream));
     }
-    HIP_TRY(hipMemcpyAsync(S.h_vbits, done_bits, 2 * (size_t)S.W32 * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                           S.stream));
     if (kbg_status st2 = comm_sync(S); st2 != KBG_OK) return st2;
     S.vstage_busy = false;
     if (timed) {
@@ -5025,6 +5065,14 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
       vc.stop[w] = hb[w];
       vc.panic[w] = hb[S.W32 + w];
     }
+    if (mapped)
+      for (size_t i = 0; i < S.big_rows.size(); ++i) {
+        const uint8_t v = S.h_vbig[i];
+        if (!v) continue;
+        const int32_t n = S.tab_lo + S.big_rows[i];
+        vc.stop[n >> 5] |= 1u << (n & 31);
+        if (v & 2) vc.panic[n >> 5] |= 1u << (n & 31);
+      }
     std::fill(vc.unk.begin(), vc.unk.end(), 0u);
     vc.lb = 0;
     for (int32_t hn : S.huge_nodes) vc.unk[hn >> 5] |= 1u << (hn & 31);  // not scanned on the device

@@ -319,6 +319,14 @@ struct Session {
   std::vector<int32_t> task_node;             // node index of a task's NodeName (-1: not a session node)
   std::vector<kbg_eviction> evictions;        // committed cache.Evict calls
   std::vector<int32_t> t_pos;                 // a task's position in the candidate lists (-1: none)
+  // what the device victim tables hold of the live state (running flags per
+  // candidate position, gang readiness, drf / proportion allocations): an
+  // action's start sends only the entries that differ (StateDelta, read in
+  // place from mapped memory) instead of re-uploading the arrays
+  bool vt_sh_valid = false;
+  std::vector<uint8_t> vt_sh_run;
+  std::vector<int32_t> vt_sh_ready;
+  std::vector<double> vt_sh_jalloc, vt_sh_qalloc;  // [3 x J], [3 x Q]
   uint8_t* c_run_pinned = nullptr;            // running flags in candidate order (pinned upload staging)
   size_t c_run_pinned_cap = 0;
   std::vector<uint32_t> sd_seen[4];           // victim_push: last-write dedup stamps per StateDelta kind
@@ -413,6 +421,9 @@ struct Session {
   std::vector<void*> vt_allocs;                       // their HBM (freed when they are rebuilt)
   std::vector<int32_t> big_rows;                      // table rows of nodes with 129 .. kMaxNodeCandidates victim candidates
   std::vector<int32_t> huge_nodes;                    // nodes (global) with more: evaluated on the host (host_stop)
+  uint8_t* h_vbig = nullptr;                          // mapped: the big-node kernel's verdict per big row
+  uint8_t* h_vbig_dev = nullptr;
+  size_t h_vbig_cap = 0;
   int32_t* d_big_rows = nullptr;
 
   // ---- NodeInfo.Tasks keys (node_info.go:101-106): AddTask of a PodKey the

@@ -340,7 +340,7 @@ extern "C" int32_t kbg_tool_sharded_allocate_rank(const kbg_snapshot* snap, cons
 // rank's own words, the collectives are the in-process hub). Every rank but
 // rank 0 has its first 64-node word at w_lo > 0, so this runs exactly the
 // device code of a multi-GPU rank that a one-GPU box cannot host over RCCL
-// (kbg_select_kernel over [w_lo, w_hi), kbg_avail_kernel with bit 1 << r).
+// (kbg_firstfit_kernel over [w_lo, w_hi), availability bit 1 << r per shape).
 namespace {
 struct DeviceLocalIO final : ShardIO {
   LocalHub& hub;

@@ -2,8 +2,8 @@
 kbg_session.cpp allocate_sharded) with its device side on the MI355X: R real
 device sessions on device 0, rank r holding the node rows of 64-node words
 [r*Wl, (r+1)*Wl) (tools/engine_bench.cpp kbg_tool_sharded_allocate_device).
-Every rank but 0 starts at a word w_lo > 0, so kbg_scan_kernel,
-kbg_select_kernel over [w_lo, w_hi) and kbg_avail_kernel with bit 1 << r run
+Every rank but 0 starts at a word w_lo > 0, so kbg_firstfit_kernel over its
+own words [w_lo, w_hi), with its availability bit 1 << r per shape, runs
 exactly as on rank r of an R-GPU clique; only the collectives are the
 in-process hub instead of RCCL (RCCL refuses two ranks on one device).
 First-fit is the global minimum index (allocate.go:119-162): every rank's
