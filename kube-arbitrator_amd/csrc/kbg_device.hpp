@@ -214,14 +214,17 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
 // output may end. The writer row of shape s writes, for the words [w_lo,
 // w_lo + covered) in node order, the pair of 64-node masks {fits Idle or
 // Releasing, fits Idle} (static predicate, pod cap and LessEqual applied)
-// into masks[s * mw + (w - w_lo)], and info[s] = covered | kInfoAnyBit (some
-// node of the walked words fits) | kCountIncompleteBit (covered < w_hi -
-// w_lo: the list is cut after the word holding its want-th fit). Every fit of
+// into masks[s * mw + (w - w_lo)], and info[s * splits + part] = covered |
+// kInfoAnyBit (some node of the part's walked words fits) |
+// kCountIncompleteBit (covered < the part's words: the list is cut after the
+// word holding its want-th fit; never with `complete`). Every fit of
 // a covered word is in the masks, so the host reads the first-fit candidates
 // in node order by scanning bits. The shape table is in the kernel arguments
 // (n_shapes <= kInlineShapes: no PCIe read at launch) or host-mapped;
 // row_shape, info, masks, avail may be host-mapped (zero-copy).
 constexpr int kInlineShapes = 96;
+constexpr int kFfRoundWords = 128;  // words per round of the fused walk (one round: no early exit)
+constexpr int kFfMaxSplits = 8;
 constexpr uint32_t kRowWriter = 0x80000000u;
 constexpr int kRowWantShift = 1;
 constexpr uint32_t kInfoAnyBit = 0x20000000u;
@@ -245,6 +248,9 @@ struct FirstFitArgs {
   int32_t n_nodes, W, w_lo, w_hi, tab_lo, tab_n;
   int32_t cap_check;            // the predicates plugin's pod cap is on
   int32_t early_exit;           // stop once every row's list is full (production mode)
+  int32_t complete;             // every word's masks go out (want ignored): lists are never cut
+  int32_t splits, split_words;  // the words [w_lo, w_hi) in `splits` parts of split_words, one workgroup
+                                // each (a short batch's walk spread over more CUs); info is per (shape, part)
   TaskRec inl[kInlineShapes];
 };
 // Rows per workgroup of a launch of G rows (16, 24 or 32).

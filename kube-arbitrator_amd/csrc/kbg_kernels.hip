@@ -233,7 +233,7 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
 // change it); full-scan mode evaluates every node for every row (SURVEY
 // §8(d)).
 constexpr int kFfWaves = 16;
-constexpr int kFfMaxRound = 128;  // words per round (LDS: 2 x 128 x ROWS x 8 B); a multiple of kFfWaves
+constexpr int kFfMaxRound = kFfRoundWords;  // words per round (LDS: 2 x 128 x ROWS x 8 B); a multiple of kFfWaves
 // rows whose requests are read from LDS together
 template <bool INT_MODE>
 constexpr int kFfGroup = INT_MODE ? 4 : 2;
@@ -254,7 +254,9 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
   __shared__ uint32_t s_done[ROWS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g0 = blockIdx.x * ROWS;
+  const int rb = blockIdx.x / a.splits, part = blockIdx.x - rb * a.splits;  // row block, word part
+  const int g0 = rb * ROWS;
+  const int w_lo = a.w_lo + part * a.split_words, w_hi = min(a.w_hi, w_lo + a.split_words);
   FF_STAMP(0);
   if (wave == 0 && lane < ROWS) {
     const int g = min(g0 + lane, a.G - 1);  // rows past G evaluate a copy of the last row, write nothing
@@ -268,12 +270,12 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
     s_flags[lane] = (uint32_t)tr.flags;
     s_map[lane] = g0 + lane < a.G ? m : (m & ~kRowWriter);
   }
-  const int32_t tw = a.w_hi - a.w_lo;  // words this launch covers
+  const int32_t tw = w_hi - w_lo;  // words this workgroup covers
   if (tw <= 0) {  // no words (a session without nodes): empty complete lists, no table or mask read
     __syncthreads();
     if (wave == 0 && lane < ROWS && (s_map[lane] & kRowWriter)) {
       const uint32_t sh = s_map[lane] & ~kRowWriter;
-      a.info[sh] = 0u;
+      a.info[sh * a.splits + part] = 0u;
       if (a.avail) a.avail[sh] = 0u;
     }
     return;
@@ -308,9 +310,9 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
     w.nt = q[0];
     w.mt = q[a.stride];
   };
-  const int w_last = a.w_hi - 1;
+  const int w_last = w_hi - 1;
   Word cur;
-  load_word(min(a.w_lo + wave, w_last), cur);
+  load_word(min(w_lo + wave, w_last), cur);
   __syncthreads();
   FF_STAMP(1);
   // the extraction state of the rows this wave owns (rows wave, wave + 16)
@@ -322,7 +324,7 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
     found[i] = 0u;
     covered[i] = 0u;
     writer[i] = j < ROWS && (s_map[j] & kRowWriter);
-    want[i] = j < ROWS ? (s_flags[j] >> kRowWantShift) : 0u;
+    want[i] = j >= ROWS ? 0u : a.complete ? 0xffffffffu : (s_flags[j] >> kRowWantShift);
     done[i] = !writer[i];
   }
   const int lrow = lane < ROWS ? lane : 0;
@@ -331,10 +333,10 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
   // rounds are kFfMaxRound (a multiple of kFfWaves) words apart, so a wave's
   // words are c, c + kFfWaves, ... across rounds too; lanes >= ROWS load a
   // row's mask word they never use
-  uint64_t lane_mw = a.class_mask[(size_t)cls_l * a.W + min(a.w_lo + wave, w_last)];
+  uint64_t lane_mw = a.class_mask[(size_t)cls_l * a.W + min(w_lo + wave, w_last)];
 #pragma unroll 1
-  for (int r0 = a.w_lo; r0 < a.w_hi; r0 += kFfMaxRound) {
-    const int nw = min(kFfMaxRound, a.w_hi - r0);  // words of this round
+  for (int r0 = w_lo; r0 < w_hi; r0 += kFfMaxRound) {
+    const int nw = min(kFfMaxRound, w_hi - r0);  // words of this round
 #pragma unroll 1
     for (int k = wave; k < nw; k += kFfWaves) {     // this wave's words of the round
       // the row requests are re-read from LDS per word (kept in registers
@@ -368,10 +370,10 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
       cur = nxt;
       lane_mw = nxt_mw;
     }
-    if (r0 == a.w_lo) FF_STAMP(2);
+    if (r0 == w_lo) FF_STAMP(2);
     __syncthreads();
-    if (r0 == a.w_lo) FF_STAMP(3);
-    if (r0 == a.w_lo) FF_STAMP(4);
+    if (r0 == w_lo) FF_STAMP(3);
+    if (r0 == w_lo) FF_STAMP(4);
     // Extraction: the owner wave of row j takes its words 64 at a time. Lane
     // k holds word k's fit count; the exclusive prefix sum over lanes (one
     // ballot + mbcnt per bit of the count) is the list position of the word's
@@ -399,15 +401,15 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
         if (put) out[k] = MaskPair{f, s_i[k][j]};
         const uint32_t nput = (uint32_t)__popcll(__ballot(put));
         found[i] += tot;
-        covered[i] = (uint32_t)(r0 - a.w_lo + k0) + nput;
+        covered[i] = (uint32_t)(r0 - w_lo + k0) + nput;
         if (found[i] >= want[i]) {  // every later word starts at or past want
           done[i] = true;
           break;
         }
       }
     }
-    if (r0 == a.w_lo) FF_STAMP(5);
-    if (r0 + kFfMaxRound >= a.w_hi) break;  // the last round: no second barrier
+    if (r0 == w_lo) FF_STAMP(5);
+    if (r0 + kFfMaxRound >= w_hi) break;  // the last round: no second barrier
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
       const int j = wave + i * kFfWaves;
@@ -426,7 +428,8 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
     const uint32_t sh = s_map[j] & ~kRowWriter;
     // covered: the words written; a row whose walk ended with its list not
     // full covered every word of the walk (EARLY_EXIT: the rounds walked)
-    a.info[sh] = covered[i] | (covered[i] < (uint32_t)tw ? kCountIncompleteBit : 0u) | (found[i] ? kInfoAnyBit : 0u);
+    a.info[sh * a.splits + part] =
+        covered[i] | (covered[i] < (uint32_t)tw ? kCountIncompleteBit : 0u) | (found[i] ? kInfoAnyBit : 0u);
     if (a.avail) a.avail[sh] = found[i] ? a.avail_bit : 0u;
   }
   FF_STAMP(6);
@@ -435,7 +438,7 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
 template <bool INT_MODE, bool EARLY_EXIT>
 hipError_t launch_firstfit_rows(const FirstFitArgs& a, int rows, hipStream_t stream, hipEvent_t start,
                                 hipEvent_t stop) {
-  const dim3 grid((a.G + rows - 1) / rows), block(64 * kFfWaves);
+  const dim3 grid((a.G + rows - 1) / rows * a.splits), block(64 * kFfWaves);
   if (rows == 16)
     hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 16>), grid, block, 0, stream, start, stop, 0, a);
   else if (rows == 24)

@@ -479,7 +479,7 @@ int32_t soa_stride(const Session& S) { return std::max(64, (S.tab_n + 63) / 64 *
 // owner-resolve availability. mw = the words one launch covers (this rank's
 // words when the session is sharded).
 int32_t fused_mask_words(const Session& S) { return std::max(1, S.comm ? S.Wl : S.W); }
-inline size_t fused_mask_off(int32_t K) { return ((size_t)K + 3) & ~(size_t)3; }
+inline size_t fused_mask_off(int32_t K) { return ((size_t)K * kbg::kFfMaxSplits + 3) & ~(size_t)3; }
 inline size_t fused_avail_off(int32_t K, int32_t mw) { return fused_mask_off(K) + (size_t)K * mw * 4; }
 inline size_t fused_down_words(int32_t K, int32_t mw) { return fused_avail_off(K, mw) + (size_t)K; }
 size_t soa_bytes(const Session& S) { return (size_t)soa_stride(S) * (6 * 8 + 2 * 4); }
@@ -653,6 +653,21 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
     a.tab_n = S.tab_n;
     a.cap_check = S.pred_active ? 1 : 0;
     a.early_exit = S.opts.full_scan ? 0 : 1;  // full-scan evaluates every node for every row
+    // A table of one round (<= 128 words) is walked whole anyway: every
+    // word's masks go out, so no list is ever cut (no truncation rescans).
+    // Then a short batch's walk is split into word parts, one workgroup
+    // each, so its handful of row blocks spreads over the CUs instead of
+    // walking 5 words per wave on 6 of them.
+    const int32_t tw = a.w_hi - a.w_lo;
+    a.complete = tw <= kbg::kFfRoundWords ? 1 : 0;
+    a.splits = 1;
+    if (a.complete && !S.comm) {
+      const int32_t blocks = (G + kbg::firstfit_rows(G) - 1) / kbg::firstfit_rows(G);
+      a.splits = std::max(1, std::min({kbg::kFfMaxSplits, 256 / std::max(1, blocks), tw / 8}));
+    }
+    a.split_words = (tw + a.splits - 1) / a.splits;
+    a.splits = std::max(1, (tw + a.split_words - 1) / a.split_words);  // no empty part
+    sg.splits = a.splits;
     if (sg.n_slots <= kbg::kInlineShapes) {
       std::copy(sg.h_shapes, sg.h_shapes + sg.n_slots, a.inl);
     } else if (!(a.shapes = dev_ptr(S, sg.h_shapes))) {
@@ -728,6 +743,16 @@ kbg_status device_wait(Session& S, kbg::Stage& sg) {
   const int32_t G = sg.G;
   if (sg.fused) {
     sg.h_info = sg.h_down;
+    if (sg.splits > 1) {  // parts of a complete walk: the slot's list covers every word, fits if any part did
+      const int32_t P = sg.splits, tw = S.owner ? std::min(S.W, (S.shard + 1) * S.Wl) - S.shard * S.Wl : S.W;
+      sg.info_comb.resize(sg.n_slots);
+      for (int32_t sl = 0; sl < sg.n_slots; ++sl) {
+        uint32_t any = 0;
+        for (int32_t p = 0; p < P; ++p) any |= sg.h_down[(size_t)sl * P + p] & kbg::kInfoAnyBit;
+        sg.info_comb[sl] = (uint32_t)tw | any;
+      }
+      sg.h_info = sg.info_comb.data();
+    }
     sg.h_mask = reinterpret_cast<kbg::MaskPair*>(sg.h_down + fused_mask_off(S.K));
     sg.mw = fused_mask_words(S);
     sg.w_lo = S.owner ? S.shard * S.Wl : 0;

@@ -201,6 +201,8 @@ struct Stage {
   uint32_t* h_rowshape = nullptr;    // full-scan: row -> slot | kRowWriter (inside h_up)
   TaskRec* h_shapes = nullptr;       // full-scan: the shape table (inside h_up; grouped: h_tasks)
   uint32_t* h_info = nullptr;        // per slot: words covered | kInfoAnyBit | kCountIncompleteBit
+  int32_t splits = 1;                // word parts of the launch (one info word per slot and part)
+  std::vector<uint32_t> info_comb;   // splits > 1: the parts' info words combined per slot
   MaskPair* h_mask = nullptr;        // per slot: mw word masks from word w_lo
   uint32_t* h_avail = nullptr;       // owner-resolve: per slot, the ranks with a fitting node (summed)
   int32_t mw = 0, w_lo = 0;

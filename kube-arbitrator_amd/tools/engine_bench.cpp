@@ -480,7 +480,7 @@ extern "C" int32_t kbg_tool_firstfit_stamps(const kbg_snapshot* snap, const kbg_
       return -2;
     }
   const int32_t per = kbg::firstfit_rows(rows);
-  const int32_t n_wg = std::min((rows + per - 1) / per, max_wg);
+  const int32_t n_wg = std::min((rows + per - 1) / per * sg.splits, max_wg);
   const bool ok = kbg::read_ff_stamps(out, n_wg) == hipSuccess;
   free_device(S);
   return ok ? n_wg : -3;
