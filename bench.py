@@ -507,6 +507,8 @@ def main():
                 out["traffic_frac_of_peak"] = pmc["hbm_bytes_per_launch"] / avg_s / 1e9 / HBM_PEAK_GBS
             if pmc.get("valu_insts_per_launch") is not None:
                 out["binding"] = dict(valu_ceiling(pmc, avg_s * 1e6, rows), bound="valu issue")
+            if pmc.get("wait_any_share") is not None:  # share of the waves' lifetime parked at s_waitcnt / barriers
+                out["wait_any_share"] = pmc["wait_any_share"]
             out["pmc_source"] = pmc.get("source")
         return out
 
@@ -521,7 +523,7 @@ def main():
         launches = max(1, agg["launches"])
         algo = agg["visits"] * NODE_RECORD_B + agg["evals"] * TASK_RECORD_B
         avg_us = agg["scan_ms"] * 1e3 / launches
-        out = {"kernel": "kbg_scan_kernel", "avg_launch_us": avg_us, "launches_per_cycle": launches / max(1, agg["steps"]),
+        out = {"kernel": "kbg_firstfit_kernel", "avg_launch_us": avg_us, "launches_per_cycle": launches / max(1, agg["steps"]),
                "rows_per_launch": agg["evals"] / launches, "algo_bytes_per_launch": algo / launches,
                "algo_reuse_gbs": algo / (agg["scan_ms"] * 1e-3) / 1e9 if agg["scan_ms"] > 0 else 0.0}
         pmc = load_pmc(agg["n_nodes"], mode) if comm is None else None

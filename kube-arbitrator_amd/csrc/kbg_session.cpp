@@ -2984,6 +2984,8 @@ void begin_cycle(Session& S) {
   }
   S.trun.assign(S.n_tasks, 0);
   for (int32_t t : S.nt_task) S.trun[t] = 1;
+  if (S.has_dupkeys) S.t_detached.assign(S.n_tasks, 0);
+  else S.t_detached.clear();
   S.pend = S.pend_all;
   S.pend_off = S.pend_off_all;
   S.pend_len = S.pend_len_all;
@@ -4735,9 +4737,10 @@ kbg_status vt_setup(Session& S) {
     for (size_t k = 0; k < P; ++k) S.vt_sh_run[k] = S.trun[S.nt_task[k]];
     for (int32_t j = 0; j < S.n_jobs; ++j) std::memcpy(&S.vt_sh_jalloc[3 * (size_t)j], &S.fin.jalloc[j].c, 24);
     for (int32_t q = 0; q < S.n_queues; ++q) std::memcpy(&S.vt_sh_qalloc[3 * (size_t)q], &S.fin.qalloc[q].c, 24);
-    HIP_TRY(hipMemcpyAsync(S.vt.c_run, S.vt_sh_run.data(), std::max<size_t>(1, P), hipMemcpyHostToDevice, S.stream));
-    HIP_TRY(hipMemcpyAsync(S.vt.j_ready, S.vt_sh_ready.data(), (size_t)S.n_jobs * 4, hipMemcpyHostToDevice,
-                           S.stream));
+    if (P > 0) HIP_TRY(hipMemcpyAsync(S.vt.c_run, S.vt_sh_run.data(), P, hipMemcpyHostToDevice, S.stream));
+    if (S.n_jobs > 0)
+      HIP_TRY(hipMemcpyAsync(S.vt.j_ready, S.vt_sh_ready.data(), (size_t)S.n_jobs * 4, hipMemcpyHostToDevice,
+                             S.stream));
     HIP_TRY(hipMemcpyAsync(S.vt.j_alloc, S.vt_sh_jalloc.data(), S.vt_sh_jalloc.size() * 8, hipMemcpyHostToDevice,
                            S.stream));
     HIP_TRY(hipMemcpyAsync(S.vt.q_alloc, S.vt_sh_qalloc.data(), S.vt_sh_qalloc.size() * 8, hipMemcpyHostToDevice,
@@ -4871,13 +4874,68 @@ struct Live {
     return plugins(t, true);
   }
   // statement.go:81-108: job Running again; node.AddTask fails (the task is
-  // still there, as Releasing), so the node is unchanged; AllocateFunc
-  void unevict(int32_t v) {
+  // still there, as Releasing), so the node is unchanged; AllocateFunc. A
+  // task whose copy a discard's RemoveTask took off the node (unpipeline_dup)
+  // is added back as Running, unless another pod holds its key there now.
+  // false: AddTask's Idle.Sub would panic.
+  bool unevict(int32_t v) {
     const int32_t j = S.task_job[v];
     S.tstat[v] = KBG_RUNNING;
     lister(v, +1);
     ready(j, +1);
+    const int32_t n = S.task_node[v];
+    if (!S.t_detached.empty() && S.t_detached[v] && n >= 0 && !node_has_key(S, v, n)) {
+      if (!S.nil_node[n] && !kbg::res_sub(S.idle[n], S.treq[v])) return false;  // node_info.go:123-124
+      S.ntasks[n]++;
+      S.node_keys.insert(node_key_of(S, v, n));
+      S.trun[v] = 1;
+      if (S.t_pos[v] >= 0) vt_delta(S, 0, S.t_pos[v], 1.0, 0, 0);
+      S.t_detached[v] = 0;
+      touch(n);
+    }
     plugins(v, true);
+    return true;
+  }
+  // unpipeline of a pipeline whose AddTask found its pod key already on the
+  // node (statement.go:156-192): NodeInfo.RemoveTask removes by key, so the
+  // pod that held the key leaves the node (node_info.go:131-157), by the
+  // status of its node copy: Running (Idle += req) or, evicted since,
+  // Releasing (Releasing -= req, Idle += req). The holder is found among the
+  // node's tasks Running at open; any other holder (placed this cycle, a pod
+  // outside the session) or one with host ports is refused.
+  kbg_status unpipeline_dup(int32_t t, int32_t n) {
+    const int32_t j = S.task_job[t];
+    ready(j, -1);
+    S.tstat[t] = KBG_PENDING;
+    if (node_has_key(S, t, n)) {
+      int32_t h = -1;
+      for (int32_t k = S.nt_off[n]; k < S.nt_off[n + 1] && h < 0; ++k) {
+        const int32_t u = S.nt_task[k];
+        if (u != t && S.task_key[u] == S.task_key[t] && !S.t_detached[u]) h = u;
+      }
+      const int32_t hs = h >= 0 ? S.tasks_in[h].spec : -1;
+      if (h < 0 || (hs >= 0 && S.specs_in[hs].has_host_ports))
+        return fail(KBG_E_UNSUPPORTED, "statement discard of a pipeline whose pod key is held on the node by a pod "
+                                       "the session did not find Running there at open, or one with host ports "
+                                       "(node_info.go:131-157 removes it): run the reference path");
+      if (!S.nil_node[n]) {
+        const Res& r = S.treq[h];
+        if (!S.trun[h] && !kbg::res_sub(S.rel[n], r))  // the copy is Releasing (evicted since open)
+          return fail(KBG_E_REF_PANIC, "statement discard: RemoveTask Releasing.Sub underflow (node_info.go:143)");
+        kbg::res_add(S.idle[n], r);
+      }
+      S.ntasks[n]--;
+      S.node_keys.erase(node_key_of(S, t, n));
+      if (S.trun[h]) {
+        S.trun[h] = 0;  // no longer in node.Tasks: not a victim candidate
+        if (S.t_pos[h] >= 0) vt_delta(S, 0, S.t_pos[h], 0, 0, 0);
+      }
+      S.t_detached[h] = 1;
+      touch(n);
+    }
+    if (!plugins(t, false))
+      return fail(KBG_E_REF_PANIC, "statement discard: DeallocateFunc Sub underflow (resource_info.go:100-110)");
+    return KBG_OK;
   }
   // statement.go:156-192: job Pending; node.RemoveTask; DeallocateFunc
   bool unpipeline(int32_t t, int32_t n) {
@@ -5187,14 +5245,15 @@ void stmt_commit(Session& S, Stmt& stmt) {  // statement.go:207-217
 
 kbg_status stmt_discard(Session& S, Live& L, Stmt& stmt) {  // statement.go:194-205
   bool ok = true;
-  for (const Stmt::Op& op : stmt.ops)
-    if (!op.evict && op.dup)  // unpipeline's RemoveTask would drop the pod that held the key
-      return fail(KBG_E_UNSUPPORTED, "statement discard of a pipeline whose pod key was already on the node "
-                                     "(node_info.go:131-157 removes the other pod): run the reference path");
   for (size_t k = stmt.ops.size(); k-- > 0;) {
     const Stmt::Op& op = stmt.ops[k];
-    if (op.evict) L.unevict(op.task);
-    else ok = L.unpipeline(op.task, op.node) && ok;
+    if (op.evict) {
+      if (!L.unevict(op.task)) return fail(KBG_E_REF_PANIC, "statement discard: unevict's AddTask Idle.Sub underflow");
+    } else if (op.dup) {  // unpipeline's RemoveTask drops the pod that held the key
+      if (kbg_status st = L.unpipeline_dup(op.task, op.node); st != KBG_OK) return st;
+    } else {
+      ok = L.unpipeline(op.task, op.node) && ok;
+    }
   }
   stmt.ops.clear();
   return ok ? KBG_OK : fail(KBG_E_REF_PANIC, "statement discard: DeallocateFunc Sub underflow (resource_info.go:100-110)");

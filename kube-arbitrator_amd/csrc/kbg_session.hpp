@@ -316,6 +316,7 @@ struct Session {
   std::vector<int32_t> nt_off_buf, nt_task_buf;  // the next derive's copy (an update rebuilds by swap)
   std::vector<int32_t> upd_nodes;             // nodes an update's events touched (kbg_session_update) ...
   bool upd_nodes_valid = false;               // ... set for the derive that follows them
+  std::vector<uint8_t> t_detached;            // a statement discard's RemoveTask took the task's copy off its node
   std::vector<uint8_t> trun;                  // node-side copy still Running (an eviction makes it Releasing
                                               // for good: unevict's AddTask fails, node_info.go:101-106)
   std::vector<int32_t> task_node;             // node index of a task's NodeName (-1: not a session node)

@@ -817,6 +817,7 @@ struct Session {  // framework/session.go:35-61
   std::unordered_map<TaskInfo*, int> decisionOf;
   std::vector<std::pair<std::string, std::string>> binds;  // (ns/name, node) in dispatch order
   int64_t predicate_calls = 0;
+  int64_t dup_discards = 0;  // statement discards whose unpipeline removed another pod holding the key (stats only)
   int threads = 1;  // > 1: allocate's node loop evaluated by a team of threads (B-omp CPU baseline only)
   size_t min_parallel_nodes = 512;  // B-omp: smaller clusters walk the nodes on one thread
   std::vector<TaskInfo*> evaluated;  // every task whose node loop ran, in order
@@ -1795,7 +1796,11 @@ struct Statement {
           if (eh.allocate) eh.allocate(t);
       } else {  // unpipeline :156-192
         if (jit != ssn->jobIndex.end()) jit->second->UpdateTaskStatus(t, Pending);
-        if (nit != ssn->nodeIndex.end()) nit->second->RemoveTask(t);
+        if (nit != ssn->nodeIndex.end()) {
+          TaskInfo** held = nit->second->tasks.find(pod_key(t->pod));
+          if (held && (*held)->uid != t->uid) ssn->dup_discards++;
+          nit->second->RemoveTask(t);
+        }
         for (auto& eh : ssn->eventHandlers)
           if (eh.deallocate) eh.deallocate(t);
       }
@@ -2219,7 +2224,8 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache, in
          ",\"used\":" + res_json(n->used) + ",\"ntasks\":" + std::to_string(n->tasks.size()) + "}";
   }
   o += "],\"stats\":{\"seconds\":" + kbjson::num(secs) + ",\"predicate_calls\":" + std::to_string(ssn->predicate_calls) +
-       ",\"decisions\":" + std::to_string(ssn->decisions.size()) + "}}";
+       ",\"decisions\":" + std::to_string(ssn->decisions.size()) + ",\"dup_discards\":" +
+       std::to_string(ssn->dup_discards) + "}}";
   return o;
 }
 

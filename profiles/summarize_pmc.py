@@ -8,7 +8,8 @@ Usage: python profiles/summarize_pmc.py <session dir> <config> > summary.json
 Kernels are keyed by their name up to the argument list, template arguments
 kept: kbg_firstfit_kernel<true, false> runs the full-scan mode's batches
 (every node of every row), kbg_firstfit_kernel<true, true> the production
-mode's grouped batches (a workgroup stops once its rows' lists are full).
+mode's grouped batches; the rows-per-workgroup argument (16 / 24 / 32) is
+dropped, so each mode's variants are one entry.
 Derived figures (MI355X_MICROARCH.md):
   hbm_read_bytes  = 2 x FETCH_SIZE KiB x 1024 (gfx950 tallies 128-B requests
                     at 64 B; Infinity-Cache hits are counted too)
@@ -37,7 +38,9 @@ WANT = ("kbg_firstfit_kernel", "kbg_fitdelta_kernel", "kbg_scan_kernel", "kbg_se
 def key(name):
     base = name.split("(")[0]
     base = re.sub(r"^void ", "", base)
-    return base.replace("kbg::", "")
+    base = base.replace("kbg::", "")
+    # the fused kernel's rows-per-workgroup variants (16 / 24 / 32) of one mode are one entry
+    return re.sub(r"^(kbg_firstfit_kernel<\w+, \w+), \d+>$", r"\1>", base)
 
 
 def rows(path):
@@ -99,6 +102,12 @@ def main():
             v["valu_issue_frac"] = v["valu_issue_floor_us"] * 1e3 / v["avg_ns"]
             if avg.get("SQ_WAVES"):
                 v["valu_insts_per_wave"] = avg["SQ_INSTS_VALU"] / avg["SQ_WAVES"]
+        if avg.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in avg:  # share of the waves' lifetime parked (s_waitcnt / barrier)
+            v["wait_any_share"] = avg["SQ_WAIT_ANY"] / avg["SQ_WAVE_CYCLES"]
+            if "SQ_WAIT_INST_ANY" in avg:
+                v["wait_inst_share"] = avg["SQ_WAIT_INST_ANY"] / avg["SQ_WAVE_CYCLES"]
+            if "SQ_ACTIVE_INST_ANY" in avg:
+                v["active_inst_share"] = avg["SQ_ACTIVE_INST_ANY"] / avg["SQ_WAVE_CYCLES"]
         if "GRBM_GUI_ACTIVE" in avg:
             pd = statistics.mean(c["_dur"]["GRBM_GUI_ACTIVE"].values())
             v["profiled_avg_ns"] = pd

@@ -439,6 +439,28 @@ def test_victim_big_node_parity(seed):
         ssn.close()
 
 
+# seeds of synth.contended_dupkey_fixture whose oracle run discards a statement
+# holding a pipeline onto a node that already had its pod key (oracle stats
+# dup_discards > 0; the first 300 seeds)
+DUP_DISCARD_SEEDS = [66, 73, 89, 106, 117, 154, 179, 208, 212, 227, 240, 253, 273, 295]
+
+
+@pytest.mark.parametrize("seed", DUP_DISCARD_SEEDS + [0, 1, 2, 3, 4, 5])
+def test_dupkey_statement_discard_parity(seed):
+    """A discarded preempt statement whose pipeline found its pod key already
+    on the node: unpipeline's RemoveTask removes the pod that held the key
+    (statement.go:156-192, node_info.go:131-157), and the holder's own
+    unevict then adds it back as Running. No KBG_E_UNSUPPORTED."""
+    fx = synth.contended_dupkey_fixture(seed)
+    ref = run_oracle(fx)
+    if seed in DUP_DISCARD_SEEDS:
+        assert ref["stats"]["dup_discards"] > 0
+    got, ssn = run_fixture(fx)
+    compare_outputs(ref, got)
+    if ssn:
+        ssn.close()
+
+
 @pytest.mark.parametrize("seed", range(10))
 def test_victim_huge_node_parity(seed):
     """Nodes with more than kMaxNodeCandidates (1024) Running pods, which the
