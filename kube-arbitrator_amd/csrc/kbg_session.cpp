@@ -665,8 +665,13 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
       const int32_t blocks = (G + kbg::firstfit_rows(G) - 1) / kbg::firstfit_rows(G);
       a.splits = std::max(1, std::min({kbg::kFfMaxSplits, 256 / std::max(1, blocks), tw / 8}));
     }
-    a.split_words = (tw + a.splits - 1) / a.splits;
-    a.splits = std::max(1, (tw + a.split_words - 1) / a.split_words);  // no empty part
+    if (tw > 0) {
+      a.split_words = (tw + a.splits - 1) / a.splits;
+      a.splits = (tw + a.split_words - 1) / a.split_words;  // no empty part
+    } else {  // no words (a session without nodes)
+      a.splits = 1;
+      a.split_words = 0;
+    }
     sg.splits = a.splits;
     if (sg.n_slots <= kbg::kInlineShapes) {
       std::copy(sg.h_shapes, sg.h_shapes + sg.n_slots, a.inl);
