@@ -1569,12 +1569,12 @@ std::vector<int32_t> ranks_of(const Session& S, const std::vector<int32_t>& ids)
 // String id of `v` for an event: an existing content's canonical id, or a new entry.
 int32_t intern(Session& S, const char* v) {
   const std::string_view key(v ? v : "");
-  auto it = S.canon_of.find(key);
-  if (it != S.canon_of.end()) return it->second;  // a canonical id is its own canonical id
+  const int32_t known = S.canon_of.find(S.strs, key);
+  if (known >= 0) return known;  // a canonical id is its own canonical id
   const int32_t id = (int32_t)S.strs.size();
   S.strs.emplace_back(key);
   S.canon.push_back(id);
-  S.canon_of.emplace(S.strs.back(), id);
+  S.canon_of.insert(S.strs, id);
   return id;
 }
 
@@ -1603,7 +1603,7 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   S.canon_of.clear();
   S.canon_of.reserve(S.strs.size());
   S.canon.resize(S.strs.size());
-  for (size_t i = 0; i < S.strs.size(); ++i) S.canon[i] = S.canon_of.emplace(S.strs[i], (int32_t)i).first->second;
+  for (size_t i = 0; i < S.strs.size(); ++i) S.canon[i] = S.canon_of.insert(S.strs, (int32_t)i);
   S.n_nodes = snap->n_nodes;
   S.n_jobs = snap->n_jobs;
   S.n_queues = snap->n_queues;
@@ -5783,9 +5783,9 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
         const int32_t t = T++;
         if (!holders) break;
         int32_t key;
-        auto ci = S.canon_of.find(e.pod_key);
-        if (ci != S.canon_of.end()) {
-          key = ci->second;
+        const int32_t known = S.canon_of.find(S.strs, e.pod_key);
+        if (known >= 0) {
+          key = known;
         } else {
           key = (int32_t)S.strs.size() + (int32_t)fresh.size();
           key = fresh.emplace(e.pod_key, key).first->second;

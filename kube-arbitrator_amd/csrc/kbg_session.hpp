@@ -25,6 +25,62 @@ struct StrHash {
   size_t operator()(std::string_view v) const noexcept { return std::hash<std::string_view>{}(v); }
 };
 
+// String content -> canonical id, an open-addressing table of ids into the
+// session's string vector: an entry is an id and its hash, so interning a new
+// pod key or UID allocates nothing beyond the string itself (a node-based
+// map allocated a node and a second copy of the key per entry).
+struct StrIndex {
+  std::vector<int32_t> ids;  // -1: empty
+  std::vector<uint64_t> hs;
+  size_t n = 0;
+  static uint64_t hash(std::string_view v) { return std::hash<std::string_view>{}(v); }
+  void clear() {
+    ids.clear();
+    hs.clear();
+    n = 0;
+  }
+  void reserve(size_t want) {
+    size_t cap = 64;
+    while (cap < 2 * want) cap <<= 1;
+    if (cap <= ids.size()) return;
+    std::vector<int32_t> oi(cap, -1);
+    std::vector<uint64_t> oh(cap, 0);
+    oi.swap(ids);
+    oh.swap(hs);
+    for (size_t i = 0; i < oi.size(); ++i)
+      if (oi[i] >= 0) {
+        size_t k = oh[i] & (cap - 1);
+        while (ids[k] >= 0) k = (k + 1) & (cap - 1);
+        ids[k] = oi[i];
+        hs[k] = oh[i];
+      }
+  }
+  int32_t find(const std::vector<std::string>& strs, std::string_view v) const {
+    if (ids.empty()) return -1;
+    const uint64_t h = hash(v);
+    const size_t m = ids.size() - 1;
+    for (size_t k = h & m;; k = (k + 1) & m) {
+      const int32_t id = ids[k];
+      if (id < 0) return -1;
+      if (hs[k] == h && strs[id] == v) return id;
+    }
+  }
+  // strs[id]'s canonical id: the first id holding the same content (id itself if new)
+  int32_t insert(const std::vector<std::string>& strs, int32_t id) {
+    if (2 * (n + 1) > ids.size()) reserve(n + 1);
+    const std::string_view v = strs[id];
+    const uint64_t h = hash(v);
+    const size_t m = ids.size() - 1;
+    size_t k = h & m;
+    for (; ids[k] >= 0; k = (k + 1) & m)
+      if (hs[k] == h && strs[ids[k]] == v) return ids[k];
+    ids[k] = id;
+    hs[k] = h;
+    ++n;
+    return id;
+  }
+};
+
 // resource_info.go:142-146
 inline bool res_le(const Res& r, const Res& a) {
   return (r.c < a.c || __builtin_fabs(a.c - r.c) < kMinMilliCPU) &&
@@ -401,7 +457,7 @@ struct Session {
   std::vector<int32_t> aff_gain_classes;
 
   // ---- resident session (kbg_session_update edits the inputs above)
-  std::unordered_map<std::string, int32_t, StrHash, std::equal_to<>> canon_of;  // string content -> canonical id
+  StrIndex canon_of;  // string content -> canonical id
   std::unordered_map<int32_t, int32_t> node_of;       // canonical node name -> node index
   std::vector<uint8_t> task_live;                     // 0: the pod was deleted (event_handlers.go deletePod)
   std::vector<std::vector<int32_t>> job_task_order;   // per job: its tasks in JobInfo.Tasks insertion order
