@@ -41,3 +41,24 @@ def test_launcher_world_size_must_match():
                                              MASTER_PORT="29555"))
     assert p.returncode != 0
     assert "WORLD_SIZE=3" in p.stderr and not p.stdout.strip()
+
+
+def test_parity_verdict_against_golden_digest():
+    """bench.py's own parity check: the oracle's C1 output digested as the
+    bench digests its timed cycles matches tests/golden/digest_c1.json, and a
+    perturbed decision log or share is reported (and would exit non-zero)."""
+    import importlib.util
+    from helpers import run_oracle
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    sys.path.insert(0, os.path.join(ROOT, "kube-arbitrator_amd"))
+    from kbgpu import synth
+    from kbgpu.digest import digest_outputs
+    dg = digest_outputs(run_oracle(synth.config_fixture(1)))
+    v = bench.parity_verdict(1, {"production": dg, "full_scan": dg})
+    assert v["ok"] is True and v["production"] is True and v["full_scan"] is True
+    bad = dict(dg, binds="0" * 64)
+    v = bench.parity_verdict(1, {"production": dg, "full_scan": bad})
+    assert v["ok"] is False and v["full_scan"] == {"mismatch": ["binds"]}
+    assert bench.parity_verdict(99, {"production": dg})["ok"] is None  # no golden digest for the config
