@@ -108,6 +108,8 @@ def main():
                 v["wait_inst_share"] = avg["SQ_WAIT_INST_ANY"] / avg["SQ_WAVE_CYCLES"]
             if "SQ_ACTIVE_INST_ANY" in avg:
                 v["active_inst_share"] = avg["SQ_ACTIVE_INST_ANY"] / avg["SQ_WAVE_CYCLES"]
+            if "SQ_WAIT_INST_LDS" in avg:  # issue stalls on the LDS pipe (not lgkmcnt drains)
+                v["wait_inst_lds_share"] = avg["SQ_WAIT_INST_LDS"] / avg["SQ_WAVE_CYCLES"]
         if "GRBM_GUI_ACTIVE" in avg:
             pd = statistics.mean(c["_dur"]["GRBM_GUI_ACTIVE"].values())
             v["profiled_avg_ns"] = pd
