@@ -30,18 +30,19 @@
 extern "C" {
 #endif
 
-#define KBG_ABI_VERSION 9
+#define KBG_ABI_VERSION 10
 
 typedef enum kbg_status {
   KBG_OK = 0,
   KBG_E_INVALID = 1,     /* malformed snapshot / arguments */
   KBG_E_UNSUPPORTED = 2, /* a case the device path declines, named in
-                            kbg_last_error: reclaim / preempt with more than
-                            1024 Running session tasks on one node, a
-                            statement discard of a pipeline onto a node that
-                            already held its pod key, and the session-update
-                            cases listed at kbg_session_update. The caller
-                            runs the reference path. Never a silent fallback. */
+                            kbg_last_error: a statement discard of a pipeline
+                            whose pod key the node holds for a pod placed this
+                            cycle (or for a pod outside the session jobs when
+                            the snapshot carried no node_pods), and the
+                            session-update cases listed at kbg_session_update.
+                            The caller runs the reference path. Never a silent
+                            fallback. */
   KBG_E_REF_PANIC = 3,   /* the reference would panic here (Resource.Sub underflow
                             resource_info.go:100-110, proportion water-fill F9
                             proportion.go:119-140, nil-Node predicate
@@ -113,6 +114,21 @@ typedef struct kbg_node {
                                    there is logged but leaves the node unchanged (AddTask's "already on
                                    node" error, node_info.go:101-106) */
 } kbg_node;
+
+/* The NodeInfo.Tasks copy behind one node_pod_keys entry, as NodeInfo.RemoveTask
+ * reads it (node_info.go:131-157) when a pod key collision makes the session
+ * remove it by key: a statement discard's unpipeline of a pipeline whose key
+ * the node already held (statement.go:156-192), or an update that deletes a
+ * session pod whose key another pod holds on its node (event_handlers.go:
+ * 90-120 -> deleteTask). Optional (n_node_pods == 0): without it such a
+ * removal of a pod outside the session jobs is refused (KBG_E_UNSUPPORTED). */
+typedef struct kbg_node_pod {
+  kbg_resource resreq; /* TaskInfo.Resreq */
+  int32_t status;      /* TaskStatus of the copy: Releasing (Releasing -= req, Idle += req), Pipelined
+                          (Releasing += req), anything else (Idle += req) */
+  int32_t port_len;    /* how many of the node's ports[port_off ..] entries are this pod's (the entries
+                          follow NodeInfo.Tasks order, as node_pod_keys does) */
+} kbg_node_pod;
 
 /* One v1.ContainerPort as HostPortInfo sees it (vendor cache/host_ports.go). */
 typedef struct kbg_host_port {
@@ -235,6 +251,7 @@ typedef struct kbg_snapshot {
   const kbg_pod_term* pod_terms;   int32_t n_pod_terms;
   const int32_t* pod_labels;       int32_t n_pod_labels;  /* 2*n_pod_labels ints */
   const int32_t* node_pod_keys;    int32_t n_node_pod_keys;
+  const kbg_node_pod* node_pods;   int32_t n_node_pods;   /* 0, or one per node_pod_keys entry */
 } kbg_snapshot;
 
 typedef struct kbg_options {
@@ -401,8 +418,9 @@ kbg_status kbg_backfill(kbg_session* s, kbg_decision* out, int32_t cap, int32_t*
  * Both write the cycle's decision log (pipelines carry the action); the
  * evictions are read with kbg_evictions_get. Pod (anti)affinity and host
  * ports are re-derived per eviction / pipeline (kbg_affinity.cpp, the port
- * atoms); nodes with up to 1024 Running session tasks are scanned in 64-wide
- * candidate chunks; more than that is refused (KBG_E_UNSUPPORTED). */
+ * atoms); nodes with up to 1024 Running session tasks are scanned on the
+ * device in 64-wide candidate chunks, larger ones on the host when a stop
+ * search reaches them (same victims, same order). */
 kbg_status kbg_reclaim(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out);
 kbg_status kbg_preempt(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out);
 
@@ -461,7 +479,9 @@ typedef struct kbg_event {
  * KBG_E_UNSUPPORTED and KBG_E_INVALID found before the first event is applied
  * leave the session unchanged: an event naming a deleted task or an index out
  * of range, a removed pod whose key is held on its node by a pod outside the
- * session jobs, a node update of a node the cache only knows from a pod. KBG_E_REF_PANIC (the cache itself would
+ * session jobs when the snapshot carried no node_pods (kbg_node_pod: with
+ * them that pod leaves the node as RemoveTask takes it), a node update of a
+ * node the cache only knows from a pod. KBG_E_REF_PANIC (the cache itself would
  * panic: a Resource.Sub underflow in AddTask / RemoveTask / SetNode) is found
  * while the events are applied: the session is then unusable and every later
  * call on it but kbg_session_close returns KBG_E_INVALID (re-open it). */
@@ -492,7 +512,7 @@ void kbg_session_close(kbg_session* s);
 /* Snapshot wire format: the flat kbg_snapshot as one
  * little-endian byte string — the header "KBGS", format version, layout
  * word (a hash of every snapshot struct's size: blobs survive ABI bumps that
- * leave those structs unchanged), the 21 counts of kbg_snapshot in
+ * leave those structs unchanged), the 22 counts of kbg_snapshot in
  * declaration order, then every
  * string as (uint32 length, bytes) and every array as its raw struct bytes in
  * declaration order. A cache adapter builds it once per scheduling cycle (or a
@@ -502,7 +522,7 @@ void kbg_session_close(kbg_session* s);
  * before anything is allocated, so a corrupt blob is KBG_E_INVALID.
  * kbg_snapshot_encode with out == NULL / cap == 0 stores the size in *n_out. */
 typedef struct kbg_snapshot_blob kbg_snapshot_blob;
-#define KBG_SNAPSHOT_FORMAT 2
+#define KBG_SNAPSHOT_FORMAT 3
 kbg_status kbg_snapshot_encode(const kbg_snapshot* snap, uint8_t* out, int64_t cap, int64_t* n_out);
 kbg_status kbg_snapshot_decode(const uint8_t* data, int64_t n, kbg_snapshot_blob** out);
 kbg_status kbg_snapshot_save(const kbg_snapshot* snap, const char* path);

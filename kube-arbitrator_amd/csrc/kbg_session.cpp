@@ -1245,9 +1245,15 @@ void add_ports(Session& S, int32_t c, int32_t nd) {
 // NodeInfo.RemoveTask): an atom no other pod holds — and that no pod held at
 // open — is free again, and the classes it blocked get the node back where
 // nothing else forbids it.
+int32_t open_ports_left(const Session& S, int32_t nd, int32_t a) {  // entries of open pods still on the node
+  const int64_t k = ((int64_t)nd << 32) | (uint32_t)a;
+  auto o = S.port_open.find(k);
+  if (o == S.port_open.end()) return 0;
+  auto g = S.port_gone.find(k);
+  return o->second - (g == S.port_gone.end() ? 0 : g->second);
+}
 void remove_ports(Session& S, int32_t c, int32_t nd) {
   uint64_t* np = &S.node_ports[(size_t)nd * S.PW];
-  const uint64_t* np0 = &S.node_ports0[(size_t)nd * S.PW];
   const uint64_t* add = &S.cls_add[(size_t)c * S.PW];
   for (int32_t w = 0; w < S.PW; ++w)
     for (uint64_t b = add[w]; b; b &= b - 1) {
@@ -1256,10 +1262,34 @@ void remove_ports(Session& S, int32_t c, int32_t nd) {
       if (it == S.port_hold.end() || --it->second > 0) continue;
       S.port_hold.erase(it);
       const uint64_t bit = 1ull << (a & 63);
-      if (np0[w] & bit) continue;  // a pod on the node at open holds it
+      if (open_ports_left(S, nd, a) > 0) continue;  // a pod on the node at open still holds it
       np[w] &= ~bit;
       for (int32_t c2 : S.atom_cls[a]) refresh_mask_bit(S, c2, nd);
     }
+}
+
+// A pod that was on the node at open leaves node.Pods() (a statement
+// discard's RemoveTask by key of the pod holding the key): each of its port
+// entries goes; an atom no pod holds any more is free again.
+void release_open_ports(Session& S, int32_t nd, const kbg_host_port* ports, int32_t n) {
+  if (!S.has_ports) return;
+  uint64_t* np = &S.node_ports[(size_t)nd * S.PW];
+  for (int32_t i = 0; i < n; ++i) {
+    const kbg_host_port& hp = ports[i];
+    if (hp.host_port <= 0) continue;
+    const std::string ip = S.strs[hp.host_ip].empty() ? std::string("0.0.0.0") : S.strs[hp.host_ip];
+    const std::string pr = S.strs[hp.protocol].empty() ? std::string("TCP") : S.strs[hp.protocol];
+    auto ai = S.atom_of.find(ip + "|" + pr + "|" + std::to_string(hp.host_port));
+    if (ai == S.atom_of.end()) continue;  // (every port a pod on the node uses is an atom)
+    const int32_t a = ai->second;
+    const int64_t k = ((int64_t)nd << 32) | (uint32_t)a;
+    S.port_gone[k]++;
+    if (open_ports_left(S, nd, a) > 0 || S.port_hold.count(k)) continue;
+    const uint64_t bit = 1ull << (a & 63);
+    if (!(np[a / 64] & bit)) continue;
+    np[a / 64] &= ~bit;
+    for (int32_t c2 : S.atom_cls[a]) refresh_mask_bit(S, c2, nd);
+  }
 }
 
 // NodeInfo.Tasks already holds the task's PodKey (node_info.go:101-106)
@@ -1419,6 +1449,12 @@ void setup_host_ports(Session& S) {
   for (int32_t c = 0; c < C; ++c)
     for (int32_t a = 0; a < A; ++a)
       if ((S.cls_conf[(size_t)c * S.PW + a / 64] >> (a % 64)) & 1ull) S.atom_cls[a].push_back(c);
+  S.atom_of.clear();
+  for (int32_t a = 0; a < A; ++a)
+    S.atom_of[std::get<0>(atom_list[a]) + "|" + std::get<1>(atom_list[a]) + "|" + std::to_string(std::get<2>(atom_list[a]))] = a;
+  S.port_open.clear();  // one entry per pod and port: how many pods at open use each atom
+  for (int32_t n = 0; n < S.n_nodes; ++n)
+    for (int32_t a : used[n]) S.port_open[((int64_t)n << 32) | (uint32_t)a]++;
   S.node_ports.assign((size_t)S.n_nodes * S.PW, 0);
   S.mask_dirty_flag.assign(S.h_class_mask.size(), 0);
   S.mask_dirty.clear();
@@ -1447,7 +1483,7 @@ kbg_status validate(const kbg_snapshot* s) {
         {s->tolerations, s->n_tolerations}, {s->labels, s->n_labels},   {s->taints, s->n_taints},
         {s->selectors, s->n_selectors}, {s->plugins, s->n_plugins},     {s->tier_sizes, s->n_tiers},
         {s->ports, s->n_ports},         {s->node_tasks, s->n_node_tasks}, {s->pod_terms, s->n_pod_terms},
-        {s->pod_labels, s->n_pod_labels}, {s->node_pod_keys, s->n_node_pod_keys}};
+        {s->pod_labels, s->n_pod_labels}, {s->node_pod_keys, s->n_node_pod_keys}, {s->node_pods, s->n_node_pods}};
     for (const auto& a : arrays)
       if (a.second < 0 || (a.second > 0 && !a.first)) return fail(KBG_E_INVALID, "negative count or null array");
   }
@@ -1522,6 +1558,19 @@ kbg_status validate(const kbg_snapshot* s) {
   }
   for (int32_t i = 0; i < s->n_node_pod_keys; ++i)
     if (!in(s->node_pod_keys[i], NS)) return fail(KBG_E_INVALID, "node pod key string");
+  if (s->n_node_pods != 0 && s->n_node_pods != s->n_node_pod_keys)
+    return fail(KBG_E_INVALID, "node_pods: none or one per node_pod_keys entry");
+  for (int32_t i = 0; i < s->n_nodes && s->n_node_pods; ++i) {  // each pod's ports: the node's, in order
+    const kbg_node& n = s->nodes[i];
+    int64_t pl = 0;
+    for (int32_t k = 0; k < n.key_len; ++k) {
+      const kbg_node_pod& q = s->node_pods[n.key_off + k];
+      if (q.port_len < 0 || q.status <= 0 || q.status > KBG_UNKNOWN || (q.status & (q.status - 1)))
+        return fail(KBG_E_INVALID, "node pod " + std::to_string(n.key_off + k));
+      pl += q.port_len;
+    }
+    if (pl != n.port_len) return fail(KBG_E_INVALID, "node " + std::to_string(i) + ": node_pods port_len sum != port_len");
+  }
   for (int32_t i = 0; i < s->n_ports; ++i)
     if (!in(s->ports[i].host_ip, NS) || !in(s->ports[i].protocol, NS)) return fail(KBG_E_INVALID, "port");
   for (int32_t i = 0; i < s->n_tolerations; ++i) {
@@ -1643,15 +1692,29 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
     S.node_task_order[n].assign(snap->node_tasks + nd.task_off, snap->node_tasks + nd.task_off + nd.task_len);
     for (int32_t i = 0; i < nd.key_len; ++i) S.node_key_order[n].push_back(S.canon[snap->node_pod_keys[nd.key_off + i]]);
   }
-  // keys held on a node by pods outside the session jobs: no event ever
-  // names those pods, so the set holds for the whole resident session
-  S.outsider_keys.clear();
+  // keys held on a node by pods outside the session jobs, with their node
+  // copies when the snapshot carries them (kbg_node_pod): no event ever adds
+  // such a pod, only a removal by key takes one off (in_node_remove)
+  S.outsiders.clear();
   for (int32_t n = 0; n < S.n_nodes; ++n) {
     if (S.node_key_order[n].size() == S.node_task_order[n].size()) continue;  // every entry is a session task's
+    const kbg_node& nd = S.nodes_in[n];
     std::unordered_set<int32_t> mine;
     for (int32_t t : S.node_task_order[n]) mine.insert(S.canon[S.tasks_in[t].pod_key]);
-    for (int32_t k : S.node_key_order[n])
-      if (!mine.count(k)) S.outsider_keys.insert(((int64_t)n << 32) | (uint32_t)k);
+    int32_t po = nd.port_off;  // the entry's own ports follow NodeInfo.Tasks order
+    for (int32_t i = 0; i < (int32_t)S.node_key_order[n].size(); ++i) {
+      const kbg_node_pod* q = snap->n_node_pods ? &snap->node_pods[nd.key_off + i] : nullptr;
+      const int32_t k = S.node_key_order[n][i];
+      if (!mine.count(k)) {
+        Session::Outsider& o = S.outsiders[((int64_t)n << 32) | (uint32_t)k];
+        if (q) {
+          o.req = q->resreq;
+          o.status = q->status;
+          o.ports.assign(S.ports_in.begin() + po, S.ports_in.begin() + po + q->port_len);
+        }
+      }
+      if (q) po += q->port_len;
+    }
   }
   S.broken.clear();
   S.node_of.clear();
@@ -2980,6 +3043,8 @@ void begin_cycle(Session& S) {
   S.dec_dup.clear();
   S.node_keys = S.node_keys0;
   S.port_hold.clear();
+  S.port_gone.clear();
+  S.outsider_gone.clear();
   S.evictions.clear();
   if ((int32_t)S.tstat_in.size() == S.n_tasks) {
     S.tstat.assign(S.tstat_in.begin(), S.tstat_in.end());  // tasks_in[t].status, packed by derive_host
@@ -4904,38 +4969,73 @@ struct Live {
   // unpipeline of a pipeline whose AddTask found its pod key already on the
   // node (statement.go:156-192): NodeInfo.RemoveTask removes by key, so the
   // pod that held the key leaves the node (node_info.go:131-157), by the
-  // status of its node copy: Running (Idle += req) or, evicted since,
-  // Releasing (Releasing -= req, Idle += req). The holder is found among the
-  // node's tasks Running at open; any other holder (placed this cycle, a pod
-  // outside the session) or one with host ports is refused.
+  // status of its node copy: Releasing (Releasing -= req, Idle += req),
+  // Pipelined (Releasing += req), anything else (Idle += req), and its host
+  // ports leave node.Pods(). The holder is a session task on the node at open
+  // (Running then — Releasing if evicted since — or any other status it kept)
+  // or a pod outside the session jobs (its copy from kbg_node_pod). A holder
+  // placed this cycle (two Pending pods sharing a key) is refused.
   kbg_status unpipeline_dup(int32_t t, int32_t n) {
     const int32_t j = S.task_job[t];
     ready(j, -1);
     S.tstat[t] = KBG_PENDING;
     if (node_has_key(S, t, n)) {
+      const int64_t hk = node_key_of(S, t, n);
       int32_t h = -1;
       for (int32_t k = S.nt_off[n]; k < S.nt_off[n + 1] && h < 0; ++k) {
         const int32_t u = S.nt_task[k];
         if (u != t && S.task_key[u] == S.task_key[t] && !S.t_detached[u]) h = u;
       }
-      const int32_t hs = h >= 0 ? S.tasks_in[h].spec : -1;
-      if (h < 0 || (hs >= 0 && S.specs_in[hs].has_host_ports))
+      if (h < 0)  // a session task on the node at open in another status (it keeps it all cycle)
+        for (int32_t u : S.node_task_order[n])
+          if (u != t && S.task_key[u] == S.task_key[t] && S.tstat_in[u] != KBG_RUNNING && !S.t_detached[u]) {
+            h = u;
+            break;
+          }
+      const Session::Outsider* o = nullptr;
+      if (h < 0) {
+        auto oit = S.outsiders.find(hk);
+        if (oit != S.outsiders.end() && oit->second.status != 0 && !S.outsider_gone.count(hk)) o = &oit->second;
+      }
+      if (h < 0 && !o)
         return fail(KBG_E_UNSUPPORTED, "statement discard of a pipeline whose pod key is held on the node by a pod "
-                                       "the session did not find Running there at open, or one with host ports "
-                                       "(node_info.go:131-157 removes it): run the reference path");
+                                       "placed this cycle, or by a pod outside the session jobs with no node_pods "
+                                       "entry (node_info.go:131-157 removes it): run the reference path");
+      Res r;
+      int32_t status;
+      if (h >= 0) {
+        r = S.treq[h];
+        status = S.tstat_in[h] != KBG_RUNNING ? S.tstat_in[h] : S.trun[h] ? KBG_RUNNING : KBG_RELEASING;
+      } else {
+        r = to_res(o->req);
+        status = o->status;
+      }
       if (!S.nil_node[n]) {
-        const Res& r = S.treq[h];
-        if (!S.trun[h] && !kbg::res_sub(S.rel[n], r))  // the copy is Releasing (evicted since open)
-          return fail(KBG_E_REF_PANIC, "statement discard: RemoveTask Releasing.Sub underflow (node_info.go:143)");
-        kbg::res_add(S.idle[n], r);
+        if (status == KBG_RELEASING) {
+          if (!kbg::res_sub(S.rel[n], r))
+            return fail(KBG_E_REF_PANIC, "statement discard: RemoveTask Releasing.Sub underflow (node_info.go:143)");
+          kbg::res_add(S.idle[n], r);
+        } else if (status == KBG_PIPELINED) {
+          kbg::res_add(S.rel[n], r);
+        } else {
+          kbg::res_add(S.idle[n], r);
+        }
       }
       S.ntasks[n]--;
-      S.node_keys.erase(node_key_of(S, t, n));
-      if (S.trun[h]) {
-        S.trun[h] = 0;  // no longer in node.Tasks: not a victim candidate
-        if (S.t_pos[h] >= 0) vt_delta(S, 0, S.t_pos[h], 0, 0, 0);
+      S.node_keys.erase(hk);
+      if (h >= 0) {
+        const int32_t hs = S.tasks_in[h].spec;
+        if (hs >= 0 && S.specs_in[hs].port_len > 0)
+          release_open_ports(S, n, &S.ports_in[S.specs_in[hs].port_off], S.specs_in[hs].port_len);
+        if (S.trun[h]) {
+          S.trun[h] = 0;  // no longer in node.Tasks: not a victim candidate
+          if (S.t_pos[h] >= 0) vt_delta(S, 0, S.t_pos[h], 0, 0, 0);
+        }
+        S.t_detached[h] = 1;
+      } else {
+        if (!o->ports.empty()) release_open_ports(S, n, o->ports.data(), (int32_t)o->ports.size());
+        S.outsider_gone.insert(hk);
       }
-      S.t_detached[h] = 1;
       touch(n);
     }
     if (!plugins(t, false))
@@ -5552,25 +5652,40 @@ int in_node_remove(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
   if (kit == keys.end()) return 1;
   std::vector<int32_t>& tl = S.node_task_order[n];
   // a node's session tasks hold distinct keys (AddTask refuses a key already
-  // there), so the task holding t's key is t itself whenever t is on the node
+  // there), so the task holding t's key is t itself whenever t is on the node;
+  // otherwise another session task, or a pod outside the session jobs
   auto hit = std::find(tl.begin(), tl.end(), t);
   if (hit == tl.end())
     hit = std::find_if(tl.begin(), tl.end(), [&](int32_t u) { return S.canon[S.tasks_in[u].pod_key] == key; });
-  if (hit == tl.end())
+  const int64_t hk = ((int64_t)n << 32) | (uint32_t)key;
+  auto oit = hit == tl.end() ? S.outsiders.find(hk) : S.outsiders.end();
+  if (hit == tl.end() && (oit == S.outsiders.end() || oit->second.status == 0))
     return fail(KBG_E_UNSUPPORTED, "the pod key is held on the node by a pod outside the session jobs "
-                                   "(its resources are unknown): re-open the session");
-  const int32_t u = *hit;
-  const int32_t sp = S.tasks_in[u].spec;
-  if (sp >= 0 && S.specs_in[sp].port_len > 0) {
+                                   "and the snapshot carried no node_pods (its resources are unknown): re-open");
+  // the holder's copy: its ports, Resreq and status
+  std::vector<kbg_host_port> gone;
+  Res r;
+  int32_t status;
+  if (hit != tl.end()) {
+    const int32_t u = *hit;
+    const int32_t sp = S.tasks_in[u].spec;
+    if (sp >= 0)
+      for (int32_t i = 0; i < S.specs_in[sp].port_len; ++i) gone.push_back(S.ports_in[S.specs_in[sp].port_off + i]);
+    r = S.treq[u];
+    status = S.tasks_in[u].status;
+  } else {
+    gone = oit->second.ports;
+    r = to_res(oit->second.req);
+    status = oit->second.status;
+  }
+  if (!gone.empty()) {
     // the pod's host ports leave the node's: node.Pods() no longer lists it,
     // so a port stays used exactly while another pod's entry remains (the
     // node's list holds one entry per pod and port, kbgpu.h kbg_node)
     auto canon_ip = [&](int32_t id) { return S.strs[id].empty() ? std::string("0.0.0.0") : S.strs[id]; };
     auto canon_proto = [&](int32_t id) { return S.strs[id].empty() ? std::string("TCP") : S.strs[id]; };
     std::vector<kbg_host_port> mine(S.ports_in.begin() + nd.port_off, S.ports_in.begin() + nd.port_off + nd.port_len);
-    const kbg_spec& spec = S.specs_in[sp];
-    for (int32_t i = 0; i < spec.port_len; ++i) {
-      const kbg_host_port& hp = S.ports_in[spec.port_off + i];
+    for (const kbg_host_port& hp : gone) {
       if (hp.host_port <= 0) continue;
       const std::string ip = canon_ip(hp.host_ip), pr = canon_proto(hp.protocol);
       auto it = std::find_if(mine.begin(), mine.end(), [&](const kbg_host_port& x) {
@@ -5582,9 +5697,8 @@ int in_node_remove(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
     nd.port_len = (int32_t)mine.size();
     S.ports_in.insert(S.ports_in.end(), mine.begin(), mine.end());
   }
-  const Res r = S.treq[u];
   if (nd.has_node) {
-    switch (S.tasks_in[u].status) {
+    switch (status) {
       case KBG_RELEASING:
         if (!kres_sub(nd.releasing, r)) return fail(KBG_E_REF_PANIC, "RemoveTask: Releasing.Sub underflow");
         kres_add(nd.idle, r);
@@ -5600,7 +5714,8 @@ int in_node_remove(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
   keys.erase(kit);
   if ((size_t)key < S.kc_node.size()) S.kc_node[key]--;
   S.upd_keys.push_back(key);
-  tl.erase(hit);
+  if (hit != tl.end()) tl.erase(hit);
+  else S.outsiders.erase(oit);  // the cache's node no longer holds it, for good
   U.touch(n);
   return 0;
 }
@@ -5714,7 +5829,7 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
   auto status_ok = [](int32_t st) { return st > 0 && st <= KBG_UNKNOWN && !(st & (st - 1)); };
   bool port_specs = false;
   for (const kbg_spec& sp : S.specs_in) port_specs |= sp.has_host_ports != 0;
-  const bool holders = port_specs || !S.outsider_keys.empty();  // else no removal can be refused
+  const bool holders = port_specs || !S.outsiders.empty();  // else no removal can be refused
   int32_t adds = 0;
   for (int32_t i = 0; i < n; ++i) adds += ev[i].kind == KBG_EV_POD_ADD;
   const int32_t T0 = S.n_tasks;
@@ -5730,11 +5845,12 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
     const kbg_task& k = S.tasks_in[t];
     return Now{S.task_node[t], k.status, S.canon[k.pod_key], k.spec};
   };
-  auto holder = [&](int32_t nd, int32_t key) -> int32_t {  // -2: a pod outside the session jobs
+  auto holder = [&](int32_t nd, int32_t key) -> int32_t {  // -2 / -3: a pod outside the session jobs (-3: unknown)
     const int64_t hk = ((int64_t)nd << 32) | (uint32_t)key;
     auto it = hold.find(hk);
     if (it != hold.end()) return it->second;
-    if (S.outsider_keys.count(hk)) return -2;
+    auto ot = S.outsiders.find(hk);
+    if (ot != S.outsiders.end()) return ot->second.status ? -2 : -3;
     for (int32_t u : S.node_task_order[nd])
       if (S.canon[S.tasks_in[u].pod_key] == key) return u;
     return -1;
@@ -5757,10 +5873,10 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
         bool found = false;
         if (c.node >= 0) {
           const int32_t h = holder(c.node, c.key);
-          if (h == -2)
+          if (h == -3)
             return fail(KBG_E_UNSUPPORTED, "the pod key is held on the node by a pod outside the session jobs "
-                                           "(its resources are unknown): re-open the session");
-          if (h >= 0) {
+                                           "and the snapshot carried no node_pods (its resources are unknown): re-open");
+          if (h >= 0 || h == -2) {  // the holder leaves the node (in_node_remove)
             hold[((int64_t)c.node << 32) | (uint32_t)c.key] = -1;
             found = true;
           }
@@ -5928,6 +6044,8 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
     S.ntasks = S.ntasks0;
     S.node_keys = S.node_keys0;
     S.port_hold.clear();
+    S.port_gone.clear();
+    S.outsider_gone.clear();
     // host ports / pod affinity live in the class masks: refold them
     if (had_masks || S.has_ports || S.has_aff) {
       S.h_class_mask = S.h_class_mask_static;
@@ -6120,6 +6238,8 @@ kbg_status kbg_session_reset(kbg_session* s) {
   S.allocated = S.backfilled = S.reclaimed = S.preempted = S.cycle_started = false;
   S.node_keys = S.node_keys0;
   S.port_hold.clear();
+  S.port_gone.clear();
+  S.outsider_gone.clear();
   if (S.has_ports || S.has_aff) {  // the class masks carry the port fit / affinity: back to the snapshot's
     S.node_ports = S.node_ports0;
     S.h_class_mask = S.h_class_mask0;
@@ -6315,7 +6435,7 @@ struct kbg_snapshot_blob {
 namespace {
 
 constexpr char kSnapMagic[4] = {'K', 'B', 'G', 'S'};
-constexpr int kSnapCounts = 21;
+constexpr int kSnapCounts = 22;
 
 // Layout word of the wire format: a hash of the element size of every array
 // (FNV-1a over the sizes). Blobs stay readable across ABI bumps that leave the
@@ -6324,7 +6444,7 @@ uint32_t snapshot_layout() {
   const size_t sizes[] = {sizeof(kbg_node), sizeof(kbg_job), sizeof(kbg_queue), sizeof(kbg_task),
                           sizeof(kbg_resource), sizeof(kbg_spec), sizeof(kbg_term), sizeof(kbg_requirement),
                           sizeof(kbg_toleration), sizeof(kbg_taint), sizeof(kbg_plugin_option),
-                          sizeof(kbg_host_port), sizeof(kbg_pod_term)};
+                          sizeof(kbg_host_port), sizeof(kbg_pod_term), sizeof(kbg_node_pod)};
   uint32_t h = 2166136261u;
   for (size_t v : sizes) {
     h ^= (uint32_t)v;
@@ -6357,6 +6477,7 @@ void for_each_array(kbg_snapshot& s, F f) {
   f((const void**)&s.pod_terms, &s.n_pod_terms, sizeof(kbg_pod_term), 1);
   f((const void**)&s.pod_labels, &s.n_pod_labels, sizeof(int32_t), 2);
   f((const void**)&s.node_pod_keys, &s.n_node_pod_keys, sizeof(int32_t), 1);
+  f((const void**)&s.node_pods, &s.n_node_pods, sizeof(kbg_node_pod), 1);
 }
 
 struct Writer {

@@ -440,6 +440,9 @@ struct Session {
   int32_t PW = 0;                              // u64 words per port-atom set
   std::vector<uint64_t> node_ports, node_ports0;  // [N][PW] used (ip, protocol, port) atoms
   std::unordered_map<int64_t, int32_t> port_hold; // (node << 32 | atom) -> pods placed this cycle holding it
+  std::unordered_map<int64_t, int32_t> port_open; // (node << 32 | atom) -> entries of the pods there at open
+  std::unordered_map<int64_t, int32_t> port_gone; //   ... of pods a statement discard removed this cycle
+  std::unordered_map<std::string, int32_t> atom_of;  // "ip|protocol|port" -> atom
   std::vector<uint64_t> cls_conf, cls_add;     // [class][PW] atoms a class conflicts with / records
   std::vector<std::vector<int32_t>> atom_cls;  // classes that conflict with each atom
   std::vector<uint64_t> h_class_mask0, h_class_mask_static;  // at open (ports applied) / static predicate only
@@ -465,7 +468,16 @@ struct Session {
   std::vector<std::vector<int32_t>> node_task_order;  // per node: the session tasks in NodeInfo.Tasks order
   std::vector<std::vector<int32_t>> node_key_order;   // per node: PodKey (canonical id) of every pod on it
   std::vector<kbg_resource> others_in;                // Session.Others resreq
-  std::unordered_set<int64_t> outsider_keys;          // (node << 32 | key) held by pods outside the session jobs
+  // (node << 32 | key) held by pods outside the session jobs, with the node's
+  // copy as RemoveTask reads it (kbgpu.h kbg_node_pod; status 0: the snapshot
+  // carried no node_pods, so a removal by key is refused)
+  struct Outsider {
+    kbg_resource req{};
+    int32_t status = 0;
+    std::vector<kbg_host_port> ports;
+  };
+  std::unordered_map<int64_t, Outsider> outsiders;
+  std::unordered_set<int64_t> outsider_gone;          // removed by a statement discard this cycle
   std::string broken;                                 // non-empty: an update failed part-way, re-open
   bool task_ranks_stale = false;                      // tasks were added: re-rank their jobs' UIDs
   std::vector<int32_t> rank_dirty_jobs;

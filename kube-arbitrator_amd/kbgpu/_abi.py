@@ -37,7 +37,7 @@ DISABLE_QUEUE_ORDER = 1 << 5
 DISABLE_PREDICATE = 1 << 6
 PLUGIN_REGISTERED = 0x80000000  # kbg_plugin_option.flags, read when kbg_options.plugin_registry = 1
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 COMM_ID_BYTES = 128
 
 KIND_ALLOCATE = 0
@@ -59,6 +59,10 @@ class kbg_node(ctypes.Structure):
                 ("label_off", i32), ("label_len", i32), ("taint_off", i32), ("taint_len", i32),
                 ("port_off", i32), ("port_len", i32), ("task_off", i32), ("task_len", i32),
                 ("key_off", i32), ("key_len", i32)]
+
+
+class kbg_node_pod(ctypes.Structure):
+    _fields_ = [("resreq", kbg_resource), ("status", i32), ("port_len", i32)]
 
 
 class kbg_host_port(ctypes.Structure):
@@ -134,6 +138,7 @@ class kbg_snapshot(ctypes.Structure):
         ("pod_terms", P(kbg_pod_term)), ("n_pod_terms", i32),
         ("pod_labels", P(i32)), ("n_pod_labels", i32),
         ("node_pod_keys", P(i32)), ("n_node_pod_keys", i32),
+        ("node_pods", P(kbg_node_pod)), ("n_node_pods", i32),
     ]
 
 

@@ -235,6 +235,23 @@ class NodeInfo:
         self.tasks[key] = ti
         return True
 
+    def remove_task(self, ti):  # node_info.go:131-157: by PodKey, the node's copy's status
+        key = pod_key(ti.pod)
+        task = self.tasks.get(key)
+        if task is None:
+            return False  # "failed to find task"
+        if self.node is not None:
+            if task.status == RELEASING:
+                self.releasing.sub(task.resreq)
+                self.idle.add(task.resreq)
+            elif task.status == PIPELINED:
+                self.releasing.add(task.resreq)
+            else:
+                self.idle.add(task.resreq)
+            self.used.sub(task.resreq)
+        del self.tasks[key]
+        return True
+
 
 # ------------------------------------------------------------- JobInfo
 class JobInfo:

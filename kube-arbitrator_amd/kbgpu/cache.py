@@ -58,6 +58,40 @@ class SchedulerCache:
     def add_pod(self, pod):
         self._add_task(TaskInfo(pod))
 
+    # event_handlers.go:105-130: the job side, then the node side (RemoveTask by
+    # PodKey: whatever pod holds the key leaves the node); False on an error
+    def _delete_task(self, pi):
+        ok = True
+        if pi.job:
+            job = self.jobs.get(pi.job)
+            ok = job is not None and job.delete_task_info(pi)
+        if pi.node_name:
+            node = self.nodes.get(pi.node_name)
+            if node is not None and not node.remove_task(pi):
+                ok = False
+        return ok
+
+    def delete_pod(self, pod):  # :132-152 (the cache's own copy of the task when it has one)
+        pi = TaskInfo(pod)
+        job = self.jobs.get(pi.job)
+        task = job.tasks.get(pi.uid, pi) if job is not None else pi
+        if not self._delete_task(task):
+            return False
+        job = self.jobs.get(pi.job)
+        if job is not None and job.pod_group is None and job.pdb is None and not job.tasks:  # JobTerminated
+            del self.jobs[pi.job]
+        return True
+
+    def update_pod(self, old_pod, new_pod):  # :96-101: deletePod's error stops the update
+        if not self.delete_pod(old_pod):
+            return False
+        self.add_pod(new_pod)
+        return True
+
+    def update_node(self, node):  # :249-259 (every churn node update changes Allocatable)
+        if node["name"] in self.nodes:
+            self.nodes[node["name"]].set_node(node)
+
     def add_node(self, node):  # :232-240
         if node["name"] in self.nodes:  # a pod named the node first: NodeInfo(nil) gets its Node (SetNode)
             self.nodes[node["name"]].set_node(node)

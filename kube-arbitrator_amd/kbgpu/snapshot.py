@@ -64,7 +64,7 @@ class FlatSnapshot:
             qs[i].weight = q.weight
         # nodes
         nd = np.zeros(len(nodes), dtype=np.dtype(_abi.kbg_node))
-        labels, taints, ports, node_keys = [], [], [], []
+        labels, taints, ports, node_keys, node_pods = [], [], [], [], []
         for i, n in enumerate(nodes):
             obj = n.node or {}
             r = nd[i]
@@ -89,9 +89,12 @@ class FlatSnapshot:
             # leaves the node (kbg_session_update) takes exactly its own entries
             r["port_off"] = len(ports)
             for t in n.tasks.values():
+                p0 = len(ports)
                 for ip, proto, port in container_ports(t.pod):
                     if port > 0:
                         ports.append((S(ip or "0.0.0.0"), S(proto or "TCP"), port))
+                # the node's copy as RemoveTask reads it (kbgpu.h kbg_node_pod)
+                node_pods.append((t.resreq.as_tuple(), t.status, len(ports) - p0))
             r["port_len"] = len(ports) - r["port_off"]
             # NodeInfo.Tasks keys (PodKey) of every pod on the node, in order
             r["key_off"] = len(node_keys)
@@ -223,7 +226,7 @@ class FlatSnapshot:
             plugins=arr(_abi.kbg_plugin_option, plugin_rows), tier_sizes=np.asarray(tier_sizes or [0], dtype=np.int32),
             ports=arr(_abi.kbg_host_port, ports), node_tasks=np.asarray(node_tasks or [0], dtype=np.int32),
             pod_terms=arr(_abi.kbg_pod_term, pterms), pod_labels=np.asarray(plabels or [0, 0], dtype=np.int32),
-            node_pod_keys=np.asarray(node_keys or [0], dtype=np.int32))
+            node_pod_keys=np.asarray(node_keys or [0], dtype=np.int32), node_pods=arr(_abi.kbg_node_pod, node_pods))
         A = self.arrays
 
         def ptr(a, ctype):
@@ -254,6 +257,7 @@ class FlatSnapshot:
         snap.pod_terms, snap.n_pod_terms = ptr(A["pod_terms"], _abi.kbg_pod_term), len(pterms)
         snap.pod_labels, snap.n_pod_labels = ptr(A["pod_labels"], ctypes.c_int32), len(plabels) // 2
         snap.node_pod_keys, snap.n_node_pod_keys = ptr(A["node_pod_keys"], ctypes.c_int32), len(node_keys)
+        snap.node_pods, snap.n_node_pods = ptr(A["node_pods"], _abi.kbg_node_pod), len(node_pods)
         self.snap = snap
 
 

@@ -73,7 +73,7 @@ def test_corrupt_input_is_rejected():
     with pytest.raises(_abi.KbgError):
         SnapshotBlob.decode(bytes(wrong_layout))
     # inflated counts: rejected before anything is allocated (no bad_alloc, no OOM)
-    for off in range(12, 12 + 4 * 22, 4):  # n_strings, then the 21 array counts
+    for off in range(12, 12 + 4 * 23, 4):  # n_strings, then the 22 array counts
         big = bytearray(data)
         big[off:off + 4] = (0x7FFFFFFF).to_bytes(4, "little")
         with pytest.raises(_abi.KbgError):
