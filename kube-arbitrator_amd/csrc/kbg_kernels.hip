@@ -119,40 +119,6 @@ __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, d
     scan_rows<INT_MODE, REL_ZERO, ROWS, J + GROUP, GROUP>(s_req, ic, im, ig, rc, rm, rg, keep);
 }
 
-// Two words of one wave against the same rows (the fused kernel's inner
-// loop): a row's request is read from LDS once for both. Same-address LDS
-// reads cost the LDS array as many cycles as full-width ones (4 per
-// ds_read_b128, MI355X_MICROARCH.md §LDS), so with one word per read the
-// rows' broadcasts, not the compares, bound the scan; two words per read halve
-// them and give each row two independent compare chains.
-template <bool INT_MODE, int J>
-__device__ __forceinline__ void scan_row2(double q0, double q1, double q2, const double (&a)[3],
-                                          const double (&b)[3], uint32_t (&ka)[2], uint32_t (&kb)[2]) {
-  const uint64_t ma = fit_mask<INT_MODE>(a[0], a[1], a[2], q0, q1, q2);
-  const uint64_t mb = fit_mask<INT_MODE>(b[0], b[1], b[2], q0, q1, q2);
-  asm("v_writelane_b32 %0, %4, %8\n\t"
-      "v_writelane_b32 %1, %5, %8\n\t"
-      "v_writelane_b32 %2, %6, %8\n\t"
-      "v_writelane_b32 %3, %7, %8"
-      : "+v"(ka[0]), "+v"(ka[1]), "+v"(kb[0]), "+v"(kb[1])
-      : "s"((uint32_t)ma), "s"((uint32_t)(ma >> 32)), "s"((uint32_t)mb), "s"((uint32_t)(mb >> 32)), "i"(J));
-}
-template <bool INT_MODE, int ROWS, int J, int GROUP>
-__device__ __forceinline__ void scan_rows2(const double (*s_req)[3], const double (&a)[3], const double (&b)[3],
-                                           uint32_t (&ka)[2], uint32_t (&kb)[2]) {
-  double q[GROUP][3];
-#pragma unroll
-  for (int u = 0; u < GROUP; ++u) {
-    q[u][0] = s_req[J + u][0];
-    q[u][1] = s_req[J + u][1];
-    q[u][2] = s_req[J + u][2];
-  }
-  [&]<int... U>(std::integer_sequence<int, U...>) {
-    (scan_row2<INT_MODE, J + U>(q[U][0], q[U][1], q[U][2], a, b, ka, kb), ...);
-  }(std::make_integer_sequence<int, GROUP>{});
-  if constexpr (J + GROUP < ROWS) scan_rows2<INT_MODE, ROWS, J + GROUP, GROUP>(s_req, a, b, ka, kb);
-}
-
 template <bool INT_MODE, int ROWS>
 __global__ __launch_bounds__(256) void kbg_scan_kernel(NodeSoA nd, ScanGeom geo,
                                                        const uint64_t* __restrict__ class_mask,
@@ -280,7 +246,6 @@ template <bool INT_MODE, bool EARLY_EXIT, int ROWS>
 __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArgs a) {
   static_assert(ROWS % 8 == 0 && ROWS <= 2 * kFfWaves, "rows per workgroup");
   constexpr int RPW = (ROWS + kFfWaves - 1) / kFfWaves;  // rows a wave extracts (1 or 2)
-  constexpr int NW = ROWS <= 24 ? 2 : 1;  // words a wave scans per row read (32 rows: one, within 128 VGPRs)
   __shared__ double s_req[ROWS][3];
   __shared__ int32_t s_cls[ROWS];
   __shared__ uint32_t s_flags[ROWS], s_map[ROWS];  // shape flags (want << 1 | rel-zero fit); shape | writer
@@ -346,9 +311,8 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
     w.mt = q[a.stride];
   };
   const int w_last = w_hi - 1;
-  Word cur, cur2;  // this wave's words of the iteration (cur2: NW == 2)
+  Word cur;
   load_word(min(w_lo + wave, w_last), cur);
-  if constexpr (NW == 2) load_word(min(w_lo + wave + kFfWaves, w_last), cur2);
   __syncthreads();
   FF_STAMP(1);
   // the extraction state of the rows this wave owns (rows wave, wave + 16)
@@ -370,61 +334,41 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
   // words are c, c + kFfWaves, ... across rounds too; lanes >= ROWS load a
   // row's mask word they never use
   uint64_t lane_mw = a.class_mask[(size_t)cls_l * a.W + min(w_lo + wave, w_last)];
-  uint64_t lane_mw2 = NW == 2 ? a.class_mask[(size_t)cls_l * a.W + min(w_lo + wave + kFfWaves, w_last)] : 0ull;
 #pragma unroll 1
   for (int r0 = w_lo; r0 < w_hi; r0 += kFfMaxRound) {
     const int nw = min(kFfMaxRound, w_hi - r0);  // words of this round
 #pragma unroll 1
-    for (int k = wave; k < nw; k += NW * kFfWaves) {  // this wave's words of the round, NW at a time
+    for (int k = wave; k < nw; k += kFfWaves) {     // this wave's words of the round
+      // the row requests are re-read from LDS per word (kept in registers
+      // across the loop they would take 6 VGPRs per row)
       asm volatile("" ::: "memory");
-      const int c = r0 + k;                              // global 64-node words c (and c + kFfWaves)
-      const bool two = NW == 2 && k + kFfWaves < nw;     // wave-uniform
-      const int cn = min(c + NW * kFfWaves, w_last), cn2 = min(c + (NW + 1) * kFfWaves, w_last);  // the next ones
-      Word nxt, nxt2;
+      const int c = r0 + k;                           // global 64-node word
+      const int cn = min(c + kFfWaves, w_last);       // this wave's next word (the last one again at the end)
+      Word nxt;
       load_word(cn, nxt);
-      if constexpr (NW == 2) load_word(cn2, nxt2);
       const uint64_t nxt_mw = a.class_mask[(size_t)cls_l * a.W + cn];
-      const uint64_t nxt_mw2 = NW == 2 ? a.class_mask[(size_t)cls_l * a.W + cn2] : 0ull;
       const uint64_t okm = __ballot(cur.valid && (!a.cap_check || cur.nt < cur.mt));  // predicates.go:125-127 pod cap
-      const uint64_t okm2 = __ballot(cur2.valid && (!a.cap_check || cur2.nt < cur2.mt));
-      const bool rz = __ballot(cur.valid && !(cur.rc == 0.0 && cur.rm == 0.0 && cur.rg == 0.0)) == 0ull;
-      const bool rz2 = __ballot(cur2.valid && !(cur2.rc == 0.0 && cur2.rm == 0.0 && cur2.rg == 0.0)) == 0ull;
-      const uint64_t mr_zero = (flags_l & kRowRelZeroFits) ? ~0ull : 0ull;
-      // lane j < ROWS parks row j's masks of word k of the round
-      auto park = [&](int kk, const uint32_t (&keep)[4], uint64_t mr, uint64_t okw, uint64_t mwl) {
-        if (lane < ROWS) {
-          const uint64_t mw = mwl & okw;
-          const uint64_t fi = ((uint64_t)keep[0] | ((uint64_t)keep[1] << 32)) & mw;
-          s_f[kk][lane] = fi | (mr & mw);
-          s_i[kk][lane] = fi;
-        }
-      };
-      if (NW == 2 && two && rz && rz2) {  // the common case: no Releasing on either word
-        const double ia[3] = {cur.ic, cur.im, cur.ig}, ib[3] = {cur2.ic, cur2.im, cur2.ig};
-        uint32_t ka[2] = {0u, 0u}, kb[2] = {0u, 0u};
-        if constexpr (NW == 2) scan_rows2<INT_MODE, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, ia, ib, ka, kb);
-        park(k, {ka[0], ka[1], 0u, 0u}, mr_zero, okm, lane_mw);
-        park(k + kFfWaves, {kb[0], kb[1], 0u, 0u}, mr_zero, okm2, lane_mw2);
+      const bool rel_zero_wave =
+          __ballot(cur.valid && !(cur.rc == 0.0 && cur.rm == 0.0 && cur.rg == 0.0)) == 0ull;
+      uint32_t keep[4] = {0u, 0u, 0u, 0u};
+      uint64_t mr;
+      if (rel_zero_wave) {
+        scan_rows<INT_MODE, true, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm, cur.rg,
+                                                               keep);
+        mr = (flags_l & kRowRelZeroFits) ? ~0ull : 0ull;
       } else {
-        auto one = [&](int kk, const Word& w, bool z, uint64_t okw, uint64_t mwl) {
-          uint32_t keep[4] = {0u, 0u, 0u, 0u};
-          if (z) {
-            scan_rows<INT_MODE, true, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, w.ic, w.im, w.ig, w.rc, w.rm, w.rg,
-                                                                           keep);
-            park(kk, keep, mr_zero, okw, mwl);
-          } else {
-            scan_rows<INT_MODE, false, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, w.ic, w.im, w.ig, w.rc, w.rm, w.rg,
-                                                                            keep);
-            park(kk, keep, (uint64_t)keep[2] | ((uint64_t)keep[3] << 32), okw, mwl);
-          }
-        };
-        one(k, cur, rz, okm, lane_mw);
-        if (two) one(k + kFfWaves, cur2, rz2, okm2, lane_mw2);
+        scan_rows<INT_MODE, false, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm,
+                                                                cur.rg, keep);
+        mr = (uint64_t)keep[2] | ((uint64_t)keep[3] << 32);
+      }
+      if (lane < ROWS) {
+        const uint64_t mw = lane_mw & okm;
+        const uint64_t fi = ((uint64_t)keep[0] | ((uint64_t)keep[1] << 32)) & mw;
+        s_f[k][lane] = fi | (mr & mw);
+        s_i[k][lane] = fi;
       }
       cur = nxt;
-      cur2 = nxt2;
       lane_mw = nxt_mw;
-      lane_mw2 = nxt_mw2;
     }
     if (r0 == w_lo) FF_STAMP(2);
     __syncthreads();

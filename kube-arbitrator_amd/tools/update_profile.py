@@ -31,7 +31,7 @@ def main():
     uids = {t.uid for t in f0.task_objs}
     changes, _ = synth.churn(fx, 5, uids, decided, bind=1.0, done=churn, delete=0.0, add=churn, node_frac=0.0)
     evs, keep, tidx = events(f0, changes)
-    L = ctypes.CDLL(os.path.join(HERE, "libkbg_tools.so"))
+    L = ctypes.CDLL(os.environ.get("TOOLS_LIB", os.path.join(HERE, "libkbg_tools.so")))
     N = len(f0.node_names)
     idle, rel = (ctypes.c_double * (3 * N))(), (ctypes.c_double * (3 * N))()
     nt = (ctypes.c_int32 * N)()
