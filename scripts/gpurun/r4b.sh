@@ -20,4 +20,8 @@ if [ -z "$NO_TRACE" ]; then
   timeout -k 10 180 python tools/open_profile.py 3 > $O/open_c3.txt 2>&1 || { tail -20 $O/open_c3.txt; exit 1; }
   tail -30 $O/open_c3.txt
 fi
+if [ -z "$NO_RPROF" ]; then  # in-order commit cycle counters (KBG_PROFILE_RESOLVE), C3 production
+  KBG_PROFILE_RESOLVE=1 timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-resident > $O/rprof_c3.json 2> $O/rprof_c3.err || { tail -20 $O/rprof_c3.err; exit 1; }
+  grep -i "resolve" $O/rprof_c3.err | tail -6
+fi
 echo R4B_DONE
