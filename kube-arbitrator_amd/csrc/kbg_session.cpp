@@ -1067,35 +1067,52 @@ struct Resolver {
     }
     int res = -1;
     int64_t steps = 0, rechecks = 0;
-    while (k < end) {
+    // A word's candidates are taken lowest first by clearing bits (a short
+    // dependency chain: the checks of successive candidates overlap), the
+    // mirror's rows through pointers held in registers. In contended
+    // cycles most candidates are nodes touched since the scan that no
+    // longer fit, so this loop is the in-order commit's hot spot.
+    const char* panic = S.panic_node.data();
+    const int32_t* mk = mark.data();
+    const int32_t* nt = S.ntasks.data();
+    const int32_t* mt = S.maxtasks.data();
+    const Res* idle = S.idle.data();
+    const Res* rel = S.rel.data();
+    const bool cap = S.pred_active, masked = S.has_ports || S.has_aff, aff = S.has_aff, be = S.be_task[t];
+    const uint64_t* cmask = S.h_class_mask.data() + (size_t)S.task_class[t] * S.W;
+    const int32_t bs = base;
+    while (k < end && res < 0) {
       const int32_t w = k >> 6;
-      const uint64_t f = m[w].f & (~0ull << (k & 63));
-      if (!f) {
-        k = (w + 1) << 6;
-        continue;
+      uint64_t bits = m[w].f & (~0ull << (k & 63));
+      while (bits) {
+        const int32_t nd = (w << 6) | __builtin_ctzll(bits);
+        bits &= bits - 1;
+        ++steps;
+        if (panic[nd]) {
+          k = nd;
+          res = RES_PANIC;
+          break;
+        }
+        if (!(mk[nd] > bs || (aff && S.mwmark[(size_t)S.task_class[t] * S.W + w] > bs))) {
+          k = nd;
+          *node = nd;
+          *kind = ((m[w].i >> (nd & 63)) & 1ull) ? KBG_KIND_ALLOCATE : KBG_KIND_PIPELINE;
+          res = RES_OK;
+          break;
+        }
+        ++rechecks;  // touched since the scan: re-check on the host mirror (recheck())
+        if (cap && nt[nd] >= mt[nd]) continue;
+        if (masked && !((cmask[w] >> (nd & 63)) & 1ull)) continue;
+        const int v = be ? 1 : kbg::res_le(r, idle[nd]) ? 1 : kbg::res_le(r, rel[nd]) ? 2 : 0;
+        if (v) {
+          k = nd;
+          *node = nd;
+          *kind = v == 1 ? KBG_KIND_ALLOCATE : KBG_KIND_PIPELINE;
+          res = RES_OK;
+          break;
+        }
       }
-      const int32_t nd = (w << 6) | __builtin_ctzll(f);
-      k = nd;
-      ++steps;
-      if (S.panic_node[nd]) {
-        res = RES_PANIC;
-        break;
-      }
-      if (!dirty(t, nd)) {
-        *node = nd;
-        *kind = ((m[w].i >> (nd & 63)) & 1ull) ? KBG_KIND_ALLOCATE : KBG_KIND_PIPELINE;
-        res = RES_OK;
-        break;
-      }
-      ++rechecks;  // touched since the scan: re-check on the host mirror
-      const int v = recheck(t, nd, r);
-      if (v) {
-        *node = nd;
-        *kind = v == 1 ? KBG_KIND_ALLOCATE : KBG_KIND_PIPELINE;
-        res = RES_OK;
-        break;
-      }
-      ++k;
+      if (res < 0) k = (w + 1) << 6;
     }
     S.stats.resolve_steps += steps;
     S.stats.resolve_rechecks += rechecks;

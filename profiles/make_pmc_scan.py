@@ -13,7 +13,7 @@ import os
 import sys
 
 FIELDS = ("avg_ns", "launches", "hbm_bytes_per_launch", "hbm_write_bytes_per_launch", "l2_hit_rate",
-          "valu_insts_per_launch", "wait_any_share", "wait_inst_share", "active_inst_share")
+          "valu_insts_per_launch", "wait_any_share", "wait_inst_share", "active_inst_share", "wait_inst_lds_share")
 
 
 def section(k):
