@@ -51,6 +51,7 @@
 #include <vector>
 
 #include "kbg_session.hpp"
+#include "kbg_walk.hpp"
 
 // An RCCL clique of node-axis shards, one rank per GPU (kbgpu.h).
 struct kbg_comm {
@@ -1014,6 +1015,13 @@ struct Grouper {
 // (same inputs, same table): the prefix an earlier row of the shape rejected
 // is skipped instead of re-checked (`shape_skip`).
 enum { RES_OK = 0, RES_TRUNC = 1, RES_PANIC = 2 };
+// KBG_PROFILE_RESOLVE: words the mask walk visited, by how many candidates
+// touched since the scan it re-checked in them node by node (0, 1, 2-3, 4-7,
+// 8+), and words checked whole (kbg_walk.cpp)
+thread_local int64_t t_walk_words[6];
+// a word's candidates are checked whole from this many on (and half as many touched)
+constexpr int kWalkSimdMin = 8;
+constexpr double kResMins[3] = {kbg::kMinMilliCPU, kbg::kMinMemory, kbg::kMinMilliGPU};
 struct Resolver {
   Session& S;
   std::vector<int32_t>& mark;
@@ -1081,9 +1089,51 @@ struct Resolver {
     const bool cap = S.pred_active, masked = S.has_ports || S.has_aff, aff = S.has_aff, be = S.be_task[t];
     const uint64_t* cmask = S.h_class_mask.data() + (size_t)S.task_class[t] * S.W;
     const int32_t bs = base;
+    const bool simd = !be && kbg::walk_simd();
     while (k < end && res < 0) {
       const int32_t w = k >> 6;
       uint64_t bits = m[w].f & (~0ull << (k & 63));
+      const int64_t rc0 = rechecks;
+      if (simd && __builtin_popcountll(bits) >= kWalkSimdMin) {
+        // many candidates: the word's touched ones are re-checked all at once
+        // (kbg_walk.cpp), the walk stops at the first candidate that is a
+        // panic node, untouched, or fits now — what the node-by-node walk
+        // below finds, with the same counts
+        const int32_t n0 = w << 6, cnt = std::min(64, S.n_nodes - n0);
+        const uint64_t dirty =
+            bits & ((aff && S.mwmark[(size_t)S.task_class[t] * S.W + w] > bs) ? ~0ull : kbg::word_newer(mk, n0, cnt, bs));
+        if (__builtin_popcountll(dirty) >= kWalkSimdMin / 2) {
+          uint64_t fi, fr;
+          kbg::word_fits(&idle[0].c, &rel[0].c, nt, mt, cap, &r.c, kResMins, n0, cnt, &fi, &fr);
+          if (masked) {
+            fi &= cmask[w];
+            fr &= cmask[w];
+          }
+          const uint64_t pan = bits & kbg::word_flags(panic, n0, cnt);
+          const uint64_t stop = pan | (bits & ~dirty) | (dirty & (fi | fr));
+          const uint64_t upto = stop ? (2ull << __builtin_ctzll(stop)) - 1 : ~0ull;  // candidates visited
+          steps += __builtin_popcountll(bits & upto);
+          rechecks += __builtin_popcountll(dirty & upto & ~pan);
+          if (!stop) {
+            k = (w + 1) << 6;
+            t_walk_words[5]++;
+            continue;
+          }
+          const int32_t j = __builtin_ctzll(stop), nd = n0 + j;
+          k = nd;
+          if ((pan >> j) & 1ull) {
+            res = RES_PANIC;
+          } else {
+            *node = nd;
+            *kind = !((dirty >> j) & 1ull) ? (((m[w].i >> j) & 1ull) ? KBG_KIND_ALLOCATE : KBG_KIND_PIPELINE)
+                    : ((fi >> j) & 1ull)   ? KBG_KIND_ALLOCATE
+                                           : KBG_KIND_PIPELINE;
+            res = RES_OK;
+          }
+          t_walk_words[5]++;
+          break;
+        }
+      }
       while (bits) {
         const int32_t nd = (w << 6) | __builtin_ctzll(bits);
         bits &= bits - 1;
@@ -1113,6 +1163,8 @@ struct Resolver {
         }
       }
       if (res < 0) k = (w + 1) << 6;
+      const int64_t d = rechecks - rc0;
+      t_walk_words[d == 0 ? 0 : d == 1 ? 1 : d < 4 ? 2 : d < 8 ? 3 : 4]++;
     }
     S.stats.resolve_steps += steps;
     S.stats.resolve_rechecks += rechecks;
@@ -4004,6 +4056,12 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   S.fin = E_truth;
   S.stats.engine_ms = pr.engine_ms;
   S.stats.replayed = pr.replayed;
+  if (rprof) {
+    fprintf(stderr, "[kbg resolve] words walked by re-checks in them: 0: %lld, 1: %lld, 2-3: %lld, 4-7: %lld, 8+: %lld; checked whole: %lld\n",
+            (long long)t_walk_words[0], (long long)t_walk_words[1], (long long)t_walk_words[2], (long long)t_walk_words[3],
+            (long long)t_walk_words[4], (long long)t_walk_words[5]);
+    for (int64_t& x : t_walk_words) x = 0;
+  }
   if (rprof)
     fprintf(stderr, "[kbg resolve] %lld tasks, cycles/task: walk %.1f mirror %.1f log %.1f loop %.1f (incl. rescans)\n",
             (long long)S.stats.task_evaluations, (double)rcyc[0] / std::max<int64_t>(1, S.stats.task_evaluations),
