@@ -489,54 +489,3 @@ extern "C" int32_t kbg_tool_firstfit_stamps(const kbg_snapshot* snap, const kbg_
 }
 #endif
 
-// kbg_walk.cpp's word checks against the node-by-node host checks (res_le, the
-// pod cap, the touched and panic tests) on seeded random words whose values sit
-// on and around the LessEqual tolerance edges. Returns the mismatches, -1 when
-// this CPU has no AVX-512 (the library then walks node by node).
-extern "C" int64_t kbg_tool_walk_check(uint64_t seed, int32_t trials) {
-  if (!kbg::walk_simd()) return -1;
-  std::mt19937_64 rng(seed);
-  int64_t bad = 0;
-  for (int32_t trial = 0; trial < trials; ++trial) {
-    const int32_t N = 1 + (int32_t)(rng() % 200);
-    std::vector<Res> idle(N), rel(N);
-    std::vector<int32_t> nt(N), mt(N), mark(N);
-    std::vector<char> pan(N);
-    const Res r{(double)(rng() % 4000), (double)(rng() % (1ull << 33)), (double)(rng() % 3) * 1000};
-    auto pick = [&](double q, double mn) {
-      switch (rng() % 7) {
-        case 0: return q;
-        case 1: return q + mn * 0.5;
-        case 2: return q - mn * 0.5;
-        case 3: return q - mn;
-        case 4: return q + mn;
-        case 5: return std::nextafter(q - mn, 0.0);
-        default: return (double)(rng() % (uint64_t)(2 * q + 100));
-      }
-    };
-    for (int32_t n = 0; n < N; ++n) {
-      idle[n] = Res{pick(r.c, kbg::kMinMilliCPU), pick(r.m, kbg::kMinMemory), pick(r.g, kbg::kMinMilliGPU)};
-      rel[n] = Res{pick(r.c, kbg::kMinMilliCPU), pick(r.m, kbg::kMinMemory), pick(r.g, kbg::kMinMilliGPU)};
-      nt[n] = (int32_t)(rng() % 5);
-      mt[n] = (int32_t)(rng() % 5);
-      mark[n] = (int32_t)(rng() % 10);
-      pan[n] = rng() % 17 == 0;
-    }
-    const bool cap = rng() & 1;
-    const int32_t n0 = (int32_t)(rng() % N), cnt = std::min<int32_t>(64, N - n0), base = (int32_t)(rng() % 10);
-    uint64_t fi, fr;
-    kbg::word_fits(&idle[0].c, &rel[0].c, nt.data(), mt.data(), cap, &r.c, kResMins, n0, cnt, &fi, &fr);
-    const uint64_t nw = kbg::word_newer(mark.data(), n0, cnt, base), pf = kbg::word_flags(pan.data(), n0, cnt);
-    for (int32_t j = 0; j < cnt; ++j) {
-      const int32_t n = n0 + j;
-      int v = 0;
-      if (!(cap && nt[n] >= mt[n])) v = kbg::res_le(r, idle[n]) ? 1 : kbg::res_le(r, rel[n]) ? 2 : 0;
-      const int got = ((fi >> j) & 1) ? 1 : ((fr >> j) & 1) ? 2 : 0;
-      bad += got != v;
-      bad += (int)((nw >> j) & 1) != (int)(mark[n] > base);
-      bad += (int)((pf >> j) & 1) != (int)(pan[n] != 0);
-    }
-    if (cnt < 64) bad += ((fi | fr | nw | pf) >> cnt) != 0;
-  }
-  return bad;
-}
