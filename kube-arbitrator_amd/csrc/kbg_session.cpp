@@ -29,7 +29,6 @@
 #include <sched.h>
 
 #include <algorithm>
-#include <limits>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -1015,11 +1014,6 @@ struct Grouper {
 // (same inputs, same table): the prefix an earlier row of the shape rejected
 // is skipped instead of re-checked (`shape_skip`).
 enum { RES_OK = 0, RES_TRUNC = 1, RES_PANIC = 2 };
-// KBG_PROFILE_RESOLVE: words the mask walk visited, by how many candidates
-// touched since the scan it re-checked in them (0, 1, 2-3, 4-7, 8+)
-thread_local int64_t t_walk_words[6];
-// a group's bounds are refreshed after this many failed re-checks in it by one walk
-constexpr int kTightenFails = 2;
 struct Resolver {
   Session& S;
   std::vector<int32_t>& mark;
@@ -1028,47 +1022,6 @@ struct Resolver {
   std::vector<int32_t> cursor;
   std::vector<int32_t> shape_skip, skip_stamp;
   int32_t skip_gen = 0;
-  // Per 8-node group: upper bounds of the nodes' Idle and Releasing cpu and
-  // memory (idle c, idle m, rel c, rel m), unknown (+inf) until a walk
-  // re-checks kTightenFails of the group's nodes in vain and takes their
-  // current maxima. Within a walk of the cycle Idle and Releasing only shrink
-  // (mirror_add), so a bound stays an upper bound; the sharded rollback,
-  // which restores rows, raises them (raise). res_le is monotone in the
-  // capacity, so a request whose cpu or memory exceeds a group's Idle bound
-  // and whose cpu or memory exceeds its Releasing bound fits none of the
-  // group's nodes: its touched candidates there fail without their rows
-  // being read.
-  std::vector<double> gb;
-  bool beyond(int32_t g, const Res& r) const {
-    const double* b = &gb[(size_t)g * 4];
-    auto le1 = [](double q, double a, double mn) { return q < a || __builtin_fabs(a - q) < mn; };
-    return (!le1(r.c, b[0], kbg::kMinMilliCPU) || !le1(r.m, b[1], kbg::kMinMemory)) &&
-           (!le1(r.c, b[2], kbg::kMinMilliCPU) || !le1(r.m, b[3], kbg::kMinMemory));
-  }
-  void tighten(int32_t g) {
-    const int32_t n0 = g << 3, n1 = std::min(S.n_nodes, n0 + 8);
-    double a = -std::numeric_limits<double>::infinity(), b = a, c = a, d = a;
-    for (int32_t n = n0; n < n1; ++n) {
-      a = std::max(a, S.idle[n].c);
-      b = std::max(b, S.idle[n].m);
-      c = std::max(c, S.rel[n].c);
-      d = std::max(d, S.rel[n].m);
-    }
-    double* o = &gb[(size_t)g * 4];
-    o[0] = a;
-    o[1] = b;
-    o[2] = c;
-    o[3] = d;
-    t_walk_words[5]++;
-  }
-  void raise(int32_t n) {  // node n's rows were restored (sharded rollback)
-    if (gb.empty()) return;
-    double* o = &gb[(size_t)(n >> 3) * 4];
-    o[0] = std::max(o[0], S.idle[n].c);
-    o[1] = std::max(o[1], S.idle[n].m);
-    o[2] = std::max(o[2], S.rel[n].c);
-    o[3] = std::max(o[3], S.rel[n].m);
-  }
   void reset(const kbg::Stage& stage) {
     sg = &stage;
     base = stage.base;
@@ -1128,14 +1081,9 @@ struct Resolver {
     const bool cap = S.pred_active, masked = S.has_ports || S.has_aff, aff = S.has_aff, be = S.be_task[t];
     const uint64_t* cmask = S.h_class_mask.data() + (size_t)S.task_class[t] * S.W;
     const int32_t bs = base;
-    const bool bound = !be && S.n_nodes > 0;
-    if (bound && gb.empty()) gb.assign((size_t)((S.n_nodes + 7) >> 3) * 4, std::numeric_limits<double>::infinity());
     while (k < end && res < 0) {
       const int32_t w = k >> 6;
       uint64_t bits = m[w].f & (~0ull << (k & 63));
-      const int64_t rc0 = rechecks;
-      int32_t g = -1, gfails = 0;
-      bool hopeless = false;
       while (bits) {
         const int32_t nd = (w << 6) | __builtin_ctzll(bits);
         bits &= bits - 1;
@@ -1153,13 +1101,8 @@ struct Resolver {
           break;
         }
         ++rechecks;  // touched since the scan: re-check on the host mirror (recheck())
-        if (bound && (nd >> 3) != g) {
-          g = nd >> 3;
-          gfails = 0;
-          hopeless = beyond(g, r);
-        }
-        if (hopeless) continue;  // fits no node of its group: not read
-        if ((cap && nt[nd] >= mt[nd]) || (masked && !((cmask[w] >> (nd & 63)) & 1ull))) continue;
+        if (cap && nt[nd] >= mt[nd]) continue;
+        if (masked && !((cmask[w] >> (nd & 63)) & 1ull)) continue;
         const int v = be ? 1 : kbg::res_le(r, idle[nd]) ? 1 : kbg::res_le(r, rel[nd]) ? 2 : 0;
         if (v) {
           k = nd;
@@ -1168,13 +1111,7 @@ struct Resolver {
           res = RES_OK;
           break;
         }
-        if (bound && ++gfails == kTightenFails) {  // the group's bounds are stale: take its current maxima
-          tighten(g);
-          hopeless = beyond(g, r);
-        }
       }
-      const int64_t d = rechecks - rc0;
-      t_walk_words[d == 0 ? 0 : d == 1 ? 1 : d < 4 ? 2 : d < 8 ? 3 : 4]++;
       if (res < 0) k = (w + 1) << 6;
     }
     S.stats.resolve_steps += steps;
@@ -4067,12 +4004,6 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   S.fin = E_truth;
   S.stats.engine_ms = pr.engine_ms;
   S.stats.replayed = pr.replayed;
-  if (rprof) {
-    fprintf(stderr, "[kbg resolve] words walked by re-checks in them: 0: %lld, 1: %lld, 2-3: %lld, 4-7: %lld, 8+: %lld; group refreshes %lld\n",
-            (long long)t_walk_words[0], (long long)t_walk_words[1], (long long)t_walk_words[2], (long long)t_walk_words[3],
-            (long long)t_walk_words[4], (long long)t_walk_words[5]);
-    for (int64_t& x : t_walk_words) x = 0;
-  }
   if (rprof)
     fprintf(stderr, "[kbg resolve] %lld tasks, cycles/task: walk %.1f mirror %.1f log %.1f loop %.1f (incl. rescans)\n",
             (long long)S.stats.task_evaluations, (double)rcyc[0] / std::max<int64_t>(1, S.stats.task_evaluations),
@@ -4276,7 +4207,6 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
       const int32_t t = bt[u.pos];
       if (!u.dup) {
         if (!S.nil_node[u.node]) (u.kind == KBG_KIND_ALLOCATE ? S.idle[u.node] : S.rel[u.node]) = u.old;
-        rs.raise(u.node);
         S.ntasks[u.node]--;
         if (S.has_ports) remove_ports(S, S.task_class[t], u.node);
         if (S.has_dupkeys && S.key_hot[S.task_key[t]]) S.node_keys.erase(node_key_of(S, t, u.node));
