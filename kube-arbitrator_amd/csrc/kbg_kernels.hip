@@ -102,6 +102,50 @@ constexpr int kRowGroup = 8;
 #define KBG_SMALL_BATCH_ROWS 1024
 #endif
 constexpr int kSmallBatchRows = KBG_SMALL_BATCH_ROWS;  // launch_scan: batches up to this many rows use 16-row workgroups
+// Integer mode, no Releasing: rows J and J+1 together, their six compares
+// issued back to back into six SGPR pairs before the first scalar AND reads
+// one (a row's compares no longer wait on each other through VCC).
+template <int J>
+__device__ __forceinline__ void scan_row_pair(const double (&q)[2][3], double ic, double im, double ig,
+                                              uint32_t (&keep)[4]) {
+  uint64_t a0, a1, a2, b0, b1, b2;
+  asm("v_cmp_gt_f64_e64 %0, %6, %9\n\t"
+      "v_cmp_gt_f64_e64 %1, %7, %10\n\t"
+      "v_cmp_gt_f64_e64 %2, %8, %11\n\t"
+      "v_cmp_gt_f64_e64 %3, %6, %12\n\t"
+      "v_cmp_gt_f64_e64 %4, %7, %13\n\t"
+      "v_cmp_gt_f64_e64 %5, %8, %14"
+      : "=&s"(a0), "=&s"(a1), "=&s"(a2), "=&s"(b0), "=&s"(b1), "=&s"(b2)
+      : "v"(ic), "v"(im), "v"(ig), "v"(q[0][0]), "v"(q[0][1]), "v"(q[0][2]), "v"(q[1][0]), "v"(q[1][1]), "v"(q[1][2]));
+  const uint64_t ma = a0 & a1 & a2, mb = b0 & b1 & b2;
+  asm("v_writelane_b32 %0, %2, %6\n\t"
+      "v_writelane_b32 %1, %3, %6\n\t"
+      "v_writelane_b32 %0, %4, %7\n\t"
+      "v_writelane_b32 %1, %5, %7"
+      : "+v"(keep[0]), "+v"(keep[1])
+      : "s"((uint32_t)ma), "s"((uint32_t)(ma >> 32)), "s"((uint32_t)mb), "s"((uint32_t)(mb >> 32)), "i"(J), "i"(J + 1));
+}
+
+// (integer mode, no Releasing: the next group's requests are read from LDS
+// while this group's compares run)
+template <int ROWS, int J, int GROUP>
+__device__ __forceinline__ void scan_rows_int(const double (*s_req)[3], const double (&q)[GROUP][3], double ic,
+                                              double im, double ig, uint32_t (&keep)[4]) {
+  double qn[GROUP][3];
+  if constexpr (J + GROUP < ROWS) {
+#pragma unroll
+    for (int u = 0; u < GROUP; ++u) {
+      qn[u][0] = s_req[J + GROUP + u][0];
+      qn[u][1] = s_req[J + GROUP + u][1];
+      qn[u][2] = s_req[J + GROUP + u][2];
+    }
+  }
+  [&]<int... U>(std::integer_sequence<int, U...>) {
+    (scan_row_pair<J + 2 * U>(*reinterpret_cast<const double(*)[2][3]>(&q[2 * U][0]), ic, im, ig, keep), ...);
+  }(std::make_integer_sequence<int, GROUP / 2>{});
+  if constexpr (J + GROUP < ROWS) scan_rows_int<ROWS, J + GROUP, GROUP>(s_req, qn, ic, im, ig, keep);
+}
+
 template <bool INT_MODE, bool REL_ZERO, int ROWS, int J = 0, int GROUP = kRowGroup>
 __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, double im, double ig, double rc,
                                           double rm, double rg, uint32_t (&keep)[4]) {
@@ -112,9 +156,18 @@ __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, d
     q[u][1] = s_req[J + u][1];
     q[u][2] = s_req[J + u][2];
   }
-  [&]<int... U>(std::integer_sequence<int, U...>) {
-    (scan_row<INT_MODE, REL_ZERO, J + U>(q[U][0], q[U][1], q[U][2], ic, im, ig, rc, rm, rg, keep), ...);
-  }(std::make_integer_sequence<int, GROUP>{});
+  if constexpr (INT_MODE && REL_ZERO && GROUP % 2 == 0 && J == 0) {
+    scan_rows_int<ROWS, 0, GROUP>(s_req, q, ic, im, ig, keep);
+    return;
+  } else if constexpr (INT_MODE && REL_ZERO && GROUP % 2 == 0) {
+    [&]<int... U>(std::integer_sequence<int, U...>) {
+      (scan_row_pair<J + 2 * U>(*reinterpret_cast<const double(*)[2][3]>(&q[2 * U][0]), ic, im, ig, keep), ...);
+    }(std::make_integer_sequence<int, GROUP / 2>{});
+  } else {
+    [&]<int... U>(std::integer_sequence<int, U...>) {
+      (scan_row<INT_MODE, REL_ZERO, J + U>(q[U][0], q[U][1], q[U][2], ic, im, ig, rc, rm, rg, keep), ...);
+    }(std::make_integer_sequence<int, GROUP>{});
+  }
   if constexpr (J + GROUP < ROWS)
     scan_rows<INT_MODE, REL_ZERO, ROWS, J + GROUP, GROUP>(s_req, ic, im, ig, rc, rm, rg, keep);
 }
