@@ -688,7 +688,9 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
       a.avail = S.d_down;
       a.avail_bit = 1u << S.shard;
     }
-    HIP_TRY(kbg::launch_firstfit(a, S.int_mode ? 1 : 0, S.stream, sg.ev[0], sg.ev[1]));
+    sg.timed = !S.untimed_launches;
+    HIP_TRY(kbg::launch_firstfit(a, S.int_mode ? 1 : 0, S.stream, sg.timed ? sg.ev[0] : nullptr,
+                                 sg.timed ? sg.ev[1] : nullptr));
     trace_add("l.firstfit");
 
     if (avail) {
@@ -767,8 +769,10 @@ kbg_status device_wait(Session& S, kbg::Stage& sg) {
     sg.h_cand = sg.h_down + G;
   }
   float ms = 0;
-  HIP_TRY(hipEventElapsedTime(&ms, sg.ev[0], sg.ev[1]));
-  S.stats.scan_kernel_ms += ms;
+  if (!sg.fused || sg.timed) {
+    HIP_TRY(hipEventElapsedTime(&ms, sg.ev[0], sg.ev[1]));
+    S.stats.scan_kernel_ms += ms;
+  }
   if (!sg.fused) {
     HIP_TRY(hipEventElapsedTime(&ms, sg.ev[2], sg.ev[3]));
     S.stats.select_kernel_ms += ms;

@@ -265,6 +265,7 @@ struct Stage {
   int32_t G = 0;
   int32_t base = 0;                  // the scan saw every node delta of resolutions with stamp <= base
   bool inflight = false;             // launched, results not yet collected
+  bool timed = true;                 // the fused launch carries start / stop events (ev[0], ev[1])
   bool fused = false;                // kbg_firstfit_kernel (no select kernel, no copies)
   hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // scan, select,
                                      // exchange start/stop; [6] = results on the host
@@ -436,6 +437,7 @@ struct Session {
   // grow during a cycle, so a (class, node) pair only ever loses feasibility:
   // the port fit is folded into the class masks and kept current by clearing
   // bits as placements record ports (monotone, like the pod cap).
+  bool untimed_launches = false;  // (developer tools) fused launches without start / stop events
   bool has_ports = false;
   int32_t PW = 0;                              // u64 words per port-atom set
   std::vector<uint64_t> node_ports, node_ports0;  // [N][PW] used (ip, protocol, port) atoms

@@ -489,3 +489,38 @@ extern "C" int32_t kbg_tool_firstfit_stamps(const kbg_snapshot* snap, const kbg_
 }
 #endif
 
+
+// Host cost of one fused launch (device_launch: arguments, the launch call,
+// the completion event) and of the whole round trip (launch + wait), medians
+// over `reps` launches of the first G pending tasks' rows; untimed != 0
+// launches without the kernel's start / stop events.
+extern "C" int32_t kbg_tool_launch_cost(const kbg_snapshot* snap, const kbg_options* o, int32_t G, int32_t reps,
+                                        int32_t untimed, double* launch_us, double* roundtrip_us) {
+  Session S;
+  if (open_session(S, snap, o, nullptr) != KBG_OK) return -1;
+  S.untimed_launches = untimed != 0;
+  std::vector<int32_t> bt;
+  for (int32_t t : S.pend_all) {
+    if ((int32_t)bt.size() == std::min(G, S.K)) break;
+    bt.push_back(t);
+  }
+  Grouper grouper(S);
+  kbg::Stage& sg = S.stages[0];
+  const int32_t rows = grouper.build(sg, bt.data(), (int32_t)bt.size());
+  std::vector<double> l, rt;
+  for (int32_t r = 0; r < reps; ++r) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (device_launch(S, sg, rows, S.res_stamp) != KBG_OK) return free_device(S), -2;
+    const auto t1 = std::chrono::steady_clock::now();
+    if (device_wait(S, sg) != KBG_OK) return free_device(S), -3;
+    const auto t2 = std::chrono::steady_clock::now();
+    l.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+    rt.push_back(std::chrono::duration<double, std::micro>(t2 - t0).count());
+  }
+  free_device(S);
+  std::sort(l.begin(), l.end());
+  std::sort(rt.begin(), rt.end());
+  *launch_us = l[l.size() / 2];
+  *roundtrip_us = rt[rt.size() / 2];
+  return rows;
+}
