@@ -311,7 +311,8 @@ typedef struct kbg_stats {
   int64_t mispredictions;  /* batches cut by an unpredicted failure */
   int64_t truncations;     /* rescans of a batch remainder after an exhausted candidate list */
   int64_t scan_launches;
-  double scan_kernel_ms;   /* summed HIP-event time of the scan kernel */
+  double scan_kernel_ms;   /* scan-kernel time: the fused kernel's HIP-event time of every 4th launch x
+                              launches / timed launches (events lengthen a round trip by ≈ 7 µs) */
   double select_kernel_ms; /* summed HIP-event time of the candidate-select kernel */
   double allocate_ms;      /* wall time of the last kbg_allocate */
   double open_ms;          /* wall time of kbg_session_open */

@@ -629,6 +629,7 @@ struct Trace;
 thread_local Trace* t_trace = nullptr;  // the committer's KBG_TRACE timeline, if on
 void trace_add(const char* what, int64_t v = 0);
 
+constexpr int64_t kFfTimeEvery = 4;  // fused launches: one in this many carries start / stop events
 kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   trace_add("l.begin", G);
   const int32_t Gp = kbg::kbg_pad_rows(G);  // Grouper::build padded the rows
@@ -688,7 +689,7 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
       a.avail = S.d_down;
       a.avail_bit = 1u << S.shard;
     }
-    sg.timed = !S.untimed_launches;
+    sg.timed = !S.untimed_launches && S.ff_launch_seq++ % kFfTimeEvery == 0;
     HIP_TRY(kbg::launch_firstfit(a, S.int_mode ? 1 : 0, S.stream, sg.timed ? sg.ev[0] : nullptr,
                                  sg.timed ? sg.ev[1] : nullptr));
     trace_add("l.firstfit");
@@ -769,9 +770,13 @@ kbg_status device_wait(Session& S, kbg::Stage& sg) {
     sg.h_cand = sg.h_down + G;
   }
   float ms = 0;
-  if (!sg.fused || sg.timed) {
+  if (!sg.fused) {
     HIP_TRY(hipEventElapsedTime(&ms, sg.ev[0], sg.ev[1]));
     S.stats.scan_kernel_ms += ms;
+  } else if (sg.timed) {
+    HIP_TRY(hipEventElapsedTime(&ms, sg.ev[0], sg.ev[1]));
+    S.ff_timed_ms += ms;
+    S.ff_timed++;
   }
   if (!sg.fused) {
     HIP_TRY(hipEventElapsedTime(&ms, sg.ev[2], sg.ev[3]));
@@ -782,6 +787,7 @@ kbg_status device_wait(Session& S, kbg::Stage& sg) {
     S.stats.exchange_ms += ms;
   }
   S.stats.scan_launches++;
+  if (sg.fused && S.ff_timed) S.stats.scan_kernel_ms = S.ff_timed_ms / S.ff_timed * (double)S.stats.scan_launches;
   S.stats.evaluations += G;
   S.stats.node_visits += (int64_t)G * (S.comm ? S.tab_n : S.n_nodes);
   return KBG_OK;
@@ -3055,6 +3061,8 @@ void begin_cycle(Session& S) {
   S.stats = kbg_stats{};
   S.vk_timed_ms = 0;
   S.vk_timed = 0;
+  S.ff_timed_ms = 0;
+  S.ff_timed = 0;
   S.stats.n_classes = prev.n_classes;
   S.stats.shards = prev.shards;
   S.stats.shard_index = prev.shard_index;
@@ -3346,7 +3354,11 @@ struct Predictor {
         all.push_back(b);
       }
       const auto tp = clk::now();
-      if (!truth_mode) b->ckpt = E;
+      if (!truth_mode) {
+        tr.add("ckpt.begin");
+        b->ckpt = E;
+        tr.add("ckpt");
+      }
       b->epoch = my_epoch;
       b->bt.clear();
       b->bpred.clear();
@@ -3765,7 +3777,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     for (int32_t i = 0; i < nb; ++i) {
       const int32_t t = bt[i];
       if ((i & 511) == 511) to_truth(bt, i);  // keep the truth engine a few hundred tasks behind
-      if ((i & 1023) == 1023 && !nxt && !pred_failed && !reuse) {
+      if ((i & 255) == 255 && !nxt && !pred_failed && !reuse) {
         // the predictor's next batch, if it is ready now, scans while this one resolves
         nxt = next_batch(false);
         if (nxt && !nxt->bt.empty()) {

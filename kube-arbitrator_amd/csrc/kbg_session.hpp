@@ -422,6 +422,11 @@ struct Session {
   bool vstage_busy = false;                   // a prep launch may still read the staging buffers
   double vk_timed_ms = 0;                     // sampled victim-scan kernel time (this cycle)
   int64_t vk_timed = 0;
+  // fused first-fit launches: start / stop events on one launch in
+  // kFfTimeEvery (each timed launch adds ≈ 7 µs to its round trip); the
+  // sampled time scaled to every launch of the cycle is scan_kernel_ms
+  double ff_timed_ms = 0;
+  int64_t ff_timed = 0, ff_launch_seq = 0;
   std::vector<kbg::StateDelta> sdeltas;       // queued victim-table changes
   std::vector<int32_t> be_shape;              // per pod-spec class: grouping id of its BestEffort tasks
   std::vector<int32_t> committed_ready;

@@ -1,13 +1,20 @@
 """Developer tool: A/B of library builds on the C3 bench (production and full-scan
-p50), alternating in one GPU session: python kube-arbitrator_amd/tools/ab_bench.py lib1.so lib2.so"""
-import json, subprocess, sys
+p50), alternating in one GPU session: python kube-arbitrator_amd/tools/ab_bench.py lib1.so lib2.so
+(CONFIG=4: another BASELINE config; REPS: rounds; lib.so@KEY=VAL sets a variant's environment)"""
+import json, os, subprocess, sys
 res = {}
-for rep in range(3):
+cfg = os.environ.get("CONFIG", "3")
+for rep in range(int(os.environ.get("REPS", "3"))):
     for v in sys.argv[1:]:
         code = ("import sys; sys.path.insert(0,'kube-arbitrator_amd'); from kbgpu import _abi; _abi.LIB_PATH='%s'; "
-                "sys.argv=['bench.py','--steps','10','--warmup','2','--no-cpu-baseline','--no-resident']; "
-                "import runpy; runpy.run_path('bench.py', run_name='__main__')") % v
-        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+                "sys.argv=['bench.py','--config','%s','--steps','10','--warmup','2','--no-cpu-baseline','--no-resident']; "
+                "import runpy; runpy.run_path('bench.py', run_name='__main__')") % (v, cfg)
+        env = dict(os.environ)
+        for kv in v.split("@")[1:]:  # lib.so@KEY=VAL@...: the variant's environment
+            k, _, val = kv.partition("=")
+            env[k] = val
+        out = subprocess.run([sys.executable, "-c", code.replace(v, v.split("@")[0])], capture_output=True, text=True,
+                             timeout=300, env=env)
         d = json.loads(out.stdout.strip().splitlines()[-1])
         res.setdefault(v, []).append((round(d["p50_cycle_ms"], 2), round(d["full_scan_mode"]["p50_cycle_ms"], 2)))
         print(v, res[v][-1], flush=True)

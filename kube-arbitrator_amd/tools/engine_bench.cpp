@@ -443,6 +443,7 @@ extern "C" double kbg_tool_firstfit_bench(const kbg_snapshot* snap, const kbg_op
   const int32_t rows = grouper.build(sg, bt.data(), (int32_t)bt.size());
   std::vector<double> us;
   for (int32_t r = 0; r < reps; ++r) {
+    S.ff_launch_seq = 0;  // every launch of the probe carries its events
     if (device_scan(S, sg, rows, S.res_stamp) != KBG_OK) {
       free_device(S);
       return -2.0;
@@ -509,6 +510,7 @@ extern "C" int32_t kbg_tool_launch_cost(const kbg_snapshot* snap, const kbg_opti
   const int32_t rows = grouper.build(sg, bt.data(), (int32_t)bt.size());
   std::vector<double> l, rt;
   for (int32_t r = 0; r < reps; ++r) {
+    S.ff_launch_seq = 0;  // timed variant: events on every launch
     const auto t0 = std::chrono::steady_clock::now();
     if (device_launch(S, sg, rows, S.res_stamp) != KBG_OK) return free_device(S), -2;
     const auto t1 = std::chrono::steady_clock::now();
