@@ -231,20 +231,28 @@ kbg::JobKey make_job_key(const Session& S, const Engine& E, int32_t j) {
   return (k << 32) | (uint32_t)S.job_frank[j];
 }
 
-// Min-heap sift of `x` from the root over h[0..n); h[n] holds the sentinel,
-// so the right-child probe needs no bounds test (hole-based).
+// Min-heap sift of `x` from the root over h[0..n), four children per node
+// (4i+1 .. 4i+4: half the levels of a binary heap, the siblings on one or two
+// cache lines). h[n .. n+2] hold the sentinel, so the child probes need no
+// bounds test (hole-based). The job heaps' keys are static and strictly
+// ordered while they are in the heap, so the pop sequence is that of any
+// valid heap (the reference's binary container/heap included).
 inline void job_heap_down(kbg::JobKey* h, int n, kbg::JobKey x) {
   int i = 0;
   for (;;) {
-    int j = 2 * i + 1;
-    if (j >= n) break;
-    j += h[j + 1] < h[j] ? 1 : 0;
-    if (!(h[j] < x)) break;
-    h[i] = h[j];
-    i = j;
+    const int c = 4 * i + 1;
+    if (c >= n) break;
+    // a tournament of index selects (no data-dependent branches)
+    const int a = c + (h[c + 1] < h[c] ? 1 : 0), b = c + 2 + (h[c + 3] < h[c + 2] ? 1 : 0);
+    const int m = h[b] < h[a] ? b : a;
+    const kbg::JobKey mk = h[m];
+    if (!(mk < x)) break;
+    h[i] = mk;
+    i = m;
   }
   h[i] = x;
 }
+constexpr int32_t kJobHeapPad = 3;  // sentinel slots past a job heap's capacity
 
 // container/heap on queue ids compared through a rank table (rk[q] = position
 // of q in QueueOrderFn order). Hole-based sifting is the same algorithm as
@@ -430,7 +438,7 @@ struct Ops {
 // allocate.go:45-59: one queue entry per job (queue heap) and every job in
 // its queue's job heap, keyed from E's plugin state.
 void build_heaps(const Session& S, Engine& E) {
-  E.jheap.assign((size_t)S.n_jobs + S.n_queues, kbg::kJobKeySentinel);
+  E.jheap.assign((size_t)S.n_jobs + (size_t)S.n_queues * kJobHeapPad, kbg::kJobKeySentinel);
   E.jlen.assign(S.n_queues, 0);
   E.qheap.assign((size_t)S.n_jobs + 1, S.n_queues);
   E.qlen = 0;
@@ -2428,7 +2436,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   S.joff.assign(S.n_queues, 0);
   S.jcap.assign(S.n_queues, 0);
   for (int32_t j = 0; j < S.n_jobs; ++j) S.jcap[S.job_queue[j]]++;
-  for (int32_t q = 1; q < S.n_queues; ++q) S.joff[q] = S.joff[q - 1] + S.jcap[q - 1] + 1;
+  for (int32_t q = 1; q < S.n_queues; ++q) S.joff[q] = S.joff[q - 1] + S.jcap[q - 1] + kJobHeapPad;
   S.pend_all = S.pend;
   S.pend_off_all = S.pend_off;
   S.pend_len_all = S.pend_len;

@@ -157,7 +157,7 @@ inline uint32_t job_key_frank(JobKey k) { return (uint32_t)(uint64_t)k; }
 struct Engine {
   std::vector<int32_t> qheap;   // queue heap items (queue index), util.PriorityQueue; qheap[qlen] = sentinel
   int32_t qlen = 0;
-  std::vector<JobKey> jheap;    // per-queue job heaps (binary, inline keys), flat at joff[q]; [jlen] = sentinel
+  std::vector<JobKey> jheap;    // per-queue job heaps (4-ary, inline keys), flat at joff[q]; [jlen ..] = sentinels
   std::vector<int32_t> jlen;    // live length of each per-queue heap
   std::vector<int32_t> cursor;  // per job: next position in its sorted pending list
   int32_t cur_q = -1, cur_j = -1;
@@ -311,7 +311,7 @@ struct Session {
   std::vector<uint32_t> job_prank;                       // dense rank of -Priority
   std::vector<int32_t> job_queue;                        // job -> queue index
   std::vector<int32_t> task_job;                         // task -> job index
-  std::vector<int32_t> joff, jcap;                       // per-queue job-heap segment (jcap + 1 slots)
+  std::vector<int32_t> joff, jcap;                       // per-queue job-heap segment (jcap + 3 slots)
   std::vector<int32_t> pend, pend_off, pend_len;         // per-job pending tasks in TaskOrderFn order (this cycle)
   std::vector<int32_t> pend_all, pend_off_all, pend_len_all;  // the same at open
   std::vector<int32_t> job_min;  // jobs_in[j].min_available, packed for the engine
