@@ -499,7 +499,8 @@ def main():
                "traffic": None, "kernel": "kbg_firstfit_kernel (full-scan mode)", "avg_launch_us": avg_s * 1e6,
                "rows_per_launch": rows, "algo_bytes_per_launch": per_launch,
                "definition": "SURVEY 8(d) bytes per task evaluation x rows per launch / average launch time "
-                             "(HIP events on the library stream over the timed steps)"}
+                             "(HIP events on the library stream over the timed steps, on one fused launch in "
+                             "four: kbg_stats.scan_kernel_ms)"}
         pmc = load_pmc(agg["n_nodes"], mode) if comm is None else None
         if pmc:
             if pmc.get("hbm_bytes_per_launch") is not None:
