@@ -14,7 +14,7 @@ for cfg in 4 5; do
   timeout -k 10 600 python bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline > $O/bench_c$cfg.json 2> $O/bench_c$cfg.err || { tail -30 $O/bench_c$cfg.err; exit 1; }
 done
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-resident > $O/kt_bench.json 2> $O/kt.err || { tail -20 $O/kt.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-resident > $O/kt_bench.json 2> $O/kt.err || { tail -20 $O/kt.err; exit 1; }
 cd $R
 timeout -k 10 300 python kube-arbitrator_amd/tools/trace_cycle.py 4 0 > $O/c4_trace.txt 2> $O/c4_trace.log || { tail -20 $O/c4_trace.log; exit 1; }
 cat $O/c4_trace.txt
