@@ -3614,6 +3614,23 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   // b+1's resolve re-checks every node b touched (mark > that scan's base).
   int64_t cur_epoch = 0;
   int32_t pushed = S.res_stamp;  // newest resolution whose node deltas are enqueued
+  int32_t rstamp = S.res_stamp;  // the stamp of the commits being made (mark[] of their nodes)
+  // The rows the commits since the last write-back touched reach HBM right
+  // before a scan is launched (or the cycle ends), not after every batch: a
+  // batch resolved against earlier lists (contended cycles) needs no
+  // write-back, and a scan launched mid-batch sees the batch's commits so
+  // far. Commits after the write-back take a new stamp, above the scan's base.
+  auto flush = [&]() -> kbg_status {
+    if (touched.empty() && S.mask_dirty.empty()) return KBG_OK;
+    const auto t0 = clk::now();
+    const kbg_status st = push_deltas(S, touched);
+    touched.clear();
+    pushed = rstamp;
+    rstamp = ++S.res_stamp;
+    S.mstamp = rstamp;
+    S.stats.delta_ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    return st;
+  };
   bool pred_failed = false;
   // the next batch of the current epoch (stale ones are recycled); nullptr:
   // none ready (non-blocking) or the predictor failed (pred_failed)
@@ -3634,6 +3651,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     }
   };
   auto launch = [&](kbg::Stage& sg, Batch* b) -> kbg_status {
+    if (kbg_status fs = flush(); fs != KBG_OK) return fs;
     int32_t G;
     if (b->G >= 0) {  // built by the builder thread: take its row buffer and row maps
       std::swap(sg.h_up, b->st.h_up);
@@ -3769,15 +3787,13 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     // commit in order
     tp = clk::now();
     if (!reuse) rs.reset(*sg);  // reuse: the stage's cursors carry on
-    const int32_t stamp = ++S.res_stamp;  // this resolution's commits
-    S.mstamp = stamp;
-    touched.clear();
+    rstamp = ++S.res_stamp;  // this resolution's commits (touched keeps the rows not yet written back)
+    S.mstamp = rstamp;
     bactual.assign(bt.size(), 0);
     int32_t cut = -1;
     bool aff_cut = false;  // a pod-affinity gain: the lists miss the gained nodes
     int32_t seg = 0;  // first batch entry covered by the current scan of this stage
     bool panic = false;
-    int32_t rstamp = stamp;
     const uint64_t cl0 = rprof ? cycles() : 0;
     const int32_t nb = (int32_t)bt.size();
     ctr.add("resolve", nb);
@@ -3820,8 +3836,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         S.stats.resolve_ms += ms_since(tp);
         tp = clk::now();
         S.stats.truncations++;
-        st = push_deltas(S, touched);
-        pushed = rstamp;
+        st = flush();
         if (st == KBG_OK) {
           const int32_t* list = bt.data() + i;
           int32_t len = nb - i;
@@ -3855,10 +3870,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         S.stats.device_ms += ms_since(tp);
         tp = clk::now();
         seg = i;
-        rs.reset(*sg);
-        rstamp = ++S.res_stamp;  // commits after the rescan
-        S.mstamp = rstamp;
-        touched.clear();
+        rs.reset(*sg);  // (flush gave the commits after the rescan a new stamp)
         if (keep_reuse) {
           map_shapes(*sg, scan_list, 0);
           reuse = true;
@@ -3935,9 +3947,6 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     if (pred_failed) return abort(fail(KBG_E_INVALID, pr.error));  // seen by the look-ahead above
     S.stats.resolve_ms += ms_since(tp);
     tp = clk::now();
-    if ((st = push_deltas(S, touched)) != KBG_OK) return abort(st);
-    pushed = rstamp;
-    S.stats.delta_ms += ms_since(tp);
     if (panic) {
       recycle(cur);
       recycle(nxt);
@@ -4017,7 +4026,8 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   if (!truth.error.empty()) return fail(KBG_E_INVALID, truth.error);
   if (lg) lg->join();  // the decision log and FitError records are complete
   ctr.add("logged");
-  HIP_TRY(hipStreamSynchronize(S.stream));  // last delta write-back
+  if (kbg_status st = flush(); st != KBG_OK) return st;  // the cycle's last write-back
+  HIP_TRY(hipStreamSynchronize(S.stream));
   if (kbg_status st = compute_fit_deltas(S, dec, dec_old, dec_oldp, last); st != KBG_OK) return st;
   ctr.add("fit");
   if (S.has_aff && getenv("KBG_PROFILE_AFF"))
