@@ -670,7 +670,10 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
     const int32_t tw = a.w_hi - a.w_lo;
     a.complete = tw <= kbg::kFfRoundWords ? 1 : 0;
     a.splits = 1;
-    if (a.complete && !S.comm) {
+    // Production walks of larger tables (C4's 313 words) split too: each part
+    // stops at the row's `want` within its own words, and the parts' lists
+    // join in node order up to the first one that stopped early (device_wait)
+    if ((a.complete || a.early_exit) && !S.comm) {
       const int32_t blocks = (G + kbg::firstfit_rows(G) - 1) / kbg::firstfit_rows(G);
       a.splits = std::max(1, std::min({kbg::kFfMaxSplits, 256 / std::max(1, blocks), tw / 8}));
     }
@@ -759,13 +762,24 @@ kbg_status device_wait(Session& S, kbg::Stage& sg) {
   const int32_t G = sg.G;
   if (sg.fused) {
     sg.h_info = sg.h_down;
-    if (sg.splits > 1) {  // parts of a complete walk: the slot's list covers every word, fits if any part did
-      const int32_t P = sg.splits, tw = S.owner ? std::min(S.W, (S.shard + 1) * S.Wl) - S.shard * S.Wl : S.W;
+    if (sg.splits > 1) {
+      // the parts' lists in node order: the slot's list covers the words of
+      // every part up to and including the first that stopped at the row's
+      // want before its last word (a complete walk: every word); it fits
+      // somewhere if any part found a node
+      const int32_t P = sg.splits;
       sg.info_comb.resize(sg.n_slots);
       for (int32_t sl = 0; sl < sg.n_slots; ++sl) {
-        uint32_t any = 0;
-        for (int32_t p = 0; p < P; ++p) any |= sg.h_down[(size_t)sl * P + p] & kbg::kInfoAnyBit;
-        sg.info_comb[sl] = (uint32_t)tw | any;
+        uint32_t any = 0, covered = 0;
+        bool cut = false;
+        for (int32_t p = 0; p < P; ++p) {
+          const uint32_t v = sg.h_down[(size_t)sl * P + p];
+          any |= v & kbg::kInfoAnyBit;
+          if (cut) continue;
+          covered += v & kbg::kInfoWordsMask;
+          cut = (v & kbg::kCountIncompleteBit) != 0;
+        }
+        sg.info_comb[sl] = covered | (cut ? kbg::kCountIncompleteBit : 0u) | any;
       }
       sg.h_info = sg.info_comb.data();
     }

@@ -1,6 +1,7 @@
 """Developer tool: A/B of library builds on the C3 bench (production and full-scan
 p50), alternating in one GPU session: python kube-arbitrator_amd/tools/ab_bench.py lib1.so lib2.so
-(CONFIG=4: another BASELINE config; REPS: rounds; lib.so@KEY=VAL sets a variant's environment)"""
+(CONFIG=4: another BASELINE config; REPS: rounds; lib.so@KEY=VAL sets a variant's environment).
+Per run: p50 cycle ms (production, full-scan), production scan launch us, production device round trip ms"""
 import json, os, subprocess, sys
 res = {}
 cfg = os.environ.get("CONFIG", "3")
@@ -16,6 +17,9 @@ for rep in range(int(os.environ.get("REPS", "3"))):
         out = subprocess.run([sys.executable, "-c", code.replace(v, v.split("@")[0])], capture_output=True, text=True,
                              timeout=300, env=env)
         d = json.loads(out.stdout.strip().splitlines()[-1])
-        res.setdefault(v, []).append((round(d["p50_cycle_ms"], 2), round(d["full_scan_mode"]["p50_cycle_ms"], 2)))
+        pm = d.get("production_mode", {})
+        res.setdefault(v, []).append((round(d["p50_cycle_ms"], 2), round(d["full_scan_mode"]["p50_cycle_ms"], 2),
+                                      round(pm.get("scan_kernel", {}).get("avg_launch_us") or 0, 1),
+                                      round(pm.get("breakdown", {}).get("device_roundtrip_ms") or 0, 2)))
         print(v, res[v][-1], flush=True)
 print(json.dumps(res))
