@@ -1676,6 +1676,13 @@ int32_t intern(Session& S, const char* v) {
   return id;
 }
 
+// The canonical id of "" (an event's NodeName of a pod on no node).
+int32_t empty_str(Session& S) {
+  if (S.str_empty < 0 || S.str_empty >= (int32_t)S.strs.size() || !S.strs[S.str_empty].empty())
+    S.str_empty = intern(S, "");
+  return S.str_empty;
+}
+
 // A string only ever read as text (a task UID: TaskOrderFn's fallback compares
 // UIDs as strings, nothing looks it up by content): appended without the
 // content map, as its own canonical id.
@@ -1869,15 +1876,16 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   return KBG_OK;
 }
 
-// S.task_uid_key[from, n_tasks): each UID's first 8 bytes, big-endian and
+// S.task_uid_key[from, n_tasks): each UID's first 16 bytes, big-endian and
 // zero-padded, so unequal keys order the UIDs as their bytes do
 void fill_uid_keys(Session& S, int32_t from) {
   S.task_uid_key.resize(S.n_tasks);
   for (int32_t t = from; t < S.n_tasks; ++t) {
     const std::string& u = S.strs[S.tasks_in[t].uid];
-    uint64_t k = 0;
-    for (size_t i = 0; i < 8; ++i) k = k << 8 | (i < u.size() ? (uint8_t)u[i] : 0);
-    S.task_uid_key[t] = k;
+    uint64_t a = 0, b = 0;
+    for (size_t i = 0; i < 8; ++i) a = a << 8 | (i < u.size() ? (uint8_t)u[i] : 0);
+    for (size_t i = 8; i < 16; ++i) b = b << 8 | (i < u.size() ? (uint8_t)u[i] : 0);
+    S.task_uid_key[t] = Session::UidKey{a, b};
   }
 }
 
@@ -1887,6 +1895,8 @@ enum { DERIVE_OK = 0, DERIVE_REBUILD = 1 };  // REBUILD: the static classes / ma
 // the static predicate classes (build); null: keep the session's classes and
 // map each candidate task to its spec's class (update), or ask for a rebuild
 // when a candidate needs a class the session does not have.
+void pin_near(int cpu, int nth);
+
 kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   *outcome = DERIVE_OK;
   S.job_chain_pgd = S.job_chain == std::vector<int32_t>{kbg::JO_PRIORITY, kbg::JO_GANG, kbg::JO_DRF};
@@ -1912,10 +1922,14 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     for (int32_t t = 0; t < T; ++t) S.task_rank[t] = (int64_t)dense[t] * kRankGap;
     fill_uid_keys(S, 0);
     S.job_rank_order.assign(S.n_jobs, {});
+    S.job_rank_key.assign(S.n_jobs, {});
     for (int32_t j = 0; j < S.n_jobs; ++j) {
       std::vector<int32_t>& ro = S.job_rank_order[j];
       ro = S.job_task_order[j];
       std::stable_sort(ro.begin(), ro.end(), [&](int32_t a, int32_t b) { return S.task_rank[a] < S.task_rank[b]; });
+      std::vector<Session::UidKey>& rk = S.job_rank_key[j];
+      rk.resize(ro.size());
+      for (size_t i = 0; i < ro.size(); ++i) rk[i] = S.task_uid_key[ro[i]];
     }
   } else if (S.task_ranks_stale) {
     // a job that gained tasks: each new UID takes a rank between the ranked
@@ -1930,40 +1944,54 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     std::sort(S.rank_dirty_jobs.begin(), S.rank_dirty_jobs.end());
     S.rank_dirty_jobs.erase(std::unique(S.rank_dirty_jobs.begin(), S.rank_dirty_jobs.end()), S.rank_dirty_jobs.end());
     const auto uid = [&](int32_t t) -> const std::string& { return S.strs[S.tasks_in[t].uid]; };
-    // bytewise UID order: the 8-byte keys decide unless they tie
-    const uint64_t* key = S.task_uid_key.data();
-    const auto uid_less = [&](int32_t a, int32_t b) { return key[a] != key[b] ? key[a] < key[b] : uid(a) < uid(b); };
+    // bytewise UID order: the 16-byte keys decide unless they tie
+    const Session::UidKey* key = S.task_uid_key.data();
+    const auto uid_less = [&](int32_t a, int32_t b) { return !(key[a] == key[b]) ? key[a] < key[b] : uid(a) < uid(b); };
     std::vector<int32_t> news;
-    // the jobs' lists and the first levels of their binary searches are
-    // requested a few jobs ahead (scattered rows: latency, not work)
+    // a job's ranked tasks and their keys sit in two contiguous arrays; the
+    // next jobs' arrays are requested a few jobs ahead (scattered rows:
+    // latency, not work)
     const std::vector<int32_t>& dj = S.rank_dirty_jobs;
+    auto ahead = [&](const void* p, size_t bytes) {
+      const char* c = static_cast<const char*>(p);
+      for (size_t o = 0; o < std::min<size_t>(bytes, 1024); o += 64) __builtin_prefetch(c + o);
+    };
     for (size_t k = 0; k < dj.size(); ++k) {
       const int32_t j = dj[k];
       if (k + 4 < dj.size()) {
         __builtin_prefetch(&S.job_task_order[dj[k + 4]]);
         __builtin_prefetch(&S.job_rank_order[dj[k + 4]]);
+        __builtin_prefetch(&S.job_rank_key[dj[k + 4]]);
       }
       if (k + 2 < dj.size()) {
-        const std::vector<int32_t>& r2 = S.job_rank_order[dj[k + 2]];
-        __builtin_prefetch(S.job_task_order[dj[k + 2]].data());
-        if (!r2.empty()) {
-          const size_t h = r2.size() / 2;
-          __builtin_prefetch(&key[r2[h]]);
-          __builtin_prefetch(&key[r2[h / 2]]);
-          __builtin_prefetch(&key[r2[h + (r2.size() - h) / 2]]);
-        } else {
-          __builtin_prefetch(r2.data());
-        }
+        const std::vector<int32_t>& t2 = S.job_task_order[dj[k + 2]];
+        const std::vector<Session::UidKey>& k2 = S.job_rank_key[dj[k + 2]];
+        ahead(t2.data(), t2.size() * 4);
+        ahead(k2.data(), k2.size() * sizeof(Session::UidKey));
+        ahead(S.job_rank_order[dj[k + 2]].data(), S.job_rank_order[dj[k + 2]].size() * 4);
       }
       news.clear();
       for (int32_t t : S.job_task_order[j])
         if (t >= T_old) news.push_back(t);
       if (news.size() > 1) std::stable_sort(news.begin(), news.end(), uid_less);
       std::vector<int32_t>& ro = S.job_rank_order[j];
+      std::vector<Session::UidKey>& rk = S.job_rank_key[j];
+      if (rk.size() != ro.size()) {  // (never expected: kept beside ro)
+        rk.resize(ro.size());
+        for (size_t i = 0; i < ro.size(); ++i) rk[i] = key[ro[i]];
+      }
       for (int32_t nt : news) {
-        const auto it = std::upper_bound(ro.begin(), ro.end(), nt, uid_less);
-        size_t pos = it - ro.begin();
-        if (pos > 0 && key[ro[pos - 1]] == key[nt] && uid(ro[pos - 1]) == uid(nt)) {
+        // upper_bound by (key, then UID string) over the contiguous keys
+        const Session::UidKey kn = key[nt];
+        size_t lo_i = 0, hi_i = ro.size();
+        while (lo_i < hi_i) {
+          const size_t mid = (lo_i + hi_i) / 2;
+          const bool before = !(kn == rk[mid]) ? kn < rk[mid] : uid(nt) < uid(ro[mid]);
+          if (before) hi_i = mid;
+          else lo_i = mid + 1;
+        }
+        const size_t pos = lo_i;
+        if (pos > 0 && rk[pos - 1] == kn && uid(ro[pos - 1]) == uid(nt)) {
           S.task_rank[nt] = S.task_rank[ro[pos - 1]];
         } else {
           auto bounds = [&](int64_t* lo, int64_t* hi) {
@@ -1974,17 +2002,18 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
           bounds(&lo, &hi);
           if (hi - lo < 2) {  // no rank left between the neighbours: renumber the job (equal ranks stay equal)
             int64_t r = 0, prev = 0;
-            for (size_t k = 0; k < ro.size(); ++k) {
-              const int64_t old = S.task_rank[ro[k]];
-              if (k > 0 && old != prev) ++r;
+            for (size_t k2 = 0; k2 < ro.size(); ++k2) {
+              const int64_t old = S.task_rank[ro[k2]];
+              if (k2 > 0 && old != prev) ++r;
               prev = old;
-              S.task_rank[ro[k]] = r * kRankGap;
+              S.task_rank[ro[k2]] = r * kRankGap;
             }
             bounds(&lo, &hi);
           }
           S.task_rank[nt] = lo + (hi - lo) / 2;
         }
         ro.insert(ro.begin() + pos, nt);
+        rk.insert(rk.begin() + pos, kn);
       }
     }
   }
@@ -2073,6 +2102,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   S.idle0 = S.idle;
   S.rel0 = S.rel;
   S.ntasks0 = S.ntasks;
+  phase("nodes");
   // victim candidates (preempt/reclaim): session tasks Running on each node,
   // in NodeInfo.Tasks order; a task's node by NodeName (ssn.NodeIndex)
   if (full || (int32_t)S.task_node.size() != T) {  // an update's events keep task_node current (apply_event)
@@ -2098,37 +2128,53 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
       if (S.task_node[t] >= 0 && S.task_node[t] < N) vdirty[S.task_node[t]] = 1;
     vt.reserve(S.nt_task.size() + S.upd_tasks.size());
   }
-  off.assign(N + 1, 0);
-  vt.clear();
-  S.max_candidates = 0;
-  for (int32_t n = 0; n < N; ++n) {
-    if (vincr && !vdirty[n]) {
-      vt.insert(vt.end(), S.nt_task.begin() + S.nt_off[n], S.nt_task.begin() + S.nt_off[n + 1]);
-    } else {
-      for (int32_t t : S.node_task_order[n])
-        if (S.tstat_in[t] == KBG_RUNNING) vt.push_back(t);
-    }
-    off[n + 1] = (int32_t)vt.size();
-    S.max_candidates = std::max(S.max_candidates, off[n + 1] - off[n]);
-  }
-  if (vincr) {
-    S.nt_off.swap(S.nt_off_buf);
-    S.nt_task.swap(S.nt_task_buf);
-  }
   S.upd_nodes_valid = false;
-  // KBG_CHECK_DERIVE=1 (tests): an update's incremental results against the
-  // full recomputation, bit for bit
+  // The lists are built on a thread of their own while the phases below run
+  // (none of them reads the lists or writes what the lists are built from:
+  // node_task_order, tstat_in, task_node); joined before derive_host returns.
   const bool check = !full && getenv("KBG_CHECK_DERIVE") != nullptr;
-  if (check) {
-    std::vector<int32_t> o2(N + 1, 0), t2;
+  bool vbad = false;
+  const int vcpu = sched_getcpu();
+  auto victims = [&S, &off, &vt, &vbad, N, vincr, check, vcpu, vdirty = std::move(vdirty)] {
+    pin_near(vcpu, 1);  // beside this thread, on its last-level cache (the lists are warm there)
+    off.assign(N + 1, 0);
+    vt.clear();
+    int32_t mc = 0;
     for (int32_t n = 0; n < N; ++n) {
-      for (int32_t t : S.node_task_order[n])
-        if (S.tstat_in[t] == KBG_RUNNING) t2.push_back(t);
-      o2[n + 1] = (int32_t)t2.size();
+      if (vincr && !vdirty[n]) {
+        vt.insert(vt.end(), S.nt_task.begin() + S.nt_off[n], S.nt_task.begin() + S.nt_off[n + 1]);
+      } else {
+        for (int32_t t : S.node_task_order[n])
+          if (S.tstat_in[t] == KBG_RUNNING) vt.push_back(t);
+      }
+      off[n + 1] = (int32_t)vt.size();
+      mc = std::max(mc, off[n + 1] - off[n]);
     }
-    if (o2 != S.nt_off || t2 != S.nt_task) return fail(KBG_E_INVALID, "internal: incremental victim lists differ");
-  }
-  phase("nodes+victims");
+    S.max_candidates = mc;
+    if (vincr) {
+      S.nt_off.swap(S.nt_off_buf);
+      S.nt_task.swap(S.nt_task_buf);
+    }
+    // KBG_CHECK_DERIVE=1 (tests): an update's incremental results against the
+    // full recomputation, bit for bit
+    if (check) {
+      std::vector<int32_t> o2(N + 1, 0), t2;
+      for (int32_t n = 0; n < N; ++n) {
+        for (int32_t t : S.node_task_order[n])
+          if (S.tstat_in[t] == KBG_RUNNING) t2.push_back(t);
+        o2[n + 1] = (int32_t)t2.size();
+      }
+      vbad = o2 != S.nt_off || t2 != S.nt_task;
+    }
+  };
+  struct Joiner {
+    std::thread th;
+    ~Joiner() {
+      if (th.joinable()) th.join();
+    }
+  } vjoin;
+  vjoin.th = std::thread(std::move(victims));
+  phase("victims");
   setup_pod_keys(S, incr, &S.upd_tasks, &was);
 
   phase("pod keys");
@@ -2583,6 +2629,9 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   }
   S.upd_tasks.clear();
   phase("shapes");
+  vjoin.th.join();
+  phase("victims join");
+  if (vbad) return fail(KBG_E_INVALID, "internal: incremental victim lists differ");
   return KBG_OK;
 }
 
@@ -5790,11 +5839,11 @@ int in_node_remove(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
 int in_delete_task(Session& S, UpdateCtx& U, int32_t t) {
   std::vector<int32_t>& jl = S.job_task_order[S.tasks_in[t].job];
   jl.erase(std::find(jl.begin(), jl.end(), t));  // JobInfo.DeleteTaskInfo
-  const std::string& nn = S.strs[S.tasks_in[t].node_name];
-  if (nn.empty()) return 0;
-  auto it = S.node_of.find(S.canon[S.tasks_in[t].node_name]);
-  if (it == S.node_of.end()) return 0;  // sc.Nodes[...] == nil
-  return in_node_remove(S, U, it->second, t);
+  // the node its NodeName names (task_node: derive_host's lookup, kept
+  // current by the events); -1: no NodeName, or sc.Nodes[...] == nil
+  const int32_t n = S.task_node[t];
+  if (n < 0) return 0;
+  return in_node_remove(S, U, n, t);
 }
 
 kbg_status in_add_task(Session& S, UpdateCtx& U, int32_t t) {  // event_handlers.go addTask
@@ -5826,12 +5875,16 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
         if ((size_t)j < S.job_rank_order.size()) {
           std::vector<int32_t>& ro = S.job_rank_order[j];
           auto it = std::find(ro.begin(), ro.end(), t);
-          if (it != ro.end()) ro.erase(it);
+          if (it != ro.end()) {
+            if ((size_t)j < S.job_rank_key.size() && S.job_rank_key[j].size() == ro.size())
+              S.job_rank_key[j].erase(S.job_rank_key[j].begin() + (it - ro.begin()));
+            ro.erase(it);
+          }
         }
         return KBG_OK;
       }
       S.tasks_in[t].status = e.status;
-      S.tasks_in[t].node_name = e.node >= 0 ? S.nodes_in[e.node].name : intern(S, "");
+      S.tasks_in[t].node_name = e.node >= 0 ? S.nodes_in[e.node].name : empty_str(S);
       S.task_node[t] = e.node;
       if (e.status == KBG_PENDING) S.pend_new.push_back(t);
       return in_add_task(S, U, t);
@@ -5847,7 +5900,7 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
       k.priority = e.priority;
       k.resreq = e.resource;
       k.spec = e.spec;
-      k.node_name = e.node >= 0 ? S.nodes_in[e.node].name : intern(S, "");
+      k.node_name = e.node >= 0 ? S.nodes_in[e.node].name : empty_str(S);
       k.pod_key = intern(S, e.pod_key);
       const int32_t t = S.n_tasks++;
       S.tasks_in.push_back(k);
@@ -6007,51 +6060,71 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
   uint64_t kc[5] = {0, 0, 0, 0, 0}, kn[5] = {0, 0, 0, 0, 0};
   // An event touches a handful of rows of task-, node- and job-indexed state
   // spread over the whole session (cache misses, not work): the rows of the
-  // events ahead are requested before they are applied, in two hops (the
-  // task's row, then what it names). Prefetches only; the order of application
-  // is unchanged.
-  constexpr int32_t kAhead = 16;
+  // events ahead are requested before they are applied, in three hops (the
+  // task's row; what it names — its job's and nodes' list headers, its key;
+  // then the lists themselves and the key's count), each hop's addresses
+  // read from rows the hop before requested. Prefetches only; the order of
+  // application is unchanged.
+  constexpr int32_t kFar = 24, kMid = 12, kNear = 4;
   auto task_of = [&](const kbg_event& e) -> int32_t {
     const bool pod = e.kind == KBG_EV_POD_UPDATE || e.kind == KBG_EV_POD_DELETE;
     return pod && e.task >= 0 && e.task < S.n_tasks ? e.task : -1;
   };
+  auto job_of_add = [&](const kbg_event& e) -> int32_t {
+    return e.kind == KBG_EV_POD_ADD && e.job >= 0 && e.job < S.n_jobs ? e.job : -1;
+  };
+  auto node_ok = [&](int32_t nd) { return nd >= 0 && nd < S.n_nodes; };
   auto ahead_far = [&](const kbg_event& e) {
     if (const int32_t t = task_of(e); t >= 0) {
       __builtin_prefetch(&S.tasks_in[t]);
       __builtin_prefetch(&S.task_node[t]);
       __builtin_prefetch(&S.task_live[t]);
-    } else if (e.kind == KBG_EV_POD_ADD && e.job >= 0 && e.job < S.n_jobs) {
-      __builtin_prefetch(&S.job_task_order[e.job]);
+      __builtin_prefetch(&S.treq[t]);
+    } else if (const int32_t j = job_of_add(e); j >= 0) {
+      __builtin_prefetch(&S.job_task_order[j]);
     }
-    if (e.node >= 0 && e.node < S.n_nodes) {
+    if (node_ok(e.node)) {
       __builtin_prefetch(&S.nodes_in[e.node]);
       __builtin_prefetch(&S.node_key_order[e.node]);
       __builtin_prefetch(&S.node_task_order[e.node]);
     }
   };
-  auto ahead_near = [&](const kbg_event& e) {
+  auto ahead_mid = [&](const kbg_event& e) {
     if (const int32_t t = task_of(e); t >= 0) {
       const kbg_task& k = S.tasks_in[t];
       __builtin_prefetch(&S.job_task_order[k.job]);
       __builtin_prefetch(&S.canon[k.pod_key]);
-      __builtin_prefetch(&S.strs[k.node_name]);
       const int32_t on = S.task_node[t];  // the node the task leaves
-      if (on >= 0 && on < S.n_nodes) {
+      if (node_ok(on)) {
         __builtin_prefetch(&S.nodes_in[on]);
-        __builtin_prefetch(S.node_key_order[on].data());
-        __builtin_prefetch(S.node_task_order[on].data());
+        __builtin_prefetch(&S.node_key_order[on]);
+        __builtin_prefetch(&S.node_task_order[on]);
       }
-    } else if (e.kind == KBG_EV_POD_ADD && e.job >= 0 && e.job < S.n_jobs) {
-      __builtin_prefetch(S.job_task_order[e.job].data() + S.job_task_order[e.job].size());
+    } else if (const int32_t j = job_of_add(e); j >= 0) {
+      __builtin_prefetch(S.job_task_order[j].data() + S.job_task_order[j].size());
     }
-    if (e.node >= 0 && e.node < S.n_nodes) {
+    if (node_ok(e.node)) {
       __builtin_prefetch(S.node_key_order[e.node].data());
       __builtin_prefetch(S.node_task_order[e.node].data() + S.node_task_order[e.node].size());
     }
   };
+  auto ahead_near = [&](const kbg_event& e) {
+    if (const int32_t t = task_of(e); t >= 0) {
+      const kbg_task& k = S.tasks_in[t];
+      __builtin_prefetch(S.job_task_order[k.job].data());
+      const int32_t key = S.canon[k.pod_key];
+      if ((size_t)key < S.kc_node.size()) __builtin_prefetch(&S.kc_node[key]);
+      const int32_t on = S.task_node[t];
+      if (node_ok(on)) {
+        __builtin_prefetch(S.node_key_order[on].data());
+        __builtin_prefetch(S.node_task_order[on].data());
+      }
+    }
+  };
   for (int32_t i = 0; i < n; ++i) {
-    if (i + kAhead < n) ahead_far(ev[i + kAhead]);
-    if (i + kAhead / 2 < n) ahead_near(ev[i + kAhead / 2]);
+    if (i + kFar < n) ahead_far(ev[i + kFar]);
+    if (i + kMid < n) ahead_mid(ev[i + kMid]);
+    if (i + kNear < n) ahead_near(ev[i + kNear]);
     const uint64_t c0 = prof ? __builtin_readcyclecounter() : 0;
     kbg_status st = apply_event(S, U, ev[i]);
     if (st != KBG_OK) return st;

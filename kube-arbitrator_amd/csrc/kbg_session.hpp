@@ -275,6 +275,7 @@ struct Session {
   // ---- copied snapshot
   std::vector<std::string> strs;
   std::vector<int32_t> canon;  // string id -> canonical id of its content
+  int32_t str_empty = -1;      // the canonical id of "" once an event needed it (empty_str)
   int32_t n_nodes = 0, n_jobs = 0, n_queues = 0, n_tasks = 0;
   std::vector<kbg_node> nodes_in;
   std::vector<kbg_job> jobs_in;
@@ -305,7 +306,14 @@ struct Session {
   // so a task added by an update takes a rank between its neighbours' without
   // re-ranking its job; equal UIDs share a rank. Only compared within a job.
   std::vector<int64_t> task_rank;
-  std::vector<uint64_t> task_uid_key;  // first 8 UID bytes, big-endian, zero-padded: a prefix of the byte order
+  // first 16 UID bytes, big-endian, zero-padded: unequal keys order the UIDs
+  // as their bytes do (equal keys: the strings decide)
+  struct UidKey {
+    uint64_t a = 0, b = 0;
+    bool operator<(const UidKey& o) const { return a != o.a ? a < o.a : b < o.b; }
+    bool operator==(const UidKey& o) const { return a == o.a && b == o.b; }
+  };
+  std::vector<UidKey> task_uid_key;
   std::vector<int32_t> job_frank;                       // (CreationTimestamp, UID) order
   std::vector<int32_t> job_by_frank;                     // inverse of job_frank
   std::vector<uint32_t> job_prank;                       // dense rank of -Priority
@@ -472,6 +480,8 @@ struct Session {
   std::vector<uint8_t> task_live;                     // 0: the pod was deleted (event_handlers.go deletePod)
   std::vector<std::vector<int32_t>> job_task_order;   // per job: its tasks in JobInfo.Tasks insertion order
   std::vector<std::vector<int32_t>> job_rank_order;   // per job: its ranked tasks in task_rank order
+  std::vector<std::vector<UidKey>> job_rank_key;      // per job: their UID keys, in the same order (a
+                                                      // new task's place is searched in contiguous keys)
   std::vector<std::vector<int32_t>> node_task_order;  // per node: the session tasks in NodeInfo.Tasks order
   std::vector<std::vector<int32_t>> node_key_order;   // per node: PodKey (canonical id) of every pod on it
   std::vector<kbg_resource> others_in;                // Session.Others resreq
