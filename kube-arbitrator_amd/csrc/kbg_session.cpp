@@ -1914,6 +1914,24 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   // a full derive (open, or a rebuild after an update) recomputes everything;
   // an update's derive keeps what its events cannot have changed
   const bool full = sh != nullptr;
+  // The ranks are computed on a worker of their own, beside this thread on
+  // its last-level cache, while the phases up to the pending lists run (none
+  // of them reads a rank or writes what the ranks are computed from: UIDs,
+  // job task lists); joined before the pending lists sort by rank. The
+  // victim lists below take a second worker.
+  struct Worker {
+    std::thread th;
+    bool nomem = false;
+    void join() {
+      if (th.joinable()) th.join();
+    }
+    ~Worker() { join(); }
+  };
+  const int hcpu = sched_getcpu();
+  Worker rwork;
+  rwork.th = std::thread([&S, T, hcpu, &rwork] {
+    pin_near(hcpu, 1);
+    try {
   if (S.task_rank.empty() && T > 0) {
     std::vector<int32_t> ids(T);
     for (int32_t t = 0; t < T; ++t) ids[t] = S.tasks_in[t].uid;
@@ -2019,7 +2037,10 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   }
   S.task_ranks_stale = false;
   S.rank_dirty_jobs.clear();
-  phase("ranks");
+    } catch (const std::bad_alloc&) {
+      rwork.nomem = true;
+    }
+  });
   // per-task vectors grow with every update's new pods: keep headroom so an
   // update does not reallocate (and copy) them
   auto headroom = [](auto& v, size_t n) {
@@ -2134,9 +2155,10 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   // node_task_order, tstat_in, task_node); joined before derive_host returns.
   const bool check = !full && getenv("KBG_CHECK_DERIVE") != nullptr;
   bool vbad = false;
-  const int vcpu = sched_getcpu();
-  auto victims = [&S, &off, &vt, &vbad, N, vincr, check, vcpu, vdirty = std::move(vdirty)] {
-    pin_near(vcpu, 1);  // beside this thread, on its last-level cache (the lists are warm there)
+  Worker vwork;
+  auto victims = [&S, &off, &vt, &vbad, &vwork, N, vincr, check, hcpu, vdirty = std::move(vdirty)] {
+    pin_near(hcpu, 2);  // beside this thread, on its last-level cache (the lists are warm there)
+    try {
     off.assign(N + 1, 0);
     vt.clear();
     int32_t mc = 0;
@@ -2166,14 +2188,11 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
       }
       vbad = o2 != S.nt_off || t2 != S.nt_task;
     }
-  };
-  struct Joiner {
-    std::thread th;
-    ~Joiner() {
-      if (th.joinable()) th.join();
+    } catch (const std::bad_alloc&) {
+      vwork.nomem = true;
     }
-  } vjoin;
-  vjoin.th = std::thread(std::move(victims));
+  };
+  vwork.th = std::thread(std::move(victims));
   phase("victims");
   setup_pod_keys(S, incr, &S.upd_tasks, &was);
 
@@ -2424,6 +2443,9 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   }
 
   phase("preconditions");
+  rwork.join();
+  phase("ranks join");
+  if (rwork.nomem) throw std::bad_alloc();
   // ---- pending task lists in TaskOrderFn order (session_plugins.go:266-276)
   // an update's derive copies the lists of the jobs no event touched
   const bool keep_lists = !full && (int32_t)S.pend_off_all.size() == S.n_jobs;
@@ -2629,8 +2651,9 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   }
   S.upd_tasks.clear();
   phase("shapes");
-  vjoin.th.join();
+  vwork.join();
   phase("victims join");
+  if (vwork.nomem) throw std::bad_alloc();
   if (vbad) return fail(KBG_E_INVALID, "internal: incremental victim lists differ");
   return KBG_OK;
 }
