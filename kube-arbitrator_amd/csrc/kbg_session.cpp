@@ -1694,8 +1694,17 @@ int32_t append_str(Session& S, const char* v) {
 }
 
 kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
+  static const bool prof = getenv("KBG_PROFILE_OPEN") != nullptr;
+  auto tl = std::chrono::steady_clock::now();
+  auto phase = [&](const char* name) {
+    if (!prof) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[kbg ingest] %-20s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(now - tl).count());
+    tl = now;
+  };
   kbg_status st = validate(snap);
   if (st != KBG_OK) return st;
+  phase("validate");
   if (o) S.opts = *o;
   S.heap_go111 = S.opts.heap_rule == 0;
   S.K = S.opts.batch_tasks > 0 ? S.opts.batch_tasks : (S.opts.full_scan ? kFullScanK : 8192);
@@ -1704,11 +1713,41 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   // full-scan: K rows x (M + rank) slots; grouped: sum over shapes of min(n_s + slack, 4096)
 
 
-  S.strs.assign(snap->strings, snap->strings + snap->n_strings);
+  // headroom for pods added by session updates (no reallocation per event batch)
+  const size_t more = (size_t)std::max(0, snap->n_tasks) / 4 + 1024;
+  // The strings are copied and hashed by a few workers (each its own range),
+  // then entered into the content index in id order (the first id of a
+  // content is its canonical id), each slot requested a few strings ahead.
+  const size_t NS = (size_t)std::max(0, snap->n_strings);
+  S.strs.clear();
+  S.strs.reserve(NS + 2 * more);
+  S.strs.resize(NS);
+  std::vector<uint64_t> sh(NS);
+  {
+    const size_t P = NS < 65536 ? 1 : std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency()));
+    auto copy_range = [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        S.strs[i].assign(snap->strings[i]);
+        sh[i] = kbg::StrIndex::hash(S.strs[i]);
+      }
+    };
+    std::vector<std::thread> th;
+    const size_t chunk = (NS + P - 1) / P;
+    for (size_t p = 1; p < P; ++p) th.emplace_back(copy_range, std::min(NS, p * chunk), std::min(NS, (p + 1) * chunk));
+    copy_range(0, std::min(NS, chunk));
+    for (std::thread& t : th) t.join();
+  }
+  phase("strings copy");
   S.canon_of.clear();
-  S.canon_of.reserve(S.strs.size());
-  S.canon.resize(S.strs.size());
-  for (size_t i = 0; i < S.strs.size(); ++i) S.canon[i] = S.canon_of.insert(S.strs, (int32_t)i);
+  S.canon_of.reserve(NS);
+  S.canon.reserve(NS + 2 * more);
+  S.canon.resize(NS);
+  constexpr size_t kStrAhead = 16;
+  for (size_t i = 0; i < NS; ++i) {
+    if (i + kStrAhead < NS) S.canon_of.prefetch(sh[i + kStrAhead]);
+    S.canon[i] = S.canon_of.insert_h(S.strs, (int32_t)i, sh[i]);
+  }
+  phase("strings");
   S.n_nodes = snap->n_nodes;
   S.n_jobs = snap->n_jobs;
   S.n_queues = snap->n_queues;
@@ -1716,7 +1755,9 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   S.nodes_in = copy_arr(snap->nodes, snap->n_nodes);
   S.jobs_in = copy_arr(snap->jobs, snap->n_jobs);
   S.queues_in = copy_arr(snap->queues, snap->n_queues);
-  S.tasks_in = copy_arr(snap->tasks, snap->n_tasks);
+  S.tasks_in.clear();
+  S.tasks_in.reserve((size_t)std::max(0, snap->n_tasks) + more);
+  if (snap->tasks && snap->n_tasks > 0) S.tasks_in.assign(snap->tasks, snap->tasks + snap->n_tasks);
   S.specs_in = copy_arr(snap->specs, snap->n_specs);
   S.terms_in = copy_arr(snap->terms, snap->n_terms);
   S.reqs_in = copy_arr(snap->reqs, snap->n_reqs);
@@ -1729,14 +1770,10 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   S.pod_terms_in = copy_arr(snap->pod_terms, snap->n_pod_terms);
   S.pod_labels_in = copy_arr(snap->pod_labels, 2 * snap->n_pod_labels);
   S.others_in = copy_arr(snap->others, snap->n_others);
+  S.task_live.clear();
+  S.task_live.reserve(S.n_tasks + more);
   S.task_live.assign(S.n_tasks, 1);
-  {  // headroom for pods added by session updates (no reallocation per event batch)
-    const size_t more = (size_t)S.n_tasks / 4 + 1024;
-    S.tasks_in.reserve(S.n_tasks + more);
-    S.task_live.reserve(S.n_tasks + more);
-    S.strs.reserve(S.strs.size() + 2 * more);
-    S.canon.reserve(S.strs.size() + 2 * more);
-  }
+  phase("arrays");
   // JobInfo.Tasks / NodeInfo.Tasks insertion orders, kept as lists
   // an update reorders the way the cache's delete + add does
   S.job_task_order.assign(S.n_jobs, {});
@@ -1775,6 +1812,7 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   S.broken.clear();
   S.node_of.clear();
   for (int32_t n = 0; n < S.n_nodes; ++n) S.node_of[S.canon[S.nodes_in[n].name]] = n;
+  phase("orders");
 
   // ---- plugins (framework.go:26-46): a tier entry counts only when the
   // caller's process has a builder under its name (GetPluginBuilder); one of
@@ -1873,6 +1911,7 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
     for (int32_t j = 0; j < S.n_jobs; ++j) S.job_queue[j] = S.jobs_in[j].queue;
   }
   S.task_rank.clear();  // computed by derive_host
+  phase("plugins+rest");
   return KBG_OK;
 }
 
@@ -1933,21 +1972,30 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     pin_near(hcpu, 1);
     try {
   if (S.task_rank.empty() && T > 0) {
-    std::vector<int32_t> ids(T);
-    for (int32_t t = 0; t < T; ++t) ids[t] = S.tasks_in[t].uid;
-    const std::vector<int32_t> dense = ranks_of(S, ids);
-    S.task_rank.resize(T);
-    for (int32_t t = 0; t < T; ++t) S.task_rank[t] = (int64_t)dense[t] * kRankGap;
+    // ranks are only ever compared between tasks of one job (the pending
+    // lists, a job's re-rank after an update): each job's UIDs are ranked
+    // alone, by their 16-byte keys and, on a tie, the strings
     fill_uid_keys(S, 0);
+    S.task_rank.resize(T);
     S.job_rank_order.assign(S.n_jobs, {});
     S.job_rank_key.assign(S.n_jobs, {});
+    const Session::UidKey* key = S.task_uid_key.data();
+    const auto uid = [&](int32_t t) -> const std::string& { return S.strs[S.tasks_in[t].uid]; };
+    const auto same = [&](int32_t a, int32_t b) { return key[a] == key[b] && uid(a) == uid(b); };
     for (int32_t j = 0; j < S.n_jobs; ++j) {
       std::vector<int32_t>& ro = S.job_rank_order[j];
       ro = S.job_task_order[j];
-      std::stable_sort(ro.begin(), ro.end(), [&](int32_t a, int32_t b) { return S.task_rank[a] < S.task_rank[b]; });
+      std::stable_sort(ro.begin(), ro.end(), [&](int32_t a, int32_t b) {
+        return !(key[a] == key[b]) ? key[a] < key[b] : uid(a) < uid(b);
+      });
       std::vector<Session::UidKey>& rk = S.job_rank_key[j];
       rk.resize(ro.size());
-      for (size_t i = 0; i < ro.size(); ++i) rk[i] = S.task_uid_key[ro[i]];
+      int64_t r = 0;
+      for (size_t i = 0; i < ro.size(); ++i) {
+        if (i > 0 && !same(ro[i - 1], ro[i])) ++r;  // equal UIDs share a rank
+        S.task_rank[ro[i]] = r * kRankGap;
+        rk[i] = key[ro[i]];
+      }
     }
   } else if (S.task_ranks_stale) {
     // a job that gained tasks: each new UID takes a rank between the ranked

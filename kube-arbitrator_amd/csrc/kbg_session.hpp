@@ -55,6 +55,13 @@ struct StrIndex {
         hs[k] = oh[i];
       }
   }
+  // the slot a content of hash h is looked up from (a prefetch ahead of insert_h)
+  void prefetch(uint64_t h) const {
+    if (ids.empty()) return;
+    const size_t k = h & (ids.size() - 1);
+    __builtin_prefetch(&ids[k]);
+    __builtin_prefetch(&hs[k]);
+  }
   int32_t find(const std::vector<std::string>& strs, std::string_view v) const {
     if (ids.empty()) return -1;
     const uint64_t h = hash(v);
@@ -66,10 +73,11 @@ struct StrIndex {
     }
   }
   // strs[id]'s canonical id: the first id holding the same content (id itself if new)
-  int32_t insert(const std::vector<std::string>& strs, int32_t id) {
+  int32_t insert(const std::vector<std::string>& strs, int32_t id) { return insert_h(strs, id, hash(strs[id])); }
+  // the same with the content's hash already computed (h = hash(strs[id]))
+  int32_t insert_h(const std::vector<std::string>& strs, int32_t id, uint64_t h) {
     if (2 * (n + 1) > ids.size()) reserve(n + 1);
     const std::string_view v = strs[id];
-    const uint64_t h = hash(v);
     const size_t m = ids.size() - 1;
     size_t k = h & m;
     for (; ids[k] >= 0; k = (k + 1) & m)

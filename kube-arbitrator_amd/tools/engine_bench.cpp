@@ -51,10 +51,16 @@ extern "C" int32_t kbg_tool_update_nodes(const kbg_snapshot* snap, const kbg_opt
                                          int32_t n, double* idle, double* rel, int32_t* ntasks, int32_t* pend,
                                          int32_t* n_pend) {
   kbg::Session S;
+  const auto i0 = std::chrono::steady_clock::now();
   if (ingest(S, snap, o) != KBG_OK) return -1;
+  const auto i1 = std::chrono::steady_clock::now();
   kbg::StaticHost sh;
   int outcome;
   if (derive_host(S, &sh, &outcome) != KBG_OK) return -2;
+  if (getenv("KBG_TOOL_TIME"))
+    fprintf(stderr, "[tool] open: ingest %.3f ms, derive %.3f ms\n",
+            std::chrono::duration<double, std::milli>(i1 - i0).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - i1).count());
   S.n_classes = sh.n_classes;
   UpdateCtx U;
   U.seen.assign(S.n_nodes, 0);
