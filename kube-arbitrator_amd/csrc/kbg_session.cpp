@@ -36,6 +36,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <climits>
 #include <cmath>
@@ -1733,8 +1734,16 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
     };
     std::vector<std::thread> th;
     const size_t chunk = (NS + P - 1) / P;
-    for (size_t p = 1; p < P; ++p) th.emplace_back(copy_range, std::min(NS, p * chunk), std::min(NS, (p + 1) * chunk));
+    size_t done_to = chunk;  // a range no worker took is copied here
+    try {
+      for (size_t p = 1; p < P; ++p) {
+        th.emplace_back(copy_range, std::min(NS, p * chunk), std::min(NS, (p + 1) * chunk));
+        done_to = (p + 1) * chunk;
+      }
+    } catch (const std::system_error&) {
+    }
     copy_range(0, std::min(NS, chunk));
+    copy_range(std::min(NS, done_to), NS);
     for (std::thread& t : th) t.join();
   }
   phase("strings copy");
@@ -1967,8 +1976,16 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
     ~Worker() { join(); }
   };
   const int hcpu = sched_getcpu();
+  // a worker that cannot be started runs inline
+  auto start = [](Worker& w, auto&& fn) {
+    try {
+      w.th = std::thread(fn);
+    } catch (const std::system_error&) {
+      fn();
+    }
+  };
   Worker rwork;
-  rwork.th = std::thread([&S, T, hcpu, &rwork] {
+  start(rwork, [&S, T, hcpu, &rwork] {
     pin_near(hcpu, 1);
     try {
   if (S.task_rank.empty() && T > 0) {
@@ -2240,7 +2257,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
       vwork.nomem = true;
     }
   };
-  vwork.th = std::thread(std::move(victims));
+  start(vwork, victims);
   phase("victims");
   setup_pod_keys(S, incr, &S.upd_tasks, &was);
 
