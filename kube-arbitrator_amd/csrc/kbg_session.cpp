@@ -1666,15 +1666,18 @@ std::vector<int32_t> ranks_of(const Session& S, const std::vector<int32_t>& ids)
 // re-runs without recompiling the static predicate or reallocating HBM.
 
 // String id of `v` for an event: an existing content's canonical id, or a new entry.
-int32_t intern(Session& S, const char* v) {
-  const std::string_view key(v ? v : "");
-  const int32_t known = S.canon_of.find(S.strs, key);
+int32_t intern_h(Session& S, std::string_view key, uint64_t h) {  // h = StrIndex::hash(key)
+  const int32_t known = S.canon_of.find_h(S.strs, key, h);
   if (known >= 0) return known;  // a canonical id is its own canonical id
   const int32_t id = (int32_t)S.strs.size();
   S.strs.emplace_back(key);
   S.canon.push_back(id);
-  S.canon_of.insert(S.strs, id);
+  S.canon_of.insert_h(S.strs, id, h);
   return id;
+}
+int32_t intern(Session& S, const char* v) {
+  const std::string_view key(v ? v : "");
+  return intern_h(S, key, kbg::StrIndex::hash(key));
 }
 
 // The canonical id of "" (an event's NodeName of a pod on no node).
@@ -5942,7 +5945,9 @@ kbg_status in_add_task(Session& S, UpdateCtx& U, int32_t t) {  // event_handlers
   return KBG_OK;
 }
 
-kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
+// key_hash: StrIndex::hash of a POD_ADD's pod key when the caller computed it
+// ahead (session_update's prefetch), else null
+kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e, const uint64_t* key_hash = nullptr) {
   auto status_ok = [](int32_t st) { return st > 0 && st <= KBG_UNKNOWN && !(st & (st - 1)); };
   switch (e.kind) {
     case KBG_EV_POD_UPDATE:
@@ -5989,7 +5994,7 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e) {
       k.resreq = e.resource;
       k.spec = e.spec;
       k.node_name = e.node >= 0 ? S.nodes_in[e.node].name : empty_str(S);
-      k.pod_key = intern(S, e.pod_key);
+      k.pod_key = key_hash ? intern_h(S, e.pod_key, *key_hash) : intern(S, e.pod_key);
       const int32_t t = S.n_tasks++;
       S.tasks_in.push_back(k);
       S.task_live.push_back(1);
@@ -6177,7 +6182,17 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
       __builtin_prefetch(&S.node_task_order[e.node]);
     }
   };
-  auto ahead_mid = [&](const kbg_event& e) {
+  // a new pod's key: hashed here, its index slot requested, the hash kept
+  // for the apply (events at least kMid ahead of the first)
+  constexpr int32_t kRing = 32;
+  static_assert(kRing > kMid, "the ring holds the hashes between the mid hop and the apply");
+  uint64_t key_hash[kRing];
+  auto ahead_mid = [&](const kbg_event& e, int32_t at) {
+    if (e.kind == KBG_EV_POD_ADD && e.pod_key) {
+      const uint64_t h = kbg::StrIndex::hash(std::string_view(e.pod_key));
+      key_hash[at % kRing] = h;
+      S.canon_of.prefetch(h);
+    }
     if (const int32_t t = task_of(e); t >= 0) {
       const kbg_task& k = S.tasks_in[t];
       __builtin_prefetch(&S.job_task_order[k.job]);
@@ -6211,10 +6226,11 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
   };
   for (int32_t i = 0; i < n; ++i) {
     if (i + kFar < n) ahead_far(ev[i + kFar]);
-    if (i + kMid < n) ahead_mid(ev[i + kMid]);
+    if (i + kMid < n) ahead_mid(ev[i + kMid], i + kMid);
     if (i + kNear < n) ahead_near(ev[i + kNear]);
     const uint64_t c0 = prof ? __builtin_readcyclecounter() : 0;
-    kbg_status st = apply_event(S, U, ev[i]);
+    const bool hashed = i >= kMid && ev[i].kind == KBG_EV_POD_ADD && ev[i].pod_key;
+    kbg_status st = apply_event(S, U, ev[i], hashed ? &key_hash[i % kRing] : nullptr);
     if (st != KBG_OK) return st;
     if (prof) {
       const int k = std::min(4, std::max(0, (int)ev[i].kind));

@@ -62,9 +62,9 @@ struct StrIndex {
     __builtin_prefetch(&ids[k]);
     __builtin_prefetch(&hs[k]);
   }
-  int32_t find(const std::vector<std::string>& strs, std::string_view v) const {
+  int32_t find(const std::vector<std::string>& strs, std::string_view v) const { return find_h(strs, v, hash(v)); }
+  int32_t find_h(const std::vector<std::string>& strs, std::string_view v, uint64_t h) const {
     if (ids.empty()) return -1;
-    const uint64_t h = hash(v);
     const size_t m = ids.size() - 1;
     for (size_t k = h & m;; k = (k + 1) & m) {
       const int32_t id = ids[k];
