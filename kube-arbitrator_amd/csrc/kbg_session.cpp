@@ -2680,6 +2680,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   {
     if (full) {
       S.shape_ids.clear();
+      S.shape_task.clear();
       S.shape_of_task.assign(T, -1);
       S.be_shape.assign(std::max(1, S.n_classes), -1);
       S.n_shapes = 0;
@@ -2696,6 +2697,9 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
         sh_t = it.first->second;
       }
       S.task_shape[t] = sh_t;
+      if ((int32_t)S.shape_task.size() <= sh_t) S.shape_task.resize((size_t)sh_t + 1, -1);
+      int32_t& rep = S.shape_task[sh_t];
+      if (rep < 0 || rep >= T || S.task_shape[rep] != sh_t) rep = t;
     };
     // backfill rows: one grouping id per class (the request does not matter)
     auto be_shape = [&](int32_t t) {
@@ -3856,6 +3860,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   // evaluation scans the table); pod affinity (gains cut) and
   // sharded sessions too.
   const bool no_reuse = getenv("KBG_NO_CUT_REUSE") != nullptr;  // read per cycle (A/B parity tests)
+  const bool rescan_all = [] {  // KBG_RESCAN_ALL=0: a contended rescan lists the shapes seen so far only
+    const char* e = getenv("KBG_RESCAN_ALL");
+    return !(e && e[0] == '0');
+  }();
   const bool reuse_ok = !S.opts.full_scan && !S.comm && !S.has_aff && !no_reuse;
   bool reuse = false;
   // From the first cut on (the contended part of the cycle) every batch
@@ -4012,6 +4020,19 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
               shape_in[sh] = shape_in_stamp;
               scan_list.push_back(shape_rep[sh]);
             }
+            // and every other candidate shape not known to fit nowhere (a
+            // task of it, kept by derive_host): a shape that first appears in
+            // a later batch finds a row instead of cutting for a rescan
+            if (rescan_all)
+              for (int32_t sh = 0; sh < (int32_t)S.shape_task.size() && sh < (int32_t)shape_in.size(); ++sh) {
+                if ((int32_t)scan_list.size() >= S.K) break;
+                const int32_t rep = S.shape_task[sh];
+                if (rep < 0 || rep >= S.n_tasks || S.task_shape[rep] != sh || shape_in[sh] == shape_in_stamp ||
+                    failed[sh].load(std::memory_order_relaxed))
+                  continue;
+                shape_in[sh] = shape_in_stamp;
+                scan_list.push_back(rep);
+              }
             list = scan_list.data();
             len = (int32_t)scan_list.size();
           }
