@@ -21,7 +21,7 @@ for rep in range(int(os.environ.get("REPS", "3"))):
                              timeout=300, env=env)
         d = json.loads(out.stdout.strip().splitlines()[-1])
         pm = d.get("production_mode", {})
-        res.setdefault(v, []).append((round(d["p50_cycle_ms"], 2), round(d["full_scan_mode"]["p50_cycle_ms"], 2),
+        res.setdefault(v, []).append((round(d["p50_cycle_ms"], 2), round(d.get("full_scan_mode", {}).get("p50_cycle_ms") or 0, 2),
                                       round(pm.get("scan_kernel", {}).get("avg_launch_us") or 0, 1),
                                       round(pm.get("breakdown", {}).get("device_roundtrip_ms") or 0, 2))
                                      + ((round(d["resident_session"]["churn_update_ms_p50"], 2),) if resident else ()))
