@@ -11,11 +11,14 @@ value       = placements/sec (Allocate + Pipeline decisions / wall time), whole 
               production mode (identical (class, request) shapes share a scan row)
 ms_per_step = mean allocate-cycle wall time; p50_cycle_ms = median
 roofline    = the dominant kernel (kbg_firstfit_kernel, full-scan mode: every
-              task evaluation scans the whole node table on the device):
-              SURVEY §8(d) bytes per task evaluation (N x 64 B + 32 B) x rows
-              per launch / average launch time (HIP events on the library's
-              stream), against 8 TB/s HBM3E; traffic = PMC HBM bytes per launch
-              (profiles/pmc_scan.json); binding = its VALU-issue ceiling
+              task evaluation scans the whole node table on the device)
+              against the ceiling that binds it, VALU issue: PMC wave64 VALU
+              instructions per launch (profiles/pmc_scan.json, scaled to this
+              run's rows x words) / average launch time (HIP events on the
+              library's stream), peak 1024 SIMDs x 2.4 GHz / 4 cycles; traffic
+              = PMC HBM bytes per launch with traffic_frac_of_peak against 8
+              TB/s; equivalent_8d = SURVEY §8(d) bytes per task evaluation (N x
+              64 B + 32 B) x rows / launch time (on-chip reuse, above 1)
 cycle_roofline_8d = BASELINE's north-star form: the same bytes per allocate
               cycle / p50 cycle wall time
 scan_kernel = the dominant kernel against its physical ceilings: PMC HBM bytes
@@ -57,6 +60,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 SIMDS = 256 * 4        # 256 CUs x 4 SIMDs
 CLOCK_GHZ = 2.4        # peak engine clock
 VALU_CYC = 4           # issue cycles of one wave64 VALU instruction on a SIMD (fp64 compare, lane moves)
+VALU_PEAK_GIPS = SIMDS * CLOCK_GHZ / VALU_CYC  # chip-wide wave64 VALU issue ceiling, G instructions/s
 NODE_RECORD_B = 64     # SURVEY §8(d) algorithmic bytes per node record
 TASK_RECORD_B = 32
 
@@ -299,10 +303,10 @@ def load_pmc(n_nodes, mode):
         d = json.load(open(p))
         sec = d.get(mode)
         if sec and sec.get("n_nodes", d.get("n_nodes")) == n_nodes:
-            return dict(sec, source=d.get("source"))
+            return dict(sec, source=d.get("source"), n_nodes=n_nodes)
         other = d.get("by_nodes", {}).get(str(n_nodes), {})  # other workloads' profiles (C4)
         if other.get(mode):
-            return dict(other[mode], source=other.get("source"))
+            return dict(other[mode], source=other.get("source"), n_nodes=n_nodes)
     except (OSError, ValueError):
         pass
     return None
@@ -382,9 +386,14 @@ def main():
     cache = cache_from_fixture(fx)
     base_opts = {"device": device}
     comm = None
+    rccl_ranks = None  # ranks the RCCL communicator itself reports (ncclCommCount); None: no communicator (N=1)
     if world > 1 or args.comm:
         comm = kdist.ShardComm(device)
         base_opts["comm"] = comm
+        rccl_ranks, rccl_rank = comm.ranks()
+        if rccl_ranks != world or rccl_rank != rank:
+            log(f"bench: the RCCL communicator reports rank {rccl_rank} of {rccl_ranks}, the launcher {rank} of {world}")
+            sys.exit(2)
     if args.batch:
         base_opts["batch_tasks"] = args.batch
     if args.candidates:
@@ -437,6 +446,7 @@ def main():
         replay(ssn, decs, "allocate")
         agg["digest"] = digest_outputs(session_output(ssn, binder.binds))
         agg["n_nodes"] = len(ssn.nodes)
+        agg["words"] = (((agg["n_nodes"] + 63) // 64) + world - 1) // world  # 64-node words a rank's launch walks
         agg["pending"] = ssn.flat.pending_count
         agg["jobs"] = len(ssn.jobs)
         agg["queues"] = len(ssn.queues)
@@ -478,39 +488,73 @@ def main():
                                   "wall time of kbg_allocate", "equivalent_8d": eq})
         return out
 
+    def pmc_scaled(pmc, rows, words):
+        """The profiled kernel's PMC figures per launch, scaled from the
+        profiled command's rows per launch (and 64-node words per launch: a
+        sharded rank walks its own words) to this run's: VALU instructions grow
+        with rows x words."""
+        f = 1.0
+        if rows and pmc.get("rows_per_launch"):
+            f *= rows / pmc["rows_per_launch"]
+        pw = pmc.get("words_per_launch") or (pmc.get("n_nodes", 5000) + 63) // 64
+        if words and pw:
+            f *= words / pw
+        return f
+
     def kernel_roofline(agg, mode):
         """The contract's roofline of the dominant kernel, kbg_firstfit_kernel
         in full-scan mode (every row is one task evaluation scanning all N
-        nodes, SURVEY 8(d) cursor rule): achieved = 8(d) bytes per unit (N x
-        64 B + 32 B) x the rows one launch evaluates / the launch's average
-        duration (HIP events around every launch on the library's stream,
-        over the timed steps); traffic = PMC HBM bytes per launch of the same
-        command (profiles/pmc_scan.json). The 8(d) count charges a node
-        record per (row, node) pair; the kernel holds a wave's 64 node records
-        in registers for all the rows of its workgroup, so the count can pass
-        the HBM peak — `binding` is then the ceiling that holds: VALU issue
-        (the kernel's PMC wave instructions at full issue on every SIMD)."""
+        nodes, SURVEY 8(d) cursor rule), against the ceiling that binds it.
+        The kernel holds a wave's 64 node records in registers for every row of
+        its workgroup and the node table is L2-resident, so HBM is far from
+        binding (traffic_frac_of_peak); what bounds a launch is VALU issue:
+        achieved = PMC wave64 VALU instructions per launch (profiles/pmc_scan.json,
+        scaled to this run's rows and words per launch) / the launch's average
+        duration (HIP events around the fused launches on the library's
+        stream, over the timed steps), peak = 1024 SIMDs x 2.4 GHz / 4 cycles
+        per wave64 instruction. The SURVEY 8(d) byte count (N x 64 B + 32 B per
+        task evaluation) over the same launch time is kept as equivalent_8d:
+        it charges a node read per (row, node) pair, i.e. on-chip reuse, and
+        is not a fraction of a physical peak."""
         launches = max(1, agg["launches"])
         rows = agg["evals"] / launches
         avg_s = agg["scan_ms"] * 1e-3 / launches
+        words = agg["words"]
         per_launch = rows * (agg["n_nodes"] * NODE_RECORD_B + TASK_RECORD_B)
-        ach = per_launch / avg_s / 1e9 if avg_s > 0 else 0.0
-        out = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-               "traffic": None, "kernel": "kbg_firstfit_kernel (full-scan mode)", "avg_launch_us": avg_s * 1e6,
-               "rows_per_launch": rows, "algo_bytes_per_launch": per_launch,
-               "definition": "SURVEY 8(d) bytes per task evaluation x rows per launch / average launch time "
-                             "(HIP events on the library stream over the timed steps, on one fused launch in "
-                             "four: kbg_stats.scan_kernel_ms)"}
-        pmc = load_pmc(agg["n_nodes"], mode) if comm is None else None
+        eq = {"achieved": per_launch / avg_s / 1e9 if avg_s > 0 else 0.0, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "algo_bytes_per_launch": per_launch,
+              "definition": "SURVEY 8(d) bytes per task evaluation (N x 64 B + 32 B) x rows per launch / average "
+                            "launch time: counts a node record per (row, node) pair, above the HBM peak because "
+                            "the kernel reuses each node record on chip for every row"}
+        eq["frac"] = eq["achieved"] / HBM_PEAK_GBS
+        out = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_GIPS, "unit": "G wave64 VALU instructions/s",
+               "frac": None, "traffic": None, "kernel": "kbg_firstfit_kernel (full-scan mode)",
+               "avg_launch_us": avg_s * 1e6, "rows_per_launch": rows, "words_per_launch": words,
+               "timing": "HIP events on the library stream around one fused launch in four over the timed steps "
+                         "(kbg_stats.scan_kernel_ms)",
+               "equivalent_8d": eq}
+        pmc = load_pmc(agg["n_nodes"], mode)
         if pmc:
+            f = pmc_scaled(pmc, rows, words)
+            if pmc.get("valu_insts_per_launch") is not None and avg_s > 0:
+                insts = pmc["valu_insts_per_launch"] * f
+                out["achieved"] = insts / avg_s / 1e9
+                out["frac"] = out["achieved"] / VALU_PEAK_GIPS
+                out["valu_insts_per_launch"] = insts
+                out["issue_floor_us"] = insts * VALU_CYC / (SIMDS * CLOCK_GHZ * 1e3)
             if pmc.get("hbm_bytes_per_launch") is not None:
-                out["traffic"] = pmc["hbm_bytes_per_launch"]
-                out["traffic_frac_of_peak"] = pmc["hbm_bytes_per_launch"] / avg_s / 1e9 / HBM_PEAK_GBS
-            if pmc.get("valu_insts_per_launch") is not None:
-                out["binding"] = dict(valu_ceiling(pmc, avg_s * 1e6, rows), bound="valu issue")
+                out["traffic"] = pmc["hbm_bytes_per_launch"] * f
+                out["traffic_frac_of_peak"] = out["traffic"] / avg_s / 1e9 / HBM_PEAK_GBS if avg_s > 0 else None
             if pmc.get("wait_any_share") is not None:  # share of the waves' lifetime parked at s_waitcnt / barriers
                 out["wait_any_share"] = pmc["wait_any_share"]
+            out["pmc_scale"] = f
             out["pmc_source"] = pmc.get("source")
+            out["definition"] = ("achieved = PMC SQ_INSTS_VALU per launch (scaled by pmc_scale to this run's rows x "
+                                 "words per launch) / average launch time; peak = 1024 SIMDs x 2.4 GHz / 4 cycles "
+                                 "per wave64 VALU instruction; traffic = PMC HBM bytes per launch "
+                                 "(2 x FETCH_SIZE + WRITE_SIZE)")
+        else:  # no profile of this workload: the physical figure is unknown, the 8(d) one stays beside it
+            out["definition"] = "no PMC profile of this workload committed under profiles/: achieved unmeasured"
         return out
 
     def scan_kernel(agg, mode):
@@ -588,7 +632,9 @@ def main():
                    "candidates": base_opts.get("candidates", 32)},
         "roofline": kernel_roofline(full, "full_scan"),
         "roofline_note": "full-scan mode (every task evaluation scans all N nodes on the device, SURVEY 8(d) cursor "
-                         "rule); `value` is the production mode, which groups identical (class, request) shapes",
+                         "rule); bound = VALU issue (PMC), HBM traffic and the 8(d) byte figure beside it; `value` "
+                         "is the production mode, which groups identical (class, request) shapes",
+        "rccl_ranks": rccl_ranks,
         "cycle_roofline_8d": cycle_roofline(full, "full_scan"),
         "scan_kernel": scan_kernel(full, "full_scan"),
         "full_scan_mode": {"placements_per_s": full["decisions"] / full["elapsed"],
@@ -795,12 +841,24 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid, open_ms_
     launch_us = vms * 1e3 / max(1, vscans)
     ach = algo / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
     pmc = load_pmc(n_nodes, "victim") if comm is None else None
+    # both physical ceilings of the victim kernel; `bound` is the one it is closest to
     roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
             "traffic": pmc["hbm_bytes_per_launch"] if pmc else None, "kernel": "kbg_victim_kernel",
-            "avg_launch_us": launch_us, "algo_bytes_per_launch": algo}
+            "avg_launch_us": launch_us, "algo_bytes_per_launch": algo,
+            "definition": "N x 64 B + R x 32 B per launch (DESIGN.md §5) / average launch time (HIP events, one "
+                          "launch in 16)"}
     if pmc:
         roof["valu"] = valu_ceiling(pmc, launch_us)
         roof["pmc_source"] = pmc.get("source")
+        roof["traffic_frac_of_peak"] = pmc["hbm_bytes_per_launch"] / (launch_us * 1e-6) / 1e9 / HBM_PEAK_GBS
+        vf = roof["valu"].get("frac")
+        if vf is not None and vf > roof["frac"]:
+            hbm = {k: roof[k] for k in ("achieved", "peak", "unit", "frac", "definition")}
+            insts = roof["valu"]["wave_insts_per_launch"]
+            roof.update({"bound": "valu", "achieved": insts / (launch_us * 1e-6) / 1e9, "peak": VALU_PEAK_GIPS,
+                         "unit": "G wave64 VALU instructions/s", "frac": vf, "hbm_algorithmic": hbm,
+                         "definition": "PMC SQ_INSTS_VALU per launch / average launch time; peak = 1024 SIMDs x "
+                                       "2.4 GHz / 4 cycles per wave64 instruction"})
     line = {
         "metric": "task placements/sec + p50 scheduling-cycle latency, contended cluster (reclaim/preempt)",
         "value": total / elapsed,
@@ -820,6 +878,7 @@ def contended_bench(args, fx, cache, base_opts, comm, rank, world, cid, open_ms_
                    "parallelism": f"node-axis shards x{world} (RCCL min-reduce of the victim-scan stop node)"
                                   if world > 1 else "single-gpu"},
         "roofline": roof,
+        "rccl_ranks": comm.ranks()[0] if comm is not None else None,
         "decisions_per_cycle": dec // max(1, args.steps),
         "evictions_per_cycle": ev // max(1, args.steps),
         "victim_scans_per_cycle": vscans // max(1, args.steps),

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KBG_ABI_VERSION 10
+#define KBG_ABI_VERSION 11
 
 typedef enum kbg_status {
   KBG_OK = 0,
@@ -372,6 +372,11 @@ kbg_status kbg_comm_unique_id(uint8_t out[KBG_COMM_ID_BYTES]);
 kbg_status kbg_comm_init(const uint8_t id[KBG_COMM_ID_BYTES], int32_t n_ranks, int32_t rank, int32_t device,
                          kbg_comm** out);
 void kbg_comm_destroy(kbg_comm* c);
+/* The RCCL communicator's own view of the clique (ncclCommCount,
+ * ncclCommUserRank): how many ranks it spans and this process's rank (ABI 11).
+ * A bench line reports it so a multi-GPU figure names the ranks that actually
+ * took part. */
+kbg_status kbg_comm_ranks(const kbg_comm* c, int32_t* n_ranks, int32_t* rank);
 
 /* ABI version and the last error message of this thread. */
 int32_t kbg_abi_version(void);

@@ -1318,6 +1318,16 @@ void remove_ports(Session& S, int32_t c, int32_t nd) {
     }
 }
 
+// The port atom of one of a pod's host-port entries (-1: no atom; every port
+// a pod on a node uses is one).
+int32_t port_atom(const Session& S, const kbg_host_port& hp) {
+  if (hp.host_port <= 0) return -1;
+  const std::string ip = S.strs[hp.host_ip].empty() ? std::string("0.0.0.0") : S.strs[hp.host_ip];
+  const std::string pr = S.strs[hp.protocol].empty() ? std::string("TCP") : S.strs[hp.protocol];
+  auto ai = S.atom_of.find(ip + "|" + pr + "|" + std::to_string(hp.host_port));
+  return ai == S.atom_of.end() ? -1 : ai->second;
+}
+
 // A pod that was on the node at open leaves node.Pods() (a statement
 // discard's RemoveTask by key of the pod holding the key): each of its port
 // entries goes; an atom no pod holds any more is free again.
@@ -1325,19 +1335,34 @@ void release_open_ports(Session& S, int32_t nd, const kbg_host_port* ports, int3
   if (!S.has_ports) return;
   uint64_t* np = &S.node_ports[(size_t)nd * S.PW];
   for (int32_t i = 0; i < n; ++i) {
-    const kbg_host_port& hp = ports[i];
-    if (hp.host_port <= 0) continue;
-    const std::string ip = S.strs[hp.host_ip].empty() ? std::string("0.0.0.0") : S.strs[hp.host_ip];
-    const std::string pr = S.strs[hp.protocol].empty() ? std::string("TCP") : S.strs[hp.protocol];
-    auto ai = S.atom_of.find(ip + "|" + pr + "|" + std::to_string(hp.host_port));
-    if (ai == S.atom_of.end()) continue;  // (every port a pod on the node uses is an atom)
-    const int32_t a = ai->second;
+    const int32_t a = port_atom(S, ports[i]);
+    if (a < 0) continue;
     const int64_t k = ((int64_t)nd << 32) | (uint32_t)a;
     S.port_gone[k]++;
     if (open_ports_left(S, nd, a) > 0 || S.port_hold.count(k)) continue;
     const uint64_t bit = 1ull << (a & 63);
     if (!(np[a / 64] & bit)) continue;
     np[a / 64] &= ~bit;
+    for (int32_t c2 : S.atom_cls[a]) refresh_mask_bit(S, c2, nd);
+  }
+}
+
+// The reverse: a discarded statement's unevict adds that pod back to the node
+// (statement.go:81-108 node.AddTask), so it is in node.Pods() again and its
+// port entries are used again (vendor cache/node_info.go:593-605): every class
+// one of them conflicts with loses the node.
+void restore_open_ports(Session& S, int32_t nd, const kbg_host_port* ports, int32_t n) {
+  if (!S.has_ports) return;
+  uint64_t* np = &S.node_ports[(size_t)nd * S.PW];
+  for (int32_t i = 0; i < n; ++i) {
+    const int32_t a = port_atom(S, ports[i]);
+    if (a < 0) continue;
+    const int64_t k = ((int64_t)nd << 32) | (uint32_t)a;
+    auto g = S.port_gone.find(k);
+    if (g != S.port_gone.end() && --g->second <= 0) S.port_gone.erase(g);
+    const uint64_t bit = 1ull << (a & 63);
+    if (np[a / 64] & bit) continue;
+    np[a / 64] |= bit;
     for (int32_t c2 : S.atom_cls[a]) refresh_mask_bit(S, c2, nd);
   }
 }
@@ -1970,11 +1995,17 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   // of them reads a rank or writes what the ranks are computed from: UIDs,
   // job task lists); joined before the pending lists sort by rank. The
   // victim lists below take a second worker.
+  // A worker's exception (std::bad_alloc, std::length_error from a resize,
+  // anything the KBG_CHECK_DERIVE comparison throws) is kept and rethrown on
+  // this thread after the join, where derive_host's callers catch it.
   struct Worker {
     std::thread th;
-    bool nomem = false;
+    std::exception_ptr err;
     void join() {
       if (th.joinable()) th.join();
+    }
+    void rethrow() {
+      if (err) std::rethrow_exception(err);
     }
     ~Worker() { join(); }
   };
@@ -2105,8 +2136,8 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   }
   S.task_ranks_stale = false;
   S.rank_dirty_jobs.clear();
-    } catch (const std::bad_alloc&) {
-      rwork.nomem = true;
+    } catch (...) {
+      rwork.err = std::current_exception();
     }
   });
   // per-task vectors grow with every update's new pods: keep headroom so an
@@ -2256,8 +2287,8 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
       }
       vbad = o2 != S.nt_off || t2 != S.nt_task;
     }
-    } catch (const std::bad_alloc&) {
-      vwork.nomem = true;
+    } catch (...) {
+      vwork.err = std::current_exception();
     }
   };
   start(vwork, victims);
@@ -2513,7 +2544,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   phase("preconditions");
   rwork.join();
   phase("ranks join");
-  if (rwork.nomem) throw std::bad_alloc();
+  rwork.rethrow();
   // ---- pending task lists in TaskOrderFn order (session_plugins.go:266-276)
   // an update's derive copies the lists of the jobs no event touched
   const bool keep_lists = !full && (int32_t)S.pend_off_all.size() == S.n_jobs;
@@ -2725,7 +2756,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   phase("shapes");
   vwork.join();
   phase("victims join");
-  if (vwork.nomem) throw std::bad_alloc();
+  vwork.rethrow();
   if (vbad) return fail(KBG_E_INVALID, "internal: incremental victim lists differ");
   return KBG_OK;
 }
@@ -2780,13 +2811,20 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   if ((st = alloc_soa(S, &S.d_nodes)) || (st = alloc_soa(S, &S.d_nodes0))) return st;
   const size_t up_cap = up_bytes_for(S.K);
   S.up_cap = up_cap;
-  // counts, candidates and owner-resolve availability (replicated path), or
-  // per-slot info, the slots' word masks and availability (fused path); u32 units
-  const size_t down_cap =
-      std::max(2 * (size_t)S.K + (size_t)S.cand_cap, fused_down_words(S.K, fused_mask_words(S)));
-  if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) || (st = dalloc(S, &S.d_up, up_cap)) ||
+  // Host side (pinned, per stage; u32 units): per-slot info, the slots' word
+  // masks and availability (fused path), and on a communicator also counts
+  // and candidates (replicated path). Device side: the replicated path's
+  // select output or the owner-resolve availability (K words, summed over
+  // RCCL) — only a communicator needs either; the fused kernel writes its
+  // results straight into the pinned buffer.
+  const size_t repl_cap = 2 * (size_t)S.K + (size_t)S.cand_cap;
+  const size_t fused_cap = fused_down_words(S.K, fused_mask_words(S));
+  const size_t down_cap = S.comm ? std::max(repl_cap, fused_cap) : fused_cap;
+  const size_t d_down_cap = S.comm ? std::max(repl_cap, (size_t)S.K) : 1;
+  if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) ||
+      (st = dalloc(S, &S.d_up, S.comm ? up_cap : 1)) ||
       (st = dalloc(S, &S.d_bits, S.comm ? (size_t)S.R * 2 * S.K * kbg::kbg_slot_words(S.Wl) : 1)) ||
-      (st = dalloc(S, &S.d_down, down_cap)))
+      (st = dalloc(S, &S.d_down, d_down_cap)))
     return st;
   for (kbg::Stage& g : S.stages) {
     if ((st = host_alloc((void**)&g.h_up, up_cap)) || (st = host_alloc((void**)&g.h_down, down_cap * 4))) return st;
@@ -5187,6 +5225,10 @@ struct Live {
       S.trun[v] = 1;
       if (S.t_pos[v] >= 0) vt_delta(S, 0, S.t_pos[v], 1.0, 0, 0);
       S.t_detached[v] = 0;
+      // back in node.Pods(): its host ports are used again (release_open_ports' reverse)
+      const int32_t vs = S.tasks_in[v].spec;
+      if (vs >= 0 && S.specs_in[vs].port_len > 0)
+        restore_open_ports(S, n, &S.ports_in[S.specs_in[vs].port_off], S.specs_in[vs].port_len);
       touch(n);
     }
     plugins(v, true);
@@ -6364,6 +6406,8 @@ static kbg_status session_open(const kbg_snapshot* snap, const kbg_options* opts
     st = open_session(s->s, snap, opts, comm);
   } catch (const std::bad_alloc&) {
     st = fail(KBG_E_NOMEM, "host allocation failed");
+  } catch (const std::exception& e) {  // a derive worker's error, rethrown after its join
+    st = fail(KBG_E_INVALID, std::string("internal: ") + e.what());
   }
   if (st != KBG_OK) {
     free_device(s->s);
@@ -6418,6 +6462,18 @@ kbg_status kbg_comm_init(const uint8_t id[KBG_COMM_ID_BYTES], int32_t n_ranks, i
   return KBG_OK;
 }
 
+kbg_status kbg_comm_ranks(const kbg_comm* c, int32_t* n_ranks, int32_t* rank) {
+  if (!c || !n_ranks || !rank) return fail(KBG_E_INVALID, "null argument");
+  if (!c->nccl || c->aborted.load()) return fail(KBG_E_RCCL, "the communicator is not live");
+  int n = 0, r = 0;
+  ncclResult_t nr = ncclCommCount(c->nccl, &n);
+  if (nr == ncclSuccess) nr = ncclCommUserRank(c->nccl, &r);
+  if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclCommCount: ") + ncclGetErrorString(nr));
+  *n_ranks = n;
+  *rank = r;
+  return KBG_OK;
+}
+
 void kbg_comm_destroy(kbg_comm* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
@@ -6436,6 +6492,8 @@ kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t*
     return allocate_cycle(s->s, out, cap, n_out);
   } catch (const std::bad_alloc&) {
     return fail(KBG_E_NOMEM, "host allocation failed");
+  } catch (const std::exception& e) {
+    return fail(KBG_E_INVALID, std::string("internal: ") + e.what());
   }
 }
 
@@ -6446,6 +6504,8 @@ kbg_status kbg_backfill(kbg_session* s, kbg_decision* out, int32_t cap, int32_t*
     return backfill_cycle(s->s, out, cap, n_out);
   } catch (const std::bad_alloc&) {
     return fail(KBG_E_NOMEM, "host allocation failed");
+  } catch (const std::exception& e) {
+    return fail(KBG_E_INVALID, std::string("internal: ") + e.what());
   }
 }
 
@@ -6456,6 +6516,8 @@ kbg_status kbg_reclaim(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* 
     return reclaim_cycle(s->s, out, cap, n_out);
   } catch (const std::bad_alloc&) {
     return fail(KBG_E_NOMEM, "host allocation failed");
+  } catch (const std::exception& e) {
+    return fail(KBG_E_INVALID, std::string("internal: ") + e.what());
   }
 }
 
@@ -6466,6 +6528,8 @@ kbg_status kbg_preempt(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* 
     return preempt_cycle(s->s, out, cap, n_out);
   } catch (const std::bad_alloc&) {
     return fail(KBG_E_NOMEM, "host allocation failed");
+  } catch (const std::exception& e) {
+    return fail(KBG_E_INVALID, std::string("internal: ") + e.what());
   }
 }
 
@@ -6533,6 +6597,8 @@ kbg_status kbg_session_update(kbg_session* s, const kbg_event* events, int32_t n
     st = session_update(S, events, n);
   } catch (const std::bad_alloc&) {
     st = fail(KBG_E_NOMEM, "host allocation failed");
+  } catch (const std::exception& e) {  // a derive worker's error, rethrown after its join
+    st = fail(KBG_E_INVALID, std::string("internal: ") + e.what());
   }
   if (st != KBG_OK) S.broken = g_err;  // events were applied part-way
   return st;

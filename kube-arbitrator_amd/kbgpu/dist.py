@@ -59,6 +59,13 @@ class ShardComm:
         _abi.check(L.kbg_comm_init(uid, world, rank, device, ctypes.byref(self.handle)))
         self.rank, self.world, self.device = rank, world, device
 
+    def ranks(self):
+        """(ranks, this rank) as the RCCL communicator itself counts them (ncclCommCount / ncclCommUserRank)."""
+        from . import _abi
+        n, r = ctypes.c_int32(), ctypes.c_int32()
+        _abi.check(_abi.lib().kbg_comm_ranks(self.handle, ctypes.byref(n), ctypes.byref(r)))
+        return n.value, r.value
+
     def close(self):
         if self.handle:
             from . import _abi

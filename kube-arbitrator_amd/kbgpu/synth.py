@@ -602,14 +602,16 @@ def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3, aff=0.0, ports=0
             "queues": qs, "actions": acts}
 
 
-def contended_dupkey_fixture(seed):
+def contended_dupkey_fixture(seed, ports=0.0):
     """contended_fixture with half of the Running pods renamed after a Pending
     pod (PodKey = "<ns>/<name>" shared: a StatefulSet pod recreated while its
     predecessor still runs): preempt pipelines a pod onto the node that holds
     its key — AddTask refuses it (node_info.go:101-106) — and when the
     statement is discarded, unpipeline's RemoveTask removes by key the pod
-    that held it (statement.go:156-192, node_info.go:131-157)."""
-    fx = contended_fixture(8800 + seed, nodes=6, jobs=10, tasks=6)
+    that held it (statement.go:156-192, node_info.go:131-157). `ports`: the
+    share of pod specs with host ports (contended_fixture), so the holder's
+    ports leave node.Pods() with it and come back with its unevict."""
+    fx = contended_fixture(8800 + seed, nodes=6, jobs=10, tasks=6, ports=ports)
     rng = random.Random(seed)
     pods = fx["pods"]
     pend = [p for p in pods if p["phase"] == "Pending"]
@@ -619,7 +621,7 @@ def contended_dupkey_fixture(seed):
             if rng.random() < 0.5:
                 q = rng.choice(pend)
                 p["namespace"], p["name"] = q["namespace"], q["name"]
-    fx["name"] = f"contended-dupkey-{seed}"
+    fx["name"] = f"contended-dupkey-{seed}" + (f"-ports{ports}" if ports else "")
     return fx
 
 

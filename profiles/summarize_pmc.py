@@ -17,8 +17,8 @@ Derived figures (MI355X_MICROARCH.md):
   valu_issue_floor_us = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x 2.4 GHz):
                     the time the kernel's wave64 VALU instructions need at
                     full issue on every SIMD of the chip
-  eff_clock_ghz   = GRBM_GUI_ACTIVE / 8 XCDs / profiled duration (reads high
-                    below ~0.3 ms dispatches)
+(No clock is derived from GRBM_GUI_ACTIVE: on dispatches of a few µs that
+quotient reads far above the 2.4 GHz peak, MI355X_MICROARCH.md DVFS note.)
 """
 import csv
 import glob
@@ -110,10 +110,6 @@ def main():
                 v["active_inst_share"] = avg["SQ_ACTIVE_INST_ANY"] / avg["SQ_WAVE_CYCLES"]
             if "SQ_WAIT_INST_LDS" in avg:  # issue stalls on the LDS pipe (not lgkmcnt drains)
                 v["wait_inst_lds_share"] = avg["SQ_WAIT_INST_LDS"] / avg["SQ_WAVE_CYCLES"]
-        if "GRBM_GUI_ACTIVE" in avg:
-            pd = statistics.mean(c["_dur"]["GRBM_GUI_ACTIVE"].values())
-            v["profiled_avg_ns"] = pd
-            v["eff_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / pd
     json.dump(out, sys.stdout, indent=1)
     print()
 

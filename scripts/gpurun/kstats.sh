@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-4 end: rocprofv3 kernel statistics of the C3 and C4 benches (the
+# rocprofv3 kernel statistics of the C3 and C4 benches (the
 # kernels' average launch durations behind the bench lines' roofline objects).
 # Each step has its own time limit; stops at the first failure.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r4prof
+O=$R/gpurun_out/${RUN:-kstats}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 for cfg in ${CFGS:-3 4}; do

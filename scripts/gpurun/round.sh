@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-4 GPU session: the -m gpu suite (TESTS / K select a part), smoke(),
+# GPU session of a round: the -m gpu suite (TESTS / K select a part), smoke(),
 # the driver's default bench command, optional extra bench configs (CFGS,
 # e.g. "5 4") and the PMC passes (PMC=1, configs PMC_CFGS). Every GPU step has
 # its own time limit; the script stops at the first failure.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r4
+O=$R/gpurun_out/${RUN:-r5}
 mkdir -p $O
 cd $R
 if [ -z "$NO_TESTS" ]; then
@@ -27,4 +27,4 @@ done
 if [ -n "$PMC" ]; then
   CFGS=${PMC_CFGS:-3} bash $R/scripts/gpurun/pmc.sh
 fi
-echo R4_DONE
+echo ROUND_DONE

@@ -461,6 +461,27 @@ def test_dupkey_statement_discard_parity(seed):
         ssn.close()
 
 
+# seeds of synth.contended_dupkey_fixture(seed, ports=0.4) whose oracle run
+# discards such a statement (the first 900 seeds): the holders carry host ports
+DUP_DISCARD_PORT_SEEDS = [79, 89, 126, 231, 293, 369, 444, 469, 509, 570, 598, 669, 681, 793, 816, 884]
+
+
+@pytest.mark.parametrize("seed", DUP_DISCARD_PORT_SEEDS)
+def test_dupkey_statement_discard_ports_parity(seed):
+    """The discarded statement's RemoveTask by key takes the holder's host
+    ports out of node.Pods(); its unevict adds the holder back
+    (statement.go:81-108), so its ports are used again and a later pipeline
+    onto a conflicting port must fail as the reference's does
+    (predicates.go:144-155, vendor cache/node_info.go:593-605)."""
+    fx = synth.contended_dupkey_fixture(seed, ports=0.4)
+    ref = run_oracle(fx)
+    assert ref["stats"]["dup_discards"] > 0
+    got, ssn = run_fixture(fx)
+    compare_outputs(ref, got)
+    if ssn:
+        ssn.close()
+
+
 @pytest.mark.parametrize("seed", range(10))
 def test_victim_huge_node_parity(seed):
     """Nodes with more than kMaxNodeCandidates (1024) Running pods, which the
