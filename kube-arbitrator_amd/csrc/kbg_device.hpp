@@ -251,10 +251,22 @@ struct FirstFitArgs {
   int32_t complete;             // every word's masks go out (want ignored): lists are never cut
   int32_t splits, split_words;  // the words [w_lo, w_hi) in `splits` parts of split_words, one workgroup
                                 // each (a short batch's walk spread over more CUs); info is per (shape, part)
+  int32_t rows;                 // rows per workgroup (firstfit_geometry; at most the kernel's ROWS)
+  int32_t runs;                 // full-scan with inline shapes: launch row l belongs to the slot s with
+                                // run_end[s - 1] <= l < run_end[s] and the run's last row writes the slot
+                                // (no row -> shape map to read: rows of a slot are identical evaluations)
   TaskRec inl[kInlineShapes];
+  uint16_t run_end[kInlineShapes];
 };
-// Rows per workgroup of a launch of G rows (16, 24 or 32).
-int firstfit_rows(int32_t G);
+// Launch geometry of G rows: the kernel's rows-per-workgroup variant (16, 24
+// or 32) and the rows each workgroup takes (<= that). Production (grouped)
+// batches take whole 16/24/32-row blocks; full-scan batches spread their rows
+// evenly over the 256 CUs (ceil(G / 256) rounded up to a pair), so a launch of
+// 4.2k rows runs 17-18 rows on each CU instead of 24 on 174 of them.
+struct FfGeometry {
+  int32_t variant, rows;
+};
+FfGeometry firstfit_geometry(int32_t G, bool full_scan);
 hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t stream, hipEvent_t start = nullptr,
                            hipEvent_t stop = nullptr);
 

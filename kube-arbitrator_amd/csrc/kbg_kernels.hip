@@ -20,6 +20,7 @@
 // with -ffp-contract=off so nothing is fused.
 #include <hip/hip_ext.h>
 
+#include <algorithm>
 #include <utility>
 
 #include "kbg_device.hpp"
@@ -130,7 +131,7 @@ __device__ __forceinline__ void scan_row_pair(const double (&q)[2][3], double ic
 // while this group's compares run)
 template <int ROWS, int J, int GROUP>
 __device__ __forceinline__ void scan_rows_int(const double (*s_req)[3], const double (&q)[GROUP][3], double ic,
-                                              double im, double ig, uint32_t (&keep)[4]) {
+                                              double im, double ig, uint32_t (&keep)[4], int nrows) {
   double qn[GROUP][3];
   if constexpr (J + GROUP < ROWS) {
 #pragma unroll
@@ -143,12 +144,16 @@ __device__ __forceinline__ void scan_rows_int(const double (*s_req)[3], const do
   [&]<int... U>(std::integer_sequence<int, U...>) {
     (scan_row_pair<J + 2 * U>(*reinterpret_cast<const double(*)[2][3]>(&q[2 * U][0]), ic, im, ig, keep), ...);
   }(std::make_integer_sequence<int, GROUP / 2>{});
-  if constexpr (J + GROUP < ROWS) scan_rows_int<ROWS, J + GROUP, GROUP>(s_req, qn, ic, im, ig, keep);
+  if constexpr (J + GROUP < ROWS)
+    if (J + GROUP < nrows) scan_rows_int<ROWS, J + GROUP, GROUP>(s_req, qn, ic, im, ig, keep, nrows);
 }
 
+// `nrows` (wave-uniform, <= ROWS): the rows of the block that are real; the
+// groups past it are skipped (a full-scan workgroup takes fewer rows than its
+// variant holds, firstfit_geometry).
 template <bool INT_MODE, bool REL_ZERO, int ROWS, int J = 0, int GROUP = kRowGroup>
 __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, double im, double ig, double rc,
-                                          double rm, double rg, uint32_t (&keep)[4]) {
+                                          double rm, double rg, uint32_t (&keep)[4], int nrows = ROWS) {
   double q[GROUP][3];
 #pragma unroll
   for (int u = 0; u < GROUP; ++u) {
@@ -157,7 +162,7 @@ __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, d
     q[u][2] = s_req[J + u][2];
   }
   if constexpr (INT_MODE && REL_ZERO && GROUP % 2 == 0 && J == 0) {
-    scan_rows_int<ROWS, 0, GROUP>(s_req, q, ic, im, ig, keep);
+    scan_rows_int<ROWS, 0, GROUP>(s_req, q, ic, im, ig, keep, nrows);
     return;
   } else if constexpr (INT_MODE && REL_ZERO && GROUP % 2 == 0) {
     [&]<int... U>(std::integer_sequence<int, U...>) {
@@ -169,7 +174,7 @@ __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, d
     }(std::make_integer_sequence<int, GROUP>{});
   }
   if constexpr (J + GROUP < ROWS)
-    scan_rows<INT_MODE, REL_ZERO, ROWS, J + GROUP, GROUP>(s_req, ic, im, ig, rc, rm, rg, keep);
+    if (J + GROUP < nrows) scan_rows<INT_MODE, REL_ZERO, ROWS, J + GROUP, GROUP>(s_req, ic, im, ig, rc, rm, rg, keep, nrows);
 }
 
 template <bool INT_MODE, int ROWS>
@@ -305,23 +310,43 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
   __shared__ uint64_t s_f[kFfMaxRound][ROWS];      // [word of the round][row]: fits (Idle or Releasing)
   __shared__ uint64_t s_i[kFfMaxRound][ROWS];      //                        fits in Idle
   __shared__ uint32_t s_done[ROWS];
+  __shared__ uint16_t s_runs[kInlineShapes];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int rb = blockIdx.x / a.splits, part = blockIdx.x - rb * a.splits;  // row block, word part
-  const int g0 = rb * ROWS;
+  const int nrows = a.rows;  // rows of this block (<= ROWS; the rest of the variant's rows are skipped)
+  const int g0 = rb * nrows;
   const int w_lo = a.w_lo + part * a.split_words, w_hi = min(a.w_hi, w_lo + a.split_words);
   FF_STAMP(0);
-  if (wave == 0 && lane < ROWS) {
-    const int g = min(g0 + lane, a.G - 1);  // rows past G evaluate a copy of the last row, write nothing
-    const uint32_t m = a.row_shape ? a.row_shape[g] : ((uint32_t)g | kRowWriter);
-    const uint32_t sh = m & ~kRowWriter;
-    const TaskRec tr = a.shapes ? a.shapes[sh] : a.inl[sh];
-    s_req[lane][0] = tr.req[0];
-    s_req[lane][1] = tr.req[1];
-    s_req[lane][2] = tr.req[2];
-    s_cls[lane] = tr.cls;
-    s_flags[lane] = (uint32_t)tr.flags;
-    s_map[lane] = g0 + lane < a.G ? m : (m & ~kRowWriter);
+  if (wave == 0) {
+    // runs: the slots' run ends (kernel arguments) into LDS, then each row
+    // lane finds its slot by a binary search there — no row -> shape map
+    if (a.runs)
+      for (int i = lane; i < a.n_shapes; i += 64) s_runs[i] = a.run_end[i];
+    if (lane < ROWS) {
+      const bool real = lane < nrows && g0 + lane < a.G;
+      const int g = min(g0 + min(lane, nrows - 1), a.G - 1);  // padding rows evaluate a copy of a real row
+      uint32_t m;
+      if (a.runs) {
+        int lo = 0, hi = a.n_shapes - 1;  // the first slot whose run ends past g
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (s_runs[mid] > g) hi = mid;
+          else lo = mid + 1;
+        }
+        m = (uint32_t)lo | (g + 1 == (int)s_runs[lo] ? kRowWriter : 0u);
+      } else {
+        m = a.row_shape ? a.row_shape[g] : ((uint32_t)g | kRowWriter);
+      }
+      const uint32_t sh = m & ~kRowWriter;
+      const TaskRec tr = a.shapes ? a.shapes[sh] : a.inl[sh];
+      s_req[lane][0] = tr.req[0];
+      s_req[lane][1] = tr.req[1];
+      s_req[lane][2] = tr.req[2];
+      s_cls[lane] = tr.cls;
+      s_flags[lane] = (uint32_t)tr.flags;
+      s_map[lane] = real ? m : (m & ~kRowWriter);
+    }
   }
   const int32_t tw = w_hi - w_lo;  // words this workgroup covers
   if (tw <= 0) {  // no words (a session without nodes): empty complete lists, no table or mask read
@@ -407,11 +432,11 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
       uint64_t mr;
       if (rel_zero_wave) {
         scan_rows<INT_MODE, true, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm, cur.rg,
-                                                               keep);
+                                                               keep, nrows);
         mr = (flags_l & kRowRelZeroFits) ? ~0ull : 0ull;
       } else {
         scan_rows<INT_MODE, false, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm,
-                                                                cur.rg, keep);
+                                                                cur.rg, keep, nrows);
         mr = (uint64_t)keep[2] | ((uint64_t)keep[3] << 32);
       }
       if (lane < ROWS) {
@@ -489,38 +514,48 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
 }
 
 template <bool INT_MODE, bool EARLY_EXIT>
-hipError_t launch_firstfit_rows(const FirstFitArgs& a, int rows, hipStream_t stream, hipEvent_t start,
+hipError_t launch_firstfit_rows(const FirstFitArgs& a, int variant, hipStream_t stream, hipEvent_t start,
                                 hipEvent_t stop) {
-  const dim3 grid((a.G + rows - 1) / rows * a.splits), block(64 * kFfWaves);
-  if (rows == 16)
+  const dim3 grid((a.G + a.rows - 1) / a.rows * a.splits), block(64 * kFfWaves);
+  if (variant == 16)
     hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 16>), grid, block, 0, stream, start, stop, 0, a);
-  else if (rows == 24)
+  else if (variant == 24)
     hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 24>), grid, block, 0, stream, start, stop, 0, a);
   else
     hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 32>), grid, block, 0, stream, start, stop, 0, a);
   return hipGetLastError();
 }
 
-// Rows per workgroup: one workgroup per CU at a time (16 waves), so a launch
-// of more than 256 workgroups runs a second, mostly idle round; 24 or 32 rows
-// per workgroup keep batches of up to 8192 rows in one.
-int firstfit_rows(int32_t G) {
+// One workgroup per CU at a time (16 waves, 80-128 VGPRs), so a launch of
+// more than 256 workgroups runs a second, mostly idle round. Production
+// batches take whole blocks of 16, 24 or 32 rows (short ones split their walk
+// into word parts instead). Full-scan batches spread their rows evenly: every
+// row costs the same walk of the whole table, so ceil(G / 256) rows (rounded
+// up to a pair, the unit the scan's unrolled row walk skips by) on each CU
+// gives the shortest launch — 4.2k rows: 17-18 rows per CU on ~232 CUs
+// instead of 24 rows on 174.
+FfGeometry firstfit_geometry(int32_t G, bool full_scan) {
   constexpr int kCUs = 256;
-  if (G <= 16 * kCUs) return 16;
-  if (G <= 24 * kCUs) return 24;
-  return 32;
+  if (!full_scan) {
+    const int v = G <= 16 * kCUs ? 16 : G <= 24 * kCUs ? 24 : 32;
+    return {v, v};
+  }
+  int rows = (G + kCUs - 1) / kCUs;
+  rows = std::min(32, std::max(2, (rows + 1) & ~1));
+  return {rows <= 16 ? 16 : rows <= 24 ? 24 : 32, rows};
 }
 
 hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t stream, hipEvent_t start,
                            hipEvent_t stop) {
   if (a.G <= 0) return hipSuccess;
-  const int rows = firstfit_rows(a.G);
+  const FfGeometry geo = firstfit_geometry(a.G, !a.early_exit);
+  if (a.rows <= 0 || a.rows > geo.variant) return hipErrorInvalidValue;  // the host sizes both (device_launch)
   // <.., false>: full-scan mode (every node of every row), <.., true>: production
   if (int_mode)
-    return a.early_exit ? launch_firstfit_rows<true, true>(a, rows, stream, start, stop)
-                        : launch_firstfit_rows<true, false>(a, rows, stream, start, stop);
-  return a.early_exit ? launch_firstfit_rows<false, true>(a, rows, stream, start, stop)
-                      : launch_firstfit_rows<false, false>(a, rows, stream, start, stop);
+    return a.early_exit ? launch_firstfit_rows<true, true>(a, geo.variant, stream, start, stop)
+                        : launch_firstfit_rows<true, false>(a, geo.variant, stream, start, stop);
+  return a.early_exit ? launch_firstfit_rows<false, true>(a, geo.variant, stream, start, stop)
+                      : launch_firstfit_rows<false, false>(a, geo.variant, stream, start, stop);
 }
 
 // ------------------------------------------------------- FitError counts

@@ -674,8 +674,10 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
     // Production walks of larger tables (C4's 313 words) split too: each part
     // stops at the row's `want` within its own words, and the parts' lists
     // join in node order up to the first one that stopped early (device_wait)
+    const kbg::FfGeometry geo = kbg::firstfit_geometry(G, !a.early_exit);
+    a.rows = geo.rows;
     if ((a.complete || a.early_exit) && !S.comm) {
-      const int32_t blocks = (G + kbg::firstfit_rows(G) - 1) / kbg::firstfit_rows(G);
+      const int32_t blocks = (G + geo.rows - 1) / geo.rows;
       a.splits = std::max(1, std::min({kbg::kFfMaxSplits, 256 / std::max(1, blocks), tw / 8}));
     }
     if (tw > 0) {
@@ -691,8 +693,18 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
     } else if (!(a.shapes = dev_ptr(S, sg.h_shapes))) {
       return fail(KBG_E_HIP, "hipHostGetDevicePointer of a stage buffer failed");
     }
-    if (sg.h_rowshape && !(a.row_shape = dev_ptr(S, sg.h_rowshape)))
+    // Full-scan rows of one slot are identical evaluations and only the
+    // slot's writer row produces output, so with the shapes inline the launch
+    // takes its rows slot by slot from the run lengths in its arguments (no
+    // row -> shape map read over PCIe at the start of every workgroup)
+    if (sg.h_rowshape && sg.n_slots <= kbg::kInlineShapes && (int32_t)sg.slot_rows.size() == sg.n_slots) {
+      a.runs = 1;
+      uint32_t end = 0;
+      for (int32_t sl = 0; sl < sg.n_slots; ++sl) a.run_end[sl] = (uint16_t)(end += sg.slot_rows[sl]);
+      if ((int32_t)end != G) return fail(KBG_E_INVALID, "internal: full-scan slot rows do not add up to the batch");
+    } else if (sg.h_rowshape && !(a.row_shape = dev_ptr(S, sg.h_rowshape))) {
       return fail(KBG_E_HIP, "hipHostGetDevicePointer of a stage buffer failed");
+    }
     a.info = dev_ptr(S, sg.h_down);
     a.masks = reinterpret_cast<kbg::MaskPair*>(dev_ptr(S, sg.h_down + fused_mask_off(S.K)));
     if (!a.info || !a.masks) return fail(KBG_E_HIP, "hipHostGetDevicePointer of a stage buffer failed");
@@ -1021,10 +1033,12 @@ struct Grouper {
           ext_slot[g] = ns;
           sg.h_shapes[ns++] = sg.h_tasks[g];
         }
+      sg.slot_rows.assign(ns, 0);
       for (int32_t g = 0; g < G; ++g) {
         const int32_t sl = ext_slot[sg.row_ext[g]];
         sg.row_slot[g] = sl;
         sg.h_rowshape[g] = (uint32_t)sl | (sg.row_ext[g] == g ? kbg::kRowWriter : 0u);
+        sg.slot_rows[sl]++;
       }
       sg.n_slots = ns;
     } else {
@@ -1032,6 +1046,7 @@ struct Grouper {
       sg.h_rowshape = nullptr;
       sg.h_shapes = sg.h_tasks;
       sg.n_slots = G;
+      sg.slot_rows.clear();
     }
     return G;
   }

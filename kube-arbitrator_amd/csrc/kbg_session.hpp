@@ -264,6 +264,7 @@ struct Stage {
   std::vector<int32_t> row_slot;     // row -> its shape's slot
   uint32_t* h_rowshape = nullptr;    // full-scan: row -> slot | kRowWriter (inside h_up)
   TaskRec* h_shapes = nullptr;       // full-scan: the shape table (inside h_up; grouped: h_tasks)
+  std::vector<uint16_t> slot_rows;   // full-scan: rows of each slot (the kernel's run-length rows, FirstFitArgs.runs)
   uint32_t* h_info = nullptr;        // per slot: words covered | kInfoAnyBit | kCountIncompleteBit
   int32_t splits = 1;                // word parts of the launch (one info word per slot and part)
   std::vector<uint32_t> info_comb;   // splits > 1: the parts' info words combined per slot

@@ -488,7 +488,7 @@ extern "C" int32_t kbg_tool_firstfit_stamps(const kbg_snapshot* snap, const kbg_
       free_device(S);
       return -2;
     }
-  const int32_t per = kbg::firstfit_rows(rows);
+  const int32_t per = kbg::firstfit_geometry(rows, S.opts.full_scan != 0).rows;
   const int32_t n_wg = std::min((rows + per - 1) / per * sg.splits, max_wg);
   const bool ok = kbg::read_ff_stamps(out, n_wg) == hipSuccess;
   free_device(S);

@@ -24,7 +24,7 @@ def one(cid):
     f = FlatSnapshot(s.nodes, s.jobs, s.queues, s.others, fixture_tiers(fx))
     res = {"config": cid}
     for full in (1, 0):
-        for G in ((16, 64, 1024, 4096, 8192) if full else (16, 64, 256, 1024)):
+        for G in ((16, 64, 1024, 4096, 4174, 4655, 8192) if full else (16, 64, 256, 1024)):
             o = _abi.kbg_options()
             o.full_scan = full
             o.batch_tasks = 8192

@@ -28,7 +28,7 @@ def main(cid):
     f = FlatSnapshot(s.nodes, s.jobs, s.queues, s.others, fixture_tiers(fx))
     MAXWG = 8192
     buf = (ctypes.c_ulonglong * (MAXWG * 8))()
-    for full, G in ((1, 4655), (1, 8192), (0, 8192), (0, 1024)):
+    for full, G in ((1, 4174), (1, 4655), (1, 8192), (0, 8192), (0, 1024)):
         o = _abi.kbg_options()
         o.full_scan = full
         o.batch_tasks = 8192
