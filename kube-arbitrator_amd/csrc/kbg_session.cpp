@@ -3875,6 +3875,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       sg.row_shape.swap(b->st.row_shape);
       sg.row_ext.swap(b->st.row_ext);
       sg.row_slot.swap(b->st.row_slot);
+      sg.slot_rows.swap(b->st.slot_rows);
       G = b->G;
       b->G = -1;
     } else {
