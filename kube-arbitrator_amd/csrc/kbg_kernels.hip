@@ -21,7 +21,6 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <utility>
 
 #include "kbg_device.hpp"
@@ -107,11 +106,16 @@ constexpr int kSmallBatchRows = KBG_SMALL_BATCH_ROWS;  // launch_scan: batches u
 // Integer mode, no Releasing: rows J and J+1 together, their six compares
 // issued back to back into six SGPR pairs before the first scalar AND reads
 // one (a row's compares no longer wait on each other through VCC).
-template <int J>
+// WRITERS_ONLY (full-scan): only a row that writes its slot (bit J of
+// wmask) moves its masks to lane J; the other rows of a slot evaluate the
+// same inputs against the same table, their lists are the writer's
+// (Grouper::build), so they keep nothing — the compares are volatile, every
+// row is evaluated.
+template <int J, bool WRITERS_ONLY = false>
 __device__ __forceinline__ void scan_row_pair(const double (&q)[2][3], double ic, double im, double ig,
-                                              uint32_t (&keep)[4]) {
+                                              uint32_t (&keep)[4], uint32_t wmask = ~0u) {
   uint64_t a0, a1, a2, b0, b1, b2;
-  asm("v_cmp_gt_f64_e64 %0, %6, %9\n\t"
+  asm volatile("v_cmp_gt_f64_e64 %0, %6, %9\n\t"
       "v_cmp_gt_f64_e64 %1, %7, %10\n\t"
       "v_cmp_gt_f64_e64 %2, %8, %11\n\t"
       "v_cmp_gt_f64_e64 %3, %6, %12\n\t"
@@ -120,6 +124,27 @@ __device__ __forceinline__ void scan_row_pair(const double (&q)[2][3], double ic
       : "=&s"(a0), "=&s"(a1), "=&s"(a2), "=&s"(b0), "=&s"(b1), "=&s"(b2)
       : "v"(ic), "v"(im), "v"(ig), "v"(q[0][0]), "v"(q[0][1]), "v"(q[0][2]), "v"(q[1][0]), "v"(q[1][1]), "v"(q[1][2]));
   const uint64_t ma = a0 & a1 & a2, mb = b0 & b1 & b2;
+  if constexpr (WRITERS_ONLY) {
+    // the writer test and its branch on the scalar unit, in the asm: a C++
+    // `if` per row made the compiler keep one SGPR pair per row live across
+    // the word loop (and spill them)
+    asm volatile(
+        "s_bitcmp1_b32 %2, %7\n\t"
+        "s_cbranch_scc0 1f\n\t"
+        "v_writelane_b32 %0, %3, %7\n\t"
+        "v_writelane_b32 %1, %4, %7\n"
+        "1:\n\t"
+        "s_bitcmp1_b32 %2, %8\n\t"
+        "s_cbranch_scc0 2f\n\t"
+        "v_writelane_b32 %0, %5, %8\n\t"
+        "v_writelane_b32 %1, %6, %8\n"
+        "2:"
+        : "+v"(keep[0]), "+v"(keep[1])
+        : "s"(wmask), "s"((uint32_t)ma), "s"((uint32_t)(ma >> 32)), "s"((uint32_t)mb), "s"((uint32_t)(mb >> 32)),
+          "i"(J), "i"(J + 1)
+        : "scc");
+    return;
+  }
   asm("v_writelane_b32 %0, %2, %6\n\t"
       "v_writelane_b32 %1, %3, %6\n\t"
       "v_writelane_b32 %0, %4, %7\n\t"
@@ -130,9 +155,9 @@ __device__ __forceinline__ void scan_row_pair(const double (&q)[2][3], double ic
 
 // (integer mode, no Releasing: the next group's requests are read from LDS
 // while this group's compares run)
-template <int ROWS, int J, int GROUP>
+template <int ROWS, int J, int GROUP, bool WO>
 __device__ __forceinline__ void scan_rows_int(const double (*s_req)[3], const double (&q)[GROUP][3], double ic,
-                                              double im, double ig, uint32_t (&keep)[4], int nrows) {
+                                              double im, double ig, uint32_t (&keep)[4], int nrows, uint32_t wmask) {
   double qn[GROUP][3];
   if constexpr (J + GROUP < ROWS) {
 #pragma unroll
@@ -143,18 +168,20 @@ __device__ __forceinline__ void scan_rows_int(const double (*s_req)[3], const do
     }
   }
   [&]<int... U>(std::integer_sequence<int, U...>) {
-    (scan_row_pair<J + 2 * U>(*reinterpret_cast<const double(*)[2][3]>(&q[2 * U][0]), ic, im, ig, keep), ...);
+    (scan_row_pair<J + 2 * U, WO>(*reinterpret_cast<const double(*)[2][3]>(&q[2 * U][0]), ic, im, ig, keep, wmask),
+     ...);
   }(std::make_integer_sequence<int, GROUP / 2>{});
   if constexpr (J + GROUP < ROWS)
-    if (J + GROUP < nrows) scan_rows_int<ROWS, J + GROUP, GROUP>(s_req, qn, ic, im, ig, keep, nrows);
+    if (J + GROUP < nrows) scan_rows_int<ROWS, J + GROUP, GROUP, WO>(s_req, qn, ic, im, ig, keep, nrows, wmask);
 }
 
 // `nrows` (wave-uniform, <= ROWS): the rows of the block that are real; the
 // groups past it are skipped (a full-scan workgroup takes fewer rows than its
 // variant holds, firstfit_geometry).
-template <bool INT_MODE, bool REL_ZERO, int ROWS, int J = 0, int GROUP = kRowGroup>
+template <bool INT_MODE, bool REL_ZERO, int ROWS, int J = 0, int GROUP = kRowGroup, bool WO = false>
 __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, double im, double ig, double rc,
-                                          double rm, double rg, uint32_t (&keep)[4], int nrows = ROWS) {
+                                          double rm, double rg, uint32_t (&keep)[4], int nrows = ROWS,
+                                          uint32_t wmask = ~0u) {
   double q[GROUP][3];
 #pragma unroll
   for (int u = 0; u < GROUP; ++u) {
@@ -163,7 +190,7 @@ __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, d
     q[u][2] = s_req[J + u][2];
   }
   if constexpr (INT_MODE && REL_ZERO && GROUP % 2 == 0 && J == 0) {
-    scan_rows_int<ROWS, 0, GROUP>(s_req, q, ic, im, ig, keep, nrows);
+    scan_rows_int<ROWS, 0, GROUP, WO>(s_req, q, ic, im, ig, keep, nrows, wmask);
     return;
   } else if constexpr (INT_MODE && REL_ZERO && GROUP % 2 == 0) {
     [&]<int... U>(std::integer_sequence<int, U...>) {
@@ -175,7 +202,8 @@ __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, d
     }(std::make_integer_sequence<int, GROUP>{});
   }
   if constexpr (J + GROUP < ROWS)
-    if (J + GROUP < nrows) scan_rows<INT_MODE, REL_ZERO, ROWS, J + GROUP, GROUP>(s_req, ic, im, ig, rc, rm, rg, keep, nrows);
+    if (J + GROUP < nrows)
+      scan_rows<INT_MODE, REL_ZERO, ROWS, J + GROUP, GROUP, WO>(s_req, ic, im, ig, rc, rm, rg, keep, nrows, wmask);
 }
 
 template <bool INT_MODE, int ROWS>
@@ -301,91 +329,7 @@ constexpr int kFfGroup = INT_MODE ? 4 : 2;
 template <bool INT_MODE, int ROWS>
 constexpr int kFfGroupR = ROWS > 24 ? 2 : kFfGroup<INT_MODE>;
 
-// ---- rows from the scalar unit (SREQ: the shape table is in the kernel
-// arguments). A row's request is wave-uniform: instead of reading it from LDS
-// into every lane (a 24-B broadcast costs 6 LDS cycles per wave and row), the
-// wave scalar-loads the row's shape record from the arguments (rm: the rows'
-// slots, 4 per dword, bit 7 = the row writes its slot) and each compare takes
-// it as its one SGPR operand. The next group's records load while this
-// group's compares run.
-template <int J, int ROWS>
-__device__ __forceinline__ uint32_t rmap_get(const uint32_t (&rm)[ROWS / 4]) {
-  return (rm[J >> 2] >> ((J & 3) * 8)) & 0xffu;
-}
-template <int ROWS, int J>
-__device__ __forceinline__ void load_req(const FirstFitArgs& a, const uint32_t (&rm)[ROWS / 4], double (&q)[3]) {
-  const uint32_t sl = rmap_get<J, ROWS>(rm) & 0x7fu;
-  q[0] = a.inl[sl].req[0];
-  q[1] = a.inl[sl].req[1];
-  q[2] = a.inl[sl].req[2];
-}
-template <int ROWS, int J0, int GROUP>
-__device__ __forceinline__ void load_reqs(const FirstFitArgs& a, const uint32_t (&rm)[ROWS / 4], double (&q)[GROUP][3]) {
-  [&]<int... U>(std::integer_sequence<int, U...>) {
-    (load_req<ROWS, J0 + U>(a, rm, q[U]), ...);
-  }(std::make_integer_sequence<int, GROUP>{});
-}
-
-// Integer mode, no Releasing: rows J and J + 1, six compares against SGPR
-// requests. WRITERS_ONLY (full-scan): only a row that writes its slot moves
-// its mask to lane J; the other rows of a slot evaluate the same inputs
-// against the same table (their lists are the writer's, Grouper::build) and
-// keep nothing — the compares are volatile, every row is evaluated.
-template <int J, bool WRITERS_ONLY>
-__device__ __forceinline__ void scan_row_pair_s(const double (&q)[2][3], uint32_t wbits, double ic, double im,
-                                                double ig, uint32_t (&keep)[4]) {
-  uint64_t a0, a1, a2, b0, b1, b2;
-  asm volatile(
-      "v_cmp_gt_f64_e64 %0, %6, %9\n\t"
-      "v_cmp_gt_f64_e64 %1, %7, %10\n\t"
-      "v_cmp_gt_f64_e64 %2, %8, %11\n\t"
-      "v_cmp_gt_f64_e64 %3, %6, %12\n\t"
-      "v_cmp_gt_f64_e64 %4, %7, %13\n\t"
-      "v_cmp_gt_f64_e64 %5, %8, %14"
-      : "=&s"(a0), "=&s"(a1), "=&s"(a2), "=&s"(b0), "=&s"(b1), "=&s"(b2)
-      : "v"(ic), "v"(im), "v"(ig), "s"(q[0][0]), "s"(q[0][1]), "s"(q[0][2]), "s"(q[1][0]), "s"(q[1][1]), "s"(q[1][2]));
-  if (!WRITERS_ONLY || (wbits & 1u)) {
-    const uint64_t ma = a0 & a1 & a2;
-    asm("v_writelane_b32 %0, %2, %4\n\t"
-        "v_writelane_b32 %1, %3, %4"
-        : "+v"(keep[0]), "+v"(keep[1])
-        : "s"((uint32_t)ma), "s"((uint32_t)(ma >> 32)), "i"(J));
-  }
-  if (!WRITERS_ONLY || (wbits & 2u)) {
-    const uint64_t mb = b0 & b1 & b2;
-    asm("v_writelane_b32 %0, %2, %4\n\t"
-        "v_writelane_b32 %1, %3, %4"
-        : "+v"(keep[0]), "+v"(keep[1])
-        : "s"((uint32_t)mb), "s"((uint32_t)(mb >> 32)), "i"(J + 1));
-  }
-}
-
-template <bool INT_MODE, bool REL_ZERO, bool WRITERS_ONLY, int ROWS, int J, int GROUP>
-__device__ __forceinline__ void scan_rows_s(const FirstFitArgs& a, const uint32_t (&rm)[ROWS / 4],
-                                            const double (&q)[GROUP][3], double ic, double im, double ig, double rc,
-                                            double rmv, double rg, uint32_t (&keep)[4], int nrows) {
-  double qn[GROUP][3];
-  if constexpr (J + GROUP < ROWS) load_reqs<ROWS, J + GROUP, GROUP>(a, rm, qn);
-  if constexpr (INT_MODE && REL_ZERO && GROUP % 2 == 0) {
-    [&]<int... U>(std::integer_sequence<int, U...>) {
-      (scan_row_pair_s<J + 2 * U, WRITERS_ONLY>(*reinterpret_cast<const double(*)[2][3]>(&q[2 * U][0]),
-                                                (rmap_get<J + 2 * U, ROWS>(rm) >> 7) |
-                                                    ((rmap_get<J + 2 * U + 1, ROWS>(rm) >> 7) << 1),
-                                                ic, im, ig, keep),
-       ...);
-    }(std::make_integer_sequence<int, GROUP / 2>{});
-  } else {
-    [&]<int... U>(std::integer_sequence<int, U...>) {
-      (scan_row<INT_MODE, REL_ZERO, J + U>(q[U][0], q[U][1], q[U][2], ic, im, ig, rc, rmv, rg, keep), ...);
-    }(std::make_integer_sequence<int, GROUP>{});
-  }
-  if constexpr (J + GROUP < ROWS)
-    if (J + GROUP < nrows)
-      scan_rows_s<INT_MODE, REL_ZERO, WRITERS_ONLY, ROWS, J + GROUP, GROUP>(a, rm, qn, ic, im, ig, rc, rmv, rg, keep,
-                                                                           nrows);
-}
-
-template <bool INT_MODE, bool EARLY_EXIT, int ROWS, bool SREQ>
+template <bool INT_MODE, bool EARLY_EXIT, int ROWS>
 __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArgs a) {
   static_assert(ROWS % 8 == 0 && ROWS <= 2 * kFfWaves, "rows per workgroup");
   constexpr int RPW = (ROWS + kFfWaves - 1) / kFfWaves;  // rows a wave extracts (1 or 2)
@@ -493,16 +437,9 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
   const int lrow = lane < ROWS ? lane : 0;
   const int cls_l = s_cls[lrow];
   const uint32_t flags_l = s_flags[lrow];
-  // SREQ: every row's slot and writer bit in SGPRs (4 rows per dword), once
-  uint32_t rm[ROWS / 4];
-  if constexpr (SREQ) {
-    const uint32_t ml = s_map[lrow];
-    const uint32_t v = (ml & 0x7fu) | ((ml & kRowWriter) ? 0x80u : 0u);
-#pragma unroll
-    for (int d = 0; d < ROWS / 4; ++d)
-      rm[d] = __builtin_amdgcn_readlane(v, 4 * d) | (__builtin_amdgcn_readlane(v, 4 * d + 1) << 8) |
-              (__builtin_amdgcn_readlane(v, 4 * d + 2) << 16) | (__builtin_amdgcn_readlane(v, 4 * d + 3) << 24);
-  }
+  // full-scan: the rows that write their slot (the other rows of a slot
+  // evaluate the same inputs against the same table and keep nothing)
+  const uint32_t wmask = (uint32_t)__ballot(lane < ROWS && (s_map[lrow] & kRowWriter));
   // rounds are kFfMaxRound (a multiple of kFfWaves) words apart, so a wave's
   // words are c, c + kFfWaves, ... across rounds too; lanes >= ROWS load a
   // row's mask word they never use
@@ -525,31 +462,9 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
           __ballot(cur.valid && !(cur.rc == 0.0 && cur.rm == 0.0 && cur.rg == 0.0)) == 0ull;
       uint32_t keep[4] = {0u, 0u, 0u, 0u};
       uint64_t mr;
-      if constexpr (SREQ) {
-        constexpr int GR = 2;  // two rows' records in flight (12 SGPRs) while two rows compare
-        // the records are re-read for every word (scalar-cache hits): an
-        // opaque copy of the row map keeps the compiler from hoisting every
-        // row's record out of the word loop into (spilled) SGPRs
-        uint32_t rmw[ROWS / 4];
-#pragma unroll
-        for (int d = 0; d < ROWS / 4; ++d) {
-          rmw[d] = rm[d];
-          asm volatile("" : "+s"(rmw[d]));
-        }
-        double q0[GR][3];
-        load_reqs<ROWS, 0, GR>(a, rmw, q0);
-        if (rel_zero_wave) {
-          scan_rows_s<INT_MODE, true, !EARLY_EXIT, ROWS, 0, GR>(a, rmw, q0, cur.ic, cur.im, cur.ig, cur.rc, cur.rm,
-                                                                  cur.rg, keep, nrows);
-          mr = (flags_l & kRowRelZeroFits) ? ~0ull : 0ull;
-        } else {
-          scan_rows_s<INT_MODE, false, false, ROWS, 0, GR>(a, rmw, q0, cur.ic, cur.im, cur.ig, cur.rc, cur.rm, cur.rg,
-                                                            keep, nrows);
-          mr = (uint64_t)keep[2] | ((uint64_t)keep[3] << 32);
-        }
-      } else if (rel_zero_wave) {
-        scan_rows<INT_MODE, true, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm, cur.rg,
-                                                               keep, nrows);
+      if (rel_zero_wave) {
+        scan_rows<INT_MODE, true, ROWS, 0, kFfGroupR<INT_MODE, ROWS>, !EARLY_EXIT>(s_req, cur.ic, cur.im, cur.ig, cur.rc,
+                                                                              cur.rm, cur.rg, keep, nrows, wmask);
         mr = (flags_l & kRowRelZeroFits) ? ~0ull : 0ull;
       } else {
         scan_rows<INT_MODE, false, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm,
@@ -630,28 +545,17 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
   FF_STAMP(6);
 }
 
-template <bool INT_MODE, bool EARLY_EXIT, bool SREQ>
+template <bool INT_MODE, bool EARLY_EXIT>
 hipError_t launch_firstfit_rows(const FirstFitArgs& a, int variant, hipStream_t stream, hipEvent_t start,
                                 hipEvent_t stop) {
   const dim3 grid((a.G + a.rows - 1) / a.rows * a.splits), block(64 * kFfWaves);
   if (variant == 16)
-    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 16, SREQ>), grid, block, 0, stream, start, stop, 0,
-                          a);
+    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 16>), grid, block, 0, stream, start, stop, 0, a);
   else if (variant == 24)
-    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 24, SREQ>), grid, block, 0, stream, start, stop, 0,
-                          a);
+    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 24>), grid, block, 0, stream, start, stop, 0, a);
   else
-    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 32, SREQ>), grid, block, 0, stream, start, stop, 0,
-                          a);
+    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 32>), grid, block, 0, stream, start, stop, 0, a);
   return hipGetLastError();
-}
-template <bool INT_MODE, bool EARLY_EXIT>
-hipError_t launch_firstfit_mode(const FirstFitArgs& a, int variant, hipStream_t stream, hipEvent_t start,
-                                hipEvent_t stop) {
-  static const bool lds_rows = getenv("KBG_FF_LDS_ROWS") != nullptr;  // A/B: requests through LDS
-  // shapes in the arguments: rows come through the scalar unit
-  if (!a.shapes && !lds_rows) return launch_firstfit_rows<INT_MODE, EARLY_EXIT, true>(a, variant, stream, start, stop);
-  return launch_firstfit_rows<INT_MODE, EARLY_EXIT, false>(a, variant, stream, start, stop);
 }
 
 // One workgroup per CU at a time (16 waves, 80-128 VGPRs), so a launch of
@@ -680,10 +584,10 @@ hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t 
   if (a.rows <= 0 || a.rows > geo.variant) return hipErrorInvalidValue;  // the host sizes both (device_launch)
   // <.., false>: full-scan mode (every node of every row), <.., true>: production
   if (int_mode)
-    return a.early_exit ? launch_firstfit_mode<true, true>(a, geo.variant, stream, start, stop)
-                        : launch_firstfit_mode<true, false>(a, geo.variant, stream, start, stop);
-  return a.early_exit ? launch_firstfit_mode<false, true>(a, geo.variant, stream, start, stop)
-                      : launch_firstfit_mode<false, false>(a, geo.variant, stream, start, stop);
+    return a.early_exit ? launch_firstfit_rows<true, true>(a, geo.variant, stream, start, stop)
+                        : launch_firstfit_rows<true, false>(a, geo.variant, stream, start, stop);
+  return a.early_exit ? launch_firstfit_rows<false, true>(a, geo.variant, stream, start, stop)
+                      : launch_firstfit_rows<false, false>(a, geo.variant, stream, start, stop);
 }
 
 // ------------------------------------------------------- FitError counts

@@ -9,7 +9,5 @@ mkdir -p $O
 cd $R
 timeout -k 10 240 python kube-arbitrator_amd/tools/ff_bench.py ${CONFIG:-3} > $O/ff_bench.json 2> $O/ff_bench.err || { tail -20 $O/ff_bench.err; exit 1; }
 cat $O/ff_bench.json
-KBG_FF_LDS_ROWS=1 timeout -k 10 240 python kube-arbitrator_amd/tools/ff_bench.py ${CONFIG:-3} > $O/ff_bench_lds.json 2> $O/ff_bench_lds.err || { tail -20 $O/ff_bench_lds.err; exit 1; }
-cat $O/ff_bench_lds.json
 timeout -k 10 240 python kube-arbitrator_amd/tools/ff_stamps.py ${CONFIG:-3} > $O/ff_stamps.json 2> $O/ff_stamps.err || { tail -20 $O/ff_stamps.err; exit 1; }
 cat $O/ff_stamps.json
