@@ -24,8 +24,13 @@
 // allocate batch there (kbg_session.cpp), since the later rows of the batch
 // were scanned against the old mask.
 //
-// Not modelled (as in the rest of the device path): the podLister Filter case
-// of a pod naming a node it is missing from (vendor cache/node_info.go:692-702).
+// The podLister Filter (vendor cache/node_info.go:692-702: a pod whose
+// informer Spec.NodeName is the evaluated node but that the node's pods lack
+// is left out of that node's predicate) arises within a session only for a
+// holder a discarded statement's RemoveTask took off its node: aff_ok_node
+// evaluates that node with the holder's counts taken out (S.aff_filtered).
+// Tasks placed this session keep their informer Spec.NodeName "" (session.go
+// sets task.NodeName only), so the Filter always keeps them.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -162,7 +167,7 @@ void recompute_bit(Session& S, int32_t c, int32_t n) {
   const size_t idx = (size_t)c * S.W + (n >> 6);
   const uint64_t bit = 1ull << (n & 63);
   bool v = (S.h_class_mask_static[idx] & bit) != 0;
-  if (v && !S.panic_node[n]) v = ports_ok(S, c, n) && aff_ok(S, S.affm->st, c, n);
+  if (v && !S.panic_node[n]) v = ports_ok(S, c, n) && aff_ok_node(S, c, n);
   const bool old = (S.h_class_mask[idx] & bit) != 0;
   if (v == old) return;
   vc_mask_changed(S, c, n);
@@ -215,6 +220,32 @@ bool aff_ok(const Session& S, const AffState& st, int32_t c, int32_t n) {
     }
   }
   return true;
+}
+
+// The podLister's FilteredList(nodeInfo.Filter) (predicates.go:67-89) for
+// node n: a pod whose informer Spec.NodeName is n but that n's pods lack
+// (vendor cache/node_info.go:692-702) is not in the list n's predicate sees.
+// Within a session that is a holder a discarded statement's RemoveTask took
+// off its node (S.aff_filtered); its counts are taken out for n's own
+// evaluation and put back.
+bool aff_ok_node(Session& S, int32_t c, int32_t n) {
+  AffState& st = S.affm->st;
+  bool any = false;
+  for (const auto& [fn, t] : S.aff_filtered)
+    if (fn == n) {
+      aff_place(S, t, n, -1, st, false);
+      any = true;
+    }
+  const bool ok = aff_ok(S, st, c, n);
+  if (any)
+    for (const auto& [fn, t] : S.aff_filtered)
+      if (fn == n) aff_place(S, t, n, +1, st, false);
+  return ok;
+}
+
+void aff_refresh_node(Session& S, int32_t n) {
+  if (!S.has_aff || n < 0) return;
+  for (int32_t c = 0; c < S.n_classes; ++c) recompute_bit(S, c, n);
 }
 
 // One AllocatedStatus pod (task t) appears on (sign +1) or leaves (-1) node n
@@ -314,6 +345,10 @@ void aff_place(Session& S, int32_t t, int32_t n, int32_t sign, AffState& st, boo
   std::sort(full.begin(), full.end());
   full.erase(std::unique(full.begin(), full.end()), full.end());
   for (int32_t c : full) recompute_class(S, c);
+  // a node with filtered pods: its bits follow the counts without them (the
+  // domain-wide updates above keep or recompute it with them)
+  for (const auto& [fn, ft] : S.aff_filtered)
+    for (int32_t c = 0; c < S.n_classes; ++c) recompute_bit(S, c, fn);
 }
 
 // Builds the model and the counts of the pods allocated at open, and folds

@@ -106,16 +106,11 @@ constexpr int kSmallBatchRows = KBG_SMALL_BATCH_ROWS;  // launch_scan: batches u
 // Integer mode, no Releasing: rows J and J+1 together, their six compares
 // issued back to back into six SGPR pairs before the first scalar AND reads
 // one (a row's compares no longer wait on each other through VCC).
-// WRITERS_ONLY (full-scan): only a row that writes its slot (bit J of
-// wmask) moves its masks to lane J; the other rows of a slot evaluate the
-// same inputs against the same table, their lists are the writer's
-// (Grouper::build), so they keep nothing — the compares are volatile, every
-// row is evaluated.
-template <int J, bool WRITERS_ONLY = false>
+template <int J>
 __device__ __forceinline__ void scan_row_pair(const double (&q)[2][3], double ic, double im, double ig,
-                                              uint32_t (&keep)[4], uint32_t wmask = ~0u) {
+                                              uint32_t (&keep)[4]) {
   uint64_t a0, a1, a2, b0, b1, b2;
-  asm volatile("v_cmp_gt_f64_e64 %0, %6, %9\n\t"
+  asm("v_cmp_gt_f64_e64 %0, %6, %9\n\t"
       "v_cmp_gt_f64_e64 %1, %7, %10\n\t"
       "v_cmp_gt_f64_e64 %2, %8, %11\n\t"
       "v_cmp_gt_f64_e64 %3, %6, %12\n\t"
@@ -124,27 +119,6 @@ __device__ __forceinline__ void scan_row_pair(const double (&q)[2][3], double ic
       : "=&s"(a0), "=&s"(a1), "=&s"(a2), "=&s"(b0), "=&s"(b1), "=&s"(b2)
       : "v"(ic), "v"(im), "v"(ig), "v"(q[0][0]), "v"(q[0][1]), "v"(q[0][2]), "v"(q[1][0]), "v"(q[1][1]), "v"(q[1][2]));
   const uint64_t ma = a0 & a1 & a2, mb = b0 & b1 & b2;
-  if constexpr (WRITERS_ONLY) {
-    // the writer test and its branch on the scalar unit, in the asm: a C++
-    // `if` per row made the compiler keep one SGPR pair per row live across
-    // the word loop (and spill them)
-    asm volatile(
-        "s_bitcmp1_b32 %2, %7\n\t"
-        "s_cbranch_scc0 1f\n\t"
-        "v_writelane_b32 %0, %3, %7\n\t"
-        "v_writelane_b32 %1, %4, %7\n"
-        "1:\n\t"
-        "s_bitcmp1_b32 %2, %8\n\t"
-        "s_cbranch_scc0 2f\n\t"
-        "v_writelane_b32 %0, %5, %8\n\t"
-        "v_writelane_b32 %1, %6, %8\n"
-        "2:"
-        : "+v"(keep[0]), "+v"(keep[1])
-        : "s"(wmask), "s"((uint32_t)ma), "s"((uint32_t)(ma >> 32)), "s"((uint32_t)mb), "s"((uint32_t)(mb >> 32)),
-          "i"(J), "i"(J + 1)
-        : "scc");
-    return;
-  }
   asm("v_writelane_b32 %0, %2, %6\n\t"
       "v_writelane_b32 %1, %3, %6\n\t"
       "v_writelane_b32 %0, %4, %7\n\t"
@@ -155,9 +129,9 @@ __device__ __forceinline__ void scan_row_pair(const double (&q)[2][3], double ic
 
 // (integer mode, no Releasing: the next group's requests are read from LDS
 // while this group's compares run)
-template <int ROWS, int J, int GROUP, bool WO>
+template <int ROWS, int J, int GROUP>
 __device__ __forceinline__ void scan_rows_int(const double (*s_req)[3], const double (&q)[GROUP][3], double ic,
-                                              double im, double ig, uint32_t (&keep)[4], int nrows, uint32_t wmask) {
+                                              double im, double ig, uint32_t (&keep)[4], int nrows) {
   double qn[GROUP][3];
   if constexpr (J + GROUP < ROWS) {
 #pragma unroll
@@ -168,20 +142,18 @@ __device__ __forceinline__ void scan_rows_int(const double (*s_req)[3], const do
     }
   }
   [&]<int... U>(std::integer_sequence<int, U...>) {
-    (scan_row_pair<J + 2 * U, WO>(*reinterpret_cast<const double(*)[2][3]>(&q[2 * U][0]), ic, im, ig, keep, wmask),
-     ...);
+    (scan_row_pair<J + 2 * U>(*reinterpret_cast<const double(*)[2][3]>(&q[2 * U][0]), ic, im, ig, keep), ...);
   }(std::make_integer_sequence<int, GROUP / 2>{});
   if constexpr (J + GROUP < ROWS)
-    if (J + GROUP < nrows) scan_rows_int<ROWS, J + GROUP, GROUP, WO>(s_req, qn, ic, im, ig, keep, nrows, wmask);
+    if (J + GROUP < nrows) scan_rows_int<ROWS, J + GROUP, GROUP>(s_req, qn, ic, im, ig, keep, nrows);
 }
 
 // `nrows` (wave-uniform, <= ROWS): the rows of the block that are real; the
 // groups past it are skipped (a full-scan workgroup takes fewer rows than its
 // variant holds, firstfit_geometry).
-template <bool INT_MODE, bool REL_ZERO, int ROWS, int J = 0, int GROUP = kRowGroup, bool WO = false>
+template <bool INT_MODE, bool REL_ZERO, int ROWS, int J = 0, int GROUP = kRowGroup>
 __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, double im, double ig, double rc,
-                                          double rm, double rg, uint32_t (&keep)[4], int nrows = ROWS,
-                                          uint32_t wmask = ~0u) {
+                                          double rm, double rg, uint32_t (&keep)[4], int nrows = ROWS) {
   double q[GROUP][3];
 #pragma unroll
   for (int u = 0; u < GROUP; ++u) {
@@ -190,7 +162,7 @@ __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, d
     q[u][2] = s_req[J + u][2];
   }
   if constexpr (INT_MODE && REL_ZERO && GROUP % 2 == 0 && J == 0) {
-    scan_rows_int<ROWS, 0, GROUP, WO>(s_req, q, ic, im, ig, keep, nrows, wmask);
+    scan_rows_int<ROWS, 0, GROUP>(s_req, q, ic, im, ig, keep, nrows);
     return;
   } else if constexpr (INT_MODE && REL_ZERO && GROUP % 2 == 0) {
     [&]<int... U>(std::integer_sequence<int, U...>) {
@@ -202,8 +174,7 @@ __device__ __forceinline__ void scan_rows(const double (*s_req)[3], double ic, d
     }(std::make_integer_sequence<int, GROUP>{});
   }
   if constexpr (J + GROUP < ROWS)
-    if (J + GROUP < nrows)
-      scan_rows<INT_MODE, REL_ZERO, ROWS, J + GROUP, GROUP, WO>(s_req, ic, im, ig, rc, rm, rg, keep, nrows, wmask);
+    if (J + GROUP < nrows) scan_rows<INT_MODE, REL_ZERO, ROWS, J + GROUP, GROUP>(s_req, ic, im, ig, rc, rm, rg, keep, nrows);
 }
 
 template <bool INT_MODE, int ROWS>
@@ -319,7 +290,10 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
 // round in which every row's list is full (the rest of the table cannot
 // change it); full-scan mode evaluates every node for every row (SURVEY
 // §8(d)).
-constexpr int kFfWaves = 16;
+#ifndef KBG_FF_WAVES
+#define KBG_FF_WAVES 16  // experiment builds (tools/build_variants.sh) try 8
+#endif
+constexpr int kFfWaves = KBG_FF_WAVES;
 constexpr int kFfMaxRound = kFfRoundWords;  // words per round (LDS: 2 x 128 x ROWS x 8 B); a multiple of kFfWaves
 // rows whose requests are read from LDS together
 template <bool INT_MODE>
@@ -327,11 +301,18 @@ constexpr int kFfGroup = INT_MODE ? 4 : 2;
 // (32-row workgroups: 2 rows per group keep the longer unrolled row walk within
 // the register budget)
 template <bool INT_MODE, int ROWS>
+#ifdef KBG_FF_GROUP  // experiment builds (tools/build_variants.sh)
+constexpr int kFfGroupR = ROWS > 24 ? 2 : KBG_FF_GROUP;
+#else
 constexpr int kFfGroupR = ROWS > 24 ? 2 : kFfGroup<INT_MODE>;
+#endif
+#ifndef KBG_FF_WGS_PER_CU
+#define KBG_FF_WGS_PER_CU 1  // resident workgroups per CU the full-scan geometry plans for
+#endif
 
 template <bool INT_MODE, bool EARLY_EXIT, int ROWS>
-__global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArgs a) {
-  static_assert(ROWS % 8 == 0 && ROWS <= 2 * kFfWaves, "rows per workgroup");
+__global__ __launch_bounds__(64 * kFfWaves, kFfWaves / 4 * KBG_FF_WGS_PER_CU) void kbg_firstfit_kernel(FirstFitArgs a) {
+  static_assert(ROWS % 8 == 0 && ROWS <= 4 * kFfWaves, "rows per workgroup");
   constexpr int RPW = (ROWS + kFfWaves - 1) / kFfWaves;  // rows a wave extracts (1 or 2)
   __shared__ double s_req[ROWS][3];
   __shared__ int32_t s_cls[ROWS];
@@ -437,9 +418,6 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
   const int lrow = lane < ROWS ? lane : 0;
   const int cls_l = s_cls[lrow];
   const uint32_t flags_l = s_flags[lrow];
-  // full-scan: the rows that write their slot (the other rows of a slot
-  // evaluate the same inputs against the same table and keep nothing)
-  const uint32_t wmask = (uint32_t)__ballot(lane < ROWS && (s_map[lrow] & kRowWriter));
   // rounds are kFfMaxRound (a multiple of kFfWaves) words apart, so a wave's
   // words are c, c + kFfWaves, ... across rounds too; lanes >= ROWS load a
   // row's mask word they never use
@@ -463,8 +441,8 @@ __global__ __launch_bounds__(64 * kFfWaves) void kbg_firstfit_kernel(FirstFitArg
       uint32_t keep[4] = {0u, 0u, 0u, 0u};
       uint64_t mr;
       if (rel_zero_wave) {
-        scan_rows<INT_MODE, true, ROWS, 0, kFfGroupR<INT_MODE, ROWS>, !EARLY_EXIT>(s_req, cur.ic, cur.im, cur.ig, cur.rc,
-                                                                              cur.rm, cur.rg, keep, nrows, wmask);
+        scan_rows<INT_MODE, true, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm, cur.rg,
+                                                               keep, nrows);
         mr = (flags_l & kRowRelZeroFits) ? ~0ull : 0ull;
       } else {
         scan_rows<INT_MODE, false, ROWS, 0, kFfGroupR<INT_MODE, ROWS>>(s_req, cur.ic, cur.im, cur.ig, cur.rc, cur.rm,
@@ -572,7 +550,8 @@ FfGeometry firstfit_geometry(int32_t G, bool full_scan) {
     const int v = G <= 16 * kCUs ? 16 : G <= 24 * kCUs ? 24 : 32;
     return {v, v};
   }
-  int rows = (G + kCUs - 1) / kCUs;
+  const int slots = kCUs * KBG_FF_WGS_PER_CU;
+  int rows = (G + slots - 1) / slots;
   rows = std::min(32, std::max(2, (rows + 1) & ~1));
   return {rows <= 16 ? 16 : rows <= 24 ? 24 : 32, rows};
 }

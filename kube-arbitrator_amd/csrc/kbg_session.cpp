@@ -1276,7 +1276,7 @@ void refresh_mask_bit(Session& S, int32_t c, int32_t n) {
   if (v && !S.panic_node[n]) {
     for (int32_t w = 0; w < S.PW && v; ++w)
       v = (S.node_ports[(size_t)n * S.PW + w] & S.cls_conf[(size_t)c * S.PW + w]) == 0;
-    if (v && S.has_aff) v = kbg::aff_ok(S, S.affm->st, c, n);
+    if (v && S.has_aff) v = kbg::aff_ok_node(S, c, n);
   }
   if (v == ((S.h_class_mask[idx] & bit) != 0)) return;
   S.h_class_mask[idx] ^= bit;
@@ -3304,6 +3304,7 @@ void begin_cycle(Session& S) {
   for (int32_t t : S.nt_task) S.trun[t] = 1;
   if (S.has_dupkeys) S.t_detached.assign(S.n_tasks, 0);
   else S.t_detached.clear();
+  S.aff_filtered.clear();
   S.pend = S.pend_all;
   S.pend_off = S.pend_off_all;
   S.pend_len = S.pend_len_all;
@@ -5241,6 +5242,13 @@ struct Live {
       S.trun[v] = 1;
       if (S.t_pos[v] >= 0) vt_delta(S, 0, S.t_pos[v], 1.0, 0, 0);
       S.t_detached[v] = 0;
+      if (S.has_aff) {  // back among n's pods: n's predicate counts it again
+        const auto fi = std::find(S.aff_filtered.begin(), S.aff_filtered.end(), std::make_pair(n, v));
+        if (fi != S.aff_filtered.end()) {
+          S.aff_filtered.erase(fi);
+          kbg::aff_refresh_node(S, n);
+        }
+      }
       // back in node.Pods(): its host ports are used again (release_open_ports' reverse)
       const int32_t vs = S.tasks_in[v].spec;
       if (vs >= 0 && S.specs_in[vs].port_len > 0)
@@ -5316,6 +5324,10 @@ struct Live {
           if (S.t_pos[h] >= 0) vt_delta(S, 0, S.t_pos[h], 0, 0, 0);
         }
         S.t_detached[h] = 1;
+        if (S.has_aff && allocated_status(S.tstat[h])) {  // the podLister Filter now leaves it out of n's predicate
+          S.aff_filtered.emplace_back(n, h);
+          kbg::aff_refresh_node(S, n);
+        }
       } else {
         if (!o->ports.empty()) release_open_ports(S, n, o->ports.data(), (int32_t)o->ports.size());
         S.outsider_gone.insert(hk);

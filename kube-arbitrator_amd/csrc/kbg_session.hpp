@@ -393,6 +393,11 @@ struct Session {
   std::vector<int32_t> upd_nodes;             // nodes an update's events touched (kbg_session_update) ...
   bool upd_nodes_valid = false;               // ... set for the derive that follows them
   std::vector<uint8_t> t_detached;            // a statement discard's RemoveTask took the task's copy off its node
+  // (node, task): an AllocatedStatus pod whose spec names the node but that is
+  // missing from the node's pods (a detached holder); the podLister Filter
+  // leaves it out of that node's own pod-affinity predicate (vendor
+  // cache/node_info.go:692-702), every other node still counts it
+  std::vector<std::pair<int32_t, int32_t>> aff_filtered;
   std::vector<uint8_t> trun;                  // node-side copy still Running (an eviction makes it Releasing
                                               // for good: unevict's AddTask fails, node_info.go:101-106)
   std::vector<int32_t> task_node;             // node index of a task's NodeName (-1: not a session node)
@@ -592,6 +597,10 @@ void compile_static_predicates(Session& S, StaticHost* out);
 void setup_affinity(Session& S);
 void aff_place(Session& S, int32_t t, int32_t n, int32_t sign, AffState& st, bool update_bits);
 bool aff_ok(const Session& S, const AffState& st, int32_t c, int32_t n);
+// aff_ok of the session's live state with the podLister Filter of node n applied
+bool aff_ok_node(Session& S, int32_t c, int32_t n);
+// the pod-affinity bits of every class on node n (its filtered pods changed)
+void aff_refresh_node(Session& S, int32_t n);
 
 }  // namespace kbg
 

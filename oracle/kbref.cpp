@@ -1319,8 +1319,8 @@ struct Predicates {
   // (pkg/scheduler/plugins/predicates/predicates.go:185-198).
   // podLister.FilteredList(nodeInfo.Filter, Everything()) (predicates.go:67-89,
   // vendor cache/node_info.go:692-702): every AllocatedStatus task of every job
-  // as a pod whose Spec.NodeName is the task's NodeName, minus the pods that
-  // name this node but are missing from it.
+  // as a pod whose Spec.NodeName is the task's NodeName, minus the pods whose
+  // informer Spec.NodeName is this node but that are missing from its pods.
   std::vector<TaskInfo*> filtered_pods(NodeInfo* node) {
     std::vector<TaskInfo*> out;
     for (JobInfo* job : ssn->jobs)
@@ -1329,7 +1329,10 @@ struct Predicates {
         for (auto& t : kv.second.items) {
           TaskInfo* task = t.second;
           bool keep;
-          if (task->nodeName != node->node->name) keep = true;
+          // podFilter(task.Pod) (predicates.go:79): the informer pod's
+          // Spec.NodeName, which Allocate / Pipeline never change
+          // (session.go:218,260 set task.NodeName only)
+          if (task->pod->nodeName != node->node->name) keep = true;
           else {
             keep = false;
             for (auto& nt : node->tasks.items)
