@@ -6583,9 +6583,9 @@ kbg_status kbg_decision_actions_get(kbg_session* s, int32_t* out, int32_t cap, i
   return KBG_OK;
 }
 
-kbg_status kbg_session_reset(kbg_session* s) {
-  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
-  Session& S = s->s;
+namespace {
+// kbg_session_reset's body (also the tools' repeated sharded cycles)
+kbg_status session_reset(Session& S) {
   HIP_TRY(hipSetDevice(S.device));
   S.idle = S.idle0;
   S.rel = S.rel0;
@@ -6607,6 +6607,12 @@ kbg_status kbg_session_reset(kbg_session* s) {
   if (st != KBG_OK) return st;
   HIP_TRY(hipStreamSynchronize(S.stream));
   return KBG_OK;
+}
+}  // namespace
+
+kbg_status kbg_session_reset(kbg_session* s) {
+  if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
+  return session_reset(s->s);
 }
 
 kbg_status kbg_session_update(kbg_session* s, const kbg_event* events, int32_t n) {

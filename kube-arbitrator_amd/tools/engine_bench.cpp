@@ -283,14 +283,25 @@ struct CallbackIO final : HostIO {
   }
 };
 
-// stats of one rank's cycle for the caller: rounds, batches, mispredictions, truncations
-void tool_stats(const Session& S, int64_t* st) {
-  if (!st) return;
-  st[0] = S.stats.owner_rounds;
-  st[1] = S.stats.batches;
-  st[2] = S.stats.mispredictions;
-  st[3] = S.stats.truncations;
-  st[4] = S.stats.task_evaluations;
+// stats of one rank's cycle for the caller: rounds, batches, mispredictions,
+// truncations, task evaluations; with `times` also (ns) allocate, engine,
+// resolve, device round trips, collectives, and the scan launches
+void tool_stats(const Session& S, int64_t* st, int64_t* times = nullptr) {
+  if (st) {
+    st[0] = S.stats.owner_rounds;
+    st[1] = S.stats.batches;
+    st[2] = S.stats.mispredictions;
+    st[3] = S.stats.truncations;
+    st[4] = S.stats.task_evaluations;
+  }
+  if (times) {
+    times[0] = (int64_t)(S.stats.allocate_ms * 1e6);
+    times[1] = (int64_t)(S.stats.engine_ms * 1e6);
+    times[2] = (int64_t)(S.stats.resolve_ms * 1e6);
+    times[3] = (int64_t)(S.stats.device_ms * 1e6);
+    times[4] = (int64_t)(S.stats.exchange_ms * 1e6);
+    times[5] = S.stats.scan_launches;
+  }
 }
 
 }  // namespace
@@ -382,9 +393,20 @@ struct DeviceLocalIO final : ShardIO {
 };
 }  // namespace
 
+extern "C" int32_t kbg_tool_sharded_allocate_device_t(const kbg_snapshot* snap, const kbg_options* o, int32_t R,
+                                                      int32_t device, kbg_decision* out, int32_t cap, int32_t* n_out,
+                                                      int64_t* stats, int64_t* times, int32_t cycles);
 extern "C" int32_t kbg_tool_sharded_allocate_device(const kbg_snapshot* snap, const kbg_options* o, int32_t R,
                                                     int32_t device, kbg_decision* out, int32_t cap, int32_t* n_out,
                                                     int64_t* stats) {
+  return kbg_tool_sharded_allocate_device_t(snap, o, R, device, out, cap, n_out, stats, nullptr, 1);
+}
+// The same, `cycles` allocate cycles in a row (each on the sessions reset to
+// the snapshot), the last one's log and stats returned; `times` (6 per rank,
+// tool_stats) of the last cycle.
+extern "C" int32_t kbg_tool_sharded_allocate_device_t(const kbg_snapshot* snap, const kbg_options* o, int32_t R,
+                                                      int32_t device, kbg_decision* out, int32_t cap, int32_t* n_out,
+                                                      int64_t* stats, int64_t* times, int32_t cycles) {
   LocalHub hub(R);
   std::vector<kbg_status> res(R, KBG_OK);
   std::vector<std::string> err(R);
@@ -416,8 +438,17 @@ extern "C" int32_t kbg_tool_sharded_allocate_device(const kbg_snapshot* snap, co
         Session& S = *sess[r];
         (void)hipSetDevice(S.device);
         DeviceLocalIO io(hub, r);
-        kbg_status st = allocate_sharded(S, io, out + (size_t)r * cap, cap, n_out + r);
-        tool_stats(S, stats ? stats + 5 * r : nullptr);
+        kbg_status st = KBG_OK;
+        for (int32_t c = 0; c < std::max(1, cycles) && st == KBG_OK; ++c) {
+          if (c > 0) {
+            st = session_reset(S);
+            hub.bar.arrive_and_wait();  // every rank reset before any starts the next cycle
+            if (st != KBG_OK) break;
+          }
+          S.stats = kbg_stats{};
+          st = allocate_sharded(S, io, out + (size_t)r * cap, cap, n_out + r);
+        }
+        tool_stats(S, stats ? stats + 5 * r : nullptr, times ? times + 6 * r : nullptr);
         res[r] = st;
         err[r] = g_err;
       });
