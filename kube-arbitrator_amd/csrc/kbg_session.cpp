@@ -4430,12 +4430,19 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
   kbg::Stage& sg = S.stages[0];
   kbg_status result = KBG_OK;
 
-  // rank 0: the ordering engine; the others replay its committed outcomes
+  // rank 0: the ordering engine; every rank replays the committed outcomes
+  // (rank 0 into a truth engine a cut restarts its predictor from, as the
+  // single-rank committer does: no checkpoint copies, no replay of a batch
+  // prefix)
   Engine E = first ? S.init : live_engine(S);
+  Engine E_truth;
   std::unique_ptr<Predictor> pr;
   std::unique_ptr<Replayer> rp;
   if (me == 0) {
+    E_truth = E;
     pr.reset(new Predictor(S, E, failed.get()));
+    pr->truth_mode = true;
+    rp.reset(new Replayer(S, E_truth, sched_getcpu()));
     pr->start(sched_getcpu());
   } else {
     rp.reset(new Replayer(S, E));
@@ -4693,6 +4700,25 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
       }
     }
     if (lg) lg->push(std::move(items));
+    // Shapes that fit nowhere from now on, learned from the exchange every
+    // rank already holds (the predictor predicts their later tasks failed
+    // instead of each first failure cutting a batch): no rank fits the row
+    // (availability 0), or every rank that did failed it at a task before
+    // the cut (a rank fails a row only on a complete list; commits past the
+    // cut are rolled back, so later failures do not count). Monotone: Idle,
+    // Releasing and the pod cap only shrink during allocate.
+    for (int32_t g = 0; g < G; ++g) {
+      const int32_t sh = sg.row_shape[g];
+      bool nowhere = avail[g] == 0;
+      if (!nowhere) {
+        nowhere = true;
+        for (uint32_t m = avail[g]; m && nowhere; m &= m - 1) {
+          const uint32_t f = fail_at[(size_t)g * R + __builtin_ctz(m)];
+          nowhere = f != kNone && f < (uint32_t)cut;
+        }
+      }
+      if (nowhere) failed[sh].store(1, std::memory_order_relaxed);
+    }
     rollback_from(cut);
     if (rp) {
       std::vector<std::pair<int32_t, char>> v(cut);
@@ -4717,11 +4743,9 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
     if (trunc) S.stats.truncations++;
     if (me == 0) {
       if (mispred) {
-        pr->rollback(++cur_epoch, cur, seg + cut, [&] {
-          std::vector<char> a(cur->bpred.begin(), cur->bpred.begin() + seg);  // earlier segments: as predicted
-          a.insert(a.end(), bactual.begin(), bactual.begin() + cut);
-          return a;
-        }(), nullptr);
+        rp->wait_idle();  // the truth engine holds every outcome up to the cut
+        if (!rp->error.empty()) return abort(fail(KBG_E_INVALID, rp->error));
+        pr->rollback_truth(++cur_epoch, &E_truth, cur, nullptr);
         cur = nullptr;
       } else if (trunc) {
         seg += end;  // the rest of the batch, rescanned against the commits so far
@@ -4737,7 +4761,7 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
   if (kbg_status st = compute_fit_deltas(S, dec, dec_old, dec_oldp, last); st != KBG_OK) return st;
   S.stats.task_evaluations += logged;
   if (rp && !rp->error.empty()) return fail(KBG_E_INVALID, rp->error);
-  S.fin = E;
+  S.fin = me == 0 ? E_truth : E;  // the committed outcomes' engine state
   if (pr) {
     S.stats.engine_ms = pr->engine_ms;
     S.stats.replayed = pr->replayed;
