@@ -3027,6 +3027,11 @@ struct Pipe {
   std::deque<Batch*> raw;      // predicted, waiting for the builder (allocate_cycle)
   bool building = false;       // the builder holds a batch
   static constexpr size_t kDepth = 3;
+  // how far the predictor may run ahead: batches queued and tasks per batch.
+  // Past the first cut (the contended part of a cycle) every prediction
+  // beyond the next cut is work thrown away, so the committer narrows both
+  std::atomic<int32_t> depth{(int32_t)kDepth};
+  std::atomic<int32_t> kmax{INT32_MAX};
 };
 // Smallest batch the predictor hands over early to a waiting committer (the
 // first batch of an epoch, and near the end of the cycle); KBG_MIN_EMIT overrides.
@@ -3527,7 +3532,8 @@ struct Predictor {
       {
         std::unique_lock<std::mutex> lk(P.mu);
         P.cv.wait(lk, [&] {
-          return P.stop || P.rollback || (!exhausted && P.ready.size() + P.raw.size() < Pipe::kDepth);
+          return P.stop || P.rollback ||
+                 (!exhausted && P.ready.size() + P.raw.size() < (size_t)P.depth.load(std::memory_order_relaxed));
         });
         if (P.stop) return;
         if (P.rollback && P.rb_truth) {  // the engine state at the cut, kept by the truth replayer
@@ -3587,7 +3593,8 @@ struct Predictor {
       const size_t emit_at = restarted ? 64 : (size_t)min_emit();
       restarted = false;
       bool abandoned = false;
-      while ((int32_t)b->bt.size() < S.K) {
+      const int32_t kcap = std::min(S.K, P.kmax.load(std::memory_order_relaxed));
+      while ((int32_t)b->bt.size() < kcap) {
         const int32_t t = ops.next_task();
         if (t < 0) break;
         const bool p = !failed[S.task_shape[t]].load(std::memory_order_relaxed);
@@ -3920,6 +3927,15 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     return !(e && e[0] == '0');
   }();
   const bool reuse_ok = !S.opts.full_scan && !S.comm && !S.has_aff && !no_reuse;
+  // the predictor's run-ahead past the first cut (Pipe::depth / kmax; 0 = unchanged)
+  static const int32_t cont_depth = [] {
+    const char* e = getenv("KBG_CONT_DEPTH");
+    return e ? atoi(e) : 0;
+  }();
+  static const int32_t cont_batch = [] {
+    const char* e = getenv("KBG_CONT_BATCH");
+    return e ? atoi(e) : 0;
+  }();
   bool reuse = false;
   // From the first cut on (the contended part of the cycle) every batch
   // resolves against the latest stage, and a rescan covers the rest of the
@@ -4189,6 +4205,8 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       if ((st = device_drop(S, other)) != KBG_OK) return abort(st);  // nxt was predicted before the cut
       const bool will_reuse = reuse_ok && !aff_cut;
       contended = will_reuse;
+      if (cont_depth > 0) pr.P.depth.store(cont_depth, std::memory_order_relaxed);
+      if (cont_batch > 0) pr.P.kmax.store(cont_batch, std::memory_order_relaxed);
       if (will_reuse) {  // before the predictor restarts: it reads the failed shapes
         // a batch that resolved against an earlier batch's stage keeps that
         // stage's map (its own entries built no rows); otherwise the stage's

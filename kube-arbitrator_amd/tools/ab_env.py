@@ -24,9 +24,12 @@ def main():
                                  capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
             d = json.loads(out.stdout.strip().splitlines()[-1])
             fs = d.get("full_scan_mode", {})
-            r = (round(d["p50_cycle_ms"], 2), round(fs.get("p50_cycle_ms", 0.0), 2))
+            bd = d.get("production_mode", {}).get("breakdown", {})
+            r = (round(d["p50_cycle_ms"], 2), round(fs.get("p50_cycle_ms", 0.0), 2), round(bd.get("host_engine_ms", 0), 2),
+                 round(bd.get("host_resolve_ms", 0), 2), bd.get("mispredictions"))
             res.setdefault(spec or "default", []).append(r)
-            print(f"{spec or 'default':40s} prod {r[0]:.2f} ms  full {r[1]:.2f} ms", flush=True)
+            print(f"{spec or 'default':40s} prod {r[0]:.2f} ms  full {r[1]:.2f} ms  engine {r[2]:.2f}  resolve {r[3]:.2f}"
+                  f"  cuts {r[4]}", flush=True)
     print(json.dumps(res))
 
 
