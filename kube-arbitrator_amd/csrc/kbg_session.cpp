@@ -299,24 +299,63 @@ struct EngineProfile {
 };
 inline uint64_t cycles() { return __builtin_readcyclecounter(); }
 
+// The session state the engine reads on every step, copied once per engine
+// thread: pointers to the arrays and the scalars. The Session object's own
+// cache lines also hold fields the committer and logger threads write during
+// a cycle (stamps, statistics, the decision log's vector), so reading the
+// arrays through it would keep pulling those lines across cores.
+struct EngineView {
+  const int32_t *pend, *pend_off, *pend_len, *job_by_frank, *joff, *job_min, *job_queue, *queue_rank, *job_frank;
+  const uint32_t* job_prank;
+  const Res *treq, *q_deserved;
+  const char* q_has_attr;
+  const int32_t* job_chain;
+  int32_t n_job_chain, n_queues;
+  Res drf_total;
+  bool has_drf, has_prop, queue_order_prop, heap_go111, job_chain_pgd;
+  explicit EngineView(const Session& S)
+      : pend(S.pend.data()), pend_off(S.pend_off.data()), pend_len(S.pend_len.data()),
+        job_by_frank(S.job_by_frank.data()), joff(S.joff.data()), job_min(S.job_min.data()),
+        job_queue(S.job_queue.data()), queue_rank(S.queue_rank.data()), job_frank(S.job_frank.data()),
+        job_prank(S.job_prank.data()), treq(S.treq.data()), q_deserved(S.q_deserved.data()),
+        q_has_attr(S.q_has_attr.data()), job_chain(S.job_chain.data()), n_job_chain((int32_t)S.job_chain.size()),
+        n_queues(S.n_queues), drf_total(S.drf_total), has_drf(S.has_drf), has_prop(S.has_prop),
+        queue_order_prop(S.queue_order_prop), heap_go111(S.heap_go111), job_chain_pgd(S.job_chain_pgd) {}
+};
+
 struct Ops {
   const Session& S;
   Engine& E;
   EngineProfile* prof = nullptr;
+  alignas(64) const EngineView V;
+  Ops(const Session& s, Engine& e, EngineProfile* p = nullptr) : S(s), E(e), prof(p), V(s) {}
 
-  bool job_ready(int32_t j) const { return E.jready[j] >= S.job_min[j]; }
+  bool job_ready(int32_t j) const { return E.jready[j] >= V.job_min[j]; }
 
   // Session.JobOrderFn (session_plugins.go:196-221) over the configured tiers
-  // is the order of kbg_session.hpp JobKey keys, built by make_job_key.
+  // is the order of kbg_session.hpp JobKey keys, built by make_job_key (the
+  // same key from the view here).
+  kbg::JobKey job_key(int32_t j) const {
+    if (V.job_chain_pgd) {  // the default tiers' chain (priority, gang, drf), without the loop
+      const bool ready = E.jready[j] >= V.job_min[j];
+      uint64_t u;
+      __builtin_memcpy(&u, &E.jshare[j], 8);
+      const uint64_t lo = ready ? (u & ~(1ull << 63)) : 0;  // fields after a non-ready gang are zero
+      kbg::JobKey k = ((kbg::JobKey)V.job_prank[j] << 1) | (ready ? 1u : 0u);
+      k = (k << 63) | lo;
+      return (k << 32) | (uint32_t)V.job_frank[j];
+    }
+    return make_job_key(S, E, j);
+  }
   // Session.QueueOrderFn (session_plugins.go:223-245; proportion.go:146-159):
   // share, then UID. With proportion on, E.qrank holds every queue's position
   // in that order (maintained by reorder_queue), so a compare is two loads.
   bool queue_less_slow(int32_t a, int32_t b) const {
-    if (S.queue_order_prop) {
+    if (V.queue_order_prop) {
       const double sa = E.qshare[a], sb = E.qshare[b];
       if (sa != sb) return sa < sb;
     }
-    return S.queue_rank[a] < S.queue_rank[b];
+    return V.queue_rank[a] < V.queue_rank[b];
   }
   bool queue_less(int32_t a, int32_t b) const { return E.qrank[a] < E.qrank[b]; }
   void reorder_queue(int32_t q) {  // q's share changed: move it to its new position
@@ -337,8 +376,8 @@ struct Ops {
   }
   // proportion.go:188-193
   bool overused(int32_t q) const {
-    if (!S.has_prop || !S.q_has_attr[q]) return false;
-    return kbg::res_le(S.q_deserved[q], E.qalloc[q]);
+    if (!V.has_prop || !V.q_has_attr[q]) return false;
+    return kbg::res_le(V.q_deserved[q], E.qalloc[q]);
   }
   // The queue heap is a literal container/heap: it holds one entry per job
   // and entries keep stale keys, so its layout decides the order.
@@ -349,7 +388,7 @@ struct Ops {
     int32_t* h = E.qheap.data();
     const int n = E.qlen++;
     h[n] = q;
-    h[n + 1] = S.n_queues;
+    h[n + 1] = V.n_queues;
     rank_heap_up(h, n, E.qrank.data());
   }
   int32_t qpop() {  // Pop: swap(0, n-1), down(0, n-1), take h[n-1]
@@ -357,8 +396,8 @@ struct Ops {
     const int n = --E.qlen;
     const int32_t q = h[0];
     h[0] = h[n];
-    h[n] = S.n_queues;
-    rank_heap_down(h, n, E.qrank.data(), S.heap_go111);
+    h[n] = V.n_queues;
+    rank_heap_down(h, n, E.qrank.data(), V.heap_go111);
     return q;
   }
   // Per-queue job heaps. A job's key changes only while it is popped (drf and
@@ -367,9 +406,9 @@ struct Ops {
   // sequence does not depend on the heap layout. allocate.go pops
   // the job, runs its tasks and pushes it back; here the job stays at the
   // root meanwhile and is re-sifted (success) or removed (no task fitted).
-  void jfix_top(int32_t q, kbg::JobKey x) { job_heap_down(E.jheap.data() + S.joff[q], E.jlen[q], x); }
+  void jfix_top(int32_t q, kbg::JobKey x) { job_heap_down(E.jheap.data() + V.joff[q], E.jlen[q], x); }
   void jremove_top(int32_t q) {
-    kbg::JobKey* h = E.jheap.data() + S.joff[q];
+    kbg::JobKey* h = E.jheap.data() + V.joff[q];
     const int n = --E.jlen[q];
     const kbg::JobKey x = h[n];
     h[n] = kbg::kJobKeySentinel;
@@ -382,7 +421,7 @@ struct Ops {
     for (;;) {
       if (E.in_job) {
         const int32_t j = E.cur_j;
-        if (E.cursor[j] < S.pend_len[j]) return S.pend[S.pend_off[j] + E.cursor[j]++];
+        if (E.cursor[j] < V.pend_len[j]) return V.pend[V.pend_off[j] + E.cursor[j]++];
         jremove_top(E.cur_q);  // no task of the job fitted: the job is not pushed back
         qpush(E.cur_q);        // allocate.go:173-174
         E.in_job = false;
@@ -394,7 +433,7 @@ struct Ops {
       if (prof) prof->qpop += cycles() - c0;
       if (overused(q)) continue;     // :71-74
       if (E.jlen[q] == 0) continue;  // :78-81
-      E.cur_j = S.job_by_frank[kbg::job_key_frank(E.jheap[S.joff[q]])];  // :85 jobs.Pop()
+      E.cur_j = V.job_by_frank[kbg::job_key_frank(E.jheap[V.joff[q]])];  // :85 jobs.Pop()
       E.cur_q = q;
       E.in_job = true;
     }
@@ -406,23 +445,23 @@ struct Ops {
     if (!success) return;
     uint64_t c0 = prof ? cycles() : 0;
     const int32_t j = E.cur_j, q = E.cur_q;
-    const Res& r = S.treq[t];
-    if (S.has_drf) {
+    const Res& r = V.treq[t];
+    if (V.has_drf) {
       kbg::res_add(E.jalloc[j], r);
-      E.jshare[j] = share_of(E.jalloc[j], S.drf_total);
+      E.jshare[j] = share_of(E.jalloc[j], V.drf_total);
     }
-    if (S.has_prop) {
-      const int32_t jq = S.job_queue[j];
+    if (V.has_prop) {
+      const int32_t jq = V.job_queue[j];
       kbg::res_add(E.qalloc[jq], r);
-      E.qshare[jq] = share_of(E.qalloc[jq], S.q_deserved[jq]);
-      if (S.queue_order_prop) reorder_queue(jq);
+      E.qshare[jq] = share_of(E.qalloc[jq], V.q_deserved[jq]);
+      if (V.queue_order_prop) reorder_queue(jq);
     }
     E.jready[j]++;
-    const kbg::JobKey key = make_job_key(S, E, j);
+    const kbg::JobKey key = job_key(j);
     uint64_t c1 = prof ? cycles() : 0;
     // :164-168 jobs.Push(job): the popped job is still the root here; an
     // unchanged key (e.g. a gang job short of MinAvailable) leaves the heap as is
-    if (key != E.jheap[S.joff[q]]) jfix_top(q, key);
+    if (key != E.jheap[V.joff[q]]) jfix_top(q, key);
     uint64_t c2 = prof ? cycles() : 0;
     qpush(q);     // :174
     E.in_job = false;
@@ -2998,6 +3037,14 @@ struct SpinCV {
   }
 };
 
+// A shape is known to fit nowhere (the committer's side of the flags the
+// predictor reads every step): store only when the flag is still clear, so
+// the line stays shared in the predictor's cache instead of being
+// invalidated by every failed task.
+inline void mark_failed(std::atomic<uint8_t>* f, int32_t sh) {
+  if (!f[sh].load(std::memory_order_relaxed)) f[sh].store(1, std::memory_order_relaxed);
+}
+
 struct Batch {
   std::vector<int32_t> bt;
   std::vector<char> bpred;
@@ -3525,6 +3572,7 @@ struct Predictor {
     auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     pin_near(committer_cpu);
     Ops ops{S, E, prof.on ? &prof : nullptr};
+    const int32_t* const tshape = S.task_shape.data();  // (not through the Session's lines, EngineView)
     bool exhausted = false, restarted = false;
     for (;;) {
       Batch* b = nullptr;
@@ -3597,7 +3645,7 @@ struct Predictor {
       while ((int32_t)b->bt.size() < kcap) {
         const int32_t t = ops.next_task();
         if (t < 0) break;
-        const bool p = !failed[S.task_shape[t]].load(std::memory_order_relaxed);
+        const bool p = !failed[tshape[t]].load(std::memory_order_relaxed);
         b->bt.push_back(t);
         b->bpred.push_back(p);
         ops.apply(t, p);
@@ -3905,7 +3953,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   // decides every task).
   auto learn_failed = [&](const kbg::Stage& g) {
     for (int32_t r = 0; r < g.G; ++r)
-      if (row_fits_nowhere(g, r)) failed[g.row_shape[r]].store(1, std::memory_order_relaxed);
+      if (row_fits_nowhere(g, r)) mark_failed(failed.get(), g.row_shape[r]);
   };
   // opt-in cycle counters of the in-order commit (KBG_PROFILE_RESOLVE=1):
   // candidate walk, host mirror, decision log, whole loop
@@ -3975,7 +4023,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       if (row_rep[r] < 0 || failed[sh].load(std::memory_order_relaxed)) continue;
       int32_t node = -1, kind = 0;
       if (rs.resolve(r, row_rep[r], &node, &kind) == RES_OK && node < 0)
-        failed[sh].store(1, std::memory_order_relaxed);
+        mark_failed(failed.get(), sh);
     }
   };
   int si = 0;
@@ -4157,7 +4205,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
           rcyc[2] += cycles() - c2;
         }
       } else {
-        failed[S.task_shape[t]].store(1, std::memory_order_relaxed);
+        mark_failed(failed.get(), S.task_shape[t]);
         const LogItem it{t, -1, 0, false, true, false, Res{}};
         if (lg) items.push_back(it);
         else log_one(it);
@@ -4707,7 +4755,7 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
       LogItem it{t, ok ? (int32_t)(win[i] >> 1) : -1, ok && (win[i] & 1u) ? KBG_KIND_PIPELINE : KBG_KIND_ALLOCATE,
                  ok, own == me, own == me && pos_dup[i], own == me ? pos_old[i] : Res{}};
       bactual[i] = ok;
-      if (!ok) failed[S.task_shape[t]].store(1, std::memory_order_relaxed);
+      if (!ok) mark_failed(failed.get(), S.task_shape[t]);
       if (lg) items.push_back(it);
       else log_one(it, pos_oldp.data() + (size_t)i * S.PW);
       if (ok != (bool)bpred[i]) {
@@ -4735,7 +4783,7 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
           nowhere = f != kNone && f < (uint32_t)cut;
         }
       }
-      if (nowhere) failed[sh].store(1, std::memory_order_relaxed);
+      if (nowhere) mark_failed(failed.get(), sh);
     }
     rollback_from(cut);
     if (rp) {
