@@ -607,7 +607,7 @@ def main():
                 "truncations": s2.truncations, "replayed": s2.replayed, "host_engine_ms": s2.engine_ms,
                 "host_resolve_ms": s2.resolve_ms, "device_roundtrip_ms": s2.device_ms,
                 "delta_writeback_ms": s2.delta_ms, "exchange_ms": s2.exchange_ms, "shards": s2.shards,
-                "owner_rounds": s2.owner_rounds,
+                "owner_rounds": s2.owner_rounds, "refresh_scans": s2.refresh_scans,
                 "cycle_ms": s2.allocate_ms}
 
     line = {

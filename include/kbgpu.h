@@ -346,6 +346,8 @@ typedef struct kbg_stats {
   int64_t owner_rounds;      /* owner-resolve (sharded allocate): exchange rounds over all batches */
   int64_t reused_batches;    /* batches resolved against an earlier scan's candidate lists after a cut
                                 (grouped mode: no device round trip) */
+  int64_t refresh_scans;     /* contended allocate: scans of every live shape launched beside the in-order
+                                commit once it had re-checked enough nodes touched since its lists' scan (ABI 11) */
 } kbg_stats;
 
 typedef struct kbg_session kbg_session;

@@ -260,27 +260,30 @@ constexpr int32_t kJobHeapPad = 3;  // sentinel slots past a job heap's capacity
 // Go's swap-based up/down: the element being moved is one side of every
 // compare, so swapping it step by step or writing it once at the end gives
 // the same array.
-inline void rank_heap_up(int32_t* h, int j, const int32_t* rk) {
+// `rk(q)`: the rank of queue id q (a table, or nibbles of a register).
+template <class RK>
+inline void rank_heap_up(int32_t* h, int j, RK rk) {
   const int32_t x = h[j];
-  const int32_t rx = rk[x];
+  const int32_t rx = rk(x);
   while (j > 0) {
     const int p = (j - 1) / 2;
-    if (!(rx < rk[h[p]])) break;
+    if (!(rx < rk(h[p]))) break;
     h[j] = h[p];
     j = p;
   }
   h[j] = x;
 }
-// h[n] holds the sentinel queue id (rank INT32_MAX): never chosen as a child.
-inline void rank_heap_down(int32_t* h, int n, const int32_t* rk, bool go111) {
+// h[n] holds the sentinel queue id (the largest rank): never chosen as a child.
+template <class RK>
+inline void rank_heap_down(int32_t* h, int n, RK rk, bool go111) {
   if (n <= 1) return;
   const int32_t x = h[0];
-  const int32_t rx = rk[x];
+  const int32_t rx = rk(x);
   int i = 0;
   for (;;) {
     const int j1 = 2 * i + 1;
     if (j1 >= n) break;
-    const int32_t r1 = rk[h[j1]], r2 = rk[h[j1 + 1]];
+    const int32_t r1 = rk(h[j1]), r2 = rk(h[j1 + 1]);
     // go1.11: right child when !Less(j1, j2) (r2 <= r1); later: when Less(j2, j1)
     const bool right = go111 ? (r2 <= r1) : (r2 < r1);
     const int j = j1 + (right ? 1 : 0);
@@ -358,21 +361,27 @@ struct Ops {
     return V.queue_rank[a] < V.queue_rank[b];
   }
   bool queue_less(int32_t a, int32_t b) const { return E.qrank[a] < E.qrank[b]; }
+  static constexpr int32_t kPackedQueues = 15;  // qrank_pk holds ids 0..14 and the sentinel (nibble 15)
+  void set_rank(int32_t q, int32_t pos) {
+    E.qrank[q] = pos;
+    if (V.n_queues <= kPackedQueues)
+      E.qrank_pk = (E.qrank_pk & ~(15ull << (4 * q))) | ((uint64_t)pos << (4 * q));
+  }
   void reorder_queue(int32_t q) {  // q's share changed: move it to its new position
     int32_t pos = E.qrank[q];
     const int32_t Q = (int32_t)E.qorder.size();
     while (pos + 1 < Q && queue_less_slow(E.qorder[pos + 1], q)) {
       E.qorder[pos] = E.qorder[pos + 1];
-      E.qrank[E.qorder[pos]] = pos;
+      set_rank(E.qorder[pos], pos);
       ++pos;
     }
     while (pos > 0 && queue_less_slow(q, E.qorder[pos - 1])) {
       E.qorder[pos] = E.qorder[pos - 1];
-      E.qrank[E.qorder[pos]] = pos;
+      set_rank(E.qorder[pos], pos);
       --pos;
     }
     E.qorder[pos] = q;
-    E.qrank[q] = pos;
+    set_rank(q, pos);
   }
   // proportion.go:188-193
   bool overused(int32_t q) const {
@@ -389,7 +398,13 @@ struct Ops {
     const int n = E.qlen++;
     h[n] = q;
     h[n + 1] = V.n_queues;
-    rank_heap_up(h, n, E.qrank.data());
+    if (V.n_queues <= kPackedQueues) {
+      const uint64_t pk = E.qrank_pk;
+      rank_heap_up(h, n, [pk](int32_t x) { return (int32_t)((pk >> (4 * x)) & 15u); });
+    } else {
+      const int32_t* rk = E.qrank.data();
+      rank_heap_up(h, n, [rk](int32_t x) { return rk[x]; });
+    }
   }
   int32_t qpop() {  // Pop: swap(0, n-1), down(0, n-1), take h[n-1]
     int32_t* h = E.qheap.data();
@@ -397,7 +412,13 @@ struct Ops {
     const int32_t q = h[0];
     h[0] = h[n];
     h[n] = V.n_queues;
-    rank_heap_down(h, n, E.qrank.data(), V.heap_go111);
+    if (V.n_queues <= kPackedQueues) {
+      const uint64_t pk = E.qrank_pk;
+      rank_heap_down(h, n, [pk](int32_t x) { return (int32_t)((pk >> (4 * x)) & 15u); }, V.heap_go111);
+    } else {
+      const int32_t* rk = E.qrank.data();
+      rank_heap_down(h, n, [rk](int32_t x) { return rk[x]; }, V.heap_go111);
+    }
     return q;
   }
   // Per-queue job heaps. A job's key changes only while it is popped (drf and
@@ -448,7 +469,10 @@ struct Ops {
     const Res& r = V.treq[t];
     if (V.has_drf) {
       kbg::res_add(E.jalloc[j], r);
-      E.jshare[j] = share_of(E.jalloc[j], V.drf_total);
+      // with gang ahead of drf in the job order (job_chain_pgd) a job short
+      // of MinAvailable keys without its share: computed once it is ready
+      // (and for every job when the cycle ends, finalize_shares)
+      if (!V.job_chain_pgd || E.jready[j] + 1 >= V.job_min[j]) E.jshare[j] = share_of(E.jalloc[j], V.drf_total);
     }
     if (V.has_prop) {
       const int32_t jq = V.job_queue[j];
@@ -475,6 +499,14 @@ struct Ops {
   }
 };
 
+// The drf shares the engine left stale (Ops::apply: a job short of
+// MinAvailable under job_chain_pgd), from each job's allocation: exactly the
+// share an eager update computes (a function of jalloc alone).
+void finalize_shares(const Session& S, Engine& E) {
+  if (!S.has_drf) return;
+  for (int32_t j = 0; j < S.n_jobs; ++j) E.jshare[j] = share_of(E.jalloc[j], S.drf_total);
+}
+
 // allocate.go:45-59: one queue entry per job (queue heap) and every job in
 // its queue's job heap, keyed from E's plugin state.
 void build_heaps(const Session& S, Engine& E) {
@@ -488,6 +520,11 @@ void build_heaps(const Session& S, Engine& E) {
   std::sort(E.qorder.begin(), E.qorder.end(), [&](int32_t a, int32_t b) { return ops.queue_less_slow(a, b); });
   E.qrank.assign(S.n_queues + 1, INT32_MAX);  // [n_queues]: the heap sentinel
   for (int32_t i = 0; i < S.n_queues; ++i) E.qrank[E.qorder[i]] = i;
+  E.qrank_pk = 0;
+  if (S.n_queues <= Ops::kPackedQueues) {
+    for (int32_t q = 0; q < S.n_queues; ++q) E.qrank_pk |= (uint64_t)E.qrank[q] << (4 * q);
+    E.qrank_pk |= 15ull << (4 * S.n_queues);  // the sentinel id's rank: above every queue's (< n_queues <= 15)
+  }
   for (int32_t j = 0; j < S.n_jobs; ++j) {
     ops.qpush(S.job_queue[j]);
     const int32_t q = S.job_queue[j];
@@ -4026,7 +4063,82 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         mark_failed(failed.get(), sh);
     }
   };
+  // Refresh scans (the contended part, batches resolving against an earlier
+  // stage's lists): every node a commit touched since that scan is
+  // re-checked on the host mirror by every shape whose list holds it, so the
+  // re-checks grow with (live shapes) x (nodes filled since the scan). Once
+  // the commit has re-checked KBG_REFRESH_RECHECKS nodes against the current
+  // lists, the touched rows are written back and a scan of every live shape
+  // is launched into the other stage beside the resolve; when it has landed
+  // (polled, never waited for) the commit switches to its lists, whose base
+  // is the write-back: the filled nodes are no longer in them, and only nodes
+  // touched after the write-back are re-checked. Lists stay exact under the
+  // switch for the reason any stage's do (feasibility only shrinks during
+  // allocate; a node touched after the scan is re-checked).
+  static const int64_t refresh_rechecks = [] {
+    const char* e = getenv("KBG_REFRESH_RECHECKS");
+    return e ? atoll(e) : (int64_t)16384;
+  }();
+  bool refresh_inflight = false;
+  std::vector<int32_t> refresh_list;
+  int64_t rechecks_at_scan = 0;
   int si = 0;
+  kbg::Stage* sg = &S.stages[0];
+  kbg::Stage* oth = &S.stages[1];
+  // one task of every shape seen this cycle or kept by derive_host that is
+  // not known to fit nowhere (at most K)
+  auto live_list = [&](std::vector<int32_t>& out) {
+    out.clear();
+    ++shape_in_stamp;
+    for (int32_t sh : seen_shapes) {
+      if ((int32_t)out.size() >= S.K) break;
+      if (shape_in[sh] == shape_in_stamp || failed[sh].load(std::memory_order_relaxed)) continue;
+      shape_in[sh] = shape_in_stamp;
+      out.push_back(shape_rep[sh]);
+    }
+    for (int32_t sh = 0; sh < (int32_t)S.shape_task.size() && sh < (int32_t)shape_in.size(); ++sh) {
+      if ((int32_t)out.size() >= S.K) break;
+      const int32_t rep = S.shape_task[sh];
+      if (rep < 0 || rep >= S.n_tasks || S.task_shape[rep] != sh || shape_in[sh] == shape_in_stamp ||
+          failed[sh].load(std::memory_order_relaxed))
+        continue;
+      shape_in[sh] = shape_in_stamp;
+      out.push_back(rep);
+    }
+  };
+  auto refresh_start = [&]() -> kbg_status {
+    if (kbg_status fs = flush(); fs != KBG_OK) return fs;
+    live_list(refresh_list);
+    if (refresh_list.empty()) return KBG_OK;
+    const int32_t G = grouper.build(*oth, refresh_list.data(), (int32_t)refresh_list.size(), kContendedSlack);
+    if (kbg_status st = device_launch(S, *oth, G, pushed); st != KBG_OK) return st;
+    refresh_inflight = true;
+    S.stats.refresh_scans++;
+    rechecks_at_scan = S.stats.resolve_rechecks;  // (no second refresh while this one is out)
+    ctr.add("refresh", G);
+    return KBG_OK;
+  };
+  // the refresh has landed: its lists become the ones the commit reads,
+  // unless a synchronous rescan since then left fresher ones
+  auto refresh_install = [&]() -> kbg_status {
+    refresh_inflight = false;
+    if (kbg_status st = device_wait(S, *oth); st != KBG_OK) return st;
+    learn_failed(*oth);
+    if (oth->base < sg->base) return KBG_OK;
+    rs.reset(*oth);
+    map_shapes(*oth, refresh_list, 0);
+    si ^= 1;
+    std::swap(sg, oth);
+    rechecks_at_scan = S.stats.resolve_rechecks;
+    ctr.add("installed");
+    return KBG_OK;
+  };
+  auto refresh_poll = [&]() -> kbg_status {
+    if (!reuse || refresh_rechecks <= 0) return KBG_OK;
+    if (refresh_inflight) return hipEventQuery(oth->ev[6]) == hipSuccess ? refresh_install() : KBG_OK;
+    if (S.stats.resolve_rechecks - rechecks_at_scan >= refresh_rechecks) return refresh_start();
+    return KBG_OK;
+  };
   ctr.add("take");
   Batch* cur = next_batch(true);
   ctr.add("took");
@@ -4042,8 +4154,9 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   }
   while (cur && !cur->bt.empty()) {
     const std::vector<int32_t>& bt = cur->bt;
-    kbg::Stage* sg = &S.stages[si];
-    kbg::Stage& other = S.stages[si ^ 1];
+    sg = &S.stages[si];
+    oth = &S.stages[si ^ 1];
+    kbg::Stage& other = *oth;
     S.stats.batches++;
     auto tp = clk::now();
     kbg_status st = KBG_OK;
@@ -4082,6 +4195,9 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     for (int32_t i = 0; i < nb; ++i) {
       const int32_t t = bt[i];
       if ((i & 511) == 511) to_truth(bt, i);  // keep the truth engine a few hundred tasks behind
+      if ((i & 127) == 127 && reuse) {  // contended: a refresh scan to start or to switch to
+        if ((st = refresh_poll()) != KBG_OK) return abort(st);
+      }
       if ((i & 255) == 255 && !nxt && !pred_failed && !reuse) {
         // the predictor's next batch, if it is ready now, scans while this one resolves
         nxt = next_batch(false);
@@ -4168,6 +4284,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         if (keep_reuse) {
           map_shapes(*sg, scan_list, 0);
           reuse = true;
+          rechecks_at_scan = S.stats.resolve_rechecks;
         }
         r = rs.resolve(sg->row_of[0], t, &node, &kind);  // a fresh list always decides its first task
       }
@@ -4250,7 +4367,11 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       break;
     }
     if (cut >= 0) {  // restart the predictor from the engine state at the cut
-      if ((st = device_drop(S, other)) != KBG_OK) return abort(st);  // nxt was predicted before the cut
+      // a refresh scan in flight holds lists as valid as any: switch to them;
+      // anything else in flight was predicted before the cut
+      if (refresh_inflight) st = refresh_install();
+      else st = device_drop(S, *oth);
+      if (st != KBG_OK) return abort(st);
       const bool will_reuse = reuse_ok && !aff_cut;
       contended = will_reuse;
       if (cont_depth > 0) pr.P.depth.store(cont_depth, std::memory_order_relaxed);
@@ -4259,7 +4380,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         // a batch that resolved against an earlier batch's stage keeps that
         // stage's map (its own entries built no rows); otherwise the stage's
         // rows are this batch's entries from `seg` on
-        if (!reuse) map_shapes(*sg, bt, seg);
+        if (!reuse) {
+          map_shapes(*sg, bt, seg);
+          rechecks_at_scan = S.stats.resolve_rechecks;
+        }
         probe_failed(*sg);
       }
       to_truth(bt, cut);
@@ -4287,6 +4411,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     to_truth(bt, nb);
     recycle(cur);
     if (reuse) {  // the next batch resolves against the same lists while they last
+      if ((st = refresh_poll()) != KBG_OK) return abort(st);
       probe_failed(*sg);
       ctr.add("take");
       cur = next_batch(true);
@@ -4331,6 +4456,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
             (unsigned long long)S.affm->prof_calls,
             S.affm->prof_calls ? (double)S.affm->prof_cycles / S.affm->prof_calls : 0.0,
             (unsigned long long)S.affm->prof_recomputes, S.mask_dirty.size());
+  finalize_shares(S, E_truth);
   S.fin = E_truth;
   S.stats.engine_ms = pr.engine_ms;
   S.stats.replayed = pr.replayed;
@@ -4828,6 +4954,7 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
   S.stats.task_evaluations += logged;
   if (rp && !rp->error.empty()) return fail(KBG_E_INVALID, rp->error);
   S.fin = me == 0 ? E_truth : E;  // the committed outcomes' engine state
+  finalize_shares(S, S.fin);
   if (pr) {
     S.stats.engine_ms = pr->engine_ms;
     S.stats.replayed = pr->replayed;

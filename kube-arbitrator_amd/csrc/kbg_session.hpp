@@ -177,6 +177,8 @@ struct Engine {
   std::vector<double> qshare;   // proportion attr.share
   std::vector<int32_t> qorder;  // queues sorted by QueueOrderFn
   std::vector<int32_t> qrank;   // position of each queue in qorder; qrank[n_queues] = INT32_MAX (sentinel id)
+  uint64_t qrank_pk = 0;        // the same 4 bits per queue id when n_queues <= 15 (the sentinel's: 15), so a
+                                // queue-heap compare reads its ranks from a register, not memory
 };
 
 // ---- inter-pod (anti)affinity (kbg_affinity.cpp)

@@ -176,7 +176,7 @@ class kbg_stats(ctypes.Structure):
                 ("victim_tries", i64), ("victim_host_evals", i64), ("task_evaluations", i64),
                 ("resolve_steps", i64), ("resolve_rechecks", i64), ("overlapped", i64),
                 ("update_ms", f64), ("update_rebuilds", i64), ("owner_rounds", i64),
-                ("reused_batches", i64)]
+                ("reused_batches", i64), ("refresh_scans", i64)]
 
 
 EV_POD_UPDATE = 1

@@ -26,10 +26,11 @@ def main():
             fs = d.get("full_scan_mode", {})
             bd = d.get("production_mode", {}).get("breakdown", {})
             r = (round(d["p50_cycle_ms"], 2), round(fs.get("p50_cycle_ms", 0.0), 2), round(bd.get("host_engine_ms", 0), 2),
-                 round(bd.get("host_resolve_ms", 0), 2), bd.get("mispredictions"))
+                 round(bd.get("host_resolve_ms", 0), 2), bd.get("mispredictions"), bd.get("resolve_rechecks"),
+                 bd.get("refresh_scans"), round(bd.get("scan_ms", 0), 3))
             res.setdefault(spec or "default", []).append(r)
             print(f"{spec or 'default':40s} prod {r[0]:.2f} ms  full {r[1]:.2f} ms  engine {r[2]:.2f}  resolve {r[3]:.2f}"
-                  f"  cuts {r[4]}", flush=True)
+                  f"  cuts {r[4]}  rechecks {r[5]}  refreshes {r[6]}  kernel {r[7]} ms", flush=True)
     print(json.dumps(res))
 
 
