@@ -278,6 +278,8 @@ hipError_t launch_select(const uint64_t* bits, int32_t w_lo, int32_t w_hi, int32
                          hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 
 hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_deltas, hipStream_t stream);
+// dst[0..n16) = src[0..n16), 16 B per lane (the node-table restore of kbg_session_reset)
+hipError_t launch_copy16(void* dst, const void* src, size_t n16, hipStream_t stream);
 
 // FitError counts of not-ready jobs (kbg_fitdelta_kernel).
 struct FitQuery {

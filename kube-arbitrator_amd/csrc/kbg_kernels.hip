@@ -707,6 +707,19 @@ hipError_t launch_apply(const NodeSoA& n, const NodeDelta* deltas, int32_t n_del
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void kbg_copy16_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                         size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
+hipError_t launch_copy16(void* dst, const void* src, size_t n16, hipStream_t stream) {
+  if (n16 == 0) return hipSuccess;
+  hipLaunchKernelGGL(kbg_copy16_kernel, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, stream, (uint4*)dst,
+                     (const uint4*)src, n16);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void kbg_mask_apply_kernel(uint64_t* __restrict__ class_mask,
                                                              const MaskDelta* __restrict__ d, int32_t n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -806,42 +819,79 @@ __device__ __forceinline__ void apply_preemptee(const VictimTables& t, int fns, 
   }
 }
 
+// A wave-uniform 64-bit mask read back from LDS (every lane reads the same
+// word; readfirstlane makes it scalar again).
+__device__ __forceinline__ uint64_t lds_mask(const uint64_t* p) {
+  const uint64_t v = *p;
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(v >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)v);
+}
+
+// Per-chunk candidate masks of one node (preemptees, the tier's victims, the
+// deciding tier's): in registers for the main scan (NCH <= 2), in this
+// wave's LDS slice for the big-node kernel (16 chunks x 3 masks would not fit
+// the register file: they spilled to scratch).
+template <int NCH, bool LDS>
+struct ChunkMasks {
+  uint64_t pm[LDS ? 1 : NCH], tm[LDS ? 1 : NCH], vm[LDS ? 1 : NCH];
+  uint64_t* lds;  // LDS: [3][NCH] of this wave
+  int lane;
+  __device__ uint64_t get(int which, int h) const {
+    if constexpr (LDS) return lds_mask(lds + which * NCH + h);
+    else return which == 0 ? pm[h] : which == 1 ? tm[h] : vm[h];
+  }
+  __device__ void set(int which, int h, uint64_t v) {
+    if constexpr (LDS) {
+      if (lane == 0) lds[which * NCH + h] = v;
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      (which == 0 ? pm : which == 1 ? tm : vm)[h] = v;
+    }
+  }
+};
+
 // The stop key of node n with its candidates in at most NCH chunks
 // (wave-uniform), UINT32_MAX when the reference moves on to the next node.
-// NCH is a compile-time bound so the per-chunk masks stay in registers.
-template <int NCH>
+// NCH is a compile-time bound so the per-chunk masks stay in registers
+// (or, LDS, in the wave's LDS slice `lds_masks`).
+template <int NCH, bool LDS = false>
 __device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t, int n, int off, int L, int lane,
-                                      const VCand& c0) {
+                                      const VCand& c0, uint64_t* lds_masks = nullptr) {
   constexpr uint32_t kNone = 0xffffffffu;
+  constexpr int PM = 0, TM = 1, VM = 2;
   const int nch = (L + 63) >> 6;  // <= NCH
-  uint64_t pm[NCH];
+  ChunkMasks<NCH, LDS> cm;
+  cm.lds = lds_masks;
+  cm.lane = lane;
   uint64_t any_pm = 0ull;
 #pragma unroll
   for (int h = 0; h < NCH; ++h) {
-    pm[h] = h < nch ? __ballot((h == 0 ? c0 : load_cand(p, t, off, L, h * 64 + lane)).f) : 0ull;
-    any_pm |= pm[h];
+    const uint64_t m = h < nch ? __ballot((h == 0 ? c0 : load_cand(p, t, off, L, h * 64 + lane)).f) : 0ull;
+    cm.set(PM, h, m);
+    any_pm |= m;
   }
   if (!any_pm) return kNone;  // no preemptee: every fn returns nil
   // the first chunk's gang inputs, requested before the tier walk needs them
   // (one dependent level less on the node's load chain)
   const bool g0 = c0.job >= 0 && t.j_min[c0.job] <= t.j_ready[c0.job] - 1;
   bool panic = false;
-  uint64_t vm[NCH];
   bool victims = false;
   for (int ti = 0; ti < p.n_tiers && !victims && !panic; ++ti) {
     const int fns = p.tier_fns[ti];
-    uint64_t tm[NCH];
     bool any = false;
 #pragma unroll
     for (int h = 0; h < NCH; ++h) {
-      tm[h] = 0ull;
-      if (h >= nch) continue;
+      if (h >= nch) {
+        cm.set(TM, h, 0ull);
+        continue;
+      }
       const VCand c = h == 0 ? c0 : load_cand(p, t, off, L, h * 64 + lane);
-      uint64_t m = pm[h];
+      const uint64_t pmh = cm.get(PM, h);
+      uint64_t m = pmh;
       if (fns & VP_GANG)  // gang.go:104-124
         m &= __ballot(h == 0 ? g0 : (c.job >= 0 && t.j_min[c.job] <= t.j_ready[c.job] - 1));
       if (fns & (VP_DRF | VP_PROP)) {
-        const bool on = (pm[h] >> lane) & 1ull;
+        const bool on = (pmh >> lane) & 1ull;
         double xd[3], xp[3];
         for (int d = 0; d < 3; ++d) {
           xd[d] = on && (fns & VP_DRF) ? t.j_alloc[3 * (size_t)c.job + d] : 0.0;
@@ -849,7 +899,7 @@ __device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t
         }
         bool lpanic = false, vp = false;
         for (int h2 = 0; h2 < h; ++h2)  // preemptees of earlier chunks (all before this lane's k)
-          for (uint64_t b = pm[h2]; b; b &= b - 1) {
+          for (uint64_t b = cm.get(PM, h2); b; b &= b - 1) {
             const size_t p2 = (size_t)off + h2 * 64 + __builtin_ctzll(b);  // wave-uniform
             const int2 jq2 = t.c_jq[p2];
             const int32_t j2 = jq2.x;
@@ -857,7 +907,7 @@ __device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t
             const double r2[3] = {t.c_req[3 * p2], t.c_req[3 * p2 + 1], t.c_req[3 * p2 + 2]};
             if (on) apply_preemptee(t, fns, j2, q2, r2, false, c.job, c.queue, xd, xp, lpanic, vp);
           }
-        for (uint64_t b = pm[h]; b; b &= b - 1) {  // this chunk, in order, while k2 <= k
+        for (uint64_t b = pmh; b; b &= b - 1) {  // this chunk, in order, while k2 <= k
           const int l2 = __builtin_ctzll(b);
           const int32_t j2 = rl_i(c.job, l2);
           const int32_t q2 = rl_i(c.queue, l2);
@@ -873,12 +923,12 @@ __device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t
         if (fns & VP_PROP) m &= __ballot(vp);
         if (__ballot(lpanic) != 0ull) panic = true;
       }
-      tm[h] = m;
+      cm.set(TM, h, m);
       any = any || m != 0ull;
     }
     if (!panic && any) {  // the host passes only the deciding tier (session_plugins.go:59-98)
 #pragma unroll
-      for (int h = 0; h < NCH; ++h) vm[h] = tm[h];
+      for (int h = 0; h < NCH; ++h) cm.set(VM, h, cm.get(TM, h));
       victims = true;
     }
   }
@@ -887,11 +937,12 @@ __device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t
   double all[3] = {0.0, 0.0, 0.0};  // validateVictims (preempt.go:242-253), in victims order
 #pragma unroll
   for (int h = 0; h < NCH; ++h) {
-    if (!vm[h]) continue;
+    const uint64_t vmh = cm.get(VM, h);
+    if (!vmh) continue;
     // each lane reads its own candidate's request (one coalesced load), the
     // wave-uniform sum takes them lane by lane in order
     const VCand c = h == 0 ? c0 : load_cand(p, t, off, L, h * 64 + lane);
-    for (uint64_t b = vm[h]; b; b &= b - 1) {
+    for (uint64_t b = vmh; b; b &= b - 1) {
       const int l2 = __builtin_ctzll(b);
       all[0] += rl_d(c.r[0], l2);
       all[1] += rl_d(c.r[1], l2);
@@ -907,7 +958,8 @@ __device__ uint32_t victim_candidates(const VictimScan& p, const VictimTables& t
 // kbg_victim_big_kernel, whose larger per-chunk state would otherwise raise
 // the register budget of every wave.
 template <int NCH_MAX>
-__device__ uint32_t victim_node(const VictimScan& p, const VictimTables& t, int row, int lane) {
+__device__ __forceinline__ uint32_t victim_node(const VictimScan& p, const VictimTables& t, int row, int lane,
+                                uint64_t* lds_masks = nullptr) {
   constexpr uint32_t kNone = 0xffffffffu;
   const int n = p.node_lo + row;
   const int off = t.nt_off[n];
@@ -919,7 +971,11 @@ __device__ uint32_t victim_node(const VictimScan& p, const VictimTables& t, int 
   if (!((t.class_mask[(size_t)p.cls * p.W + (n >> 6)] >> (n & 63)) & 1ull)) return kNone;  // static predicate
   if (t.panic_node[n]) return ((uint32_t)n << 1) | 1u;  // SetNode(nil) inside PredicateFn (predicates.go:122-123)
   if (p.cap_check && t.ntasks[row] >= t.maxtasks[row]) return kNone;  // predicates.go:125-127
-  if (NCH_MAX > 2) return victim_candidates<NCH_MAX>(p, t, n, off, L, lane, c0);
+  if (NCH_MAX > 2) {  // inlined here: a call would pass the argument structs through scratch
+    uint32_t key;
+    [[clang::always_inline]] key = victim_candidates<NCH_MAX, true>(p, t, n, off, L, lane, c0, lds_masks);
+    return key;
+  }
   if (L <= 64) return victim_candidates<1>(p, t, n, off, L, lane, c0);
   return victim_candidates<2>(p, t, n, off, L, lane, c0);
 }
@@ -964,8 +1020,9 @@ __global__ __launch_bounds__(256) void kbg_victim_big_kernel(VictimScan p, Victi
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n_rows) return;
+  __shared__ uint64_t s_masks[4][3 * kVictimChunks];  // each wave's chunk masks (ChunkMasks)
   const int row = rows[i];
-  const uint32_t key = victim_node<kVictimChunks>(p, t, row, lane);
+  const uint32_t key = victim_node<kVictimChunks>(p, t, row, lane, s_masks[threadIdx.x >> 6]);
   if (row_out) {  // one byte per big node (host-mapped; the host ORs them into its maps): bit 0 stop, bit 1 panic
     if (lane == 0) row_out[i] = key == 0xffffffffu ? 0u : (uint8_t)(1u | ((key & 1u) << 1));
     return;

@@ -554,6 +554,44 @@ kbg_status hupload(Session& S, T** p, const std::vector<T>& v) {
   return KBG_OK;
 }
 
+// Several host arrays into ONE device block with one copy (session open's
+// static tables, the victim tables): one transfer instead of a copy per array.
+struct BulkUpload {
+  struct Item {
+    void** p;
+    size_t off;
+  };
+  std::vector<Item> items;
+  std::vector<char> host;
+  void add_raw(void** p, const void* data, size_t bytes) {
+    const size_t off = (host.size() + 255) & ~(size_t)255;
+    host.resize(off + std::max<size_t>(bytes, 16), 0);
+    if (data && bytes) std::memcpy(host.data() + off, data, bytes);
+    items.push_back({p, off});
+  }
+  template <class T>
+  void add(T** p, const std::vector<T>& v) {
+    add_raw((void**)p, v.data(), v.size() * sizeof(T));
+  }
+  template <class T>
+  void zeros(T** p, size_t count) {  // zero-filled on the device
+    add_raw((void**)p, nullptr, count * sizeof(T));
+  }
+  // allocates the block, points every item into it, copies once and waits
+  // (the host vectors the items came from may end after this)
+  kbg_status commit(Session& S) {
+    if (items.empty()) return KBG_OK;
+    char* d = nullptr;
+    if (kbg_status st = dalloc(S, &d, host.size()); st != KBG_OK) return st;
+    for (const Item& it : items) *it.p = d + it.off;
+    HIP_TRY(hipMemcpyAsync(d, host.data(), host.size(), hipMemcpyHostToDevice, S.stream));
+    HIP_TRY(hipStreamSynchronize(S.stream));
+    items.clear();
+    host.clear();
+    return KBG_OK;
+  }
+};
+
 // The node table as ONE block (FirstFitArgs.nodes): idle c/m/g and rel c/m/g
 // f64[stride], then ntasks and maxtasks i32[stride], stride = tab_n rounded
 // up to 64 rows. A reset restores it with one copy.
@@ -581,7 +619,8 @@ kbg_status alloc_soa(Session& S, kbg::NodeSoA* soa) {
 
 kbg_status copy_soa(Session& S, const kbg::NodeSoA& dst, const kbg::NodeSoA& src) {
   if (S.tab_n == 0) return KBG_OK;
-  HIP_TRY(hipMemcpyAsync(dst.idle_cpu, src.idle_cpu, soa_bytes(S), hipMemcpyDeviceToDevice, S.stream));
+  // (a kernel of ours, not the runtime's blit: soa_bytes is a multiple of 16)
+  HIP_TRY(kbg::launch_copy16(dst.idle_cpu, src.idle_cpu, soa_bytes(S) / 16, S.stream));
   return KBG_OK;
 }
 
@@ -2943,11 +2982,19 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
     kbg::ReqProg* rq;
     kbg::TermProg* tm;
     kbg::ClassProg* cl;
-    if ((st = hupload(S, &lb, sh.label_bits)) || (st = hupload(S, &tb, sh.taint_bits)) || (st = hupload(S, &mp, sh.mask_pool)) ||
-        (st = hupload(S, &tp, sh.tol_pool)) || (st = hupload(S, &nv, sh.num_vals)) || (st = hupload(S, &nok, sh.num_ok)) ||
-        (st = hupload(S, &nf, sh.node_flags)) || (st = hupload(S, &nid, sh.name_id)) || (st = hupload(S, &rq, sh.reqs)) ||
-        (st = hupload(S, &tm, sh.terms)) || (st = hupload(S, &cl, sh.classes)))
-      return st;
+    BulkUpload bu;  // the static predicate tables in one block, one copy
+    bu.add(&lb, sh.label_bits);
+    bu.add(&tb, sh.taint_bits);
+    bu.add(&mp, sh.mask_pool);
+    bu.add(&tp, sh.tol_pool);
+    bu.add(&nv, sh.num_vals);
+    bu.add(&nok, sh.num_ok);
+    bu.add(&nf, sh.node_flags);
+    bu.add(&nid, sh.name_id);
+    bu.add(&rq, sh.reqs);
+    bu.add(&tm, sh.terms);
+    bu.add(&cl, sh.classes);
+    if ((st = bu.commit(S))) return st;
     t.n_nodes = N;
     t.label_words = sh.label_words;
     t.taint_words = sh.taint_words;
@@ -5215,12 +5262,34 @@ kbg_status vt_setup(Session& S) {
     uint8_t *dpn, *drun;
     int32_t *doff, *dcjq, *djq, *djm, *djr;
     double *dcr, *dja, *dqa, *dqd;
-    if ((st = hupload(S, &dpn, pn)) || (st = hupload(S, &doff, S.nt_off)) || (st = hupload(S, &dcjq, cjq)) ||
-        (st = hupload(S, &dcr, cr)) || (st = dalloc(S, &drun, P)) ||
-        (st = hupload(S, &djq, jq)) || (st = hupload(S, &djm, jm)) || (st = dalloc(S, &djr, J)) ||
-        (st = dalloc(S, &dja, 3 * J)) || (st = dalloc(S, &dqa, 3 * Q)) || (st = hupload(S, &dqd, qd)) ||
-        (st = dalloc(S, &S.d_vbits, 2 * (size_t)S.W32)) || (st = dalloc(S, &S.d_vbits_red, 2 * (size_t)S.W32)))
-      return st;
+    // the live state (running flags, gang readiness, drf / proportion
+    // allocations) goes up whole with the tables, as vt_sh_* records it
+    const size_t Pn = S.nt_task.size();
+    S.vt_sh_valid = true;
+    S.vt_sh_run.resize(Pn);
+    S.vt_sh_ready = S.committed_ready;
+    S.vt_sh_jalloc.assign(3 * J, 0.0);
+    S.vt_sh_qalloc.assign(3 * Q, 0.0);
+    for (size_t k = 0; k < Pn; ++k) S.vt_sh_run[k] = S.trun[S.nt_task[k]];
+    for (int32_t j = 0; j < S.n_jobs; ++j) std::memcpy(&S.vt_sh_jalloc[3 * (size_t)j], &S.fin.jalloc[j].c, 24);
+    for (int32_t q = 0; q < S.n_queues; ++q) std::memcpy(&S.vt_sh_qalloc[3 * (size_t)q], &S.fin.qalloc[q].c, 24);
+    S.sdeltas.clear();
+    std::vector<int32_t> ready0(J, 0);
+    std::copy(S.committed_ready.begin(), S.committed_ready.end(), ready0.begin());
+    BulkUpload bu;  // every table (and the live state) in one block, one copy
+    bu.add(&dpn, pn);
+    bu.add(&doff, S.nt_off);
+    bu.add(&dcjq, cjq);
+    bu.add(&dcr, cr);
+    bu.add(&drun, S.vt_sh_run);
+    bu.add(&djq, jq);
+    bu.add(&djm, jm);
+    bu.add(&djr, ready0);
+    bu.add(&dja, S.vt_sh_jalloc);
+    bu.add(&dqa, S.vt_sh_qalloc);
+    bu.add(&dqd, qd);
+    bu.zeros(&S.d_vbits, 2 * (size_t)S.W32);  // other ranks' words stay 0
+    bu.zeros(&S.d_vbits_red, 2 * (size_t)S.W32);
     // nodes of this process's range holding more than 128 candidates
     // (kbg_victim_big_kernel, up to kMaxNodeCandidates); every node holding
     // more is left out of the device scans and re-evaluated on the host when
@@ -5232,9 +5301,9 @@ kbg_status vt_setup(Session& S) {
       if (L > kbg::kMaxNodeCandidates) S.huge_nodes.push_back(n);
       else if (L > 128 && n >= S.tab_lo && n < S.tab_lo + S.tab_n) S.big_rows.push_back(n - S.tab_lo);
     }
-    if ((st = hupload(S, &S.d_big_rows, S.big_rows))) return st;
+    bu.add(&S.d_big_rows, S.big_rows);
+    if ((st = bu.commit(S))) return st;
     S.vt_allocs.assign(S.d_allocs.begin() + a0, S.d_allocs.end());
-    HIP_TRY(hipMemset(S.d_vbits, 0, 2 * (size_t)S.W32 * sizeof(uint32_t)));  // other ranks' words stay 0
     if (!S.h_vbits) {
       const size_t vb = std::max<size_t>(2 * (size_t)S.W32 * sizeof(uint32_t), 64);  // W32 = 0: no nodes
       HIP_TRY(hipHostMalloc((void**)&S.h_vbits, vb, hipHostMallocCoherent | hipHostMallocMapped));
