@@ -4043,6 +4043,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   // candidate walk, host mirror, decision log, whole loop
   const bool rprof = getenv("KBG_PROFILE_RESOLVE") != nullptr;
   uint64_t rcyc[4] = {0, 0, 0, 0};
+  int64_t rk_phase[3] = {0, 0, 0};  // re-checks before the first cut, after it on fresh scans, on reused lists
   // Grouped mode, after a cut: the stage's candidate lists still hold for the
   // committed table (a list is every fitting node in order at scan time, up
   // to its length; feasibility only shrinks during allocate, and a node
@@ -4261,6 +4262,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       }
       int32_t node = -1, kind = 0;
       const uint64_t c0 = rprof ? cycles() : 0;
+      const int64_t rk0 = S.stats.resolve_rechecks;
       int r;
       if (reuse) {
         const int32_t row = shape_row_of[S.task_shape[t]];
@@ -4268,7 +4270,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       } else {
         r = rs.resolve(sg->row_of[i - seg], t, &node, &kind);
       }
-      if (rprof) rcyc[0] += cycles() - c0;
+      if (rprof) {
+        rcyc[0] += cycles() - c0;
+        rk_phase[reuse ? 2 : contended ? 1 : 0] += S.stats.resolve_rechecks - rk0;
+      }
       if (r == RES_TRUNC) {
         if (reuse) ctr.add("reuse.rescan", i);
         const bool keep_reuse = contended;  // the rescan's rows by shape (else by batch entry)
@@ -4513,6 +4518,11 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
             (double)rcyc[1] / std::max<int64_t>(1, S.stats.task_evaluations),
             (double)rcyc[2] / std::max<int64_t>(1, S.stats.task_evaluations),
             (double)rcyc[3] / std::max<int64_t>(1, S.stats.task_evaluations));
+  if (rprof)
+    fprintf(stderr, "[kbg resolve] re-checks: uncontended %lld, contended on fresh scans %lld, on reused lists %lld; "
+                    "refresh scans %lld, overlapped batches %lld, batches %lld\n",
+            (long long)rk_phase[0], (long long)rk_phase[1], (long long)rk_phase[2], (long long)S.stats.refresh_scans,
+            (long long)S.stats.overlapped, (long long)S.stats.batches);
   if (eprof.on && eprof.steps)
     fprintf(stderr, "[kbg engine] steps %llu cycles/step: qpop %.1f apply %.1f jfix %.1f qpush %.1f (engine %.3f ms)\n",
             (unsigned long long)eprof.steps, (double)eprof.qpop / eprof.steps, (double)eprof.apply / eprof.steps,
