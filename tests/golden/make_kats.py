@@ -415,6 +415,48 @@ KATS = {
                      "binds": {"ns/p1": "n1", "ns/p2": "n1"},
                      "nodes": {"n1": [[0.0, 64.0 * GI, 0.0], [0.0, 0.0, 0.0], 2]}},
     },
+    # The podLister Filter (kube-batch predicates.go:67-89, vendor
+    # cache/node_info.go:692-702): a pod whose spec names node n but that is
+    # missing from n's pods is left out of n's inter-pod affinity checks.
+    # n1 (3 CPU) runs h (app=db, key ns/px, job pgH at its minimum), v1, v2
+    # (pgV, one above its minimum). Actions preempt then allocate; job order
+    # pgW (created first) then pgP (session_plugins.go JobOrderFn fallback).
+    # preempt (preempt.go:43-171): w's anti-affinity to app=db on the host
+    # fails n1 while h is there; no node, nothing to discard. p (named like h)
+    # evicts one of v1 / v2 (gang lets pgV lose one; the first victim covers
+    # 1 CPU, preempt.go:205-219) and is pipelined: node.AddTask refuses the
+    # taken key (node_info.go:101-106). p2 (selector matches nothing) fails,
+    # pgP stays short of 2 and the statement is discarded (statement.go:
+    # 194-205): unpipeline's RemoveTask by key takes h off n1 (Idle +1 CPU,
+    # node_info.go:131-157), unevict's AddTask finds the victim still there as
+    # Releasing. n1: Idle 1, Releasing 1, pods {v1, v2}.
+    # allocate (allocate.go:40-170): w on n1 — h's spec still names n1 but h
+    # is not in n1's pods, so the Filter drops it and w's anti term matches
+    # nothing: w takes the idle CPU (without the Filter n1 fails and p takes
+    # it instead). pgW is ready and dispatched; p then pipelines onto the
+    # victim's Releasing CPU (the key is free now), p2 fails, pgP is not
+    # ready. Nothing was committed in preempt, so no evictions.
+    "kat_podlister_filter": {
+        "actions": ["preempt", "allocate"],
+        "tiers": [[{"name": "priority"}, {"name": "gang"}], [{"name": "drf"}, {"name": "predicates"}]],
+        "nodes": [node("n1", "3", labels={"kubernetes.io/hostname": "n1"})],
+        "pods": [pod("h", "px", {"cpu": "1"}, group="pgH", phase="Running", node="n1", labels={"app": "db"}),
+                 pod("v1", "v1", {"cpu": "1"}, group="pgV", phase="Running", node="n1"),
+                 pod("v2", "v2", {"cpu": "1"}, group="pgV", phase="Running", node="n1"),
+                 pod("w", "w", {"cpu": "1"}, group="pgW",
+                     affinity={"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                         {"labelSelector": {"matchLabels": {"app": "db"}},
+                          "topologyKey": "kubernetes.io/hostname"}]}}),
+                 pod("p", "px", {"cpu": "1"}, group="pgP"),
+                 pod("p2", "p2", {"cpu": "1"}, group="pgP", nodeSelector={"zone": "nowhere"})],
+        "podGroups": [pg("pgH", minMember=1), pg("pgV", minMember=1), pg("pgW", minMember=1, created=10),
+                      pg("pgP", minMember=2, created=20)],
+        "queues": Q,
+        "expected": {"decisions": [["w", "n1", "allocate"], ["p", "n1", "pipeline"]],
+                     "evictions": [], "binds": {"ns/w": "n1"},
+                     "ready": {"ns/pgH": True, "ns/pgV": True, "ns/pgW": True, "ns/pgP": False},
+                     "nodes": {"n1": [[0, 64 * GI, 0], [0, 0, 0], 4]}},
+    },
 }
 
 
