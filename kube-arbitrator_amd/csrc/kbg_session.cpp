@@ -1517,7 +1517,10 @@ bool mirror_add(Session& S, int32_t t, int32_t nd, int32_t kind) {
     }
     S.ntasks[nd]++;
     if (S.has_ports) add_ports(S, S.task_class[t], nd);
-    if (S.has_dupkeys && S.key_hot[S.task_key[t]]) S.node_keys.insert(node_key_of(S, t, nd));
+    if (S.has_dupkeys && S.key_hot[S.task_key[t]]) {
+      S.node_keys.insert(node_key_of(S, t, nd));
+      S.key_holder[node_key_of(S, t, nd)] = t << 1 | (kind != KBG_KIND_ALLOCATE);
+    }
   }
   // an Allocated pod joins the podLister (api/helpers.go:63-70); Pipelined does not
   if (S.has_aff && kind == KBG_KIND_ALLOCATE) {
@@ -3429,6 +3432,7 @@ void begin_cycle(Session& S) {
   S.port_hold.clear();
   S.port_gone.clear();
   S.outsider_gone.clear();
+  S.key_holder.clear();
   S.evictions.clear();
   if ((int32_t)S.tstat_in.size() == S.n_tasks) {
     S.tstat.assign(S.tstat_in.begin(), S.tstat_in.end());  // tasks_in[t].status, packed by derive_host
@@ -4729,7 +4733,10 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
         if (!S.nil_node[u.node]) (u.kind == KBG_KIND_ALLOCATE ? S.idle[u.node] : S.rel[u.node]) = u.old;
         S.ntasks[u.node]--;
         if (S.has_ports) remove_ports(S, S.task_class[t], u.node);
-        if (S.has_dupkeys && S.key_hot[S.task_key[t]]) S.node_keys.erase(node_key_of(S, t, u.node));
+        if (S.has_dupkeys && S.key_hot[S.task_key[t]]) {
+          S.node_keys.erase(node_key_of(S, t, u.node));
+          S.key_holder.erase(node_key_of(S, t, u.node));
+        }
       }
       undo.pop_back();
     }
@@ -5514,7 +5521,10 @@ struct Live {
     if (!*dup) {
       if (!S.nil_node[n] && !kbg::res_sub(S.rel[n], S.treq[t])) return false;  // node_info.go:117-118
       S.ntasks[n]++;
-      if (S.has_dupkeys && S.key_hot[S.task_key[t]]) S.node_keys.insert(node_key_of(S, t, n));
+      if (S.has_dupkeys && S.key_hot[S.task_key[t]]) {
+        S.node_keys.insert(node_key_of(S, t, n));
+        S.key_holder[node_key_of(S, t, n)] = t << 1 | 1;
+      }
       if (S.has_ports) add_ports(S, S.task_class[t], n);  // the pod joins node.Pods()
       touch(n);
     }
@@ -5535,6 +5545,7 @@ struct Live {
       if (!S.nil_node[n] && !kbg::res_sub(S.idle[n], S.treq[v])) return false;  // node_info.go:123-124
       S.ntasks[n]++;
       S.node_keys.insert(node_key_of(S, v, n));
+      S.key_holder[node_key_of(S, v, n)] = v << 1;
       S.trun[v] = 1;
       if (S.t_pos[v] >= 0) vt_delta(S, 0, S.t_pos[v], 1.0, 0, 0);
       S.t_detached[v] = 0;
@@ -5560,9 +5571,10 @@ struct Live {
   // status of its node copy: Releasing (Releasing -= req, Idle += req),
   // Pipelined (Releasing += req), anything else (Idle += req), and its host
   // ports leave node.Pods(). The holder is a session task on the node at open
-  // (Running then — Releasing if evicted since — or any other status it kept)
-  // or a pod outside the session jobs (its copy from kbg_node_pod). A holder
-  // placed this cycle (two Pending pods sharing a key) is refused.
+  // (Running then — Releasing if evicted since — or any other status it kept),
+  // a task placed this cycle (two Pending pods sharing a key: its copy is
+  // Allocated or Pipelined, S.key_holder) or a pod outside the session jobs
+  // (its copy from kbg_node_pod).
   kbg_status unpipeline_dup(int32_t t, int32_t n) {
     const int32_t j = S.task_job[t];
     ready(j, -1);
@@ -5570,6 +5582,12 @@ struct Live {
     if (node_has_key(S, t, n)) {
       const int64_t hk = node_key_of(S, t, n);
       int32_t h = -1;
+      bool placed = false, placed_pipe = false;  // the holder took the key this cycle (its copy: Allocated / Pipelined)
+      if (auto kh = S.key_holder.find(hk); kh != S.key_holder.end()) {
+        h = kh->second >> 1;
+        placed = S.tstat_in[h] == KBG_PENDING;
+        placed_pipe = placed && (kh->second & 1);
+      }
       for (int32_t k = S.nt_off[n]; k < S.nt_off[n + 1] && h < 0; ++k) {
         const int32_t u = S.nt_task[k];
         if (u != t && S.task_key[u] == S.task_key[t] && !S.t_detached[u]) h = u;
@@ -5587,13 +5605,14 @@ struct Live {
       }
       if (h < 0 && !o)
         return fail(KBG_E_UNSUPPORTED, "statement discard of a pipeline whose pod key is held on the node by a pod "
-                                       "placed this cycle, or by a pod outside the session jobs with no node_pods "
-                                       "entry (node_info.go:131-157 removes it): run the reference path");
+                                       "outside the session jobs with no node_pods entry (node_info.go:131-157 "
+                                       "removes it, its resources are unknown): supply node_pods");
       Res r;
       int32_t status;
       if (h >= 0) {
         r = S.treq[h];
-        status = S.tstat_in[h] != KBG_RUNNING ? S.tstat_in[h] : S.trun[h] ? KBG_RUNNING : KBG_RELEASING;
+        if (placed) status = placed_pipe ? KBG_PIPELINED : KBG_ALLOCATED;
+        else status = S.tstat_in[h] != KBG_RUNNING ? S.tstat_in[h] : S.trun[h] ? KBG_RUNNING : KBG_RELEASING;
       } else {
         r = to_res(o->req);
         status = o->status;
@@ -5611,16 +5630,22 @@ struct Live {
       }
       S.ntasks[n]--;
       S.node_keys.erase(hk);
+      S.key_holder.erase(hk);
       if (h >= 0) {
         const int32_t hs = S.tasks_in[h].spec;
-        if (hs >= 0 && S.specs_in[hs].port_len > 0)
+        if (placed) {  // its ports joined with its placement (add_ports)
+          if (S.has_ports) remove_ports(S, S.task_class[h], n);
+        } else if (hs >= 0 && S.specs_in[hs].port_len > 0) {
           release_open_ports(S, n, &S.ports_in[S.specs_in[hs].port_off], S.specs_in[hs].port_len);
+        }
         if (S.trun[h]) {
           S.trun[h] = 0;  // no longer in node.Tasks: not a victim candidate
           if (S.t_pos[h] >= 0) vt_delta(S, 0, S.t_pos[h], 0, 0, 0);
         }
         S.t_detached[h] = 1;
-        if (S.has_aff && allocated_status(S.tstat[h])) {  // the podLister Filter now leaves it out of n's predicate
+        // the podLister Filter now leaves it out of n's predicate — unless it
+        // was placed this cycle (its informer Spec.NodeName is "", kept)
+        if (S.has_aff && !placed && allocated_status(S.tstat[h])) {
           S.aff_filtered.emplace_back(n, h);
           kbg::aff_refresh_node(S, n);
         }
@@ -5634,14 +5659,24 @@ struct Live {
       return fail(KBG_E_REF_PANIC, "statement discard: DeallocateFunc Sub underflow (resource_info.go:100-110)");
     return KBG_OK;
   }
-  // statement.go:156-192: job Pending; node.RemoveTask; DeallocateFunc
+  // statement.go:156-192: job Pending; node.RemoveTask; DeallocateFunc. A
+  // task whose copy an earlier RemoveTask by key took off the node (a later
+  // pipeline of the same statement that shared its key was discarded first):
+  // RemoveTask finds nothing, the node is unchanged.
   bool unpipeline(int32_t t, int32_t n) {
     const int32_t j = S.task_job[t];
     ready(j, -1);
     S.tstat[t] = KBG_PENDING;
+    if (!S.t_detached.empty() && S.t_detached[t]) {
+      S.t_detached[t] = 0;
+      return plugins(t, false);
+    }
     if (!S.nil_node[n]) kbg::res_add(S.rel[n], S.treq[t]);  // node_info.go:145-146
     S.ntasks[n]--;
-    if (S.has_dupkeys && S.key_hot[S.task_key[t]]) S.node_keys.erase(node_key_of(S, t, n));
+    if (S.has_dupkeys && S.key_hot[S.task_key[t]]) {
+      S.node_keys.erase(node_key_of(S, t, n));
+      S.key_holder.erase(node_key_of(S, t, n));
+    }
     if (S.has_ports) remove_ports(S, S.task_class[t], n);  // the pod leaves node.Pods()
     touch(n);
     return plugins(t, false);
@@ -5941,6 +5976,17 @@ void stmt_commit(Session& S, Stmt& stmt) {  // statement.go:207-217
 }
 
 kbg_status stmt_discard(Session& S, Live& L, Stmt& stmt) {  // statement.go:194-205
+  // the one refusal (a key held by a pod outside the session jobs whose copy
+  // the snapshot did not carry) is found before any operation is undone
+  for (const Stmt::Op& op : stmt.ops) {
+    if (op.evict || !op.dup) continue;
+    const int64_t hk = node_key_of(S, op.task, op.node);
+    auto oit = S.outsiders.find(hk);
+    if (oit != S.outsiders.end() && oit->second.status == 0 && !S.outsider_gone.count(hk))
+      return fail(KBG_E_UNSUPPORTED, "statement discard of a pipeline whose pod key is held on the node by a pod "
+                                     "outside the session jobs with no node_pods entry (node_info.go:131-157 "
+                                     "removes it, its resources are unknown): supply node_pods");
+  }
   bool ok = true;
   for (size_t k = stmt.ops.size(); k-- > 0;) {
     const Stmt::Op& op = stmt.ops[k];
@@ -6675,6 +6721,7 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
     S.port_hold.clear();
     S.port_gone.clear();
     S.outsider_gone.clear();
+    S.key_holder.clear();
     // host ports / pod affinity live in the class masks: refold them
     if (had_masks || S.has_ports || S.has_aff) {
       S.h_class_mask = S.h_class_mask_static;
@@ -6891,6 +6938,7 @@ kbg_status session_reset(Session& S) {
   S.port_hold.clear();
   S.port_gone.clear();
   S.outsider_gone.clear();
+  S.key_holder.clear();
   if (S.has_ports || S.has_aff) {  // the class masks carry the port fit / affinity: back to the snapshot's
     S.node_ports = S.node_ports0;
     S.h_class_mask = S.h_class_mask0;

@@ -543,6 +543,7 @@ struct Session {
   int64_t n_hot = 0;                                  // keys with key_hot set
   std::vector<int32_t> upd_keys;                      // keys whose node entries an update's events changed
   std::unordered_set<int64_t> node_keys, node_keys0;  // (node << 32 | key) of hot keys on nodes (now / at open)
+  std::unordered_map<int64_t, int32_t> key_holder;     // of those, the ones this cycle's placements took: task << 1 | pipelined
   std::vector<uint8_t> dec_dup;                       // per decision of the cycle: the node was left unchanged
 
   // ---- device

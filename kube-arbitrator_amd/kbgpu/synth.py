@@ -602,7 +602,7 @@ def contended_fixture(seed, nodes=8, jobs=8, tasks=6, queues=3, aff=0.0, ports=0
             "queues": qs, "actions": acts}
 
 
-def contended_dupkey_fixture(seed, ports=0.0):
+def contended_dupkey_fixture(seed, ports=0.0, pending_dups=0.0):
     """contended_fixture with half of the Running pods renamed after a Pending
     pod (PodKey = "<ns>/<name>" shared: a StatefulSet pod recreated while its
     predecessor still runs): preempt pipelines a pod onto the node that holds
@@ -610,7 +610,10 @@ def contended_dupkey_fixture(seed, ports=0.0):
     statement is discarded, unpipeline's RemoveTask removes by key the pod
     that held it (statement.go:156-192, node_info.go:131-157). `ports`: the
     share of pod specs with host ports (contended_fixture), so the holder's
-    ports leave node.Pods() with it and come back with its unevict."""
+    ports leave node.Pods() with it and come back with its unevict.
+    `pending_dups`: the share of Pending pods renamed after another Pending
+    pod of their namespace, so the key's holder can be a pod placed earlier in
+    the same cycle (its node copy Allocated or Pipelined)."""
     fx = contended_fixture(8800 + seed, nodes=6, jobs=10, tasks=6, ports=ports)
     rng = random.Random(seed)
     pods = fx["pods"]
@@ -621,7 +624,13 @@ def contended_dupkey_fixture(seed, ports=0.0):
             if rng.random() < 0.5:
                 q = rng.choice(pend)
                 p["namespace"], p["name"] = q["namespace"], q["name"]
-    fx["name"] = f"contended-dupkey-{seed}" + (f"-ports{ports}" if ports else "")
+    if pending_dups:
+        for p in pend:
+            q = rng.choice(pend)
+            if rng.random() < pending_dups and q is not p and q["namespace"] == p["namespace"]:
+                p["name"] = q["name"]
+    fx["name"] = (f"contended-dupkey-{seed}" + (f"-ports{ports}" if ports else "")
+                  + (f"-pdups{pending_dups}" if pending_dups else ""))
     return fx
 
 

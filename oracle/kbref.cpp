@@ -818,6 +818,7 @@ struct Session {  // framework/session.go:35-61
   std::vector<std::pair<std::string, std::string>> binds;  // (ns/name, node) in dispatch order
   int64_t predicate_calls = 0;
   int64_t dup_discards = 0;  // statement discards whose unpipeline removed another pod holding the key (stats only)
+  int64_t dup_discards_placed = 0;  // ... a holder placed this session (informer Spec.NodeName "", stats only)
   int threads = 1;  // > 1: allocate's node loop evaluated by a team of threads (B-omp CPU baseline only)
   size_t min_parallel_nodes = 512;  // B-omp: smaller clusters walk the nodes on one thread
   std::vector<TaskInfo*> evaluated;  // every task whose node loop ran, in order
@@ -1801,7 +1802,10 @@ struct Statement {
         if (jit != ssn->jobIndex.end()) jit->second->UpdateTaskStatus(t, Pending);
         if (nit != ssn->nodeIndex.end()) {
           TaskInfo** held = nit->second->tasks.find(pod_key(t->pod));
-          if (held && (*held)->uid != t->uid) ssn->dup_discards++;
+          if (held && (*held)->uid != t->uid) {
+            ssn->dup_discards++;
+            if ((*held)->pod->nodeName.empty()) ssn->dup_discards_placed++;
+          }
           nit->second->RemoveTask(t);
         }
         for (auto& eh : ssn->eventHandlers)
@@ -2228,7 +2232,7 @@ static std::string run_session(const Value& fx, bool faithful, bool no_cache, in
   }
   o += "],\"stats\":{\"seconds\":" + kbjson::num(secs) + ",\"predicate_calls\":" + std::to_string(ssn->predicate_calls) +
        ",\"decisions\":" + std::to_string(ssn->decisions.size()) + ",\"dup_discards\":" +
-       std::to_string(ssn->dup_discards) + "}}";
+       std::to_string(ssn->dup_discards) + ",\"dup_discards_placed\":" + std::to_string(ssn->dup_discards_placed) + "}}";
   return o;
 }
 

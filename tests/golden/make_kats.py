@@ -415,47 +415,74 @@ KATS = {
                      "binds": {"ns/p1": "n1", "ns/p2": "n1"},
                      "nodes": {"n1": [[0.0, 64.0 * GI, 0.0], [0.0, 0.0, 0.0], 2]}},
     },
+    # kat_preempt_discard with the key's holder placed in the same statement:
+    # p1 and p2 share the pod key ns/px, pgP needs 3 and p3 (selector matches
+    # nothing) fits nowhere. p1 evicts one of v1..v4 (pgV, 4 running, min 2)
+    # and is pipelined (Releasing 1 -> 0, node_info.go:117-118); p2 evicts
+    # another (gang: 3 still ready) and its pipeline's AddTask finds ns/px
+    # taken by p1's copy (node_info.go:101-106), node unchanged. The discard
+    # runs backwards (statement.go:194-205): unpipeline(p2)'s RemoveTask by key
+    # removes p1's Pipelined copy (Releasing += 1 CPU, node_info.go:145-146),
+    # the second victim's unevict finds it still there, unpipeline(p1)'s
+    # RemoveTask finds no ns/px (an error, no change), the first victim's
+    # unevict as well. n1: Releasing 2 CPU (both victims), 4 pods, nothing
+    # committed.
+    "kat_preempt_discard_placed_holder": {
+        "actions": ["preempt"],
+        "tiers": [[{"name": "priority"}, {"name": "gang"}], [{"name": "drf"}, {"name": "predicates"}]],
+        "nodes": [node("n1", "4", "8Gi")],
+        "pods": [pod(u, "p" + u, {"cpu": "1"}, group="pgV", phase="Running", node="n1")
+                 for u in ("v1", "v2", "v3", "v4")]
+                + [pod("p1", "px", {"cpu": "1"}, group="pgP"), pod("p2", "px", {"cpu": "1"}, group="pgP"),
+                   pod("p3", "p3", {"cpu": "1"}, group="pgP", nodeSelector={"zone": "nowhere"})],
+        "podGroups": [pg("pgV", minMember=2), pg("pgP", minMember=3, created=10)], "queues": Q,
+        "expected": {"decisions": [], "evictions": [], "binds": {},
+                     "nodes": {"n1": [[0, 8 * GI, 0], [2000, 0, 0], 4]}},
+    },
     # The podLister Filter (kube-batch predicates.go:67-89, vendor
     # cache/node_info.go:692-702): a pod whose spec names node n but that is
     # missing from n's pods is left out of n's inter-pod affinity checks.
-    # n1 (3 CPU) runs h (app=db, key ns/px, job pgH at its minimum), v1, v2
-    # (pgV, one above its minimum). Actions preempt then allocate; job order
-    # pgW (created first) then pgP (session_plugins.go JobOrderFn fallback).
-    # preempt (preempt.go:43-171): w's anti-affinity to app=db on the host
-    # fails n1 while h is there; no node, nothing to discard. p (named like h)
-    # evicts one of v1 / v2 (gang lets pgV lose one; the first victim covers
-    # 1 CPU, preempt.go:205-219) and is pipelined: node.AddTask refuses the
-    # taken key (node_info.go:101-106). p2 (selector matches nothing) fails,
-    # pgP stays short of 2 and the statement is discarded (statement.go:
-    # 194-205): unpipeline's RemoveTask by key takes h off n1 (Idle +1 CPU,
-    # node_info.go:131-157), unevict's AddTask finds the victim still there as
-    # Releasing. n1: Idle 1, Releasing 1, pods {v1, v2}.
-    # allocate (allocate.go:40-170): w on n1 — h's spec still names n1 but h
-    # is not in n1's pods, so the Filter drops it and w's anti term matches
-    # nothing: w takes the idle CPU (without the Filter n1 fails and p takes
-    # it instead). pgW is ready and dispatched; p then pipelines onto the
-    # victim's Releasing CPU (the key is free now), p2 fails, pgP is not
-    # ready. Nothing was committed in preempt, so no evictions.
+    # One queue, action preempt; gang decides readiness (its victim fn
+    # disabled), drf picks victims (its job order disabled, so pgP — created
+    # first — precedes pgW: session_plugins.go JobOrderFn's timestamp
+    # fallback). Cluster CPU 7: n1 (3) runs h (app=db, key ns/px, pgH), v1
+    # (pgV, 3 tasks), y1 (pgY, 2 tasks); n2 (4) runs p0 (pgP), v2, v3, y2.
+    # p (key ns/px): drf (drf.go:80-105) takes a preemptee whose job keeps a
+    # share >= pgP's with p, 2/7: on n1 only v1 (pgV 2/7; pgY 1/7, pgH 0).
+    # p evicts v1 and is pipelined: AddTask refuses the taken key
+    # (node_info.go:101-106). p2 (selector matches nothing) fails; pgP (min 3)
+    # has p0 + p = 2 and the statement is discarded (statement.go:194-205):
+    # RemoveTask by key takes h off n1 (Idle +1), v1's unevict finds it still
+    # Releasing. w (anti-affinity to app=db per host) on n1: h's spec still
+    # names n1 but n1's pods lack it, so the Filter drops it and n1 passes;
+    # drf takes y1 (pgY keeps 1/7 = pgW's share with w). w is pipelined, pgW
+    # is ready, the statement commits. Without the Filter n1 fails and w goes
+    # to n2. n1: Idle 1 CPU, Releasing 1 (v1 then y1 released, w took one).
     "kat_podlister_filter": {
-        "actions": ["preempt", "allocate"],
-        "tiers": [[{"name": "priority"}, {"name": "gang"}], [{"name": "drf"}, {"name": "predicates"}]],
-        "nodes": [node("n1", "3", labels={"kubernetes.io/hostname": "n1"})],
+        "actions": ["preempt"],
+        "tiers": [[{"name": "priority"}, {"name": "gang", "disablePreemptable": True}],
+                  [{"name": "drf", "disableJobOrder": True}, {"name": "predicates"}]],
+        "nodes": [node("n1", "3", labels={"kubernetes.io/hostname": "n1"}),
+                  node("n2", "4", labels={"kubernetes.io/hostname": "n2"})],
         "pods": [pod("h", "px", {"cpu": "1"}, group="pgH", phase="Running", node="n1", labels={"app": "db"}),
                  pod("v1", "v1", {"cpu": "1"}, group="pgV", phase="Running", node="n1"),
-                 pod("v2", "v2", {"cpu": "1"}, group="pgV", phase="Running", node="n1"),
+                 pod("y1", "y1", {"cpu": "1"}, group="pgY", phase="Running", node="n1"),
+                 pod("p0", "p0", {"cpu": "1"}, group="pgP", phase="Running", node="n2"),
+                 pod("v2", "v2", {"cpu": "1"}, group="pgV", phase="Running", node="n2"),
+                 pod("v3", "v3", {"cpu": "1"}, group="pgV", phase="Running", node="n2"),
+                 pod("y2", "y2", {"cpu": "1"}, group="pgY", phase="Running", node="n2"),
+                 pod("p", "px", {"cpu": "1"}, group="pgP"),
+                 pod("p2", "p2", {"cpu": "1"}, group="pgP", nodeSelector={"zone": "nowhere"}),
                  pod("w", "w", {"cpu": "1"}, group="pgW",
                      affinity={"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
                          {"labelSelector": {"matchLabels": {"app": "db"}},
-                          "topologyKey": "kubernetes.io/hostname"}]}}),
-                 pod("p", "px", {"cpu": "1"}, group="pgP"),
-                 pod("p2", "p2", {"cpu": "1"}, group="pgP", nodeSelector={"zone": "nowhere"})],
-        "podGroups": [pg("pgH", minMember=1), pg("pgV", minMember=1), pg("pgW", minMember=1, created=10),
-                      pg("pgP", minMember=2, created=20)],
+                          "topologyKey": "kubernetes.io/hostname"}]}})],
+        "podGroups": [pg("pgH", minMember=1), pg("pgV", minMember=1), pg("pgY", minMember=1),
+                      pg("pgP", minMember=3, created=10), pg("pgW", minMember=1, created=20)],
         "queues": Q,
-        "expected": {"decisions": [["w", "n1", "allocate"], ["p", "n1", "pipeline"]],
-                     "evictions": [], "binds": {"ns/w": "n1"},
-                     "ready": {"ns/pgH": True, "ns/pgV": True, "ns/pgW": True, "ns/pgP": False},
-                     "nodes": {"n1": [[0, 64 * GI, 0], [0, 0, 0], 4]}},
+        "expected": {"decisions": [["w", "n1", "pipeline"]], "evictions": [["y1", "w"]], "binds": {},
+                     "nodes": {"n1": [[1000, 64 * GI, 0], [1000, 0, 0], 3],
+                               "n2": [[0, 64 * GI, 0], [0, 0, 0], 4]}},
     },
 }
 

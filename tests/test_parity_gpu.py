@@ -482,6 +482,23 @@ def test_dupkey_statement_discard_ports_parity(seed):
         ssn.close()
 
 
+@pytest.mark.parametrize("seed", [7] + list(range(24)))
+def test_dupkey_pending_holder_parity(seed):
+    """Pending pods sharing a pod key (synth.contended_dupkey_fixture with
+    pending_dups): the key's holder can be a pod placed earlier in the same
+    cycle, whose Allocated or Pipelined copy a discarded statement's
+    RemoveTask by key takes off the node (node_info.go:131-157); its own
+    unpipeline then finds nothing. Seed 7's oracle run has such a discard."""
+    fx = synth.contended_dupkey_fixture(seed, pending_dups=0.6)
+    ref = run_oracle(fx)
+    if seed == 7:
+        assert ref["stats"]["dup_discards_placed"] > 0
+    got, ssn = run_fixture(fx)
+    compare_outputs(ref, got)
+    if ssn:
+        ssn.close()
+
+
 @pytest.mark.parametrize("seed", range(10))
 def test_victim_huge_node_parity(seed):
     """Nodes with more than kMaxNodeCandidates (1024) Running pods, which the
