@@ -37,11 +37,14 @@ parity      = the decision log of the LAST timed cycle of each mode, replayed
 --gpus N    = N ranks: under torchrun its WORLD_SIZE must be N; without a
               launcher bench.py starts the N rank processes itself
 N > 1       = ONE cluster with its node axis sharded over the N GPUs (SURVEY §8e,
-              DESIGN.md §7): rank 0 runs the ordering engine and broadcasts each
-              batch, each rank scans its node rows and resolves the tasks its
-              rows win, RCCL min-reduces over xGMI publish the packed winners;
-              every rank returns the identical decision log (strong scaling;
-              the whole job places decisions_per_cycle per step)
+              DESIGN.md §7), the scan service: rank 0 runs the single-GPU
+              pipeline (ordering engine, in-order commit); each of its scans is
+              an RCCL broadcast of the launch and the commits since the last
+              one, every rank scans its own node rows, an RCCL sum-reduce over
+              xGMI joins the ranks' word masks; the other ranks replay rank 0's
+              commits and every rank returns the identical decision log (strong
+              scaling; the whole job places decisions_per_cycle per step).
+              KBG_OWNER_RESOLVE=1: the owner-resolve protocol instead
 """
 import argparse
 import ctypes
@@ -626,8 +629,11 @@ def main():
         "data": "synthetic (seeded BASELINE config generator, kbgpu/synth.py)",
         "config": {"workload": f"C{cid}: {n_nodes} nodes x {prod['pending']} pending tasks, "
                                f"{prod['jobs']} gang PodGroups, {prod['queues']} proportion queues, default tiers",
-                   "parallelism": (f"node-axis shards x{world} (owner-resolve: batch broadcast, RCCL sum/min-reduce "
-                                   f"of availability and packed winners)") if world > 1 else "single-gpu",
+                   "parallelism": ((f"node-axis shards x{world} (owner-resolve: batch broadcast, RCCL sum/min-reduce "
+                                    f"of availability and packed winners)") if os.environ.get("KBG_OWNER_RESOLVE") == "1"
+                                   else (f"node-axis shards x{world} (scan service: rank 0 commits, RCCL broadcast of "
+                                         f"each launch, every rank scans its rows, RCCL sum-reduce of the word masks)"))
+                                  if world > 1 else "single-gpu",
                    "batch_tasks": base_opts.get("batch_tasks", 8192),
                    "candidates": base_opts.get("candidates", 32)},
         "roofline": kernel_roofline(full, "full_scan"),

@@ -214,7 +214,7 @@ hipError_t launch_scan(const NodeSoA& n, const ScanGeom& g, const uint64_t* clas
 // output may end. The writer row of shape s writes, for the words [w_lo,
 // w_lo + covered) in node order, the pair of 64-node masks {fits Idle or
 // Releasing, fits Idle} (static predicate, pod cap and LessEqual applied)
-// into masks[s * mw + (w - w_lo)], and info[s * splits + part] = covered |
+// into masks[s * mw + (w - mask_w0)], and info[s * info_stride + part0 + part] = covered |
 // kInfoAnyBit (some node of the part's walked words fits) |
 // kCountIncompleteBit (covered < the part's words: the list is cut after the
 // word holding its want-th fit; never with `complete`). Every fit of
@@ -252,6 +252,9 @@ struct FirstFitArgs {
   int32_t splits, split_words;  // the words [w_lo, w_hi) in `splits` parts of split_words, one workgroup
                                 // each (a short batch's walk spread over more CUs); info is per (shape, part)
   int32_t rows;                 // rows per workgroup (firstfit_geometry; at most the kernel's ROWS)
+  int32_t info_stride, part0;   // info[s * info_stride + part0 + part] (a single launch: splits, 0; a rank of
+                                // the scan service: every rank's parts, this rank's first)
+  int32_t mask_w0;              // the global word masks[s * mw] holds (w_lo; 0 under the scan service)
   int32_t runs;                 // full-scan with inline shapes: launch row l belongs to the slot s with
                                 // run_end[s - 1] <= l < run_end[s] and the run's last row writes the slot
                                 // (no row -> shape map to read: rows of a slot are identical evaluations)
@@ -296,6 +299,7 @@ struct FitArgs {
   const FitQuery* q;
   int32_t nq, cap_check;
   int32_t* out;                // [nq][4]: entries, negative cpu, memory, GPU deltas
+  int32_t tab_lo, tab_n;       // the global nodes the table holds (a shard of the scan service: its own)
 };
 hipError_t launch_fitdelta(const FitArgs& a, hipStream_t stream);
 hipError_t launch_mask_apply(uint64_t* class_mask, const MaskDelta* deltas, int32_t n_deltas, hipStream_t stream);

@@ -363,7 +363,7 @@ __global__ __launch_bounds__(64 * kFfWaves, kFfWaves / 4 * KBG_FF_WGS_PER_CU) vo
     __syncthreads();
     if (wave == 0 && lane < ROWS && (s_map[lane] & kRowWriter)) {
       const uint32_t sh = s_map[lane] & ~kRowWriter;
-      a.info[sh * a.splits + part] = 0u;
+      a.info[sh * a.info_stride + a.part0 + part] = 0u;
       if (a.avail) a.avail[sh] = 0u;
     }
     return;
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(64 * kFfWaves, kFfWaves / 4 * KBG_FF_WGS_PER_CU) vo
     for (int i = 0; i < RPW; ++i) {
       const int j = wave + i * kFfWaves;
       if (j >= ROWS || done[i]) continue;  // wave-uniform
-      MaskPair* out = a.masks + (size_t)(s_map[j] & ~kRowWriter) * a.mw + (r0 - a.w_lo);
+      MaskPair* out = a.masks + (size_t)(s_map[j] & ~kRowWriter) * a.mw + (r0 - a.mask_w0);
 #pragma unroll 1
       for (int k0 = 0; k0 < nw; k0 += 64) {
         const int k = k0 + lane;
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(64 * kFfWaves, kFfWaves / 4 * KBG_FF_WGS_PER_CU) vo
     const uint32_t sh = s_map[j] & ~kRowWriter;
     // covered: the words written; a row whose walk ended with its list not
     // full covered every word of the walk (EARLY_EXIT: the rounds walked)
-    a.info[sh * a.splits + part] =
+    a.info[sh * a.info_stride + a.part0 + part] =
         covered[i] | (covered[i] < (uint32_t)tw ? kCountIncompleteBit : 0u) | (found[i] ? kInfoAnyBit : 0u);
     if (a.avail) a.avail[sh] = found[i] ? a.avail_bit : 0u;
   }
@@ -584,13 +584,15 @@ __global__ __launch_bounds__(256) void kbg_fitdelta_kernel(FitArgs a) {
   __syncthreads();
   const int32_t* ni = reinterpret_cast<const int32_t*>(a.nodes + 6 * (size_t)a.stride);
   int32_t c_nodes = 0, c_cpu = 0, c_mem = 0, c_gpu = 0;
-  for (int n = threadIdx.x; n < fq.end; n += blockDim.x) {
+  const int n_end = min(fq.end, a.tab_lo + a.tab_n);
+  for (int n = a.tab_lo + threadIdx.x; n < n_end; n += blockDim.x) {
     if (!((a.class_mask[(size_t)fq.cls * a.W + (n >> 6)] >> (n & 63)) & 1ull)) continue;  // static predicate
     const int e1 = a.hoff[n + 1];
     int e = a.hoff[n];
     while (e < e1 && (a.hk[e] & 0x7fffffff) < fq.point) ++e;  // decisions before the evaluation stay applied
-    if (a.cap_check && ni[n] - (e1 - e) >= ni[a.stride + n]) continue;  // pod cap then (predicates.go:125-127)
-    double ic = a.nodes[n], im = a.nodes[a.stride + n], ig = a.nodes[2 * (size_t)a.stride + n];
+    const int r = n - a.tab_lo;  // the node's row in this table
+    if (a.cap_check && ni[r] - (e1 - e) >= ni[a.stride + r]) continue;  // pod cap then (predicates.go:125-127)
+    double ic = a.nodes[r], im = a.nodes[a.stride + r], ig = a.nodes[2 * (size_t)a.stride + r];
     for (int x = e; x < e1; ++x)
       if (!(a.hk[x] & 0x80000000)) {  // the first undone Allocate: Idle before it
         ic = a.hold[3 * (size_t)x];

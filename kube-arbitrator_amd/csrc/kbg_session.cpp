@@ -601,7 +601,7 @@ int32_t soa_stride(const Session& S) { return std::max(64, (S.tab_n + 63) / 64 *
 // word, then (16-B aligned) per slot `mw` word-mask pairs, then per slot the
 // owner-resolve availability. mw = the words one launch covers (this rank's
 // words when the session is sharded).
-int32_t fused_mask_words(const Session& S) { return std::max(1, S.comm ? S.Wl : S.W); }
+int32_t fused_mask_words(const Session& S) { return std::max(1, S.owner ? S.Wl : S.W); }
 inline size_t fused_mask_off(int32_t K) { return ((size_t)K * kbg::kFfMaxSplits + 3) & ~(size_t)3; }
 inline size_t fused_avail_off(int32_t K, int32_t mw) { return fused_mask_off(K) + (size_t)K * mw * 4; }
 inline size_t fused_down_words(int32_t K, int32_t mw) { return fused_avail_off(K, mw) + (size_t)K; }
@@ -754,10 +754,11 @@ thread_local Trace* t_trace = nullptr;  // the committer's KBG_TRACE timeline, i
 void trace_add(const char* what, int64_t v = 0);
 
 constexpr int64_t kFfTimeEvery = 4;  // fused launches: one in this many carries start / stop events
+kbg_status svc_launch(Session& S, kbg::Stage& sg, kbg::FirstFitArgs& a, int32_t G, int32_t base);
 kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   trace_add("l.begin", G);
   const int32_t Gp = kbg::kbg_pad_rows(G);  // Grouper::build padded the rows
-  if (!S.comm || S.owner) {
+  if (!S.comm || S.owner || S.svc) {
     // one launch: kbg_firstfit_kernel takes the shapes from its arguments
     // (or the stage's mapped buffer) and writes each shape's info word and
     // word masks straight into the other one; this process's words only
@@ -771,8 +772,9 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
     a.n_shapes = sg.n_slots;
     a.n_nodes = S.n_nodes;
     a.W = S.W;
-    a.w_lo = S.owner ? S.shard * S.Wl : 0;
-    a.w_hi = S.owner ? std::min(S.W, (S.shard + 1) * S.Wl) : S.W;
+    const bool own_words = S.owner || S.svc;
+    a.w_lo = own_words ? std::min(S.W, S.shard * S.Wl) : 0;
+    a.w_hi = own_words ? std::min(S.W, (S.shard + 1) * S.Wl) : S.W;
     a.mw = fused_mask_words(S);
     a.tab_lo = S.tab_lo;
     a.tab_n = S.tab_n;
@@ -802,6 +804,9 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
       a.splits = 1;
       a.split_words = 0;
     }
+    a.info_stride = a.splits;
+    a.part0 = 0;
+    a.mask_w0 = a.w_lo;
     sg.splits = a.splits;
     if (sg.n_slots <= kbg::kInlineShapes) {
       std::copy(sg.h_shapes, sg.h_shapes + sg.n_slots, a.inl);
@@ -820,6 +825,7 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
     } else if (sg.h_rowshape && !(a.row_shape = dev_ptr(S, sg.h_rowshape))) {
       return fail(KBG_E_HIP, "hipHostGetDevicePointer of a stage buffer failed");
     }
+    if (S.svc) return svc_launch(S, sg, a, G, base);
     a.info = dev_ptr(S, sg.h_down);
     a.masks = reinterpret_cast<kbg::MaskPair*>(dev_ptr(S, sg.h_down + fused_mask_off(S.K)));
     if (!a.info || !a.masks) return fail(KBG_E_HIP, "hipHostGetDevicePointer of a stage buffer failed");
@@ -932,7 +938,7 @@ kbg_status device_wait(Session& S, kbg::Stage& sg) {
     HIP_TRY(hipEventElapsedTime(&ms, sg.ev[2], sg.ev[3]));
     S.stats.select_kernel_ms += ms;
   }
-  if (S.comm && !S.owner) {
+  if (S.comm && !S.owner && !sg.fused) {
     HIP_TRY(hipEventElapsedTime(&ms, sg.ev[4], sg.ev[5]));
     S.stats.exchange_ms += ms;
   }
@@ -954,6 +960,144 @@ kbg_status device_drop(Session& S, kbg::Stage& sg) {
 kbg_status device_scan(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   kbg_status st = device_launch(S, sg, G, base);
   return st != KBG_OK ? st : device_wait(S, sg);
+}
+
+// ============================================ the scan service: transport
+// Sharded allocate as ONE committer: rank 0 runs the single-GPU
+// pipeline (ordering engine, in-order commit, overlapped and reused scans)
+// and every scan it launches is a message to the other ranks: the launch's
+// arguments, the node rows and class-mask words its commits wrote since the
+// last message (every rank writes the rows it holds), and the committed
+// outcomes (each rank replays them into its mirror, decision log and engine,
+// beside its scans). Every rank runs the fused kernel over its own words into
+// a zeroed (slot, rank) info array and a [slot][W] mask array; one summing
+// all-reduce over the ranks (disjoint words: the sum is the union) gives rank
+// 0 the whole table's lists, joined in node order like a split launch's
+// parts. Rank 0's collectives are enqueued on its stream (no host wait); the
+// other ranks wait for each message.
+}  // namespace
+namespace kbg {
+struct SvcLink {
+  virtual ~SvcLink() = default;
+  // rank 0: msg[0 .. msg[1]) to every rank (may return before it is sent)
+  virtual kbg_status send(Session& S, const uint32_t* msg) = 0;
+  // ranks != 0: the next message
+  virtual kbg_status recv(Session& S, std::vector<uint32_t>& msg) = 0;
+  // after this rank's launch: the info words [0, info) and mask words [0, masks) of d_svc
+  // summed over the ranks; rank 0 then has them in sg->h_down (stream-ordered before its
+  // next event)
+  virtual kbg_status sum(Session& S, kbg::Stage* sg, size_t info, size_t masks) = 0;
+  // host words summed over the ranks, in place (synchronous)
+  virtual kbg_status sum_host(Session& S, uint32_t* buf, size_t n) = 0;
+};
+}  // namespace kbg
+namespace {
+using kbg::SvcLink;
+
+enum : uint32_t { kSvcLaunch = 0, kSvcEnd = 1, kSvcAbort = 2, kSvcState = 3 };
+constexpr size_t kSvcHead = 16;          // header words: kind, words, nodes, masks, outcomes, args, shapes, rowshape,
+                                         // status, G, slots
+constexpr size_t kSvcMaxWords = 1u << 19;  // one message (2 MB); a longer state goes out in kSvcState chunks
+constexpr size_t kSvcNodeWords = sizeof(kbg::NodeDelta) / 4, kSvcMaskWords = sizeof(kbg::MaskDelta) / 4;
+static_assert(sizeof(kbg::NodeDelta) % 4 == 0 && sizeof(kbg::MaskDelta) % 4 == 0, "message words");
+
+inline void svc_put(std::vector<uint32_t>& m, const void* p, size_t bytes) {
+  const size_t o = m.size();
+  m.resize(o + (bytes + 3) / 4, 0u);
+  if (bytes) std::memcpy(&m[o], p, bytes);
+}
+
+// Rank 0: the pending state (rows, mask words, outcomes) in messages of kind
+// `kind` (kSvcState chunks first when it does not fit into one message with
+// `reserve` more words); leaves the last part for the caller when `keep` is set.
+kbg_status svc_flush_state(Session& S, std::vector<uint32_t>& m, size_t reserve, bool keep, uint32_t kind,
+                           uint32_t status) {
+  size_t ni = 0, mi = 0, oi = 0;
+  for (;;) {
+    const size_t room = kSvcMaxWords - kSvcHead - reserve;
+    const size_t nn = std::min(S.svc_nodes.size() - ni, room / kSvcNodeWords);
+    const size_t nm = std::min(S.svc_masks.size() - mi, (room - nn * kSvcNodeWords) / kSvcMaskWords);
+    const size_t no = std::min((S.svc_out.size() - oi) / 2,
+                               (room - nn * kSvcNodeWords - nm * kSvcMaskWords) / 2);
+    const bool last = ni + nn == S.svc_nodes.size() && mi + nm == S.svc_masks.size() && oi + 2 * no == S.svc_out.size();
+    m.assign(kSvcHead, 0u);
+    m[0] = last ? kind : kSvcState;
+    m[2] = (uint32_t)nn;
+    m[3] = (uint32_t)nm;
+    m[4] = (uint32_t)no;
+    m[8] = status;
+    svc_put(m, S.svc_nodes.data() + ni, nn * sizeof(kbg::NodeDelta));
+    svc_put(m, S.svc_masks.data() + mi, nm * sizeof(kbg::MaskDelta));
+    svc_put(m, S.svc_out.data() + oi, no * 8);
+    ni += nn;
+    mi += nm;
+    oi += 2 * no;
+    if (last && keep) break;  // the caller appends its part and sends
+    m[1] = (uint32_t)m.size();
+    if (kbg_status st = S.svc->send(S, m.data()); st != KBG_OK) return st;
+    if (last) break;
+  }
+  S.svc_nodes.clear();
+  S.svc_masks.clear();
+  S.svc_out.clear();
+  return KBG_OK;
+}
+
+// Rank 0's part of a scan: the launch message, its own words, the sum.
+kbg_status svc_launch(Session& S, kbg::Stage& sg, kbg::FirstFitArgs& a, int32_t G, int32_t base) {
+  const int32_t ns = sg.n_slots;
+  // the arguments go out before this rank's words are set in them (each rank sets its own)
+  const size_t args_w = (sizeof(kbg::FirstFitArgs) + 3) / 4;
+  const size_t shapes_w = a.shapes ? ((size_t)ns * sizeof(kbg::TaskRec) + 3) / 4 : 0;
+  const size_t rows_w = a.row_shape ? (size_t)G : 0;
+  thread_local std::vector<uint32_t> m;
+  if (kbg_status st = svc_flush_state(S, m, args_w + shapes_w + rows_w, true, kSvcLaunch, 0); st != KBG_OK) return st;
+  m[5] = (uint32_t)args_w;
+  m[6] = (uint32_t)shapes_w;
+  m[7] = (uint32_t)rows_w;
+  m[9] = (uint32_t)G;
+  m[10] = (uint32_t)ns;
+  // payload order: args, shapes, rows, then the state svc_flush_state put
+  std::vector<uint32_t> state(m.begin() + kSvcHead, m.end());
+  m.resize(kSvcHead);
+  svc_put(m, &a, sizeof(kbg::FirstFitArgs));
+  if (shapes_w) svc_put(m, sg.h_shapes, (size_t)ns * sizeof(kbg::TaskRec));
+  if (rows_w) svc_put(m, sg.h_rowshape, (size_t)G * 4);
+  m.insert(m.end(), state.begin(), state.end());
+  m[1] = (uint32_t)m.size();
+  if (kbg_status st = S.svc->send(S, m.data()); st != KBG_OK) return st;
+  // this rank's words, every rank's info column and the whole mask width
+  a.w_lo = std::min(S.W, S.shard * S.Wl);
+  a.w_hi = std::min(S.W, (S.shard + 1) * S.Wl);
+  a.splits = 1;
+  a.split_words = a.w_hi - a.w_lo;
+  a.info_stride = S.R;
+  a.part0 = S.shard;
+  a.mask_w0 = 0;
+  a.mw = S.W;
+  a.complete = a.w_hi - a.w_lo <= kbg::kFfRoundWords ? 1 : 0;
+  a.avail = nullptr;
+  a.info = S.d_svc;
+  a.masks = reinterpret_cast<kbg::MaskPair*>(S.d_svc + fused_mask_off(S.K));
+  const size_t info_w = (size_t)ns * S.R, mask_w = (size_t)ns * S.W * 4;
+  HIP_TRY(hipMemsetAsync(S.d_svc, 0, info_w * 4, S.stream));
+  HIP_TRY(hipMemsetAsync(a.masks, 0, mask_w * 4, S.stream));
+  sg.timed = !S.untimed_launches && S.ff_launch_seq++ % kFfTimeEvery == 0;
+  HIP_TRY(kbg::launch_firstfit(a, S.int_mode ? 1 : 0, S.stream, sg.timed ? sg.ev[0] : nullptr,
+                               sg.timed ? sg.ev[1] : nullptr));
+  trace_add("l.firstfit");
+  if (kbg_status st = S.svc->sum(S, &sg, info_w, mask_w); st != KBG_OK) return st;
+  HIP_TRY(hipEventRecord(sg.ev[6], S.stream));
+  sg.splits = S.R;  // device_wait joins the ranks' parts in node order
+  sg.fused = true;
+  sg.G = G;
+  sg.base = base;
+  sg.inflight = true;
+  return KBG_OK;
+}
+
+kbg_status svc_sum_counts(Session& S, int32_t* counts, size_t n) {
+  return S.svc->sum_host(S, reinterpret_cast<uint32_t*>(counts), n);
 }
 
 // Writes the rows of the nodes touched by the last commits back to HBM (only
@@ -988,6 +1132,7 @@ kbg_status push_mask_deltas(Session& S) {
       S.h_mdeltas[k] = kbg::MaskDelta{idx, 0u, S.h_class_mask[idx]};
       S.mask_dirty_flag[idx] = 0;
     }
+    if (S.svc) S.svc_masks.insert(S.svc_masks.end(), S.h_mdeltas, S.h_mdeltas + cnt);  // for every rank's table
     const kbg::MaskDelta* md = dev_ptr(S, S.h_mdeltas);
     if (!md) return fail(KBG_E_HIP, "hipHostGetDevicePointer of the mask-delta buffer failed");
     HIP_TRY(kbg::launch_mask_apply(S.d_class_mask, md, cnt, S.stream));  // read in place
@@ -1001,6 +1146,13 @@ kbg_status push_mask_deltas(Session& S) {
 kbg_status push_deltas(Session& S, const std::vector<int32_t>& touched) {
   kbg_status st = push_mask_deltas(S);
   if (st != KBG_OK) return st;
+  if (S.svc)  // the scan service: every rank's rows go out with the next message (each rank writes its own)
+    for (const int32_t n : touched) {
+      kbg::NodeDelta d{};
+      d.node = n;
+      device_row(S, n, &d.idle[0], &d.idle[1], &d.idle[2], &d.rel[0], &d.rel[1], &d.rel[2], &d.ntasks, &d.maxtasks);
+      S.svc_nodes.push_back(d);
+    }
   size_t i = 0;
   while (i < touched.size()) {
     if ((st = stage_acquire(S)) != KBG_OK) return st;
@@ -1185,6 +1337,12 @@ struct Resolver {
   std::vector<int32_t> cursor;
   std::vector<int32_t> shape_skip, skip_stamp;
   int32_t skip_gen = 0;
+  // per shape, the first node not yet found infeasible this action (nullptr:
+  // off). Nodes only lose room while an allocate runs (a pod-affinity gain
+  // resets its class's shapes), so what a shape rejected under one scan
+  // stays rejected under every later scan: a fresh stage's cursor starts
+  // there instead of re-checking the nodes the earlier batches filled.
+  int32_t* floor = nullptr;
   void reset(const kbg::Stage& stage) {
     sg = &stage;
     base = stage.base;
@@ -1228,6 +1386,8 @@ struct Resolver {
       sh = sg->row_shape[g];
       if (skip_stamp[sh] == skip_gen) k = std::max(k, shape_skip[sh]);  // what earlier rows of the shape rejected
     }
+    int32_t* const fl = floor ? floor + S.task_shape[t] : nullptr;
+    if (fl && k < *fl) k = *fl;
     int res = -1;
     int64_t steps = 0, rechecks = 0;
     // A word's candidates are taken lowest first by clearing bits (a short
@@ -1283,6 +1443,7 @@ struct Resolver {
       shape_skip[sh] = k;
       skip_stamp[sh] = skip_gen;
     }
+    if (fl && res != RES_PANIC) *fl = k;
     if (res >= 0) return res;
     if (info & kbg::kCountIncompleteBit) return RES_TRUNC;
     *node = -1;
@@ -2957,7 +3118,8 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   if ((st = dalloc(S, &S.d_class_mask, (size_t)S.n_classes * S.W)) ||
       (st = dalloc(S, &S.d_up, S.comm ? up_cap : 1)) ||
       (st = dalloc(S, &S.d_bits, S.comm ? (size_t)S.R * 2 * S.K * kbg::kbg_slot_words(S.Wl) : 1)) ||
-      (st = dalloc(S, &S.d_down, d_down_cap)))
+      (st = dalloc(S, &S.d_down, d_down_cap)) ||
+      (st = dalloc(S, &S.d_svc, S.comm ? fused_cap : 1)))  // the scan service's summed launch results
     return st;
   for (kbg::Stage& g : S.stages) {
     if ((st = host_alloc((void**)&g.h_up, up_cap)) || (st = host_alloc((void**)&g.h_down, down_cap * 4))) return st;
@@ -3252,6 +3414,7 @@ struct LastEval {
 // undone, for sessions whose predicate at an evaluation point is the static
 // mask plus the pod cap (no host ports, no pod affinity, no nil Node) and
 // whose whole node table is local.
+kbg_status svc_sum_counts(Session& S, int32_t* counts, size_t n);
 kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, const std::vector<Res>& dec_old,
                              const std::vector<LastEval>& last, const std::vector<int32_t>& jobs) {
   std::vector<int32_t> qj;
@@ -3315,9 +3478,11 @@ kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, c
   HIP_TRY(hipMemcpyAsync(S.fit_d, S.fit_h, bytes, hipMemcpyHostToDevice, S.stream));
   kbg::FitArgs a{S.d_nodes.idle_cpu, soa_stride(S), S.W, S.d_class_mask, (const int32_t*)S.fit_d,
                  (const int32_t*)(S.fit_d + o_hk), (const double*)(S.fit_d + o_hold),
-                 (const kbg::FitQuery*)(S.fit_d + o_q), Q, S.pred_active ? 1 : 0, fit_out};
+                 (const kbg::FitQuery*)(S.fit_d + o_q), Q, S.pred_active ? 1 : 0, fit_out, S.tab_lo, S.tab_n};
   HIP_TRY(kbg::launch_fitdelta(a, S.stream));
   HIP_TRY(hipStreamSynchronize(S.stream));
+  if (S.svc)  // each rank counted its own nodes
+    if (kbg_status st = svc_sum_counts(S, S.fit_out, (size_t)Q * 4); st != KBG_OK) return st;
   for (int32_t i = 0; i < Q; ++i) {
     Session::FitCounts& fc = S.fit[qj[i]];
     fc.nodes = S.fit_out[4 * i];
@@ -3336,7 +3501,7 @@ kbg_status compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, 
     if (S.committed_ready[j] < S.jobs_in[j].min_available) jobs.push_back(j);
   if (jobs.empty()) return KBG_OK;
   const bool host_only = getenv("KBG_HOST_FITDELTA") != nullptr;  // read per cycle (A/B parity tests)
-  if (S.stream && !S.comm && !S.has_ports && !S.has_aff && !S.any_nil && !host_only)
+  if (S.stream && (!S.comm || S.svc) && !S.has_ports && !S.has_aff && !S.any_nil && !host_only)
     return fit_deltas_device(S, dec, dec_old, last, jobs);
   std::sort(jobs.begin(), jobs.end(), [&](int32_t a, int32_t b) { return last[a].before > last[b].before; });
   std::vector<Res> idle = S.idle, rel = S.rel;
@@ -3889,6 +4054,14 @@ struct Logger {
   }
 };
 
+// allocate_cycle under the scan service: the FitError inputs it leaves for
+// allocate_svc_root (same thread), which counts after the end message
+struct SvcFit {
+  std::vector<uint64_t> dec_oldp;
+  std::vector<LastEval> last;
+};
+thread_local SvcFit g_svc_fit;
+
 kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out) {
   if (S.allocated || S.backfilled || S.preempted)
     return fail(KBG_E_INVALID, "allocate runs once per cycle, before backfill and preempt; call kbg_session_reset");
@@ -3915,6 +4088,15 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   kbg_status result = KBG_OK;
   Grouper grouper(S);
   Resolver rs{S, mark};
+  static const bool use_floor = [] {
+    const char* e = getenv("KBG_SHAPE_FLOOR");
+    return !e || std::atoi(e) != 0;
+  }();
+  std::vector<int32_t> shape_floor;
+  if (use_floor) {
+    shape_floor.assign(std::max(1, S.n_shapes), 0);
+    rs.floor = shape_floor.data();
+  }
   // The log side of the walk (decision log, gang dispatch, FitError
   // bookkeeping) on a thread of its own, unless host ports or colliding pod
   // keys need the pre-commit port rows (then inline, below).
@@ -4063,7 +4245,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     const char* e = getenv("KBG_RESCAN_ALL");
     return !(e && e[0] == '0');
   }();
-  const bool reuse_ok = !S.opts.full_scan && !S.comm && !S.has_aff && !no_reuse;
+  const bool reuse_ok = !S.opts.full_scan && (!S.comm || S.svc) && !S.has_aff && !no_reuse;
   // the predictor's run-ahead past the first cut (Pipe::depth / kmax; 0 = unchanged)
   static const int32_t cont_depth = [] {
     const char* e = getenv("KBG_CONT_DEPTH");
@@ -4358,6 +4540,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
           seen_shapes.push_back(sh);
         }
       }
+      if (S.svc) {  // the scan service: every rank replays the committed outcomes
+        S.svc_out.push_back((uint32_t)t);
+        S.svc_out.push_back(ok ? ((uint32_t)node << 1 | (kind == KBG_KIND_PIPELINE ? 1u : 0u)) : ~0u);
+      }
       if (ok) {
         const Res old = kind == KBG_KIND_ALLOCATE ? S.idle[node] : S.rel[node];
         if (S.has_ports)
@@ -4395,7 +4581,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         // point and the next batch is scanned against the new masks.
         for (int32_t c : S.aff_gain_classes) {
           S.aff_gain_flag[c] = 0;
-          for (int32_t sh : S.affm->class_shapes[c]) failed[sh].store(0, std::memory_order_relaxed);
+          for (int32_t sh : S.affm->class_shapes[c]) {
+            failed[sh].store(0, std::memory_order_relaxed);
+            if (rs.floor) rs.floor[sh] = 0;  // the class's nodes may fit again
+          }
         }
         S.aff_gain_classes.clear();
         cut = i + 1;
@@ -4505,7 +4694,12 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   ctr.add("logged");
   if (kbg_status st = flush(); st != KBG_OK) return st;  // the cycle's last write-back
   HIP_TRY(hipStreamSynchronize(S.stream));
-  if (kbg_status st = compute_fit_deltas(S, dec, dec_old, dec_oldp, last); st != KBG_OK) return st;
+  if (S.svc) {  // the scan service: every rank counts its nodes after the end message (allocate_svc_root)
+    g_svc_fit.dec_oldp = std::move(dec_oldp);
+    g_svc_fit.last = std::move(last);
+  } else if (kbg_status st = compute_fit_deltas(S, dec, dec_old, dec_oldp, last); st != KBG_OK) {
+    return st;
+  }
   ctr.add("fit");
   if (S.has_aff && getenv("KBG_PROFILE_AFF"))
     fprintf(stderr, "[kbg aff] aff_place %llu calls, %.1f cycles/call, %llu bit recomputes, mask words dirty %zu\n",
@@ -5026,6 +5220,335 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
   S.stats.exchange_ms = io.ms;
   S.allocated = true;
   S.stats.allocate_ms = ms_since(t0);
+  return copy_log(S, out, cap, n_out, result);
+}
+
+// ============================================ the scan service: rank 0 and the other ranks
+// The library's transport: RCCL on the session's stream. Rank 0 stages a
+// message in a pinned ring slot and enqueues its copy and the broadcasts
+// (header, then payload); the other ranks wait for the header to learn the
+// payload's length.
+struct RcclSvc final : SvcLink {
+  Session& S;
+  static constexpr int kRing = 4;
+  uint32_t* d_msg = nullptr;
+  uint32_t* h_ring[kRing] = {};
+  hipEvent_t ev_ring[kRing] = {};
+  bool used[kRing] = {};
+  int slot = 0;
+  uint32_t* h_recv = nullptr;
+  explicit RcclSvc(Session& s) : S(s) {}
+  ~RcclSvc() override {
+    if (S.stream) (void)hipStreamSynchronize(S.stream);  // no enqueued copy still reads a ring slot
+    if (d_msg) (void)hipFree(d_msg);
+    for (int i = 0; i < kRing; ++i) {
+      if (h_ring[i]) (void)hipHostFree(h_ring[i]);
+      if (ev_ring[i]) (void)hipEventDestroy(ev_ring[i]);
+    }
+    if (h_recv) (void)hipHostFree(h_recv);
+  }
+  kbg_status init() {
+    HIP_TRY(hipMalloc((void**)&d_msg, kSvcMaxWords * 4));
+    if (S.shard == 0) {
+      for (int i = 0; i < kRing; ++i) {
+        HIP_TRY(hipHostMalloc((void**)&h_ring[i], kSvcMaxWords * 4, hipHostMallocDefault));
+        HIP_TRY(hipEventCreateWithFlags(&ev_ring[i], hipEventDisableTiming));
+      }
+    } else {
+      HIP_TRY(hipHostMalloc((void**)&h_recv, kSvcMaxWords * 4, hipHostMallocDefault));
+    }
+    return KBG_OK;
+  }
+  kbg_status bcast(uint32_t* d, size_t n) {
+    const ncclResult_t nr = ncclBroadcast(d, d, n, ncclUint32, 0, S.comm->nccl, S.stream);
+    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclBroadcast: ") + ncclGetErrorString(nr));
+    return KBG_OK;
+  }
+  kbg_status send(Session&, const uint32_t* msg) override {
+    const size_t n = msg[1];
+    if (n < kSvcHead || n > kSvcMaxWords) return fail(KBG_E_INVALID, "internal: scan service message size");
+    const int i = slot;
+    slot = (slot + 1) % kRing;
+    if (used[i]) HIP_TRY(hipEventSynchronize(ev_ring[i]));  // its last copy has been read
+    std::memcpy(h_ring[i], msg, n * 4);
+    HIP_TRY(hipMemcpyAsync(d_msg, h_ring[i], n * 4, hipMemcpyHostToDevice, S.stream));
+    HIP_TRY(hipEventRecord(ev_ring[i], S.stream));
+    used[i] = true;
+    if (kbg_status st = bcast(d_msg, kSvcHead); st != KBG_OK) return st;
+    if (n > kSvcHead) return bcast(d_msg + kSvcHead, n - kSvcHead);
+    return KBG_OK;
+  }
+  kbg_status recv(Session&, std::vector<uint32_t>& msg) override {
+    if (kbg_status st = bcast(d_msg, kSvcHead); st != KBG_OK) return st;
+    HIP_TRY(hipMemcpyAsync(h_recv, d_msg, kSvcHead * 4, hipMemcpyDeviceToHost, S.stream));
+    if (kbg_status st = comm_sync(S); st != KBG_OK) return st;
+    const size_t n = h_recv[1];
+    if (n < kSvcHead || n > kSvcMaxWords) return fail(KBG_E_INVALID, "internal: scan service message size");
+    if (n > kSvcHead) {
+      if (kbg_status st = bcast(d_msg + kSvcHead, n - kSvcHead); st != KBG_OK) return st;
+      HIP_TRY(hipMemcpyAsync(h_recv + kSvcHead, d_msg + kSvcHead, (n - kSvcHead) * 4, hipMemcpyDeviceToHost, S.stream));
+      if (kbg_status st = comm_sync(S); st != KBG_OK) return st;
+    }
+    msg.assign(h_recv, h_recv + n);
+    return KBG_OK;
+  }
+  kbg_status sum(Session&, kbg::Stage* sg, size_t info, size_t masks) override {
+    uint32_t* dm = S.d_svc + fused_mask_off(S.K);
+    ncclGroupStart();
+    ncclResult_t nr = ncclAllReduce(S.d_svc, S.d_svc, info, ncclUint32, ncclSum, S.comm->nccl, S.stream);
+    const ncclResult_t nr2 = ncclAllReduce(dm, dm, masks, ncclUint32, ncclSum, S.comm->nccl, S.stream);
+    const ncclResult_t nr3 = ncclGroupEnd();
+    if (nr == ncclSuccess) nr = nr2 != ncclSuccess ? nr2 : nr3;
+    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+    if (sg) {
+      HIP_TRY(hipMemcpyAsync(sg->h_down, S.d_svc, info * 4, hipMemcpyDeviceToHost, S.stream));
+      HIP_TRY(hipMemcpyAsync(sg->h_down + fused_mask_off(S.K), dm, masks * 4, hipMemcpyDeviceToHost, S.stream));
+    }
+    return KBG_OK;
+  }
+  kbg_status sum_host(Session&, uint32_t* buf, size_t n) override {
+    for (size_t o = 0; o < n; o += kSvcMaxWords) {  // through the message buffer
+      const size_t c = std::min(n - o, kSvcMaxWords);
+      uint32_t* h = S.shard == 0 ? h_ring[0] : h_recv;
+      if (S.shard == 0 && used[0]) HIP_TRY(hipEventSynchronize(ev_ring[0]));
+      std::memcpy(h, buf + o, c * 4);
+      HIP_TRY(hipMemcpyAsync(d_msg, h, c * 4, hipMemcpyHostToDevice, S.stream));
+      const ncclResult_t nr = ncclAllReduce(d_msg, d_msg, c, ncclUint32, ncclSum, S.comm->nccl, S.stream);
+      if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+      HIP_TRY(hipMemcpyAsync(h, d_msg, c * 4, hipMemcpyDeviceToHost, S.stream));
+      if (kbg_status st = comm_sync(S); st != KBG_OK) return st;
+      std::memcpy(buf + o, h, c * 4);
+    }
+    return KBG_OK;
+  }
+};
+
+// The sessions whose allocate runs the scan service: sharded over a
+// communicator (at most kFfMaxSplits ranks: one info word per (slot, rank)
+// in the staging). KBG_OWNER_RESOLVE=1 selects the owner-resolve protocol
+// instead; KBG_SCAN_SERVICE=1 runs the service on a one-rank communicator
+// (its RCCL path on a one-GPU box).
+bool scan_service_ok(const Session& S) {
+  const char* oe = getenv("KBG_OWNER_RESOLVE");  // (read per call: the tests switch it)
+  const char* fe = getenv("KBG_SCAN_SERVICE");
+  const bool owner = oe && oe[0] == '1', force = fe && fe[0] == '1';
+  return S.comm && S.shard >= 0 && !owner && (S.R > 1 || force) && S.R <= kbg::kFfMaxSplits;
+}
+
+// Rank 0: the single-GPU allocate with every scan served by all ranks, then
+// the end message (the rest of the state and the cycle's status).
+kbg_status allocate_svc_root(Session& S, SvcLink& link, kbg_decision* out, int32_t cap, int32_t* n_out) {
+  if (S.allocated || S.backfilled || S.preempted)  // (every rank returns this without a message)
+    return fail(KBG_E_INVALID, "allocate runs once per cycle, before backfill and preempt; call kbg_session_reset");
+  S.svc = &link;
+  S.svc_nodes.clear();
+  S.svc_masks.clear();
+  S.svc_out.clear();
+  const kbg_status st = allocate_cycle(S, out, cap, n_out);
+  const std::string err = g_err;
+  kbg_status st2 = KBG_OK;
+  if (st == KBG_E_HIP || st == KBG_E_RCCL || st == KBG_E_NOMEM) {
+    comm_abort(S.comm);  // the other ranks are in a collective this rank may never join
+  } else {
+    thread_local std::vector<uint32_t> m;
+    st2 = svc_flush_state(S, m, 0, false, kSvcEnd, (uint32_t)st);
+    if (st2 == KBG_OK) st2 = comm_sync(S);
+    // FitError counts: each rank its own nodes, summed (allocate_serve does the same after the end message)
+    if (st2 == KBG_OK && (st == KBG_OK || st == KBG_E_REF_PANIC))
+      st2 = compute_fit_deltas(S, S.dec, S.dec_old_buf, g_svc_fit.dec_oldp, g_svc_fit.last);
+  }
+  g_svc_fit = SvcFit{};
+  S.svc = nullptr;
+  if (st2 != KBG_OK) return st2;
+  g_err = err;
+  return st;
+}
+
+// Rows and class-mask words from rank 0 into this rank's table.
+kbg_status svc_apply_state(Session& S, const kbg::NodeDelta* nodes, size_t nn, const kbg::MaskDelta* masks, size_t nm) {
+  for (size_t m = 0; m < nm;) {
+    if (kbg_status st = stage_acquire(S); st != KBG_OK) return st;
+    const int32_t cnt = (int32_t)std::min<size_t>(nm - m, (size_t)kbg::kMaskDeltaCap);
+    std::memcpy(S.h_mdeltas, masks + m, (size_t)cnt * sizeof(kbg::MaskDelta));
+    const kbg::MaskDelta* md = dev_ptr(S, S.h_mdeltas);
+    if (!md) return fail(KBG_E_HIP, "hipHostGetDevicePointer of the mask-delta buffer failed");
+    HIP_TRY(kbg::launch_mask_apply(S.d_class_mask, md, cnt, S.stream));
+    if (kbg_status st = stage_release(S); st != KBG_OK) return st;
+    m += cnt;
+  }
+  for (size_t i = 0; i < nn;) {
+    if (kbg_status st = stage_acquire(S); st != KBG_OK) return st;
+    int32_t cnt = 0;
+    for (; i < nn && cnt < S.K; ++i) {
+      const kbg::NodeDelta& d = nodes[i];
+      if (d.node < S.tab_lo || d.node >= S.tab_lo + S.tab_n) continue;
+      S.h_deltas[cnt] = d;
+      S.h_deltas[cnt++].node = d.node - S.tab_lo;
+    }
+    if (cnt == 0) break;
+    HIP_TRY(kbg::launch_apply(S.d_nodes, S.h_deltas_dev, cnt, S.stream));
+    if (kbg_status st = stage_release(S); st != KBG_OK) return st;
+  }
+  return KBG_OK;
+}
+
+// Ranks != 0: serve rank 0's scans over this rank's words and follow its
+// commits until the end message; the cycle ends with the same decision log,
+// node state and plugin state as rank 0's.
+kbg_status allocate_serve(Session& S, SvcLink& link, kbg_decision* out, int32_t cap, int32_t* n_out) {
+  if (S.allocated || S.backfilled || S.preempted)
+    return fail(KBG_E_INVALID, "allocate runs once per cycle, before backfill and preempt; call kbg_session_reset");
+  const bool first = !S.cycle_started;
+  if (first) begin_cycle(S);
+  S.action = KBG_ACTION_ALLOCATE;
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  std::vector<kbg_decision>& dec = S.dec;
+  std::vector<Res>& dec_old = S.dec_old_buf;
+  dec_old.assign(dec.size(), Res{});
+  std::vector<uint64_t> dec_oldp(dec.size() * (size_t)S.PW);
+  std::vector<LastEval> last(S.n_jobs);
+  Engine E = first ? S.init : live_engine(S);
+  Replayer rp(S, E);
+  std::vector<uint32_t> msg;
+  kbg_status result = KBG_OK;
+  int64_t evals = 0;
+  for (;;) {
+    if (kbg_status st = link.recv(S, msg); st != KBG_OK) {
+      rp.join();
+      return st;
+    }
+    const uint32_t kind = msg[0];
+    size_t at = kSvcHead;
+    const size_t args_w = msg[5], shapes_w = msg[6], rows_w = msg[7];
+    const size_t nn = msg[2], nm = msg[3], no = msg[4];
+    const size_t need = kSvcHead + args_w + shapes_w + rows_w + nn * kSvcNodeWords + nm * kSvcMaskWords + 2 * no;
+    if (kind > kSvcState || need != msg.size() || (kind == kSvcLaunch && args_w * 4 < sizeof(kbg::FirstFitArgs))) {
+      rp.join();
+      comm_abort(S.comm);
+      return fail(KBG_E_INVALID, "internal: malformed scan service message");
+    }
+    if (kind == kSvcAbort) {
+      rp.join();
+      return fail((kbg_status)msg[8], "the allocate failed on rank 0");
+    }
+    const uint32_t* args_p = msg.data() + at;
+    at += args_w;
+    const uint32_t* shapes_p = msg.data() + at;
+    at += shapes_w;
+    const uint32_t* rows_p = msg.data() + at;
+    at += rows_w;
+    const kbg::NodeDelta* nodes = reinterpret_cast<const kbg::NodeDelta*>(msg.data() + at);
+    at += nn * kSvcNodeWords;
+    const kbg::MaskDelta* masks = reinterpret_cast<const kbg::MaskDelta*>(msg.data() + at);
+    at += nm * kSvcMaskWords;
+    const uint32_t* outs = msg.data() + at;
+    kbg_status st = svc_apply_state(S, nodes, nn, masks, nm);
+    if (st == KBG_OK && kind == kSvcLaunch) {
+      // this rank's part of the scan: rank 0's arguments, this rank's table, words and buffers
+      thread_local kbg::FirstFitArgs a;
+      std::memcpy(&a, args_p, sizeof(kbg::FirstFitArgs));
+      const int32_t G = (int32_t)msg[9], ns = (int32_t)msg[10];
+      char* up = S.stages[0].h_up;  // mapped staging (idle on this rank during the service)
+      const size_t shapes_b = shapes_w ? ((size_t)ns * sizeof(kbg::TaskRec) + 15) & ~(size_t)15 : 0;
+      if (G <= 0 || G > S.K || ns <= 0 || ns > G || shapes_b + rows_w * 4 > S.up_cap ||
+          (shapes_w && shapes_w * 4 < (size_t)ns * sizeof(kbg::TaskRec)) || (rows_w && rows_w != (size_t)G) ||
+          a.G != G || a.n_shapes != ns) {
+        rp.join();
+        comm_abort(S.comm);
+        return fail(KBG_E_INVALID, "internal: malformed scan service launch");
+      }
+      if (shapes_w) std::memcpy(up, shapes_p, (size_t)ns * sizeof(kbg::TaskRec));
+      if (rows_w) std::memcpy(up + shapes_b, rows_p, (size_t)G * 4);
+      a.nodes = S.d_nodes.idle_cpu;
+      a.stride = soa_stride(S);
+      a.class_mask = S.d_class_mask;
+      a.shapes = shapes_w ? dev_ptr(S, reinterpret_cast<const kbg::TaskRec*>(up)) : nullptr;
+      a.row_shape = rows_w ? dev_ptr(S, reinterpret_cast<const uint32_t*>(up + shapes_b)) : nullptr;
+      a.n_nodes = S.n_nodes;
+      a.W = S.W;
+      a.w_lo = std::min(S.W, S.shard * S.Wl);
+      a.w_hi = std::min(S.W, (S.shard + 1) * S.Wl);
+      a.tab_lo = S.tab_lo;
+      a.tab_n = S.tab_n;
+      a.splits = 1;
+      a.split_words = a.w_hi - a.w_lo;
+      a.info_stride = S.R;
+      a.part0 = S.shard;
+      a.mask_w0 = 0;
+      a.mw = S.W;
+      a.complete = a.w_hi - a.w_lo <= kbg::kFfRoundWords ? 1 : 0;
+      a.avail = nullptr;
+      a.info = S.d_svc;
+      a.masks = reinterpret_cast<kbg::MaskPair*>(S.d_svc + fused_mask_off(S.K));
+      const size_t info_w = (size_t)ns * S.R, mask_w = (size_t)ns * S.W * 4;
+      if ((shapes_w && !a.shapes) || (rows_w && !a.row_shape)) {
+        st = fail(KBG_E_HIP, "hipHostGetDevicePointer of a stage buffer failed");
+      } else if (hipMemsetAsync(S.d_svc, 0, info_w * 4, S.stream) != hipSuccess ||
+                 hipMemsetAsync(a.masks, 0, mask_w * 4, S.stream) != hipSuccess ||
+                 kbg::launch_firstfit(a, S.int_mode ? 1 : 0, S.stream) != hipSuccess) {
+        st = fail(KBG_E_HIP, "scan service launch failed");
+      } else {
+        st = link.sum(S, nullptr, info_w, mask_w);
+        S.stats.scan_launches++;
+      }
+    }
+    if (st != KBG_OK) {
+      rp.join();
+      comm_abort(S.comm);
+      return st;
+    }
+    // rank 0's commits, in order: this rank's mirror, decision log and engine
+    std::vector<std::pair<int32_t, char>> v;
+    v.reserve(no);
+    for (size_t k = 0; k < no; ++k) {
+      const int32_t t = (int32_t)outs[2 * k];
+      const uint32_t w = outs[2 * k + 1];
+      const bool ok = w != ~0u;
+      const int32_t node = ok ? (int32_t)(w >> 1) : -1;
+      const int32_t kd = ok && (w & 1u) ? KBG_KIND_PIPELINE : KBG_KIND_ALLOCATE;
+      if (t < 0 || t >= S.n_tasks || node >= S.n_nodes) {
+        rp.join();
+        comm_abort(S.comm);
+        return fail(KBG_E_INVALID, "internal: malformed scan service outcome");
+      }
+      last[S.task_job[t]] = LastEval{t, (int32_t)dec.size(), node, ok ? kd : 0};
+      if (ok) {
+        dec_old.push_back(kd == KBG_KIND_ALLOCATE ? S.idle[node] : S.rel[node]);
+        if (S.has_ports)
+          dec_oldp.insert(dec_oldp.end(), S.node_ports.begin() + (size_t)node * S.PW,
+                          S.node_ports.begin() + (size_t)(node + 1) * S.PW);
+        const bool dup = mirror_add(S, t, node, kd);
+        record_decision(S, t, node, kd, dup);
+      }
+      v.emplace_back(t, (char)ok);
+    }
+    evals += (int64_t)no;
+    if (!v.empty()) rp.push(std::move(v));
+    if (kind == kSvcEnd) {
+      result = (kbg_status)msg[8];
+      break;
+    }
+  }
+  rp.join();
+  if (!rp.error.empty()) return fail(KBG_E_INVALID, rp.error);
+  if (kbg_status st = comm_sync(S); st != KBG_OK) return st;
+  // the class-mask words this rank's mirror changed came from rank 0 already
+  for (const uint32_t idx : S.mask_dirty) S.mask_dirty_flag[idx] = 0;
+  S.mask_dirty.clear();
+  if (result == KBG_OK || result == KBG_E_REF_PANIC) {  // as rank 0 (allocate_svc_root): the counts are summed
+    SvcLink* const keep = S.svc;
+    S.svc = &link;
+    const kbg_status st = compute_fit_deltas(S, dec, dec_old, dec_oldp, last);
+    S.svc = keep;
+    if (st != KBG_OK) return st;
+  }
+  S.stats.task_evaluations += evals;
+  S.fin = E;
+  finalize_shares(S, S.fin);
+  S.allocated = true;
+  S.stats.allocate_ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+  if (result != KBG_OK) (void)fail(result, "the allocate on rank 0 ended with this status");
   return copy_log(S, out, cap, n_out, result);
 }
 
@@ -6856,6 +7379,12 @@ kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t*
   if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
   HIP_TRY(hipSetDevice(s->s.device));
   try {
+    if (scan_service_ok(s->s)) {
+      RcclSvc link(s->s);
+      if (kbg_status st = link.init(); st != KBG_OK) return st;
+      return s->s.shard == 0 ? allocate_svc_root(s->s, link, out, cap, n_out)
+                             : allocate_serve(s->s, link, out, cap, n_out);
+    }
     if (owner_resolve_ok(s->s)) {
       RcclIO io(s->s);
       return allocate_sharded(s->s, io, out, cap, n_out);

@@ -282,6 +282,8 @@ struct Stage {
                                      // exchange start/stop; [6] = results on the host
 };
 
+struct SvcLink;  // kbg_session.cpp: the scan service's transport
+
 struct Session {
   // ---- copied snapshot
   std::vector<std::string> strs;
@@ -555,6 +557,15 @@ struct Session {
   // shard `shard` (comm != null) or every shard (shard = -1)
   int32_t R = 1, Wl = 0, shard = -1;
   bool owner = false;  // owner-resolve protocol (allocate_sharded): each rank resolves the rows it owns
+  // scan service (allocate_svc_root / allocate_serve): rank 0 runs the
+  // single-GPU pipeline; each of its scans is a launch message every rank
+  // answers by scanning its own words, and the ranks' word masks are summed.
+  // `svc`: the transport while an allocate of this rank runs the service.
+  SvcLink* svc = nullptr;
+  std::vector<NodeDelta> svc_nodes;   // rank 0: node rows written back since the last message (every rank's)
+  std::vector<MaskDelta> svc_masks;   // rank 0: class-mask words written since the last message
+  std::vector<uint32_t> svc_out;      // rank 0: committed outcomes since the last message (task, node<<1|pipe / ~0)
+  uint32_t* d_svc = nullptr;          // the launch's info words and word masks, summed over the ranks in place
   int32_t tab_lo = 0, tab_n = 0;  // global node range of the device node table
   kbg_comm* comm = nullptr;
   int32_t n_classes = 0;

@@ -1,7 +1,8 @@
 """Developer tool: A/B of library builds on the C3 bench (production and full-scan
 p50), alternating in one GPU session: python kube-arbitrator_amd/tools/ab_bench.py lib1.so lib2.so
 (CONFIG=4: another BASELINE config; REPS: rounds; lib.so@KEY=VAL sets a variant's environment).
-Per run: p50 cycle ms (production, full-scan), production scan launch us, production device round trip ms
+Per run: p50 cycle ms (production, full-scan), production scan launch us, production device round trip ms,
+production re-checks and resolve ms
 (RESIDENT=1: and the p50 resident update ms; STEPS: timed steps)"""
 import json, os, subprocess, sys
 res = {}
@@ -23,7 +24,9 @@ for rep in range(int(os.environ.get("REPS", "3"))):
         pm = d.get("production_mode", {})
         res.setdefault(v, []).append((round(d["p50_cycle_ms"], 2), round(d.get("full_scan_mode", {}).get("p50_cycle_ms") or 0, 2),
                                       round(pm.get("scan_kernel", {}).get("avg_launch_us") or 0, 1),
-                                      round(pm.get("breakdown", {}).get("device_roundtrip_ms") or 0, 2))
+                                      round(pm.get("breakdown", {}).get("device_roundtrip_ms") or 0, 2),
+                                      pm.get("breakdown", {}).get("resolve_rechecks"),
+                                      round(pm.get("breakdown", {}).get("host_resolve_ms") or 0, 2))
                                      + ((round(d["resident_session"]["churn_update_ms_p50"], 2),) if resident else ()))
         print(v, res[v][-1], flush=True)
 print(json.dumps(res))

@@ -463,6 +463,120 @@ extern "C" int32_t kbg_tool_sharded_allocate_device_t(const kbg_snapshot* snap, 
 }
 
 // ---------------------------------------------------------------------------
+// The scan service (kbg_session.cpp allocate_svc_root / allocate_serve) with R
+// device sessions on ONE GPU: rank r holds shard r of R (a communicator
+// without RCCL); the messages and the sums of the ranks' launch results go
+// through the in-process hub instead of RCCL, so this runs the device code
+// and the message handling of a multi-GPU service on a one-GPU box.
+namespace {
+struct LocalSvc final : SvcLink {
+  LocalHub& hub;
+  int32_t me;
+  LocalSvc(LocalHub& h, int32_t r) : hub(h), me(r) {}
+  kbg_status send(Session&, const uint32_t* msg) override {
+    hub.slot[0].assign(msg, msg + msg[1]);
+    hub.bar.arrive_and_wait();  // the other ranks copy it
+    hub.bar.arrive_and_wait();
+    return KBG_OK;
+  }
+  kbg_status recv(Session&, std::vector<uint32_t>& msg) override {
+    hub.bar.arrive_and_wait();
+    msg = hub.slot[0];
+    hub.bar.arrive_and_wait();
+    return KBG_OK;
+  }
+  kbg_status sum(Session& S, kbg::Stage* sg, size_t info, size_t masks) override {
+    std::vector<uint32_t>& b = hub.slot[me];
+    b.assign(info + masks, 0u);
+    if (hipStreamSynchronize(S.stream) != hipSuccess ||
+        hipMemcpy(b.data(), S.d_svc, info * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(b.data() + info, S.d_svc + fused_mask_off(S.K), masks * 4, hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(KBG_E_HIP, "scan service (local): device copy failed");
+    hub.bar.arrive_and_wait();
+    if (sg) {
+      uint32_t* hi = sg->h_down;
+      uint32_t* hm = sg->h_down + fused_mask_off(S.K);
+      for (size_t i = 0; i < info + masks; ++i) {
+        uint32_t v = 0;
+        for (int32_t r = 0; r < hub.R; ++r) v += hub.slot[r][i];
+        (i < info ? hi[i] : hm[i - info]) = v;
+      }
+    }
+    hub.bar.arrive_and_wait();
+    return KBG_OK;
+  }
+  kbg_status sum_host(Session&, uint32_t* buf, size_t n) override {
+    hub.slot[me].assign(buf, buf + n);
+    hub.bar.arrive_and_wait();
+    for (size_t i = 0; i < n; ++i) {
+      uint32_t v = 0;
+      for (int32_t r = 0; r < hub.R; ++r) v += hub.slot[r][i];
+      buf[i] = v;
+    }
+    hub.bar.arrive_and_wait();
+    return KBG_OK;
+  }
+};
+}  // namespace
+
+// `cycles` allocate cycles through the scan service (each on the sessions
+// reset to the snapshot), the last one's log per rank and tool_stats.
+extern "C" int32_t kbg_tool_svc_allocate_device(const kbg_snapshot* snap, const kbg_options* o, int32_t R,
+                                                int32_t device, kbg_decision* out, int32_t cap, int32_t* n_out,
+                                                int64_t* stats, int64_t* times, int32_t cycles) {
+  LocalHub hub(R);
+  std::vector<kbg_status> res(R, KBG_OK);
+  std::vector<std::string> err(R);
+  std::vector<kbg_comm> comms(R);
+  std::vector<std::unique_ptr<Session>> sess(R);
+  std::vector<std::thread> th;
+  for (int32_t r = 0; r < R; ++r) {
+    comms[r].n_ranks = R;
+    comms[r].rank = r;
+    comms[r].device = device;
+    sess[r].reset(new Session());
+  }
+  for (int32_t r = 0; r < R; ++r)
+    th.emplace_back([&, r]() {
+      res[r] = open_session(*sess[r], snap, o, &comms[r]);
+      err[r] = g_err;
+    });
+  for (auto& t : th) t.join();
+  th.clear();
+  bool opened = true;
+  for (int32_t r = 0; r < R; ++r) opened &= res[r] == KBG_OK;
+  if (opened)
+    for (int32_t r = 0; r < R; ++r)
+      th.emplace_back([&, r]() {
+        Session& S = *sess[r];
+        (void)hipSetDevice(S.device);
+        LocalSvc link(hub, r);
+        kbg_status st = KBG_OK;
+        for (int32_t c = 0; c < std::max(1, cycles) && st == KBG_OK; ++c) {
+          if (c > 0) {
+            st = session_reset(S);
+            hub.bar.arrive_and_wait();
+            if (st != KBG_OK) break;
+          }
+          S.stats = kbg_stats{};
+          st = r == 0 ? allocate_svc_root(S, link, out + (size_t)r * cap, cap, n_out + r)
+                      : allocate_serve(S, link, out + (size_t)r * cap, cap, n_out + r);
+        }
+        tool_stats(S, stats ? stats + 5 * r : nullptr, times ? times + 6 * r : nullptr);
+        res[r] = st;
+        err[r] = g_err;
+      });
+  for (auto& t : th) t.join();
+  for (int32_t r = 0; r < R; ++r) free_device(*sess[r]);
+  for (int32_t r = 0; r < R; ++r)
+    if (res[r] != KBG_OK) {
+      g_err = err[r];
+      return -(int32_t)res[r];
+    }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
 // The fused first-fit kernel alone on a device session: the first G pending
 // tasks (session order) as one batch of rows (Grouper: full-scan or grouped
 // per the options), launched `reps` times against the session's table;

@@ -1,5 +1,7 @@
-"""Developer tool: the owner-resolve protocol's per-rank
-critical path for a node-axis sharded allocate cycle at R = 1, 2, 4, 8 ranks,
+"""Developer tool: the per-rank critical path of a node-axis
+sharded allocate cycle at R = 1, 2, 4, 8 ranks — the scan service
+(kbg_tool_svc_allocate_device, the default) or, with PROTOCOL=owner, the
+owner-resolve protocol —
 measured with R device sessions of ONE process on one MI355X (the in-process
 host transport of tests/test_shard_device.py, kbg_tool_sharded_allocate_device_t:
 rank r holds the node rows of words [r*Wl, (r+1)*Wl) and runs
@@ -20,13 +22,16 @@ FIELDS = ["allocate_ms", "engine_ms", "resolve_ms", "device_ms", "exchange_ms"]
 
 
 def main(cid, ranks):
-    os.environ["KBG_OWNER_RESOLVE"] = "1"  # (read per session open: R = 1 runs the protocol too)
+    owner = os.environ.get("PROTOCOL", "svc") == "owner"
+    if owner:
+        os.environ["KBG_OWNER_RESOLVE"] = "1"  # (R = 1 runs the protocol too)
     from kbgpu import _abi, synth
     from kbgpu.cache import FakeBinder, cache_from_fixture
     from kbgpu.fixture import _OrderedCache, fixture_tiers
     from kbgpu.snapshot import FlatSnapshot
     L = ctypes.CDLL(os.environ.get("TOOLS_LIB", os.path.join(HERE, "libkbg_tools.so")))
-    L.kbg_tool_sharded_allocate_device_t.restype = ctypes.c_int32
+    fn = L.kbg_tool_sharded_allocate_device_t if owner else L.kbg_tool_svc_allocate_device
+    fn.restype = ctypes.c_int32
     L.kbg_last_error.restype = ctypes.c_char_p
     fx = synth.config_fixture(cid)
     s = _OrderedCache(cache_from_fixture(fx, FakeBinder()), fx).snapshot()
@@ -38,8 +43,7 @@ def main(cid, ranks):
         st = (ctypes.c_int64 * (5 * R))()
         tm = (ctypes.c_int64 * (6 * R))()
         o = _abi.kbg_options()
-        rc = L.kbg_tool_sharded_allocate_device_t(ctypes.byref(f.snap), ctypes.byref(o), R, 0, out, cap, n, st, tm,
-                                                  int(os.environ.get("CYCLES", "3")))
+        rc = fn(ctypes.byref(f.snap), ctypes.byref(o), R, 0, out, cap, n, st, tm, int(os.environ.get("CYCLES", "3")))
         if rc != 0:
             print(json.dumps({"config": cid, "R": R, "error": rc, "msg": L.kbg_last_error().decode()}), flush=True)
             continue
@@ -49,7 +53,8 @@ def main(cid, ranks):
             d.update(rank=r, scan_launches=tm[6 * r + 5], owner_rounds=st[5 * r], batches=st[5 * r + 1],
                      mispredictions=st[5 * r + 2], task_evaluations=st[5 * r + 4], decisions=n[r])
             per.append(d)
-        print(json.dumps({"config": cid, "R": R, "cycle_ms": max(p["allocate_ms"] for p in per), "ranks": per}),
+        print(json.dumps({"config": cid, "R": R, "protocol": "owner" if owner else "svc",
+                          "cycle_ms": max(p["allocate_ms"] for p in per), "ranks": per}),
               flush=True)
 
 

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Per-rank critical paths of the owner-resolve protocol (tools/shard_paths.py),
+# Per-rank critical paths of a sharded allocate (tools/shard_paths.py; PROTOCOL=owner: owner-resolve),
 # R device sessions on one GPU; one run per config under its own time limit.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -185,3 +185,50 @@ def test_rccl_local_failure_aborts_comm(monkeypatch):
         assert got["status"] == "rccl" and ssn is None and "aborted" in got["error"]
     finally:
         c.close()
+
+
+@pytest.fixture
+def scan_service(monkeypatch):
+    """Allocate through the scan service (allocate_svc_root) on the one-rank
+    communicator: the launch messages' ncclBroadcasts, the own-word kernel into
+    the (slot, rank) info column and [slot][W] masks, their ncclAllReduce."""
+    monkeypatch.setenv("KBG_SCAN_SERVICE", "1")
+
+
+@pytest.mark.parametrize("cid", [1, 2])
+def test_rccl_scan_service_parity(cid, comm1, scan_service):
+    fx = synth.config_fixture(cid)
+    got, ssn = run_fixture(fx, {"comm": comm1})
+    st = ssn.stats()
+    assert st.shards == 1 and st.owner_rounds == 0 and st.scan_launches > 0
+    compare_outputs(run_oracle(fx), got)
+    ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 60, 3))
+def test_rccl_scan_service_fuzz(seed, comm1, scan_service):
+    fx = synth.random_fixture(seed)
+    opts = {"comm": comm1, "batch_tasks": 1 + seed % 9, "candidates": 1 + seed % 5, "full_scan": seed % 2}
+    got, ssn = run_fixture(fx, opts)
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 40, 4))
+def test_rccl_scan_service_contended(seed, comm1, scan_service):
+    """The service's allocate inside a reclaim, allocate, backfill, preempt cycle."""
+    fx = synth.contended_fixture(seed)
+    got, ssn = run_fixture(fx, {"comm": comm1})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 30, 5))
+def test_rccl_scan_service_affinity(seed, comm1, scan_service):
+    fx = synth.affinity_fixture(seed)
+    got, ssn = run_fixture(fx, {"comm": comm1, "batch_tasks": 1 + seed % 5})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
