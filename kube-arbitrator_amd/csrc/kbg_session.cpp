@@ -63,6 +63,23 @@ struct kbg_comm {
   std::atomic<bool> aborted{false};
 };
 
+namespace kbg {
+struct SvcLink {
+  virtual ~SvcLink() = default;
+  // rank 0: msg[0 .. msg[1]) to every rank (may return before it is sent)
+  virtual kbg_status send(Session& S, const uint32_t* msg) = 0;
+  // ranks != 0: the next message
+  virtual kbg_status recv(Session& S, std::vector<uint32_t>& msg) = 0;
+  // after this rank's launch: the info words [0, info) and mask words [0, masks) of d_svc
+  // summed over the ranks; rank 0 then has them in sg->h_down (stream-ordered before its
+  // next event)
+  virtual kbg_status sum(Session& S, kbg::Stage* sg, size_t info, size_t masks) = 0;
+  // host words summed over the ranks, in place (synchronous)
+  virtual kbg_status sum_host(Session& S, uint32_t* buf, size_t n) = 0;
+};
+}  // namespace kbg
+using kbg::SvcLink;
+
 namespace {
 
 thread_local std::string g_err;
@@ -644,6 +661,8 @@ T* dev_ptr(const Session& S, T* h) {
 
 void free_device(Session& S) {
   if (S.stream) (void)hipStreamSynchronize(S.stream);  // every enqueued reader of the staging has run
+  delete S.svc_own;
+  S.svc_own = nullptr;
   for (kbg::Stage& g : S.stages) {
     if (g.inflight) (void)hipEventSynchronize(g.ev[6]);  // nothing may still write the staging
     if (g.h_up) (void)hipHostFree(g.h_up);
@@ -975,24 +994,6 @@ kbg_status device_scan(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
 // 0 the whole table's lists, joined in node order like a split launch's
 // parts. Rank 0's collectives are enqueued on its stream (no host wait); the
 // other ranks wait for each message.
-}  // namespace
-namespace kbg {
-struct SvcLink {
-  virtual ~SvcLink() = default;
-  // rank 0: msg[0 .. msg[1]) to every rank (may return before it is sent)
-  virtual kbg_status send(Session& S, const uint32_t* msg) = 0;
-  // ranks != 0: the next message
-  virtual kbg_status recv(Session& S, std::vector<uint32_t>& msg) = 0;
-  // after this rank's launch: the info words [0, info) and mask words [0, masks) of d_svc
-  // summed over the ranks; rank 0 then has them in sg->h_down (stream-ordered before its
-  // next event)
-  virtual kbg_status sum(Session& S, kbg::Stage* sg, size_t info, size_t masks) = 0;
-  // host words summed over the ranks, in place (synchronous)
-  virtual kbg_status sum_host(Session& S, uint32_t* buf, size_t n) = 0;
-};
-}  // namespace kbg
-namespace {
-using kbg::SvcLink;
 
 enum : uint32_t { kSvcLaunch = 0, kSvcEnd = 1, kSvcAbort = 2, kSvcState = 3 };
 constexpr size_t kSvcHead = 16;          // header words: kind, words, nodes, masks, outcomes, args, shapes, rowshape,
@@ -5351,11 +5352,20 @@ kbg_status allocate_svc_root(Session& S, SvcLink& link, kbg_decision* out, int32
     comm_abort(S.comm);  // the other ranks are in a collective this rank may never join
   } else {
     thread_local std::vector<uint32_t> m;
+    static const bool prof = getenv("KBG_PROFILE_SVC") != nullptr;
+    const auto c0 = std::chrono::steady_clock::now();
     st2 = svc_flush_state(S, m, 0, false, kSvcEnd, (uint32_t)st);
+    const auto c1 = std::chrono::steady_clock::now();
     if (st2 == KBG_OK) st2 = comm_sync(S);
+    const auto c2 = std::chrono::steady_clock::now();
     // FitError counts: each rank its own nodes, summed (allocate_serve does the same after the end message)
     if (st2 == KBG_OK && (st == KBG_OK || st == KBG_E_REF_PANIC))
       st2 = compute_fit_deltas(S, S.dec, S.dec_old_buf, g_svc_fit.dec_oldp, g_svc_fit.last);
+    if (prof) {
+      auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+      fprintf(stderr, "[kbg svc] end message %.1f us, stream drain %.1f us, FitError counts %.1f us, cycle %.3f ms\n",
+              us(c0, c1), us(c1, c2), us(c2, std::chrono::steady_clock::now()), S.stats.allocate_ms);
+    }
   }
   g_svc_fit = SvcFit{};
   S.svc = nullptr;
@@ -7380,8 +7390,12 @@ kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t*
   HIP_TRY(hipSetDevice(s->s.device));
   try {
     if (scan_service_ok(s->s)) {
-      RcclSvc link(s->s);
-      if (kbg_status st = link.init(); st != KBG_OK) return st;
+      if (!s->s.svc_own) {  // pinned ring and device buffer, kept for the session's later cycles
+        std::unique_ptr<RcclSvc> link(new RcclSvc(s->s));
+        if (kbg_status st = link->init(); st != KBG_OK) return st;
+        s->s.svc_own = link.release();
+      }
+      SvcLink& link = *s->s.svc_own;
       return s->s.shard == 0 ? allocate_svc_root(s->s, link, out, cap, n_out)
                              : allocate_serve(s->s, link, out, cap, n_out);
     }

@@ -562,6 +562,7 @@ struct Session {
   // answers by scanning its own words, and the ranks' word masks are summed.
   // `svc`: the transport while an allocate of this rank runs the service.
   SvcLink* svc = nullptr;
+  SvcLink* svc_own = nullptr;         // the library's RCCL link, made at the first allocate (free_device deletes it)
   std::vector<NodeDelta> svc_nodes;   // rank 0: node rows written back since the last message (every rank's)
   std::vector<MaskDelta> svc_masks;   // rank 0: class-mask words written since the last message
   std::vector<uint32_t> svc_out;      // rank 0: committed outcomes since the last message (task, node<<1|pipe / ~0)

@@ -1,5 +1,6 @@
 """Developer tool: timeline of one allocate cycle (KBG_TRACE) on the GPU.
-python kube-arbitrator_amd/tools/trace_cycle.py [config] [full_scan] 2> trace.txt"""
+python kube-arbitrator_amd/tools/trace_cycle.py [config] [full_scan] 2> trace.txt
+(COMM=1: on a one-rank RCCL communicator, e.g. with KBG_SCAN_SERVICE=1)"""
 import ctypes
 import os
 import sys
@@ -16,7 +17,13 @@ def main():
     from kbgpu.fixture import fixture_tiers
     from kbgpu.framework import open_session
     fx = synth.config_fixture(cid)
-    ssn = open_session(cache_from_fixture(fx), fixture_tiers(fx), {"device": 0, "full_scan": full})
+    opts = {"device": 0, "full_scan": full}
+    comm = None
+    if os.environ.get("COMM") == "1":
+        from kbgpu.dist import ShardComm
+        comm = ShardComm(device=0, rank=0, world=1)
+        opts["comm"] = comm
+    ssn = open_session(cache_from_fixture(fx), fixture_tiers(fx), opts)
     L = _abi.lib()
     cap = max(1, ssn.flat.pending_count)
     buf = (_abi.kbg_decision * cap)()
@@ -31,6 +38,8 @@ def main():
               f"resolve {st.resolve_ms:.3f}, device {st.device_ms:.3f}, batches {st.batches}", flush=True)
     os.environ.pop("KBG_TRACE", None)
     ssn.close()
+    if comm:
+        comm.close()
 
 
 if __name__ == "__main__":
