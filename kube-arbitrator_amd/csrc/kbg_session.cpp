@@ -1000,6 +1000,7 @@ constexpr size_t kSvcHead = 16;          // header words: kind, words, nodes, ma
                                          // status, G, slots
 constexpr size_t kSvcMaxWords = 1u << 19;  // one message (2 MB); a longer state goes out in kSvcState chunks
 constexpr size_t kSvcNodeWords = sizeof(kbg::NodeDelta) / 4, kSvcMaskWords = sizeof(kbg::MaskDelta) / 4;
+constexpr size_t kSvcStreamWords = 2 * 2048;  // rank 0 streams its commits once this many words wait
 static_assert(sizeof(kbg::NodeDelta) % 4 == 0 && sizeof(kbg::MaskDelta) % 4 == 0, "message words");
 
 inline void svc_put(std::vector<uint32_t>& m, const void* p, size_t bytes) {
@@ -4601,6 +4602,12 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       items.reserve(bt.size());
     }
     ctr.add("resolved");
+    if (S.svc && S.svc_out.size() >= kSvcStreamWords) {
+      // the scan service: batches resolved against reused lists send no launch; stream their
+      // commits so the other ranks replay beside this one instead of after the end message
+      thread_local std::vector<uint32_t> sm;
+      if ((st = svc_flush_state(S, sm, 0, false, kSvcState, 0)) != KBG_OK) return abort(st);
+    }
     if (pred_failed) return abort(fail(KBG_E_INVALID, pr.error));  // seen by the look-ahead above
     S.stats.resolve_ms += ms_since(tp);
     tp = clk::now();
@@ -5420,12 +5427,31 @@ kbg_status allocate_serve(Session& S, SvcLink& link, kbg_decision* out, int32_t 
   std::vector<LastEval> last(S.n_jobs);
   Engine E = first ? S.init : live_engine(S);
   Replayer rp(S, E);
+  // rank 0's commits into this rank's mirror and decision log on a thread of
+  // its own (in commit order), so the main thread is back at the next
+  // message while they are applied; the engine replays them on another
+  Logger lg(
+      [&](const LogItem& it) {
+        last[S.task_job[it.t]] = LastEval{it.t, (int32_t)dec.size(), it.node, it.ok ? it.kind : 0};
+        if (!it.ok) return;
+        dec_old.push_back(it.kind == KBG_KIND_ALLOCATE ? S.idle[it.node] : S.rel[it.node]);
+        if (S.has_ports)
+          dec_oldp.insert(dec_oldp.end(), S.node_ports.begin() + (size_t)it.node * S.PW,
+                          S.node_ports.begin() + (size_t)(it.node + 1) * S.PW);
+        const bool dup = mirror_add(S, it.t, it.node, it.kind);
+        record_decision(S, it.t, it.node, it.kind, dup);
+      },
+      sched_getcpu());
+  auto stop = [&]() {
+    lg.join();
+    rp.join();
+  };
   std::vector<uint32_t> msg;
   kbg_status result = KBG_OK;
   int64_t evals = 0;
   for (;;) {
     if (kbg_status st = link.recv(S, msg); st != KBG_OK) {
-      rp.join();
+      stop();
       return st;
     }
     const uint32_t kind = msg[0];
@@ -5434,12 +5460,12 @@ kbg_status allocate_serve(Session& S, SvcLink& link, kbg_decision* out, int32_t 
     const size_t nn = msg[2], nm = msg[3], no = msg[4];
     const size_t need = kSvcHead + args_w + shapes_w + rows_w + nn * kSvcNodeWords + nm * kSvcMaskWords + 2 * no;
     if (kind > kSvcState || need != msg.size() || (kind == kSvcLaunch && args_w * 4 < sizeof(kbg::FirstFitArgs))) {
-      rp.join();
+      stop();
       comm_abort(S.comm);
       return fail(KBG_E_INVALID, "internal: malformed scan service message");
     }
     if (kind == kSvcAbort) {
-      rp.join();
+      stop();
       return fail((kbg_status)msg[8], "the allocate failed on rank 0");
     }
     const uint32_t* args_p = msg.data() + at;
@@ -5464,7 +5490,7 @@ kbg_status allocate_serve(Session& S, SvcLink& link, kbg_decision* out, int32_t 
       if (G <= 0 || G > S.K || ns <= 0 || ns > G || shapes_b + rows_w * 4 > S.up_cap ||
           (shapes_w && shapes_w * 4 < (size_t)ns * sizeof(kbg::TaskRec)) || (rows_w && rows_w != (size_t)G) ||
           a.G != G || a.n_shapes != ns) {
-        rp.join();
+        stop();
         comm_abort(S.comm);
         return fail(KBG_E_INVALID, "internal: malformed scan service launch");
       }
@@ -5504,13 +5530,15 @@ kbg_status allocate_serve(Session& S, SvcLink& link, kbg_decision* out, int32_t 
       }
     }
     if (st != KBG_OK) {
-      rp.join();
+      stop();
       comm_abort(S.comm);
       return st;
     }
-    // rank 0's commits, in order: this rank's mirror, decision log and engine
+    // rank 0's commits, in order: this rank's mirror and decision log (lg), engine (rp)
     std::vector<std::pair<int32_t, char>> v;
+    std::vector<LogItem> items;
     v.reserve(no);
+    items.reserve(no);
     for (size_t k = 0; k < no; ++k) {
       const int32_t t = (int32_t)outs[2 * k];
       const uint32_t w = outs[2 * k + 1];
@@ -5518,29 +5546,24 @@ kbg_status allocate_serve(Session& S, SvcLink& link, kbg_decision* out, int32_t 
       const int32_t node = ok ? (int32_t)(w >> 1) : -1;
       const int32_t kd = ok && (w & 1u) ? KBG_KIND_PIPELINE : KBG_KIND_ALLOCATE;
       if (t < 0 || t >= S.n_tasks || node >= S.n_nodes) {
-        rp.join();
+        stop();
         comm_abort(S.comm);
         return fail(KBG_E_INVALID, "internal: malformed scan service outcome");
       }
-      last[S.task_job[t]] = LastEval{t, (int32_t)dec.size(), node, ok ? kd : 0};
-      if (ok) {
-        dec_old.push_back(kd == KBG_KIND_ALLOCATE ? S.idle[node] : S.rel[node]);
-        if (S.has_ports)
-          dec_oldp.insert(dec_oldp.end(), S.node_ports.begin() + (size_t)node * S.PW,
-                          S.node_ports.begin() + (size_t)(node + 1) * S.PW);
-        const bool dup = mirror_add(S, t, node, kd);
-        record_decision(S, t, node, kd, dup);
-      }
+      items.push_back(LogItem{t, node, kd, ok, false, false, Res{}});
       v.emplace_back(t, (char)ok);
     }
     evals += (int64_t)no;
-    if (!v.empty()) rp.push(std::move(v));
+    if (!v.empty()) {
+      lg.push(std::move(items));
+      rp.push(std::move(v));
+    }
     if (kind == kSvcEnd) {
       result = (kbg_status)msg[8];
       break;
     }
   }
-  rp.join();
+  stop();
   if (!rp.error.empty()) return fail(KBG_E_INVALID, rp.error);
   if (kbg_status st = comm_sync(S); st != KBG_OK) return st;
   // the class-mask words this rank's mirror changed came from rank 0 already
