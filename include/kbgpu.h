@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KBG_ABI_VERSION 11
+#define KBG_ABI_VERSION 12
 
 typedef enum kbg_status {
   KBG_OK = 0,
@@ -463,9 +463,21 @@ enum {
   KBG_EV_POD_UPDATE = 1, /* cache.UpdatePod: `task` gets `status` and NodeName = node `node` (-1: none) */
   KBG_EV_POD_DELETE = 2, /* cache.DeletePod: `task` leaves its job and its node */
   KBG_EV_POD_ADD = 3,    /* cache.AddPod: a new pod of session job `job` (index = the session's task count) */
-  KBG_EV_NODE_UPDATE = 4 /* cache.UpdateNode -> NodeInfo.SetNode: node `node` gets `resource` as Allocatable,
-                            `max_task_num` pods and `unschedulable` */
+  KBG_EV_NODE_UPDATE = 4, /* cache.UpdateNode -> NodeInfo.SetNode: node `node` gets `resource` as Allocatable,
+                             `max_task_num` pods and `unschedulable` (labels and taints unchanged) */
+  KBG_EV_NODE_SET = 5     /* cache.AddNode / UpdateNode -> NodeInfo.SetNode with the whole Node (event_handlers.go
+                             232-259, node_info.go:84-99): node `node` gets `node_spec`'s name, labels and taints,
+                             `resource`, `max_task_num` and `unschedulable` — also a node the cache only knew from
+                             a pod (NewNodeInfo(nil), Name ""), which then takes the name its pods' NodeName held */
 };
+/* The Node of a KBG_EV_NODE_SET event (strings are copied). */
+typedef struct kbg_node_spec {
+  const char* name;          /* Node.Name */
+  const char* const* labels; /* Node.Labels: 2 * n_labels strings, key then value */
+  int32_t n_labels;
+  int32_t n_taints;
+  const char* const* taints; /* Node.Spec.Taints: 3 * n_taints strings, key, value, effect */
+} kbg_node_spec;
 typedef struct kbg_event {
   int32_t kind;
   int32_t task;          /* POD_UPDATE / POD_DELETE */
@@ -480,6 +492,7 @@ typedef struct kbg_event {
   int32_t reserved;
   const char* uid;       /* POD_ADD: pod UID */
   const char* pod_key;   /* POD_ADD: "<namespace>/<name>" */
+  const kbg_node_spec* node_spec; /* NODE_SET */
 } kbg_event;
 /* Applies events[0..n) in order; the cycle state is reset as by
  * kbg_session_reset (node table, class masks, plugin state back to the
@@ -488,8 +501,10 @@ typedef struct kbg_event {
  * leave the session unchanged: an event naming a deleted task or an index out
  * of range, a removed pod whose key is held on its node by a pod outside the
  * session jobs when the snapshot carried no node_pods (kbg_node_pod: with
- * them that pod leaves the node as RemoveTask takes it), a node update of a
- * node the cache only knows from a pod. KBG_E_REF_PANIC (the cache itself would
+ * them that pod leaves the node as RemoveTask takes it), a KBG_EV_NODE_UPDATE
+ * of a node the cache only knows from a pod (send KBG_EV_NODE_SET: the Node's
+ * name, labels and taints), a KBG_EV_NODE_SET of such a node holding a pod
+ * outside the session jobs without node_pods. KBG_E_REF_PANIC (the cache itself would
  * panic: a Resource.Sub underflow in AddTask / RemoveTask / SetNode) is found
  * while the events are applied: the session is then unusable and every later
  * call on it but kbg_session_close returns KBG_E_INVALID (re-open it). */

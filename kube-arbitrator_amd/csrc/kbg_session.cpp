@@ -6934,9 +6934,117 @@ kbg_status in_add_task(Session& S, UpdateCtx& U, int32_t t) {  // event_handlers
   return KBG_OK;
 }
 
+kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e, const uint64_t* key_hash);
+// The pods of node n as NodeInfo.Tasks holds them: (Resreq, status) of each
+// session task and each pod outside the session jobs. false: an outsider
+// whose copy the snapshot did not carry (no node_pods).
+bool node_pods_of(const Session& S, int32_t n, std::vector<std::pair<Res, int32_t>>* out) {
+  out->clear();
+  for (const int32_t t : S.node_task_order[n]) out->emplace_back(S.treq[t], S.tasks_in[t].status);
+  for (const int32_t key : S.node_key_order[n]) {
+    bool session = false;
+    for (const int32_t t : S.node_task_order[n]) session |= S.canon[S.tasks_in[t].pod_key] == key;
+    if (session) continue;
+    auto it = S.outsiders.find(((int64_t)n << 32) | (uint32_t)key);
+    if (it == S.outsiders.end() || it->second.status == 0) return false;
+    out->emplace_back(to_res(it->second.req), it->second.status);
+  }
+  return true;
+}
+
+// KBG_EV_NODE_SET: NodeInfo.SetNode with the whole Node (node_info.go:84-99),
+// then the snapshot's clone (NewNodeInfo(node) + AddTask of every pod,
+// cache.go:549-597). A node the cache knew only from a pod (Node nil, Name "")
+// takes the Node's name: its pods' NodeName lookups (ssn.NodeIndex) find it
+// from now on, so pods that were "ghosts" (allocated on a node outside the
+// session) are not any more. New labels, taints or schedulability recompile
+// the static predicate (a rebuild); an unchanged spec is a NODE_UPDATE.
+kbg_status apply_node_set(Session& S, UpdateCtx& U, const kbg_event& e) {
+  if (e.node < 0 || e.node >= S.n_nodes || !e.node_spec || !e.node_spec->name || e.node_spec->n_labels < 0 ||
+      e.node_spec->n_taints < 0 || (e.node_spec->n_labels && !e.node_spec->labels) ||
+      (e.node_spec->n_taints && !e.node_spec->taints))
+    return fail(KBG_E_INVALID, "NODE_SET event");
+  const kbg_node_spec& sp = *e.node_spec;
+  kbg_node& nd = S.nodes_in[e.node];
+  const int32_t name = intern(S, sp.name);
+  if (nd.has_node && S.canon[nd.name] != S.canon[name]) return fail(KBG_E_INVALID, "NODE_SET: the node's name differs");
+  std::vector<int32_t> labels;
+  for (int32_t i = 0; i < 2 * sp.n_labels; ++i) {
+    if (!sp.labels[i]) return fail(KBG_E_INVALID, "NODE_SET: null label string");
+    labels.push_back(intern(S, sp.labels[i]));
+  }
+  std::vector<kbg_taint> taints;
+  for (int32_t i = 0; i < sp.n_taints; ++i) {
+    if (!sp.taints[3 * i] || !sp.taints[3 * i + 1] || !sp.taints[3 * i + 2])
+      return fail(KBG_E_INVALID, "NODE_SET: null taint string");
+    taints.push_back(kbg_taint{intern(S, sp.taints[3 * i]), intern(S, sp.taints[3 * i + 1]), intern(S, sp.taints[3 * i + 2])});
+  }
+  // the same labels (as a map) and taints (in order)?
+  auto label_set = [&](const int32_t* p, int32_t len) {
+    std::vector<std::pair<int32_t, int32_t>> v;
+    for (int32_t i = 0; i < len; ++i) v.emplace_back(S.canon[p[2 * i]], S.canon[p[2 * i + 1]]);
+    std::sort(v.begin(), v.end());
+    return v;
+  };
+  bool same = nd.has_node && nd.label_len == sp.n_labels && nd.taint_len == sp.n_taints &&
+              label_set(labels.data(), sp.n_labels) == label_set(S.labels_in.data() + 2 * (size_t)nd.label_off, nd.label_len);
+  for (int32_t i = 0; same && i < sp.n_taints; ++i) {
+    const kbg_taint& a = S.taints_in[nd.taint_off + i];
+    same = S.canon[a.key] == S.canon[taints[i].key] && S.canon[a.value] == S.canon[taints[i].value] &&
+           S.canon[a.effect] == S.canon[taints[i].effect];
+  }
+  if (same) {  // SetNode's resources and schedulability only
+    kbg_event u = e;
+    u.kind = KBG_EV_NODE_UPDATE;
+    return apply_event(S, U, u, nullptr);
+  }
+  if (!nd.has_node) {
+    // the clone: Idle = Allocatable - every pod, Releasing pods on Releasing (AddTask, node_info.go:101-129)
+    std::vector<std::pair<Res, int32_t>> pods;
+    if (!node_pods_of(S, e.node, &pods))
+      return fail(KBG_E_UNSUPPORTED, "NODE_SET of a node holding a pod outside the session jobs whose copy the "
+                                     "snapshot did not carry (node_pods): re-open");
+    Res idle = to_res(e.resource), rel{};
+    for (const auto& [r, st] : pods) {
+      if (st == KBG_RELEASING) kbg::res_add(rel, r);
+      if (st == KBG_PIPELINED) {
+        if (!kbg::res_sub(rel, r)) return fail(KBG_E_REF_PANIC, "NodeInfo.AddTask: Releasing.Sub underflow");
+        continue;
+      }
+      if (!kbg::res_sub(idle, r)) return fail(KBG_E_REF_PANIC, "NodeInfo.AddTask: Idle.Sub underflow (node_info.go:117-123)");
+    }
+    nd.idle = to_kres(idle);
+    nd.releasing = to_kres(rel);
+    nd.has_node = 1;
+    S.node_of[S.canon[name]] = e.node;
+    nd.name = name;
+    for (int32_t t = 0; t < S.n_tasks; ++t)  // NodeIndex[NodeName] finds the node now
+      if (S.task_live[t] && S.canon[S.tasks_in[t].node_name] == S.canon[name]) S.task_node[t] = e.node;
+  } else {
+    Res idle = to_res(nd.idle);
+    const Res a0 = to_res(nd.allocatable), a1 = to_res(e.resource);
+    idle = Res{idle.c + (a1.c - a0.c), idle.m + (a1.m - a0.m), idle.g + (a1.g - a0.g)};
+    if (nd.num_tasks > 0 && !kbg::res_le(Res{}, idle))
+      return fail(KBG_E_REF_PANIC, "NodeInfo.SetNode: Idle.Sub underflow (node_info.go:84-99)");
+    nd.idle = to_kres(idle);
+  }
+  nd.allocatable = e.resource;
+  nd.max_task_num = e.max_task_num;
+  nd.unschedulable = e.unschedulable;
+  nd.label_off = (int32_t)(S.labels_in.size() / 2);
+  nd.label_len = sp.n_labels;
+  S.labels_in.insert(S.labels_in.end(), labels.begin(), labels.end());
+  nd.taint_off = (int32_t)S.taints_in.size();
+  nd.taint_len = sp.n_taints;
+  S.taints_in.insert(S.taints_in.end(), taints.begin(), taints.end());
+  U.rebuild = true;  // labels / taints / a new Node: the static predicate is recompiled
+  U.touch(e.node);
+  return KBG_OK;
+}
+
 // key_hash: StrIndex::hash of a POD_ADD's pod key when the caller computed it
 // ahead (session_update's prefetch), else null
-kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e, const uint64_t* key_hash = nullptr) {
+kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e, const uint64_t* key_hash) {
   auto status_ok = [](int32_t st) { return st > 0 && st <= KBG_UNKNOWN && !(st & (st - 1)); };
   switch (e.kind) {
     case KBG_EV_POD_UPDATE:
@@ -6996,10 +7104,14 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e, const uint6
       S.upd_tasks.push_back(t);
       return in_add_task(S, U, t);
     }
+    case KBG_EV_NODE_SET:
+      return apply_node_set(S, U, e);
     case KBG_EV_NODE_UPDATE: {
       if (e.node < 0 || e.node >= S.n_nodes) return fail(KBG_E_INVALID, "event node index");
       kbg_node& nd = S.nodes_in[e.node];
-      if (!nd.has_node) return fail(KBG_E_UNSUPPORTED, "update of a node the cache only knows from a pod: re-open");
+      if (!nd.has_node)
+        return fail(KBG_E_UNSUPPORTED, "KBG_EV_NODE_UPDATE of a node the cache only knows from a pod: send "
+                                       "KBG_EV_NODE_SET (its name, labels and taints)");
       // SetNode (node_info.go:84-99) + the snapshot clone: Idle = Allocatable - every task
       Res idle = to_res(nd.idle);
       const Res a0 = to_res(nd.allocatable), a1 = to_res(e.resource);
@@ -7056,6 +7168,7 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
     return -1;
   };
   int32_t T = T0;
+  std::vector<uint8_t> node_set(S.n_nodes, 0);  // nodes an earlier NODE_SET of the batch gave a Node
   for (int32_t i = 0; i < n; ++i) {
     const kbg_event& e = ev[i];
     switch (e.kind) {
@@ -7114,9 +7227,20 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
       }
       case KBG_EV_NODE_UPDATE:
         if (e.node < 0 || e.node >= S.n_nodes) return fail(KBG_E_INVALID, "event node index");
-        if (!S.nodes_in[e.node].has_node)
-          return fail(KBG_E_UNSUPPORTED, "update of a node the cache only knows from a pod: re-open");
+        if (!S.nodes_in[e.node].has_node && !node_set[e.node])
+          return fail(KBG_E_UNSUPPORTED, "KBG_EV_NODE_UPDATE of a node the cache only knows from a pod: send "
+                                         "KBG_EV_NODE_SET (its name, labels and taints)");
         break;
+      case KBG_EV_NODE_SET: {
+        if (e.node < 0 || e.node >= S.n_nodes || !e.node_spec || !e.node_spec->name)
+          return fail(KBG_E_INVALID, "NODE_SET event");
+        std::vector<std::pair<Res, int32_t>> pods;
+        if (!S.nodes_in[e.node].has_node && !node_set[e.node] && !node_pods_of(S, e.node, &pods))
+          return fail(KBG_E_UNSUPPORTED, "NODE_SET of a node holding a pod outside the session jobs whose copy the "
+                                         "snapshot did not carry (node_pods): re-open");
+        node_set[e.node] = 1;
+        break;
+      }
       default:
         return fail(KBG_E_INVALID, "event kind");
     }

@@ -37,7 +37,7 @@ DISABLE_QUEUE_ORDER = 1 << 5
 DISABLE_PREDICATE = 1 << 6
 PLUGIN_REGISTERED = 0x80000000  # kbg_plugin_option.flags, read when kbg_options.plugin_registry = 1
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 COMM_ID_BYTES = 128
 
 KIND_ALLOCATE = 0
@@ -183,12 +183,19 @@ EV_POD_UPDATE = 1
 EV_POD_DELETE = 2
 EV_POD_ADD = 3
 EV_NODE_UPDATE = 4
+EV_NODE_SET = 5
+
+
+class kbg_node_spec(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("labels", ctypes.POINTER(ctypes.c_char_p)), ("n_labels", i32),
+                ("n_taints", i32), ("taints", ctypes.POINTER(ctypes.c_char_p))]
 
 
 class kbg_event(ctypes.Structure):
     _fields_ = [("kind", i32), ("task", i32), ("status", i32), ("node", i32), ("job", i32), ("spec", i32),
                 ("priority", i32), ("max_task_num", i32), ("resource", kbg_resource), ("unschedulable", i32),
-                ("reserved", i32), ("uid", ctypes.c_char_p), ("pod_key", ctypes.c_char_p)]
+                ("reserved", i32), ("uid", ctypes.c_char_p), ("pod_key", ctypes.c_char_p),
+                ("node_spec", ctypes.POINTER(kbg_node_spec))]
 
 
 class kbg_eviction(ctypes.Structure):

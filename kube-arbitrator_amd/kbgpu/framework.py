@@ -158,15 +158,32 @@ class Session:
         keep = []
         objs = {}  # task index -> its TaskInfo after the events (applied once the library accepts them)
         n_objs = len(self.flat.task_objs)
+        renamed = {}  # pod-only node index -> the name its Node gave it
         for k, (kind, obj) in enumerate(changes):
             e = evs[k]
-            if kind == "node_update":
+            if kind in ("node_update", "node_add"):
+                # cache.AddNode / UpdateNode -> SetNode with the whole Node (the library
+                # compares labels and taints and rebuilds only when they change)
                 ni = NodeInfo(obj)
-                e.kind = _abi.EV_NODE_UPDATE
-                e.node = nidx[obj["name"]]
+                name = obj["name"]
+                idx = nidx.get(name)
+                if idx is None or self.flat.node_names[idx] != name:
+                    idx = self.flat.pod_only_names.get(name)
+                    if idx is None:
+                        raise ValueError(f"node {name!r}: not a node of the session (a new node needs a re-open)")
+                    renamed[idx] = name
+                e.kind = _abi.EV_NODE_SET
+                e.node = idx
                 e.resource = _abi.kbg_resource(*ni.allocatable.as_tuple())
                 e.max_task_num = ni.allocatable.max_task_num
                 e.unschedulable = 1 if obj.get("unschedulable") else 0
+                labels = [x.encode() for kv in (obj.get("labels") or {}).items() for x in kv]
+                taints = [str(t.get(f, "")).encode() for t in (obj.get("taints") or []) for f in ("key", "value", "effect")]
+                la = (ctypes.c_char_p * max(1, len(labels)))(*labels)
+                ta = (ctypes.c_char_p * max(1, len(taints)))(*taints)
+                spec = _abi.kbg_node_spec(name.encode(), la, len(labels) // 2, len(taints) // 3, ta)
+                keep += [la, ta, spec]
+                e.node_spec = ctypes.pointer(spec)
                 continue
             ti = TaskInfo(obj)
             if kind in ("pod_update", "pod_delete"):
@@ -191,6 +208,11 @@ class Session:
             else:
                 raise ValueError(f"unknown change {kind}")
         _abi.check(_abi.lib().kbg_session_update(self.handle, evs, len(changes)))
+        for i, name in renamed.items():  # the NodeInfo the cache made from a pod has its Node's name now
+            self.flat.node_names[i] = name
+            self.flat.pod_only_names.pop(name, None)
+            self.nodes[i].name = name
+            self.node_index[name] = self.nodes[i]
         for i in range(len(self.flat.task_objs), n_objs):
             self.flat.task_objs.append(None)
         for i, ti in objs.items():

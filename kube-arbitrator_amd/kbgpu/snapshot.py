@@ -101,6 +101,13 @@ class FlatSnapshot:
             node_keys.extend(S(k) for k in n.tasks.keys())
             r["key_len"] = len(node_keys) - r["key_off"]
         self.node_names = [n.name for n in nodes]
+        # a node the cache knows only from its pods (Node nil, Name ""): the NodeName they carry -> its index
+        self.pod_only_names = {}
+        for i, n in enumerate(nodes):
+            if n.node is None:
+                for t in n.tasks.values():
+                    if t.node_name:
+                        self.pod_only_names.setdefault(t.node_name, i)
         # jobs + tasks + specs (node task lists are filled once task indices exist)
         jb = np.zeros(len(jobs), dtype=np.dtype(_abi.kbg_job))
         task_rows, self.task_objs = [], []

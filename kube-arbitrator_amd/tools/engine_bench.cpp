@@ -66,7 +66,7 @@ extern "C" int32_t kbg_tool_update_nodes(const kbg_snapshot* snap, const kbg_opt
   U.seen.assign(S.n_nodes, 0);
   const auto t0 = std::chrono::steady_clock::now();
   for (int32_t i = 0; i < n; ++i)
-    if (apply_event(S, U, ev[i]) != KBG_OK) return -3;
+    if (apply_event(S, U, ev[i], nullptr) != KBG_OK) return -3;
   const auto t1 = std::chrono::steady_clock::now();
   S.upd_nodes = U.nodes;  // as kbg_session_update hands them to the derive
   S.upd_nodes_valid = true;

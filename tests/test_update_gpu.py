@@ -277,3 +277,101 @@ def test_refused_update_leaves_the_session_unchanged():
         assert abi_cycle(ssn, ["allocate"])["status"] == "ok"
     finally:
         ssn.close()
+
+
+def check_changes(fx0, changes, fx1, opts=None):
+    """open(S0) + update(changes) + the cycle's actions against open(S1) with
+    the updated session's node and job order, and S1 against the oracle."""
+    from kbgpu.api import RefPanic
+    actions = fx0.get("actions") or ["allocate"]
+    try:
+        ssn = _open(fx0, opts)
+    except (RefPanic, _abi.KbgError) as e:
+        pytest.skip(f"S0 does not open: {e}")
+    try:
+        order = {"jobs": [j.uid for j in ssn.jobs], "nodes": list(ssn.flat.node_names)}
+        try:
+            ssn.update(changes)
+        except _abi.KbgError as e:
+            if e.status != "ref_panic":
+                raise
+            # the cache's clone panics on the new Node: so must a fresh open of S1
+            fresh, _ = run_fixture(dict(fx1, sessionOrder=order), opts)
+            assert fresh["status"] == "ref_panic", fresh
+            return {"status": "ref_panic"}
+        got = abi_cycle(ssn, actions)
+        fx1 = dict(fx1, sessionOrder={"jobs": [j.uid for j in ssn.jobs], "nodes": list(ssn.flat.node_names)})
+        fresh, fssn = run_fixture(fx1, opts)
+        compare_outputs(run_oracle(fx1), fresh)
+        assert got["status"] == fresh["status"], (got, fresh.get("error"))
+        if fresh["status"] == "ok":
+            assert got["decisions"] == fresh["decisions"]
+            assert got["binds"] == fresh["binds"]
+            assert got["nodes"] == fresh["nodes"]
+            for a, b in zip(got["jobs"], fresh["jobs"]):
+                assert (a["uid"], a["ready_num"], a["ready"], a.get("fit_error")) == \
+                       (b["uid"], b["ready_num"], b["ready"], b.get("fit_error")), (a, b)
+        if fssn:
+            fssn.close()
+        return got
+    finally:
+        ssn.close()
+
+
+def _late_nodes(seed, k=2):
+    """random_fixture with `k` nodes withheld: the Running pods on them make
+    the cache create NodeInfo(nil) entries (event_handlers.go:49-53), whose
+    Node then arrives (cache.AddNode -> SetNode)."""
+    import copy
+    import random
+    fx = synth.random_fixture(seed, max_nodes=12)
+    rng = random.Random(seed)
+    held = {p["nodeName"] for p in fx["pods"] if p.get("nodeName") and p["phase"] == "Running"}
+    late = [n for n in fx["nodes"] if n["name"] in held][:k]
+    if not late:
+        pytest.skip("no node holds a Running pod")
+    for n in late:  # room for what its pods hold, so the clone does not panic
+        n["allocatable"] = dict(n["allocatable"], cpu="64", memory="256Gi", pods="110")
+    fx1 = copy.deepcopy(fx)
+    fx0 = copy.deepcopy(fx)
+    names = {n["name"] for n in late}
+    fx0["nodes"] = [n for n in fx0["nodes"] if n["name"] not in names]
+    rng.shuffle(late)
+    return fx0, [("node_add", copy.deepcopy(n)) for n in late], fx1
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_update_node_set_pod_only(seed):
+    """A node the cache knew only from its pods gets its Node (KBG_EV_NODE_SET):
+    the node takes its name, labels, taints and Allocatable, its pods stop
+    being allocated pods on a node outside the session, and the static
+    predicate is recompiled — the same cycle as a fresh open of the cache
+    with the node from the start."""
+    fx0, changes, fx1 = _late_nodes(5000 + seed)
+    got = check_changes(fx0, changes, fx1, {"batch_tasks": 1 + seed % 7})
+    assert got["status"] in ("ok", "ref_panic")
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_update_node_relabel(seed):
+    """UpdateNode with new labels and taints (isNodeInfoUpdated,
+    event_handlers.go:242-259): selectors, node affinity and taint tolerations
+    see the new Node after the update."""
+    import copy
+    import random
+    fx0 = synth.random_fixture(6000 + seed)
+    rng = random.Random(seed)
+    fx1 = copy.deepcopy(fx0)
+    changes = []
+    for n in rng.sample(fx1["nodes"], min(3, len(fx1["nodes"]))):
+        labels = dict(n.get("labels") or {})
+        if labels and rng.random() < 0.5:
+            labels.pop(rng.choice(sorted(labels)))
+        labels[rng.choice(["zone", "disk", "tier"])] = rng.choice(["a", "b", "ssd", "x"])
+        n["labels"] = labels
+        if rng.random() < 0.5:
+            n["taints"] = list(n.get("taints") or []) + [{"key": "maint", "value": "", "effect": "NoSchedule"}]
+        elif n.get("taints"):
+            n["taints"] = []
+        changes.append(("node_update", copy.deepcopy(n)))
+    check_changes(fx0, changes, fx1, {"batch_tasks": 1 + seed % 5})
