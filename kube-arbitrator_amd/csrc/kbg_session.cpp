@@ -4139,7 +4139,14 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   };
   // committed outcomes of the current batch not yet handed to the truth engine
   int32_t truth_from = 0;
+  // KBG_NO_TRUTH=1 (experiment, cut-free cycles only): no truth engine; the
+  // predictor's own engine is the cycle's final state
+  static const bool no_truth = getenv("KBG_NO_TRUTH") != nullptr;
   auto to_truth = [&](const std::vector<int32_t>& bt, int32_t end) {
+    if (no_truth) {
+      truth_from = end;
+      return;
+    }
     if (end <= truth_from) return;
     std::vector<std::pair<int32_t, char>> v(end - truth_from);
     for (int32_t k = truth_from; k < end; ++k) v[k - truth_from] = {bt[k], bactual[k]};
@@ -4714,6 +4721,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
             (unsigned long long)S.affm->prof_calls,
             S.affm->prof_calls ? (double)S.affm->prof_cycles / S.affm->prof_calls : 0.0,
             (unsigned long long)S.affm->prof_recomputes, S.mask_dirty.size());
+  if (no_truth) {
+    if (S.stats.mispredictions) return fail(KBG_E_INVALID, "KBG_NO_TRUTH: a cycle with a misprediction");
+    E_truth = E;  // (the predictor has finished)
+  }
   finalize_shares(S, E_truth);
   S.fin = E_truth;
   S.stats.engine_ms = pr.engine_ms;

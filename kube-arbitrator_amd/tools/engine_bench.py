@@ -12,7 +12,8 @@ sys.path.insert(0, PKG)
 def main():
     cid = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     lib = os.environ.get("TOOLS_LIB", os.path.join(HERE, "libkbg_tools.so"))
-    subprocess.run(["make", "-s", "-C", PKG, "tools"], check=True)
+    if not os.environ.get("NO_MAKE"):
+        subprocess.run(["make", "-s", "-C", PKG, "tools"], check=True)
     from kbgpu import _abi, synth
     from kbgpu.cache import cache_from_fixture
     from kbgpu.fixture import fixture_tiers
