@@ -341,6 +341,7 @@ struct Session {
   std::vector<int32_t> task_class;
   std::vector<int32_t> class_spec;                       // spec of each static class (-1: none)
   std::vector<int32_t> task_shape;                       // (class, request) shape id of a pending task
+  std::vector<Res> shape_req;                            // each shape's request (the engine reads it by task_shape)
   std::vector<int32_t> shape_task;                       // a candidate task of each shape (-1: none; may be
                                                          // stale: valid while task_shape[it] == the shape)
   std::unordered_map<ShapeKey, int32_t, ShapeHash> shape_ids;  // shape ids, kept across updates

@@ -560,3 +560,18 @@ def test_staging_reuse_under_overlap():
         compare_outputs(ref, got)
         if ssn:
             ssn.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 40, 2))
+def test_predictor_engine_is_final(seed, monkeypatch):
+    """At the end of a cycle the predictor's engine is the committed state
+    (its last epoch had no cut), so the truth engine's backlog is dropped:
+    KBG_CHECK_TRUTH=1 waits for it and compares the two engines field by
+    field on contended and saturated cycles (cuts, reused lists)."""
+    monkeypatch.setenv("KBG_CHECK_TRUTH", "1")
+    fx = synth.contended_fixture(12000 + seed, nodes=16, jobs=20, tasks=10) if seed % 4 else \
+        synth.saturated_config(nodes=64, jobs=40, tasks_per_job=12, seed=seed)
+    got, ssn = run_fixture(fx, {"batch_tasks": 1 + seed % 9})
+    compare_outputs(run_oracle(fx), got)
+    if ssn:
+        ssn.close()
