@@ -2272,6 +2272,22 @@ enum { DERIVE_OK = 0, DERIVE_REBUILD = 1 };  // REBUILD: the static classes / ma
 // when a candidate needs a class the session does not have.
 void pin_near(int cpu, int nth);
 
+// Sorted, duplicate-free ids in [0, n): a flag sweep when the list is a
+// sizeable share of the range (a bind update touches every placed task: a
+// comparison sort of 500k ids was a third of its derive), else a sort.
+void sort_unique_ids(std::vector<int32_t>& v, int32_t n) {
+  if (v.size() > 64 && (int64_t)v.size() * 16 > (int64_t)n) {
+    std::vector<uint8_t> flag((size_t)std::max(n, 1), 0);
+    for (const int32_t x : v) flag[x] = 1;
+    v.clear();
+    for (int32_t x = 0; x < n; ++x)
+      if (flag[x]) v.push_back(x);
+    return;
+  }
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+}
+
 kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   *outcome = DERIVE_OK;
   S.job_chain_pgd = S.job_chain == std::vector<int32_t>{kbg::JO_PRIORITY, kbg::JO_GANG, kbg::JO_DRF};
@@ -2464,8 +2480,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   // An update recomputes the tasks its events touched; their old candidate
   // state is kept aside for the counts below (`was`: bit 0 candidate, 1 BE).
   const bool incr = !full && (int32_t)S.pending_candidate.size() <= T && !S.t_aff.empty();
-  std::sort(S.upd_tasks.begin(), S.upd_tasks.end());
-  S.upd_tasks.erase(std::unique(S.upd_tasks.begin(), S.upd_tasks.end()), S.upd_tasks.end());
+  sort_unique_ids(S.upd_tasks, T);
   std::vector<uint8_t> was;
   std::vector<uint16_t> was_stat;  // the touched tasks' statuses at the last derive
   const int32_t T_prev = (int32_t)S.tstat_in.size();
@@ -6976,9 +6991,48 @@ int in_node_remove(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
 
 // event_handlers.go deleteTask: the job side always, then the node side.
 // Returns 0, 1 (the node side failed: updateTask stops there) or a status.
+// A job's task order (JobInfo.Tasks insertion order) under an update: a task
+// an event takes off its job (-1) and puts back (a sequence number) is moved
+// to the end in event order. The moves are recorded per event and applied to
+// each changed job's list once, after the events (finish_job_lists): a find
+// and erase per event scanned the job's whole list.
+void job_list_mark(Session& S, int32_t t, int64_t v) {
+  if ((size_t)t >= S.jmove.size()) S.jmove.resize((size_t)std::max<int32_t>(S.n_tasks, t + 1), 0);
+  const int32_t j = S.tasks_in[t].job;
+  if ((size_t)j >= S.jmove_dirty.size()) S.jmove_dirty.resize(S.n_jobs, 0);
+  if (!S.jmove_dirty[j]) {
+    S.jmove_dirty[j] = 1;
+    S.jmove_jobs.push_back(j);
+  }
+  S.jmove[t] = v;
+  if (v < 0) S.jmove_out.push_back(t);
+  else S.jmove_add.emplace_back(t, v);
+}
+void finish_job_lists(Session& S) {
+  if (S.jmove_jobs.empty()) return;
+  std::unordered_map<int32_t, std::vector<int32_t>> tail;  // job -> its re-added tasks, in event order
+  for (const auto& [t, v] : S.jmove_add)
+    if (S.jmove[t] == v) tail[S.tasks_in[t].job].push_back(t);
+  std::vector<int32_t> kept;
+  for (const int32_t j : S.jmove_jobs) {
+    std::vector<int32_t>& jl = S.job_task_order[j];
+    kept.clear();
+    for (const int32_t t : jl)
+      if ((size_t)t >= S.jmove.size() || S.jmove[t] == 0) kept.push_back(t);
+    auto it = tail.find(j);
+    if (it != tail.end()) kept.insert(kept.end(), it->second.begin(), it->second.end());
+    jl.swap(kept);
+    S.jmove_dirty[j] = 0;
+  }
+  for (const auto& [t, v] : S.jmove_add) S.jmove[t] = 0;
+  for (const int32_t t : S.jmove_out) S.jmove[t] = 0;
+  S.jmove_add.clear();
+  S.jmove_out.clear();
+  S.jmove_jobs.clear();
+}
+
 int in_delete_task(Session& S, UpdateCtx& U, int32_t t) {
-  std::vector<int32_t>& jl = S.job_task_order[S.tasks_in[t].job];
-  jl.erase(std::find(jl.begin(), jl.end(), t));  // JobInfo.DeleteTaskInfo
+  job_list_mark(S, t, -1);  // JobInfo.DeleteTaskInfo
   // the node its NodeName names (task_node: derive_host's lookup, kept
   // current by the events); -1: no NodeName, or sc.Nodes[...] == nil
   const int32_t n = S.task_node[t];
@@ -6987,7 +7041,7 @@ int in_delete_task(Session& S, UpdateCtx& U, int32_t t) {
 }
 
 kbg_status in_add_task(Session& S, UpdateCtx& U, int32_t t) {  // event_handlers.go addTask
-  S.job_task_order[S.tasks_in[t].job].push_back(t);            // JobInfo.AddTaskInfo
+  job_list_mark(S, t, ++S.jmove_seq);                          // JobInfo.AddTaskInfo
   const int32_t n = S.task_node[t];
   if (n >= 0 && !terminated(S.tasks_in[t].status) && !in_node_add(S, U, n, t))
     return fail(KBG_E_REF_PANIC, "NodeInfo.AddTask: Resource.Sub underflow (node_info.go:117-123)");
@@ -7411,6 +7465,7 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
       kn[k]++;
     }
   }
+  finish_job_lists(S);
   if (prof)
     for (int k = 0; k < 5; ++k)
       if (kn[k]) fprintf(stderr, "[kbg update] event kind %d: %llu, %.0f cycles each\n", k, (unsigned long long)kn[k],

@@ -341,6 +341,12 @@ struct Session {
   std::vector<int32_t> task_class;
   std::vector<int32_t> class_spec;                       // spec of each static class (-1: none)
   std::vector<int32_t> task_shape;                       // (class, request) shape id of a pending task
+  // an update's job-list moves, applied once after its events (finish_job_lists)
+  std::vector<int64_t> jmove;                            // per task: 0, -1 (left its job), or the sequence of its last re-add
+  std::vector<std::pair<int32_t, int64_t>> jmove_add;    // (task, sequence) of every re-add, in event order
+  std::vector<int32_t> jmove_out, jmove_jobs;            // tasks that left, jobs whose list changed
+  std::vector<uint8_t> jmove_dirty;
+  int64_t jmove_seq = 0;
   std::vector<Res> shape_req;                            // each shape's request (the engine reads it by task_shape)
   std::vector<int32_t> shape_task;                       // a candidate task of each shape (-1: none; may be
                                                          // stale: valid while task_shape[it] == the shape)

@@ -67,6 +67,7 @@ extern "C" int32_t kbg_tool_update_nodes(const kbg_snapshot* snap, const kbg_opt
   const auto t0 = std::chrono::steady_clock::now();
   for (int32_t i = 0; i < n; ++i)
     if (apply_event(S, U, ev[i], nullptr) != KBG_OK) return -3;
+  finish_job_lists(S);
   const auto t1 = std::chrono::steady_clock::now();
   S.upd_nodes = U.nodes;  // as kbg_session_update hands them to the derive
   S.upd_nodes_valid = true;
