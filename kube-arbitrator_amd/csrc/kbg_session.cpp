@@ -6995,8 +6995,15 @@ int in_node_remove(Session& S, UpdateCtx& U, int32_t n, int32_t t) {
 // an event takes off its job (-1) and puts back (a sequence number) is moved
 // to the end in event order. The moves are recorded per event and applied to
 // each changed job's list once, after the events (finish_job_lists): a find
-// and erase per event scanned the job's whole list.
+// and erase per event scanned the job's whole list (kept for small updates,
+// whose lists the event loop prefetches and whose jobs are few).
 void job_list_mark(Session& S, int32_t t, int64_t v) {
+  if (!S.jmove_defer) {  // a small update: in place (the event loop has requested the list's lines)
+    std::vector<int32_t>& jl = S.job_task_order[S.tasks_in[t].job];
+    if (v < 0) jl.erase(std::find(jl.begin(), jl.end(), t));
+    else jl.push_back(t);
+    return;
+  }
   if ((size_t)t >= S.jmove.size()) S.jmove.resize((size_t)std::max<int32_t>(S.n_tasks, t + 1), 0);
   const int32_t j = S.tasks_in[t].job;
   if ((size_t)j >= S.jmove_dirty.size()) S.jmove_dirty.resize(S.n_jobs, 0);
@@ -7010,18 +7017,32 @@ void job_list_mark(Session& S, int32_t t, int64_t v) {
 }
 void finish_job_lists(Session& S) {
   if (S.jmove_jobs.empty()) return;
-  std::unordered_map<int32_t, std::vector<int32_t>> tail;  // job -> its re-added tasks, in event order
+  // each changed job's re-added tasks, in event order: counted, placed by offset
+  std::vector<int32_t>& cnt = S.jmove_cnt;
+  std::vector<int32_t>& pos = S.jmove_pos;
+  if (cnt.size() < (size_t)S.n_jobs) {
+    cnt.resize(S.n_jobs, 0);
+    pos.resize(S.n_jobs, 0);
+  }
   for (const auto& [t, v] : S.jmove_add)
-    if (S.jmove[t] == v) tail[S.tasks_in[t].job].push_back(t);
-  std::vector<int32_t> kept;
+    if (S.jmove[t] == v) cnt[S.tasks_in[t].job]++;
+  int32_t total = 0;
+  for (const int32_t j : S.jmove_jobs) {
+    pos[j] = total;
+    total += cnt[j];
+  }
+  S.jmove_flat.resize(total);
+  for (const auto& [t, v] : S.jmove_add)
+    if (S.jmove[t] == v) S.jmove_flat[pos[S.tasks_in[t].job]++] = t;
+  thread_local std::vector<int32_t> kept;
   for (const int32_t j : S.jmove_jobs) {
     std::vector<int32_t>& jl = S.job_task_order[j];
     kept.clear();
     for (const int32_t t : jl)
       if ((size_t)t >= S.jmove.size() || S.jmove[t] == 0) kept.push_back(t);
-    auto it = tail.find(j);
-    if (it != tail.end()) kept.insert(kept.end(), it->second.begin(), it->second.end());
-    jl.swap(kept);
+    kept.insert(kept.end(), S.jmove_flat.begin() + (pos[j] - cnt[j]), S.jmove_flat.begin() + pos[j]);
+    jl.assign(kept.begin(), kept.end());
+    cnt[j] = 0;
     S.jmove_dirty[j] = 0;
   }
   for (const auto& [t, v] : S.jmove_add) S.jmove[t] = 0;
@@ -7082,26 +7103,28 @@ kbg_status apply_node_set(Session& S, UpdateCtx& U, const kbg_event& e) {
   kbg_node& nd = S.nodes_in[e.node];
   const int32_t name = intern(S, sp.name);
   if (nd.has_node && S.canon[nd.name] != S.canon[name]) return fail(KBG_E_INVALID, "NODE_SET: the node's name differs");
-  std::vector<int32_t> labels;
+  thread_local std::vector<int32_t> labels;
+  thread_local std::vector<kbg_taint> taints;
+  labels.clear();
+  taints.clear();
   for (int32_t i = 0; i < 2 * sp.n_labels; ++i) {
     if (!sp.labels[i]) return fail(KBG_E_INVALID, "NODE_SET: null label string");
     labels.push_back(intern(S, sp.labels[i]));
   }
-  std::vector<kbg_taint> taints;
   for (int32_t i = 0; i < sp.n_taints; ++i) {
     if (!sp.taints[3 * i] || !sp.taints[3 * i + 1] || !sp.taints[3 * i + 2])
       return fail(KBG_E_INVALID, "NODE_SET: null taint string");
     taints.push_back(kbg_taint{intern(S, sp.taints[3 * i]), intern(S, sp.taints[3 * i + 1]), intern(S, sp.taints[3 * i + 2])});
   }
-  // the same labels (as a map) and taints (in order)?
-  auto label_set = [&](const int32_t* p, int32_t len) {
-    std::vector<std::pair<int32_t, int32_t>> v;
-    for (int32_t i = 0; i < len; ++i) v.emplace_back(S.canon[p[2 * i]], S.canon[p[2 * i + 1]]);
-    std::sort(v.begin(), v.end());
-    return v;
-  };
-  bool same = nd.has_node && nd.label_len == sp.n_labels && nd.taint_len == sp.n_taints &&
-              label_set(labels.data(), sp.n_labels) == label_set(S.labels_in.data() + 2 * (size_t)nd.label_off, nd.label_len);
+  // the same labels (as a map: every new pair among the old ones, same count) and taints (in order)?
+  bool same = nd.has_node && nd.label_len == sp.n_labels && nd.taint_len == sp.n_taints;
+  const int32_t* old_l = S.labels_in.data() + 2 * (size_t)nd.label_off;
+  for (int32_t i = 0; same && i < sp.n_labels; ++i) {
+    bool found = false;
+    for (int32_t k = 0; k < nd.label_len && !found; ++k)
+      found = S.canon[old_l[2 * k]] == S.canon[labels[2 * i]] && S.canon[old_l[2 * k + 1]] == S.canon[labels[2 * i + 1]];
+    same = found;
+  }
   for (int32_t i = 0; same && i < sp.n_taints; ++i) {
     const kbg_taint& a = S.taints_in[nd.taint_off + i];
     same = S.canon[a.key] == S.canon[taints[i].key] && S.canon[a.value] == S.canon[taints[i].value] &&
@@ -7348,7 +7371,7 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
       case KBG_EV_NODE_SET: {
         if (e.node < 0 || e.node >= S.n_nodes || !e.node_spec || !e.node_spec->name)
           return fail(KBG_E_INVALID, "NODE_SET event");
-        std::vector<std::pair<Res, int32_t>> pods;
+        thread_local std::vector<std::pair<Res, int32_t>> pods;
         if (!S.nodes_in[e.node].has_node && !node_set[e.node] && !node_pods_of(S, e.node, &pods))
           return fail(KBG_E_UNSUPPORTED, "NODE_SET of a node holding a pod outside the session jobs whose copy the "
                                          "snapshot did not carry (node_pods): re-open");
@@ -7451,6 +7474,7 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
       }
     }
   };
+  S.jmove_defer = (int64_t)n * 8 > (int64_t)S.n_tasks;
   for (int32_t i = 0; i < n; ++i) {
     if (i + kFar < n) ahead_far(ev[i + kFar]);
     if (i + kMid < n) ahead_mid(ev[i + kMid], i + kMid);

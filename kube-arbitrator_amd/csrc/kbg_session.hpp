@@ -346,7 +346,9 @@ struct Session {
   std::vector<std::pair<int32_t, int64_t>> jmove_add;    // (task, sequence) of every re-add, in event order
   std::vector<int32_t> jmove_out, jmove_jobs;            // tasks that left, jobs whose list changed
   std::vector<uint8_t> jmove_dirty;
+  std::vector<int32_t> jmove_cnt, jmove_pos, jmove_flat;  // per job (zero between updates) / scratch
   int64_t jmove_seq = 0;
+  bool jmove_defer = false;                              // this update defers its moves (many events); else in place
   std::vector<Res> shape_req;                            // each shape's request (the engine reads it by task_shape)
   std::vector<int32_t> shape_task;                       // a candidate task of each shape (-1: none; may be
                                                          // stale: valid while task_shape[it] == the shape)

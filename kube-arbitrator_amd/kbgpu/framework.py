@@ -13,6 +13,7 @@ refuses the session (KBG_E_UNSUPPORTED: run the reference path). `Session.alloca
 reference's bookkeeping (session.go:205-316).
 """
 import ctypes
+import os
 
 from . import _abi
 from .api import ALLOCATED, BINDING, PIPELINED, RELEASING, pod_key
@@ -174,6 +175,12 @@ class Session:
                     renamed[idx] = name
                 e.kind = _abi.EV_NODE_SET
                 e.node = idx
+                if os.environ.get("KBG_PY_NODE_UPDATE") == "1" and idx not in renamed:  # (A/B: Allocatable only)
+                    e.kind = _abi.EV_NODE_UPDATE
+                    e.resource = _abi.kbg_resource(*ni.allocatable.as_tuple())
+                    e.max_task_num = ni.allocatable.max_task_num
+                    e.unschedulable = 1 if obj.get("unschedulable") else 0
+                    continue
                 e.resource = _abi.kbg_resource(*ni.allocatable.as_tuple())
                 e.max_task_num = ni.allocatable.max_task_num
                 e.unschedulable = 1 if obj.get("unschedulable") else 0
