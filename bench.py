@@ -533,8 +533,8 @@ def main():
         out = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_GIPS, "unit": "G wave64 VALU instructions/s",
                "frac": None, "traffic": None, "kernel": "kbg_firstfit_kernel (full-scan mode)",
                "avg_launch_us": avg_s * 1e6, "rows_per_launch": rows, "words_per_launch": words,
-               "timing": "HIP events on the library stream around one fused launch in four over the timed steps "
-                         "(kbg_stats.scan_kernel_ms)",
+               "timing": "HIP events on the library stream around every fused launch of the timed full-scan steps "
+                         "(kbg_stats.scan_kernel_ms; the production mode samples one launch in four)",
                "equivalent_8d": eq}
         pmc = load_pmc(agg["n_nodes"], mode)
         if pmc:

@@ -776,6 +776,10 @@ thread_local Trace* t_trace = nullptr;  // the committer's KBG_TRACE timeline, i
 void trace_add(const char* what, int64_t v = 0);
 
 constexpr int64_t kFfTimeEvery = 4;  // fused launches: one in this many carries start / stop events
+// Full-scan mode (the roofline measurement, not the production number) times
+// every launch: its launches alternate between batch scans and short
+// rescans, and a one-in-four sample followed that pattern instead of the mix.
+inline int64_t ff_time_every(const Session& S) { return S.opts.full_scan ? 1 : kFfTimeEvery; }
 kbg_status svc_launch(Session& S, kbg::Stage& sg, kbg::FirstFitArgs& a, int32_t G, int32_t base);
 kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   trace_add("l.begin", G);
@@ -856,7 +860,7 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
       a.avail = S.d_down;
       a.avail_bit = 1u << S.shard;
     }
-    sg.timed = !S.untimed_launches && S.ff_launch_seq++ % kFfTimeEvery == 0;
+    sg.timed = !S.untimed_launches && S.ff_launch_seq++ % ff_time_every(S) == 0;
     HIP_TRY(kbg::launch_firstfit(a, S.int_mode ? 1 : 0, S.stream, sg.timed ? sg.ev[0] : nullptr,
                                  sg.timed ? sg.ev[1] : nullptr));
     trace_add("l.firstfit");
@@ -1087,7 +1091,7 @@ kbg_status svc_launch(Session& S, kbg::Stage& sg, kbg::FirstFitArgs& a, int32_t 
   const size_t info_w = (size_t)ns * S.R, mask_w = (size_t)ns * S.W * 4;
   HIP_TRY(hipMemsetAsync(S.d_svc, 0, info_w * 4, S.stream));
   HIP_TRY(hipMemsetAsync(a.masks, 0, mask_w * 4, S.stream));
-  sg.timed = !S.untimed_launches && S.ff_launch_seq++ % kFfTimeEvery == 0;
+  sg.timed = !S.untimed_launches && S.ff_launch_seq++ % ff_time_every(S) == 0;
   HIP_TRY(kbg::launch_firstfit(a, S.int_mode ? 1 : 0, S.stream, sg.timed ? sg.ev[0] : nullptr,
                                sg.timed ? sg.ev[1] : nullptr));
   trace_add("l.firstfit");
