@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define KBG_ABI_VERSION 12
+#define KBG_ABI_VERSION 13
 
 typedef enum kbg_status {
   KBG_OK = 0,
@@ -352,33 +352,54 @@ typedef struct kbg_stats {
 
 typedef struct kbg_session kbg_session;
 
-/* Node-axis sharding across GPUs. A communicator is an RCCL
- * clique, one rank per GPU, created collectively from one unique id that the
- * caller distributes (rank 0 calls kbg_comm_unique_id; any side channel
- * carries the bytes). Shard r holds the node-table rows of 64-node words
- * [r*Wl, (r+1)*Wl), Wl = ceil(ceil(N/64)/R), so rank order is node order and
- * first-fit is the lowest rank with a fitting node. kbg_allocate (owner-
- * resolve, up to 32 ranks, sessions without pod affinity): rank 0 runs the
- * ordering engine and broadcasts each batch; every rank scans and selects its
- * own rows; a sum-reduce says which ranks fit each row; min-reduce rounds of
- * packed winners (node << 1 | kind) decide each task on the lowest rank that
- * still fits its row (a rank that fails a row hands the row's later tasks to
- * the next). The other actions (and pod-affinity sessions) all-gather the
- * per-rank bitmaps / all-reduce the victim-scan words and resolve on every
- * rank. Every rank returns the identical decision log and writes back only the
- * node rows it owns. All ranks must call kbg_session_open_sharded and the
- * actions with the same snapshot and options, in lockstep. */
+/* Node-axis sharding across GPUs (the reference has no multi-GPU
+ * counterpart: allocate.go:119-162 is one node loop). A communicator is the
+ * clique of the shards, one rank per process. Shard r holds the node-table
+ * rows of 64-node words [r*Wl, (r+1)*Wl), Wl = ceil(ceil(N/64)/R), so rank
+ * order is node order and first-fit is the lowest rank with a fitting node.
+ * kbg_allocate runs the scan service (up to 8 ranks): rank 0 runs the
+ * single-GPU pipeline, each of its scans is a launch message (ncclBroadcast)
+ * every rank answers over its own words, the ranks' candidate masks are joined
+ * by one sum-reduce, and the other ranks replay rank 0's commits.
+ * KBG_OWNER_RESOLVE=1 selects the round-4 owner-resolve protocol instead
+ * (up to 32 ranks). The other actions all-gather the per-rank bitmaps /
+ * all-reduce the victim-scan words and resolve on every rank. Every rank
+ * returns the identical decision log. All ranks must call
+ * kbg_session_open_sharded and the actions with the same snapshot and
+ * options, in lockstep.
+ *
+ * Two transports carry the same collectives in the same order:
+ *  - kbg_comm_init: an RCCL clique, one rank per GPU, created collectively
+ *    from one unique id that the caller distributes (rank 0 calls
+ *    kbg_comm_unique_id; any side channel carries the bytes); the collectives
+ *    run on the session's stream over xGMI.
+ *  - kbg_comm_init_host (ABI 13): the ranks are processes of one host that
+ *    name the same segment (`name`: letters, digits, '.', '_', '-'; fresh for
+ *    each clique, e.g. rank 0's pid and a random suffix) and may share one
+ *    device; every collective is a device -> host copy, an exchange through
+ *    POSIX shared memory and a host -> device copy. It runs the multi-rank
+ *    protocols across real processes where RCCL cannot (RCCL refuses two
+ *    ranks on one GPU). Blocks until all n_ranks ranks joined.
+ * A rank that fails inside a protocol aborts the communicator; a rank waiting
+ * on a collective polls the transport's error state, the peers' liveness
+ * (host: a peer process that exited or destroyed its communicator) and
+ * KBG_COMM_TIMEOUT_MS (default 300000), and then returns KBG_E_RCCL: a failing
+ * rank cannot hang its peers. */
 #define KBG_COMM_ID_BYTES 128
 typedef struct kbg_comm kbg_comm;
 kbg_status kbg_comm_unique_id(uint8_t out[KBG_COMM_ID_BYTES]);
 kbg_status kbg_comm_init(const uint8_t id[KBG_COMM_ID_BYTES], int32_t n_ranks, int32_t rank, int32_t device,
                          kbg_comm** out);
+kbg_status kbg_comm_init_host(const char* name, int32_t n_ranks, int32_t rank, int32_t device, kbg_comm** out);
 void kbg_comm_destroy(kbg_comm* c);
-/* The RCCL communicator's own view of the clique (ncclCommCount,
- * ncclCommUserRank): how many ranks it spans and this process's rank (ABI 11).
- * A bench line reports it so a multi-GPU figure names the ranks that actually
- * took part. */
+/* The transport's own view of the clique (RCCL: ncclCommCount,
+ * ncclCommUserRank; host: the ranks that joined the segment): how many ranks
+ * it spans and this process's rank (ABI 11). A bench line reports it so a
+ * multi-GPU figure names the ranks that actually took part. */
 kbg_status kbg_comm_ranks(const kbg_comm* c, int32_t* n_ranks, int32_t* rank);
+enum { KBG_COMM_RCCL = 0, KBG_COMM_HOST = 1 };
+/* KBG_COMM_RCCL or KBG_COMM_HOST (ABI 13); -1 for a null communicator. */
+int32_t kbg_comm_transport(const kbg_comm* c);
 
 /* ABI version and the last error message of this thread. */
 int32_t kbg_abi_version(void);

@@ -25,7 +25,6 @@
 // batch; the engine is restored from a checkpoint and replayed to the cut.
 #include <hip/hip_runtime.h>
 #include <pthread.h>
-#include <rccl/rccl.h>
 #include <sched.h>
 
 #include <algorithm>
@@ -51,17 +50,8 @@
 #include <unordered_set>
 #include <vector>
 
+#include "kbg_comm.hpp"
 #include "kbg_session.hpp"
-
-// An RCCL clique of node-axis shards, one rank per GPU (kbgpu.h).
-struct kbg_comm {
-  ncclComm_t nccl = nullptr;
-  int32_t n_ranks = 1, rank = 0, device = 0;
-  // ncclCommAbort ran (a local failure inside a collective protocol, an
-  // asynchronous RCCL error, or a peer that stopped answering): every later
-  // call on a session of this communicator fails with KBG_E_RCCL
-  std::atomic<bool> aborted{false};
-};
 
 namespace kbg {
 struct SvcLink {
@@ -88,6 +78,11 @@ kbg_status fail(kbg_status code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+}  // namespace
+
+kbg_status kbg::fail_with(kbg_status code, const std::string& msg) { return fail(code, msg); }
+
+namespace {
 
 #define HIP_TRY(expr)                                                                          \
   do {                                                                                         \
@@ -107,9 +102,9 @@ using kbg::Session;
 // progress, aborting too. Either way the call returns KBG_E_RCCL and the
 // communicator is dead for every session on it (kbgpu.h kbg_comm_init).
 void comm_abort(kbg_comm* c) {
-  if (!c || !c->nccl) return;
+  if (!c || !c->coll) return;
   bool was = false;
-  if (c->aborted.compare_exchange_strong(was, true)) (void)ncclCommAbort(c->nccl);
+  if (c->aborted.compare_exchange_strong(was, true)) c->coll->abort();
 }
 
 kbg_status comm_alive(const Session& S) {
@@ -121,7 +116,7 @@ kbg_status comm_alive(const Session& S) {
 
 // Waits for `ev` (recorded after collectives on the session's stream).
 kbg_status comm_wait(Session& S, hipEvent_t ev) {
-  if (!S.comm || !S.comm->nccl) {
+  if (!S.comm || !S.comm->coll) {
     HIP_TRY(hipEventSynchronize(ev));
     return KBG_OK;
   }
@@ -137,12 +132,11 @@ kbg_status comm_wait(Session& S, hipEvent_t ev) {
       comm_abort(S.comm);
       return fail(KBG_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
     }
-    ncclResult_t ae = ncclSuccess;
-    if ((spin & 63) == 0 && ncclCommGetAsyncError(S.comm->nccl, &ae) == ncclSuccess && ae != ncclSuccess &&
-        ae != ncclInProgress) {
-      comm_abort(S.comm);
-      return fail(KBG_E_RCCL, std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae));
-    }
+    if ((spin & 63) == 0)
+      if (const kbg_status h = S.comm->coll->health(); h != KBG_OK) {
+        comm_abort(S.comm);
+        return fail(h, S.comm->coll->err);
+      }
     if (S.comm->aborted.load()) return comm_alive(S);
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (ms > limit_ms) {
@@ -153,8 +147,11 @@ kbg_status comm_wait(Session& S, hipEvent_t ev) {
   }
 }
 
+// A collective of the session's communicator; its failure becomes this thread's error.
+kbg_status coll_rc(Session& S, kbg_status st) { return st == KBG_OK ? KBG_OK : fail(st, S.comm->coll->err); }
+
 kbg_status comm_sync(Session& S) {
-  if (!S.comm || !S.comm->nccl) {
+  if (!S.comm || !S.comm->coll) {
     HIP_TRY(hipStreamSynchronize(S.stream));
     return KBG_OK;
   }
@@ -867,10 +864,10 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
 
     if (avail) {
       const int32_t ns = sg.n_slots;
-      if (S.comm->nccl) {  // (a communicator without RCCL — R sessions of one process, tools — sums on the host)
-        const ncclResult_t nr = ncclAllReduce(S.d_down, S.d_down, (size_t)ns, ncclUint32, ncclSum, S.comm->nccl, S.stream);
-        if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
-      }
+      if (S.comm->coll)  // (a communicator without a transport — R sessions of one process, tools — sums on the host)
+        if (kbg_status st = coll_rc(S, S.comm->coll->allreduce(S.d_down, S.d_down, (size_t)ns, kbg::kCollSum, S.stream));
+            st != KBG_OK)
+          return st;
       HIP_TRY(hipMemcpyAsync(sg.h_down + fused_avail_off(S.K, a.mw), S.d_down, (size_t)ns * 4, hipMemcpyDeviceToHost,
                              S.stream));
     }
@@ -899,8 +896,8 @@ kbg_status device_launch(Session& S, kbg::Stage& sg, int32_t G, int32_t base) {
   trace_add("l.scan");
   // in-place all-gather: every rank receives every shard's slot, in rank (= node) order
   HIP_TRY(hipEventRecord(sg.ev[4], S.stream));
-  const ncclResult_t nr = ncclAllGather(out, S.d_bits, slot_words, ncclUint64, S.comm->nccl, S.stream);
-  if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
+  if (kbg_status st = coll_rc(S, S.comm->coll->allgather(out, S.d_bits, slot_words * 8, S.stream)); st != KBG_OK)
+    return st;
   HIP_TRY(hipEventRecord(sg.ev[5], S.stream));
   HIP_TRY(kbg::launch_select(S.d_bits, 0, S.W, S.Wl, G, d_capoff, S.d_down + G, S.d_down, S.stream, sg.ev[2],
                              sg.ev[3]));
@@ -4894,8 +4891,7 @@ struct RcclIO final : ShardIO {
       std::memcpy(h, buf, n * 4);
       HIP_TRY(hipMemcpyAsync(d, h, n * 4, hipMemcpyHostToDevice, S.stream));
     }
-    const ncclResult_t nr = ncclBroadcast(d, d, n, ncclUint32, 0, S.comm->nccl, S.stream);
-    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclBroadcast: ") + ncclGetErrorString(nr));
+    if (kbg_status st2 = coll_rc(S, S.comm->coll->bcast(d, n, S.stream)); st2 != KBG_OK) return st2;
     HIP_TRY(hipMemcpyAsync(h, d, n * 4, hipMemcpyDeviceToHost, S.stream));
     if (kbg_status st2 = comm_sync(S); st2 != KBG_OK) return st2;
     std::memcpy(buf, h, n * 4);
@@ -4918,8 +4914,9 @@ struct RcclIO final : ShardIO {
     if (st != KBG_OK) return st;
     std::memcpy(h, buf, n * 4);
     HIP_TRY(hipMemcpyAsync(d, h, n * 4, hipMemcpyHostToDevice, S.stream));
-    const ncclResult_t nr = ncclAllReduce(d, d, n, ncclUint32, sum ? ncclSum : ncclMin, S.comm->nccl, S.stream);
-    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+    if (kbg_status st2 = coll_rc(S, S.comm->coll->allreduce(d, d, n, sum ? kbg::kCollSum : kbg::kCollMin, S.stream));
+        st2 != KBG_OK)
+      return st2;
     HIP_TRY(hipMemcpyAsync(h, d, n * 4, hipMemcpyDeviceToHost, S.stream));
     if (kbg_status st2 = comm_sync(S); st2 != KBG_OK) return st2;
     std::memcpy(buf, h, n * 4);
@@ -5311,11 +5308,12 @@ kbg_status allocate_sharded(Session& S, ShardIO& io, kbg_decision* out, int32_t 
 }
 
 // ============================================ the scan service: rank 0 and the other ranks
-// The library's transport: RCCL on the session's stream. Rank 0 stages a
+// The library's transport: the communicator's collectives (RCCL on the
+// session's stream, or the host transport's shared memory). Rank 0 stages a
 // message in a pinned ring slot and enqueues its copy and the broadcasts
 // (header, then payload); the other ranks wait for the header to learn the
 // payload's length.
-struct RcclSvc final : SvcLink {
+struct CommSvc final : SvcLink {
   Session& S;
   static constexpr int kRing = 4;
   uint32_t* d_msg = nullptr;
@@ -5324,8 +5322,8 @@ struct RcclSvc final : SvcLink {
   bool used[kRing] = {};
   int slot = 0;
   uint32_t* h_recv = nullptr;
-  explicit RcclSvc(Session& s) : S(s) {}
-  ~RcclSvc() override {
+  explicit CommSvc(Session& s) : S(s) {}
+  ~CommSvc() override {
     if (S.stream) (void)hipStreamSynchronize(S.stream);  // no enqueued copy still reads a ring slot
     if (d_msg) (void)hipFree(d_msg);
     for (int i = 0; i < kRing; ++i) {
@@ -5347,9 +5345,7 @@ struct RcclSvc final : SvcLink {
     return KBG_OK;
   }
   kbg_status bcast(uint32_t* d, size_t n) {
-    const ncclResult_t nr = ncclBroadcast(d, d, n, ncclUint32, 0, S.comm->nccl, S.stream);
-    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclBroadcast: ") + ncclGetErrorString(nr));
-    return KBG_OK;
+    return coll_rc(S, S.comm->coll->bcast(d, n, S.stream));
   }
   kbg_status send(Session&, const uint32_t* msg) override {
     const size_t n = msg[1];
@@ -5381,12 +5377,13 @@ struct RcclSvc final : SvcLink {
   }
   kbg_status sum(Session&, kbg::Stage* sg, size_t info, size_t masks) override {
     uint32_t* dm = S.d_svc + fused_mask_off(S.K);
-    ncclGroupStart();
-    ncclResult_t nr = ncclAllReduce(S.d_svc, S.d_svc, info, ncclUint32, ncclSum, S.comm->nccl, S.stream);
-    const ncclResult_t nr2 = ncclAllReduce(dm, dm, masks, ncclUint32, ncclSum, S.comm->nccl, S.stream);
-    const ncclResult_t nr3 = ncclGroupEnd();
-    if (nr == ncclSuccess) nr = nr2 != ncclSuccess ? nr2 : nr3;
-    if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+    kbg::Coll& c = *S.comm->coll;
+    c.group_start();
+    kbg_status st = c.allreduce(S.d_svc, S.d_svc, info, kbg::kCollSum, S.stream);
+    const kbg_status st2 = c.allreduce(dm, dm, masks, kbg::kCollSum, S.stream);
+    const kbg_status st3 = c.group_end();
+    if (st == KBG_OK) st = st2 != KBG_OK ? st2 : st3;
+    if (st != KBG_OK) return coll_rc(S, st);
     if (sg) {
       HIP_TRY(hipMemcpyAsync(sg->h_down, S.d_svc, info * 4, hipMemcpyDeviceToHost, S.stream));
       HIP_TRY(hipMemcpyAsync(sg->h_down + fused_mask_off(S.K), dm, masks * 4, hipMemcpyDeviceToHost, S.stream));
@@ -5400,8 +5397,8 @@ struct RcclSvc final : SvcLink {
       if (S.shard == 0 && used[0]) HIP_TRY(hipEventSynchronize(ev_ring[0]));
       std::memcpy(h, buf + o, c * 4);
       HIP_TRY(hipMemcpyAsync(d_msg, h, c * 4, hipMemcpyHostToDevice, S.stream));
-      const ncclResult_t nr = ncclAllReduce(d_msg, d_msg, c, ncclUint32, ncclSum, S.comm->nccl, S.stream);
-      if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+      if (kbg_status st = coll_rc(S, S.comm->coll->allreduce(d_msg, d_msg, c, kbg::kCollSum, S.stream)); st != KBG_OK)
+        return st;
       HIP_TRY(hipMemcpyAsync(h, d_msg, c * 4, hipMemcpyDeviceToHost, S.stream));
       if (kbg_status st = comm_sync(S); st != KBG_OK) return st;
       std::memcpy(buf + o, h, c * 4);
@@ -6494,9 +6491,10 @@ kbg_status try_task(Session& S, Live& L, int32_t mode, int32_t t, Stmt* stmt, in
       HIP_TRY(kbg::launch_victim_big(p, S.vt, S.d_big_rows, (int32_t)S.big_rows.size(), bits, bits + S.W32,
                                      mapped ? S.h_vbig_dev : nullptr, S.stream));
     if (!mapped) {  // disjoint words of the ranks: element-wise max is their OR
-      const ncclResult_t nr =
-          ncclAllReduce(S.d_vbits, S.d_vbits_red, 2 * (size_t)S.W32, ncclUint32, ncclMax, S.comm->nccl, S.stream);
-      if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+      if (kbg_status st2 =
+              coll_rc(S, S.comm->coll->allreduce(S.d_vbits, S.d_vbits_red, 2 * (size_t)S.W32, kbg::kCollMax, S.stream));
+          st2 != KBG_OK)
+        return st2;
       HIP_TRY(hipMemcpyAsync(S.h_vbits, S.d_vbits_red, 2 * (size_t)S.W32 * sizeof(uint32_t), hipMemcpyDeviceToHost,
                              S.stream));
     }
@@ -7624,65 +7622,17 @@ kbg_status kbg_session_open_sharded(const kbg_snapshot* snap, const kbg_options*
   return session_open(snap, opts, comm, out);
 }
 
-kbg_status kbg_comm_unique_id(uint8_t out[KBG_COMM_ID_BYTES]) {
-  static_assert(sizeof(ncclUniqueId) == KBG_COMM_ID_BYTES, "ncclUniqueId size");
-  if (!out) return fail(KBG_E_INVALID, "null out");
-  ncclUniqueId id;
-  const ncclResult_t r = ncclGetUniqueId(&id);
-  if (r != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
-  std::memcpy(out, &id, sizeof(id));
-  return KBG_OK;
-}
-
-kbg_status kbg_comm_init(const uint8_t id[KBG_COMM_ID_BYTES], int32_t n_ranks, int32_t rank, int32_t device,
-                         kbg_comm** out) {
-  if (!id || !out) return fail(KBG_E_INVALID, "null argument");
-  *out = nullptr;
-  if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return fail(KBG_E_INVALID, "rank / n_ranks");
-  HIP_TRY(hipSetDevice(device));
-  ncclUniqueId uid;
-  std::memcpy(&uid, id, sizeof(uid));
-  kbg_comm* c = new (std::nothrow) kbg_comm();
-  if (!c) return fail(KBG_E_NOMEM, "comm");
-  const ncclResult_t r = ncclCommInitRank(&c->nccl, n_ranks, uid, rank);
-  if (r != ncclSuccess) {
-    delete c;
-    return fail(KBG_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-  }
-  c->n_ranks = n_ranks;
-  c->rank = rank;
-  c->device = device;
-  *out = c;
-  return KBG_OK;
-}
-
-kbg_status kbg_comm_ranks(const kbg_comm* c, int32_t* n_ranks, int32_t* rank) {
-  if (!c || !n_ranks || !rank) return fail(KBG_E_INVALID, "null argument");
-  if (!c->nccl || c->aborted.load()) return fail(KBG_E_RCCL, "the communicator is not live");
-  int n = 0, r = 0;
-  ncclResult_t nr = ncclCommCount(c->nccl, &n);
-  if (nr == ncclSuccess) nr = ncclCommUserRank(c->nccl, &r);
-  if (nr != ncclSuccess) return fail(KBG_E_RCCL, std::string("ncclCommCount: ") + ncclGetErrorString(nr));
-  *n_ranks = n;
-  *rank = r;
-  return KBG_OK;
-}
-
-void kbg_comm_destroy(kbg_comm* c) {
-  if (!c) return;
-  (void)hipSetDevice(c->device);
-  if (c->nccl && !c->aborted.load()) (void)ncclCommDestroy(c->nccl);  // (an aborted one is freed)
-  delete c;
-}
-
 kbg_status kbg_allocate(kbg_session* s, kbg_decision* out, int32_t cap, int32_t* n_out) {
   if (kbg_status st_ = usable(s); st_ != KBG_OK) return st_;
   HIP_TRY(hipSetDevice(s->s.device));
   try {
     if (scan_service_ok(s->s)) {
       if (!s->s.svc_own) {  // pinned ring and device buffer, kept for the session's later cycles
-        std::unique_ptr<RcclSvc> link(new RcclSvc(s->s));
-        if (kbg_status st = link->init(); st != KBG_OK) return st;
+        std::unique_ptr<CommSvc> link(new CommSvc(s->s));
+        if (kbg_status st = link->init(); st != KBG_OK) {
+          comm_abort(s->s.comm);  // the other ranks are about to wait on this rank's messages or sums
+          return st;
+        }
         s->s.svc_own = link.release();
       }
       SvcLink& link = *s->s.svc_own;

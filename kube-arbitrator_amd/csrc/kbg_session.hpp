@@ -613,6 +613,8 @@ inline void vc_mask_changed(Session& S, int32_t c, int32_t n) {
   if (S.vc.valid && S.vc.key.cls == c) S.vc.dirty(n);
 }
 
+// sets this thread's kbg_last_error message and returns `code`
+kbg_status fail_with(kbg_status code, const std::string& msg);
 bool parse_go_int64(const std::string& s, int64_t* out);
 bool label_key_valid(const std::string& k);    // IsQualifiedName (validation.go:42-70)
 bool label_value_valid(const std::string& v);  // IsValidLabelValue (validation.go:97-106)

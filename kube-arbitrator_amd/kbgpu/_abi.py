@@ -37,7 +37,7 @@ DISABLE_QUEUE_ORDER = 1 << 5
 DISABLE_PREDICATE = 1 << 6
 PLUGIN_REGISTERED = 0x80000000  # kbg_plugin_option.flags, read when kbg_options.plugin_registry = 1
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 COMM_ID_BYTES = 128
 
 KIND_ALLOCATE = 0
@@ -214,7 +214,9 @@ SIGNATURES = {
     "kbg_session_open_sharded": (i32, [P(kbg_snapshot), P(kbg_options), ctypes.c_void_p, P(ctypes.c_void_p)]),
     "kbg_comm_unique_id": (i32, [P(ctypes.c_uint8)]),
     "kbg_comm_init": (i32, [P(ctypes.c_uint8), i32, i32, i32, P(ctypes.c_void_p)]),
+    "kbg_comm_init_host": (i32, [ctypes.c_char_p, i32, i32, i32, P(ctypes.c_void_p)]),
     "kbg_comm_destroy": (None, [ctypes.c_void_p]),
+    "kbg_comm_transport": (i32, [ctypes.c_void_p]),
     "kbg_comm_ranks": (i32, [ctypes.c_void_p, P(i32), P(i32)]),
     "kbg_allocate": (i32, [ctypes.c_void_p, P(kbg_decision), i32, P(i32)]),
     "kbg_backfill": (i32, [ctypes.c_void_p, P(kbg_decision), i32, P(i32)]),

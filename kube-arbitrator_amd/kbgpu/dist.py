@@ -10,8 +10,11 @@ bench's barriers and the max-over-ranks wall time.
 import ctypes
 import os
 
-import torch
-import torch.distributed as dist
+
+def _td():
+    """torch.distributed, imported on first use (HostComm ranks need no torch)."""
+    import torch.distributed as dist
+    return dist
 
 
 def env_rank():
@@ -21,6 +24,7 @@ def env_rank():
 
 def init(backend):
     """Initialises the default process group from the torchrun environment."""
+    dist = _td()
     rank, world, _ = env_rank()
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -29,12 +33,14 @@ def init(backend):
 
 
 def barrier():
+    dist = _td()
     if dist.is_initialized():
         dist.barrier()
 
 
 def broadcast_bytes(data, src=0):
     """Rank `src`'s bytes on every rank (the communicator id's side channel)."""
+    dist = _td()
     if not dist.is_initialized():
         return data
     box = [data]
@@ -45,10 +51,13 @@ def broadcast_bytes(data, src=0):
 class ShardComm:
     """kbg_comm: the RCCL clique of the node-axis shards, one rank per GPU."""
 
+    transport = "rccl"
+
     def __init__(self, device, rank=None, world=None):
         from . import _abi
         L = _abi.lib()
         if rank is None:
+            dist = _td()
             rank, world = (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
         uid = (ctypes.c_uint8 * _abi.COMM_ID_BYTES)()
         if rank == 0:
@@ -60,7 +69,8 @@ class ShardComm:
         self.rank, self.world, self.device = rank, world, device
 
     def ranks(self):
-        """(ranks, this rank) as the RCCL communicator itself counts them (ncclCommCount / ncclCommUserRank)."""
+        """(ranks, this rank) as the transport itself counts them (RCCL: ncclCommCount / ncclCommUserRank;
+        host: the processes that joined the segment)."""
         from . import _abi
         n, r = ctypes.c_int32(), ctypes.c_int32()
         _abi.check(_abi.lib().kbg_comm_ranks(self.handle, ctypes.byref(n), ctypes.byref(r)))
@@ -73,10 +83,27 @@ class ShardComm:
             self.handle = ctypes.c_void_p()
 
 
+class HostComm(ShardComm):
+    """kbg_comm over the host transport (kbg_comm_init_host): the ranks are
+    processes of this host, possibly sharing one GPU, exchanging every
+    collective through POSIX shared memory. Every rank passes the same fresh
+    `name`; the call returns once all `world` ranks joined."""
+
+    transport = "host"
+
+    def __init__(self, name, rank, world, device=0):
+        from . import _abi
+        self.handle = ctypes.c_void_p()
+        _abi.check(_abi.lib().kbg_comm_init_host(name.encode(), world, rank, device, ctypes.byref(self.handle)))
+        self.rank, self.world, self.device = rank, world, device
+
+
 def aggregate(elapsed_s, decisions, sharded=False):
     """(max elapsed over ranks, placements of the whole job). Sharded ranks
     produce the same decisions for one cluster, so they count once;
     independent clusters (replicas) add up."""
+    import torch
+    dist = _td()
     if not dist.is_initialized():
         return elapsed_s, decisions
     dev = torch.device("cuda") if dist.get_backend() == "nccl" else torch.device("cpu")
@@ -88,5 +115,6 @@ def aggregate(elapsed_s, decisions, sharded=False):
 
 
 def shutdown():
+    dist = _td()
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -679,3 +679,64 @@ extern "C" int32_t kbg_tool_launch_cost(const kbg_snapshot* snap, const kbg_opti
   *roundtrip_us = rt[rt.size() / 2];
   return rows;
 }
+
+// ---------------------------------------------------------------------------
+// CPU self-test of the host transport (kbg_comm.cpp HostColl) over host
+// buffers: `iters` rounds of broadcast, sum / min / max all-reduce and
+// all-gather of n words per rank (n past 1M words crosses the 4 MB chunks),
+// every result checked against its closed form on this rank. One call per
+// process; the ranks are processes naming the same segment. Returns 0, or
+// -status with the message in kbg_last_error; *ops = collectives completed.
+extern "C" int32_t kbg_tool_hostcomm_selftest(const char* name, int32_t R, int32_t rank, int64_t n, int32_t iters,
+                                              int64_t* ops) {
+  kbg_status st = KBG_OK;
+  std::string err;
+  std::unique_ptr<kbg::Coll> c = kbg::make_host_coll(name, R, rank, &st, &err, true);
+  if (!c) {
+    g_err = err;
+    return -(int32_t)st;
+  }
+  auto val = [](int32_t r, int64_t i, int32_t it) { return (uint32_t)(r * 2654435761u + i * 40503u + it * 977u); };
+  std::vector<uint32_t> a((size_t)n), b((size_t)n), g((size_t)n * R);
+  int64_t done = 0;
+  auto bad = [&](const char* what, int32_t it, int64_t i) {
+    char m[160];
+    snprintf(m, sizeof m, "self-test: %s wrong at iteration %d word %lld", what, it, (long long)i);
+    g_err = m;
+    if (ops) *ops = done;
+    return -(int32_t)KBG_E_INVALID;
+  };
+  for (int32_t it = 0; it < iters; ++it) {
+    for (int64_t i = 0; i < n; ++i) a[i] = rank == 0 ? val(0, i, it) : 0u;
+    if ((st = c->bcast(a.data(), (size_t)n, nullptr)) != KBG_OK) break;
+    ++done;
+    for (int64_t i = 0; i < n; ++i)
+      if (a[i] != val(0, i, it)) return bad("broadcast", it, i);
+    for (int32_t op = 0; op < 3 && st == KBG_OK; ++op) {
+      for (int64_t i = 0; i < n; ++i) a[i] = val(rank, i, it);
+      if ((st = c->allreduce(a.data(), b.data(), (size_t)n, (kbg::CollOp)op, nullptr)) != KBG_OK) break;
+      ++done;
+      for (int64_t i = 0; i < n; ++i) {
+        uint32_t want = val(0, i, it);
+        for (int32_t r = 1; r < R; ++r) {
+          const uint32_t v = val(r, i, it);
+          want = op == 0 ? want + v : op == 1 ? std::min(want, v) : std::max(want, v);
+        }
+        if (b[i] != want) return bad(op == 0 ? "sum" : op == 1 ? "min" : "max", it, i);
+      }
+    }
+    if (st != KBG_OK) break;
+    for (int64_t i = 0; i < n; ++i) g[(size_t)rank * n + i] = val(rank, i, it) ^ 0x5a5a5a5au;
+    if ((st = c->allgather(g.data() + (size_t)rank * n, g.data(), (size_t)n * 4, nullptr)) != KBG_OK) break;
+    ++done;
+    for (int32_t r = 0; r < R; ++r)
+      for (int64_t i = 0; i < n; ++i)
+        if (g[(size_t)r * n + i] != (val(r, i, it) ^ 0x5a5a5a5au)) return bad("all-gather", it, i);
+  }
+  if (ops) *ops = done;
+  if (st != KBG_OK) {
+    g_err = c->err;
+    return -(int32_t)st;
+  }
+  return 0;
+}

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for fn in declared_functions():
         assert hasattr(L, fn), fn
     assert set(declared_functions()) == set(_abi.SIGNATURES)
-    assert L.kbg_abi_version() == _abi.ABI_VERSION == 12
+    assert L.kbg_abi_version() == _abi.ABI_VERSION == 13
     assert L.kbg_device_count() >= 0
 
 
