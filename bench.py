@@ -347,6 +347,10 @@ def main():
     ap.add_argument("--comm", action="store_true",
                     help="open the session through the RCCL sharded entry point even at N=1 (rehearsal)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) on MI355X; gloo to rehearse on one GPU")
+    ap.add_argument("--transport", default="rccl", choices=("rccl", "host"),
+                    help="the shards' communicator: rccl (one rank per GPU, xGMI) or host (kbg_comm_init_host: "
+                         "shared memory between the rank processes; with KBG_BENCH_DEVICE=0 and --dist-backend gloo "
+                         "the N-rank path rehearses on one GPU)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch, rendezvous and report without touching a GPU (CPU test of --gpus)")
     args = ap.parse_args()
@@ -391,7 +395,11 @@ def main():
     comm = None
     rccl_ranks = None  # ranks the RCCL communicator itself reports (ncclCommCount); None: no communicator (N=1)
     if world > 1 or args.comm:
-        comm = kdist.ShardComm(device)
+        if args.transport == "host":
+            name = kdist.broadcast_bytes(f"bench{os.getpid()}-{time.time_ns() % 10**9}".encode() if rank == 0 else b"")
+            comm = kdist.HostComm(name.decode(), rank, world, device)
+        else:
+            comm = kdist.ShardComm(device)
         base_opts["comm"] = comm
         rccl_ranks, rccl_rank = comm.ranks()
         if rccl_ranks != world or rccl_rank != rank:
@@ -598,6 +606,7 @@ def main():
     full = run_mode(1, max(1, min(10, args.steps)), 2, False)  # SURVEY roofline rule: every task scans all N
     decisions = prod["decisions"]
     elapsed, total_decisions = kdist.aggregate(prod["elapsed"], decisions, sharded=world > 1)
+    tp = "RCCL" if comm is None or comm.transport == "rccl" else "host shared-memory"
     st = prod["stats"]
     n_nodes = prod["n_nodes"]
 
@@ -629,10 +638,10 @@ def main():
         "data": "synthetic (seeded BASELINE config generator, kbgpu/synth.py)",
         "config": {"workload": f"C{cid}: {n_nodes} nodes x {prod['pending']} pending tasks, "
                                f"{prod['jobs']} gang PodGroups, {prod['queues']} proportion queues, default tiers",
-                   "parallelism": ((f"node-axis shards x{world} (owner-resolve: batch broadcast, RCCL sum/min-reduce "
+                   "parallelism": ((f"node-axis shards x{world} (owner-resolve: batch broadcast, {tp} sum/min-reduce "
                                     f"of availability and packed winners)") if os.environ.get("KBG_OWNER_RESOLVE") == "1"
-                                   else (f"node-axis shards x{world} (scan service: rank 0 commits, RCCL broadcast of "
-                                         f"each launch, every rank scans its rows, RCCL sum-reduce of the word masks)"))
+                                   else (f"node-axis shards x{world} (scan service: rank 0 commits, {tp} broadcast of "
+                                         f"each launch, every rank scans its rows, {tp} sum-reduce of the word masks)"))
                                   if world > 1 else "single-gpu",
                    "batch_tasks": base_opts.get("batch_tasks", 8192),
                    "candidates": base_opts.get("candidates", 32)},
@@ -641,6 +650,7 @@ def main():
                          "rule); bound = VALU issue (PMC), HBM traffic and the 8(d) byte figure beside it; `value` "
                          "is the production mode, which groups identical (class, request) shapes",
         "rccl_ranks": rccl_ranks,
+        "comm_transport": comm.transport if comm is not None else None,
         "cycle_roofline_8d": cycle_roofline(full, "full_scan"),
         "scan_kernel": scan_kernel(full, "full_scan"),
         "full_scan_mode": {"placements_per_s": full["decisions"] / full["elapsed"],
