@@ -310,15 +310,21 @@ constexpr int kFfGroupR = ROWS > 24 ? 2 : kFfGroup<INT_MODE>;
 #define KBG_FF_WGS_PER_CU 1  // resident workgroups per CU the full-scan geometry plans for
 #endif
 
-template <bool INT_MODE, bool EARLY_EXIT, int ROWS>
+// COMPLETE (a.complete: the walk is one round and every word's masks go out,
+// so there is no list to cut): each wave stores a writer row's masks for its
+// word right after the compares — lane j holds row j — and keeps an any-fit
+// bit per row; no LDS staging of the masks, no round barrier, no prefix-sum
+// extraction. One barrier at the end joins the any-fit bits for the info word.
+template <bool INT_MODE, bool EARLY_EXIT, bool COMPLETE, int ROWS>
 __global__ __launch_bounds__(64 * kFfWaves, kFfWaves / 4 * KBG_FF_WGS_PER_CU) void kbg_firstfit_kernel(FirstFitArgs a) {
   static_assert(ROWS % 8 == 0 && ROWS <= 4 * kFfWaves, "rows per workgroup");
   constexpr int RPW = (ROWS + kFfWaves - 1) / kFfWaves;  // rows a wave extracts (1 or 2)
+  constexpr int SW = COMPLETE ? 1 : kFfMaxRound;           // (COMPLETE: no mask staging)
   __shared__ double s_req[ROWS][3];
   __shared__ int32_t s_cls[ROWS];
   __shared__ uint32_t s_flags[ROWS], s_map[ROWS];  // shape flags (want << 1 | rel-zero fit); shape | writer
-  __shared__ uint64_t s_f[kFfMaxRound][ROWS];      // [word of the round][row]: fits (Idle or Releasing)
-  __shared__ uint64_t s_i[kFfMaxRound][ROWS];      //                        fits in Idle
+  __shared__ uint64_t s_f[SW][ROWS];               // [word of the round][row]: fits (Idle or Releasing)
+  __shared__ uint64_t s_i[SW][ROWS];               //                        fits in Idle
   __shared__ uint32_t s_done[ROWS];
   __shared__ uint16_t s_runs[kInlineShapes];
   const int lane = threadIdx.x & 63;
@@ -356,6 +362,7 @@ __global__ __launch_bounds__(64 * kFfWaves, kFfWaves / 4 * KBG_FF_WGS_PER_CU) vo
       s_cls[lane] = tr.cls;
       s_flags[lane] = (uint32_t)tr.flags;
       s_map[lane] = real ? m : (m & ~kRowWriter);
+      if (COMPLETE) s_done[lane] = 0u;  // the row's any-fit bit
     }
   }
   const int32_t tw = w_hi - w_lo;  // words this workgroup covers
@@ -418,6 +425,12 @@ __global__ __launch_bounds__(64 * kFfWaves, kFfWaves / 4 * KBG_FF_WGS_PER_CU) vo
   const int lrow = lane < ROWS ? lane : 0;
   const int cls_l = s_cls[lrow];
   const uint32_t flags_l = s_flags[lrow];
+  // COMPLETE: lane j's output row (a writer row's masks from word mask_w0), or none
+  MaskPair* const out_l =
+      COMPLETE && lane < ROWS && (s_map[lrow] & kRowWriter)
+          ? a.masks + (size_t)(s_map[lrow] & ~kRowWriter) * a.mw - a.mask_w0
+          : nullptr;
+  bool any_l = false;
   // rounds are kFfMaxRound (a multiple of kFfWaves) words apart, so a wave's
   // words are c, c + kFfWaves, ... across rounds too; lanes >= ROWS load a
   // row's mask word they never use
@@ -449,7 +462,13 @@ __global__ __launch_bounds__(64 * kFfWaves, kFfWaves / 4 * KBG_FF_WGS_PER_CU) vo
                                                                 cur.rg, keep, nrows);
         mr = (uint64_t)keep[2] | ((uint64_t)keep[3] << 32);
       }
-      if (lane < ROWS) {
+      if (COMPLETE) {
+        const uint64_t mw = lane_mw & okm;
+        const uint64_t fi = ((uint64_t)keep[0] | ((uint64_t)keep[1] << 32)) & mw;
+        const uint64_t f = fi | (mr & mw);
+        any_l |= f != 0ull;
+        if (out_l) out_l[c] = MaskPair{f, fi};
+      } else if (lane < ROWS) {
         const uint64_t mw = lane_mw & okm;
         const uint64_t fi = ((uint64_t)keep[0] | ((uint64_t)keep[1] << 32)) & mw;
         s_f[k][lane] = fi | (mr & mw);
@@ -457,6 +476,20 @@ __global__ __launch_bounds__(64 * kFfWaves, kFfWaves / 4 * KBG_FF_WGS_PER_CU) vo
       }
       cur = nxt;
       lane_mw = nxt_mw;
+    }
+    if constexpr (COMPLETE) {  // one round; the rows' any-fit bits joined over the waves
+      if (any_l && lane < ROWS) s_done[lane] = 1u;
+      FF_STAMP(2);
+      __syncthreads();
+      FF_STAMP(3);
+      if (wave == 0 && lane < ROWS && (s_map[lane] & kRowWriter)) {
+        const uint32_t sh = s_map[lane] & ~kRowWriter;
+        const bool any = s_done[lane] != 0u;
+        a.info[sh * a.info_stride + a.part0 + part] = (uint32_t)tw | (any ? kInfoAnyBit : 0u);
+        if (a.avail) a.avail[sh] = any ? a.avail_bit : 0u;
+      }
+      FF_STAMP(6);
+      return;
     }
     if (r0 == w_lo) FF_STAMP(2);
     __syncthreads();
@@ -523,16 +556,19 @@ __global__ __launch_bounds__(64 * kFfWaves, kFfWaves / 4 * KBG_FF_WGS_PER_CU) vo
   FF_STAMP(6);
 }
 
-template <bool INT_MODE, bool EARLY_EXIT>
+template <bool INT_MODE, bool EARLY_EXIT, bool COMPLETE>
 hipError_t launch_firstfit_rows(const FirstFitArgs& a, int variant, hipStream_t stream, hipEvent_t start,
                                 hipEvent_t stop) {
   const dim3 grid((a.G + a.rows - 1) / a.rows * a.splits), block(64 * kFfWaves);
   if (variant == 16)
-    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 16>), grid, block, 0, stream, start, stop, 0, a);
+    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, COMPLETE, 16>), grid, block, 0, stream, start,
+                          stop, 0, a);
   else if (variant == 24)
-    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 24>), grid, block, 0, stream, start, stop, 0, a);
+    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, COMPLETE, 24>), grid, block, 0, stream, start,
+                          stop, 0, a);
   else
-    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, 32>), grid, block, 0, stream, start, stop, 0, a);
+    hipExtLaunchKernelGGL((kbg_firstfit_kernel<INT_MODE, EARLY_EXIT, COMPLETE, 32>), grid, block, 0, stream, start,
+                          stop, 0, a);
   return hipGetLastError();
 }
 
@@ -561,12 +597,20 @@ hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t 
   if (a.G <= 0) return hipSuccess;
   const FfGeometry geo = firstfit_geometry(a.G, !a.early_exit);
   if (a.rows <= 0 || a.rows > geo.variant) return hipErrorInvalidValue;  // the host sizes both (device_launch)
-  // <.., false>: full-scan mode (every node of every row), <.., true>: production
+  // a complete walk (one round, every word out): the store-as-you-scan
+  // variant; otherwise <.., false>: full-scan mode (every node of every row),
+  // <.., true>: production
+  static const bool staged = getenv("KBG_FF_STAGED") != nullptr;  // (A/B of the round-5 extraction)
+  if (a.complete && !staged) {
+    if (a.w_hi - a.w_lo > kFfMaxRound) return hipErrorInvalidValue;
+    return int_mode ? launch_firstfit_rows<true, false, true>(a, geo.variant, stream, start, stop)
+                    : launch_firstfit_rows<false, false, true>(a, geo.variant, stream, start, stop);
+  }
   if (int_mode)
-    return a.early_exit ? launch_firstfit_rows<true, true>(a, geo.variant, stream, start, stop)
-                        : launch_firstfit_rows<true, false>(a, geo.variant, stream, start, stop);
-  return a.early_exit ? launch_firstfit_rows<false, true>(a, geo.variant, stream, start, stop)
-                      : launch_firstfit_rows<false, false>(a, geo.variant, stream, start, stop);
+    return a.early_exit ? launch_firstfit_rows<true, true, false>(a, geo.variant, stream, start, stop)
+                        : launch_firstfit_rows<true, false, false>(a, geo.variant, stream, start, stop);
+  return a.early_exit ? launch_firstfit_rows<false, true, false>(a, geo.variant, stream, start, stop)
+                      : launch_firstfit_rows<false, false, false>(a, geo.variant, stream, start, stop);
 }
 
 // ------------------------------------------------------- FitError counts

@@ -11,6 +11,6 @@ for spec in "$@"; do
   /opt/rocm/bin/hipcc -O3 -std=c++20 -fPIC -ffp-contract=off -fno-fast-math -I../include $flags --offload-arch=gfx950 \
     -c csrc/kbg_kernels.hip -o build/kern_$name.o
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o tools/variants/libkbg_tools_$name.so build/engine_bench.o \
-    build/kern_$name.o build/kbg_static.o build/kbg_affinity.o -L/opt/rocm/lib -lrccl -lpthread
+    build/kern_$name.o build/kbg_static.o build/kbg_affinity.o build/kbg_comm.o -L/opt/rocm/lib -lrccl -lpthread
   echo "built $name ($flags)"
 done
