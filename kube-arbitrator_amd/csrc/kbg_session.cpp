@@ -7308,6 +7308,7 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
   };
   int32_t T = T0;
   std::vector<uint8_t> node_set(S.n_nodes, 0);  // nodes an earlier NODE_SET of the batch gave a Node
+  std::unordered_map<int32_t, std::string> set_names;  // ... and the name it gave
   for (int32_t i = 0; i < n; ++i) {
     const kbg_event& e = ev[i];
     switch (e.kind) {
@@ -7371,8 +7372,25 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
                                          "KBG_EV_NODE_SET (its name, labels and taints)");
         break;
       case KBG_EV_NODE_SET: {
-        if (e.node < 0 || e.node >= S.n_nodes || !e.node_spec || !e.node_spec->name)
+        // every input apply_node_set rejects, so the apply step can only fail as the reference panics
+        const kbg_node_spec* sp = e.node_spec;
+        if (e.node < 0 || e.node >= S.n_nodes || !sp || !sp->name || sp->n_labels < 0 || sp->n_taints < 0 ||
+            (sp->n_labels && !sp->labels) || (sp->n_taints && !sp->taints))
           return fail(KBG_E_INVALID, "NODE_SET event");
+        for (int32_t k = 0; k < 2 * sp->n_labels; ++k)
+          if (!sp->labels[k]) return fail(KBG_E_INVALID, "NODE_SET: null label string");
+        for (int32_t k = 0; k < 3 * sp->n_taints; ++k)
+          if (!sp->taints[k]) return fail(KBG_E_INVALID, "NODE_SET: null taint string");
+        // the Node's name must stay the node's (its own, or the one an earlier NODE_SET of the batch gave it)
+        const kbg_node& nd = S.nodes_in[e.node];
+        auto named = set_names.find(e.node);
+        if (named != set_names.end()) {
+          if (named->second != sp->name) return fail(KBG_E_INVALID, "NODE_SET: the node's name differs");
+        } else if (nd.has_node) {
+          const int32_t id = S.canon_of.find(S.strs, sp->name);
+          if (id < 0 || S.canon[id] != S.canon[nd.name]) return fail(KBG_E_INVALID, "NODE_SET: the node's name differs");
+        }
+        set_names.emplace(e.node, sp->name);
         thread_local std::vector<std::pair<Res, int32_t>> pods;
         if (!S.nodes_in[e.node].has_node && !node_set[e.node] && !node_pods_of(S, e.node, &pods))
           return fail(KBG_E_UNSUPPORTED, "NODE_SET of a node holding a pod outside the session jobs whose copy the "

@@ -9,7 +9,7 @@ O=$R/gpurun_out/${RUN:-r5}
 mkdir -p $O
 cd $R
 if [ -z "$NO_TESTS" ]; then
-  timeout -k 10 ${TT:-900} python -u -m pytest ${TESTS:-tests} ${K:+-k "$K"} -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
+  timeout -k 10 ${TT:-900} python -u -m pytest ${TESTS:-tests} ${K:+-k "$K"} -m gpu -x -q -rs --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
   tail -3 $O/pytest_gpu.log
 fi
 if [ -z "$NO_SMOKE" ]; then
