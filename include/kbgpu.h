@@ -514,6 +514,9 @@ typedef struct kbg_event {
   const char* uid;       /* POD_ADD: pod UID */
   const char* pod_key;   /* POD_ADD: "<namespace>/<name>" */
   const kbg_node_spec* node_spec; /* NODE_SET */
+  const char* node_name; /* POD_UPDATE / POD_ADD (ABI 13, optional): the pod's NodeName when `node` is a node
+                            the cache knows only from pods (Node nil, Name ""); without it the session takes the
+                            NodeName that node's session pods carry, and refuses one holding none */
 } kbg_event;
 /* Applies events[0..n) in order; the cycle state is reset as by
  * kbg_session_reset (node table, class masks, plugin state back to the

@@ -211,8 +211,9 @@ struct HostColl final : Coll {
     return wait_for([&] { return hdr->bar_gen.load(std::memory_order_acquire) != g; }, what);
   }
   kbg_status enter() {
-    if (aborted_local || hdr->aborted.load(std::memory_order_acquire))
-      return failed("host communicator: aborted");
+    if (const uint32_t by = hdr->aborted.load(std::memory_order_acquire))
+      return failed("host communicator: rank " + std::to_string((int)by - 1) + " aborted it");
+    if (aborted_local) return failed("host communicator: aborted");
     hdr->ops[me].fetch_add(1, std::memory_order_relaxed);
     if (exit_after > 0 && ++ops >= exit_after) _exit(3);  // fault injection: this rank dies mid-protocol
     return KBG_OK;

@@ -2148,7 +2148,23 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   }
   S.broken.clear();
   S.node_of.clear();
-  for (int32_t n = 0; n < S.n_nodes; ++n) S.node_of[S.canon[S.nodes_in[n].name]] = n;
+  for (int32_t n = 0; n < S.n_nodes; ++n)
+    if (S.nodes_in[n].has_node) S.node_of[S.canon[S.nodes_in[n].name]] = n;
+  // sc.Nodes[NodeName] of a node the cache knows only from its pods
+  // (NewNodeInfo(nil), event_handlers.go:49-53): its Name is "", so the
+  // NodeName its pods carry is the only name it has; pod events naming it
+  // (kbg_event.node = its index) take that name
+  S.nil_name.assign(S.n_nodes, -1);
+  S.pod_only_of.clear();
+  for (int32_t n = 0; n < S.n_nodes; ++n) {
+    if (S.nodes_in[n].has_node) continue;
+    for (const int32_t t : S.node_task_order[n]) {
+      const int32_t nm = S.canon[S.tasks_in[t].node_name];
+      if (S.strs[nm].empty()) continue;
+      if (S.nil_name[n] < 0) S.nil_name[n] = nm;
+      S.pod_only_of.emplace(nm, n);
+    }
+  }
   phase("orders");
 
   // ---- plugins (framework.go:26-46): a tier entry counts only when the
@@ -2463,6 +2479,7 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   };
   headroom(S.treq, T);
   headroom(S.task_node, T);
+  headroom(S.task_cnode, T);
   headroom(S.task_job, T);
   headroom(S.tstat_in, T);
   headroom(S.pending_candidate, T);
@@ -2540,11 +2557,19 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
   phase("nodes");
   // victim candidates (preempt/reclaim): session tasks Running on each node,
   // in NodeInfo.Tasks order; a task's node by NodeName (ssn.NodeIndex)
-  if (full || (int32_t)S.task_node.size() != T) {  // an update's events keep task_node current (apply_event)
+  if (full || (int32_t)S.task_node.size() != T || (int32_t)S.task_cnode.size() != T) {
+    // (an update's events keep both current, apply_event)
     S.task_node.assign(T, -1);
+    S.task_cnode.assign(T, -1);
     for (int32_t t = 0; t < T; ++t) {
-      auto it = S.node_of.find(S.canon[S.tasks_in[t].node_name]);
-      if (it != S.node_of.end()) S.task_node[t] = it->second;
+      const int32_t nm = S.canon[S.tasks_in[t].node_name];
+      if (S.strs[nm].empty()) continue;  // no NodeName: no lookup (event_handlers.go:45-48)
+      auto it = S.node_of.find(nm);
+      if (it != S.node_of.end()) {
+        S.task_node[t] = S.task_cnode[t] = it->second;
+      } else if (auto po = S.pod_only_of.find(nm); po != S.pod_only_of.end()) {
+        S.task_cnode[t] = po->second;
+      }
     }
   }
   // An update's events change a node's list only through its NodeInfo
@@ -7056,22 +7081,39 @@ void finish_job_lists(Session& S) {
 
 int in_delete_task(Session& S, UpdateCtx& U, int32_t t) {
   job_list_mark(S, t, -1);  // JobInfo.DeleteTaskInfo
-  // the node its NodeName names (task_node: derive_host's lookup, kept
-  // current by the events); -1: no NodeName, or sc.Nodes[...] == nil
-  const int32_t n = S.task_node[t];
+  // sc.Nodes[NodeName] (task_cnode: a session node by name, or the node the
+  // cache knows only from pods carrying that NodeName; kept current by the
+  // events); -1: no NodeName, or no such NodeInfo
+  const int32_t n = S.task_cnode[t];
   if (n < 0) return 0;
   return in_node_remove(S, U, n, t);
 }
 
 kbg_status in_add_task(Session& S, UpdateCtx& U, int32_t t) {  // event_handlers.go addTask
   job_list_mark(S, t, ++S.jmove_seq);                          // JobInfo.AddTaskInfo
-  const int32_t n = S.task_node[t];
+  const int32_t n = S.task_cnode[t];
   if (n >= 0 && !terminated(S.tasks_in[t].status) && !in_node_add(S, U, n, t))
     return fail(KBG_E_REF_PANIC, "NodeInfo.AddTask: Resource.Sub underflow (node_info.go:117-123)");
   return KBG_OK;
 }
 
 kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e, const uint64_t* key_hash);
+// The NodeName a pod event's node index stands for: the node's name, or for a
+// node the cache knows only from pods the NodeName they carry (update_precheck
+// refuses a nil node whose name the session does not know); "" for -1.
+int32_t event_node_name(Session& S, const kbg_event& e) {
+  const int32_t node = e.node;
+  if (node < 0) return empty_str(S);
+  const kbg_node& nd = S.nodes_in[node];
+  if (nd.has_node) return nd.name;
+  if (e.node_name && e.node_name[0]) {  // the caller names it: the node's name from now on
+    const int32_t nm = S.canon[intern(S, e.node_name)];
+    if (S.nil_name[node] < 0) S.nil_name[node] = nm;
+    S.pod_only_of.emplace(nm, node);
+    return nm;
+  }
+  return S.nil_name[node] < 0 ? nd.name : S.nil_name[node];
+}
 // The pods of node n as NodeInfo.Tasks holds them: (Resreq, status) of each
 // session task and each pod outside the session jobs. false: an outsider
 // whose copy the snapshot did not carry (no node_pods).
@@ -7158,7 +7200,7 @@ kbg_status apply_node_set(Session& S, UpdateCtx& U, const kbg_event& e) {
     S.node_of[S.canon[name]] = e.node;
     nd.name = name;
     for (int32_t t = 0; t < S.n_tasks; ++t)  // NodeIndex[NodeName] finds the node now
-      if (S.task_live[t] && S.canon[S.tasks_in[t].node_name] == S.canon[name]) S.task_node[t] = e.node;
+      if (S.task_live[t] && S.canon[S.tasks_in[t].node_name] == S.canon[name]) S.task_node[t] = S.task_cnode[t] = e.node;
   } else {
     Res idle = to_res(nd.idle);
     const Res a0 = to_res(nd.allocatable), a1 = to_res(e.resource);
@@ -7213,8 +7255,9 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e, const uint6
         return KBG_OK;
       }
       S.tasks_in[t].status = e.status;
-      S.tasks_in[t].node_name = e.node >= 0 ? S.nodes_in[e.node].name : empty_str(S);
-      S.task_node[t] = e.node;
+      S.tasks_in[t].node_name = event_node_name(S, e);
+      S.task_node[t] = e.node >= 0 && S.nodes_in[e.node].has_node ? e.node : -1;  // ssn.NodeIndex finds it
+      S.task_cnode[t] = e.node;
       if (e.status == KBG_PENDING) S.pend_new.push_back(t);
       return in_add_task(S, U, t);
     }
@@ -7229,13 +7272,14 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e, const uint6
       k.priority = e.priority;
       k.resreq = e.resource;
       k.spec = e.spec;
-      k.node_name = e.node >= 0 ? S.nodes_in[e.node].name : empty_str(S);
+      k.node_name = event_node_name(S, e);
       k.pod_key = key_hash ? intern_h(S, e.pod_key, *key_hash) : intern(S, e.pod_key);
       const int32_t t = S.n_tasks++;
       S.tasks_in.push_back(k);
       S.task_live.push_back(1);
       S.treq.push_back(to_res(k.resreq));
-      S.task_node.push_back(e.node);
+      S.task_node.push_back(e.node >= 0 && S.nodes_in[e.node].has_node ? e.node : -1);
+      S.task_cnode.push_back(e.node);
       S.task_ranks_stale = true;
       S.rank_dirty_jobs.push_back(e.job);
       S.pend_dirty_jobs.push_back(e.job);
@@ -7294,7 +7338,7 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
     auto it = now.find(t);
     if (it != now.end()) return it->second;
     const kbg_task& k = S.tasks_in[t];
-    return Now{S.task_node[t], k.status, S.canon[k.pod_key], k.spec};
+    return Now{S.task_cnode[t], k.status, S.canon[k.pod_key], k.spec};
   };
   auto holder = [&](int32_t nd, int32_t key) -> int32_t {  // -2 / -3: a pod outside the session jobs (-3: unknown)
     const int64_t hk = ((int64_t)nd << 32) | (uint32_t)key;
@@ -7309,6 +7353,12 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
   int32_t T = T0;
   std::vector<uint8_t> node_set(S.n_nodes, 0);  // nodes an earlier NODE_SET of the batch gave a Node
   std::unordered_map<int32_t, std::string> set_names;  // ... and the name it gave
+  // a pod event's node: a node with a Node (now or from an earlier NODE_SET of
+  // the batch), or a pod-only node whose NodeName the session knows
+  auto nil_named = [&](const kbg_event& e) {
+    const int32_t nd = e.node;
+    return nd < 0 || S.nodes_in[nd].has_node || node_set[nd] || S.nil_name[nd] >= 0 || (e.node_name && e.node_name[0]);
+  };
   for (int32_t i = 0; i < n; ++i) {
     const kbg_event& e = ev[i];
     switch (e.kind) {
@@ -7318,6 +7368,9 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
         if (t < 0 || t >= T || dead[t]) return fail(KBG_E_INVALID, "event task index");
         if (e.kind == KBG_EV_POD_UPDATE && (!status_ok(e.status) || e.node < -1 || e.node >= S.n_nodes))
           return fail(KBG_E_INVALID, "event status / node");
+        if (e.kind == KBG_EV_POD_UPDATE && !nil_named(e))
+          return fail(KBG_E_UNSUPPORTED, "a pod event naming a node the cache knows only from pods outside the "
+                                         "session jobs (the NodeName is unknown to the session): re-open");
         if (!holders) {
           if (e.kind == KBG_EV_POD_DELETE) dead[t] = 1;
           break;
@@ -7349,6 +7402,9 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
         if (e.job < 0 || e.job >= S.n_jobs || e.spec < -1 || e.spec >= (int32_t)S.specs_in.size() ||
             !status_ok(e.status) || e.node < -1 || e.node >= S.n_nodes || !e.uid || !e.pod_key)
           return fail(KBG_E_INVALID, "POD_ADD event");
+        if (!nil_named(e))
+          return fail(KBG_E_UNSUPPORTED, "a pod event naming a node the cache knows only from pods outside the "
+                                         "session jobs (the NodeName is unknown to the session): re-open");
         const int32_t t = T++;
         if (!holders) break;
         int32_t key;

@@ -414,6 +414,10 @@ struct Session {
   std::vector<uint8_t> trun;                  // node-side copy still Running (an eviction makes it Releasing
                                               // for good: unevict's AddTask fails, node_info.go:101-106)
   std::vector<int32_t> task_node;             // node index of a task's NodeName (-1: not a session node)
+  std::vector<int32_t> task_cnode;            // the NodeInfo the cache's sc.Nodes[NodeName] is: task_node, or
+                                              // a node known only from pods carrying that NodeName (-1: none)
+  std::vector<int32_t> nil_name;              // per node: the NodeName its pods carry when its Node is nil (-1)
+  std::unordered_map<int32_t, int32_t> pod_only_of;  // that NodeName (canonical id) -> the node
   std::vector<kbg_eviction> evictions;        // committed cache.Evict calls
   std::vector<int32_t> t_pos;                 // a task's position in the candidate lists (-1: none)
   // what the device victim tables hold of the live state (running flags per

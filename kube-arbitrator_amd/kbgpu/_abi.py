@@ -195,7 +195,7 @@ class kbg_event(ctypes.Structure):
     _fields_ = [("kind", i32), ("task", i32), ("status", i32), ("node", i32), ("job", i32), ("spec", i32),
                 ("priority", i32), ("max_task_num", i32), ("resource", kbg_resource), ("unschedulable", i32),
                 ("reserved", i32), ("uid", ctypes.c_char_p), ("pod_key", ctypes.c_char_p),
-                ("node_spec", ctypes.POINTER(kbg_node_spec))]
+                ("node_spec", ctypes.POINTER(kbg_node_spec)), ("node_name", ctypes.c_char_p)]
 
 
 class kbg_eviction(ctypes.Structure):

@@ -154,7 +154,15 @@ class Session:
         read results through the C ABI (decisions, job / queue / node state)."""
         from .api import NodeInfo, TaskInfo, pod_key
         tidx = {t.uid: i for i, t in enumerate(self.flat.task_objs)}
-        nidx = {n: i for i, n in enumerate(self.flat.node_names)}
+        nidx = {n: i for i, n in enumerate(self.flat.node_names) if n}
+
+        def node_of(name):
+            """kbg_event.node of a pod's NodeName: the session node of that name,
+            else the node the cache knows only from pods carrying it (sc.Nodes[NodeName])."""
+            if not name:
+                return -1
+            i = nidx.get(name)
+            return i if i is not None else self.flat.pod_only_names.get(name, -1)
         evs = (_abi.kbg_event * max(1, len(changes)))()
         keep = []
         objs = {}  # task index -> its TaskInfo after the events (applied once the library accepts them)
@@ -173,6 +181,7 @@ class Session:
                     if idx is None:
                         raise ValueError(f"node {name!r}: not a node of the session (a new node needs a re-open)")
                     renamed[idx] = name
+                    nidx[name] = idx  # later events of the batch name the node by its Node's name
                 e.kind = _abi.EV_NODE_SET
                 e.node = idx
                 if os.environ.get("KBG_PY_NODE_UPDATE") == "1" and idx not in renamed:  # (A/B: Allocatable only)
@@ -197,7 +206,10 @@ class Session:
                 e.kind = _abi.EV_POD_UPDATE if kind == "pod_update" else _abi.EV_POD_DELETE
                 e.task = tidx[obj["uid"]]
                 e.status = ti.status
-                e.node = nidx.get(ti.node_name, -1) if ti.node_name else -1
+                e.node = node_of(ti.node_name)
+                if e.node >= 0 and e.node not in renamed and not self.flat.node_names[e.node]:
+                    keep.append(ti.node_name.encode())  # a node known only from pods: its NodeName
+                    e.node_name = keep[-1]
                 objs[e.task] = ti
             elif kind == "pod_add":
                 e.kind = _abi.EV_POD_ADD
@@ -205,7 +217,10 @@ class Session:
                 e.spec = self.flat.spec_index(obj)
                 e.status = ti.status
                 e.priority = ti.priority
-                e.node = nidx.get(ti.node_name, -1) if ti.node_name else -1
+                e.node = node_of(ti.node_name)
+                if e.node >= 0 and e.node not in renamed and not self.flat.node_names[e.node]:
+                    keep.append(ti.node_name.encode())
+                    e.node_name = keep[-1]
                 e.resource = _abi.kbg_resource(*ti.resreq.as_tuple())
                 keep += [ti.uid.encode(), pod_key(obj).encode()]
                 e.uid, e.pod_key = keep[-2], keep[-1]

@@ -397,6 +397,57 @@ def test_update_node_set_pod_only(seed):
     assert got["status"] in ("ok", "ref_panic")
 
 
+def _with_pods(fx, changed):
+    """fx's pods after the cache's delete + add of each changed pod (it moves to the end)."""
+    pods = {p["uid"]: p for p in fx["pods"]}
+    for p in changed:
+        pods.pop(p["uid"], None)
+        pods[p["uid"]] = p
+    return dict(fx, pods=list(pods.values()))
+
+
+@pytest.mark.parametrize("case", ["pod_only", "after_node_add", "bind_onto"])
+@pytest.mark.parametrize("seed", range(12))
+def test_update_pod_on_pod_only_node(seed, case):
+    """Pod events naming a node the cache knows only from its pods
+    (sc.Nodes[NodeName] = NewNodeInfo(nil), event_handlers.go:40-61): a
+    Running pod there completes (it leaves that NodeInfo), the same after the
+    node's Node arrived earlier in the batch (the batch's later events name it
+    by its Node's name), or a Pending pod is bound onto it. open(S0) +
+    update ≡ open(S1) ≡ the oracle on S1."""
+    import copy
+    fx0, adds, fx_full = _late_nodes(5100 + seed, k=1)
+    late = adds[0][1]["name"]
+    from kbgpu.api import RefPanic
+    try:
+        snap0 = cache_from_fixture(fx0, FakeBinder()).snapshot()
+    except RefPanic as e:
+        pytest.skip(f"S0: the reference cache panics: {e}")
+    uids = {t.uid for j in snap0.jobs for t in j.tasks.values()}
+
+    def session_pod(p):  # a pod of a job the snapshot keeps (the update names session tasks)
+        return p["uid"] in uids
+    on_late = [p for p in fx0["pods"] if p.get("nodeName") == late and p["phase"] == "Running" and session_pod(p)]
+    if case == "bind_onto":
+        pend = [p for p in fx0["pods"] if p["phase"] == "Pending" and not p.get("nodeName") and session_pod(p)]
+        if not pend:
+            pytest.skip("fixture without a Pending session pod to bind")
+        p = dict(copy.deepcopy(pend[0]), nodeName=late, phase="Running")
+    else:
+        if not on_late:
+            pytest.skip("fixture without a Running session pod on the late node")
+        p = dict(copy.deepcopy(on_late[0]), phase="Succeeded")
+    if case == "after_node_add":
+        changes = [adds[0], ("pod_update", p)]
+        fx1 = _with_pods(dict(fx0, nodes=fx0["nodes"] + [adds[0][1]]), [p])
+        fx1 = dict(fx1, nodes=[n for n in fx_full["nodes"] if n["name"] in {x["name"] for x in fx1["nodes"]}])
+    else:
+        changes = [("pod_update", p)]
+        fx1 = _with_pods(fx0, [p])
+    got = check_changes(fx0, changes, fx1, {"batch_tasks": 1 + seed % 5})
+    assert got["status"] in ("ok", "ref_panic")
+
+
 @pytest.mark.parametrize("seed", range(24))
 def test_update_node_relabel(seed):
     """UpdateNode with new labels and taints (isNodeInfoUpdated,
