@@ -339,6 +339,11 @@ __global__ __launch_bounds__(64 * kFfWaves, kFfWaves / 4 * KBG_FF_WGS_PER_CU) vo
     // lane finds its slot by a binary search there — no row -> shape map
     if (a.runs)
       for (int i = lane; i < a.n_shapes; i += 64) s_runs[i] = a.run_end[i];
+    // the search below reads entries other lanes wrote: their LDS writes are
+    // issued before its reads (wave-local ordering, no workgroup barrier)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (lane < ROWS) {
       const bool real = lane < nrows && g0 + lane < a.G;
       const int g = min(g0 + min(lane, nrows - 1), a.G - 1);  // padding rows evaluate a copy of a real row

@@ -476,6 +476,23 @@ struct Ops {
       E.in_job = true;
     }
   }
+  // After next_task() returned a task of shape known to fit nowhere: the
+  // job's following tasks whose shapes are known to fit nowhere fail too
+  // (monotone: a shape that fit nowhere fits nowhere for the rest of the
+  // action), and a failure changes no plugin state (allocate.go:163-170: the
+  // loop moves to the job's next task). They are consumed here at once; the
+  // count (0: none) is what skip() replays. The job's turn goes on with its
+  // next task, or ends when none is left.
+  int32_t skip_dead(const std::atomic<uint8_t>* failed, const int32_t* tshape) {
+    const int32_t j = E.cur_j;
+    const int32_t end = V.pend_len[j];
+    const int32_t* p = V.pend + V.pend_off[j];
+    int32_t& c = E.cursor[j];
+    const int32_t c0 = c;
+    while (c < end && failed[tshape[p[c]]].load(std::memory_order_relaxed)) ++c;
+    return c - c0;
+  }
+  void skip(int32_t n) { E.cursor[E.cur_j] += n; }  // n failed tasks of the current job (skip_dead's count)
   // Outcome of the node loop for the task returned by next_task().
   // Success = ssn.Allocate / ssn.Pipeline: drf + proportion AllocateFunc
   // (drf.go:131-139, proportion.go:197-206), then jobs.Push / queues.Push.
@@ -1335,6 +1352,27 @@ struct Grouper {
 // (same inputs, same table): the prefix an earlier row of the shape rejected
 // is skipped instead of re-checked (`shape_skip`).
 enum { RES_OK = 0, RES_TRUNC = 1, RES_PANIC = 2 };
+// The in-order commit's view of one node, in one cache line: what a
+// re-check of a candidate touched since its scan reads (Idle, Releasing, pod
+// count and cap, the stamp of the node's last commit, the nil-Node panic
+// flag), instead of five separate arrays. The allocate committer keeps it
+// current with every commit (mirror_row).
+struct alignas(64) MirrorRow {
+  double ic, im, ig, rc, rm, rg;
+  int32_t nt, mt;
+  int32_t mark;
+  int32_t panic;
+};
+static_assert(sizeof(MirrorRow) == 64, "one cache line per node");
+inline void mirror_row(const Session& S, MirrorRow& q, int32_t nd) {
+  q.ic = S.idle[nd].c;
+  q.im = S.idle[nd].m;
+  q.ig = S.idle[nd].g;
+  q.rc = S.rel[nd].c;
+  q.rm = S.rel[nd].m;
+  q.rg = S.rel[nd].g;
+  q.nt = S.ntasks[nd];
+}
 struct Resolver {
   Session& S;
   std::vector<int32_t>& mark;
@@ -1349,6 +1387,8 @@ struct Resolver {
   // stays rejected under every later scan: a fresh stage's cursor starts
   // there instead of re-checking the nodes the earlier batches filled.
   int32_t* floor = nullptr;
+  // the committer's packed mirror (nullptr: the separate arrays and `mark`)
+  const MirrorRow* rows = nullptr;
   void reset(const kbg::Stage& stage) {
     sg = &stage;
     base = stage.base;
@@ -1410,6 +1450,51 @@ struct Resolver {
     const bool cap = S.pred_active, masked = S.has_ports || S.has_aff, aff = S.has_aff, be = S.be_task[t];
     const uint64_t* cmask = S.h_class_mask.data() + (size_t)S.task_class[t] * S.W;
     const int32_t bs = base;
+    if (rows) {  // the same walk over one cache line per candidate
+      const int32_t* awm = aff ? S.mwmark.data() + (size_t)S.task_class[t] * S.W : nullptr;
+      const double rc_ = r.c, rm_ = r.m, rg_ = r.g;
+      auto fits = [&](double a0, double a1, double a2) {  // Resource.LessEqual (resource_info.go:142-146)
+        return (rc_ < a0 || __builtin_fabs(a0 - rc_) < kbg::kMinMilliCPU) &&
+               (rm_ < a1 || __builtin_fabs(a1 - rm_) < kbg::kMinMemory) &&
+               (rg_ < a2 || __builtin_fabs(a2 - rg_) < kbg::kMinMilliGPU);
+      };
+      while (k < end && res < 0) {
+        const int32_t w = k >> 6;
+        uint64_t bits = m[w].f & (~0ull << (k & 63));
+        const bool wdirty = aff && awm[w] > bs;
+        while (bits) {
+          const int32_t nd = (w << 6) | __builtin_ctzll(bits);
+          bits &= bits - 1;
+          if (bits) __builtin_prefetch(rows + ((w << 6) | __builtin_ctzll(bits)));
+          const MirrorRow& q = rows[nd];
+          ++steps;
+          if (q.panic) {
+            k = nd;
+            res = RES_PANIC;
+            break;
+          }
+          if (!(q.mark > bs || wdirty)) {
+            k = nd;
+            *node = nd;
+            *kind = ((m[w].i >> (nd & 63)) & 1ull) ? KBG_KIND_ALLOCATE : KBG_KIND_PIPELINE;
+            res = RES_OK;
+            break;
+          }
+          ++rechecks;  // touched since the scan: re-check on the host mirror
+          if (cap && q.nt >= q.mt) continue;
+          if (masked && !((cmask[w] >> (nd & 63)) & 1ull)) continue;
+          const int v = be ? 1 : fits(q.ic, q.im, q.ig) ? 1 : fits(q.rc, q.rm, q.rg) ? 2 : 0;
+          if (v) {
+            k = nd;
+            *node = nd;
+            *kind = v == 1 ? KBG_KIND_ALLOCATE : KBG_KIND_PIPELINE;
+            res = RES_OK;
+            break;
+          }
+        }
+        if (res < 0) k = (w + 1) << 6;
+      }
+    }
     while (k < end && res < 0) {
       const int32_t w = k >> 6;
       uint64_t bits = m[w].f & (~0ull << (k & 63));
@@ -3350,6 +3435,9 @@ inline void mark_failed(std::atomic<uint8_t>* f, int32_t sh) {
 struct Batch {
   std::vector<int32_t> bt;
   std::vector<char> bpred;
+  // per entry: the tasks of its job right after it, of shapes known to fit
+  // nowhere, consumed with it as failures (Ops::skip_dead); 0 for most
+  std::vector<int32_t> brun;
   Engine ckpt;
   int64_t epoch = 0;
   // rows built ahead by the builder thread (G >= 0) into a pinned buffer
@@ -3370,6 +3458,7 @@ struct Pipe {
   const Engine* rb_truth = nullptr;  // the committed outcomes' engine, idle until the next batch
   std::vector<int32_t> rb_tasks;
   std::vector<char> rb_actual;
+  std::vector<int32_t> rb_runs;
   bool stop = false;
   std::atomic<bool> hungry{false};  // the committer is blocked on an empty queue: emit what is predicted
   std::atomic<int64_t> epoch_now{0};  // = epoch, read without the lock: a batch of an older epoch is abandoned
@@ -3746,13 +3835,19 @@ kbg_status copy_log(Session& S, kbg_decision* out, int32_t cap, int32_t* n_out, 
 // single-rank allocate it is the engine's "truth" a few tasks behind the
 // committer: at a cut the predictor takes its state instead of restoring a
 // checkpoint and replaying the batch's prefix.
+// One committed outcome for an engine replay: task, placed or not, and the
+// failed tasks of its job consumed with it (Batch::brun).
+struct Outcome {
+  int32_t t, run;
+  char ok;
+};
 struct Replayer {
   Session& S;
   Engine& E;
   std::thread th;
   std::mutex mu;
   SpinCV cv;
-  std::deque<std::vector<std::pair<int32_t, char>>> q;
+  std::deque<std::vector<Outcome>> q;
   bool done = false, busy = false;
   std::string error;
   // committer_cpu >= 0: on its own core of the committer's last-level cache
@@ -3764,10 +3859,15 @@ struct Replayer {
     });
   }
   ~Replayer() { join(); }
-  void push(std::vector<std::pair<int32_t, char>>&& v) {
+  void push(std::vector<Outcome>&& v) {
     std::lock_guard<std::mutex> lk(mu);
     q.push_back(std::move(v));
     cv.notify_all();
+  }
+  void push(const std::vector<std::pair<int32_t, char>>& v) {
+    std::vector<Outcome> o(v.size());
+    for (size_t k = 0; k < v.size(); ++k) o[k] = Outcome{v[k].first, 0, v[k].second};
+    push(std::move(o));
   }
   void join() {
     {
@@ -3797,7 +3897,7 @@ struct Replayer {
   void run() {
     Ops ops{S, E, nullptr};
     for (;;) {
-      std::vector<std::pair<int32_t, char>> v;
+      std::vector<Outcome> v;
       {
         std::unique_lock<std::mutex> lk(mu);
         busy = false;
@@ -3808,13 +3908,14 @@ struct Replayer {
         q.pop_front();
         busy = true;
       }
-      for (const auto& [t, ok] : v) {
+      for (const Outcome& o : v) {
         if (!error.empty()) break;
-        if (ops.next_task() != t) {
+        if (ops.next_task() != o.t) {
           error = "internal: engine replay diverged from the committed outcomes";
           break;
         }
-        ops.apply(t, ok);
+        ops.apply(o.t, o.ok);
+        if (o.run) ops.skip(o.run);
       }
     }
   }
@@ -3836,6 +3937,7 @@ struct Predictor {
   std::thread th, bth;
   bool builder = false;       // a builder thread turns predicted batches into device rows (allocate_cycle)
   bool truth_mode = false;    // rollbacks copy a truth engine (rollback_truth): no batch checkpoints
+  bool runs = false;          // consume a job's tasks of shapes known to fit nowhere as one entry (Batch::brun)
   std::vector<Batch*> all;    // every batch of this predictor (freed by finish)
   Predictor(Session& s, Engine& e, std::atomic<uint8_t>* f) : S(s), E(e), failed(f) {
     prof.on = getenv("KBG_PROFILE_ENGINE") != nullptr;
@@ -3922,6 +4024,7 @@ struct Predictor {
               return;
             }
             ops.apply(t, P.rb_actual[k]);
+            if (k < P.rb_runs.size() && P.rb_runs[k]) ops.skip(P.rb_runs[k]);
           }
           replayed += (int64_t)P.rb_tasks.size();
           engine_ms += ms_since(tp);
@@ -3953,6 +4056,7 @@ struct Predictor {
       b->epoch = my_epoch;
       b->bt.clear();
       b->bpred.clear();
+      b->brun.clear();
       // right after a cut the committer waits with nothing to scan: hand it
       // the first 64 tasks (the next cut is often a few tasks away)
       const size_t emit_at = restarted ? 64 : (size_t)min_emit();
@@ -3966,6 +4070,7 @@ struct Predictor {
         b->bt.push_back(t);
         b->bpred.push_back(p);
         ops.apply(t, p);
+        b->brun.push_back(!p && runs ? ops.skip_dead(failed, tshape) : 0);
         if ((b->bt.size() & 63) == 0) {
           // the committer cut an earlier batch: this one follows a wrong
           // prediction, stop here and roll back
@@ -4028,6 +4133,7 @@ struct Predictor {
     P.rb_ckpt = cur->ckpt;
     P.rb_tasks.assign(cur->bt.begin(), cur->bt.begin() + cut);
     P.rb_actual.assign(actual.begin(), actual.begin() + cut);
+    P.rb_runs.assign(cur->brun.begin(), cur->brun.begin() + std::min<size_t>(cut, cur->brun.size()));
     P.free.push_back(cur);
     if (nxt) P.free.push_back(nxt);
     P.cv.notify_all();
@@ -4176,6 +4282,21 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     shape_floor.assign(std::max(1, S.n_shapes), 0);
     rs.floor = shape_floor.data();
   }
+  static const bool packed = [] {
+    const char* e = getenv("KBG_PACKED_MIRROR");
+    return !e || std::atoi(e) != 0;
+  }();
+  std::vector<MirrorRow> mrow;
+  if (packed) {
+    mrow.resize(S.n_nodes);
+    for (int32_t n = 0; n < S.n_nodes; ++n) {
+      mirror_row(S, mrow[n], n);
+      mrow[n].mt = S.maxtasks[n];
+      mrow[n].mark = -1;
+      mrow[n].panic = S.panic_node[n];
+    }
+    rs.rows = mrow.data();
+  }
   // The log side of the walk (decision log, gang dispatch, FitError
   // bookkeeping) on a thread of its own, unless host ports or colliding pod
   // keys need the pre-commit port rows (then inline, below).
@@ -4196,6 +4317,11 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   Replayer truth(S, E_truth, sched_getcpu());
   Predictor pr(S, E, failed.get());
   pr.truth_mode = true;
+  // a job's run of tasks of shapes known to fit nowhere is one batch entry
+  // (Batch::brun); not in full-scan mode, where every task evaluation scans
+  // the table. KBG_NO_RUNS=1 (A/B) turns it off.
+  static const bool no_runs = getenv("KBG_NO_RUNS") != nullptr;
+  pr.runs = !S.opts.full_scan && !no_runs;
   EngineProfile& eprof = pr.prof;
   Trace ctr;
   ctr.start(t0);
@@ -4219,14 +4345,14 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   // KBG_NO_TRUTH=1 (experiment, cut-free cycles only): no truth engine; the
   // predictor's own engine is the cycle's final state
   static const bool no_truth = getenv("KBG_NO_TRUTH") != nullptr;
-  auto to_truth = [&](const std::vector<int32_t>& bt, int32_t end) {
+  auto to_truth = [&](const Batch* b, int32_t end) {
     if (no_truth) {
       truth_from = end;
       return;
     }
     if (end <= truth_from) return;
-    std::vector<std::pair<int32_t, char>> v(end - truth_from);
-    for (int32_t k = truth_from; k < end; ++k) v[k - truth_from] = {bt[k], bactual[k]};
+    std::vector<Outcome> v(end - truth_from);
+    for (int32_t k = truth_from; k < end; ++k) v[k - truth_from] = Outcome{b->bt[k], b->brun[k], bactual[k]};
     truth.push(std::move(v));
     truth_from = end;
   };
@@ -4514,7 +4640,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     truth_from = 0;
     for (int32_t i = 0; i < nb; ++i) {
       const int32_t t = bt[i];
-      if ((i & 511) == 511) to_truth(bt, i);  // keep the truth engine a few hundred tasks behind
+      if ((i & 511) == 511) to_truth(cur, i);  // keep the truth engine a few hundred tasks behind
       if ((i & 127) == 127 && reuse) {  // contended: a refresh scan to start or to switch to
         if ((st = refresh_poll()) != KBG_OK) return abort(st);
       }
@@ -4619,6 +4745,26 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       const bool ok = node >= 0;
       bactual[i] = ok;
       S.stats.task_evaluations++;
+      // the failed tasks of the job the predictor consumed with this one
+      // (their shapes fit nowhere: the committer marked them so itself)
+      const int32_t run = cur->brun[i];
+      int32_t t_last = t;
+      if (run && ok) return abort(fail(KBG_E_INVALID, "internal: a task of a shape known to fit nowhere was placed"));
+      if (run) {
+        const int32_t j = S.task_job[t];
+        const int32_t* jp = S.pend.data() + S.pend_off[j];
+        const int32_t pos = (int32_t)(std::find(jp, jp + S.pend_len[j], t) - jp);  // t's place in its job's order
+        t_last = jp[pos + run];
+        S.stats.task_evaluations += run;
+        if (S.svc) {  // every rank replays them one by one
+          S.svc_out.push_back((uint32_t)t);
+          S.svc_out.push_back(~0u);
+          for (int32_t k = 1; k < run; ++k) {
+            S.svc_out.push_back((uint32_t)jp[pos + k]);
+            S.svc_out.push_back(~0u);
+          }
+        }
+      }
       if (reuse_ok) {
         const int32_t sh = S.task_shape[t];
         if (shape_rep[sh] < 0) {
@@ -4627,7 +4773,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         }
       }
       if (S.svc) {  // the scan service: every rank replays the committed outcomes
-        S.svc_out.push_back((uint32_t)t);
+        S.svc_out.push_back((uint32_t)t_last);
         S.svc_out.push_back(ok ? ((uint32_t)node << 1 | (kind == KBG_KIND_PIPELINE ? 1u : 0u)) : ~0u);
       }
       if (ok) {
@@ -4641,6 +4787,10 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
           mark[node] = rstamp;
           touched.push_back(node);
         }
+        if (packed) {
+          mirror_row(S, mrow[node], node);
+          mrow[node].mark = rstamp;
+        }
         const uint64_t c2 = rprof ? cycles() : 0;
         const LogItem it{t, node, kind, true, true, dup, old};
         if (lg) items.push_back(it);
@@ -4651,7 +4801,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         }
       } else {
         mark_failed(failed.get(), S.task_shape[t]);
-        const LogItem it{t, -1, 0, false, true, false, Res{}};
+        const LogItem it{t_last, -1, 0, false, true, false, Res{}};  // the job's last evaluated task (FitError)
         if (lg) items.push_back(it);
         else log_one(it);
       }
@@ -4723,7 +4873,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
         }
         probe_failed(*sg);
       }
-      to_truth(bt, cut);
+      to_truth(cur, cut);
       ctr.add("cut", cut);
       truth.wait_idle();
       ctr.add("truth", cut);
@@ -4745,7 +4895,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
       }
       continue;
     }
-    to_truth(bt, nb);
+    to_truth(cur, nb);
     recycle(cur);
     if (reuse) {  // the next batch resolves against the same lists while they last
       if ((st = refresh_poll()) != KBG_OK) return abort(st);
