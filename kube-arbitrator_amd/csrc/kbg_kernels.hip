@@ -605,8 +605,7 @@ hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t 
   // a complete walk (one round, every word out): the store-as-you-scan
   // variant; otherwise <.., false>: full-scan mode (every node of every row),
   // <.., true>: production
-  static const bool staged = getenv("KBG_FF_STAGED") != nullptr;  // (A/B of the round-5 extraction)
-  if (a.complete && !staged) {
+  if (a.complete) {
     if (a.w_hi - a.w_lo > kFfMaxRound) return hipErrorInvalidValue;
     return int_mode ? launch_firstfit_rows<true, false, true>(a, geo.variant, stream, start, stop)
                     : launch_firstfit_rows<false, false, true>(a, geo.variant, stream, start, stop);

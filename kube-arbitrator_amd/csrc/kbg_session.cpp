@@ -4282,10 +4282,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
     shape_floor.assign(std::max(1, S.n_shapes), 0);
     rs.floor = shape_floor.data();
   }
-  static const bool packed = [] {
-    const char* e = getenv("KBG_PACKED_MIRROR");
-    return !e || std::atoi(e) != 0;
-  }();
+  constexpr bool packed = true;
   std::vector<MirrorRow> mrow;
   if (packed) {
     mrow.resize(S.n_nodes);

@@ -14,10 +14,10 @@ for lib in kube-arbitrator_amd/tools/variants/libkbg_tools_*.so; do
   echo "$n $(cat $O/$n.$i.json)"
 done
 done
-for kv in "" "HIP_FORCE_DEV_KERNARG=1" "HIP_FORCE_DEV_KERNARG=0"; do
-  env $kv timeout -k 10 240 python kube-arbitrator_amd/tools/ff_bench.py ${CONFIG:-3} > $O/kernarg.json 2> $O/kernarg.err || { tail -20 $O/kernarg.err; exit 1; }
-  echo "kernarg[$kv] $(cat $O/kernarg.json)"
-done
+if [ -n "$TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
+  tail -2 $O/pytest.log
+fi
 timeout -k 10 240 python kube-arbitrator_amd/tools/ff_stamps.py ${CONFIG:-3} > $O/ff_stamps.json 2> $O/ff_stamps.err || { tail -20 $O/ff_stamps.err; exit 1; }
 cat $O/ff_stamps.json
 echo FFVAR_DONE
