@@ -106,11 +106,18 @@ def cpu_model():
     return "unknown"
 
 
+_JOB_CPUS = None
+
+
 def job_cpus():
-    """The CPUs this process may run on (the GPU box gives a job a share of the host)."""
-    if hasattr(os, "sched_getaffinity"):
-        return sorted(os.sched_getaffinity(0))
-    return list(range(os.cpu_count() or 1))
+    """The CPUs this process may run on (the GPU box gives a job a share of
+    the host), as at the first call: the CPU baselines pin this process to one
+    of them meanwhile."""
+    global _JOB_CPUS
+    if _JOB_CPUS is None:
+        _JOB_CPUS = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else \
+            list(range(os.cpu_count() or 1))
+    return list(_JOB_CPUS)
 
 
 def cpu_quota():
@@ -143,10 +150,14 @@ def usable_cpus():
 
 def omp_sweep():
     """B-omp thread counts (the node loop parallelised over all
-    host cores, stated): 4, 8, 16, 32, 64 and every CPU the job can use, none
-    above that (past the cgroup quota threads only time-slice)."""
+    host cores, stated): 4, 8, 16, 32, 64 and every CPU the job can use less
+    two, none above that. Past the cgroup quota threads only time-slice, and
+    the two left over keep the bench process and the HIP runtime's own threads
+    off the team's CPUs (round 5's 16-thread run on a 16-CPU quota collapsed
+    to a quarter of its 8-thread rate sharing them)."""
     n = usable_cpus()
-    return sorted({t for t in (4, 8, 16, 32, 64) if t < n} | {n})
+    top = max(1, n - 2) if n > 4 else n
+    return sorted({t for t in (4, 8, 16, 32, 64) if t < top} | {top})
 
 
 def spawn_ranks(n):
@@ -220,7 +231,10 @@ def cpu_baseline(fx, label, threads=1, faithful=False, budget=0.0):
         src = fixture_file(fx)
         with tempfile.TemporaryDirectory() as d:
             dst = os.path.join(d, "out.json")
-            cpus = ",".join(str(c) for c in job_cpus()[:threads])
+            # the team on the job's last CPUs, away from this process (pinned to
+            # the first one below while the baseline runs)
+            mine = job_cpus()
+            cpus = ",".join(str(c) for c in (mine[-threads:] if len(mine) > threads else mine))
             cmd = ["taskset", "-c", cpus, ref, "--threads", str(threads)]
             if faithful:
                 cmd.append("--faithful")
@@ -673,6 +687,9 @@ def main():
         # bounded samples where a full cycle takes longer than ~30 s of CPU
         # (C3's failing tasks walk every node, C4 is 500k tasks)
         budget = {1: 0.0, 2: 0.0, 3: 20.0}.get(cid, 60.0)
+        mask = job_cpus()
+        if hasattr(os, "sched_setaffinity") and len(mask) > 2:
+            os.sched_setaffinity(0, {mask[0]})  # this process (and its idle runtime threads) off the team's CPUs
         line["cpu_baseline"] = cpu_baseline(fx, f"C{cid}", 1, budget=budget)
         sweep = [cpu_baseline(fx, f"C{cid}", t, budget=budget) for t in omp_sweep()]
         sweep = [b for b in sweep if b]
@@ -682,6 +699,8 @@ def main():
                                               for b in sweep]
         if not args.no_faithful:
             line["cpu_baseline_faithful"] = cpu_baseline(fx, f"C{cid}", 1, faithful=True, budget=20.0)
+        if hasattr(os, "sched_setaffinity") and len(mask) > 2:
+            os.sched_setaffinity(0, set(mask))
     if rank == 0:
         emit(line)
     if comm is not None:
