@@ -486,10 +486,29 @@ enum {
   KBG_EV_POD_ADD = 3,    /* cache.AddPod: a new pod of session job `job` (index = the session's task count) */
   KBG_EV_NODE_UPDATE = 4, /* cache.UpdateNode -> NodeInfo.SetNode: node `node` gets `resource` as Allocatable,
                              `max_task_num` pods and `unschedulable` (labels and taints unchanged) */
-  KBG_EV_NODE_SET = 5     /* cache.AddNode / UpdateNode -> NodeInfo.SetNode with the whole Node (event_handlers.go
+  KBG_EV_NODE_SET = 5,    /* cache.AddNode / UpdateNode -> NodeInfo.SetNode with the whole Node (event_handlers.go
                              232-259, node_info.go:84-99): node `node` gets `node_spec`'s name, labels and taints,
                              `resource`, `max_task_num` and `unschedulable` — also a node the cache only knew from
                              a pod (NewNodeInfo(nil), Name ""), which then takes the name its pods' NodeName held */
+  /* Structural events (ABI 13): the session's sets of nodes, jobs and queues
+   * change. Indices in a batch are those before the batch (new ones take the
+   * next index of their kind, in event order); after the batch every kind is
+   * renumbered — what left is dropped, the rest keeps its order, new ones
+   * last — and kbg_session_renumbering gives the old -> new maps. */
+  KBG_EV_NODE_ADD = 6,     /* cache.AddNode of a node new to the cache (event_handlers.go:232-240, NewNodeInfo):
+                              `node_spec`, `resource`, `max_task_num`, `unschedulable`; it joins ssn.Nodes last */
+  KBG_EV_NODE_DELETE = 7,  /* cache.DeleteNode (event_handlers.go:262-268): node `node` leaves sc.Nodes with the
+                              pods on it; their tasks stay in their jobs, on no node (NodeName unchanged) */
+  KBG_EV_JOB_ADD = 8,      /* cache.AddPodGroup of a new job (event_handlers.go:344-358, setPodGroup): JobID
+                              `name`, queue index `queue`, `min_available`, `creation_ns`, `priority`; it joins
+                              ssn.Jobs last, its pods follow as KBG_EV_POD_ADD */
+  KBG_EV_JOB_DELETE = 9,   /* cache.DeletePodGroup (event_handlers.go:361-381, UnsetPodGroup): job `job` leaves
+                              ssn.Jobs; its pods stay on their nodes as pods outside the session jobs and its
+                              Running tasks join Session.Others (cache.go:570-582) */
+  KBG_EV_QUEUE_ADD = 10,   /* cache.AddQueue (event_handlers.go:635-640): queue `name` with `weight` joins ssn.Queues
+                              last */
+  KBG_EV_QUEUE_DELETE = 11 /* cache.DeleteQueue (event_handlers.go:650-654): queue `queue` leaves ssn.Queues, and
+                              every job of it leaves ssn.Jobs (cache.go:584-588; not into Others) */
 };
 /* The Node of a KBG_EV_NODE_SET event (strings are copied). */
 typedef struct kbg_node_spec {
@@ -517,6 +536,12 @@ typedef struct kbg_event {
   const char* node_name; /* POD_UPDATE / POD_ADD (ABI 13, optional): the pod's NodeName when `node` is a node
                             the cache knows only from pods (Node nil, Name ""); without it the session takes the
                             NodeName that node's session pods carry, and refuses one holding none */
+  const char* name;      /* JOB_ADD: JobID "<namespace>/<podgroup>"; QUEUE_ADD: the queue's name */
+  int64_t creation_ns;   /* JOB_ADD: CreationTimestamp */
+  int32_t queue;         /* JOB_ADD: its queue; QUEUE_DELETE: the queue */
+  int32_t min_available; /* JOB_ADD: PodGroup.Spec.MinMember */
+  int32_t weight;        /* QUEUE_ADD: Queue.Spec.Weight */
+  int32_t reserved2;
 } kbg_event;
 /* Applies events[0..n) in order; the cycle state is reset as by
  * kbg_session_reset (node table, class masks, plugin state back to the
@@ -533,6 +558,16 @@ typedef struct kbg_event {
  * while the events are applied: the session is then unusable and every later
  * call on it but kbg_session_close returns KBG_E_INVALID (re-open it). */
 kbg_status kbg_session_update(kbg_session* s, const kbg_event* events, int32_t n);
+/* After an update with structural events: the map old index -> new index
+ * (-1: it left the session) of tasks, nodes, jobs or queues (kind
+ * KBG_RENUM_*), over the indices valid before the update plus the ones its
+ * events created. *n_out = the map's length (0: the last update renumbered
+ * nothing — every index kept). A structural update rebuilds the session from
+ * its own updated snapshot (the cost of an open, without the caller's
+ * snapshot); pods that predate their PodGroup or queue (already on a node
+ * as pods outside the session jobs) are refused (KBG_E_UNSUPPORTED). */
+enum { KBG_RENUM_TASKS = 0, KBG_RENUM_NODES = 1, KBG_RENUM_JOBS = 2, KBG_RENUM_QUEUES = 3 };
+kbg_status kbg_session_renumbering(kbg_session* s, int32_t kind, int32_t* out, int32_t cap, int32_t* n_out);
 
 /* Restores the state captured at kbg_session_open (device-side copy); used to
  * re-run a cycle on the same snapshot without re-uploading it. */

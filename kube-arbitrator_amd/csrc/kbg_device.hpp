@@ -296,9 +296,10 @@ struct FitArgs {
   const int32_t* hoff;         // [N + 1] each node's decisions
   const int32_t* hk;           // decision index | 0x80000000 for a Pipeline
   const double* hold;          // [3] per decision: the Idle (Allocate) / Releasing (Pipeline) before it
+  const int32_t* na;           // per decision: the first Allocate at or after it on its node, -1 none
   const FitQuery* q;
   int32_t nq, cap_check;
-  int32_t* out;                // [nq][4]: entries, negative cpu, memory, GPU deltas
+  int32_t* out;                // [nq][4]: entries, negative cpu, memory, GPU deltas (host-mapped)
   int32_t tab_lo, tab_n;       // the global nodes the table holds (a shard of the scan service: its own)
 };
 hipError_t launch_fitdelta(const FitArgs& a, hipStream_t stream);

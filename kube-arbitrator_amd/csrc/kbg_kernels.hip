@@ -620,59 +620,98 @@ hipError_t launch_firstfit(const FirstFitArgs& a, int32_t int_mode, hipStream_t 
 // ------------------------------------------------------- FitError counts
 // JobInfo.NodesFitDelta of a not-ready job's last evaluated task
 // (allocate.go:116-144), summarised as JobInfo.FitError counts it
-// (job_info.go:329-358), for every such job at once: one workgroup per job,
-// its threads over the nodes before the task's end. A node's state at the
+// (job_info.go:329-358), for every such job at once. A node's state at the
 // task's evaluation point is the final table with the decisions at or after
 // that point undone: the node's decisions in order (hk, hold), the first
 // undone Allocate giving its Idle, the undone count its pod count.
-__global__ __launch_bounds__(256) void kbg_fitdelta_kernel(FitArgs a) {
-  __shared__ int32_t s_cnt[4];
-  const FitQuery fq = a.q[blockIdx.x];
-  if (threadIdx.x < 4) s_cnt[threadIdx.x] = 0;
+// A workgroup of 16 waves takes kFitJobs jobs and walks the table 1024
+// nodes at a time, a lane per node: the node's records (decision range, pod
+// counts, Idle) are loaded once for all the group's jobs, whose static mask
+// words are wave-uniform loads. A node's decisions are in log order, so the
+// first one at or after a job's point is a binary search of its range, and
+// the first undone Allocate from there one load of the host's next-Allocate
+// index (na), then the Idle logged before it. Counts: per-wave ballots and
+// popcounts, summed in LDS per job. Measured at C3 (937 jobs x 5120 nodes,
+// profiles/r06/fitdelta_ab.txt): one workgroup per job walking each node's
+// decisions a load at a time (round 5) 40 µs per launch — first-fit piles
+// hundreds of decisions on the first nodes; one workgroup per job with
+// binary searches 33 µs; 2 / 4 / 8 / 16 jobs per workgroup 19.9 / 23.4 / 41 /
+// 119 µs (sharing the node loads against fewer workgroups, each a chain of
+// dependent loads per pass); a grid over (node chunk, job) with
+// cross-workgroup sums 540 µs (device-scope fences and atomics between XCDs).
+constexpr int kFitBlock = 1024;
+constexpr int kFitJobs = 2;
+__global__ __launch_bounds__(kFitBlock) void kbg_fitdelta_kernel(FitArgs a) {
+  __shared__ int32_t s_cnt[kFitJobs][4];
+  const int q0 = blockIdx.x * kFitJobs;
+  const int nj = min(kFitJobs, a.nq - q0);
+  if (threadIdx.x < kFitJobs * 4) s_cnt[threadIdx.x >> 2][threadIdx.x & 3] = 0;
   __syncthreads();
   const int32_t* ni = reinterpret_cast<const int32_t*>(a.nodes + 6 * (size_t)a.stride);
-  int32_t c_nodes = 0, c_cpu = 0, c_mem = 0, c_gpu = 0;
-  const int n_end = min(fq.end, a.tab_lo + a.tab_n);
-  for (int n = a.tab_lo + threadIdx.x; n < n_end; n += blockDim.x) {
-    if (!((a.class_mask[(size_t)fq.cls * a.W + (n >> 6)] >> (n & 63)) & 1ull)) continue;  // static predicate
-    const int e1 = a.hoff[n + 1];
-    int e = a.hoff[n];
-    while (e < e1 && (a.hk[e] & 0x7fffffff) < fq.point) ++e;  // decisions before the evaluation stay applied
-    const int r = n - a.tab_lo;  // the node's row in this table
-    if (a.cap_check && ni[r] - (e1 - e) >= ni[a.stride + r]) continue;  // pod cap then (predicates.go:125-127)
-    double ic = a.nodes[r], im = a.nodes[a.stride + r], ig = a.nodes[2 * (size_t)a.stride + r];
-    for (int x = e; x < e1; ++x)
-      if (!(a.hk[x] & 0x80000000)) {  // the first undone Allocate: Idle before it
-        ic = a.hold[3 * (size_t)x];
-        im = a.hold[3 * (size_t)x + 1];
-        ig = a.hold[3 * (size_t)x + 2];
-        break;
+  int n_end = 0;  // the furthest end of the group's jobs
+  for (int jj = 0; jj < nj; ++jj) n_end = max(n_end, min(a.q[q0 + jj].end, a.tab_lo + a.tab_n));
+  const int last = max(a.tab_lo, n_end - 1);  // a legal node for clamped loads
+  int cnt[kFitJobs][4] = {};
+  for (int base = a.tab_lo; base < n_end; base += kFitBlock) {
+    const int n = base + (int)threadIdx.x;
+    const int nc = min(n, last);
+    const int r = nc - a.tab_lo;
+    const int e0 = a.hoff[nc], e1 = a.hoff[nc + 1], nt = ni[r], mt = ni[a.stride + r];
+    const double ic = a.nodes[r], im = a.nodes[a.stride + r], ig = a.nodes[2 * (size_t)a.stride + r];
+#pragma unroll
+    for (int jj = 0; jj < kFitJobs; ++jj) {
+      if (jj >= nj) break;
+      const FitQuery& fq = a.q[q0 + jj];
+      const int end = min(fq.end, a.tab_lo + a.tab_n);
+      if (__builtin_amdgcn_readfirstlane(base + (int)(threadIdx.x & ~63)) >= end) continue;  // the wave is past it
+      const uint64_t mw = a.class_mask[(size_t)fq.cls * a.W + (nc >> 6)];
+      bool hit = false, bc = false, bm = false, bg = false;
+      if (n < end && ((mw >> (n & 63)) & 1ull)) {  // static predicate
+        int lo = e0, hi = e1;  // decisions before the evaluation stay applied: the first at or after it
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if ((a.hk[mid] & 0x7fffffff) < fq.point) lo = mid + 1;
+          else hi = mid;
+        }
+        double c = ic, m = im, g = ig;
+        const int x = lo < e1 ? a.na[lo] : -1;  // the first undone Allocate: Idle before it
+        if (x >= 0) {
+          c = a.hold[3 * (size_t)x];
+          m = a.hold[3 * (size_t)x + 1];
+          g = a.hold[3 * (size_t)x + 2];
+        }
+        const bool capped = a.cap_check && nt - (e1 - lo) >= mt;  // pod cap then (predicates.go:125-127)
+        const bool chosen = n != fq.win && le(fq.req[0], c, kMinMilliCPU) && le(fq.req[1], m, kMinMemory) &&
+                            le(fq.req[2], g, kMinMilliGPU);
+        if (!capped && !chosen) {  // Resource.FitDelta (resource_info.go:116-129)
+          hit = true;
+          bc = (fq.req[0] > 0 ? c - (fq.req[0] + kMinMilliCPU) : c) < 0;
+          bm = (fq.req[1] > 0 ? m - (fq.req[1] + kMinMemory) : m) < 0;
+          bg = (fq.req[2] > 0 ? g - (fq.req[2] + kMinMilliGPU) : g) < 0;
+        }
       }
-    if (n != fq.win && le(fq.req[0], ic, kMinMilliCPU) && le(fq.req[1], im, kMinMemory) &&
-        le(fq.req[2], ig, kMinMilliGPU))
-      continue;  // would have been chosen
-    // Resource.FitDelta (resource_info.go:116-129)
-    const double dc = fq.req[0] > 0 ? ic - (fq.req[0] + kMinMilliCPU) : ic;
-    const double dm = fq.req[1] > 0 ? im - (fq.req[1] + kMinMemory) : im;
-    const double dg = fq.req[2] > 0 ? ig - (fq.req[2] + kMinMilliGPU) : ig;
-    ++c_nodes;
-    c_cpu += dc < 0;
-    c_mem += dm < 0;
-    c_gpu += dg < 0;
+      cnt[jj][0] += __popcll(__ballot(hit));
+      cnt[jj][1] += __popcll(__ballot(bc));
+      cnt[jj][2] += __popcll(__ballot(bm));
+      cnt[jj][3] += __popcll(__ballot(bg));
+    }
   }
-  if (c_nodes) {
-    atomicAdd(&s_cnt[0], c_nodes);
-    atomicAdd(&s_cnt[1], c_cpu);
-    atomicAdd(&s_cnt[2], c_mem);
-    atomicAdd(&s_cnt[3], c_gpu);
-  }
+  if ((threadIdx.x & 63) == 0)  // (the counts are wave-uniform)
+#pragma unroll
+    for (int jj = 0; jj < kFitJobs; ++jj)
+      if (cnt[jj][0]) {
+        atomicAdd(&s_cnt[jj][0], cnt[jj][0]);
+        atomicAdd(&s_cnt[jj][1], cnt[jj][1]);
+        atomicAdd(&s_cnt[jj][2], cnt[jj][2]);
+        atomicAdd(&s_cnt[jj][3], cnt[jj][3]);
+      }
   __syncthreads();
-  if (threadIdx.x < 4) a.out[4 * (size_t)blockIdx.x + threadIdx.x] = s_cnt[threadIdx.x];
+  if (threadIdx.x < nj * 4) a.out[4 * (size_t)q0 + threadIdx.x] = s_cnt[threadIdx.x >> 2][threadIdx.x & 3];
 }
 
 hipError_t launch_fitdelta(const FitArgs& a, hipStream_t stream) {
   if (a.nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(kbg_fitdelta_kernel, dim3(a.nq), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(kbg_fitdelta_kernel, dim3((a.nq + kFitJobs - 1) / kFitJobs), dim3(kFitBlock), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -2192,6 +2192,8 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   S.pod_terms_in = copy_arr(snap->pod_terms, snap->n_pod_terms);
   S.pod_labels_in = copy_arr(snap->pod_labels, 2 * snap->n_pod_labels);
   S.others_in = copy_arr(snap->others, snap->n_others);
+  S.plugins_in = copy_arr(snap->plugins, snap->n_plugins);
+  S.tier_sizes_in = copy_arr(snap->tier_sizes, snap->n_tiers);
   S.task_live.clear();
   S.task_live.reserve(S.n_tasks + more);
   S.task_live.assign(S.n_tasks, 1);
@@ -3575,8 +3577,8 @@ kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, c
     if (!S.dec_dup[k]) cnt[dec[k].node + 1]++;
   for (int32_t n = 0; n < N; ++n) cnt[n + 1] += cnt[n];
   const int32_t E = cnt[N];
-  // one block: hoff[N+1] | hk[E] | pad | hold[E][3] | queries[Q]; results [Q][4] mapped
-  const size_t o_hk = (size_t)(N + 1) * 4, o_hold = (o_hk + (size_t)E * 4 + 15) / 16 * 16,
+  // one block: hoff[N+1] | hk[E] | na[E] | pad | hold[E][3] | queries[Q]; results [Q][4] mapped
+  const size_t o_hk = (size_t)(N + 1) * 4, o_na = o_hk + (size_t)E * 4, o_hold = (o_na + (size_t)E * 4 + 15) / 16 * 16,
                o_q = o_hold + (size_t)E * 24, bytes = o_q + (size_t)Q * sizeof(kbg::FitQuery),
                out_bytes = (size_t)Q * 16;
   if (bytes > S.fit_cap) {
@@ -3609,6 +3611,14 @@ kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, c
     hold[3 * (size_t)e + 1] = dec_old[k].m;
     hold[3 * (size_t)e + 2] = dec_old[k].g;
   }
+  int32_t* na = (int32_t*)(S.fit_h + o_na);  // each decision's first Allocate at or after it on its node
+  for (int32_t n = 0; n < N; ++n) {
+    int32_t next = -1;
+    for (int32_t e = hoff[n + 1] - 1; e >= hoff[n]; --e) {
+      if (!(hk[e] & (int32_t)0x80000000)) next = e;
+      na[e] = next;
+    }
+  }
   for (int32_t i = 0; i < Q; ++i) {
     const LastEval& le = last[qj[i]];
     const Res& r = S.treq[le.task];
@@ -3619,7 +3629,7 @@ kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, c
   if (!fit_out) return fail(KBG_E_HIP, "hipHostGetDevicePointer of the FitError buffer failed");
   HIP_TRY(hipMemcpyAsync(S.fit_d, S.fit_h, bytes, hipMemcpyHostToDevice, S.stream));
   kbg::FitArgs a{S.d_nodes.idle_cpu, soa_stride(S), S.W, S.d_class_mask, (const int32_t*)S.fit_d,
-                 (const int32_t*)(S.fit_d + o_hk), (const double*)(S.fit_d + o_hold),
+                 (const int32_t*)(S.fit_d + o_hk), (const double*)(S.fit_d + o_hold), (const int32_t*)(S.fit_d + o_na),
                  (const kbg::FitQuery*)(S.fit_d + o_q), Q, S.pred_active ? 1 : 0, fit_out, S.tab_lo, S.tab_n};
   HIP_TRY(kbg::launch_fitdelta(a, S.stream));
   HIP_TRY(hipStreamSynchronize(S.stream));
@@ -7370,6 +7380,90 @@ kbg_status apply_node_set(Session& S, UpdateCtx& U, const kbg_event& e) {
   return KBG_OK;
 }
 
+// Structural events (kbgpu.h KBG_EV_NODE_ADD ... QUEUE_DELETE) on the inputs:
+// what joins is appended (its pod events in the same batch find it), what
+// leaves is marked; restructure() then rebuilds the session from the updated
+// snapshot. update_precheck has validated every field.
+kbg_status apply_structural(Session& S, UpdateCtx& U, const kbg_event& e) {
+  switch (e.kind) {
+    case KBG_EV_NODE_ADD: {  // cache.AddNode of a new name -> NewNodeInfo (event_handlers.go:232-240)
+      kbg_node nd{};
+      const int32_t n = S.n_nodes++;
+      if (const kbg_node_spec* sp = e.node_spec) {
+        nd.name = intern(S, sp->name);
+        nd.has_node = 1;
+        nd.allocatable = nd.idle = e.resource;  // Idle = Allocatable, Releasing empty (node_info.go:44-71)
+        nd.max_task_num = e.max_task_num;
+        nd.unschedulable = e.unschedulable;
+        nd.label_off = (int32_t)(S.labels_in.size() / 2);
+        nd.label_len = sp->n_labels;
+        for (int32_t i = 0; i < 2 * sp->n_labels; ++i) S.labels_in.push_back(intern(S, sp->labels[i]));
+        nd.taint_off = (int32_t)S.taints_in.size();
+        nd.taint_len = sp->n_taints;
+        for (int32_t i = 0; i < sp->n_taints; ++i)
+          S.taints_in.push_back(kbg_taint{intern(S, sp->taints[3 * i]), intern(S, sp->taints[3 * i + 1]),
+                                          intern(S, sp->taints[3 * i + 2])});
+        S.node_of[S.canon[nd.name]] = n;
+        S.nil_name.push_back(-1);
+      } else {  // NewNodeInfo(nil): Name "", known by the NodeName that made it
+        nd.name = empty_str(S);
+        const int32_t nm = S.canon[intern(S, e.node_name)];
+        S.nil_name.push_back(nm);
+        S.pod_only_of[nm] = n;
+      }
+      nd.port_off = (int32_t)S.ports_in.size();
+      S.nodes_in.push_back(nd);
+      S.node_task_order.emplace_back();
+      S.node_key_order.emplace_back();
+      S.node_dead.push_back(0);
+      U.seen.push_back(0);
+      return KBG_OK;
+    }
+    case KBG_EV_NODE_DELETE: {  // cache.DeleteNode (event_handlers.go:262-268)
+      const int32_t n = e.node;
+      S.node_dead[n] = 1;
+      const kbg_node& nd = S.nodes_in[n];
+      if (nd.has_node) {
+        auto it = S.node_of.find(S.canon[nd.name]);
+        if (it != S.node_of.end() && it->second == n) S.node_of.erase(it);
+      } else if (S.nil_name[n] >= 0) {
+        auto it = S.pod_only_of.find(S.nil_name[n]);
+        if (it != S.pod_only_of.end() && it->second == n) S.pod_only_of.erase(it);
+      }
+      return KBG_OK;
+    }
+    case KBG_EV_JOB_ADD: {  // cache.AddPodGroup of a new JobID -> NewJobInfo + SetPodGroup (event_handlers.go:344-358)
+      kbg_job j{};
+      j.uid = intern(S, e.name);
+      j.queue = e.queue;
+      j.min_available = e.min_available;
+      j.priority = e.priority;
+      j.creation_ns = e.creation_ns;
+      S.jobs_in.push_back(j);
+      S.job_task_order.emplace_back();
+      S.job_dead.push_back(0);
+      S.job_to_others.push_back(0);
+      S.n_jobs++;
+      return KBG_OK;
+    }
+    case KBG_EV_JOB_DELETE:  // UnsetPodGroup: its Running tasks are Others from now on (cache.go:570-582)
+      S.job_dead[e.job] = 1;
+      S.job_to_others[e.job] = 1;
+      return KBG_OK;
+    case KBG_EV_QUEUE_ADD:  // cache.AddQueue (event_handlers.go:635-640)
+      S.queues_in.push_back(kbg_queue{intern(S, e.name), e.weight});
+      S.queue_dead.push_back(0);
+      S.n_queues++;
+      return KBG_OK;
+    case KBG_EV_QUEUE_DELETE:  // its jobs are not in the snapshot any more (cache.go:584-588)
+      S.queue_dead[e.queue] = 1;
+      for (int32_t j = 0; j < S.n_jobs; ++j)
+        if (S.jobs_in[j].queue == e.queue) S.job_dead[j] = 1;
+      return KBG_OK;
+  }
+  return fail(KBG_E_INVALID, "event kind");
+}
+
 // key_hash: StrIndex::hash of a POD_ADD's pod key when the caller computed it
 // ahead (session_update's prefetch), else null
 kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e, const uint64_t* key_hash) {
@@ -7436,6 +7530,13 @@ kbg_status apply_event(Session& S, UpdateCtx& U, const kbg_event& e, const uint6
     }
     case KBG_EV_NODE_SET:
       return apply_node_set(S, U, e);
+    case KBG_EV_NODE_ADD:
+    case KBG_EV_NODE_DELETE:
+    case KBG_EV_JOB_ADD:
+    case KBG_EV_JOB_DELETE:
+    case KBG_EV_QUEUE_ADD:
+    case KBG_EV_QUEUE_DELETE:
+      return apply_structural(S, U, e);
     case KBG_EV_NODE_UPDATE: {
       if (e.node < 0 || e.node >= S.n_nodes) return fail(KBG_E_INVALID, "event node index");
       kbg_node& nd = S.nodes_in[e.node];
@@ -7471,9 +7572,16 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
   auto status_ok = [](int32_t st) { return st > 0 && st <= KBG_UNKNOWN && !(st & (st - 1)); };
   bool port_specs = false;
   for (const kbg_spec& sp : S.specs_in) port_specs |= sp.has_host_ports != 0;
-  const bool holders = port_specs || !S.outsiders.empty();  // else no removal can be refused
+  bool structural = false;
   int32_t adds = 0;
-  for (int32_t i = 0; i < n; ++i) adds += ev[i].kind == KBG_EV_POD_ADD;
+  for (int32_t i = 0; i < n; ++i) {
+    adds += ev[i].kind == KBG_EV_POD_ADD;
+    structural |= ev[i].kind >= KBG_EV_NODE_ADD;
+  }
+  if (structural && S.comm)
+    return fail(KBG_E_UNSUPPORTED, "structural events on a session sharded over a communicator: re-open it on every rank");
+  // else no removal can be refused (a structural batch walks every pod's node: pods on deleted nodes)
+  const bool holders = port_specs || !S.outsiders.empty() || structural;
   const int32_t T0 = S.n_tasks;
   std::vector<uint8_t> dead(S.n_tasks + adds, 0);
   for (int32_t t = 0; t < T0; ++t) dead[t] = !S.task_live[t];
@@ -7491,6 +7599,7 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
     const int64_t hk = ((int64_t)nd << 32) | (uint32_t)key;
     auto it = hold.find(hk);
     if (it != hold.end()) return it->second;
+    if (nd >= S.n_nodes) return -1;  // a node this batch added: no pod yet
     auto ot = S.outsiders.find(hk);
     if (ot != S.outsiders.end()) return ot->second.status ? -2 : -3;
     for (int32_t u : S.node_task_order[nd])
@@ -7498,13 +7607,68 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
     return -1;
   };
   int32_t T = T0;
+  // structural events: the counts as the batch grows them, what it removed,
+  // the names it gave (-1: removed by the batch)
+  int32_t N = S.n_nodes, J = S.n_jobs, Q = S.n_queues;
+  std::vector<uint8_t> ndead, jdead, qdead;
+  std::vector<int32_t> jq, add_job;  // queues of the jobs this batch added; jobs of the tasks it added
+  std::unordered_map<std::string, int32_t> bnodes, bjobs, bqueues;
+  std::unordered_map<int32_t, int32_t> job_of_uid, queue_of_uid;  // canonical JobID / QueueID -> index
+  if (structural) {
+    ndead.assign(N, 0);
+    jdead.assign(J, 0);
+    qdead.assign(Q, 0);
+    for (int32_t j = 0; j < J; ++j) job_of_uid.emplace(S.canon[S.jobs_in[j].uid], j);
+    for (int32_t q = 0; q < Q; ++q) queue_of_uid.emplace(S.canon[S.queues_in[q].uid], q);
+  }
+  auto task_job = [&](int32_t t) { return t < T0 ? S.tasks_in[t].job : add_job[t - T0]; };
+  auto job_queue_of = [&](int32_t j) { return j < S.n_jobs ? S.jobs_in[j].queue : jq[j - S.n_jobs]; };
+  // a live name among the session's (or the batch's) nodes, jobs or queues
+  auto node_live = [&](const std::string& nm) {
+    if (auto b = bnodes.find(nm); b != bnodes.end()) return b->second >= 0;
+    const int32_t id = S.canon_of.find(S.strs, nm.c_str());
+    if (id < 0) return false;
+    auto a = S.node_of.find(S.canon[id]);
+    if (a != S.node_of.end() && !ndead[a->second]) return true;
+    auto b = S.pod_only_of.find(S.canon[id]);
+    return b != S.pod_only_of.end() && !ndead[b->second];
+  };
+  auto uid_live = [&](const std::unordered_map<std::string, int32_t>& batch,
+                      const std::unordered_map<int32_t, int32_t>& have, const std::vector<uint8_t>& gone,
+                      const std::string& nm) {
+    if (auto b = batch.find(nm); b != batch.end()) return b->second >= 0;
+    const int32_t id = S.canon_of.find(S.strs, nm.c_str());
+    if (id < 0) return false;
+    auto a = have.find(S.canon[id]);
+    return a != have.end() && !gone[a->second];
+  };
+  auto node_name_of = [&](int32_t nd) -> std::string {  // "" : a pod-only node without a known name
+    if (nd >= S.n_nodes) {
+      for (const auto& [nm, i] : bnodes)
+        if (i == nd) return nm;
+      return "";
+    }
+    if (S.nodes_in[nd].has_node) return S.strs[S.nodes_in[nd].name];
+    return S.nil_name[nd] >= 0 ? S.strs[S.nil_name[nd]] : "";
+  };
+  auto spec_ok = [](const kbg_node_spec* sp) {
+    if (!sp || !sp->name || sp->n_labels < 0 || sp->n_taints < 0 || (sp->n_labels && !sp->labels) ||
+        (sp->n_taints && !sp->taints))
+      return false;
+    for (int32_t k = 0; k < 2 * sp->n_labels; ++k)
+      if (!sp->labels[k]) return false;
+    for (int32_t k = 0; k < 3 * sp->n_taints; ++k)
+      if (!sp->taints[k]) return false;
+    return true;
+  };
   std::vector<uint8_t> node_set(S.n_nodes, 0);  // nodes an earlier NODE_SET of the batch gave a Node
   std::unordered_map<int32_t, std::string> set_names;  // ... and the name it gave
   // a pod event's node: a node with a Node (now or from an earlier NODE_SET of
   // the batch), or a pod-only node whose NodeName the session knows
   auto nil_named = [&](const kbg_event& e) {
     const int32_t nd = e.node;
-    return nd < 0 || S.nodes_in[nd].has_node || node_set[nd] || S.nil_name[nd] >= 0 || (e.node_name && e.node_name[0]);
+    return nd < 0 || nd >= S.n_nodes || S.nodes_in[nd].has_node || node_set[nd] || S.nil_name[nd] >= 0 ||
+           (e.node_name && e.node_name[0]);
   };
   for (int32_t i = 0; i < n; ++i) {
     const kbg_event& e = ev[i];
@@ -7513,8 +7677,14 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
       case KBG_EV_POD_DELETE: {
         const int32_t t = e.task;
         if (t < 0 || t >= T || dead[t]) return fail(KBG_E_INVALID, "event task index");
-        if (e.kind == KBG_EV_POD_UPDATE && (!status_ok(e.status) || e.node < -1 || e.node >= S.n_nodes))
+        if (e.kind == KBG_EV_POD_UPDATE && (!status_ok(e.status) || e.node < -1 || e.node >= N))
           return fail(KBG_E_INVALID, "event status / node");
+        if (structural) {
+          const int32_t on = task_now(t).node;
+          if (jdead[task_job(t)] || (on >= 0 && ndead[on]) || (e.kind == KBG_EV_POD_UPDATE && e.node >= 0 && ndead[e.node]))
+            return fail(KBG_E_UNSUPPORTED, "a pod event after its job or its node left the session in the same "
+                                           "batch: send it in the next update");
+        }
         if (e.kind == KBG_EV_POD_UPDATE && !nil_named(e))
           return fail(KBG_E_UNSUPPORTED, "a pod event naming a node the cache knows only from pods outside the "
                                          "session jobs (the NodeName is unknown to the session): re-open");
@@ -7546,9 +7716,15 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
         break;
       }
       case KBG_EV_POD_ADD: {
-        if (e.job < 0 || e.job >= S.n_jobs || e.spec < -1 || e.spec >= (int32_t)S.specs_in.size() ||
-            !status_ok(e.status) || e.node < -1 || e.node >= S.n_nodes || !e.uid || !e.pod_key)
+        if (e.job < 0 || e.job >= J || e.spec < -1 || e.spec >= (int32_t)S.specs_in.size() ||
+            !status_ok(e.status) || e.node < -1 || e.node >= N || !e.uid || !e.pod_key)
           return fail(KBG_E_INVALID, "POD_ADD event");
+        if (structural) {
+          if (jdead[e.job]) return fail(KBG_E_INVALID, "POD_ADD into a job that left the session in the same batch");
+          if (e.node >= 0 && ndead[e.node])
+            return fail(KBG_E_UNSUPPORTED, "POD_ADD onto a node that left the session in the same batch");
+          add_job.push_back(e.job);
+        }
         if (!nil_named(e))
           return fail(KBG_E_UNSUPPORTED, "a pod event naming a node the cache knows only from pods outside the "
                                          "session jobs (the NodeName is unknown to the session): re-open");
@@ -7564,12 +7740,16 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
         }
         const Now c{e.node, e.status, key, e.spec};
         now[t] = c;
+        if (c.node >= 0 && e.job >= S.n_jobs && holder(c.node, c.key) <= -2)
+          return fail(KBG_E_UNSUPPORTED, "POD_ADD of a pod of a job new to the session whose key a pod outside the "
+                                         "session jobs holds on the node (the pod predates its PodGroup): re-open");
         if (c.node >= 0 && !terminated(c.status) && holder(c.node, c.key) == -1)
           hold[((int64_t)c.node << 32) | (uint32_t)c.key] = t;
         break;
       }
       case KBG_EV_NODE_UPDATE:
         if (e.node < 0 || e.node >= S.n_nodes) return fail(KBG_E_INVALID, "event node index");
+        if (structural && ndead[e.node]) return fail(KBG_E_INVALID, "NODE_UPDATE of a node deleted in the batch");
         if (!S.nodes_in[e.node].has_node && !node_set[e.node])
           return fail(KBG_E_UNSUPPORTED, "KBG_EV_NODE_UPDATE of a node the cache only knows from a pod: send "
                                          "KBG_EV_NODE_SET (its name, labels and taints)");
@@ -7577,9 +7757,17 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
       case KBG_EV_NODE_SET: {
         // every input apply_node_set rejects, so the apply step can only fail as the reference panics
         const kbg_node_spec* sp = e.node_spec;
-        if (e.node < 0 || e.node >= S.n_nodes || !sp || !sp->name || sp->n_labels < 0 || sp->n_taints < 0 ||
-            (sp->n_labels && !sp->labels) || (sp->n_taints && !sp->taints))
+        if (e.node < 0 || e.node >= N || !sp || !sp->name || sp->n_labels < 0 || sp->n_taints < 0 ||
+            (sp->n_labels && !sp->labels) || (sp->n_taints && !sp->taints) || (structural && ndead[e.node]))
           return fail(KBG_E_INVALID, "NODE_SET event");
+        if (e.node >= S.n_nodes) {  // the Node of a node this batch added without one (a pod's NodeName made it)
+          if (!spec_ok(sp)) return fail(KBG_E_INVALID, "NODE_SET event");
+          auto named = set_names.find(e.node);
+          if (named != set_names.end() && named->second != sp->name)
+            return fail(KBG_E_INVALID, "NODE_SET: the node's name differs");
+          set_names.emplace(e.node, sp->name);
+          break;
+        }
         for (int32_t k = 0; k < 2 * sp->n_labels; ++k)
           if (!sp->labels[k]) return fail(KBG_E_INVALID, "NODE_SET: null label string");
         for (int32_t k = 0; k < 3 * sp->n_taints; ++k)
@@ -7601,6 +7789,61 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
         node_set[e.node] = 1;
         break;
       }
+      case KBG_EV_NODE_ADD: {
+        // with a Node (NewNodeInfo(node)), or without one: the node a pod's NodeName makes (NewNodeInfo(nil))
+        if ((e.node_spec && !spec_ok(e.node_spec)) || (!e.node_spec && !(e.node_name && e.node_name[0])))
+          return fail(KBG_E_INVALID, "NODE_ADD event");
+        const std::string nm = e.node_spec ? e.node_spec->name : e.node_name;
+        if (nm.empty() || node_live(nm))
+          return fail(KBG_E_INVALID, "NODE_ADD of a node name the session holds (its Node: KBG_EV_NODE_SET)");
+        bnodes[nm] = N++;
+        ndead.push_back(0);
+        break;
+      }
+      case KBG_EV_NODE_DELETE: {
+        if (e.node < 0 || e.node >= N || ndead[e.node]) return fail(KBG_E_INVALID, "NODE_DELETE event node");
+        const std::string nm = node_name_of(e.node);
+        if (!nm.empty()) bnodes[nm] = -1;
+        ndead[e.node] = 1;
+        break;
+      }
+      case KBG_EV_JOB_ADD: {
+        if (!e.name || !e.name[0] || e.queue < 0 || e.queue >= Q || qdead[e.queue])
+          return fail(KBG_E_INVALID, "JOB_ADD event (name, queue)");
+        if (uid_live(bjobs, job_of_uid, jdead, e.name))
+          return fail(KBG_E_INVALID, "JOB_ADD of a JobID the session holds");
+        bjobs[e.name] = J++;
+        jdead.push_back(0);
+        jq.push_back(e.queue);
+        break;
+      }
+      case KBG_EV_JOB_DELETE:
+        if (e.job < 0 || e.job >= J || jdead[e.job]) return fail(KBG_E_INVALID, "JOB_DELETE event job");
+        jdead[e.job] = 1;
+        for (auto& [nm, j] : bjobs)
+          if (j == e.job) j = -1;
+        break;
+      case KBG_EV_QUEUE_ADD: {
+        if (!e.name || !e.name[0]) return fail(KBG_E_INVALID, "QUEUE_ADD event name");
+        if (uid_live(bqueues, queue_of_uid, qdead, e.name))
+          return fail(KBG_E_INVALID, "QUEUE_ADD of a queue the session holds");
+        bqueues[e.name] = Q++;
+        qdead.push_back(0);
+        break;
+      }
+      case KBG_EV_QUEUE_DELETE: {
+        if (e.queue < 0 || e.queue >= Q || qdead[e.queue]) return fail(KBG_E_INVALID, "QUEUE_DELETE event queue");
+        qdead[e.queue] = 1;
+        for (auto& [nm, q] : bqueues)
+          if (q == e.queue) q = -1;
+        for (int32_t j = 0; j < J; ++j)  // its jobs leave ssn.Jobs (cache.go:584-588)
+          if (!jdead[j] && job_queue_of(j) == e.queue) {
+            jdead[j] = 1;
+            for (auto& [nm, k] : bjobs)
+              if (k == j) k = -1;
+          }
+        break;
+      }
       default:
         return fail(KBG_E_INVALID, "event kind");
     }
@@ -7608,8 +7851,176 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
   return KBG_OK;
 }
 
+// After a batch with structural events: the session's updated snapshot as
+// cache.Snapshot() would marshal it (cache.go:549-597) — live nodes, queues
+// and jobs in their order, the new ones last; each job's tasks in JobInfo.Tasks
+// order; the pods of jobs that left stay on their nodes as pods outside the
+// session jobs (with their node copies when every pod on a live node has one),
+// the Running tasks of a job whose PodGroup was deleted join Others — opened
+// as a new session that replaces this one; renum[] maps the old indices.
+kbg_status restructure(Session& S) {
+  const int32_t N = S.n_nodes, J = S.n_jobs, Q = S.n_queues, T = S.n_tasks;
+  auto gone = [](const std::vector<uint8_t>& v, int32_t i) { return (size_t)i < v.size() && v[i] != 0; };
+  std::vector<int32_t> rq(Q, -1), rj(J, -1), rn(N, -1), rt(T, -1);
+  std::vector<kbg_queue> queues;
+  for (int32_t q = 0; q < Q; ++q)
+    if (!gone(S.queue_dead, q)) {
+      rq[q] = (int32_t)queues.size();
+      queues.push_back(S.queues_in[q]);
+    }
+  std::vector<kbg_job> jobs;
+  std::vector<kbg_task> tasks;
+  std::vector<kbg_resource> others = S.others_in;
+  for (int32_t j = 0; j < J; ++j) {
+    if (gone(S.job_dead, j)) {
+      if (gone(S.job_to_others, j))  // PodGroup == nil: its Running tasks are Others
+        for (const int32_t t : S.job_task_order[j])
+          if (S.task_live[t] && S.tasks_in[t].status == KBG_RUNNING) others.push_back(S.tasks_in[t].resreq);
+      continue;
+    }
+    kbg_job jb = S.jobs_in[j];
+    jb.queue = rq[jb.queue];
+    if (jb.queue < 0) return fail(KBG_E_INVALID, "internal: a live job of a deleted queue");
+    rj[j] = (int32_t)jobs.size();
+    jobs.push_back(jb);
+    for (const int32_t t : S.job_task_order[j]) {
+      if (!S.task_live[t]) continue;
+      rt[t] = (int32_t)tasks.size();
+      kbg_task k = S.tasks_in[t];
+      k.job = rj[j];
+      tasks.push_back(k);
+    }
+  }
+  // the pod behind each key of a live node: a task (of a session job or of one
+  // that left) or a pod outside the session jobs
+  auto holder_task = [&](int32_t n, int32_t key) -> int32_t {
+    for (const int32_t t : S.node_task_order[n])
+      if (S.canon[S.tasks_in[t].pod_key] == key) return t;
+    return -1;
+  };
+  bool copies = true;
+  for (int32_t n = 0; n < N && copies; ++n) {
+    if (gone(S.node_dead, n) || S.node_key_order[n].size() == S.node_task_order[n].size()) continue;
+    for (const int32_t key : S.node_key_order[n]) {
+      if (holder_task(n, key) >= 0) continue;
+      auto it = S.outsiders.find(((int64_t)n << 32) | (uint32_t)key);
+      if (it == S.outsiders.end() || it->second.status == 0) {
+        copies = false;
+        break;
+      }
+    }
+  }
+  std::vector<kbg_node> nodes;
+  std::vector<int32_t> node_tasks, node_keys;
+  std::vector<kbg_node_pod> node_pods;
+  std::vector<kbg_host_port> ports = S.ports_in;  // the specs' ports keep their offsets
+  for (int32_t n = 0; n < N; ++n) {
+    if (gone(S.node_dead, n)) continue;
+    kbg_node nd = S.nodes_in[n];
+    nd.task_off = (int32_t)node_tasks.size();
+    for (const int32_t t : S.node_task_order[n])
+      if (rt[t] >= 0) node_tasks.push_back(rt[t]);
+    nd.task_len = (int32_t)node_tasks.size() - nd.task_off;
+    nd.key_off = (int32_t)node_keys.size();
+    node_keys.insert(node_keys.end(), S.node_key_order[n].begin(), S.node_key_order[n].end());
+    nd.key_len = (int32_t)node_keys.size() - nd.key_off;
+    if (nd.key_len != nd.num_tasks) return fail(KBG_E_INVALID, "internal: node pod keys != num_tasks");
+    if (copies) {  // NodeInfo.Tasks order: each pod's ports after the one before (kbg_node_pod)
+      nd.port_off = (int32_t)ports.size();
+      for (const int32_t key : S.node_key_order[n]) {
+        const int32_t u = holder_task(n, key);
+        const size_t p0 = ports.size();
+        if (u >= 0) {
+          const int32_t sp = S.tasks_in[u].spec;
+          if (sp >= 0)
+            for (int32_t i = 0; i < S.specs_in[sp].port_len; ++i)
+              if (S.ports_in[S.specs_in[sp].port_off + i].host_port > 0)
+                ports.push_back(S.ports_in[S.specs_in[sp].port_off + i]);
+          node_pods.push_back(kbg_node_pod{S.tasks_in[u].resreq, S.tasks_in[u].status, (int32_t)(ports.size() - p0)});
+        } else {
+          const Session::Outsider& o = S.outsiders.at(((int64_t)n << 32) | (uint32_t)key);
+          ports.insert(ports.end(), o.ports.begin(), o.ports.end());
+          node_pods.push_back(kbg_node_pod{o.req, o.status, (int32_t)o.ports.size()});
+        }
+      }
+      nd.port_len = (int32_t)ports.size() - nd.port_off;
+    }
+    rn[n] = (int32_t)nodes.size();
+    nodes.push_back(nd);
+  }
+  std::vector<const char*> strs(S.strs.size());
+  for (size_t i = 0; i < strs.size(); ++i) strs[i] = S.strs[i].c_str();
+  kbg_snapshot sn{};
+  sn.strings = strs.data();
+  sn.n_strings = (int32_t)strs.size();
+  sn.nodes = nodes.data(), sn.n_nodes = (int32_t)nodes.size();
+  sn.jobs = jobs.data(), sn.n_jobs = (int32_t)jobs.size();
+  sn.queues = queues.data(), sn.n_queues = (int32_t)queues.size();
+  sn.tasks = tasks.data(), sn.n_tasks = (int32_t)tasks.size();
+  sn.others = others.data(), sn.n_others = (int32_t)others.size();
+  sn.specs = S.specs_in.data(), sn.n_specs = (int32_t)S.specs_in.size();
+  sn.terms = S.terms_in.data(), sn.n_terms = (int32_t)S.terms_in.size();
+  sn.reqs = S.reqs_in.data(), sn.n_reqs = (int32_t)S.reqs_in.size();
+  sn.values = S.values_in.data(), sn.n_values = (int32_t)S.values_in.size();
+  sn.tolerations = S.tols_in.data(), sn.n_tolerations = (int32_t)S.tols_in.size();
+  sn.labels = S.labels_in.data(), sn.n_labels = (int32_t)(S.labels_in.size() / 2);
+  sn.taints = S.taints_in.data(), sn.n_taints = (int32_t)S.taints_in.size();
+  sn.selectors = S.selectors_in.data(), sn.n_selectors = (int32_t)(S.selectors_in.size() / 2);
+  sn.plugins = S.plugins_in.data(), sn.n_plugins = (int32_t)S.plugins_in.size();
+  sn.tier_sizes = S.tier_sizes_in.data(), sn.n_tiers = (int32_t)S.tier_sizes_in.size();
+  sn.ports = ports.data(), sn.n_ports = (int32_t)ports.size();
+  sn.node_tasks = node_tasks.data(), sn.n_node_tasks = (int32_t)node_tasks.size();
+  sn.pod_terms = S.pod_terms_in.data(), sn.n_pod_terms = (int32_t)S.pod_terms_in.size();
+  sn.pod_labels = S.pod_labels_in.data(), sn.n_pod_labels = (int32_t)(S.pod_labels_in.size() / 2);
+  sn.node_pod_keys = node_keys.data(), sn.n_node_pod_keys = (int32_t)node_keys.size();
+  sn.node_pods = copies ? node_pods.data() : nullptr;
+  sn.n_node_pods = copies ? (int32_t)node_pods.size() : 0;
+  kbg_options o = S.opts;
+  o.device = S.device;
+  std::unique_ptr<Session> R(new Session());
+  kbg_status st = open_session(*R, &sn, &o, nullptr);
+  if (st != KBG_OK) {
+    free_device(*R);
+    return st;
+  }
+  // a node the cache knows only from pods keeps the NodeName that made it even
+  // when no session task carries it any more (the snapshot has no field for
+  // it: its Name is ""): pod events naming it find it (sc.Nodes[NodeName])
+  std::unordered_map<int32_t, int32_t> named;
+  for (int32_t n = 0; n < N; ++n) {
+    const int32_t m = rn[n];
+    if (m < 0 || S.nodes_in[n].has_node || S.nil_name[n] < 0 || R->nil_name[m] >= 0) continue;
+    const int32_t nm = R->canon[S.nil_name[n]];
+    R->nil_name[m] = nm;
+    R->pod_only_of.emplace(nm, m);
+    named.emplace(nm, m);
+  }
+  if (!named.empty())
+    for (int32_t t = 0; t < R->n_tasks; ++t)
+      if (R->task_cnode[t] < 0)
+        if (auto it = named.find(R->canon[R->tasks_in[t].node_name]); it != named.end()) R->task_cnode[t] = it->second;
+  R->updates = S.updates;
+  R->rebuilds = S.rebuilds + 1;
+  free_device(S);
+  S = std::move(*R);
+  S.renum[KBG_RENUM_TASKS] = std::move(rt);
+  S.renum[KBG_RENUM_NODES] = std::move(rn);
+  S.renum[KBG_RENUM_JOBS] = std::move(rj);
+  S.renum[KBG_RENUM_QUEUES] = std::move(rq);
+  return KBG_OK;
+}
+
 kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
   const auto t0 = std::chrono::steady_clock::now();
+  for (auto& r : S.renum) r.clear();
+  bool structural = false;
+  for (int32_t i = 0; i < n; ++i) structural |= ev[i].kind >= KBG_EV_NODE_ADD;
+  if (structural) {
+    S.node_dead.assign(S.n_nodes, 0);
+    S.job_dead.assign(S.n_jobs, 0);
+    S.job_to_others.assign(S.n_jobs, 0);
+    S.queue_dead.assign(S.n_queues, 0);
+  }
   if (n < 0 || (n > 0 && !ev)) return fail(KBG_E_INVALID, "events");
   // the cycle state goes back to "just opened"
   S.allocated = S.backfilled = S.reclaimed = S.preempted = S.cycle_started = false;
@@ -7718,6 +8129,15 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
       if (kn[k]) fprintf(stderr, "[kbg update] event kind %d: %llu, %.0f cycles each\n", k, (unsigned long long)kn[k],
                          (double)kc[k] / kn[k]);
   phase("events");
+  if (structural) {  // the sets of nodes, jobs or queues changed: the session is rebuilt from its snapshot
+    if (kbg_status st = restructure(S); st != KBG_OK) return st;
+    phase("restructure");
+    S.updates++;
+    S.update_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    S.stats.update_ms = S.update_ms;
+    S.stats.update_rebuilds = S.rebuilds;
+    return KBG_OK;
+  }
   S.vt_stale = true;
   S.vc.valid = false;
   const bool had_masks = S.has_ports || S.has_aff;
@@ -7984,6 +8404,18 @@ kbg_status kbg_session_update(kbg_session* s, const kbg_event* events, int32_t n
   }
   if (st != KBG_OK) S.broken = g_err;  // events were applied part-way
   return st;
+}
+
+kbg_status kbg_session_renumbering(kbg_session* s, int32_t kind, int32_t* out, int32_t cap, int32_t* n_out) {
+  if (kbg_status st = usable(s); st != KBG_OK) return st;
+  if (kind < KBG_RENUM_TASKS || kind > KBG_RENUM_QUEUES) return fail(KBG_E_INVALID, "renumbering kind");
+  const std::vector<int32_t>& r = s->s.renum[kind];
+  if (n_out) *n_out = (int32_t)r.size();
+  if (!out && cap == 0) return KBG_OK;  // size query
+  if ((int32_t)r.size() > cap || (!out && !r.empty()))
+    return fail(KBG_E_CAPACITY, "renumbering buffer too small: need " + std::to_string(r.size()));
+  if (!r.empty()) std::memcpy(out, r.data(), r.size() * sizeof(int32_t));
+  return KBG_OK;
 }
 
 kbg_status kbg_select(kbg_session* s, const int32_t* tasks, int32_t n, int32_t stop_at_first_success, int32_t* out_node,

@@ -529,6 +529,15 @@ struct Session {
   std::unordered_map<int64_t, Outsider> outsiders;
   std::unordered_set<int64_t> outsider_gone;          // removed by a statement discard this cycle
   std::string broken;                                 // non-empty: an update failed part-way, re-open
+  // structural events (KBG_EV_NODE_ADD ... QUEUE_DELETE): what left during the
+  // update (dropped when the session is rebuilt from its updated snapshot),
+  // and the old -> new maps of the last update that rebuilt (kbgpu.h
+  // kbg_session_renumbering; empty: nothing renumbered)
+  bool structural = false;
+  std::vector<uint8_t> node_dead, job_dead, queue_dead, job_to_others;
+  std::vector<int32_t> renum[4];
+  std::vector<kbg_plugin_option> plugins_in;          // the snapshot's tier entries, for the rebuild
+  std::vector<int32_t> tier_sizes_in;
   bool task_ranks_stale = false;                      // tasks were added: re-rank their jobs' UIDs
   std::vector<int32_t> rank_dirty_jobs;
   std::vector<int32_t> spec_class;                    // per spec: its static class (-1: none compiled)

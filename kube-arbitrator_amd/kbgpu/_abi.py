@@ -184,6 +184,13 @@ EV_POD_DELETE = 2
 EV_POD_ADD = 3
 EV_NODE_UPDATE = 4
 EV_NODE_SET = 5
+EV_NODE_ADD = 6
+EV_NODE_DELETE = 7
+EV_JOB_ADD = 8
+EV_JOB_DELETE = 9
+EV_QUEUE_ADD = 10
+EV_QUEUE_DELETE = 11
+RENUM_TASKS, RENUM_NODES, RENUM_JOBS, RENUM_QUEUES = 0, 1, 2, 3
 
 
 class kbg_node_spec(ctypes.Structure):
@@ -195,7 +202,9 @@ class kbg_event(ctypes.Structure):
     _fields_ = [("kind", i32), ("task", i32), ("status", i32), ("node", i32), ("job", i32), ("spec", i32),
                 ("priority", i32), ("max_task_num", i32), ("resource", kbg_resource), ("unschedulable", i32),
                 ("reserved", i32), ("uid", ctypes.c_char_p), ("pod_key", ctypes.c_char_p),
-                ("node_spec", ctypes.POINTER(kbg_node_spec)), ("node_name", ctypes.c_char_p)]
+                ("node_spec", ctypes.POINTER(kbg_node_spec)), ("node_name", ctypes.c_char_p),
+                ("name", ctypes.c_char_p), ("creation_ns", ctypes.c_int64), ("queue", i32), ("min_available", i32),
+                ("weight", i32), ("reserved2", i32)]
 
 
 class kbg_eviction(ctypes.Structure):
@@ -226,6 +235,7 @@ SIGNATURES = {
     "kbg_decision_actions_get": (i32, [ctypes.c_void_p, P(i32), i32, P(i32)]),
     "kbg_session_reset": (i32, [ctypes.c_void_p]),
     "kbg_session_update": (i32, [ctypes.c_void_p, P(kbg_event), i32]),
+    "kbg_session_renumbering": (i32, [ctypes.c_void_p, i32, P(i32), i32, P(i32)]),
     "kbg_select": (i32, [ctypes.c_void_p, P(i32), i32, i32, P(i32), P(i32), P(i32)]),
     "kbg_apply": (i32, [ctypes.c_void_p, i32, P(kbg_resource), i32]),
     "kbg_job_state_get": (i32, [ctypes.c_void_p, i32, P(kbg_job_state)]),

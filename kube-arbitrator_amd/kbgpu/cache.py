@@ -98,6 +98,17 @@ class SchedulerCache:
         else:
             self.nodes[node["name"]] = NodeInfo(node)
 
+    def delete_node(self, node):  # :262-268 (its pods stay in their jobs, NodeName unchanged)
+        self.nodes.pop(node["name"], None)
+
+    def delete_pod_group(self, pg):  # :361-381: UnsetPodGroup; the job stays until it has no pods
+        job = self.jobs.get(f"{pg.get('namespace', '')}/{pg['name']}")
+        if job is not None:
+            job.pod_group = None
+
+    def delete_queue(self, q):  # :650-654
+        self.queues.pop(q["name"], None)
+
     def add_pod_group(self, pg):  # :344-358
         jid = f"{pg.get('namespace', '')}/{pg['name']}"
         if jid not in self.jobs:

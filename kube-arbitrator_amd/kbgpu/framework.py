@@ -148,79 +148,204 @@ class Session:
         """kbg_session_update: cache events since the session's snapshot,
         applied to the resident session (include/kbgpu.h). `changes` is a list
         of ("pod_update", pod) | ("pod_delete", pod) | ("pod_add", pod) |
-        ("node_update", node) in event order, pods and nodes as the informer
-        delivers them. New pods must use a pod spec the session already has.
-        The host-side objects (jobs / nodes of this wrapper) are not replayed:
-        read results through the C ABI (decisions, job / queue / node state)."""
-        from .api import NodeInfo, TaskInfo, pod_key
-        tidx = {t.uid: i for i, t in enumerate(self.flat.task_objs)}
-        nidx = {n: i for i, n in enumerate(self.flat.node_names) if n}
+        ("node_add", node) | ("node_update", node) | ("node_delete", node) |
+        ("pod_group_add", pg) | ("pod_group_delete", pg) | ("queue_add", q) |
+        ("queue_delete", q) in event order, objects as the informer delivers
+        them (event_handlers.go). New pods must use a pod spec the session
+        already has. Structural changes (a node, PodGroup or queue joins or
+        leaves; a pod naming a node the cache does not know, which makes a
+        NodeInfo(nil), event_handlers.go:49-53) renumber the session: the
+        wrapper's task, node, job and queue lists follow the library's
+        renumbering (kbg_session_renumbering). The host-side objects are not
+        replayed: read results through the C ABI (decisions, job / queue /
+        node state)."""
+        from .api import JobInfo, NodeInfo, QueueInfo, TaskInfo, pod_key
+        L = _abi.lib()
+        flat = self.flat
+        tidx = {t.uid: i for i, t in enumerate(flat.task_objs) if t is not None}
+        nidx = {n: i for i, n in enumerate(flat.node_names) if n}
+        pod_only = dict(flat.pod_only_names)  # NodeName -> index of a node the cache knows only from pods
+        jidx = dict(flat.job_index)
+        qidx = dict(flat.queue_index)
+        n_nodes, n_jobs, n_queues = len(flat.node_names), len(self.jobs), len(self.queues)
+        new_nodes, new_jobs, new_queues = {}, {}, {}  # new index -> NodeInfo / JobInfo / QueueInfo
+        # at most two events per change: a pod naming a node new to the cache makes it first
+        evs = (_abi.kbg_event * max(1, 2 * len(changes)))()
+        n_ev = 0
+        keep = []
+        objs = {}  # task index -> its TaskInfo after the events (applied once the library accepts them)
+        n_objs = len(flat.task_objs)
+        renamed = {}  # pod-only node index -> the name its Node gave it
+
+        def ev():
+            nonlocal n_ev
+            n_ev += 1
+            return evs[n_ev - 1]
+
+        def job_of(j):
+            return self.jobs[j] if j < len(self.jobs) else new_jobs[j]
+
+        def node_spec(e, obj):
+            ni = NodeInfo(obj)
+            e.resource = _abi.kbg_resource(*ni.allocatable.as_tuple())
+            e.max_task_num = ni.allocatable.max_task_num
+            e.unschedulable = 1 if obj.get("unschedulable") else 0
+            labels = [x.encode() for kv in (obj.get("labels") or {}).items() for x in kv]
+            taints = [str(t.get(f, "")).encode() for t in (obj.get("taints") or []) for f in ("key", "value", "effect")]
+            la = (ctypes.c_char_p * max(1, len(labels)))(*labels)
+            ta = (ctypes.c_char_p * max(1, len(taints)))(*taints)
+            spec = _abi.kbg_node_spec(obj["name"].encode(), la, len(labels) // 2, len(taints) // 3, ta)
+            keep.extend([la, ta, spec])
+            e.node_spec = ctypes.pointer(spec)
 
         def node_of(name):
             """kbg_event.node of a pod's NodeName: the session node of that name,
-            else the node the cache knows only from pods carrying it (sc.Nodes[NodeName])."""
+            else the node the cache knows only from pods carrying it
+            (sc.Nodes[NodeName]); a name the cache does not know makes that
+            node (NewNodeInfo(nil), event_handlers.go:49-53): KBG_EV_NODE_ADD."""
+            nonlocal n_nodes
             if not name:
                 return -1
             i = nidx.get(name)
-            return i if i is not None else self.flat.pod_only_names.get(name, -1)
-        evs = (_abi.kbg_event * max(1, len(changes)))()
-        keep = []
-        objs = {}  # task index -> its TaskInfo after the events (applied once the library accepts them)
-        n_objs = len(self.flat.task_objs)
-        renamed = {}  # pod-only node index -> the name its Node gave it
-        for k, (kind, obj) in enumerate(changes):
-            e = evs[k]
+            if i is None:
+                i = pod_only.get(name)
+            if i is None:
+                e = ev()
+                e.kind = _abi.EV_NODE_ADD
+                keep.append(name.encode())
+                e.node_name = keep[-1]
+                i = pod_only[name] = n_nodes
+                new_nodes[i] = NodeInfo(None)
+                n_nodes += 1
+            return i
+
+        def pod_node(e, name):
+            e.node = node_of(name)
+            if e.node >= 0 and name not in nidx:
+                keep.append(name.encode())  # a node known only from pods: its NodeName
+                e.node_name = keep[-1]
+
+        for kind, obj in changes:
             if kind in ("node_update", "node_add"):
                 # cache.AddNode / UpdateNode -> SetNode with the whole Node (the library
                 # compares labels and taints and rebuilds only when they change)
-                ni = NodeInfo(obj)
                 name = obj["name"]
                 idx = nidx.get(name)
-                if idx is None or self.flat.node_names[idx] != name:
-                    idx = self.flat.pod_only_names.get(name)
+                if idx is None:
+                    idx = pod_only.get(name)
                     if idx is None:
-                        raise ValueError(f"node {name!r}: not a node of the session (a new node needs a re-open)")
-                    renamed[idx] = name
+                        if kind == "node_update":  # updateNode: "node does not exist" (event_handlers.go:249-259)
+                            continue
+                        e = ev()  # a new node: NewNodeInfo(node), last in the session's node order
+                        e.kind = _abi.EV_NODE_ADD
+                        node_spec(e, obj)
+                        nidx[name] = n_nodes
+                        new_nodes[n_nodes] = NodeInfo(obj)
+                        n_nodes += 1
+                        continue
+                    pod_only.pop(name, None)
+                    if idx in new_nodes:  # made by a pod earlier in the batch
+                        new_nodes[idx] = NodeInfo(obj)
+                    else:
+                        renamed[idx] = name
                     nidx[name] = idx  # later events of the batch name the node by its Node's name
+                e = ev()
                 e.kind = _abi.EV_NODE_SET
                 e.node = idx
                 if os.environ.get("KBG_PY_NODE_UPDATE") == "1" and idx not in renamed:  # (A/B: Allocatable only)
+                    ni = NodeInfo(obj)
                     e.kind = _abi.EV_NODE_UPDATE
                     e.resource = _abi.kbg_resource(*ni.allocatable.as_tuple())
                     e.max_task_num = ni.allocatable.max_task_num
                     e.unschedulable = 1 if obj.get("unschedulable") else 0
                     continue
-                e.resource = _abi.kbg_resource(*ni.allocatable.as_tuple())
-                e.max_task_num = ni.allocatable.max_task_num
-                e.unschedulable = 1 if obj.get("unschedulable") else 0
-                labels = [x.encode() for kv in (obj.get("labels") or {}).items() for x in kv]
-                taints = [str(t.get(f, "")).encode() for t in (obj.get("taints") or []) for f in ("key", "value", "effect")]
-                la = (ctypes.c_char_p * max(1, len(labels)))(*labels)
-                ta = (ctypes.c_char_p * max(1, len(taints)))(*taints)
-                spec = _abi.kbg_node_spec(name.encode(), la, len(labels) // 2, len(taints) // 3, ta)
-                keep += [la, ta, spec]
-                e.node_spec = ctypes.pointer(spec)
+                node_spec(e, obj)
+                continue
+            if kind == "node_delete":  # deleteNode (event_handlers.go:262-268); an unknown name is an error there
+                name = obj["name"]
+                idx = nidx.pop(name, None)
+                if idx is None:
+                    idx = pod_only.pop(name, None)
+                if idx is None:
+                    continue
+                e = ev()
+                e.kind, e.node = _abi.EV_NODE_DELETE, idx
+                continue
+            if kind in ("pod_group_add", "pod_group_delete"):
+                jid = f"{obj.get('namespace', '')}/{obj['name']}"
+                if kind == "pod_group_delete":  # UnsetPodGroup: the job leaves ssn.Jobs
+                    j = jidx.pop(jid, None)
+                    if j is not None:
+                        e = ev()
+                        e.kind, e.job = _abi.EV_JOB_DELETE, j
+                        self._outside_jobs().add(jid)  # its pods stay in the cache, outside the session jobs
+                    continue
+                if jid in jidx:
+                    raise ValueError(f"PodGroup {jid!r}: an update of a session job's PodGroup needs a re-open")
+                if jid in self._outside_jobs():
+                    raise ValueError(f"PodGroup {jid!r}: the cache holds pods of it outside the session jobs "
+                                     "(they predate the PodGroup): re-open")
+                job = JobInfo(jid)
+                job.set_pod_group(obj, getattr(self.cache, "default_queue", ""))
+                if job.queue not in qidx:
+                    raise ValueError(f"PodGroup {jid!r}: queue {job.queue!r} is not a session queue (re-open when it "
+                                     "exists)")
+                e = ev()
+                e.kind = _abi.EV_JOB_ADD
+                keep.append(jid.encode())
+                e.name = keep[-1]
+                e.queue = qidx[job.queue]
+                e.min_available = job.min_available
+                e.priority = job.priority
+                e.creation_ns = job.creation_timestamp
+                jidx[jid] = n_jobs
+                new_jobs[n_jobs] = job
+                n_jobs += 1
+                continue
+            if kind in ("queue_add", "queue_delete"):
+                qi = QueueInfo(obj["name"], obj.get("weight", 0))
+                if kind == "queue_delete":
+                    q = qidx.pop(qi.uid, None)
+                    if q is not None:
+                        e = ev()
+                        e.kind, e.queue = _abi.EV_QUEUE_DELETE, q
+                        for jid in [k for k, j in jidx.items() if job_of(j).queue == qi.uid]:
+                            jidx.pop(jid)  # its jobs leave ssn.Jobs (cache.go:584-588)
+                            self._outside_jobs().add(jid)
+                    continue
+                if qi.uid in qidx:
+                    raise ValueError(f"queue {qi.uid!r}: an update of a session queue needs a re-open")
+                e = ev()
+                e.kind = _abi.EV_QUEUE_ADD
+                keep.append(qi.uid.encode())
+                e.name = keep[-1]
+                e.weight = qi.weight
+                qidx[qi.uid] = n_queues
+                new_queues[n_queues] = qi
+                n_queues += 1
                 continue
             ti = TaskInfo(obj)
             if kind in ("pod_update", "pod_delete"):
+                if kind == "pod_update":
+                    node_of(ti.node_name)  # a NodeInfo(nil) first, when the name is new to the cache
+                e = ev()
                 e.kind = _abi.EV_POD_UPDATE if kind == "pod_update" else _abi.EV_POD_DELETE
                 e.task = tidx[obj["uid"]]
                 e.status = ti.status
-                e.node = node_of(ti.node_name)
-                if e.node >= 0 and e.node not in renamed and not self.flat.node_names[e.node]:
-                    keep.append(ti.node_name.encode())  # a node known only from pods: its NodeName
-                    e.node_name = keep[-1]
+                if kind == "pod_update":
+                    pod_node(e, ti.node_name)
                 objs[e.task] = ti
             elif kind == "pod_add":
+                if ti.job not in jidx:
+                    raise ValueError(f"pod {ti.uid!r}: job {ti.job!r} is not a session job (re-open)")
+                node_of(ti.node_name)
+                e = ev()
                 e.kind = _abi.EV_POD_ADD
-                e.job = self.flat.job_index[ti.job]
-                e.spec = self.flat.spec_index(obj)
+                e.job = jidx[ti.job]
+                e.spec = flat.spec_index(obj)
                 e.status = ti.status
                 e.priority = ti.priority
-                e.node = node_of(ti.node_name)
-                if e.node >= 0 and e.node not in renamed and not self.flat.node_names[e.node]:
-                    keep.append(ti.node_name.encode())
-                    e.node_name = keep[-1]
+                pod_node(e, ti.node_name)
                 e.resource = _abi.kbg_resource(*ti.resreq.as_tuple())
                 keep += [ti.uid.encode(), pod_key(obj).encode()]
                 e.uid, e.pod_key = keep[-2], keep[-1]
@@ -229,21 +354,72 @@ class Session:
                 n_objs += 1
             else:
                 raise ValueError(f"unknown change {kind}")
-        _abi.check(_abi.lib().kbg_session_update(self.handle, evs, len(changes)))
+        _abi.check(L.kbg_session_update(self.handle, evs, n_ev))
         for i, name in renamed.items():  # the NodeInfo the cache made from a pod has its Node's name now
-            self.flat.node_names[i] = name
-            self.flat.pod_only_names.pop(name, None)
+            flat.node_names[i] = name
+            flat.pod_only_names.pop(name, None)
             self.nodes[i].name = name
             self.node_index[name] = self.nodes[i]
-        for i in range(len(self.flat.task_objs), n_objs):
-            self.flat.task_objs.append(None)
+        task_objs = flat.task_objs + [None] * (n_objs - len(flat.task_objs))
         for i, ti in objs.items():
-            self.flat.task_objs[i] = ti
+            task_objs[i] = ti
+        structural = any(evs[k].kind >= _abi.EV_NODE_ADD for k in range(n_ev))
+        if structural:
+            self._renumber(task_objs, new_nodes, new_jobs, new_queues, pod_only)
+        else:
+            flat.task_objs = task_objs
         from .api import PENDING
         live = set(tidx)  # (deleted pods keep their index; counts only size output buffers)
-        self.flat.pending_all = max(self.flat.pending_all, sum(1 for t in self.flat.task_objs
-                                                               if t.uid in live and t.status == PENDING))
-        self.flat.pending_count = max(self.flat.pending_count, self.flat.pending_all)
+        flat.pending_all = max(flat.pending_all, sum(1 for t in flat.task_objs
+                                                     if t is not None and t.uid in live and t.status == PENDING))
+        flat.pending_count = max(flat.pending_count, flat.pending_all)
+
+    def _outside_jobs(self):
+        """JobIDs with pods the snapshot holds outside the session jobs
+        (Others, pods on nodes): a PodGroup for one of them needs a re-open."""
+        if getattr(self, "_outside", None) is None:
+            mine = {t.uid for t in self.flat.task_objs if t is not None}
+            out = {t.job for t in self.others}
+            out |= {t.job for n in self.nodes for t in n.tasks.values() if t.uid not in mine}
+            self._outside = out
+        return self._outside
+
+    def _renumber(self, task_objs, new_nodes, new_jobs, new_queues, pod_only):
+        """The wrapper's lists after a structural update, by the library's
+        old -> new index maps (kbg_session_renumbering)."""
+        L = _abi.lib()
+        flat = self.flat
+
+        def renum(kind):
+            n = ctypes.c_int32(0)
+            _abi.check(L.kbg_session_renumbering(self.handle, kind, None, 0, ctypes.byref(n)))
+            buf = (ctypes.c_int32 * max(1, n.value))()
+            _abi.check(L.kbg_session_renumbering(self.handle, kind, buf, n.value, ctypes.byref(n)))
+            return list(buf[:n.value])
+
+        def remap(old, r):
+            out = [None] * (max(r) + 1 if r and max(r) >= 0 else 0)
+            for i, x in enumerate(old):
+                if i < len(r) and r[i] >= 0:
+                    out[r[i]] = x
+            return out
+
+        rt, rn, rj, rq = (renum(k) for k in (_abi.RENUM_TASKS, _abi.RENUM_NODES, _abi.RENUM_JOBS, _abi.RENUM_QUEUES))
+        flat.task_objs = remap(task_objs, rt)
+        nodes = list(self.nodes) + [new_nodes[i] for i in sorted(new_nodes)]
+        names = list(flat.node_names) + [new_nodes[i].name for i in sorted(new_nodes)]
+        self.nodes = remap(nodes, rn)
+        flat.node_names = remap(names, rn)
+        self.node_index = {n.name: n for n in self.nodes if n.name}
+        flat.pod_only_names = {nm: rn[i] for nm, i in pod_only.items() if i < len(rn) and rn[i] >= 0}
+        jobs = list(self.jobs) + [new_jobs[i] for i in sorted(new_jobs)]
+        self.jobs = remap(jobs, rj)
+        self.job_index = {j.uid: j for j in self.jobs}
+        flat.job_index = {j.uid: i for i, j in enumerate(self.jobs)}
+        queues = list(self.queues) + [new_queues[i] for i in sorted(new_queues)]
+        self.queues = remap(queues, rq)
+        self.queue_index = {q.uid: q for q in self.queues}
+        flat.queue_index = {q.uid: i for i, q in enumerate(self.queues)}
 
     def job_state(self, j):
         st = _abi.kbg_job_state()

@@ -310,6 +310,73 @@ def churn(fx, seed, session_uids, decided=(), bind=0.6, done=0.08, delete=0.03, 
     return changes, fx1
 
 
+def structural(fx, seed, session_jobs, session_uids, session_queues):
+    """Structural cache events between two cycles of session `fx`
+    (kbg_session_update KBG_EV_NODE_ADD ... QUEUE_DELETE): new nodes, a
+    deleted node (its pods stay in their jobs on no NodeInfo), a new PodGroup
+    with pods (one of them may run on a new node), a deleted PodGroup (its
+    pods stay in the cache outside the session jobs), a new queue with a job,
+    a deleted queue (its jobs leave the session), then completions of
+    unaffected Running pods. Returns the change list in event order."""
+    rng = random.Random(seed)
+    changes = []
+    pods = {p["uid"]: p for p in fx["pods"]}
+    groups = {(g.get("namespace", ""), g["name"]): g for g in fx.get("podGroups", [])}
+    sess = [k for k in groups if f"{k[0]}/{k[1]}" in session_jobs]
+    gone_nodes, gone_jobs, gone_queues = set(), set(), set()
+    new_nodes = []
+    for i in range(rng.randint(0, 2)):
+        base = rng.choice(fx["nodes"])
+        n = dict(base, name=f"nx{seed}-{i}")
+        new_nodes.append(n["name"])
+        changes.append(("node_add", n))
+    if fx["nodes"] and rng.random() < 0.6:
+        n = rng.choice(fx["nodes"])
+        gone_nodes.add(n["name"])
+        changes.append(("node_delete", n))
+    if sess and rng.random() < 0.6:
+        k = rng.choice(sess)
+        gone_jobs.add(f"{k[0]}/{k[1]}")
+        changes.append(("pod_group_delete", groups[k]))
+    if session_queues and rng.random() < 0.4:
+        q = rng.choice(sorted(session_queues))
+        gone_queues.add(q)
+        changes.append(("queue_delete", {"name": q}))
+        for k, g in groups.items():  # (the default queue's jobs too: their queue is the job's own field)
+            if f"{k[0]}/{k[1]}" in session_jobs and g.get("queue") == q:
+                gone_jobs.add(f"{k[0]}/{k[1]}")
+    queues = [q for q in session_queues if q not in gone_queues]
+    if rng.random() < 0.5:
+        q = {"name": f"qx{seed}", "weight": rng.randint(1, 4)}
+        changes.append(("queue_add", q))
+        queues.append(q["name"])
+    # a new job: a copy of a session job's pods under a new PodGroup
+    live_pods = [p for p in pods.values() if p["uid"] in session_uids]
+    if live_pods and queues and rng.random() < 0.8:
+        base = rng.choice(live_pods)
+        ns = base.get("namespace", "")
+        gname = f"pgx{seed}"
+        changes.append(("pod_group_add", {"namespace": ns, "name": gname, "minMember": rng.randint(1, 3),
+                                          "queue": rng.choice(queues), "creationTimestamp": 10 ** 12 + seed}))
+        for i in range(rng.randint(1, 4)):
+            p = dict(base, uid=f"px{seed}-{i}", name=f"px{seed}-{i}", phase="Pending", nodeName="",
+                     annotations=dict(base.get("annotations") or {}, **{"scheduling.k8s.io/group-name": gname}))
+            p.pop("deletionTimestamp", None)
+            if new_nodes and i == 0 and rng.random() < 0.5:
+                p = dict(p, phase="Running", nodeName=new_nodes[0])
+            changes.append(("pod_add", p))
+    # completions of Running session pods the structural events left alone
+    left = [p for p in live_pods if p.get("phase") == "Running" and p.get("nodeName") not in gone_nodes]
+    job_of = {}
+    for p in left:
+        g = (p.get("annotations") or {}).get("scheduling.k8s.io/group-name")
+        job_of[p["uid"]] = f"{p.get('namespace', '')}/{g}" if g else None
+    left = [p for p in left if job_of[p["uid"]] not in gone_jobs and job_of[p["uid"]] in session_jobs]
+    for p in rng.sample(left, min(len(left), rng.randint(0, 2))):
+        changes.append(("pod_update", dict(p, phase="Succeeded")))
+    return changes
+
+
 # ------------------------------------------------------------------ fuzz
 _OPS = ("In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt")
 

@@ -471,3 +471,166 @@ def test_update_node_relabel(seed):
             n["taints"] = []
         changes.append(("node_update", copy.deepcopy(n)))
     check_changes(fx0, changes, fx1, {"batch_tasks": 1 + seed % 5})
+
+
+def _replay(fx0, changes):
+    """The cache of fx0 after `changes` (event_handlers.go): what a fresh open
+    of the updated cache sees, including what a fixture cannot say (pods
+    whose node was deleted, PodGroup-less jobs that still hold pods)."""
+    cache = cache_from_fixture(fx0, FakeBinder())
+    pods = {p["uid"]: p for p in fx0["pods"]}
+    for kind, obj in changes:
+        if kind == "pod_add":
+            cache.add_pod(obj)
+            pods[obj["uid"]] = obj
+        elif kind == "pod_update":
+            cache.update_pod(pods[obj["uid"]], obj)
+            pods[obj["uid"]] = obj
+        elif kind == "pod_delete":
+            cache.delete_pod(obj)
+            pods.pop(obj["uid"], None)
+        else:
+            getattr(cache, {"node_add": "add_node", "node_update": "update_node", "node_delete": "delete_node",
+                            "pod_group_add": "add_pod_group", "pod_group_delete": "delete_pod_group",
+                            "queue_add": "add_queue", "queue_delete": "delete_queue"}[kind])(obj)
+    return cache
+
+
+def check_structural(fx0, changes_of, opts=None):
+    """open(S0) + update(structural changes) + the cycle's actions against a
+    fresh open of the replayed cache in the updated session's order."""
+    from kbgpu.api import RefPanic
+    actions = fx0.get("actions") or ["allocate"]
+    try:
+        ssn = _open(fx0, opts)
+    except RefPanic as e:
+        pytest.skip(f"S0: the reference cache panics: {e}")
+    except _abi.KbgError as e:
+        if e.status not in ("ref_panic", "unsupported"):
+            raise
+        pytest.skip(f"S0 does not open ({e.status}, documented refusal): {e}")
+    fssn = None
+    try:
+        changes = changes_of(ssn)
+        try:
+            ssn.update(changes)
+        except ValueError as e:  # the wrapper's documented re-open cases (a PodGroup of pods outside the session)
+            pytest.skip(f"update needs a re-open: {e}")
+        except _abi.KbgError as e:
+            if e.status == "unsupported":
+                pytest.skip(f"update refused (unsupported, documented): {e}")
+            assert e.status == "ref_panic", e
+            return {"status": "ref_panic"}
+        got = abi_cycle(ssn, actions)
+        order = {"jobs": [j.uid for j in ssn.jobs], "nodes": list(ssn.flat.node_names),
+                 "queues": [q.uid for q in ssn.queues]}
+        try:
+            fssn = open_session(_OrderedCache(_replay(fx0, changes), {"sessionOrder": order}), fixture_tiers(fx0),
+                                opts or {})
+        except RefPanic:
+            assert got["status"] == "ref_panic", got
+            return got
+        assert [j.uid for j in fssn.jobs] == order["jobs"]
+        assert [q.uid for q in fssn.queues] == order["queues"]
+        assert [t.uid for t in fssn.flat.task_objs] == [t.uid for t in ssn.flat.task_objs]
+        fresh = abi_cycle(fssn, actions)
+        assert got == fresh
+        return got
+    finally:
+        ssn.close()
+        if fssn:
+            fssn.close()
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_update_structural(seed):
+    """Nodes, PodGroups and queues that join or leave (KBG_EV_NODE_ADD ...
+    QUEUE_DELETE, event_handlers.go:232-268,344-381,635-654): the session is
+    renumbered (kbg_session_renumbering) and its next cycle equals a fresh
+    open of the cache after the same events."""
+    fx0 = synth.random_fixture(11000 + seed) if seed % 3 else synth.contended_fixture(11000 + seed, nodes=12, jobs=8,
+                                                                                      tasks=6)
+
+    def changes_of(ssn):
+        return synth.structural(fx0, seed, {j.uid for j in ssn.jobs}, {t.uid for t in ssn.flat.task_objs},
+                                [q.uid for q in ssn.queues])
+    check_structural(fx0, changes_of, {"batch_tasks": 1 + seed % 7, "full_scan": seed % 2})
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_update_structural_chain(seed):
+    """Structural and pod churn over several updates of one session: each
+    round's cycle equals a fresh open of the replayed cache."""
+    fx0 = synth.contended_fixture(11500 + seed, nodes=16, jobs=10, tasks=6)
+    ssn = _open(fx0)
+    changes_all = []
+    try:
+        for r in range(3):
+            ch = synth.structural(fx0, 100 * seed + r, {j.uid for j in ssn.jobs},
+                                  {t.uid for t in ssn.flat.task_objs}, [q.uid for q in ssn.queues])
+            # (new names carry the round's seed: unique over the chain)
+            try:
+                ssn.update(ch)
+            except (ValueError, _abi.KbgError) as e:
+                if isinstance(e, _abi.KbgError) and e.status not in ("unsupported", "ref_panic"):
+                    raise
+                pytest.skip(f"round {r}: {e}")
+            changes_all += ch
+            got = abi_cycle(ssn, ["allocate"])
+            order = {"jobs": [j.uid for j in ssn.jobs], "nodes": list(ssn.flat.node_names),
+                     "queues": [q.uid for q in ssn.queues]}
+            fssn = open_session(_OrderedCache(_replay(fx0, changes_all), {"sessionOrder": order}),
+                                fixture_tiers(fx0), {})
+            try:
+                assert got == abi_cycle(fssn, ["allocate"]), r
+            finally:
+                fssn.close()
+            _abi.check(_abi.lib().kbg_session_reset(ssn.handle))
+    finally:
+        ssn.close()
+
+
+@pytest.mark.parametrize("cid", [1, pytest.param(3, marks=pytest.mark.slow)])
+def test_update_structural_configs(cid):
+    """BASELINE C1 and C3 with structural events: the rebuild from the
+    session's own updated snapshot (update_ms reported) against a fresh open
+    of the replayed cache."""
+    fx0 = synth.config_fixture(cid)
+
+    def changes_of(ssn):
+        ch = synth.structural(fx0, 40 + cid, {j.uid for j in ssn.jobs}, {t.uid for t in ssn.flat.task_objs},
+                              [q.uid for q in ssn.queues])
+        return [(k, o) for k, o in ch if k != "queue_delete" or len(ssn.queues) > 1]  # (C1: one queue)
+    got = check_structural(fx0, changes_of)
+    assert got["status"] == "ok"
+
+
+def test_refused_structural_leaves_the_session_unchanged():
+    """Invalid structural events (a NODE_ADD of a name the session holds, a
+    JOB_ADD into a queue the batch deleted, a pod event after its job left in
+    the same batch) are refused before anything applies."""
+    fx = synth.config_fixture(1)
+    ssn = _open(fx)
+    try:
+        before = abi_cycle(ssn, ["allocate"])
+        L = _abi.lib()
+        name = ssn.flat.node_names[0].encode()
+        spec = _abi.kbg_node_spec(name, None, 0, 0, None)
+        evs = (_abi.kbg_event * 2)()
+        evs[0].kind, evs[0].node_spec = _abi.EV_NODE_ADD, ctypes.pointer(spec)
+        assert L.kbg_session_update(ssn.handle, evs, 1) == _abi.KBG_E_INVALID
+        evs[0] = _abi.kbg_event(kind=_abi.EV_QUEUE_DELETE, queue=0)
+        evs[1] = _abi.kbg_event(kind=_abi.EV_JOB_ADD, name=b"ns/new", queue=0)
+        assert L.kbg_session_update(ssn.handle, evs, 2) == _abi.KBG_E_INVALID
+        t = 0
+        j = ssn.flat.job_index[ssn.flat.task_objs[t].job]
+        evs[0] = _abi.kbg_event(kind=_abi.EV_JOB_DELETE, job=j)
+        evs[1] = _abi.kbg_event(kind=_abi.EV_POD_DELETE, task=t)
+        assert L.kbg_session_update(ssn.handle, evs, 2) == _abi.KBG_E_UNSUPPORTED
+        n = ctypes.c_int32(-1)
+        _abi.check(L.kbg_session_renumbering(ssn.handle, _abi.RENUM_TASKS, None, 0, ctypes.byref(n)))
+        assert n.value == 0
+        _abi.check(L.kbg_session_reset(ssn.handle))
+        assert abi_cycle(ssn, ["allocate"]) == before
+    finally:
+        ssn.close()
