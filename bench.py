@@ -786,12 +786,37 @@ def resident_bench(cache, fx, base_opts, steps=5, churn=0.01, seed=5):
         out["churn_allocate_ms"].append(ssn.stats().allocate_ms)
         out["churn_placements"].append(n.value)
         binds = [(buf[j].task, buf[j].node) for j in range(n.value) if buf[j].kind == _abi.KIND_ALLOCATE]
+    # one structural update (ABI 13): a node and a PodGroup with 8 pods join, the last job's PodGroup
+    # leaves — the session rebuilds from its own updated snapshot — then an allocate cycle
+    nd0 = ssn.flat.arrays["nodes"][0]
+    spec = _abi.kbg_node_spec(b"bench-new-node", None, 0, 0, None)
+    evs = (_abi.kbg_event * 11)()
+    evs[0].kind, evs[0].node_spec = _abi.EV_NODE_ADD, ctypes.pointer(spec)
+    evs[0].resource = _abi.kbg_resource(*[float(x) for x in nd0["allocatable"]])
+    evs[0].max_task_num = int(nd0["max_task_num"])
+    evs[1].kind, evs[1].name, evs[1].queue, evs[1].min_available = _abi.EV_JOB_ADD, b"bench/new-job", 0, 8
+    new_job = len(ssn.jobs)
+    src = tasks[jobs_of[job_ids[0]]]
+    for a in range(8):
+        e = evs[2 + a]
+        e.kind, e.job, e.spec, e.status, e.node = _abi.EV_POD_ADD, new_job, int(src["spec"]), 1, -1
+        e.priority = int(src["priority"])
+        e.resource = _abi.kbg_resource(*[float(x) for x in src["resreq"]])
+        keep += [f"struct-{a}".encode(), f"bench/struct-{a}".encode()]
+        e.uid, e.pod_key = keep[-2], keep[-1]
+    evs[10].kind, evs[10].job = _abi.EV_JOB_DELETE, job_ids[-1]
+    _abi.check(L.kbg_session_update(ssn.handle, evs, 11))
+    out["structural_events"] = 11
+    out["structural_update_ms"] = ssn.stats().update_ms
+    _abi.check(L.kbg_allocate(ssn.handle, buf, cap, ctypes.byref(n)))
+    out["structural_allocate_ms"] = ssn.stats().allocate_ms
     ssn.close()
     out["churn_update_ms_p50"] = statistics.median(out["churn_update_ms"])
     out["churn_allocate_ms_p50"] = statistics.median(out["churn_allocate_ms"])
     out["note"] = ("kbg_session_update replaces a session open per cycle (open_ms): binds of the first cycle, then "
                    f"{churn:.0%} completions + {churn:.0%} new pods + the last cycle's binds per update, each "
-                   "followed by an allocate cycle")
+                   "followed by an allocate cycle; structural_update_ms: one update in which a node and a PodGroup "
+                   "with 8 pods join and a PodGroup leaves (the session rebuilds from its own updated snapshot)")
     return out
 
 

@@ -7858,19 +7858,37 @@ kbg_status update_precheck(const Session& S, const kbg_event* ev, int32_t n) {
 // session jobs (with their node copies when every pod on a live node has one),
 // the Running tasks of a job whose PodGroup was deleted join Others — opened
 // as a new session that replaces this one; renum[] maps the old indices.
-kbg_status restructure(Session& S) {
+struct Rebuilt {  // a session's updated snapshot (pointing into the session's own arrays too) and its renumbering
+  std::vector<int32_t> rq, rj, rn, rt;
+  std::vector<kbg_queue> queues;
+  std::vector<kbg_job> jobs;
+  std::vector<kbg_task> tasks;
+  std::vector<kbg_resource> others;
+  std::vector<kbg_node> nodes;
+  std::vector<int32_t> node_tasks, node_keys;
+  std::vector<kbg_node_pod> node_pods;
+  std::vector<kbg_host_port> ports;
+  std::vector<const char*> strs;
+  kbg_snapshot sn{};
+};
+kbg_status rebuild_snapshot(const Session& S, Rebuilt& B) {
   const int32_t N = S.n_nodes, J = S.n_jobs, Q = S.n_queues, T = S.n_tasks;
   auto gone = [](const std::vector<uint8_t>& v, int32_t i) { return (size_t)i < v.size() && v[i] != 0; };
-  std::vector<int32_t> rq(Q, -1), rj(J, -1), rn(N, -1), rt(T, -1);
-  std::vector<kbg_queue> queues;
+  std::vector<int32_t>&rq = B.rq, &rj = B.rj, &rn = B.rn, &rt = B.rt;
+  rq.assign(Q, -1);
+  rj.assign(J, -1);
+  rn.assign(N, -1);
+  rt.assign(T, -1);
+  std::vector<kbg_queue>& queues = B.queues;
   for (int32_t q = 0; q < Q; ++q)
     if (!gone(S.queue_dead, q)) {
       rq[q] = (int32_t)queues.size();
       queues.push_back(S.queues_in[q]);
     }
-  std::vector<kbg_job> jobs;
-  std::vector<kbg_task> tasks;
-  std::vector<kbg_resource> others = S.others_in;
+  std::vector<kbg_job>& jobs = B.jobs;
+  std::vector<kbg_task>& tasks = B.tasks;
+  std::vector<kbg_resource>& others = B.others;
+  others = S.others_in;
   for (int32_t j = 0; j < J; ++j) {
     if (gone(S.job_dead, j)) {
       if (gone(S.job_to_others, j))  // PodGroup == nil: its Running tasks are Others
@@ -7910,10 +7928,11 @@ kbg_status restructure(Session& S) {
       }
     }
   }
-  std::vector<kbg_node> nodes;
-  std::vector<int32_t> node_tasks, node_keys;
-  std::vector<kbg_node_pod> node_pods;
-  std::vector<kbg_host_port> ports = S.ports_in;  // the specs' ports keep their offsets
+  std::vector<kbg_node>& nodes = B.nodes;
+  std::vector<int32_t>&node_tasks = B.node_tasks, &node_keys = B.node_keys;
+  std::vector<kbg_node_pod>& node_pods = B.node_pods;
+  std::vector<kbg_host_port>& ports = B.ports;
+  ports = S.ports_in;  // the specs' ports keep their offsets
   for (int32_t n = 0; n < N; ++n) {
     if (gone(S.node_dead, n)) continue;
     kbg_node nd = S.nodes_in[n];
@@ -7948,9 +7967,10 @@ kbg_status restructure(Session& S) {
     rn[n] = (int32_t)nodes.size();
     nodes.push_back(nd);
   }
-  std::vector<const char*> strs(S.strs.size());
+  std::vector<const char*>& strs = B.strs;
+  strs.resize(S.strs.size());
   for (size_t i = 0; i < strs.size(); ++i) strs[i] = S.strs[i].c_str();
-  kbg_snapshot sn{};
+  kbg_snapshot& sn = B.sn;
   sn.strings = strs.data();
   sn.n_strings = (int32_t)strs.size();
   sn.nodes = nodes.data(), sn.n_nodes = (int32_t)nodes.size();
@@ -7975,10 +7995,18 @@ kbg_status restructure(Session& S) {
   sn.node_pod_keys = node_keys.data(), sn.n_node_pod_keys = (int32_t)node_keys.size();
   sn.node_pods = copies ? node_pods.data() : nullptr;
   sn.n_node_pods = copies ? (int32_t)node_pods.size() : 0;
+  return KBG_OK;
+}
+
+kbg_status restructure(Session& S) {
+  Rebuilt B;
+  if (kbg_status st = rebuild_snapshot(S, B); st != KBG_OK) return st;
+  const int32_t N = S.n_nodes;
+  const std::vector<int32_t>& rn = B.rn;
   kbg_options o = S.opts;
   o.device = S.device;
   std::unique_ptr<Session> R(new Session());
-  kbg_status st = open_session(*R, &sn, &o, nullptr);
+  kbg_status st = open_session(*R, &B.sn, &o, nullptr);
   if (st != KBG_OK) {
     free_device(*R);
     return st;
@@ -8003,10 +8031,10 @@ kbg_status restructure(Session& S) {
   R->rebuilds = S.rebuilds + 1;
   free_device(S);
   S = std::move(*R);
-  S.renum[KBG_RENUM_TASKS] = std::move(rt);
-  S.renum[KBG_RENUM_NODES] = std::move(rn);
-  S.renum[KBG_RENUM_JOBS] = std::move(rj);
-  S.renum[KBG_RENUM_QUEUES] = std::move(rq);
+  S.renum[KBG_RENUM_TASKS] = std::move(B.rt);
+  S.renum[KBG_RENUM_NODES] = std::move(B.rn);
+  S.renum[KBG_RENUM_JOBS] = std::move(B.rj);
+  S.renum[KBG_RENUM_QUEUES] = std::move(B.rq);
   return KBG_OK;
 }
 

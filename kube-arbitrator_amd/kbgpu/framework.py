@@ -159,8 +159,16 @@ class Session:
         renumbering (kbg_session_renumbering). The host-side objects are not
         replayed: read results through the C ABI (decisions, job / queue /
         node state)."""
+        plan = self.marshal(changes)
+        _abi.check(_abi.lib().kbg_session_update(self.handle, plan.evs, plan.n_ev))
+        self._accept(plan)
+
+    def marshal(self, changes):
+        """The kbg_event batch of `changes` against this session's current
+        numbering (update's first half; host-only, also used by the CPU tests
+        of the structural path through the tool library)."""
+        from types import SimpleNamespace
         from .api import JobInfo, NodeInfo, QueueInfo, TaskInfo, pod_key
-        L = _abi.lib()
         flat = self.flat
         tidx = {t.uid: i for i, t in enumerate(flat.task_objs) if t is not None}
         nidx = {n: i for i, n in enumerate(flat.node_names) if n}
@@ -354,8 +362,16 @@ class Session:
                 n_objs += 1
             else:
                 raise ValueError(f"unknown change {kind}")
-        _abi.check(L.kbg_session_update(self.handle, evs, n_ev))
-        for i, name in renamed.items():  # the NodeInfo the cache made from a pod has its Node's name now
+        return SimpleNamespace(evs=evs, n_ev=n_ev, keep=keep, objs=objs, n_objs=n_objs, renamed=renamed, tidx=tidx,
+                               new_nodes=new_nodes, new_jobs=new_jobs, new_queues=new_queues, pod_only=pod_only)
+
+    def _accept(self, plan):
+        """update's second half, once the library applied the batch: the
+        wrapper's lists follow it (renumbered after a structural batch)."""
+        flat = self.flat
+        evs, n_ev, objs, n_objs, tidx = plan.evs, plan.n_ev, plan.objs, plan.n_objs, plan.tidx
+        new_nodes, new_jobs, new_queues, pod_only = plan.new_nodes, plan.new_jobs, plan.new_queues, plan.pod_only
+        for i, name in plan.renamed.items():  # the NodeInfo the cache made from a pod has its Node's name now
             flat.node_names[i] = name
             flat.pod_only_names.pop(name, None)
             self.nodes[i].name = name
@@ -384,13 +400,15 @@ class Session:
             self._outside = out
         return self._outside
 
-    def _renumber(self, task_objs, new_nodes, new_jobs, new_queues, pod_only):
+    def _renumber(self, task_objs, new_nodes, new_jobs, new_queues, pod_only, maps=None):
         """The wrapper's lists after a structural update, by the library's
-        old -> new index maps (kbg_session_renumbering)."""
+        old -> new index maps (kbg_session_renumbering; `maps`: given)."""
         L = _abi.lib()
         flat = self.flat
 
         def renum(kind):
+            if maps is not None:
+                return maps[kind]
             n = ctypes.c_int32(0)
             _abi.check(L.kbg_session_renumbering(self.handle, kind, None, 0, ctypes.byref(n)))
             buf = (ctypes.c_int32 * max(1, n.value))()

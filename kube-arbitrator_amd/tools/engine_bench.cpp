@@ -91,6 +91,46 @@ extern "C" int32_t kbg_tool_update_nodes(const kbg_snapshot* snap, const kbg_opt
   return outcome;
 }
 
+// Structural events (kbg_session_update KBG_EV_NODE_ADD ... QUEUE_DELETE)
+// without a device: the session's host state opened from the snapshot, the
+// batch prechecked and applied as the library does, then the updated snapshot
+// the library would open from (rebuild_snapshot), encoded in the wire format
+// into out (KBG_E_CAPACITY with *n_out = the size needed), and the four
+// renumbering maps (tasks, nodes, jobs, queues; each renum[k] sized by the
+// caller to the old count plus the batch's additions). Returns the precheck /
+// apply status, or 100 + the status of opening the snapshot's host state (a
+// session on it would not open: e.g. proportion's panic at OnSessionOpen).
+// Test infrastructure only (tests/test_update_structural_host.py).
+extern "C" int32_t kbg_tool_structural(const kbg_snapshot* snap, const kbg_options* o, const kbg_event* ev, int32_t n,
+                                       uint8_t* out, int64_t cap, int64_t* n_out, int32_t* renum[4], int32_t lens[4]) {
+  kbg::Session S;
+  if (kbg_status st = ingest(S, snap, o); st != KBG_OK) return 100 + st;
+  kbg::StaticHost sh;
+  int outcome;
+  if (kbg_status st = derive_host(S, &sh, &outcome); st != KBG_OK) return 100 + st;
+  S.n_classes = sh.n_classes;
+  if (kbg_status st = update_precheck(S, ev, n); st != KBG_OK) return st;
+  S.node_dead.assign(S.n_nodes, 0);
+  S.job_dead.assign(S.n_jobs, 0);
+  S.job_to_others.assign(S.n_jobs, 0);
+  S.queue_dead.assign(S.n_queues, 0);
+  UpdateCtx U;
+  U.seen.assign(S.n_nodes, 0);
+  S.jmove_defer = (int64_t)n * 8 > (int64_t)S.n_tasks;
+  for (int32_t i = 0; i < n; ++i)
+    if (kbg_status st = apply_event(S, U, ev[i], nullptr); st != KBG_OK) return st;
+  finish_job_lists(S);
+  Rebuilt B;
+  if (kbg_status st = rebuild_snapshot(S, B); st != KBG_OK) return st;
+  const std::vector<int32_t>* maps[4] = {&B.rt, &B.rn, &B.rj, &B.rq};
+  for (int k = 0; k < 4; ++k) {
+    if ((int32_t)maps[k]->size() > lens[k]) return KBG_E_CAPACITY;
+    lens[k] = (int32_t)maps[k]->size();
+    std::copy(maps[k]->begin(), maps[k]->end(), renum[k]);
+  }
+  return kbg_snapshot_encode(&B.sn, out, cap, n_out);
+}
+
 // ---------------------------------------------------------------------------
 // The owner-resolve protocol of a sharded allocate (allocate_sharded) without a
 // device: each rank's host state is opened from the snapshot, the class masks

@@ -40,7 +40,7 @@ def key(name):
     base = re.sub(r"^void ", "", base)
     base = base.replace("kbg::", "")
     # the fused kernel's rows-per-workgroup variants (16 / 24 / 32) of one mode are one entry
-    return re.sub(r"^(kbg_firstfit_kernel<\w+, \w+), \d+>$", r"\1>", base)
+    return re.sub(r"^(kbg_firstfit_kernel<\w+, \w+)(, \w+)?, \d+>$", r"\1>", base)  # (COMPLETE merged)
 
 
 def rows(path):
