@@ -2133,10 +2133,15 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   // then entered into the content index in id order (the first id of a
   // content is its canonical id), each slot requested a few strings ahead.
   const size_t NS = (size_t)std::max(0, snap->n_strings);
+  // a session rebuilt from its own updated snapshot (restructure) adopts its
+  // string table and content index: the snapshot's strings are that table
+  const bool adopted = S.adopt_strings && S.strs.size() == NS && S.canon.size() == NS;
+  S.adopt_strings = false;
+  std::vector<uint64_t> sh(adopted ? 0 : NS);
+  if (!adopted) {
   S.strs.clear();
   S.strs.reserve(NS + 2 * more);
   S.strs.resize(NS);
-  std::vector<uint64_t> sh(NS);
   {
     const size_t P = NS < 65536 ? 1 : std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency()));
     auto copy_range = [&](size_t lo, size_t hi) {
@@ -2168,6 +2173,7 @@ kbg_status ingest(Session& S, const kbg_snapshot* snap, const kbg_options* o) {
   for (size_t i = 0; i < NS; ++i) {
     if (i + kStrAhead < NS) S.canon_of.prefetch(sh[i + kStrAhead]);
     S.canon[i] = S.canon_of.insert_h(S.strs, (int32_t)i, sh[i]);
+  }
   }
   phase("strings");
   S.n_nodes = snap->n_nodes;
@@ -8006,6 +8012,12 @@ kbg_status restructure(Session& S) {
   kbg_options o = S.opts;
   o.device = S.device;
   std::unique_ptr<Session> R(new Session());
+  // the string table moves over as it is (the vector's elements keep their
+  // addresses, so the snapshot's string pointers stay valid)
+  R->strs = std::move(S.strs);
+  R->canon = std::move(S.canon);
+  R->canon_of = std::move(S.canon_of);
+  R->adopt_strings = true;
   kbg_status st = open_session(*R, &B.sn, &o, nullptr);
   if (st != KBG_OK) {
     free_device(*R);

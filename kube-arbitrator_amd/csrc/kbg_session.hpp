@@ -533,7 +533,7 @@ struct Session {
   // update (dropped when the session is rebuilt from its updated snapshot),
   // and the old -> new maps of the last update that rebuilt (kbgpu.h
   // kbg_session_renumbering; empty: nothing renumbered)
-  bool structural = false;
+  bool adopt_strings = false;                         // ingest keeps strs / canon / canon_of (restructure)
   std::vector<uint8_t> node_dead, job_dead, queue_dead, job_to_others;
   std::vector<int32_t> renum[4];
   std::vector<kbg_plugin_option> plugins_in;          // the snapshot's tier entries, for the rebuild

@@ -35,12 +35,20 @@ WANT = ("kbg_firstfit_kernel", "kbg_fitdelta_kernel", "kbg_scan_kernel", "kbg_se
         "kbg_victim_big_kernel", "kbg_victim_prep_kernel", "kbg_apply_kernel", "copyBuffer")
 
 
-def key(name):
+def key(name, grid=0):
+    """grid: the launch's work-items. The complete variant (<INT, false, true,
+    ROWS>: one round, every word out) runs both modes' batches at C3's table
+    size; its launches are told apart by size — a full-scan batch is one row
+    per task (thousands of rows, >= 64 workgroups of 1024), a grouped batch
+    one row per shape — and filed under <INT, false> / <INT, true>."""
     base = name.split("(")[0]
     base = re.sub(r"^void ", "", base)
     base = base.replace("kbg::", "")
+    m = re.match(r"^kbg_firstfit_kernel<(\w+), (\w+), true, \d+>$", base)
+    if m:
+        return f"kbg_firstfit_kernel<{m.group(1)}, {'false' if grid // 1024 >= 64 else 'true'}>"
     # the fused kernel's rows-per-workgroup variants (16 / 24 / 32) of one mode are one entry
-    return re.sub(r"^(kbg_firstfit_kernel<\w+, \w+)(, \w+)?, \d+>$", r"\1>", base)  # (COMPLETE merged)
+    return re.sub(r"^(kbg_firstfit_kernel<\w+, \w+)(, false)?, \d+>$", r"\1>", base)
 
 
 def rows(path):
@@ -55,7 +63,7 @@ def main():
            "config": int(cfg), "kernels": {}}
     ks = out["kernels"]
     for r in rows(os.path.join(d, f"c{cfg}_kt", "kt_kernel_trace.csv")):
-        k = key(r["Kernel_Name"])
+        k = key(r["Kernel_Name"], int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]))
         if not any(w in k for w in WANT):
             continue
         ks.setdefault(k, {"durations_ns": []})["durations_ns"].append(
@@ -63,7 +71,7 @@ def main():
     counters = {}
     for p in sorted(glob.glob(os.path.join(d, f"c{cfg}_pmc*", "*_counter_collection.csv"))):
         for r in rows(p):
-            k = key(r["Kernel_Name"])
+            k = key(r["Kernel_Name"], int(r["Grid_Size"]))
             if k not in ks:
                 continue
             c = counters.setdefault(k, {}).setdefault(r["Counter_Name"], {})

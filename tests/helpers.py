@@ -99,3 +99,15 @@ def churn_chain(fx0, seed, rounds, run):
             return
         changes, fx = synth.churn(fx, seed * 31 + r, uids, out["decisions"])
         uids |= {p["uid"] for kind, p in changes if kind == "pod_add"}
+
+
+def build_tools():
+    """`make tools` (the CPU tool library) under a file lock: parallel test
+    workers must not relink the library while another loads it."""
+    import fcntl
+    import subprocess
+    pkg = os.path.join(ROOT, "kube-arbitrator_amd")
+    with open(os.path.join(pkg, "tools", ".build.lock"), "w") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", pkg, "tools"], check=True)
+        return os.path.join(pkg, "tools", "libkbg_tools.so")

@@ -18,7 +18,7 @@ import subprocess
 
 import pytest
 
-from helpers import ROOT, run_oracle
+from helpers import ROOT, run_oracle, build_tools
 
 PKG = os.path.join(ROOT, "kube-arbitrator_amd")
 TOOLS = os.path.join(PKG, "tools", "libkbg_tools.so")
@@ -27,7 +27,7 @@ COLL = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.
 
 
 def tools_lib():
-    subprocess.run(["make", "-s", "-C", PKG, "tools"], check=True)
+    build_tools()
     L = ctypes.CDLL(TOOLS)
     L.kbg_tool_sharded_allocate_local.restype = ctypes.c_int32
     L.kbg_tool_sharded_allocate_rank.restype = ctypes.c_int32

@@ -12,7 +12,7 @@ import subprocess
 
 import pytest
 
-from helpers import ROOT, run_oracle
+from helpers import ROOT, run_oracle, build_tools
 
 os.environ["KBG_CHECK_DERIVE"] = "1"  # read per derive, by the tool library only in this process
 
@@ -22,7 +22,7 @@ TOOLS = os.path.join(PKG, "tools", "libkbg_tools.so")
 
 @pytest.fixture(scope="module")
 def tools():
-    subprocess.run(["make", "-s", "-C", PKG, "tools"], check=True)
+    build_tools()
     L = ctypes.CDLL(TOOLS)
     L.kbg_tool_update_nodes.restype = ctypes.c_int32
     return L

@@ -16,7 +16,7 @@ import subprocess
 
 import pytest
 
-from helpers import ROOT
+from helpers import ROOT, build_tools
 
 PKG = os.path.join(ROOT, "kube-arbitrator_amd")
 TOOLS = os.path.join(PKG, "tools", "libkbg_tools.so")
@@ -24,7 +24,7 @@ TOOLS = os.path.join(PKG, "tools", "libkbg_tools.so")
 
 @pytest.fixture(scope="module")
 def tools():
-    subprocess.run(["make", "-s", "-C", PKG, "tools"], check=True)
+    build_tools()
     L = ctypes.CDLL(TOOLS)
     L.kbg_tool_structural.restype = ctypes.c_int32
     return L
