@@ -496,6 +496,41 @@ def _replay(fx0, changes):
     return cache
 
 
+def _fixture_after(fx0, changes):
+    """fx0 after `changes` as a fixture, or None when a fixture cannot say it:
+    a deleted node that pods still name (a fresh cache would make a
+    NodeInfo(nil) for them; the live one has none)."""
+    pods = {p["uid"]: p for p in fx0["pods"]}
+    nodes = {n["name"]: n for n in fx0["nodes"]}
+    groups = {(g.get("namespace", ""), g["name"]): g for g in fx0.get("podGroups", [])}
+    queues = {q["name"]: q for q in fx0.get("queues", [])}
+    gone = set()
+    for kind, o in changes:
+        if kind in ("pod_add", "pod_update"):
+            pods.pop(o["uid"], None)
+            pods[o["uid"]] = o
+        elif kind == "pod_delete":
+            pods.pop(o["uid"], None)
+        elif kind in ("node_add", "node_update"):
+            nodes[o["name"]] = o
+            gone.discard(o["name"])
+        elif kind == "node_delete":
+            nodes.pop(o["name"], None)
+            gone.add(o["name"])
+        elif kind == "pod_group_add":
+            groups[(o.get("namespace", ""), o["name"])] = o
+        elif kind == "pod_group_delete":
+            groups.pop((o.get("namespace", ""), o["name"]), None)
+        elif kind == "queue_add":
+            queues[o["name"]] = o
+        elif kind == "queue_delete":
+            queues.pop(o["name"], None)
+    if any(p.get("nodeName") in gone for p in pods.values()):
+        return None
+    return dict(fx0, pods=list(pods.values()), nodes=list(nodes.values()), podGroups=list(groups.values()),
+                queues=list(queues.values()))
+
+
 def check_structural(fx0, changes_of, opts=None):
     """open(S0) + update(structural changes) + the cycle's actions against a
     fresh open of the replayed cache in the updated session's order."""
@@ -535,6 +570,17 @@ def check_structural(fx0, changes_of, opts=None):
         assert [t.uid for t in fssn.flat.task_objs] == [t.uid for t in ssn.flat.task_objs]
         fresh = abi_cycle(fssn, actions)
         assert got == fresh
+        fx1 = _fixture_after(fx0, changes)
+        if fx1 is not None and not fx0.get("namespaces"):  # also pinned to the oracle on S1
+            fx1 = dict(fx1, sessionOrder=order)
+            out, fs = run_fixture(fx1, opts)
+            try:
+                compare_outputs(run_oracle(fx1), out)
+                if out["status"] == "ok":
+                    assert got["decisions"] == out["decisions"] and got["binds"] == out["binds"]
+            finally:
+                if fs:
+                    fs.close()
         return got
     finally:
         ssn.close()
