@@ -225,7 +225,7 @@ kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, c
                o_q = o_hold + (size_t)E * 24, bytes = o_q + (size_t)Q * sizeof(kbg::FitQuery),
                out_bytes = (size_t)Q * 16;
   if (bytes > S.fit_cap) {
-    if (S.fit_h) (void)hipHostFree(S.fit_h);
+    pool_put(S.fit_h);
     if (S.fit_d) (void)hipFree(S.fit_d);
     S.fit_h = nullptr;
     S.fit_d = nullptr;
@@ -235,7 +235,7 @@ kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, c
     S.fit_cap = bytes;
   }
   if (out_bytes > S.fit_out_cap) {
-    if (S.fit_out) (void)hipHostFree(S.fit_out);
+    pool_put(S.fit_out);
     S.fit_out = nullptr;
     S.fit_out_cap = 0;
     if (host_alloc((void**)&S.fit_out, out_bytes) != KBG_OK) return fail(KBG_E_HIP, "FitError results");

@@ -571,11 +571,74 @@ void build_heaps(const Session& S, Engine& E) {
 
 
 // ---------------------------------------------------------------- device
+// Buffers a closed (or rebuilt) session returns are kept for the next open in
+// the process — a scheduler re-opens or rebuilds sessions every few cycles,
+// and pinned allocations and frees cost milliseconds (hipHostMalloc maps the
+// pages; hipFree synchronizes the device). Per kind (pinned host / device),
+// device and size (rounded up to 64 KiB); at most kPoolKeep bytes idle per
+// kind, the rest freed. A buffer is returned only after its session's stream
+// has drained (free_device), so no kernel still reads or writes it.
+struct BufPool {
+  struct Buf {
+    size_t bytes;
+    int device;
+    bool host;
+  };
+  std::mutex mu;
+  std::unordered_map<void*, Buf> out;                       // every buffer handed out
+  std::multimap<std::tuple<bool, int, size_t>, void*> idle;  // returned ones
+  size_t idle_bytes[2] = {0, 0};
+  static constexpr size_t kPoolKeep = size_t(1) << 30;
+};
+BufPool& buf_pool() {
+  static BufPool* p = new BufPool();  // (never destroyed: buffers may be returned during process exit)
+  return *p;
+}
+kbg_status pool_get(bool host, size_t bytes, void** p) {
+  bytes = (std::max<size_t>(bytes, 64) + 65535) & ~size_t(65535);
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  BufPool& P = buf_pool();
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    auto it = P.idle.lower_bound({host, dev, bytes});
+    if (it != P.idle.end() && std::get<0>(it->first) == host && std::get<1>(it->first) == dev &&
+        std::get<2>(it->first) <= 2 * bytes) {
+      *p = it->second;
+      P.idle_bytes[host] -= std::get<2>(it->first);
+      P.idle.erase(it);
+      return KBG_OK;
+    }
+  }
+  if (host) HIP_TRY(hipHostMalloc(p, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  else HIP_TRY(hipMalloc(p, bytes));
+  std::lock_guard<std::mutex> lk(P.mu);
+  P.out[*p] = BufPool::Buf{bytes, dev, host};
+  return KBG_OK;
+}
+void pool_put(void* p) {
+  if (!p) return;
+  BufPool& P = buf_pool();
+  std::unique_lock<std::mutex> lk(P.mu);
+  auto it = P.out.find(p);
+  if (it == P.out.end()) return;  // (not a pooled buffer: never happens)
+  const BufPool::Buf b = it->second;
+  if (P.idle_bytes[b.host] + b.bytes <= BufPool::kPoolKeep) {
+    P.idle.emplace(std::make_tuple(b.host, b.device, b.bytes), p);
+    P.idle_bytes[b.host] += b.bytes;
+    return;
+  }
+  P.out.erase(it);
+  lk.unlock();
+  if (b.host) (void)hipHostFree(p);
+  else (void)hipFree(p);
+}
+
 template <class T>
 kbg_status dalloc(Session& S, T** p, size_t count) {
   void* q = nullptr;
   if (count == 0) count = 1;
-  HIP_TRY(hipMalloc(&q, count * sizeof(T)));
+  if (kbg_status st = pool_get(false, count * sizeof(T), &q); st != KBG_OK) return st;
   S.d_allocs.push_back(q);
   *p = (T*)q;
   return KBG_OK;
@@ -663,8 +726,7 @@ kbg_status copy_soa(Session& S, const kbg::NodeSoA& dst, const kbg::NodeSoA& src
 // (coherent), so a kernel's stores are on the host when its completion event
 // fires and the host's stores are seen by the next launch.
 kbg_status host_alloc(void** p, size_t bytes) {
-  HIP_TRY(hipHostMalloc(p, std::max<size_t>(bytes, 64), hipHostMallocMapped | hipHostMallocCoherent));  // never 0 B
-  return KBG_OK;
+  return pool_get(true, bytes, p);  // (pool_put returns it)
 }
 // The device address of such memory (the host address itself under unified
 // addressing, which build() checks once).
@@ -682,8 +744,8 @@ void free_device(Session& S) {
   S.svc_own = nullptr;
   for (kbg::Stage& g : S.stages) {
     if (g.inflight) (void)hipEventSynchronize(g.ev[6]);  // nothing may still write the staging
-    if (g.h_up) (void)hipHostFree(g.h_up);
-    if (g.h_down) (void)hipHostFree(g.h_down);
+    pool_put(g.h_up);
+    pool_put(g.h_down);
     for (auto& e : g.ev)
       if (e) {
         (void)hipEventDestroy(e);
@@ -691,13 +753,13 @@ void free_device(Session& S) {
       }
     g = kbg::Stage{};
   }
-  for (char* b : S.up_pool) (void)hipHostFree(b);
+  for (char* b : S.up_pool) pool_put(b);
   S.up_pool.clear();
-  if (S.h_deltas) (void)hipHostFree(S.h_deltas);
-  if (S.h_mdeltas) (void)hipHostFree(S.h_mdeltas);
+  pool_put(S.h_deltas);
+  pool_put(S.h_mdeltas);
   S.h_mdeltas = nullptr;
-  if (S.fit_h) (void)hipHostFree(S.fit_h);
-  if (S.fit_out) (void)hipHostFree(S.fit_out);
+  pool_put(S.fit_h);
+  pool_put(S.fit_out);
   if (S.fit_d) (void)hipFree(S.fit_d);
   S.fit_h = nullptr;
   S.fit_out = nullptr;
@@ -718,7 +780,7 @@ void free_device(Session& S) {
   S.vt_sh_valid = false;
   S.vt_allocs.clear();
   S.h_deltas = nullptr;
-  for (void* p : S.d_allocs) (void)hipFree(p);
+  for (void* p : S.d_allocs) pool_put(p);
   S.d_allocs.clear();
   for (auto& e : S.ev)
     if (e) {

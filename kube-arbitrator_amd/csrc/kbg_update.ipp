@@ -997,6 +997,10 @@ kbg_status restructure(Session& S) {
   R->canon = std::move(S.canon);
   R->canon_of = std::move(S.canon_of);
   R->adopt_strings = true;
+  // the old device tables and pinned buffers go back to the process's pool
+  // first, so the new open takes them from there (an open that fails leaves
+  // the session unusable either way: its events are applied)
+  free_device(S);
   kbg_status st = open_session(*R, &B.sn, &o, nullptr);
   if (st != KBG_OK) {
     free_device(*R);
@@ -1020,7 +1024,6 @@ kbg_status restructure(Session& S) {
         if (auto it = named.find(R->canon[R->tasks_in[t].node_name]); it != named.end()) R->task_cnode[t] = it->second;
   R->updates = S.updates;
   R->rebuilds = S.rebuilds + 1;
-  free_device(S);
   S = std::move(*R);
   S.renum[KBG_RENUM_TASKS] = std::move(B.rt);
   S.renum[KBG_RENUM_NODES] = std::move(B.rn);

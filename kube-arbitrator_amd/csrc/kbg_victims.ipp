@@ -110,7 +110,7 @@ kbg_status vt_setup(Session& S) {
   kbg_status st;
   if (S.vt_ready && S.vt_stale) {  // a session update changed the tasks behind them
     for (void* p : S.vt_allocs) {
-      (void)hipFree(p);
+      pool_put(p);
       S.d_allocs.erase(std::find(S.d_allocs.begin(), S.d_allocs.end(), p));
     }
     S.vt_allocs.clear();
