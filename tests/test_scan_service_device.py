@@ -72,6 +72,19 @@ def test_svc_ranks_saturated_digest(tools, R):
     assert hashlib.sha256(json.dumps(rows, separators=(",", ":")).encode()).hexdigest() == ref["decisions"]
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("R", [4, 8])
+def test_svc_ranks_config4_digest(tools, R):
+    """C4 (20k nodes x 500k tasks, SURVEY §8(e)'s meaningful scaling point:
+    2.5k nodes per rank at R = 8) through the scan service: the decision
+    log's digest equals the oracle's (tests/golden/digest_c4.json)."""
+    ref = load_golden("digest_c4.json")
+    log, _ = run_svc(tools, synth.config_fixture(4), R, {})
+    rows = [[d["task"], d["job"], d["node"], d["kind"], d["dispatched_at"], ""] for d in log]
+    assert len(rows) == ref["n_decisions"]
+    assert hashlib.sha256(json.dumps(rows, separators=(",", ":")).encode()).hexdigest() == ref["decisions"]
+
+
 @pytest.mark.parametrize("seed", range(0, 48, 3))
 def test_svc_ranks_fuzz(tools, seed):
     fx = synth.random_fixture(15000 + seed) if seed % 2 else \
