@@ -207,4 +207,3 @@ def test_update_host_outsider_holder(tools, seed):
     in the first round)."""
     from kbgpu import synth
     check(tools, synth.contended_dupkey_fixture(seed), seed, 2, strict=True)
-
