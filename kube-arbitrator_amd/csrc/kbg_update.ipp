@@ -1032,6 +1032,32 @@ kbg_status restructure(Session& S) {
   return KBG_OK;
 }
 
+// Room for a large batch's growth, reserved before its events apply: each
+// target node's pod lists (a cycle's binds grow a node's lists by tens of
+// entries, one reallocation per doubling otherwise) and the update's own
+// per-event lists.
+void reserve_for_events(Session& S, const kbg_event* ev, int32_t n) {
+  if (n < 4096) return;
+  thread_local std::vector<int32_t> adds;
+  adds.assign(S.n_nodes, 0);
+  for (int32_t i = 0; i < n; ++i) {
+    const kbg_event& e = ev[i];
+    if ((e.kind == KBG_EV_POD_UPDATE || e.kind == KBG_EV_POD_ADD) && e.node >= 0 && e.node < S.n_nodes &&
+        !terminated(e.status))
+      adds[e.node]++;
+  }
+  for (int32_t nd = 0; nd < S.n_nodes; ++nd)
+    if (adds[nd]) {
+      S.node_key_order[nd].reserve(S.node_key_order[nd].size() + adds[nd]);
+      S.node_task_order[nd].reserve(S.node_task_order[nd].size() + adds[nd]);
+    }
+  S.upd_tasks.reserve(S.upd_tasks.size() + n);
+  S.pend_dirty_jobs.reserve(S.pend_dirty_jobs.size() + n);
+  S.upd_keys.reserve(S.upd_keys.size() + 2 * (size_t)n);
+  S.jmove_out.reserve(S.jmove_out.size() + n);
+  S.jmove_add.reserve(S.jmove_add.size() + n);
+}
+
 kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
   const auto t0 = std::chrono::steady_clock::now();
   for (auto& r : S.renum) r.clear();
@@ -1131,6 +1157,7 @@ kbg_status session_update(Session& S, const kbg_event* ev, int32_t n) {
     }
   };
   S.jmove_defer = (int64_t)n * 8 > (int64_t)S.n_tasks;
+  reserve_for_events(S, ev, n);
   for (int32_t i = 0; i < n; ++i) {
     if (i + kFar < n) ahead_far(ev[i + kFar]);
     if (i + kMid < n) ahead_mid(ev[i + kMid], i + kMid);

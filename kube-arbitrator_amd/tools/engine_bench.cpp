@@ -66,6 +66,7 @@ extern "C" int32_t kbg_tool_update_nodes(const kbg_snapshot* snap, const kbg_opt
   U.seen.assign(S.n_nodes, 0);
   const auto t0 = std::chrono::steady_clock::now();
   S.jmove_defer = (int64_t)n * 8 > (int64_t)S.n_tasks;
+  reserve_for_events(S, ev, n);  // as session_update
   for (int32_t i = 0; i < n; ++i)
     if (apply_event(S, U, ev[i], nullptr) != KBG_OK) return -3;
   finish_job_lists(S);
