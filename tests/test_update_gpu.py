@@ -600,7 +600,8 @@ def test_update_structural(seed):
     def changes_of(ssn):
         return synth.structural(fx0, seed, {j.uid for j in ssn.jobs}, {t.uid for t in ssn.flat.task_objs},
                                 [q.uid for q in ssn.queues])
-    check_structural(fx0, changes_of, {"batch_tasks": 1 + seed % 7, "full_scan": seed % 2})
+    opts = {"batch_tasks": 1 + seed % 7, "full_scan": seed % 2, "shards": 1 + seed % 3}  # (in-process node shards)
+    check_structural(fx0, changes_of, opts)
 
 
 @pytest.mark.parametrize("seed", range(6))
