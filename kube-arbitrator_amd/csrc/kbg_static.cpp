@@ -339,20 +339,27 @@ void compile_static_predicates(Session& S, StaticHost* out) {
   } else {
     std::unordered_map<std::string, int32_t> class_of_key;
     std::vector<int32_t> class_spec;
+    // a spec's class is its key's: each spec's key is built once (the tasks
+    // share a few specs), classes numbered in order of their first task
+    std::vector<int32_t> memo(S.specs_in.size() + 1, -1);  // [spec + 1] -> class; [0]: no spec
     for (int32_t t = 0; t < S.n_tasks; ++t) {
       if (!S.pending_candidate[t] && !S.be_task[t]) continue;  // allocate and backfill candidates
       const int32_t sp = S.tasks_in[t].spec;
-      const kbg_spec* spec = sp >= 0 ? &S.specs_in[sp] : nullptr;
-      std::string key = spec_key(S, spec);
-      auto it = class_of_key.find(key);
-      if (it == class_of_key.end()) {
-        const int32_t id = (int32_t)class_spec.size();
-        class_of_key.emplace(std::move(key), id);
-        class_spec.push_back(sp);
-        S.task_class[t] = id;
-      } else {
-        S.task_class[t] = it->second;
+      int32_t& m = memo[(size_t)(sp + 1)];
+      if (m < 0) {
+        const kbg_spec* spec = sp >= 0 ? &S.specs_in[sp] : nullptr;
+        std::string key = spec_key(S, spec);
+        auto it = class_of_key.find(key);
+        if (it == class_of_key.end()) {
+          const int32_t id = (int32_t)class_spec.size();
+          class_of_key.emplace(std::move(key), id);
+          class_spec.push_back(sp);
+          m = id;
+        } else {
+          m = it->second;
+        }
       }
+      S.task_class[t] = m;
     }
     if (class_spec.empty()) class_spec.push_back(-1);
     S.class_spec = class_spec;
