@@ -1086,13 +1086,23 @@ kbg_status derive_host(Session& S, kbg::StaticHost* sh, int* outcome) {
       S.shape_of_task.resize(T, -1);
       if ((int32_t)S.be_shape.size() < std::max(1, S.n_classes)) S.be_shape.resize(std::max(1, S.n_classes), -1);
     }
+    // (a job's tasks usually share one (class, request): the last key found
+    // answers most lookups without the hash map)
+    kbg::ShapeKey last_key{-1, 0.0, 0.0, 0.0};
+    int32_t last_id = -1;
     auto cand_shape = [&](int32_t t) {
       if (!S.pending_candidate[t]) return;
       int32_t& sh_t = S.shape_of_task[t];
       if (sh_t < 0) {
-        auto it = S.shape_ids.emplace(kbg::ShapeKey{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g}, S.n_shapes);
-        if (it.second) S.n_shapes++;
-        sh_t = it.first->second;
+        const kbg::ShapeKey k{S.task_class[t], S.treq[t].c, S.treq[t].m, S.treq[t].g};
+        if (last_id >= 0 && k == last_key) {
+          sh_t = last_id;
+        } else {
+          auto it = S.shape_ids.emplace(k, S.n_shapes);
+          if (it.second) S.n_shapes++;
+          sh_t = last_id = it.first->second;
+          last_key = k;
+        }
       }
       S.task_shape[t] = sh_t;
       if ((int32_t)S.shape_task.size() <= sh_t) S.shape_task.resize((size_t)sh_t + 1, -1);
