@@ -3,7 +3,7 @@
 // anonymous namespace, after the parts before it; not compiled on its own).
 
 // The host side of one allocate cycle runs on two threads:
-//   predictor (std::thread) — the ordering engine: predicts batches of K task
+//   predictor (pool thread) — the ordering engine: predicts batches of K task
 //                             evaluations ahead, each with a checkpoint of the
 //                             engine state it started from;
 //   committer (caller)      — per batch: device scan, in-order commit against
@@ -184,6 +184,107 @@ void pin_near(int cpu, int nth = 1) {
     return;
   }
 }
+
+// A helper thread of a cycle (predictor, builder, truth engine, logger) from
+// a process-wide pool: every cycle starts four and joins them, and creating
+// and joining an OS thread cost tens of microseconds each on the box (a
+// resident churn cycle is about a millisecond). Same use as std::thread:
+// construct with the function, join() waits until it has returned. A pool
+// thread gets its CPU mask back after each function (pin_near narrows it).
+// A forked child starts a pool of its own (the parent's threads are not in it).
+class PoolThread {
+  struct Slot {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<void()> fn;
+    bool has = false, done = false;
+  };
+  struct Pool {
+    std::mutex mu;
+    std::vector<Slot*> idle;
+    pid_t pid = 0;
+  };
+  static Pool& pool() {
+    static Pool* p = new Pool();  // (never destroyed: its threads outlive static destruction)
+    return *p;
+  }
+  static void loop(Slot* s) {
+    cpu_set_t mask;
+    const bool have_mask = pthread_getaffinity_np(pthread_self(), sizeof(mask), &mask) == 0;
+    for (;;) {
+      std::function<void()> fn;
+      {
+        std::unique_lock<std::mutex> lk(s->mu);
+        s->cv.wait(lk, [&] { return s->has; });
+        fn = std::move(s->fn);
+        s->has = false;
+      }
+      fn();
+      fn = nullptr;  // (captured state released before the joiner returns)
+      {
+        std::lock_guard<std::mutex> lk(s->mu);
+        s->done = true;
+        s->cv.notify_all();
+      }
+      if (have_mask) (void)pthread_setaffinity_np(pthread_self(), sizeof(mask), &mask);
+    }
+  }
+  Slot* slot_ = nullptr;
+
+ public:
+  PoolThread() = default;
+  explicit PoolThread(std::function<void()> fn) {
+    Pool& P = pool();
+    Slot* s = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(P.mu);
+      if (P.pid != getpid()) {  // first use, or a forked child: the listed threads are not this process's
+        P.idle.clear();
+        P.pid = getpid();
+      }
+      if (!P.idle.empty()) {
+        s = P.idle.back();
+        P.idle.pop_back();
+      }
+    }
+    if (!s) {
+      s = new Slot();
+      std::thread(loop, s).detach();
+    }
+    {
+      std::lock_guard<std::mutex> lk(s->mu);
+      s->fn = std::move(fn);
+      s->done = false;
+      s->has = true;
+    }
+    s->cv.notify_all();
+    slot_ = s;
+  }
+  PoolThread(const PoolThread&) = delete;
+  PoolThread& operator=(const PoolThread&) = delete;
+  PoolThread& operator=(PoolThread&& o) noexcept {
+    if (this != &o) {
+      join();
+      slot_ = o.slot_;
+      o.slot_ = nullptr;
+    }
+    return *this;
+  }
+  ~PoolThread() { join(); }
+  bool joinable() const { return slot_ != nullptr; }
+  void join() {
+    if (!slot_) return;
+    Slot* s = slot_;
+    slot_ = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(s->mu);
+      s->cv.wait(lk, [&] { return s->done; });
+    }
+    Pool& P = pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.idle.push_back(s);
+  }
+};
 
 // Last node-loop run of a job: the task, how many decisions preceded it and
 // where it ended (node -1 = fitted nowhere).
@@ -497,7 +598,7 @@ struct Outcome {
 struct Replayer {
   Session& S;
   Engine& E;
-  std::thread th;
+  PoolThread th;
   std::mutex mu;
   SpinCV cv;
   std::deque<std::vector<Outcome>> q;
@@ -506,7 +607,7 @@ struct Replayer {
   // committer_cpu >= 0: on its own core of the committer's last-level cache
   // (after the predictor, logger and builder), never time-sharing the predictor's
   Replayer(Session& s, Engine& e, int committer_cpu = -1) : S(s), E(e) {
-    th = std::thread([this, committer_cpu]() {
+    th = PoolThread([this, committer_cpu]() {
       pin_near(committer_cpu, 4);
       run();
     });
@@ -587,7 +688,7 @@ struct Predictor {
   std::string error;
   EngineProfile prof;
   Trace tr;
-  std::thread th, bth;
+  PoolThread th, bth;
   bool builder = false;       // a builder thread turns predicted batches into device rows (allocate_cycle)
   bool truth_mode = false;    // rollbacks copy a truth engine (rollback_truth): no batch checkpoints
   bool runs = false;          // consume a job's tasks of shapes known to fit nowhere as one entry (Batch::brun)
@@ -597,8 +698,8 @@ struct Predictor {
   }
   void start(int committer_cpu, bool with_builder = false) {
     builder = with_builder;
-    th = std::thread([this, committer_cpu]() { run(committer_cpu); });
-    if (builder) bth = std::thread([this, committer_cpu]() { build_run(committer_cpu); });
+    th = PoolThread([this, committer_cpu]() { run(committer_cpu); });
+    if (builder) bth = PoolThread([this, committer_cpu]() { build_run(committer_cpu); });
   }
   // Builder: Grouper::build of each predicted batch into the batch's own
   // pinned row buffer, so the committer only swaps buffers at launch.
@@ -837,13 +938,13 @@ struct LogItem {
 // outcomes in commit order.
 struct Logger {
   std::function<void(const LogItem&)> fn;
-  std::thread th;
+  PoolThread th;
   std::mutex mu;
   std::condition_variable cv;
   std::deque<std::vector<LogItem>> q;
   bool done = false;
   explicit Logger(std::function<void(const LogItem&)> f, int committer_cpu) : fn(std::move(f)) {
-    th = std::thread([this, committer_cpu]() {
+    th = PoolThread([this, committer_cpu]() {
       pin_near(committer_cpu, 2);  // not the predictor's core (the builder takes the third)
       run();
     });

@@ -3,7 +3,7 @@ p50), alternating in one GPU session: python kube-arbitrator_amd/tools/ab_bench.
 (CONFIG=4: another BASELINE config; REPS: rounds; lib.so@KEY=VAL sets a variant's environment).
 Per run: p50 cycle ms (production, full-scan), production scan launch us, production device round trip ms,
 production re-checks and resolve ms
-(RESIDENT=1: and the p50 resident churn update ms, the bind update ms; STEPS: timed steps)"""
+(RESIDENT=1: and the p50 resident churn update ms, the bind update ms, the p50 churn allocate ms; STEPS: timed steps)"""
 import json, os, subprocess, sys
 res = {}
 cfg = os.environ.get("CONFIG", "3")
@@ -28,6 +28,7 @@ for rep in range(int(os.environ.get("REPS", "3"))):
                                       pm.get("breakdown", {}).get("resolve_rechecks"),
                                       round(pm.get("breakdown", {}).get("host_resolve_ms") or 0, 2))
                                      + ((round(d["resident_session"]["churn_update_ms_p50"], 2),
-                                         round(d["resident_session"]["bind_update_ms"], 2)) if resident else ()))
+                                         round(d["resident_session"]["bind_update_ms"], 2),
+                                         round(d["resident_session"]["churn_allocate_ms_p50"], 2)) if resident else ()))
         print(v, res[v][-1], flush=True)
 print(json.dumps(res))
