@@ -346,6 +346,7 @@ kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, c
   int32_t* hk = (int32_t*)(S.fit_h + o_hk);
   double* hold = (double*)(S.fit_h + o_hold);
   kbg::FitQuery* fq = (kbg::FitQuery*)(S.fit_h + o_q);
+  trace_add("fit.count", E);
   std::copy(cnt.begin(), cnt.end(), hoff);
   for (int32_t k = kmin; k < (int32_t)dec.size(); ++k) {
     if (S.dec_dup[k]) continue;
@@ -364,6 +365,11 @@ kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, c
     }
   }
   for (int32_t i = 0; i < Q; ++i) {
+    if (i + 8 < Q) {  // the queried tasks are scattered over the task arrays
+      const int32_t t8 = last[qj[i + 8]].task;
+      __builtin_prefetch(&S.treq[t8]);
+      __builtin_prefetch(&S.task_class[t8]);
+    }
     const LastEval& le = last[qj[i]];
     const Res& r = S.treq[le.task];
     fq[i] = kbg::FitQuery{S.task_class[le.task], le.node < 0 ? N : le.node + (le.kind == KBG_KIND_PIPELINE ? 1 : 0),
@@ -375,8 +381,10 @@ kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, c
   kbg::FitArgs a{S.d_nodes.idle_cpu, soa_stride(S), S.W, S.d_class_mask, (const int32_t*)S.fit_d,
                  (const int32_t*)(S.fit_d + o_hk), (const double*)(S.fit_d + o_hold), (const int32_t*)(S.fit_d + o_na),
                  (const kbg::FitQuery*)(S.fit_d + o_q), Q, S.pred_active ? 1 : 0, fit_out, S.tab_lo, S.tab_n};
+  trace_add("fit.staged", Q);
   HIP_TRY(kbg::launch_fitdelta(a, S.stream));
   HIP_TRY(hipStreamSynchronize(S.stream));
+  trace_add("fit.kernel", 0);
   if (S.svc)  // each rank counted its own nodes
     if (kbg_status st = svc_sum_counts(S, S.fit_out, (size_t)Q * 4); st != KBG_OK) return st;
   for (int32_t i = 0; i < Q; ++i) {
@@ -394,7 +402,7 @@ kbg_status compute_fit_deltas(Session& S, const std::vector<kbg_decision>& dec, 
   S.fit.assign(S.n_jobs, Session::FitCounts{});
   std::vector<int32_t> jobs;
   for (int32_t j = 0; j < S.n_jobs; ++j)
-    if (S.committed_ready[j] < S.jobs_in[j].min_available) jobs.push_back(j);
+    if (S.committed_ready[j] < S.job_min[j]) jobs.push_back(j);  // (job_min: jobs_in[j].min_available, compact)
   if (jobs.empty()) return KBG_OK;
   const bool host_only = getenv("KBG_HOST_FITDELTA") != nullptr;  // read per cycle (A/B parity tests)
   if (S.stream && (!S.comm || S.svc) && !S.has_ports && !S.has_aff && !S.any_nil && !host_only)
@@ -1700,6 +1708,7 @@ kbg_status allocate_cycle(Session& S, kbg_decision* out, int32_t cap, int32_t* n
   ctr.add("logged");
   if (kbg_status st = flush(); st != KBG_OK) return st;  // the cycle's last write-back
   HIP_TRY(hipStreamSynchronize(S.stream));
+  ctr.add("flushed");
   if (S.svc) {  // the scan service: every rank counts its nodes after the end message (allocate_svc_root)
     g_svc_fit.dec_oldp = std::move(dec_oldp);
     g_svc_fit.last = std::move(last);
