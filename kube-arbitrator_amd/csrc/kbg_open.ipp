@@ -1187,10 +1187,10 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   if (S.opts.device < 0) HIP_TRY(hipGetDevice(&S.device));
   if (comm) S.device = comm->device;
   HIP_TRY(hipSetDevice(S.device));
-  HIP_TRY(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
-  for (auto& e : S.ev) HIP_TRY(hipEventCreate(&e));
-  HIP_TRY(hipEventCreateWithFlags(&S.stage_ev, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&S.comm_ev, hipEventDisableTiming));
+  if ((st = stream_get(&S.stream))) return st;  // streams and events from the process's cache
+  for (auto& e : S.ev)
+    if ((st = event_get(&e, true))) return st;
+  if ((st = event_get(&S.stage_ev, false)) || (st = event_get(&S.comm_ev, false))) return st;
   S.stage_pending = false;
   if ((st = alloc_soa(S, &S.d_nodes)) || (st = alloc_soa(S, &S.d_nodes0))) return st;
   const size_t up_cap = up_bytes_for(S.K);
@@ -1213,8 +1213,9 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
     return st;
   for (kbg::Stage& g : S.stages) {
     if ((st = host_alloc((void**)&g.h_up, up_cap)) || (st = host_alloc((void**)&g.h_down, down_cap * 4))) return st;
-    for (int e = 0; e < 6; ++e) HIP_TRY(hipEventCreate(&g.ev[e]));
-    HIP_TRY(hipEventCreateWithFlags(&g.ev[6], hipEventDisableTiming));
+    for (int e = 0; e < 6; ++e)
+      if ((st = event_get(&g.ev[e], true))) return st;
+    if ((st = event_get(&g.ev[6], false))) return st;
   }
   {  // unified addressing: a mapped host buffer has the same address on the device
     void* d = nullptr;

@@ -984,8 +984,17 @@ kbg_status rebuild_snapshot(const Session& S, Rebuilt& B) {
 }
 
 kbg_status restructure(Session& S) {
+  static const bool prof = getenv("KBG_PROFILE_OPEN") != nullptr;
+  auto tl = std::chrono::steady_clock::now();
+  auto phase = [&](const char* name) {
+    if (!prof) return;
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[kbg rebuild] %-20s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(now - tl).count());
+    tl = now;
+  };
   Rebuilt B;
   if (kbg_status st = rebuild_snapshot(S, B); st != KBG_OK) return st;
+  phase("snapshot");
   const int32_t N = S.n_nodes;
   const std::vector<int32_t>& rn = B.rn;
   kbg_options o = S.opts;
@@ -1001,7 +1010,9 @@ kbg_status restructure(Session& S) {
   // first, so the new open takes them from there (an open that fails leaves
   // the session unusable either way: its events are applied)
   free_device(S);
+  phase("free device");
   kbg_status st = open_session(*R, &B.sn, &o, nullptr);
+  phase("open");
   if (st != KBG_OK) {
     free_device(*R);
     return st;
@@ -1024,7 +1035,9 @@ kbg_status restructure(Session& S) {
         if (auto it = named.find(R->canon[R->tasks_in[t].node_name]); it != named.end()) R->task_cnode[t] = it->second;
   R->updates = S.updates;
   R->rebuilds = S.rebuilds + 1;
+  phase("pod-only names");
   S = std::move(*R);
+  phase("session move");
   S.renum[KBG_RENUM_TASKS] = std::move(B.rt);
   S.renum[KBG_RENUM_NODES] = std::move(B.rn);
   S.renum[KBG_RENUM_JOBS] = std::move(B.rj);
