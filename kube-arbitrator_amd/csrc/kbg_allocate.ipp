@@ -327,12 +327,12 @@ kbg_status fit_deltas_device(Session& S, const std::vector<kbg_decision>& dec, c
                out_bytes = (size_t)Q * 16;
   if (bytes > S.fit_cap) {
     pool_put(S.fit_h);
-    pool_put(S.fit_d);
+    if (S.fit_d) (void)hipFree(S.fit_d);
     S.fit_h = nullptr;
     S.fit_d = nullptr;
     S.fit_cap = 0;
     if (host_alloc((void**)&S.fit_h, bytes) != KBG_OK) return fail(KBG_E_HIP, "FitError staging");
-    if (pool_get(false, bytes, (void**)&S.fit_d) != KBG_OK) return fail(KBG_E_HIP, "FitError device staging");
+    HIP_TRY(hipMalloc((void**)&S.fit_d, bytes));
     S.fit_cap = bytes;
   }
   if (out_bytes > S.fit_out_cap) {

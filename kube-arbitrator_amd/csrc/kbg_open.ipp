@@ -1187,10 +1187,12 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   if (S.opts.device < 0) HIP_TRY(hipGetDevice(&S.device));
   if (comm) S.device = comm->device;
   HIP_TRY(hipSetDevice(S.device));
-  if ((st = stream_get(&S.stream))) return st;  // streams and events from the process's cache
+  // (a rebuilt session arrives with its predecessor's stream and events, restructure)
+  if (!S.stream) HIP_TRY(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
   for (auto& e : S.ev)
-    if ((st = event_get(&e, true))) return st;
-  if ((st = event_get(&S.stage_ev, false)) || (st = event_get(&S.comm_ev, false))) return st;
+    if (!e) HIP_TRY(hipEventCreate(&e));
+  if (!S.stage_ev) HIP_TRY(hipEventCreateWithFlags(&S.stage_ev, hipEventDisableTiming));
+  if (!S.comm_ev) HIP_TRY(hipEventCreateWithFlags(&S.comm_ev, hipEventDisableTiming));
   S.stage_pending = false;
   if ((st = alloc_soa(S, &S.d_nodes)) || (st = alloc_soa(S, &S.d_nodes0))) return st;
   const size_t up_cap = up_bytes_for(S.K);
@@ -1214,8 +1216,8 @@ kbg_status build(Session& S, kbg_comm* comm, const std::function<void(const char
   for (kbg::Stage& g : S.stages) {
     if ((st = host_alloc((void**)&g.h_up, up_cap)) || (st = host_alloc((void**)&g.h_down, down_cap * 4))) return st;
     for (int e = 0; e < 6; ++e)
-      if ((st = event_get(&g.ev[e], true))) return st;
-    if ((st = event_get(&g.ev[6], false))) return st;
+      if (!g.ev[e]) HIP_TRY(hipEventCreate(&g.ev[e]));
+    if (!g.ev[6]) HIP_TRY(hipEventCreateWithFlags(&g.ev[6], hipEventDisableTiming));
   }
   {  // unified addressing: a mapped host buffer has the same address on the device
     void* d = nullptr;

@@ -634,70 +634,6 @@ void pool_put(void* p) {
   else (void)hipFree(p);
 }
 
-// Streams and events of closed (or rebuilt) sessions, kept for the next open
-// in the process like the buffers above: creating and destroying a stream and
-// its twenty events costs about a millisecond per session. Per device and
-// event kind (timing or not); a returned stream has been synchronized, so it
-// and its events are idle. At most kObjKeep of each kind per device.
-struct ObjCache {
-  std::mutex mu;
-  std::unordered_map<void*, std::pair<int, int>> out;  // object -> (device, kind: 0 stream, 1 timing event, 2 event)
-  std::multimap<std::pair<int, int>, void*> idle;
-  static constexpr size_t kObjKeep = 64;
-};
-ObjCache& obj_cache() {
-  static ObjCache* c = new ObjCache();  // (never destroyed, as buf_pool)
-  return *c;
-}
-void* obj_take(int kind) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  ObjCache& C = obj_cache();
-  std::lock_guard<std::mutex> lk(C.mu);
-  auto it = C.idle.find({dev, kind});
-  if (it == C.idle.end()) return nullptr;
-  void* o = it->second;
-  C.idle.erase(it);
-  return o;
-}
-void obj_made(void* o, int kind) {
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  ObjCache& C = obj_cache();
-  std::lock_guard<std::mutex> lk(C.mu);
-  C.out[o] = {dev, kind};
-}
-kbg_status stream_get(hipStream_t* s) {
-  if ((*s = (hipStream_t)obj_take(0))) return KBG_OK;
-  HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
-  obj_made(*s, 0);
-  return KBG_OK;
-}
-kbg_status event_get(hipEvent_t* e, bool timing) {
-  if ((*e = (hipEvent_t)obj_take(timing ? 1 : 2))) return KBG_OK;
-  if (timing) HIP_TRY(hipEventCreate(e));
-  else HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  obj_made(*e, timing ? 1 : 2);
-  return KBG_OK;
-}
-// Back to the cache (or destroyed past its bound); null is ignored.
-void obj_put(void* o) {
-  if (!o) return;
-  ObjCache& C = obj_cache();
-  std::unique_lock<std::mutex> lk(C.mu);
-  auto it = C.out.find(o);
-  if (it == C.out.end()) return;  // (not a cached object: never happens)
-  const std::pair<int, int> key = it->second;
-  if (C.idle.count(key) < ObjCache::kObjKeep) {
-    C.idle.emplace(key, o);
-    return;
-  }
-  C.out.erase(it);
-  lk.unlock();
-  if (key.second == 0) (void)hipStreamDestroy((hipStream_t)o);
-  else (void)hipEventDestroy((hipEvent_t)o);
-}
-
 template <class T>
 kbg_status dalloc(Session& S, T** p, size_t count) {
   void* q = nullptr;
@@ -810,10 +746,11 @@ void free_device(Session& S) {
     if (g.inflight) (void)hipEventSynchronize(g.ev[6]);  // nothing may still write the staging
     pool_put(g.h_up);
     pool_put(g.h_down);
-    for (auto& e : g.ev) {
-      obj_put(e);
-      e = nullptr;
-    }
+    for (auto& e : g.ev)
+      if (e) {
+        (void)hipEventDestroy(e);
+        e = nullptr;
+      }
     g = kbg::Stage{};
   }
   for (char* b : S.up_pool) pool_put(b);
@@ -823,7 +760,7 @@ void free_device(Session& S) {
   S.h_mdeltas = nullptr;
   pool_put(S.fit_h);
   pool_put(S.fit_out);
-  pool_put(S.fit_d);
+  if (S.fit_d) (void)hipFree(S.fit_d);
   S.fit_h = nullptr;
   S.fit_out = nullptr;
   S.fit_d = nullptr;
@@ -845,16 +782,17 @@ void free_device(Session& S) {
   S.h_deltas = nullptr;
   for (void* p : S.d_allocs) pool_put(p);
   S.d_allocs.clear();
-  for (auto& e : S.ev) {
-    obj_put(e);
-    e = nullptr;
-  }
-  obj_put(S.stage_ev);
+  for (auto& e : S.ev)
+    if (e) {
+      (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+  if (S.stage_ev) (void)hipEventDestroy(S.stage_ev);
   S.stage_ev = nullptr;
-  obj_put(S.comm_ev);
+  if (S.comm_ev) (void)hipEventDestroy(S.comm_ev);
   S.comm_ev = nullptr;
   S.stage_pending = false;
-  obj_put(S.stream);  // (synchronized above: idle)
+  if (S.stream) (void)hipStreamDestroy(S.stream);
   S.stream = nullptr;
 }
 

@@ -1006,9 +1006,22 @@ kbg_status restructure(Session& S) {
   R->canon = std::move(S.canon);
   R->canon_of = std::move(S.canon_of);
   R->adopt_strings = true;
-  // the old device tables and pinned buffers go back to the process's pool
-  // first, so the new open takes them from there (an open that fails leaves
-  // the session unusable either way: its events are applied)
+  // the stream and its events move to the rebuilt session (creating and
+  // destroying them cost milliseconds) once everything enqueued has run; the
+  // old device tables and pinned buffers go back to the process's pool first,
+  // so the new open takes them from there (an open that fails leaves the
+  // session unusable either way: its events are applied)
+  if (S.stream) HIP_TRY(hipStreamSynchronize(S.stream));
+  for (kbg::Stage& g : S.stages) {
+    if (g.inflight) HIP_TRY(hipEventSynchronize(g.ev[6]));
+    g.inflight = false;
+  }
+  std::swap(R->stream, S.stream);
+  for (size_t k = 0; k < std::size(S.ev); ++k) std::swap(R->ev[k], S.ev[k]);
+  std::swap(R->stage_ev, S.stage_ev);
+  std::swap(R->comm_ev, S.comm_ev);
+  for (size_t g = 0; g < std::size(S.stages); ++g)
+    for (size_t k = 0; k < std::size(S.stages[g].ev); ++k) std::swap(R->stages[g].ev[k], S.stages[g].ev[k]);
   free_device(S);
   phase("free device");
   kbg_status st = open_session(*R, &B.sn, &o, nullptr);
