@@ -895,11 +895,22 @@ kbg_status rebuild_snapshot(const Session& S, Rebuilt& B) {
     }
   }
   // the pod behind each key of a live node: a task (of a session job or of one
-  // that left) or a pod outside the session jobs
+  // that left) or a pod outside the session jobs. Per node, its tasks' keys
+  // sorted by (key, position): the first task in node order holding a key is
+  // a binary search away (a node holds tens of pods; a linear scan per key
+  // was quadratic, 40 ms at C4 with every task bound).
+  std::vector<std::pair<int32_t, int32_t>> held;  // (canonical key, position in node_task_order[n])
+  int32_t held_node = -1;
   auto holder_task = [&](int32_t n, int32_t key) -> int32_t {
-    for (const int32_t t : S.node_task_order[n])
-      if (S.canon[S.tasks_in[t].pod_key] == key) return t;
-    return -1;
+    const std::vector<int32_t>& order = S.node_task_order[n];
+    if (held_node != n) {
+      held.clear();
+      for (int32_t i = 0; i < (int32_t)order.size(); ++i) held.emplace_back(S.canon[S.tasks_in[order[i]].pod_key], i);
+      std::sort(held.begin(), held.end());
+      held_node = n;
+    }
+    auto it = std::lower_bound(held.begin(), held.end(), std::make_pair(key, INT32_MIN));
+    return it != held.end() && it->first == key ? order[it->second] : -1;
   };
   bool copies = true;
   for (int32_t n = 0; n < N && copies; ++n) {
